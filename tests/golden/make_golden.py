@@ -1,0 +1,300 @@
+"""Generate the golden fixtures under tests/golden/*.npz from the REFERENCE implementation.
+
+Runs ONLY in the development container, where the reference is mounted read-only at
+/root/reference. Never run on the GPU box (the reference does not exist there); the committed
+.npz files are what travels.
+
+How the reference is exercised:
+  * bytecode writing disabled (sys.dont_write_bytecode) so nothing is written under /root/reference;
+  * torch_scatter (absent offline) replaced by tests/golden/_shim/torch_scatter.py (2.1.2 semantics);
+  * `from models.gnn import GNN` etc. imported from /root/reference/src unmodified;
+  * the BFS (src/datasets/features.py: build_numba_adjacency_list, compute_multi_hop_edges_bfs_numba)
+    and the collate (src/datasets/molecular.py: MyBatch.from_data_list) are located with `ast` in the
+    reference source and executed with a numba stand-in (njit = identity, typed.List = list) and
+    Batch = types.SimpleNamespace (their own imports need rdkit / numba / torch_geometric / h5py).
+Inputs: QM9 graphs from the committed asset aimnet-x2d_amd/data/qm9_val_graphs.npz (RDKit-free
+featuriser over the reference's sample split) and synthetic 40-atom molecules (aimx/synth.py).
+Weights: oracle.model.seeded_params(cfg, seed) loaded into the reference with load_state_dict.
+
+Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.npz)
+"""
+import ast
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference/src"
+sys.path.insert(0, os.path.join(HERE, "_shim"))
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(ROOT, "aimnet-x2d_amd"))
+sys.path.insert(0, ROOT)
+
+from models.gnn import GNN  # noqa: E402  (reference)
+from models.layers import ShellConvolutionLayer  # noqa: E402  (reference)
+from models.pooling import MultiHeadAttentionPoolingLayer  # noqa: E402  (reference)
+
+from oracle.model import default_config, seeded_params  # noqa: E402
+from aimx.synth import QM9Asset, adjacency, synth_molecules  # noqa: E402
+
+FS = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+
+
+def _load_ref_functions(path, names, env):
+    src = open(path).read()
+    tree = ast.parse(src)
+    found = {}
+    for node in ast.walk(tree):
+        if isinstance(node, ast.FunctionDef) and node.name in names and node.name not in found:
+            seg = ast.get_source_segment(src, node)
+            found[node.name] = seg
+    for nm in names:
+        code = found[nm]
+        lines = code.splitlines()
+        # strip decorators / dedent method bodies
+        lines = [ln for ln in lines if not ln.strip().startswith("@")]
+        ind = len(lines[0]) - len(lines[0].lstrip())
+        code = "\n".join(ln[ind:] if len(ln) >= ind else ln for ln in lines)
+        exec(compile(code, f"<ref:{os.path.basename(path)}:{nm}>", "exec"), env)
+    return env
+
+
+def ref_bfs_env():
+    env = {"np": np, "NumbaList": list, "boolean": np.bool_, "njit": lambda f: f}
+    return _load_ref_functions(os.path.join(REF, "datasets", "features.py"),
+                               ["build_numba_adjacency_list", "compute_multi_hop_edges_bfs_numba"], env)
+
+
+def ref_collate_env():
+    env = {"torch": torch, "Batch": types.SimpleNamespace}
+    return _load_ref_functions(os.path.join(REF, "datasets", "molecular.py"), ["from_data_list"], env)
+
+
+BFS = ref_bfs_env()
+COLLATE = ref_collate_env()
+
+
+def ref_hops(n, bonds, hops):
+    adj = adjacency(n, bonds)
+    al = BFS["build_numba_adjacency_list"](adj)
+    return BFS["compute_multi_hop_edges_bfs_numba"](al, hops)
+
+
+def ref_batch(mols, hops, targets=None, charges=None):
+    """Run the reference collate on per-molecule data objects."""
+    data = []
+    for k, (n, bonds, feats) in enumerate(mols):
+        hl = ref_hops(n, bonds, hops)
+        d = types.SimpleNamespace()
+        d.x = torch.zeros(n, 1)
+        d.multi_hop_edges = [torch.from_numpy(np.asarray(e)).long() for e in hl]
+        d.atom_features_map = {
+            "atom_type": torch.from_numpy(feats[:, 0]).long(),
+            "hydrogen_count": torch.from_numpy(feats[:, 1]).long(),
+            "degree": torch.from_numpy(feats[:, 2]).long(),
+            "hybridization": torch.from_numpy(feats[:, 3]).long(),
+        }
+        d.chiral_tensors, d.cis_bonds_tensors, d.trans_bonds_tensors = [], [], []
+        d.target = torch.tensor(targets[k] if targets is not None else [0.0], dtype=torch.float)
+        d.total_charge = torch.tensor([charges[k] if charges is not None else 0.0], dtype=torch.float)
+        d.smiles = ""
+        d.atomic_numbers = torch.from_numpy(feats[:, 0] + 1).long()
+        data.append(d)
+    b = COLLATE["from_data_list"](data)
+    per_mol = [[np.asarray(e) for e in ref_hops(n, bonds, hops)] for (n, bonds, _) in mols]
+    return b, per_mol
+
+
+def build_ref_model(cfg):
+    m = GNN(FS, cfg["hidden_dim"], cfg["output_dim"], num_shells=cfg["num_shells"],
+            num_message_passing_layers=cfg["num_message_passing_layers"], ffn_num_layers=cfg["ffn_num_layers"],
+            pooling_type=cfg["pooling_type"], embedding_dim=cfg["embedding_dim"],
+            use_partial_charges=cfg["use_partial_charges"], activation_type=cfg["activation"],
+            shell_conv_num_mlp_layers=cfg["shell_conv_num_mlp_layers"], attention_num_heads=cfg["attention_num_heads"],
+            loss_function=cfg["loss_function"])
+    return m
+
+
+def run_case(name, cfg, mols, seed, grads="all", targets=None, charges=None, extra=None, intermediates=False):
+    torch.manual_seed(0)
+    b, per_mol = ref_batch(mols, cfg["num_shells"], targets, charges)
+    model = build_ref_model(cfg)
+    params = seeded_params(cfg, seed)
+    sd = model.state_dict()
+    assert list(sd.keys()) == list(params.keys()), "param order mismatch"
+    model.load_state_dict(params)
+    model.eval()
+    mp_in, mp_out = {}, {}
+    hooks = []
+    for l, layer in enumerate(model.message_passing_layers):
+        hooks.append(layer.register_forward_pre_hook(lambda m, a, l=l: mp_in.__setitem__(l, a[0].detach().clone())))
+        hooks.append(layer.register_forward_hook(lambda m, a, o, l=l: mp_out.__setitem__(l, o.detach().clone())))
+    af = b.atom_features_map
+    edges = b.multi_hop_edge_indices
+    out, attn, q = model(af, edges, b.batch_indices, b.total_charges,
+                         b.final_tetrahedral_chiral_tensor, b.final_cis_tensor, b.final_trans_tensor)
+    rng = np.random.default_rng(seed + 1000)
+    w = torch.tensor(rng.standard_normal(tuple(out.shape)), dtype=torch.float32)
+    loss = (out * w).sum()
+    model.zero_grad()
+    loss.backward()
+    for h in hooks:
+        h.remove()
+    rec = {
+        "cfg_json": np.array(repr(sorted(cfg.items()))),
+        "seed": np.array(seed),
+        "feats": np.stack([af[k].numpy() for k in ("atom_type", "hydrogen_count", "degree", "hybridization")], 1).astype(np.int8),
+        "edges": edges.numpy().astype(np.int32),
+        "batch": b.batch_indices.numpy().astype(np.int32),
+        "total_charges": b.total_charges.numpy().astype(np.float32),
+        "out": out.detach().numpy(),
+        "loss_w": w.numpy(),
+    }
+    if attn is not None:
+        rec["attn"] = attn.detach().numpy()
+    if q is not None:
+        rec["q"] = q.detach().numpy()
+    for l in (mp_out if intermediates else []):
+        rec[f"mp_in{l}"] = mp_in[l].numpy()
+        rec[f"mp_out{l}"] = mp_out[l].numpy()
+    if len(mp_in) and intermediates:
+        layer0 = model.message_passing_layers[0]
+        with torch.no_grad():
+            ch = layer0.message_passing(mp_in[0], edges[:, 0], edges[:, 1])
+        rec["chunks0"] = torch.cat(list(ch), 0).numpy()
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        if grads == "all" or any(k.startswith(s) for s in grads):
+            rec["grad." + k] = p.grad.numpy()
+    rec["n_mol_atoms"] = np.array([m[0] for m in mols], np.int32)
+    if extra:
+        rec.update(extra)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: N={rec['feats'].shape[0]} E={rec['edges'].shape[0]} G={len(mols)} -> {os.path.getsize(path)} B")
+
+
+def case_edges():
+    asset = QM9Asset()
+    mols = asset.molecules(range(64))
+    rec = {}
+    for hops in (3, 4, 6):
+        b, per_mol = ref_batch(mols, hops)
+        rec[f"edges_h{hops}"] = b.multi_hop_edge_indices.numpy().astype(np.int32)
+        rec[f"batch_h{hops}"] = b.batch_indices.numpy().astype(np.int32)
+        flat = [e for pm in per_mol for e in pm]
+        rec[f"hop_sizes_h{hops}"] = np.array([e.shape[1] for e in flat], np.int32)
+        rec[f"hop_pairs_h{hops}"] = (np.concatenate(flat, 1) if flat else np.empty((2, 0))).astype(np.int16)
+    syn = synth_molecules(8, seed=7)
+    b, per_mol = ref_batch(syn, 6)
+    rec["syn_edges_h6"] = b.multi_hop_edge_indices.numpy().astype(np.int32)
+    rec["syn_n_atoms"] = np.array([m[0] for m in syn], np.int32)
+    rec["syn_bonds"] = np.concatenate([m[1] for m in syn]).astype(np.int16)
+    rec["syn_n_bonds"] = np.array([len(m[1]) for m in syn], np.int32)
+    path = os.path.join(HERE, "edges.npz")
+    np.savez_compressed(path, **rec)
+    print("edges:", os.path.getsize(path))
+
+
+def case_mp_general():
+    """ShellConvolutionLayer with hop-offset targets, src >= N and negative src (layers.py:133-167)."""
+    rng = np.random.default_rng(11)
+    n, d, h, e = 50, 38, 3, 400
+    layer = ShellConvolutionLayer(d, d, num_hops=h)
+    params = {}
+    for k, p in layer.named_parameters():
+        r = np.random.default_rng([5, len(k), sum(map(ord, k))])
+        params[k] = torch.tensor(r.standard_normal(tuple(p.shape)) / (np.sqrt(p.shape[1]) if p.dim() == 2 else 10.0),
+                                 dtype=torch.float32)
+    layer.load_state_dict(params)
+    layer.eval()
+    x = torch.tensor(rng.standard_normal((n, d)), dtype=torch.float32, requires_grad=True)
+    tgt = torch.tensor(rng.integers(0, h * n, e), dtype=torch.long)
+    src = torch.tensor(rng.integers(-100, 300, e), dtype=torch.long)
+    with torch.no_grad():
+        chunks = torch.cat(list(layer.message_passing(x, tgt, src)), 0)
+    y = layer(x, tgt, src)
+    w = torch.tensor(rng.standard_normal(tuple(y.shape)), dtype=torch.float32)
+    (y * w).sum().backward()
+    rec = {"x": x.detach().numpy(), "tgt": tgt.numpy(), "src": src.numpy(), "chunks": chunks.numpy(),
+           "y": y.detach().numpy(), "w": w.numpy(), "grad_x": x.grad.numpy()}
+    for k, p in layer.named_parameters():
+        rec["param." + k] = params[k].numpy()
+        rec["grad." + k] = p.grad.numpy()
+    path = os.path.join(HERE, "mp_general.npz")
+    np.savez_compressed(path, **rec)
+    print("mp_general:", os.path.getsize(path))
+
+
+def case_attn_pool():
+    """MultiHeadAttentionPoolingLayer standalone with a loss on both outputs (pooling.py:122-172)."""
+    rng = np.random.default_rng(21)
+    sizes = [1, 5, 17, 3, 29, 2, 9]
+    n, c, hh = sum(sizes), 64, 4
+    batch = torch.tensor(np.repeat(np.arange(len(sizes)), sizes), dtype=torch.long)
+    pool = MultiHeadAttentionPoolingLayer(c, num_heads=hh, initial_temperature=0.7)
+    params = {}
+    for k, p in pool.named_parameters():
+        r = np.random.default_rng([9, sum(map(ord, k))])
+        params[k] = torch.tensor(r.standard_normal(tuple(p.shape)) * (0.3 if p.dim() else 0.1) + (0.8 if p.dim() == 0 else 0),
+                                 dtype=torch.float32)
+    pool.load_state_dict(params)
+    x = torch.tensor(rng.standard_normal((n, c)) * 2, dtype=torch.float32, requires_grad=True)
+    pooled, attn = pool(x, batch)
+    wp = torch.tensor(rng.standard_normal(tuple(pooled.shape)), dtype=torch.float32)
+    wa = torch.tensor(rng.standard_normal(tuple(attn.shape)), dtype=torch.float32)
+    ((pooled * wp).sum() + (attn * wa).sum()).backward()
+    rec = {"x": x.detach().numpy(), "batch": batch.numpy(), "pooled": pooled.detach().numpy(),
+           "attn": attn.detach().numpy(), "wp": wp.numpy(), "wa": wa.numpy(), "grad_x": x.grad.numpy()}
+    for k, p in pool.named_parameters():
+        rec["param." + k] = params[k].numpy()
+        rec["grad." + k] = p.grad.numpy()
+    path = os.path.join(HERE, "attn_pool.npz")
+    np.savez_compressed(path, **rec)
+    print("attn_pool:", os.path.getsize(path))
+
+
+def main():
+    torch.set_num_threads(8)
+    asset = QM9Asset()
+    case_edges()
+    case_mp_general()
+    case_attn_pool()
+    c1 = default_config(hidden_dim=128, num_shells=3, pooling_type="attention")
+    run_case("c1", c1, asset.molecules(range(32)), seed=1, intermediates=True)
+    c2 = default_config(hidden_dim=256, num_shells=3)
+    run_case("c2", c2, asset.molecules(range(512)), seed=2)
+    c3 = default_config(hidden_dim=256, num_shells=4, output_dim=12, use_partial_charges=True)
+    idx = np.arange(512, 1024)
+    run_case("c3", c3, asset.molecules(idx), seed=3, targets=asset.targets[idx],
+             charges=asset.total_charge[idx])
+    c4 = default_config(hidden_dim=512, num_shells=3)
+    run_case("c4s", c4, synth_molecules(16, seed=4), seed=4,
+             grads=("message_passing_layers.0.", "pooling.", "concat_self_other."))
+    c5 = default_config(hidden_dim=1024, num_shells=6)
+    run_case("c5s", c5, synth_molecules(4, seed=5), seed=5, grads=("pooling.",))
+    for kind in ("mean", "max", "sum"):
+        cfg = default_config(hidden_dim=128, num_shells=3, pooling_type=kind)
+        run_case(f"pool_{kind}", cfg, asset.molecules(range(32, 64)), seed=6,
+                 grads=("concat_self_other.", "message_passing_layers.2."))
+    for a in ("relu", "leakyrelu", "elu", "gelu"):
+        cfg = default_config(hidden_dim=128, num_shells=3, activation=a)
+        run_case(f"act_{a}", cfg, asset.molecules(range(64, 80)), seed=8,
+                 grads=("message_passing_layers.0.", "embedding_projection."))
+    cfg = default_config(hidden_dim=128, num_shells=3, loss_function="evidential", output_dim=2)
+    run_case("evidential", cfg, asset.molecules(range(80, 96)), seed=9, grads=("output_layer.",))
+    # E == 0: single-atom molecules -> message passing skipped (gnn.py:287)
+    single = [(1, np.zeros((0, 2), np.int32), np.array([[5, 4, 0, 3]], np.int64)) for _ in range(5)]
+    run_case("noedges", default_config(hidden_dim=128), single, seed=10, grads=("pooling.", "concat_self_other.", "embedding_projection."))
+
+
+if __name__ == "__main__":
+    main()
