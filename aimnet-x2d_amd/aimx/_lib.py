@@ -1,0 +1,150 @@
+"""ctypes binding of the C ABI in include/aimx.h (libaimx.so, HIP / gfx950).
+
+The library is built in-tree (`make -C aimnet-x2d_amd/csrc`, or __graft_entry__.build()). There is
+no fallback: if the library or a HIP device is missing, every op raises AimxError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libaimx.so")
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_u32 = ctypes.c_uint32
+c_f32 = ctypes.c_float
+c_ptr = ctypes.c_void_p
+c_size = ctypes.c_size_t
+
+ACT_KIND = {"relu": 0, "leakyrelu": 1, "elu": 2, "gelu": 3, "silu": 4}
+
+
+class AimxError(RuntimeError):
+    pass
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("A", c_ptr), ("sam", c_i64), ("sak", c_i64),
+        ("B", c_ptr), ("sbk", c_i64), ("sbn", c_i64),
+        ("C", c_ptr), ("ldc", c_i64),
+        ("beta", c_f32),
+        ("bias", c_ptr),
+        ("res", c_ptr * 3), ("ldres", c_i64 * 3),
+        ("act", c_i32), ("act_ncols", c_i64),
+        ("pre", c_ptr), ("ldpre", c_i64),
+        ("dact_pre", c_ptr), ("lddact", c_i64), ("dact_kind", c_i32),
+        ("drop_p", c_f32), ("drop_seed", c_ptr), ("drop_salt", c_u32),
+        ("mask_out", c_ptr), ("mask_in", c_ptr), ("ldmask", c_i64),
+        ("ones_col", c_i32), ("col_out", c_ptr),
+        ("splits", c_i32), ("workspace", c_ptr), ("workspace_bytes", c_size),
+    ]
+
+
+class ShellStack(ctypes.Structure):
+    _fields_ = [
+        ("N", c_i64), ("D", c_i64), ("num_hops", c_i64), ("num_layers", c_i64), ("num_mlp", c_i64),
+        ("act", c_i32), ("use_pc", c_i32), ("training", c_i32), ("mode_single", c_i32),
+        ("drop_p", c_f32), ("drop_seed", c_ptr),
+        ("fwd_rowptr", c_ptr), ("fwd_col", c_ptr), ("bwd_rowptr", c_ptr), ("bwd_col", c_ptr),
+        ("gptr", c_ptr), ("gperm", c_ptr), ("G", c_i64), ("total_charges", c_ptr),
+        ("w_ig", c_ptr), ("b_ig", c_ptr), ("w1", c_ptr), ("b1", c_ptr), ("w2", c_ptr), ("b2", c_ptr),
+        ("F", c_ptr), ("X", c_ptr), ("UG", c_ptr), ("U", c_ptr),
+        ("V", c_ptr), ("R", c_ptr), ("A", c_ptr), ("M", c_ptr),
+        ("x_in", c_ptr), ("x_in_ld", c_i64),
+        ("out", c_ptr), ("out_ld", c_i64),
+        ("workspace", c_ptr), ("workspace_bytes", c_size),
+    ]
+
+
+class ShellStackGrad(ctypes.Structure):
+    _fields_ = [
+        ("d_out", c_ptr), ("d_out_ld", c_i64),
+        ("d_x_in", c_ptr), ("d_x_in_ld", c_i64),
+        ("d_w_ig", c_ptr), ("d_b_ig", c_ptr), ("d_w1", c_ptr), ("d_b1", c_ptr), ("d_w2", c_ptr), ("d_b2", c_ptr),
+        ("dF", c_ptr), ("dUG", c_ptr), ("dT0", c_ptr), ("dT1", c_ptr), ("dT2", c_ptr), ("dT3", c_ptr),
+    ]
+
+
+_SIGS = {
+    "aimx_version": (ctypes.c_char_p, []),
+    "aimx_csr_workspace_bytes": (c_size, [c_i64, c_i64]),
+    "aimx_csr_build": (c_i32, [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_size,
+                               c_ptr, c_ptr]),
+    "aimx_segment_gather_sum": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i64,
+                                        c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_gemm_workspace_bytes": (c_size, [ctypes.POINTER(GemmArgs)]),
+    "aimx_gemm": (c_i32, [ctypes.POINTER(GemmArgs), c_ptr]),
+    "aimx_shell_stack_workspace_bytes": (c_size, [ctypes.POINTER(ShellStack)]),
+    "aimx_shell_stack_forward": (c_i32, [ctypes.POINTER(ShellStack), c_ptr]),
+    "aimx_shell_stack_backward": (c_i32, [ctypes.POINTER(ShellStack), ctypes.POINTER(ShellStackGrad), c_ptr]),
+    "aimx_partial_charge_forward": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                            c_ptr]),
+    "aimx_partial_charge_backward": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                             c_ptr, c_i64, c_ptr]),
+    "aimx_attn_pool_workspace_bytes": (c_size, [c_i64, c_i64, c_i64, c_i64]),
+    "aimx_attn_pool_forward": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                       c_ptr, c_ptr, c_ptr, c_ptr]),
+    "aimx_attn_pool_backward": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr,
+                                        c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
+    "aimx_segment_pool_forward": (c_i32, [c_i32, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
+                                          c_ptr]),
+    "aimx_segment_pool_backward": (c_i32, [c_i32, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                           c_ptr]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def load():
+    """Load libaimx.so (once). Raises AimxError if it is missing or incomplete."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AimxError(f"aimx: HIP library not built: {LIB_PATH} (run `make -C aimnet-x2d_amd/csrc`)")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        raise AimxError(f"aimx: cannot load {LIB_PATH}: {e}") from e
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            raise AimxError(f"aimx: {LIB_PATH} does not export {name}")
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        if rc < 0:
+            raise AimxError(f"aimx: {what}: invalid arguments (code {rc})")
+        raise AimxError(f"aimx: {what}: HIP error {rc}")
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise AimxError("aimx: tensors must live on the HIP device (MI355X); there is no CPU path")
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def ptr_array(tensors):
+    arr = (c_ptr * max(1, len(tensors)))(*[ptr(t) for t in tensors])
+    return arr

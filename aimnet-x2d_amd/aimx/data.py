@@ -1,0 +1,94 @@
+"""Host-side batch construction: multi-hop pair lists and the collate step.
+
+Product implementation of the two host stages that define the hot path's inputs:
+  * multi-hop BFS pair lists — reference src/datasets/features.py:82-150
+    (build_numba_adjacency_list + compute_multi_hop_edges_bfs_numba): hop 1 = every (v, w)
+    neighbour pair ordered by v then w; hop k expands the previous hop's frontier in order and
+    keeps first-visit (u, w) pairs, w != u;
+  * collate — reference src/datasets/molecular.py:339-458 (MyBatch.from_data_list): per-molecule
+    hop arrays offset by the molecule's atom offset ONLY (never by hop), concatenated molecule-
+    major then hop-major and transposed to [E, 2] int64; batch_indices = repeat(arange(G), atoms).
+Both are bit-exact against the reference (tests/test_data.py vs tests/golden/edges.npz).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
+
+
+def bfs_multi_hop(n_atoms, bonds, max_hops):
+    """List of `max_hops` int32 [2, E_h] arrays for one molecule (bonds: [B, 2] undirected)."""
+    nbr = [[] for _ in range(n_atoms)]
+    for a, b in np.asarray(bonds).reshape(-1, 2).tolist():
+        if a != b:
+            nbr[a].append(b)
+            nbr[b].append(a)
+    for lst in nbr:
+        lst.sort()
+    seen = set()
+    frontier = []
+    for v in range(n_atoms):
+        for w in nbr[v]:
+            key = v * n_atoms + w
+            if key not in seen:
+                seen.add(key)
+                frontier.append((v, w))
+    out = [frontier]
+    for _ in range(1, max_hops):
+        nxt = []
+        for u, v in frontier:
+            base = u * n_atoms
+            for w in nbr[v]:
+                if w != u and (base + w) not in seen:
+                    seen.add(base + w)
+                    nxt.append((u, w))
+        if not nxt:
+            out.append([])
+            break
+        out.append(nxt)
+        frontier = nxt
+    while len(out) < max_hops:
+        out.append([])
+    return [np.array(h, dtype=np.int32).reshape(-1, 2).T.copy() for h in out]
+
+
+def collate(mols, max_hops, hops=None):
+    """mols: list of (n_atoms, bonds, feats [n,4]). Returns numpy arrays of the collated batch."""
+    n_atoms = np.array([m[0] for m in mols], dtype=np.int64)
+    offsets = np.concatenate([[0], np.cumsum(n_atoms)[:-1]]).astype(np.int64)
+    parts = []
+    for i, (n, bonds, _) in enumerate(mols):
+        per = hops[i] if hops is not None else bfs_multi_hop(n, bonds, max_hops)
+        for e in per:
+            if e.shape[1]:
+                parts.append(e.astype(np.int64) + offsets[i])
+    edges = np.concatenate(parts, axis=1).T.copy() if parts else np.empty((0, 2), np.int64)
+    feats = np.concatenate([m[2] for m in mols], axis=0).astype(np.int64)
+    batch = np.repeat(np.arange(len(mols), dtype=np.int64), n_atoms)
+    return {"edges": edges, "feats": feats, "batch": batch, "n_atoms": n_atoms}
+
+
+class DeviceBatch:
+    """A collated batch resident in HBM, in the reference trainer's argument layout."""
+
+    def __init__(self, col, device, targets=None, total_charges=None):
+        self.atom_features = {k: torch.from_numpy(np.ascontiguousarray(col["feats"][:, i])).to(device)
+                              for i, k in enumerate(FEATURE_KEYS)}
+        self.edges = torch.from_numpy(col["edges"]).to(device)
+        self.batch = torch.from_numpy(col["batch"]).to(device)
+        g = len(col["n_atoms"])
+        self.num_graphs = g
+        self.num_atoms = int(col["batch"].shape[0])
+        tc = total_charges if total_charges is not None else np.zeros(g, np.float32)
+        self.total_charges = torch.from_numpy(np.asarray(tc, np.float32)).to(device)
+        tg = targets if targets is not None else np.zeros((g, 1), np.float32)
+        self.targets = torch.from_numpy(np.asarray(tg, np.float32)).to(device)
+        self.tetrahedral = torch.empty(0, 4, dtype=torch.long, device=device)
+        self.cis = torch.empty(0, 2, dtype=torch.long, device=device)
+        self.trans = torch.empty(0, 2, dtype=torch.long, device=device)
+
+    def model_args(self):
+        return (self.atom_features, self.edges, self.batch, self.total_charges, self.tetrahedral, self.cis,
+                self.trans)

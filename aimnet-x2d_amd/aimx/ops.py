@@ -1,0 +1,362 @@
+"""Autograd operators over the C ABI (include/aimx.h). HIP device only — no CPU fallback.
+
+Each operator corresponds to a reference interface:
+  message_passing_stack  <- GNN._message_passing_forward + ShellConvolutionLayer.forward
+                            (src/models/gnn.py:276-308, 622-658; src/models/layers.py:63-108)
+  hop                    <- ShellConvolutionLayer.message_passing (layers.py:133-167)
+  attention_pool         <- MultiHeadAttentionPoolingLayer.forward (pooling.py:122-172)
+  segment_pool           <- Mean/Max/SumPoolingLayer.forward (pooling.py:15-80)
+  partial_charges        <- GNN._partial_charge_calculation (gnn.py:622-658)
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import ShellStack, ShellStackGrad, check, ptr, ptr_array, stream_ptr
+
+_F32 = torch.float32
+
+
+class Arena:
+    """One allocation carved into 256-byte aligned views (fewer allocator round trips per step)."""
+
+    def __init__(self, device, dtype=_F32):
+        self.device, self.dtype = device, dtype
+        self.specs = []
+        self.total = 0
+
+    def add(self, *shape):
+        n = 1
+        for s in shape:
+            n *= int(s)
+        off = self.total
+        self.total += (n + 63) // 64 * 64
+        self.specs.append((off, n, shape))
+        return len(self.specs) - 1
+
+    def alloc(self):
+        buf = torch.empty(max(self.total, 64), dtype=self.dtype, device=self.device)
+        return buf, [buf.narrow(0, off, n).view(*shape) for off, n, shape in self.specs]
+
+
+def _rows(t):
+    """(tensor, leading dim) for a row-major-compatible 2-D view (stride(1) == 1)."""
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        return t, t.stride(0)
+    t = t.contiguous()
+    return t, t.shape[1]
+
+
+# ---------------------------------------------------------------------------------------------
+# Message-passing stack
+# ---------------------------------------------------------------------------------------------
+class _MPStack(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, plan, x_in, total_charges, drop_seed, *params):
+        lib = _lib.load()
+        dev = x_in.device
+        n, d, h, nl, nm = spec["N"], spec["D"], spec["num_hops"], spec["num_layers"], spec["num_mlp"]
+        k = d * (h + 1)
+        x_in, x_ld = _rows(x_in)
+        ar = Arena(dev)
+        iF = [ar.add(n, k) for _ in range(nl)]
+        iX = [ar.add(n, d) if (spec["use_pc"] and l > 0) else None for l in range(nl)]
+        iUG = [ar.add(n, 2 * d) for _ in range(nl)]
+        iU = [ar.add(n, d) for _ in range(nl)]
+        iV = [ar.add(n, d) for _ in range(nl * nm)]
+        iR = [ar.add(n, d) for _ in range(nl * nm)]
+        iA = [ar.add(n, d) if (j % nm) != nm - 1 else None for j in range(nl * nm)]
+        iOut = ar.add(n, d)
+        buf, views = ar.alloc()
+        F = [views[i] for i in iF]
+        X = [views[i] if i is not None else None for i in iX]
+        UG = [views[i] for i in iUG]
+        U = [views[i] for i in iU]
+        V = [views[i] for i in iV]
+        R = [views[i] for i in iR]
+        A = [views[i] if i is not None else None for i in iA]
+        out = views[iOut]
+        drop = bool(spec["training"]) and spec["drop_p"] > 0
+        M = [torch.empty(n, d, dtype=torch.uint8, device=dev) for _ in range(nl * nm)] if drop else []
+        w_ig = [params[l * (2 + 4 * nm)] for l in range(nl)]
+        b_ig = [params[l * (2 + 4 * nm) + 1] for l in range(nl)]
+        w1, b1, w2, b2 = [], [], [], []
+        for l in range(nl):
+            base = l * (2 + 4 * nm) + 2
+            for j in range(nm):
+                w1.append(params[base + 4 * j])
+                b1.append(params[base + 4 * j + 1])
+                w2.append(params[base + 4 * j + 2])
+                b2.append(params[base + 4 * j + 3])
+        s = ShellStack()
+        s.N, s.D, s.num_hops, s.num_layers, s.num_mlp = n, d, h, nl, nm
+        s.act, s.use_pc, s.training, s.mode_single = spec["act"], int(spec["use_pc"]), int(drop), int(spec["single"])
+        s.drop_p = float(spec["drop_p"]) if drop else 0.0
+        s.drop_seed = ptr(drop_seed) if drop else None
+        s.fwd_rowptr, s.fwd_col = ptr(plan.fwd.rowptr), ptr(plan.fwd.col)
+        s.bwd_rowptr, s.bwd_col = ptr(plan.bwd.rowptr), ptr(plan.bwd.col)
+        if plan.graph is not None:
+            s.gptr, s.gperm, s.G = ptr(plan.graph.rowptr), ptr(plan.graph.col), plan.G
+        s.total_charges = ptr(total_charges)
+        keep = [ptr_array(w_ig), ptr_array(b_ig), ptr_array(w1), ptr_array(b1), ptr_array(w2), ptr_array(b2),
+                ptr_array(F), ptr_array(X), ptr_array(UG), ptr_array(U), ptr_array(V), ptr_array(R), ptr_array(A),
+                ptr_array(M)]
+        (s.w_ig, s.b_ig, s.w1, s.b1, s.w2, s.b2, s.F, s.X, s.UG, s.U, s.V, s.R, s.A, s.M) = [
+            _ct_addr(a) for a in keep]
+        s.x_in, s.x_in_ld = ptr(x_in), x_ld
+        s.out, s.out_ld = ptr(out), d
+        wsb = lib.aimx_shell_stack_workspace_bytes(s)
+        ws = torch.empty(max(wsb // 4, 1), dtype=_F32, device=dev)
+        s.workspace, s.workspace_bytes = ptr(ws), wsb
+        check(lib.aimx_shell_stack_forward(s, stream_ptr(dev)), "shell_stack_forward")
+        ctx.spec, ctx.plan = spec, plan
+        ctx.state = dict(buf=buf, M=M, F=F, X=X, UG=UG, U=U, V=V, R=R, A=A, w_ig=w_ig, b_ig=b_ig, w1=w1, b1=b1,
+                         w2=w2, b2=b2, x_in=x_in, x_ld=x_ld, tc=total_charges, seed=drop_seed, ws=ws, drop=drop)
+        ctx.param_shapes = [p.shape for p in params]
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        lib = _lib.load()
+        st, spec, plan = ctx.state, ctx.spec, ctx.plan
+        dev = d_out.device
+        n, d, h, nl, nm = spec["N"], spec["D"], spec["num_hops"], spec["num_layers"], spec["num_mlp"]
+        k = d * (h + 1)
+        d_out, d_ld = _rows(d_out)
+        ar = Arena(dev)
+        i_dx = ar.add(n, d)
+        i_wig = [ar.add(2 * d, k) for _ in range(nl)]
+        i_big = [ar.add(2 * d) for _ in range(nl)]
+        i_w1 = [ar.add(d, d) for _ in range(nl * nm)]
+        i_b1 = [ar.add(d) for _ in range(nl * nm)]
+        i_w2 = [ar.add(d, d) for _ in range(nl * nm)]
+        i_b2 = [ar.add(d) for _ in range(nl * nm)]
+        i_dF, i_dUG = ar.add(n, k), ar.add(n, 2 * d)
+        i_T = [ar.add(n, d) for _ in range(4)]
+        buf, v = ar.alloc()
+        s = ShellStack()
+        s.N, s.D, s.num_hops, s.num_layers, s.num_mlp = n, d, h, nl, nm
+        s.act, s.use_pc, s.training, s.mode_single = spec["act"], int(spec["use_pc"]), int(st["drop"]), int(spec["single"])
+        s.drop_p = float(spec["drop_p"]) if st["drop"] else 0.0
+        s.drop_seed = ptr(st["seed"]) if st["drop"] else None
+        s.fwd_rowptr, s.fwd_col = ptr(plan.fwd.rowptr), ptr(plan.fwd.col)
+        s.bwd_rowptr, s.bwd_col = ptr(plan.bwd.rowptr), ptr(plan.bwd.col)
+        if plan.graph is not None:
+            s.gptr, s.gperm, s.G = ptr(plan.graph.rowptr), ptr(plan.graph.col), plan.G
+        s.total_charges = ptr(st["tc"])
+        keep = [ptr_array(st[nm_]) for nm_ in ("w_ig", "b_ig", "w1", "b1", "w2", "b2", "F", "X", "UG", "U", "V", "R",
+                                               "A", "M")]
+        (s.w_ig, s.b_ig, s.w1, s.b1, s.w2, s.b2, s.F, s.X, s.UG, s.U, s.V, s.R, s.A, s.M) = [
+            _ct_addr(a) for a in keep]
+        s.x_in, s.x_in_ld = ptr(st["x_in"]), st["x_ld"]
+        s.workspace, s.workspace_bytes = ptr(st["ws"]), st["ws"].numel() * 4
+        g = ShellStackGrad()
+        g.d_out, g.d_out_ld = ptr(d_out), d_ld
+        g.d_x_in, g.d_x_in_ld = ptr(v[i_dx]), d
+        dw_ig = [v[i] for i in i_wig]
+        db_ig = [v[i] for i in i_big]
+        dw1 = [v[i] for i in i_w1]
+        db1 = [v[i] for i in i_b1]
+        dw2 = [v[i] for i in i_w2]
+        db2 = [v[i] for i in i_b2]
+        gkeep = [ptr_array(x) for x in (dw_ig, db_ig, dw1, db1, dw2, db2)]
+        g.d_w_ig, g.d_b_ig, g.d_w1, g.d_b1, g.d_w2, g.d_b2 = [_ct_addr(a) for a in gkeep]
+        g.dF, g.dUG = ptr(v[i_dF]), ptr(v[i_dUG])
+        g.dT0, g.dT1, g.dT2, g.dT3 = [ptr(v[i]) for i in i_T]
+        check(lib.aimx_shell_stack_backward(s, g, stream_ptr(dev)), "shell_stack_backward")
+        grads = []
+        for l in range(nl):
+            grads += [dw_ig[l], db_ig[l]]
+            for j in range(nm):
+                idx = l * nm + j
+                grads += [dw1[idx], db1[idx], dw2[idx], db2[idx]]
+        del keep, gkeep, buf
+        return (None, None, v[i_dx], None, None, *grads)
+
+
+def _ct_addr(arr):
+    import ctypes
+    return ctypes.cast(arr, ctypes.c_void_p).value
+
+
+def message_passing_stack(plan, x, params, *, num_hops, num_layers, num_mlp, act, use_pc=False, total_charges=None,
+                          training=False, drop_p=0.0, drop_seed=None, single=False):
+    """params: per layer [w_ig (2D,K), b_ig (2D), then per MLP block w1, b1, w2, b2]."""
+    _lib.require_device(x)
+    if x.dtype != _F32:
+        raise _lib.AimxError("aimx: message passing runs in fp32 (the reference dtype)")
+    n, d = x.shape
+    spec = dict(N=n, D=d, num_hops=num_hops, num_layers=num_layers, num_mlp=num_mlp, act=_lib.ACT_KIND[act]
+                if isinstance(act, str) else int(act), use_pc=bool(use_pc), training=bool(training),
+                drop_p=float(drop_p), single=bool(single))
+    if use_pc and (plan.graph is None or total_charges is None):
+        raise _lib.AimxError("aimx: partial charges need batch indices and total charges")
+    tc = total_charges.contiguous().float() if total_charges is not None else None
+    return _MPStack.apply(spec, plan, x, tc, drop_seed, *params)
+
+
+# ---------------------------------------------------------------------------------------------
+# The hop alone (ShellConvolutionLayer.message_passing)
+# ---------------------------------------------------------------------------------------------
+class _Hop(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan, x):
+        lib = _lib.load()
+        n, d = x.shape
+        h = plan.num_hops
+        x, ldx = _rows(x)
+        out = torch.empty(h * n, d, dtype=_F32, device=x.device)
+        check(lib.aimx_segment_gather_sum(ptr(x), ldx, 0, 0, d, ptr(plan.fwd.rowptr), ptr(plan.fwd.col), h * n,
+                                          ptr(out), d, 0, 0, None, 0, None, 0, stream_ptr(x.device)), "hop_forward")
+        ctx.plan = plan
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        plan = ctx.plan
+        n = plan.N
+        g = g.contiguous()
+        d = g.shape[1]
+        dx = torch.empty(n, d, dtype=_F32, device=g.device)
+        check(lib.aimx_segment_gather_sum(ptr(g), d, 0, 0, d, ptr(plan.bwd.rowptr), ptr(plan.bwd.col), n, ptr(dx), d,
+                                          0, 0, None, 0, None, 0, stream_ptr(g.device)), "hop_backward")
+        return None, dx
+
+
+def hop(plan, x):
+    """[num_hops*N, D] = scatter_add(x[src % N], target) (bit-exact in edge order)."""
+    _lib.require_device(x)
+    return _Hop.apply(plan, x)
+
+
+# ---------------------------------------------------------------------------------------------
+# Attention pooling
+# ---------------------------------------------------------------------------------------------
+class _AttnPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan, x, W, b, tau):
+        lib = _lib.load()
+        x, ldx = _rows(x)
+        n, c = x.shape
+        H = W.shape[0]
+        G = plan.G
+        W = W.contiguous()
+        b = b.contiguous()
+        tau = tau.contiguous().float()
+        pooled = torch.empty(G, c, dtype=_F32, device=x.device)
+        attn = torch.empty(H, n, dtype=_F32, device=x.device)
+        scores = torch.empty(H, n, dtype=_F32, device=x.device)
+        check(lib.aimx_attn_pool_forward(ptr(x), ldx, n, c, ptr(W), ptr(b), ptr(tau), H, ptr(plan.graph.rowptr),
+                                         ptr(plan.graph.col), G, ptr(pooled), ptr(attn), ptr(scores),
+                                         stream_ptr(x.device)), "attn_pool_forward")
+        ctx.plan = plan
+        ctx.ldx = ldx
+        ctx.save_for_backward(x, W, tau, attn, scores)
+        return pooled, attn
+
+    @staticmethod
+    def backward(ctx, d_pooled, d_attn):
+        lib = _lib.load()
+        x, W, tau, attn, scores = ctx.saved_tensors
+        plan = ctx.plan
+        n, c = x.shape
+        H = W.shape[0]
+        G = plan.G
+        dev = x.device
+        if d_pooled is None:
+            d_pooled = torch.zeros(G, c, dtype=_F32, device=dev)
+        d_pooled = d_pooled.contiguous()
+        d_attn = d_attn.contiguous() if d_attn is not None else None
+        dx = torch.zeros(n, c, dtype=_F32, device=dev)
+        dW = torch.empty(H, c, dtype=_F32, device=dev)
+        db = torch.empty(H, dtype=_F32, device=dev)
+        dtau = torch.empty(1, dtype=_F32, device=dev)
+        wsb = lib.aimx_attn_pool_workspace_bytes(n, c, H, G)
+        ws = torch.empty(wsb // 4 + 1, dtype=_F32, device=dev)
+        check(lib.aimx_attn_pool_backward(ptr(x), ctx.ldx, n, c, ptr(W), ptr(tau), H, ptr(plan.graph.rowptr),
+                                          ptr(plan.graph.col), G, ptr(attn), ptr(scores), ptr(d_pooled), ptr(d_attn),
+                                          ptr(dx), c, ptr(dW), ptr(db), ptr(dtau), ptr(ws), wsb, stream_ptr(dev)),
+              "attn_pool_backward")
+        return None, dx, dW, db, dtau.view(())
+
+
+def attention_pool(plan, x, W, b, tau):
+    _lib.require_device(x, W, b, tau)
+    return _AttnPool.apply(plan, x, W, b, tau)
+
+
+# ---------------------------------------------------------------------------------------------
+# Mean / max / sum pooling
+# ---------------------------------------------------------------------------------------------
+_POOL_KIND = {"mean": 0, "max": 1, "sum": 2}
+
+
+class _SegPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan, kind, x):
+        lib = _lib.load()
+        x, ldx = _rows(x)
+        n, c = x.shape
+        G = plan.G
+        out = torch.empty(G, c, dtype=_F32, device=x.device)
+        am = torch.empty(G, c, dtype=torch.int32, device=x.device) if kind == 1 else None
+        check(lib.aimx_segment_pool_forward(kind, ptr(x), ldx, n, c, ptr(plan.graph.rowptr), ptr(plan.graph.col), G,
+                                            ptr(out), ptr(am), stream_ptr(x.device)), "segment_pool_forward")
+        ctx.plan, ctx.kind, ctx.n = plan, kind, n
+        ctx.am = am
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        plan = ctx.plan
+        g = g.contiguous()
+        c = g.shape[1]
+        dx = torch.zeros(ctx.n, c, dtype=_F32, device=g.device)
+        check(lib.aimx_segment_pool_backward(ctx.kind, ptr(g), ctx.n, c, ptr(plan.graph.rowptr), ptr(plan.graph.col),
+                                             plan.G, ptr(ctx.am), ptr(dx), c, stream_ptr(g.device)),
+              "segment_pool_backward")
+        return None, None, dx
+
+
+def segment_pool(plan, kind, x):
+    _lib.require_device(x)
+    return _SegPool.apply(plan, _POOL_KIND[kind], x)
+
+
+# ---------------------------------------------------------------------------------------------
+# Partial charges (standalone; fused inside the stack otherwise)
+# ---------------------------------------------------------------------------------------------
+class _Charges(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan, x, total_charges):
+        lib = _lib.load()
+        x, ldx = _rows(x)
+        n, d = x.shape
+        tc = total_charges.contiguous().float()
+        out = torch.empty(n, d, dtype=_F32, device=x.device)
+        check(lib.aimx_partial_charge_forward(ptr(x), ldx, n, d, ptr(plan.graph.rowptr), ptr(plan.graph.col), plan.G,
+                                              ptr(tc), ptr(out), d, stream_ptr(x.device)), "partial_charge_forward")
+        ctx.plan, ctx.ldx = plan, ldx
+        ctx.save_for_backward(x, tc)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        x, tc = ctx.saved_tensors
+        plan = ctx.plan
+        g = g.contiguous()
+        n, d = g.shape
+        dx = torch.zeros(n, d, dtype=_F32, device=g.device)
+        check(lib.aimx_partial_charge_backward(ptr(x), ctx.ldx, n, d, ptr(plan.graph.rowptr), ptr(plan.graph.col),
+                                               plan.G, ptr(tc), ptr(g), d, ptr(dx), d, stream_ptr(g.device)),
+              "partial_charge_backward")
+        return None, dx, None
+
+
+def partial_charges(plan, x, total_charges):
+    _lib.require_device(x, total_charges)
+    return _Charges.apply(plan, x, total_charges)

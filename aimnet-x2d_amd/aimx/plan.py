@@ -1,0 +1,98 @@
+"""Graph plan: the device-side CSR views of one collated batch, built once per forward.
+
+Inputs are the reference's own tensors (MyBatch.from_data_list, molecular.py:339-458):
+  multi_hop_edge_indices [E, 2] int64, column 0 = target, column 1 = source (gnn.py:302-306)
+  batch_indices [N] int64, molecule id per atom
+From them, on the device and without a host synchronisation (sizes come from tensor shapes and
+from total_charges.shape[0] = G):
+  fwd CSR: rows = num_hops*N keyed by target, col = source % N  (the hop, layers.py:154-163)
+  bwd CSR: rows = N keyed by source % N,   col = target          (the hop's backward)
+  graph CSR: rows = G keyed by batch index, col = atom id         (pooling / partial charges)
+All three keep ascending item order inside a row (stable), i.e. the reference summation order.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _lib
+
+_VALIDATE = os.environ.get("AIMX_VALIDATE", "0") == "1"
+
+
+def _col(t2d, j):
+    """(base pointer, element stride) of column j of an int64 [E, 2] tensor (any strides)."""
+    return t2d.data_ptr() + j * t2d.stride(1) * t2d.element_size(), t2d.stride(0)
+
+
+def _as_i64(t):
+    return t if t.dtype == torch.int64 else t.long()
+
+
+class CSR:
+    __slots__ = ("rowptr", "col", "rows")
+
+    def __init__(self, rowptr, col, rows):
+        self.rowptr, self.col, self.rows = rowptr, col, rows
+
+
+def build_csr(key_ptr, key_stride, key_mod, val_ptr, val_stride, val_mod, n_items, n_rows, device, status):
+    lib = _lib.load()
+    rowptr = torch.empty(n_rows + 1, dtype=torch.int32, device=device)
+    col = torch.empty(max(n_items, 1), dtype=torch.int32, device=device)
+    wsb = lib.aimx_csr_workspace_bytes(n_items, n_rows)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=device)
+    rc = lib.aimx_csr_build(key_ptr, key_stride, key_mod, val_ptr, val_stride, val_mod, n_items, n_rows,
+                            rowptr.data_ptr(), col.data_ptr(), ws.data_ptr(), wsb, status.data_ptr(),
+                            _lib.stream_ptr(device))
+    _lib.check(rc, "csr_build")
+    return CSR(rowptr, col, n_rows)
+
+
+class GraphPlan:
+    """CSR views for one batch. `edges` [E,2] (target, source) or separate target/src vectors."""
+
+    def __init__(self, num_atoms, num_hops, edges=None, target=None, src=None, batch=None, num_graphs=None):
+        self.N = int(num_atoms)
+        self.num_hops = int(num_hops)
+        ref = edges if edges is not None else (target if target is not None else batch)
+        self.device = ref.device
+        _lib.require_device(ref)
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.fwd = self.bwd = self.graph = None
+        if edges is not None:
+            e = _as_i64(edges)
+            self._keep = [e]
+            self.E = e.shape[0]
+            (t_ptr, t_st), (s_ptr, s_st) = _col(e, 0), _col(e, 1)
+        elif target is not None:
+            t, s = _as_i64(target), _as_i64(src)
+            self._keep = [t, s]
+            self.E = t.shape[0]
+            t_ptr, t_st, s_ptr, s_st = t.data_ptr(), t.stride(0), s.data_ptr(), s.stride(0)
+        else:
+            self._keep = []
+            self.E = 0
+            e = torch.zeros(0, 2, dtype=torch.int64, device=self.device)
+            (t_ptr, t_st), (s_ptr, s_st) = _col(e, 0), _col(e, 1)
+        if self.N > 0:  # E == 0 gives all-empty rows: every hop chunk is zero (layers.py:148-149)
+            n, h = self.N, self.num_hops
+            self.fwd = build_csr(t_ptr, t_st, 0, s_ptr, s_st, n, self.E, h * n, self.device, self.status)
+            self.bwd = build_csr(s_ptr, s_st, n, t_ptr, t_st, 0, self.E, n, self.device, self.status)
+        self.batch = batch
+        self.G = None
+        if batch is not None:
+            b = _as_i64(batch)
+            self._keep.append(b)
+            g = int(num_graphs) if num_graphs is not None else int(b.max().item()) + 1 if b.numel() else 0
+            self.G = g
+            self.graph = build_csr(b.data_ptr(), b.stride(0), 0, None, 0, 0, b.shape[0], g, self.device, self.status)
+        if _VALIDATE:
+            self.validate()
+
+    def validate(self):
+        """Synchronising check (opt-in via AIMX_VALIDATE=1): the reference raises on bad indices."""
+        if int(self.status.item()) != 0:
+            raise RuntimeError("aimx: index out of range in edge/batch tensors "
+                               "(target >= num_hops * N, or batch index >= num_graphs)")

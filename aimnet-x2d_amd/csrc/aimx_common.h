@@ -1,0 +1,86 @@
+// Internal helpers shared by the aimx HIP translation units (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/aimx.h"
+
+#define AIMX_CHECK_HIP(expr)                         \
+  do {                                               \
+    hipError_t _e = (expr);                          \
+    if (_e != hipSuccess) return (int)_e;            \
+  } while (0)
+
+#define AIMX_CHECK_LAUNCH() AIMX_CHECK_HIP(hipGetLastError())
+
+namespace aimx {
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Activation kinds (reference: src/utils/activation.py:9-34).
+enum Act : int { ACT_NONE = -1, ACT_RELU = 0, ACT_LEAKYRELU = 1, ACT_ELU = 2, ACT_GELU = 3, ACT_SILU = 4 };
+
+__device__ __forceinline__ float act_fwd(int kind, float v) {
+  switch (kind) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_LEAKYRELU: return v > 0.f ? v : 0.01f * v;
+    case ACT_ELU: return v > 0.f ? v : expm1f(v);
+    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case ACT_SILU: return v / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+// d act / d v evaluated at the pre-activation v (matches ATen's *_backward formulas).
+__device__ __forceinline__ float act_grad(int kind, float v) {
+  switch (kind) {
+    case ACT_RELU: return v > 0.f ? 1.f : 0.f;
+    case ACT_LEAKYRELU: return v > 0.f ? 1.f : 0.01f;
+    case ACT_ELU: return v > 0.f ? 1.f : expf(v);
+    case ACT_GELU: {
+      const float cdf = 0.5f * (1.f + erff(v * 0.70710678118654752f));
+      const float pdf = expf(-0.5f * v * v) * 0.39894228040143268f;
+      return cdf + v * pdf;
+    }
+    case ACT_SILU: {
+      const float s = 1.f / (1.f + expf(-v));
+      return s * (1.f + v * (1.f - s));
+    }
+    default: return 1.f;
+  }
+}
+
+// Counter-based hash for dropout masks: uniform in [0,1) from (seed, salt, index).
+__device__ __forceinline__ float hash_uniform(uint64_t seed, uint32_t salt, uint64_t idx) {
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(salt + 1)) ^ (idx * 0xD1B54A32D192ED03ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Internal launchers shared across translation units.
+int launch_gemm(const AimxGemmArgs& a, hipStream_t s);
+size_t gemm_workspace_floats(const AimxGemmArgs& a);
+int launch_charge_fwd(const float* x, int64_t ldx, int64_t N, int64_t D, const int32_t* gptr, const int32_t* gperm,
+                      int64_t G, const float* tc, float* out, int64_t ldo, hipStream_t s);
+int launch_charge_bwd(const float* x, int64_t ldx, int64_t N, int64_t D, const int32_t* gptr, const int32_t* gperm,
+                      int64_t G, const float* tc, const float* dout, int64_t ldd, float* dx, int64_t lddx,
+                      hipStream_t s);
+
+}  // namespace aimx

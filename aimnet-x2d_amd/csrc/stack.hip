@@ -1,0 +1,326 @@
+// Message-passing stack orchestration (host side of the C ABI): one call enqueues a whole
+// GNN._message_passing_forward (reference src/models/gnn.py:276-308) — per layer the partial
+// charges (gnn.py:622-658), the hop (layers.py:133-167) written straight into the column chunks
+// of the concatenated feature matrix F (layers.py:76-79, no cat), and the node-update MLP
+// (layers.py:82-106) as five fused MFMA GEMMs whose epilogues carry bias, activation, dropout,
+// the per-block residual, the global skip and the outer residual (gnn.py:302-306). The next
+// layer's input is written by the last GEMM directly into chunk 0 of the next layer's F.
+// The backward replays the same structure in reverse with fused act'/dropout epilogues, the
+// weight/bias gradients as split-K GEMMs with an implicit ones column, and the hop backward as
+// the same segmented gather-sum over the src-keyed CSR with the two residual terms fused.
+#include <algorithm>
+#include <cstring>
+
+#include "aimx_common.h"
+
+namespace aimx {
+namespace {
+
+AimxGemmArgs gemm0() {
+  AimxGemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.act = ACT_NONE;
+  a.dact_kind = ACT_NONE;
+  return a;
+}
+
+// C[M=rows, N=out] = X[rows, in] (ld ldx) . W[out, in]^T  (nn.Linear forward)
+AimxGemmArgs linear_fwd(int64_t rows, int64_t in, int64_t out, const float* X, int64_t ldx, const float* W,
+                        float* C, int64_t ldc) {
+  AimxGemmArgs a = gemm0();
+  a.M = rows;
+  a.N = out;
+  a.K = in;
+  a.A = X;
+  a.sam = ldx;
+  a.sak = 1;
+  a.B = W;
+  a.sbk = 1;
+  a.sbn = in;
+  a.C = C;
+  a.ldc = ldc;
+  return a;
+}
+
+// C[rows, in] = dY[rows, out] (ld) . W[out, in]  (input gradient)
+AimxGemmArgs linear_dx(int64_t rows, int64_t in, int64_t out, const float* dY, int64_t ldy, const float* W, float* C,
+                       int64_t ldc) {
+  AimxGemmArgs a = gemm0();
+  a.M = rows;
+  a.N = in;
+  a.K = out;
+  a.A = dY;
+  a.sam = ldy;
+  a.sak = 1;
+  a.B = W;
+  a.sbk = in;
+  a.sbn = 1;
+  a.C = C;
+  a.ldc = ldc;
+  return a;
+}
+
+// dW[out, in] = dY^T . X, db[out] = sum_rows dY  (weight + bias gradient, K = rows)
+AimxGemmArgs linear_dw(int64_t rows, int64_t in, int64_t out, const float* dY, int64_t ldy, const float* X,
+                       int64_t ldx, float* dW, float* db) {
+  AimxGemmArgs a = gemm0();
+  a.M = out;
+  a.N = in + 1;
+  a.K = rows;
+  a.A = dY;
+  a.sam = 1;
+  a.sak = ldy;
+  a.B = X;
+  a.sbk = ldx;
+  a.sbn = 1;
+  a.C = dW;
+  a.ldc = in;
+  a.ones_col = 1;
+  a.col_out = db;
+  return a;
+}
+
+struct Ws {
+  float* p;
+  size_t bytes;
+};
+
+int run(AimxGemmArgs a, const Ws& ws, hipStream_t s) {
+  a.workspace = ws.p;
+  a.workspace_bytes = ws.bytes;
+  return launch_gemm(a, s);
+}
+
+int gather(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D, const int32_t* rowptr,
+           const int32_t* col, int64_t rows, float* out, int64_t out_ld, int64_t out_rpc, int64_t out_cs,
+           const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld, hipStream_t s) {
+  return aimx_segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
+                                 add0_ld, add1, add1_ld, (aimx_stream_t)s);
+}
+
+bool valid(const AimxShellStack* s) {
+  if (!s || s->N < 0 || s->D < 1 || s->num_hops < 1 || s->num_layers < 1 || s->num_mlp < 1) return false;
+  if (s->mode_single && (s->num_layers != 1 || s->use_pc)) return false;
+  if (s->use_pc && (s->D < 2 || !s->gptr || !s->gperm || !s->total_charges)) return false;
+  return true;
+}
+
+#define RUN(expr)                 \
+  do {                            \
+    int _r = (expr);              \
+    if (_r != AIMX_OK) return _r; \
+  } while (0)
+
+}  // namespace
+}  // namespace aimx
+
+using namespace aimx;
+
+extern "C" size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s) {
+  if (!valid(s)) return 0;
+  const int64_t N = s->N, D = s->D, K = D * (s->num_hops + 1);
+  size_t need = 0;
+  // The largest split-K products: weight gradients with K = N rows.
+  AimxGemmArgs a = linear_dw(N, K, 2 * D, nullptr, 2 * D, nullptr, K, nullptr, nullptr);
+  need = std::max(need, gemm_workspace_floats(a));
+  a = linear_dw(N, D, D, nullptr, D, nullptr, D, nullptr, nullptr);
+  need = std::max(need, gemm_workspace_floats(a));
+  a = linear_fwd(N, K, 2 * D, nullptr, K, nullptr, nullptr, 2 * D);
+  need = std::max(need, gemm_workspace_floats(a));
+  a = linear_dx(N, K, 2 * D, nullptr, 2 * D, nullptr, nullptr, K);
+  need = std::max(need, gemm_workspace_floats(a));
+  return sizeof(float) * need + 256;
+}
+
+extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  if (!valid(s)) return AIMX_EARG;
+  const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
+  const int64_t K = D * (h + 1), D2 = 2 * D;
+  if (N == 0) return AIMX_OK;
+  const Ws ws{s->workspace, s->workspace_bytes};
+  const bool drop = s->training && s->drop_p > 0.f;
+  for (int64_t l = 0; l < L; ++l) {
+    float* F = s->F[l];
+    // 1) layer input -> chunk 0 of F (after partial charges when enabled)
+    if (s->use_pc) {
+      const float* raw = (l == 0) ? s->x_in : s->X[l];
+      const int64_t ldr = (l == 0) ? s->x_in_ld : D;
+      RUN(launch_charge_fwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, F, K, st));
+    } else if (l == 0) {
+      AIMX_CHECK_HIP(hipMemcpy2DAsync(F, sizeof(float) * K, s->x_in, sizeof(float) * s->x_in_ld, sizeof(float) * D, N,
+                                      hipMemcpyDeviceToDevice, st));
+    }
+    // 2) hop: chunks 1..h of F = scatter_add(x[src % N], target) in edge order
+    RUN(gather(F, K, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, K, N, D, nullptr, 0, nullptr, 0, st));
+    // 3) [u | g] = F [Wi ; Wg]^T + [bi ; bg], a0 = act(u)
+    {
+      AimxGemmArgs a = linear_fwd(N, K, D2, F, K, s->w_ig[l], s->UG[l], D2);
+      a.bias = s->b_ig[l];
+      a.act = s->act;
+      a.act_ncols = D;
+      a.pre = s->U[l];
+      a.ldpre = D;
+      RUN(run(a, ws, st));
+    }
+    // 4) MLP blocks
+    for (int64_t k = 0; k < nm; ++k) {
+      const int64_t idx = l * nm + k;
+      const float* in = (k == 0) ? s->UG[l] : s->A[idx - 1];
+      const int64_t ldin = (k == 0) ? D2 : D;
+      {
+        AimxGemmArgs a = linear_fwd(N, D, D, in, ldin, s->w1[idx], s->R[idx], D);
+        a.bias = s->b1[idx];
+        a.act = s->act;
+        a.act_ncols = D;
+        a.pre = s->V[idx];
+        a.ldpre = D;
+        if (drop) {
+          a.drop_p = s->drop_p;
+          a.drop_seed = s->drop_seed;
+          a.drop_salt = (uint32_t)idx;
+          a.mask_out = s->M[idx];
+          a.ldmask = D;
+        }
+        RUN(run(a, ws, st));
+      }
+      {
+        const bool last = (k == nm - 1);
+        float* dst;
+        int64_t ldd;
+        if (!last) {
+          dst = s->A[idx];
+          ldd = D;
+        } else if (l == L - 1) {
+          dst = s->out;
+          ldd = s->out_ld;
+        } else if (s->use_pc) {
+          dst = s->X[l + 1];
+          ldd = D;
+        } else {
+          dst = s->F[l + 1];
+          ldd = K;
+        }
+        AimxGemmArgs a = linear_fwd(N, D, D, s->R[idx], D, s->w2[idx], dst, ldd);
+        a.bias = s->b2[idx];
+        a.res[0] = in;  // per-block skip (layers.py:103)
+        a.ldres[0] = ldin;
+        if (last) {
+          a.res[1] = s->UG[l] + D;  // global skip (layers.py:106)
+          a.ldres[1] = D2;
+          if (!s->mode_single) {
+            a.res[2] = F;  // outer residual x (gnn.py:302-306), after partial charges
+            a.ldres[2] = K;
+          }
+        }
+        RUN(run(a, ws, st));
+      }
+    }
+  }
+  return AIMX_OK;
+}
+
+extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShellStackGrad* g, aimx_stream_t stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  if (!valid(s) || !g) return AIMX_EARG;
+  const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
+  const int64_t K = D * (h + 1), D2 = 2 * D;
+  if (N == 0) return AIMX_OK;
+  const Ws ws{s->workspace, s->workspace_bytes};
+  const bool drop = s->training && s->drop_p > 0.f;
+  float* T[3] = {g->dT1, g->dT2, g->dT3};
+  float* dV = g->dT0;
+  const float* dY = g->d_out;
+  int64_t ldy = g->d_out_ld;
+  int y_slot = -1;  // which T holds dY (-1: caller's d_out)
+  for (int64_t l = L - 1; l >= 0; --l) {
+    const float* F = s->F[l];
+    int free_slots[3], nf = 0;
+    for (int i = 0; i < 3; ++i)
+      if (i != y_slot) free_slots[nf++] = i;
+    // MLP blocks, last to first. da_out of the last block is dY.
+    const float* da_out = dY;
+    int64_t ld_out = ldy;
+    int ping = 0;
+    for (int64_t k = nm - 1; k >= 0; --k) {
+      const int64_t idx = l * nm + k;
+      const float* in = (k == 0) ? s->UG[l] : s->A[idx - 1];
+      const int64_t ldin = (k == 0) ? D2 : D;
+      {  // dV = (da_out W2) * mask/(1-p) * act'(V)
+        AimxGemmArgs a = linear_dx(N, D, D, da_out, ld_out, s->w2[idx], dV, D);
+        if (drop) {
+          a.drop_p = s->drop_p;
+          a.mask_in = s->M[idx];
+          a.ldmask = D;
+        }
+        a.dact_pre = s->V[idx];
+        a.lddact = D;
+        a.dact_kind = s->act;
+        RUN(run(a, ws, st));
+      }
+      RUN(run(linear_dw(N, D, D, da_out, ld_out, s->R[idx], D, g->d_w2[idx], g->d_b2[idx]), ws, st));
+      RUN(run(linear_dw(N, D, D, dV, D, in, ldin, g->d_w1[idx], g->d_b1[idx]), ws, st));
+      {  // da_in = da_out + dV W1 ; for k == 0 also * act'(u) -> du into dUG[:, :D]
+        float* dst;
+        int64_t ldd;
+        if (k == 0) {
+          dst = g->dUG;
+          ldd = D2;
+        } else {
+          dst = T[free_slots[ping]];
+          ldd = D;
+        }
+        AimxGemmArgs a = linear_dx(N, D, D, dV, D, s->w1[idx], dst, ldd);
+        a.res[0] = da_out;
+        a.ldres[0] = ld_out;
+        if (k == 0) {
+          a.dact_pre = s->U[l];
+          a.lddact = D;
+          a.dact_kind = s->act;
+        }
+        RUN(run(a, ws, st));
+        if (k != 0) {
+          da_out = dst;
+          ld_out = D;
+          ping ^= 1;
+        }
+      }
+    }
+    // dg = dY -> dUG[:, D:]
+    AIMX_CHECK_HIP(hipMemcpy2DAsync(g->dUG + D, sizeof(float) * D2, dY, sizeof(float) * ldy, sizeof(float) * D, N,
+                                    hipMemcpyDeviceToDevice, st));
+    RUN(run(linear_dw(N, K, D2, g->dUG, D2, F, K, g->d_w_ig[l], g->d_b_ig[l]), ws, st));
+    RUN(run(linear_dx(N, K, D2, g->dUG, D2, s->w_ig[l], g->dF, K), ws, st));
+    // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]
+    const bool first = (l == 0);
+    float* dst;
+    int64_t ldd;
+    if (s->use_pc) {
+      dst = T[free_slots[0]];
+      ldd = D;
+    } else if (first) {
+      dst = g->d_x_in;
+      ldd = g->d_x_in_ld;
+    } else {
+      dst = T[free_slots[1]];
+      ldd = D;
+    }
+    RUN(gather(g->dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, g->dF, K,
+               s->mode_single ? nullptr : dY, ldy, st));
+    int new_slot = s->use_pc ? -1 : (first ? -1 : free_slots[1]);
+    if (s->use_pc) {
+      const float* raw = first ? s->x_in : s->X[l];
+      const int64_t ldr = first ? s->x_in_ld : D;
+      float* pdst = first ? g->d_x_in : T[free_slots[1]];
+      const int64_t pld = first ? g->d_x_in_ld : D;
+      RUN(launch_charge_bwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, dst, D, pdst, pld, st));
+      new_slot = first ? -1 : free_slots[1];
+    }
+    if (!first) {
+      y_slot = new_slot;
+      dY = T[y_slot];
+      ldy = D;
+    }
+  }
+  return AIMX_OK;
+}

@@ -1,0 +1,197 @@
+"""Distributed utilities — drop-in for reference src/utils/distributed.py (12-228) plus the
+DDP-equivalent gradient synchronisation the hot path needs.
+
+The reference's helpers keep their names, arguments and rank-0 return conventions
+(gather_*_to_rank0 return the gathered data on rank 0 and an empty result elsewhere). On ROCm the
+"nccl" backend of torch.distributed is RCCL, which runs over xGMI inside an MI355X node.
+
+GradientSync replaces DistributedDataParallel's reducer (reference runner.py:703-707) for the
+hot loop: gradients are packed into flat fp32 buckets (<= bucket_mb each, reverse registration
+order, i.e. roughly the order backward produces them), each bucket is all-reduced with ONE RCCL
+call as soon as every gradient in it has been accumulated (post-accumulate-grad hooks), so the
+collectives overlap the rest of the backward, and finish() waits, averages (DDP semantics:
+sum / world_size) and writes the result back into .grad. Parameters whose gradient is still None
+after backward (e.g. the reference's never-used long_range_projection) are reduced as zeros and
+left None, as DDP(find_unused_parameters=True) leaves them. One process per GPU; molecules are
+sharded across ranks, so this all-reduce is the only data-path collective.
+"""
+import pickle
+from typing import Any, List
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _ready() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def is_main_process() -> bool:
+    """True on rank 0 or when torch.distributed is not initialised."""
+    return (not _ready()) or dist.get_rank() == 0
+
+
+def safe_get_rank() -> int:
+    return dist.get_rank() if _ready() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if _ready() else 1
+
+
+def gather_ndarray_to_rank0(arr: np.ndarray, device: str = "cpu") -> np.ndarray:
+    """All ranks' arrays (possibly different lengths) concatenated on rank 0 (as float32, like the
+    reference); other ranks get an empty array of the input dtype."""
+    if not _ready():
+        return arr
+    local = torch.from_numpy(arr).float().to(device)
+    n_local = torch.tensor([local.shape[0]], dtype=torch.long, device=device)
+    world = dist.get_world_size()
+    sizes = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(sizes, n_local)
+    n_max = max(int(s.item()) for s in sizes)
+    if local.shape[0] < n_max:
+        pad = torch.zeros((n_max - local.shape[0],) + tuple(local.shape[1:]), device=device)
+        local = torch.cat([local, pad], dim=0)
+    parts = [torch.zeros_like(local) for _ in range(world)]
+    dist.all_gather(parts, local)
+    if dist.get_rank() != 0:
+        return np.array([], dtype=arr.dtype)
+    return np.concatenate([p[: int(s.item())].cpu().numpy() for p, s in zip(parts, sizes)], axis=0)
+
+
+def _gather_bytes(payload: bytes, device: str):
+    world = dist.get_world_size()
+    n_local = torch.tensor([len(payload)], dtype=torch.long, device=device)
+    sizes = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(sizes, n_local)
+    n_max = max(int(s.item()) for s in sizes)
+    buf = torch.zeros(n_max, dtype=torch.uint8, device=device)
+    if payload:
+        buf[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
+    parts = [torch.zeros(n_max, dtype=torch.uint8, device=device) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    return [p[: int(s.item())].cpu().numpy().tobytes() for p, s in zip(parts, sizes)]
+
+
+def gather_strings_to_rank0(local_list: List[str], device: str = "cpu") -> List[str]:
+    """All ranks' string lists concatenated on rank 0 (rank order); [] elsewhere."""
+    if not _ready():
+        return local_list
+    chunks = _gather_bytes(pickle.dumps(local_list), device)
+    if dist.get_rank() != 0:
+        return []
+    out: List[str] = []
+    for c in chunks:
+        out.extend(pickle.loads(c))
+    return out
+
+
+def broadcast_object(obj: Any, src_rank: int = 0, device: str = "cpu") -> Any:
+    """Pickle-broadcast `obj` from `src_rank` to every rank."""
+    if not _ready():
+        return obj
+    rank = dist.get_rank()
+    payload = pickle.dumps(obj) if rank == src_rank else b""
+    size = torch.tensor([len(payload)], dtype=torch.long, device=device)
+    dist.broadcast(size, src=src_rank)
+    buf = torch.zeros(int(size.item()), dtype=torch.uint8, device=device)
+    if rank == src_rank and payload:
+        buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device))
+    dist.broadcast(buf, src=src_rank)
+    return obj if rank == src_rank else pickle.loads(buf.cpu().numpy().tobytes())
+
+
+def all_reduce_tensor(tensor: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """In-place all-reduce; op in {sum, mean, max, min} (mean = sum / world_size)."""
+    if not _ready():
+        return tensor
+    ops = {"sum": dist.ReduceOp.SUM, "mean": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+    if op not in ops:
+        raise ValueError(f"Unsupported operation: {op}")
+    dist.all_reduce(tensor, op=ops[op])
+    if op == "mean":
+        tensor /= dist.get_world_size()
+    return tensor
+
+
+def barrier() -> None:
+    if _ready():
+        dist.barrier()
+
+
+class GradientSync:
+    """Bucketed, backward-overlapped gradient all-reduce over one flat fp32 buffer per bucket.
+
+    usage:  sync = GradientSync(model.parameters())
+            loss.backward(); sync.finish(); clip; optimizer.step()
+    """
+
+    def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = process_group
+        self.world = dist.get_world_size(process_group) if _ready() else 1
+        self.overlap = overlap and self.world > 1
+        cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        self.buckets: List[List[torch.nn.Parameter]] = []
+        cur, size = [], 0
+        for p in reversed(self.params):  # backward produces late layers first
+            if cur and size + p.numel() > cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += p.numel()
+        if cur:
+            self.buckets.append(cur)
+        self._bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
+        self._flat = [None] * len(self.buckets)
+        self._pending = [0] * len(self.buckets)
+        self._handles = [None] * len(self.buckets)
+        self._hooks = []
+        if self.overlap:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._reset()
+
+    def _reset(self):
+        self._pending = [len(b) for b in self.buckets]
+        self._handles = [None] * len(self.buckets)
+
+    def _launch(self, i):
+        bucket = self.buckets[i]
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        self._flat[i] = flat
+        self._handles[i] = dist.all_reduce(flat, group=self.group, async_op=True)
+
+    def _on_grad(self, p):
+        i = self._bucket_of[id(p)]
+        self._pending[i] -= 1
+        if self._pending[i] == 0 and self._handles[i] is None:
+            self._launch(i)
+
+    def finish(self):
+        """Complete every bucket's all-reduce and write averaged gradients back into .grad."""
+        if self.world == 1:
+            self._reset()
+            return
+        for i in range(len(self.buckets)):
+            if self._handles[i] is None:
+                self._launch(i)
+        for i, bucket in enumerate(self.buckets):
+            self._handles[i].wait()
+            flat = self._flat[i].div_(self.world)
+            off = 0
+            for p in bucket:
+                n = p.numel()
+                if p.grad is not None:
+                    p.grad.copy_(flat[off:off + n].view_as(p))
+                off += n
+            self._flat[i] = None
+        self._reset()
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

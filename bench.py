@@ -1,0 +1,243 @@
+"""Throughput bench of the AIMNet-X2D hot path on MI355X (BASELINE.json metric).
+
+metric: molecules/sec of a full training step (forward + backward + grad-norm clip 1.0 + Adam,
+dropout on, L1 loss) on QM9-shaped batches, plus the achieved HBM GB/s of the scatter-add hop.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (default c2 = BASELINE configs[1]): QM9, hidden 256, 3 hops, 512 molecules per GPU per
+step, single task, attention pooling. Data: synthetic QM9-shaped batches resampled from the
+committed QM9-val graph asset (rng 1234 + rank), collated by aimx.data and resident in HBM
+before timing; weights random (GNN.init_weights). Each rank trains on its own molecules (weak
+scaling); gradients are averaged with one bucketed RCCL all-reduce per step (GradientSync).
+Rank 0 prints one JSON line. `roofline` times the hop kernel alone at the roofline size
+(4M QM9-shaped atoms, working set >> 256 MiB MALL) with HIP events on its launch stream;
+`cpu_baseline` times the oracle's CPU restatement of the reference train step (kind "port") on a
+bounded sample at N = 1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aimnet-x2d_amd")]
+
+from aimx import data as adata  # noqa: E402
+from aimx.synth import QM9Asset, synth_molecules  # noqa: E402
+
+CONFIGS = {
+    "c1": dict(source="qm9", hidden=128, hops=3, batch=32, tasks=1, pc=False),
+    "c2": dict(source="qm9", hidden=256, hops=3, batch=512, tasks=1, pc=False),
+    "c3": dict(source="qm9", hidden=256, hops=4, batch=512, tasks=12, pc=True),
+    "c4": dict(source="synth40", hidden=512, hops=3, batch=512, tasks=1, pc=False),
+    "c5": dict(source="synth40", hidden=1024, hops=6, batch=256, tasks=1, pc=False),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FS = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+
+
+def make_batches(cfg, n_batches, seed, device):
+    rng = np.random.default_rng(seed)
+    out = []
+    if cfg["source"] == "qm9":
+        asset = QM9Asset()
+        for _ in range(n_batches):
+            idx = rng.integers(0, len(asset), cfg["batch"])
+            col = adata.collate(asset.molecules(idx), cfg["hops"])
+            tg = asset.targets[idx][:, : cfg["tasks"]].astype(np.float32)
+            tg = (tg - tg.mean(0)) / (tg.std(0) + 1e-6)
+            out.append(adata.DeviceBatch(col, device, targets=tg, total_charges=asset.total_charge[idx]))
+    else:
+        for b in range(n_batches):
+            mols = synth_molecules(cfg["batch"], seed=int(rng.integers(1 << 30)))
+            col = adata.collate(mols, cfg["hops"])
+            tg = rng.standard_normal((cfg["batch"], cfg["tasks"])).astype(np.float32)
+            out.append(adata.DeviceBatch(col, device, targets=tg))
+    return out
+
+
+def build_model(cfg, device):
+    from models import GNN
+    m = GNN(FS, cfg["hidden"], cfg["tasks"], num_shells=cfg["hops"], use_partial_charges=cfg["pc"])
+    return m.to(device).train()
+
+
+def hop_roofline(batch, hops, device, target_atoms=4_000_000, launches=20):
+    """Time the hop kernel alone on a QM9-shaped graph of ~target_atoms atoms (tiled copies of a
+    real collated batch), with HIP events on the stream it is launched on."""
+    from aimx import ops
+    from aimx.plan import GraphPlan
+    n0 = batch.num_atoms
+    d = int(0.3 * 256)
+    reps = max(1, target_atoms // n0)
+    e0 = batch.edges
+    off = (torch.arange(reps, device=device, dtype=torch.int64) * n0).view(reps, 1, 1)
+    edges = (e0.unsqueeze(0) + off).reshape(-1, 2)
+    n = n0 * reps
+    e = edges.shape[0]
+    plan = GraphPlan(n, hops, edges=edges)
+    x = torch.randn(n, d, device=device)
+    del edges
+    torch.cuda.synchronize()
+    for _ in range(3):
+        ops.hop(plan, x)
+    stream = torch.cuda.current_stream()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record(stream)
+    for _ in range(launches):
+        ops.hop(plan, x)
+    t1.record(stream)
+    t1.synchronize()
+    ms = t0.elapsed_time(t1) / launches
+    alg_bytes = 4 * (n * d + e + (hops * n + 1) + hops * n * d)
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "hop_traffic.json")
+    if os.path.exists(tp):
+        try:
+            rec = json.load(open(tp))
+            if rec.get("atoms") == n and rec.get("edges") == e:
+                traffic = rec.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    del plan, x
+    torch.cuda.empty_cache()
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "k_gather_sum (hop fwd)", "atoms": n, "edges": e, "D": d, "hops": hops,
+            "algorithmic_bytes_per_launch": alg_bytes, "ms_per_launch": round(ms, 4)}
+
+
+def cpu_baseline(cfg, seconds=10.0, max_steps=40):
+    """Oracle CPU restatement of the reference train step (fwd+bwd+clip+Adam, dropout on)."""
+    from oracle import model as om
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    mcfg = om.default_config(hidden_dim=cfg["hidden"], num_shells=cfg["hops"], output_dim=cfg["tasks"],
+                             use_partial_charges=cfg["pc"])
+    params = {k: v.requires_grad_() for k, v in om.seeded_params(mcfg, 0).items()}
+    opt = torch.optim.Adam(params.values(), lr=2.5e-4)
+    b = make_batches(cfg, 1, 4321, "cpu")[0]
+    af, edges, batch, tc, _, _, _ = b.model_args()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out, _, _ = om.gnn_forward(params, mcfg, af, edges, batch, tc, training=True)
+        loss = torch.nn.functional.l1_loss(out, b.targets)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
+        opt.step()
+
+    step()
+    n, t0 = 0, time.perf_counter()
+    while n < max_steps and (time.perf_counter() - t0) < seconds:
+        step()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(cfg["batch"] * n / dt, 1), "unit": "molecules/s", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps x {cfg['batch']} molecules ({cfg['source']}, hidden {cfg['hidden']}, "
+                      f"{cfg['hops']} hops), oracle/model.py fp32 torch-CPU, {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--pool", type=int, default=8, help="distinct resident batches cycled per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true", help="only run the hop roofline launches (profiling)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    cfg = CONFIGS[args.config]
+    torch.manual_seed(1234 + rank)
+
+    batches = make_batches(cfg, args.pool, 1234 + rank, device)
+    if args.roofline_only:
+        print(json.dumps(hop_roofline(batches[0], cfg["hops"], device)))
+        return
+
+    from utils.distributed import GradientSync
+    model = build_model(cfg, device)
+    opt = torch.optim.Adam(model.parameters(), lr=2.5e-4)
+    sync = GradientSync(model.parameters()) if world > 1 else None
+    loss_fn = torch.nn.L1Loss()
+
+    def step(i):
+        b = batches[i % len(batches)]
+        opt.zero_grad(set_to_none=True)
+        out, _, _ = model(*b.model_args())
+        loss = loss_fn(out, b.targets)
+        loss.backward()
+        if sync is not None:
+            sync.finish()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    mol = cfg["batch"] * world * args.steps
+    value = mol / dt
+
+    roof = None
+    if rank == 0 and not args.no_roofline:
+        roof = hop_roofline(batches[0], cfg["hops"], device)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg)
+    if rank == 0:
+        atoms = sum(b.num_atoms for b in batches) / len(batches)
+        edges = sum(b.edges.shape[0] for b in batches) / len(batches)
+        line = {
+            "metric": "molecules/sec fwd+bwd on QM9-shaped batches; achieved HBM GB/s on scatter-add hop",
+            "value": round(value, 1), "unit": "molecules/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: " + ("QM9-shaped" if cfg["source"] == "qm9" else "40-atom synthetic")
+                       + f", hidden {cfg['hidden']}, {cfg['hops']} hops, {cfg['tasks']} task(s), attention pool, "
+                       "train step fwd+bwd+clip+Adam, dropout 0.05",
+                       "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
+                       "mean_atoms_per_batch": round(atoms, 1), "mean_edges_per_batch": round(edges, 1),
+                       "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        if cpu is not None:
+            line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,209 @@
+/*
+ * aimx.h — C ABI of the MI355X-native AIMNet-X2D message-passing / attention-pool hot path.
+ *
+ * Library: aimnet-x2d_amd/lib/libaimx.so (HIP, gfx950). Plain pointers and sizes only; every
+ * device pointer is a HIP device allocation owned by the caller (the PyTorch caching allocator in
+ * the Python mirror), and every call only ENQUEUES work on `stream` (a hipStream_t): no host
+ * synchronisation, no allocation, no global mutable state. Functions return 0 on success, a
+ * hipError_t value (> 0) if a HIP call failed, or AIMX_EARG (< 0) on invalid arguments.
+ *
+ * The reference (mahdi-shafiei/AIMNet-X2D) has no FFI: its hot path is pure PyTorch plus
+ * torch_scatter. Each entry point below names the reference interface it replaces; the Python
+ * mirror (aimnet-x2d_amd/models, aimnet-x2d_amd/utils) binds them with ctypes behind the
+ * reference's own module API.
+ */
+#ifndef AIMX_H_
+#define AIMX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* aimx_stream_t; /* hipStream_t */
+
+#define AIMX_OK 0
+#define AIMX_EARG (-1)
+
+/* Status bits written (OR-ed) into the optional device `status` word. */
+#define AIMX_STATUS_KEY_OUT_OF_RANGE 1 /* an index outside [0, n_rows): item dropped (reference raises) */
+
+/* Activation kinds (reference src/utils/activation.py:9-34). */
+#define AIMX_ACT_NONE (-1)
+#define AIMX_ACT_RELU 0
+#define AIMX_ACT_LEAKYRELU 1
+#define AIMX_ACT_ELU 2
+#define AIMX_ACT_GELU 3
+#define AIMX_ACT_SILU 4
+
+/* Library identity (for load checks): returns "aimx/<version>/gfx950". */
+const char* aimx_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Stable CSR build (device): rows sorted by key, ties kept in ascending item order — exactly the
+ * order in which CPU ATen scatter_add_ visits edges (reference layers.py:158 via torch_scatter
+ * scatter_add, and pooling.py:145/159 via scatter_softmax/scatter_sum). Replaces the implicit
+ * COO->segment step inside torch_scatter.
+ *   key(i) = key[i*key_stride], taken modulo key_mod (Python semantics) when key_mod > 0
+ *   val(i) = val ? val[i*val_stride] (mod val_mod) : i
+ *   rowptr[n_rows+1] (int32), col[n_items] (int32).
+ * Items with key outside [0, n_rows) are dropped and AIMX_STATUS_KEY_OUT_OF_RANGE is OR-ed into
+ * *status (if non-NULL) — the reference would raise an index error instead.
+ * ------------------------------------------------------------------------------------------ */
+size_t aimx_csr_workspace_bytes(int64_t n_items, int64_t n_rows);
+int aimx_csr_build(const int64_t* key, int64_t key_stride, int64_t key_mod,
+                   const int64_t* val, int64_t val_stride, int64_t val_mod,
+                   int64_t n_items, int64_t n_rows, int32_t* rowptr, int32_t* col,
+                   void* workspace, size_t workspace_bytes, int32_t* status, aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-hop scatter-add as a segmented gather-sum (the hop).
+ * Replaces ShellConvolutionLayer.message_passing (reference src/models/layers.py:133-167):
+ *   out[t,:] = sum over edges e with target_e == t of x[src_e % N, :], summed in edge order
+ * (bit-exact with the reference forward). The same kernel is the backward of the hop over the
+ * src-keyed CSR (grad_x[j] = sum over e with src_e % N == j of grad_out[target_e]).
+ * Row addressing (src and out): row r lives at base + (r % rows_per_chunk)*ld
+ * + (r / rows_per_chunk)*chunk_stride (rows_per_chunk <= 0: base + r*ld), so the output can be
+ * written straight into the column chunks of the concatenated [N, D*(h+1)] feature matrix
+ * (layers.py:76-79) without a cat. add0/add1 (nullable, indexed by output row, plain ld) are
+ * added to each output row (fused residual terms in the backward).
+ * ------------------------------------------------------------------------------------------ */
+int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rows_per_chunk,
+                            int64_t src_chunk_stride, int64_t D,
+                            const int32_t* rowptr, const int32_t* col, int64_t rows,
+                            float* out, int64_t out_ld, int64_t out_rows_per_chunk,
+                            int64_t out_chunk_stride,
+                            const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld,
+                            aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused fp32 GEMM on the matrix cores (v_mfma_f32_16x16x4_f32; exact f32 fmaf chains), the
+ * building block of the node-update MLP (reference layers.py:82-106, nn.Linear/addmm):
+ *   C(m,n) = epilogue( sum_k A(m,k) * B(k,n) )
+ *   A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]
+ * Epilogue, in order: (+ beta*C_old) (+ bias[n]) (+ res0 + res1 + res2) (pre <- v for
+ * n < act_ncols) (v = act(v) for n < act_ncols) (forward dropout with hash(seed, salt, m, n),
+ * mask written to mask_out) (v *= mask_in ? 1/(1-p) : 0) (v *= act'(dact_pre)) -> C.
+ * ones_col != 0: B gets an implicit all-ones column at n == N-1 and column N-1 of the result is
+ * written to col_out[m] instead of C (bias gradient fused into the weight-gradient GEMM).
+ * splits > 1: split-K with partial slabs in `workspace` and a deterministic ordered reduce.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct AimxGemmArgs {
+  int64_t M, N, K;
+  const float* A; int64_t sam, sak;
+  const float* B; int64_t sbk, sbn;
+  float* C; int64_t ldc;
+  float beta;
+  const float* bias;
+  const float* res[3]; int64_t ldres[3];
+  int32_t act; int64_t act_ncols;
+  float* pre; int64_t ldpre;
+  const float* dact_pre; int64_t lddact; int32_t dact_kind;
+  float drop_p; const int64_t* drop_seed; uint32_t drop_salt;
+  uint8_t* mask_out; const uint8_t* mask_in; int64_t ldmask;
+  int32_t ones_col; float* col_out;
+  int32_t splits; float* workspace; size_t workspace_bytes;
+} AimxGemmArgs;
+
+size_t aimx_gemm_workspace_bytes(const AimxGemmArgs* args);
+int aimx_gemm(const AimxGemmArgs* args, aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Message-passing stack: L x (partial charges?) -> ShellConvolutionLayer -> +x, fused.
+ * Replaces GNN._message_passing_forward (reference src/models/gnn.py:276-308) with
+ * ShellConvolutionLayer.forward (layers.py:63-108) and _partial_charge_calculation
+ * (gnn.py:622-658). All activations are kept for the backward in caller-owned buffers:
+ *   F[l]  [N, K=D*(h+1)]  concat features; column chunk 0 = layer input x_l (after charges)
+ *   X[l]  [N, D]          raw layer input before partial charges (use_pc only)
+ *   UG[l] [N, 2D]         [a0 | g] = [act(u) | global skip]       U[l] [N, D] = u (pre-act)
+ *   V[l*nm+k], R[l*nm+k], A[l*nm+k] [N, D]  per MLP block: pre-act, dropped act, block output
+ *   M[l*nm+k] [N, D] uint8 dropout masks (training && drop_p > 0)
+ * w_ig[l] is the stacked [input_proj.weight ; global_skip_proj.weight] ([2D, K]), b_ig[l] [2D].
+ * x_in [N, D] (ld x_in_ld) is the stack input; out [N, D] (ld out_ld) the output.
+ * mode_single != 0 runs one ShellConvolutionLayer.forward without the outer residual and without
+ * charges (the standalone layer API).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct AimxShellStack {
+  int64_t N, D, num_hops, num_layers, num_mlp;
+  int32_t act, use_pc, training, mode_single;
+  float drop_p; const int64_t* drop_seed;
+  const int32_t* fwd_rowptr; const int32_t* fwd_col; /* rows N*num_hops, col = src % N */
+  const int32_t* bwd_rowptr; const int32_t* bwd_col; /* rows N, col = target */
+  const int32_t* gptr; const int32_t* gperm; int64_t G; const float* total_charges;
+  const float* const* w_ig; const float* const* b_ig;
+  const float* const* w1; const float* const* b1; const float* const* w2; const float* const* b2;
+  float* const* F; float* const* X; float* const* UG; float* const* U;
+  float* const* V; float* const* R; float* const* A; uint8_t* const* M;
+  const float* x_in; int64_t x_in_ld;
+  float* out; int64_t out_ld;
+  float* workspace; size_t workspace_bytes;
+} AimxShellStack;
+
+typedef struct AimxShellStackGrad {
+  const float* d_out; int64_t d_out_ld;  /* grad w.r.t. out [N, D] */
+  float* d_x_in; int64_t d_x_in_ld;      /* grad w.r.t. x_in (written) */
+  float* const* d_w_ig; float* const* d_b_ig;   /* per layer [2D,K], [2D] (written) */
+  float* const* d_w1; float* const* d_b1; float* const* d_w2; float* const* d_b2;
+  /* scratch, caller-owned: dF [N,K], dUG [N,2D], dA, dV [N,D] x2, dX [N,D] x2 */
+  float* dF; float* dUG; float* dT0; float* dT1; float* dT2; float* dT3;
+} AimxShellStackGrad;
+
+size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s);
+int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t stream);
+int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShellStackGrad* g,
+                              aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Partial-charge equilibration (reference src/models/gnn.py:622-658), one molecule per
+ * workgroup over the graph CSR (gptr [G+1], gperm [N]).
+ * ------------------------------------------------------------------------------------------ */
+int aimx_partial_charge_forward(const float* x, int64_t ldx, int64_t N, int64_t D,
+                                const int32_t* gptr, const int32_t* gperm, int64_t G,
+                                const float* total_charges, float* out, int64_t ldo,
+                                aimx_stream_t stream);
+int aimx_partial_charge_backward(const float* x, int64_t ldx, int64_t N, int64_t D,
+                                 const int32_t* gptr, const int32_t* gperm, int64_t G,
+                                 const float* total_charges, const float* d_out, int64_t ldd,
+                                 float* d_x, int64_t lddx, aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-head attention graph pooling (reference src/models/pooling.py:122-172):
+ *   s[h,n] = (x_n . W[h] + b[h]) / tau ; a = per-molecule softmax of s over its atoms (per head,
+ *   torch_scatter.scatter_softmax) ; pooled[g] = mean_h sum_{n in g} a[h,n] x_n.
+ * One workgroup per molecule. tau is a device scalar (the learnable temperature). scores [H,N]
+ * is saved for the backward. The backward writes dx (every row), dW [H,C], db [H], dtau [1];
+ * d_attn (nullable) is an upstream gradient on the returned attention weights.
+ * ------------------------------------------------------------------------------------------ */
+size_t aimx_attn_pool_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t G);
+int aimx_attn_pool_forward(const float* x, int64_t ldx, int64_t N, int64_t C,
+                           const float* W, const float* b, const float* tau, int64_t H,
+                           const int32_t* gptr, const int32_t* gperm, int64_t G,
+                           float* pooled, float* attn, float* scores, aimx_stream_t stream);
+int aimx_attn_pool_backward(const float* x, int64_t ldx, int64_t N, int64_t C,
+                            const float* W, const float* tau, int64_t H,
+                            const int32_t* gptr, const int32_t* gperm, int64_t G,
+                            const float* attn, const float* scores,
+                            const float* d_pooled, const float* d_attn,
+                            float* dx, int64_t lddx, float* dW, float* db, float* dtau,
+                            void* workspace, size_t workspace_bytes, aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Mean / max / sum graph pooling (reference src/models/pooling.py:15-80, torch_scatter
+ * scatter_mean / scatter_max / scatter_add over molecules). kind: 0 = mean, 1 = max, 2 = sum.
+ * max records the first arg-max atom per (molecule, channel) for the backward (empty molecule:
+ * value 0, argmax = -1).
+ * ------------------------------------------------------------------------------------------ */
+int aimx_segment_pool_forward(int32_t kind, const float* x, int64_t ldx, int64_t N, int64_t C,
+                              const int32_t* gptr, const int32_t* gperm, int64_t G,
+                              float* out, int32_t* argmax, aimx_stream_t stream);
+int aimx_segment_pool_backward(int32_t kind, const float* d_out, int64_t N, int64_t C,
+                               const int32_t* gptr, const int32_t* gperm, int64_t G,
+                               const int32_t* argmax, float* dx, int64_t lddx,
+                               aimx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AIMX_H_ */

@@ -47,7 +47,7 @@ def message_passing(x, target, src, num_hops):
         return [torch.zeros_like(x) for _ in range(num_hops)]
     true_src = src % n
     rows = x[true_src]
-    agg = torch.zeros(num_hops * n, d, dtype=x.dtype).scatter_add_(
+    agg = torch.zeros(num_hops * n, d, dtype=x.dtype, device=x.device).scatter_add_(
         0, target.unsqueeze(1).expand(-1, d), rows)
     return list(torch.split(agg, n, dim=0))
 
@@ -74,8 +74,8 @@ def partial_charges(x, batch, total_charges):
     q, f, rest = x.split([1, 1, x.shape[-1] - 2], dim=-1)
     f = torch.clamp(f, min=1e-6)
     g = total_charges.shape[0]
-    qu = torch.zeros(g, 1, dtype=q.dtype).scatter_add(0, batch.unsqueeze(1), q)
-    fu = torch.zeros(g, 1, dtype=q.dtype).scatter_add(0, batch.unsqueeze(1), f) + 1e-6
+    qu = torch.zeros(g, 1, dtype=q.dtype, device=q.device).scatter_add(0, batch.unsqueeze(1), q)
+    fu = torch.zeros(g, 1, dtype=q.dtype, device=q.device).scatter_add(0, batch.unsqueeze(1), f) + 1e-6
     fu = torch.clamp(fu, min=1e-6)
     dq = total_charges.unsqueeze(-1) - qu
     f_new = f / fu[batch]
@@ -87,10 +87,10 @@ def segment_softmax(scores, batch, num_graphs):
     """torch_scatter.scatter_softmax along dim 1 of [H, N] (pooling.py:143-145)."""
     h, n = scores.shape
     idx = batch.unsqueeze(0).expand(h, n)
-    mx = torch.full((h, num_graphs), float("-inf"), dtype=scores.dtype).scatter_reduce(1, idx, scores, "amax", include_self=True)
+    mx = torch.full((h, num_graphs), float("-inf"), dtype=scores.dtype, device=scores.device).scatter_reduce(1, idx, scores, "amax", include_self=True)
     mx = torch.where(torch.isinf(mx) & (mx < 0), torch.zeros_like(mx), mx)
     e = (scores - mx.gather(1, idx)).exp()
-    s = torch.zeros(h, num_graphs, dtype=scores.dtype).scatter_add_(1, idx, e)
+    s = torch.zeros(h, num_graphs, dtype=scores.dtype, device=scores.device).scatter_add_(1, idx, e)
     return e / s.gather(1, idx)
 
 
@@ -102,21 +102,21 @@ def attention_pool(p, pre, x, batch, num_heads, num_graphs):
     a = segment_softmax(scores, batch, num_graphs)
     weighted = x.unsqueeze(0).expand(num_heads, -1, -1) * a.unsqueeze(-1)
     idx = batch.view(1, -1, 1).expand_as(weighted)
-    pooled = torch.zeros(num_heads, num_graphs, x.shape[1], dtype=x.dtype).scatter_add_(1, idx, weighted)
+    pooled = torch.zeros(num_heads, num_graphs, x.shape[1], dtype=x.dtype, device=x.device).scatter_add_(1, idx, weighted)
     return pooled.mean(dim=0), a
 
 
 def simple_pool(kind, x, batch, num_graphs):
     """pooling.py:15-80 (Mean / Max / Sum pooling via torch_scatter)."""
     idx = batch.unsqueeze(1).expand_as(x)
-    s = torch.zeros(num_graphs, x.shape[1], dtype=x.dtype).scatter_add_(0, idx, x)
+    s = torch.zeros(num_graphs, x.shape[1], dtype=x.dtype, device=x.device).scatter_add_(0, idx, x)
     if kind == "sum":
         return s
     if kind == "mean":
-        cnt = torch.zeros(num_graphs, dtype=x.dtype).scatter_add_(0, batch, torch.ones(x.shape[0], dtype=x.dtype)).clamp(min=1)
+        cnt = torch.zeros(num_graphs, dtype=x.dtype, device=x.device).scatter_add_(0, batch, torch.ones(x.shape[0], dtype=x.dtype, device=x.device)).clamp(min=1)
         return s / cnt.unsqueeze(1)
     if kind == "max":
-        m = torch.full((num_graphs, x.shape[1]), float("-inf"), dtype=x.dtype).scatter_reduce(0, idx, x, "amax", include_self=True)
+        m = torch.full((num_graphs, x.shape[1]), float("-inf"), dtype=x.dtype, device=x.device).scatter_reduce(0, idx, x, "amax", include_self=True)
         return torch.where(torch.isinf(m) & (m < 0), torch.zeros_like(m), m)
     raise ValueError(kind)
 

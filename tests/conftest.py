@@ -40,7 +40,7 @@ def golden():
 def _scale_for(key, ref64):
     """Gradients whose exact value is 0 (softmax shift invariance: d/db_h of the attention bias,
     pooling.py:136-145) are pure rounding noise; judge them against their sibling weight's scale."""
-    if key.startswith("grad.pooling.attention_weights.") and key.endswith(".bias"):
+    if ".attention_weights." in key and key.startswith("grad.") and key.endswith(".bias"):
         w = key[:-len("bias")] + "weight"
         if w in ref64:
             return float(np.abs(ref64[w]).max())

@@ -1,0 +1,348 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures and the oracle.
+
+Integer work (CSR / edge order) bit-exact; the hop forward bit-exact (same summation order as the
+reference's CPU scatter_add_); floating point per tensor within the north-star tolerance
+(conftest.parity_failures: <= max(1e-5, 3x the reference's own fp32 error vs fp64)).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, norm_rel, parity_failures
+from golden_cases import CASES, load_case
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import aimx
+    aimx.load()
+
+
+def _oracle():
+    from oracle import graph as og
+    from oracle import model as om
+    return og, om
+
+
+# ------------------------------------------------------------------------------------------ CSR
+@pytest.mark.parametrize("case", ["c1", "c2", "c3", "c5s"])
+def test_csr_bit_exact(case):
+    from aimx.plan import GraphPlan
+    og, _ = _oracle()
+    z = load_golden(case)
+    edges = torch.from_numpy(z["edges"].astype(np.int64)).to(DEV)
+    batch = torch.from_numpy(z["batch"].astype(np.int64)).to(DEV)
+    n = z["feats"].shape[0]
+    h = 6 if case == "c5s" else (4 if case == "c3" else 3)
+    g = len(z["n_mol_atoms"])
+    plan = GraphPlan(n, h, edges=edges, batch=batch, num_graphs=g)
+    e = z["edges"].astype(np.int64)
+    rp, col = og.stable_csr(e[:, 0], np.mod(e[:, 1], n), h * n)
+    assert np.array_equal(plan.fwd.rowptr.cpu().numpy(), rp)
+    assert np.array_equal(plan.fwd.col.cpu().numpy()[: len(col)], col)
+    rp, col = og.stable_csr(np.mod(e[:, 1], n), e[:, 0], n)
+    assert np.array_equal(plan.bwd.rowptr.cpu().numpy(), rp)
+    assert np.array_equal(plan.bwd.col.cpu().numpy()[: len(col)], col)
+    rp, col = og.stable_csr(z["batch"].astype(np.int64), np.arange(n), g)
+    assert np.array_equal(plan.graph.rowptr.cpu().numpy(), rp)
+    assert np.array_equal(plan.graph.col.cpu().numpy()[: len(col)], col)
+    assert int(plan.status.item()) == 0
+
+
+def test_csr_general_and_out_of_range():
+    from aimx.plan import GraphPlan
+    og, _ = _oracle()
+    rng = np.random.default_rng(3)
+    n, h, e = 1000, 4, 50000
+    t = rng.integers(0, h * n, e)
+    s = rng.integers(-5 * n, 5 * n, e)
+    plan = GraphPlan(n, h, target=torch.from_numpy(t).to(DEV), src=torch.from_numpy(s).to(DEV))
+    rp, col = og.stable_csr(t, np.mod(s, n), h * n)
+    assert np.array_equal(plan.fwd.rowptr.cpu().numpy(), rp)
+    assert np.array_equal(plan.fwd.col.cpu().numpy(), col)
+    assert int(plan.status.item()) == 0
+    t2 = t.copy()
+    t2[7] = h * n + 3  # the reference would raise: flagged and dropped, never a fault
+    plan = GraphPlan(n, h, target=torch.from_numpy(t2).to(DEV), src=torch.from_numpy(s).to(DEV))
+    assert int(plan.status.item()) == 1
+    with pytest.raises(RuntimeError):
+        plan.validate()
+
+
+def test_csr_large_rows_multiblock_scan():
+    from aimx.plan import GraphPlan
+    og, _ = _oracle()
+    rng = np.random.default_rng(4)
+    n, h, e = 700_000, 3, 2_000_000
+    t = rng.integers(0, h * n, e)
+    s = rng.integers(0, n, e)
+    plan = GraphPlan(n, h, target=torch.from_numpy(t).to(DEV), src=torch.from_numpy(s).to(DEV))
+    rp, col = og.stable_csr(t, s, h * n)
+    assert np.array_equal(plan.fwd.rowptr.cpu().numpy(), rp)
+    assert np.array_equal(plan.fwd.col.cpu().numpy(), col)
+
+
+# ------------------------------------------------------------------------------------------ hop
+def test_hop_forward_bit_exact_general():
+    """Hop-offset targets, src >= N and negative src (the general layers.py:133-167 contract)."""
+    from models.layers import ShellConvolutionLayer
+    z = load_golden("mp_general")
+    layer = ShellConvolutionLayer(38, 38, num_hops=3).to(DEV)
+    x = torch.from_numpy(z["x"]).to(DEV)
+    chunks = layer.message_passing(x, torch.from_numpy(z["tgt"]).to(DEV), torch.from_numpy(z["src"]).to(DEV))
+    assert np.array_equal(torch.cat(chunks, 0).cpu().numpy(), z["chunks"])
+
+
+@pytest.mark.parametrize("d", [38, 76, 153, 307, 64, 2])
+def test_hop_forward_bit_exact_widths(d):
+    """Every vector width path (float4 / float2 / scalar) is bit-exact vs CPU scatter_add_."""
+    from aimx.plan import GraphPlan
+    from aimx import ops
+    _, om = _oracle()
+    z = load_golden("c2")
+    e = torch.from_numpy(z["edges"].astype(np.int64))
+    n = z["feats"].shape[0]
+    x = torch.randn(n, d, generator=torch.Generator().manual_seed(d))
+    ref = torch.cat(om.message_passing(x, e[:, 0], e[:, 1], 3), 0)
+    plan = GraphPlan(n, 3, edges=e.to(DEV))
+    out = ops.hop(plan, x.to(DEV))
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_hop_backward():
+    from aimx.plan import GraphPlan
+    from aimx import ops
+    _, om = _oracle()
+    z = load_golden("mp_general")
+    x = torch.from_numpy(z["x"]).double().requires_grad_()
+    t, s = torch.from_numpy(z["tgt"]), torch.from_numpy(z["src"])
+    ref = torch.cat(om.message_passing(x, t, s, 3), 0)
+    w = torch.randn(ref.shape, dtype=torch.float64, generator=torch.Generator().manual_seed(1))
+    (ref * w).sum().backward()
+    xg = torch.from_numpy(z["x"]).to(DEV).requires_grad_()
+    plan = GraphPlan(50, 3, target=t.to(DEV), src=s.to(DEV))
+    out = ops.hop(plan, xg)
+    (out * w.float().to(DEV)).sum().backward()
+    assert norm_rel(xg.grad.cpu().numpy(), x.grad.numpy()) < 1e-6
+
+
+# ----------------------------------------------------------------------------------------- GEMM
+def _gemm(M, N, K, layout, **epi):
+    """Run aimx_gemm on random data; returns (C_gpu, inputs) for checking against torch fp64."""
+    import ctypes
+    from aimx import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g) if layout[0] == "N" else torch.randn(K, M, generator=g)
+    B = torch.randn(K, N, generator=g) if layout[1] == "N" else torch.randn(N, K, generator=g)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    ones = epi.get("ones", False)
+    Nt = N + 1 if ones else N
+    C = torch.zeros(M, N, device=DEV)
+    col = torch.zeros(M, device=DEV)
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = M, Nt, K
+    a.A = Ad.data_ptr()
+    a.sam, a.sak = (K, 1) if layout[0] == "N" else (1, M)
+    a.B = Bd.data_ptr()
+    a.sbk, a.sbn = (N, 1) if layout[1] == "N" else (1, K)
+    a.C, a.ldc = C.data_ptr(), N
+    a.act, a.dact_kind = -1, -1
+    bias = torch.randn(N, generator=g).to(DEV) if epi.get("bias") else None
+    if bias is not None:
+        a.bias = bias.data_ptr()
+    pre = torch.zeros(M, N, device=DEV)
+    if epi.get("act") is not None:
+        a.act, a.act_ncols, a.pre, a.ldpre = epi["act"], N, pre.data_ptr(), N
+    res = torch.randn(M, N, generator=g).to(DEV) if epi.get("res") else None
+    if res is not None:
+        a.res[0], a.ldres[0] = res.data_ptr(), N
+    if ones:
+        a.ones_col, a.col_out = 1, col.data_ptr()
+    a.splits = epi.get("splits", 0)
+    wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
+    ws = torch.empty(max(wsb // 4, 1) + 64 * 1024, device=DEV)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    assert lib.aimx_gemm(ctypes.byref(a), torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    Am = A if layout[0] == "N" else A.t()
+    Bm = B if layout[1] == "N" else B.t()
+    ref = Am.double() @ Bm.double()
+    if bias is not None:
+        ref = ref + bias.cpu().double()
+    if res is not None:
+        ref = ref + res.cpu().double()
+    return C.cpu(), col.cpu(), pre.cpu(), ref, Am
+
+
+@pytest.mark.parametrize("M,N,K,layout", [
+    (9170, 152, 304, "NT"), (9170, 76, 76, "NT"), (1000, 304, 152, "NN"), (153, 613, 2000, "TN"),
+    (17, 5, 3, "NT"), (64, 64, 16, "NN"), (307, 307, 10240, "TN"), (100, 2149, 614, "NN")])
+def test_gemm_layouts(M, N, K, layout):
+    C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True)
+    err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+
+
+def test_gemm_ones_column_bias_grad_and_splitk():
+    C, col, _, ref, Am = _gemm(76, 304, 9170, "TN", ones=True, splits=24)
+    assert (C.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    rs = Am.double().sum(1)
+    assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
+
+
+@pytest.mark.parametrize("act,fn", [(0, torch.relu), (1, lambda v: torch.nn.functional.leaky_relu(v, 0.01)),
+                                    (2, torch.nn.functional.elu), (3, torch.nn.functional.gelu),
+                                    (4, torch.nn.functional.silu)])
+def test_gemm_activation_epilogue(act, fn):
+    C, _, pre, ref, _ = _gemm(500, 76, 304, "NT", bias=True, act=act)
+    assert (pre.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    assert (C.double() - fn(ref)).abs().max().item() / fn(ref).abs().max().item() < 2e-6
+
+
+# --------------------------------------------------------------------------------------- layers
+def test_shell_layer_standalone():
+    from models.layers import ShellConvolutionLayer
+    z = load_golden("mp_general")
+    layer = ShellConvolutionLayer(38, 38, num_hops=3)
+    layer.load_state_dict({k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param.")})
+    layer = layer.to(DEV).eval()
+    x = torch.from_numpy(z["x"]).to(DEV).requires_grad_()
+    y = layer(x, torch.from_numpy(z["tgt"]).to(DEV), torch.from_numpy(z["src"]).to(DEV))
+    (y * torch.from_numpy(z["w"]).to(DEV)).sum().backward()
+    ours = {"y": y.detach().cpu().numpy(), "grad_x": x.grad.cpu().numpy()}
+    for k, p in layer.named_parameters():
+        ours["grad." + k] = p.grad.cpu().numpy()
+    ref = {k: z[k] for k in ours}
+    bad = parity_failures(ours, None, ref)
+    assert not bad, bad
+
+
+def test_attention_pool_standalone():
+    from models.pooling import MultiHeadAttentionPoolingLayer
+    _, om = _oracle()
+    z = load_golden("attn_pool")
+    params = {k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param.")}
+    pool = MultiHeadAttentionPoolingLayer(64, num_heads=4, initial_temperature=0.7)
+    pool.load_state_dict(params)
+    pool = pool.to(DEV)
+    x = torch.from_numpy(z["x"]).to(DEV).requires_grad_()
+    pooled, attn = pool(x, torch.from_numpy(z["batch"]).to(DEV))
+    ((pooled * torch.from_numpy(z["wp"]).to(DEV)).sum() + (attn * torch.from_numpy(z["wa"]).to(DEV)).sum()).backward()
+    ours = {"pooled": pooled.detach().cpu().numpy(), "attn": attn.detach().cpu().numpy(),
+            "grad_x": x.grad.cpu().numpy()}
+    for k, p in pool.named_parameters():
+        ours["grad." + k] = p.grad.cpu().numpy()
+    # fp64 oracle of the same layer
+    p64 = {"pool." + k: v.double().requires_grad_() for k, v in params.items()}
+    x64 = torch.from_numpy(z["x"]).double().requires_grad_()
+    b = torch.from_numpy(z["batch"])
+    pp, aa = om.attention_pool(p64, "pool.", x64, b, 4, int(b.max()) + 1)
+    ((pp * torch.from_numpy(z["wp"]).double()).sum() + (aa * torch.from_numpy(z["wa"]).double()).sum()).backward()
+    ref64 = {"pooled": pp.detach().numpy(), "attn": aa.detach().numpy(), "grad_x": x64.grad.numpy()}
+    ref64.update({"grad." + k[5:]: v.grad.numpy() for k, v in p64.items()})
+    bad = parity_failures(ours, {k: z[k] for k in ours}, ref64)
+    assert not bad, bad
+
+
+# ----------------------------------------------------------------------------------- full model
+def _build_model(cfg, seed):
+    from models import GNN
+    _, om = _oracle()
+    fs = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+    m = GNN(fs, cfg["hidden_dim"], cfg["output_dim"], num_shells=cfg["num_shells"],
+            num_message_passing_layers=cfg["num_message_passing_layers"], ffn_num_layers=cfg["ffn_num_layers"],
+            pooling_type=cfg["pooling_type"], embedding_dim=cfg["embedding_dim"],
+            use_partial_charges=cfg["use_partial_charges"], activation_type=cfg["activation"],
+            shell_conv_num_mlp_layers=cfg["shell_conv_num_mlp_layers"], attention_num_heads=cfg["attention_num_heads"],
+            loss_function=cfg["loss_function"])
+    m.load_state_dict(om.seeded_params(cfg, seed))
+    return m.to(DEV).eval()
+
+
+def _oracle_run(z, cfg, inputs, dtype):
+    _, om = _oracle()
+    af, edges, batch, tc = inputs
+    p = {k: v.to(dtype).requires_grad_() for k, v in om.seeded_params(cfg, int(z["seed"])).items()}
+    out, attn, q = om.gnn_forward(p, cfg, af, edges, batch, tc.to(dtype))
+    (out * torch.from_numpy(z["loss_w"]).to(dtype)).sum().backward()
+    res = {"out": out.detach().numpy()}
+    if attn is not None:
+        res["attn"] = attn.detach().numpy()
+    if q is not None:
+        res["q"] = q.detach().numpy()
+    for k, v in p.items():
+        if v.grad is not None:
+            res["grad." + k] = v.grad.numpy()
+    return res
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_model_case(name):
+    z, cfg, inputs = load_case(name)
+    torch.set_num_threads(8)
+    ref64 = _oracle_run(z, cfg, inputs, torch.float64)
+    ref32 = {k: z[k] for k in z.files if k in ("out", "attn", "q") or k.startswith("grad.")}
+    model = _build_model(cfg, int(z["seed"]))
+    af, edges, batch, tc = load_case(name, DEV)[2]
+    e_empty = torch.empty(0, 2, dtype=torch.long, device=DEV)
+    out, attn, q = model(af, edges, batch, tc, torch.empty(0, 4, dtype=torch.long, device=DEV), e_empty, e_empty)
+    (out * torch.from_numpy(z["loss_w"]).to(DEV)).sum().backward()
+    ours = {"out": out.detach().cpu().numpy()}
+    if attn is not None:
+        ours["attn"] = attn.detach().cpu().numpy()
+    if q is not None:
+        ours["q"] = q.detach().cpu().numpy()
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            ours["grad." + k] = p.grad.cpu().numpy()
+    # every gradient the reference produced must be produced here too
+    for k in ref32:
+        assert k in ours, k
+    bad = parity_failures(ours, ref32, ref64)
+    assert not bad, bad
+
+
+def test_forward_hooks_fire():
+    z, cfg, _ = load_case("c1")
+    model = _build_model(cfg, int(z["seed"]))
+    seen = {}
+    model.pooling.register_forward_hook(lambda m, a, o: seen.__setitem__("pool", o[0].shape))
+    model.concat_self_other.register_forward_hook(lambda m, a, o: seen.__setitem__("cat", o.shape))
+    af, edges, batch, tc = load_case("c1", DEV)[2]
+    e0 = torch.empty(0, 2, dtype=torch.long, device=DEV)
+    with torch.no_grad():
+        model(af, edges, batch, tc, torch.empty(0, 4, dtype=torch.long, device=DEV), e0, e0)
+    assert seen["pool"] == (32, cfg["hidden_dim"]) and seen["cat"][0] == z["feats"].shape[0]
+
+
+def test_train_mode_dropout_statistics_and_determinism():
+    """Dropout (p=0.05) in the fused epilogue: ~5% of block activations dropped; a fixed seed gives
+    identical results; eval mode is deterministic and dropout-free."""
+    from aimx import ops
+    from aimx.plan import GraphPlan
+    z, cfg, _ = load_case("c2")
+    model = _build_model(cfg, int(z["seed"]))
+    af, edges, batch, tc = load_case("c2", DEV)[2]
+    layers = model.message_passing_layers
+    params = []
+    for l in layers:
+        params += l._aimx_params()
+    n, d = z["feats"].shape[0], cfg["x_other_dim"]
+    x = torch.randn(n, d, device=DEV)
+    plan = GraphPlan(n, 3, edges=edges, batch=batch, num_graphs=512)
+    seed = torch.tensor([1234], device=DEV)
+    kw = dict(num_hops=3, num_layers=3, num_mlp=2, act="silu", training=True, drop_p=0.05, drop_seed=seed)
+    y1 = ops.message_passing_stack(plan, x, params, **kw)
+    y2 = ops.message_passing_stack(plan, x, params, **kw)
+    assert torch.equal(y1, y2)
+    y3 = ops.message_passing_stack(plan, x, params, **dict(kw, drop_seed=torch.tensor([99], device=DEV)))
+    assert not torch.equal(y1, y3)
+    y0 = ops.message_passing_stack(plan, x, params, **dict(kw, training=False))
+    assert not torch.equal(y0, y1)
