@@ -43,6 +43,7 @@ class GemmArgs(ctypes.Structure):
         ("mask_out", c_ptr), ("mask_in", c_ptr), ("ldmask", c_i64),
         ("ones_col", c_i32), ("col_out", c_ptr),
         ("splits", c_i32), ("workspace", c_ptr), ("workspace_bytes", c_size),
+        ("counters", c_ptr), ("n_counters", c_i64),
     ]
 
 
@@ -59,6 +60,7 @@ class ShellStack(ctypes.Structure):
         ("x_in", c_ptr), ("x_in_ld", c_i64),
         ("out", c_ptr), ("out_ld", c_i64),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
+        ("counters", c_ptr), ("n_counters", c_i64),
     ]
 
 
@@ -68,6 +70,13 @@ class ShellStackGrad(ctypes.Structure):
         ("d_x_in", c_ptr), ("d_x_in_ld", c_i64),
         ("d_w_ig", c_ptr), ("d_b_ig", c_ptr), ("d_w1", c_ptr), ("d_b1", c_ptr), ("d_w2", c_ptr), ("d_b2", c_ptr),
         ("dF", c_ptr), ("dUG", c_ptr), ("dT0", c_ptr), ("dT1", c_ptr), ("dT2", c_ptr), ("dT3", c_ptr),
+    ]
+
+
+class EmbeddingTables(ctypes.Structure):
+    _fields_ = [
+        ("n_tables", c_i32), ("dim", c_i64),
+        ("table", c_ptr * 8), ("index", c_ptr * 8), ("rows", c_i64 * 8), ("grad", c_ptr * 8),
     ]
 
 
@@ -96,6 +105,10 @@ _SIGS = {
                                           c_ptr]),
     "aimx_segment_pool_backward": (c_i32, [c_i32, c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                                            c_ptr]),
+    "aimx_embedding_gather": (c_i32, [ctypes.POINTER(EmbeddingTables), c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_embedding_backward_workspace_bytes": (c_size, [ctypes.POINTER(EmbeddingTables), c_i64]),
+    "aimx_embedding_backward": (c_i32, [ctypes.POINTER(EmbeddingTables), c_i64, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
+    "aimx_act_backward": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -139,6 +152,20 @@ def require_device(*tensors):
 
 def stream_ptr(device=None):
     return torch.cuda.current_stream(device).cuda_stream
+
+
+_COUNTERS = {}
+N_COUNTERS = 1 << 16
+
+
+def counters(device):
+    """Per-device split-K arrival counters: zeroed once, kept zero by the kernels themselves."""
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    buf = _COUNTERS.get(key)
+    if buf is None:
+        buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=device)
+        _COUNTERS[key] = buf
+    return buf
 
 
 def ptr(t):

@@ -109,6 +109,7 @@ class _MPStack(torch.autograd.Function):
         wsb = lib.aimx_shell_stack_workspace_bytes(s)
         ws = torch.empty(max(wsb // 4, 1), dtype=_F32, device=dev)
         s.workspace, s.workspace_bytes = ptr(ws), wsb
+        s.counters, s.n_counters = ptr(_lib.counters(dev)), _lib.N_COUNTERS
         check(lib.aimx_shell_stack_forward(s, stream_ptr(dev)), "shell_stack_forward")
         ctx.spec, ctx.plan = spec, plan
         ctx.state = dict(buf=buf, M=M, F=F, X=X, UG=UG, U=U, V=V, R=R, A=A, w_ig=w_ig, b_ig=b_ig, w1=w1, b1=b1,
@@ -151,6 +152,7 @@ class _MPStack(torch.autograd.Function):
             _ct_addr(a) for a in keep]
         s.x_in, s.x_in_ld = ptr(st["x_in"]), st["x_ld"]
         s.workspace, s.workspace_bytes = ptr(st["ws"]), st["ws"].numel() * 4
+        s.counters, s.n_counters = ptr(_lib.counters(dev)), _lib.N_COUNTERS
         g = ShellStackGrad()
         g.d_out, g.d_out_ld = ptr(d_out), d_ld
         g.d_x_in, g.d_x_in_ld = ptr(v[i_dx]), d
@@ -360,3 +362,172 @@ class _Charges(torch.autograd.Function):
 def partial_charges(plan, x, total_charges):
     _lib.require_device(x, total_charges)
     return _Charges.apply(plan, x, total_charges)
+
+
+# ---------------------------------------------------------------------------------------------
+# Dense layers on the fused fp32 MFMA GEMM (nn.Linear semantics, optional fused activation)
+# ---------------------------------------------------------------------------------------------
+def _gemm_args(M, N, K):
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.act, a.dact_kind = -1, -1
+    return a
+
+
+def _run_gemm(a, dev):
+    import ctypes
+    lib = _lib.load()
+    a.counters, a.n_counters = ptr(_lib.counters(dev)), _lib.N_COUNTERS
+    wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
+    ws = None
+    if wsb:
+        ws = torch.empty(wsb // 4 + 1, dtype=_F32, device=dev)
+        a.workspace, a.workspace_bytes = ws.data_ptr(), wsb
+    check(lib.aimx_gemm(ctypes.byref(a), stream_ptr(dev)), "gemm")
+    return ws
+
+
+def gemm_linear_fwd(x, ldx, W, b, out, ldo, act=-1, pre=None):
+    """out[M, n_out] = act(x[M, n_in] W^T + b)  (pre-activation to `pre` when act >= 0)."""
+    M, n_in = x.shape
+    n_out = W.shape[0]
+    a = _gemm_args(M, n_out, n_in)
+    a.A, a.sam, a.sak = ptr(x), ldx, 1
+    a.B, a.sbk, a.sbn = ptr(W), 1, n_in
+    a.C, a.ldc = ptr(out), ldo
+    a.bias = ptr(b)
+    if act >= 0:
+        a.act, a.act_ncols = act, n_out
+        if pre is not None:
+            a.pre, a.ldpre = ptr(pre), n_out
+    return _run_gemm(a, x.device)
+
+
+def gemm_linear_bwd(dy, ldy, x, ldx, W, dx, dW, db):
+    """dx = dy W ; dW = dy^T x ; db = sum_rows dy (ones-column fusion, split-K)."""
+    M, n_out = dy.shape
+    n_in = W.shape[1]
+    dev = dy.device
+    if dx is not None:
+        a = _gemm_args(M, n_in, n_out)
+        a.A, a.sam, a.sak = ptr(dy), ldy, 1
+        a.B, a.sbk, a.sbn = ptr(W), n_in, 1
+        a.C, a.ldc = ptr(dx), n_in
+        _run_gemm(a, dev)
+    a = _gemm_args(n_out, n_in + 1, M)
+    a.A, a.sam, a.sak = ptr(dy), 1, ldy
+    a.B, a.sbk, a.sbn = ptr(x), ldx, 1
+    a.C, a.ldc = ptr(dW), n_in
+    a.ones_col, a.col_out = 1, ptr(db)
+    _run_gemm(a, dev)
+
+
+def act_backward(kind, dy, pre):
+    lib = _lib.load()
+    dy, ldy = _rows(dy)
+    out = torch.empty(pre.shape, dtype=_F32, device=pre.device)
+    check(lib.aimx_act_backward(kind, ptr(dy), ldy, ptr(pre), pre.shape[1], pre.shape[0], pre.shape[1], ptr(out),
+                                pre.shape[1], stream_ptr(pre.device)), "act_backward")
+    return out
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b, act):
+        shape = x.shape
+        x2, ldx = _rows(x.reshape(-1, shape[-1]))
+        M = x2.shape[0]
+        out = torch.empty(M, W.shape[0], dtype=_F32, device=x.device)
+        pre = torch.empty_like(out) if act >= 0 else None
+        gemm_linear_fwd(x2, ldx, W.contiguous(), b.contiguous() if b is not None else None, out, W.shape[0], act, pre)
+        ctx.act, ctx.ldx, ctx.shape, ctx.has_b = act, ldx, shape, b is not None
+        ctx.save_for_backward(x2, W, pre)
+        return out.view(*shape[:-1], W.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, W, pre = ctx.saved_tensors
+        dy2 = dy.reshape(-1, W.shape[0])
+        if ctx.act >= 0:
+            dy2 = act_backward(ctx.act, dy2, pre)
+        dy2, ldy = _rows(dy2)
+        dx = torch.empty(x2.shape[0], W.shape[1], dtype=_F32, device=dy.device) if ctx.needs_input_grad[0] else None
+        dW = torch.empty_like(W)
+        db = torch.empty(W.shape[0], dtype=_F32, device=dy.device)
+        gemm_linear_bwd(dy2, ldy, x2, ctx.ldx, W.contiguous(), dx, dW, db)
+        dx = dx.view(*ctx.shape[:-1], W.shape[1]) if dx is not None else None
+        return dx, dW, (db if ctx.has_b else None), None
+
+
+def linear(x, W, b=None, act=None):
+    """y = act(x W^T + b) on the MFMA GEMM (act: None or an activation name)."""
+    _lib.require_device(x, W)
+    kind = -1 if act is None else (_lib.ACT_KIND[act] if isinstance(act, str) else int(act))
+    if b is None:
+        raise _lib.AimxError("aimx.linear: bias-free layers are not used on the hot path")
+    return _Linear.apply(x, W, b, kind)
+
+
+# ---------------------------------------------------------------------------------------------
+# Atom-feature embeddings + projection (gnn.py:221-225 fused)
+# ---------------------------------------------------------------------------------------------
+def _tables_struct(indices, tables, grads=None):
+    t = _lib.EmbeddingTables()
+    t.n_tables = len(tables)
+    t.dim = tables[0].shape[1]
+    for i, (ix, tb) in enumerate(zip(indices, tables)):
+        t.table[i] = ptr(tb)
+        t.index[i] = ptr(ix)
+        t.rows[i] = tb.shape[0]
+        if grads is not None:
+            t.grad[i] = ptr(grads[i])
+    return t
+
+
+class _EmbedProject(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, indices, act, W, b, *tables):
+        import ctypes
+        lib = _lib.load()
+        dev = W.device
+        idx = [i if i.dtype == torch.int64 else i.long() for i in indices]
+        idx = [i.contiguous() for i in idx]
+        tables = [t.contiguous() for t in tables]
+        n = idx[0].shape[0]
+        width = len(tables) * tables[0].shape[1]
+        E = torch.empty(n, width, dtype=_F32, device=dev)
+        ts = _tables_struct(idx, tables)
+        check(lib.aimx_embedding_gather(ctypes.byref(ts), n, ptr(E), width, stream_ptr(dev)), "embedding_gather")
+        out = torch.empty(n, W.shape[0], dtype=_F32, device=dev)
+        pre = torch.empty_like(out) if act >= 0 else None
+        gemm_linear_fwd(E, width, W.contiguous(), b.contiguous(), out, W.shape[0], act, pre)
+        ctx.act = act
+        ctx.idx = idx
+        ctx.save_for_backward(E, W, pre, *tables)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        import ctypes
+        lib = _lib.load()
+        E, W, pre, *tables = ctx.saved_tensors
+        dev = dy.device
+        dpre = act_backward(ctx.act, dy, pre) if ctx.act >= 0 else dy.contiguous()
+        dE = torch.empty_like(E)
+        dW = torch.empty_like(W)
+        db = torch.empty(W.shape[0], dtype=_F32, device=dev)
+        gemm_linear_bwd(dpre, dpre.shape[1], E, E.shape[1], W.contiguous(), dE, dW, db)
+        grads = [torch.empty_like(t) for t in tables]
+        ts = _tables_struct(ctx.idx, tables, grads)
+        wsb = lib.aimx_embedding_backward_workspace_bytes(ctypes.byref(ts), E.shape[0])
+        ws = torch.empty(wsb // 4 + 1, dtype=_F32, device=dev)
+        check(lib.aimx_embedding_backward(ctypes.byref(ts), E.shape[0], ptr(dE), dE.shape[1], ptr(ws), wsb,
+                                          stream_ptr(dev)), "embedding_backward")
+        return (None, None, dW, db, *grads)
+
+
+def embed_project(indices, tables, W, b, act=None):
+    """act(cat_t(table_t[indices_t]) W^T + b) — gather, GEMM and activation on the device."""
+    _lib.require_device(W, *indices)
+    kind = -1 if act is None else _lib.ACT_KIND[act]
+    return _EmbedProject.apply(list(indices), kind, W, b, *tables)

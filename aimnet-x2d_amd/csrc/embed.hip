@@ -1,0 +1,145 @@
+// Atom-feature embeddings (reference src/models/gnn.py:262-274: four nn.Embedding lookups + cat)
+// and elementwise activation backward.
+//
+// Forward: E[j, t*dim + c] = table_t[index_t[j], c] — one coalesced pass writing the concatenated
+// [N, T*dim] matrix the embedding projection GEMM consumes.
+// Backward (deterministic, no float atomics): the tables are tiny (119/9/7/7 rows x 64), so each
+// workgroup accumulates a chunk of atoms into a private copy of ALL tables in LDS — thread (t, c)
+// owns column c of table t, so it is the only writer of those LDS words and adds its chunk's
+// rows in atom order — then writes the partial tables; a second kernel sums the partials in
+// chunk order. PyTorch's embedding backward instead sorts the indices (radix sort + segment
+// offsets, several launches per table).
+#include <algorithm>
+
+#include "aimx_common.h"
+
+namespace aimx {
+namespace {
+
+constexpr int kChunk = 256;  // atoms per workgroup in the backward
+
+__global__ void k_embed_gather(AimxEmbeddingTables t, int64_t N, float* __restrict__ out, int64_t ldo) {
+  const int64_t width = (int64_t)t.n_tables * t.dim;
+  const int64_t total = N * width;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = i / width, k = i - j * width;
+    const int tb = (int)(k / t.dim);
+    const int64_t c = k - (int64_t)tb * t.dim;
+    const int64_t r = t.index[tb][j];
+    out[j * ldo + k] = (r >= 0 && r < t.rows[tb]) ? t.table[tb][r * t.dim + c] : 0.f;
+  }
+}
+
+// blockDim.x == n_tables * dim (<= 1024); dynamic LDS = total_rows * dim floats.
+__global__ void k_embed_bwd_partial(AimxEmbeddingTables t, int64_t N, const float* __restrict__ dE, int64_t ldd,
+                                    float* __restrict__ partial, int64_t total_rows) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tb = threadIdx.x / (int)t.dim;
+  const int c = threadIdx.x - tb * (int)t.dim;
+  int64_t row0 = 0;
+  for (int i = 0; i < tb; ++i) row0 += t.rows[i];
+  for (int64_t i = threadIdx.x; i < total_rows * t.dim; i += blockDim.x) lds[i] = 0.f;
+  __syncthreads();
+  const int64_t j0 = (int64_t)blockIdx.x * kChunk, j1 = min(N, j0 + kChunk);
+  const int64_t rows_tb = t.rows[tb];
+  const int64_t* __restrict__ idx = t.index[tb];
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = idx[j];
+    if (r >= 0 && r < rows_tb) lds[(row0 + r) * t.dim + c] += dE[j * ldd + (int64_t)tb * t.dim + c];
+  }
+  __syncthreads();
+  float* out = partial + (int64_t)blockIdx.x * total_rows * t.dim;
+  for (int64_t i = threadIdx.x; i < total_rows * t.dim; i += blockDim.x) out[i] = lds[i];
+}
+
+__global__ void k_embed_bwd_reduce(AimxEmbeddingTables t, const float* __restrict__ partial, int64_t nblk,
+                                   int64_t total_rows) {
+  const int64_t total = total_rows * t.dim;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t b = 0; b < nblk; ++b) s += partial[b * total + i];
+    int64_t r = i / t.dim;
+    const int64_t c = i - r * t.dim;
+    int tb = 0;
+    while (r >= t.rows[tb]) r -= t.rows[tb++];
+    t.grad[tb][r * t.dim + c] = s;
+  }
+}
+
+__global__ void k_act_bwd(int kind, const float* __restrict__ dy, int64_t ldy, const float* __restrict__ pre,
+                          int64_t ldp, int64_t M, int64_t N, float* __restrict__ out, int64_t ldo) {
+  const int64_t total = M * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / N, n = i - m * N;
+    out[m * ldo + n] = dy[m * ldy + n] * act_grad(kind, pre[m * ldp + n]);
+  }
+}
+
+int64_t total_rows_of(const AimxEmbeddingTables* t) {
+  int64_t s = 0;
+  for (int i = 0; i < t->n_tables; ++i) s += t->rows[i];
+  return s;
+}
+
+bool tables_ok(const AimxEmbeddingTables* t) {
+  if (!t || t->n_tables < 1 || t->n_tables > AIMX_MAX_TABLES || t->dim < 1) return false;
+  if ((int64_t)t->n_tables * t->dim > 1024) return false;
+  for (int i = 0; i < t->n_tables; ++i)
+    if (t->rows[i] < 1 || !t->index[i]) return false;
+  return total_rows_of(t) * t->dim * (int64_t)sizeof(float) <= 160 * 1024;
+}
+
+}  // namespace
+}  // namespace aimx
+
+using namespace aimx;
+
+extern "C" int aimx_embedding_gather(const AimxEmbeddingTables* t, int64_t N, float* out, int64_t ldo,
+                                     aimx_stream_t s) {
+  if (!tables_ok(t) || N < 0 || !out) return AIMX_EARG;
+  if (N == 0) return AIMX_OK;
+  const int64_t total = N * t->n_tables * t->dim;
+  hipLaunchKernelGGL(k_embed_gather, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)), dim3(256), 0,
+                     (hipStream_t)s, *t, N, out, ldo);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
+extern "C" size_t aimx_embedding_backward_workspace_bytes(const AimxEmbeddingTables* t, int64_t N) {
+  if (!tables_ok(t)) return 0;
+  return sizeof(float) * (size_t)(cdiv(std::max<int64_t>(N, 1), kChunk) * total_rows_of(t) * t->dim);
+}
+
+extern "C" int aimx_embedding_backward(const AimxEmbeddingTables* t, int64_t N, const float* dE, int64_t ldd,
+                                       void* ws, size_t ws_bytes, aimx_stream_t s_) {
+  hipStream_t s = (hipStream_t)s_;
+  if (!tables_ok(t) || N < 0) return AIMX_EARG;
+  for (int i = 0; i < t->n_tables; ++i)
+    if (!t->grad[i]) return AIMX_EARG;
+  const int64_t tr = total_rows_of(t);
+  if (N == 0) {
+    for (int i = 0; i < t->n_tables; ++i)
+      AIMX_CHECK_HIP(hipMemsetAsync(t->grad[i], 0, sizeof(float) * t->rows[i] * t->dim, s));
+    return AIMX_OK;
+  }
+  if (ws_bytes < aimx_embedding_backward_workspace_bytes(t, N) || !ws) return AIMX_EARG;
+  const int64_t nblk = cdiv(N, kChunk);
+  const size_t lds = sizeof(float) * (size_t)(tr * t->dim);
+  hipLaunchKernelGGL(k_embed_bwd_partial, dim3((unsigned)nblk), dim3((unsigned)(t->n_tables * t->dim)), lds, s, *t, N,
+                     dE, ldd, (float*)ws, tr);
+  AIMX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_embed_bwd_reduce, dim3((unsigned)cdiv(tr * t->dim, 256)), dim3(256), 0, s, *t,
+                     (const float*)ws, nblk, tr);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
+extern "C" int aimx_act_backward(int32_t kind, const float* dy, int64_t ldy, const float* pre, int64_t ldp, int64_t M,
+                                 int64_t N, float* out, int64_t ldo, aimx_stream_t s) {
+  if (M < 0 || N < 0) return AIMX_EARG;
+  if (M == 0 || N == 0) return AIMX_OK;
+  hipLaunchKernelGGL(k_act_bwd, dim3((unsigned)std::min<int64_t>(cdiv(M * N, 256), 8192)), dim3(256), 0,
+                     (hipStream_t)s, (int)kind, dy, ldy, pre, ldp, M, N, out, ldo);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}

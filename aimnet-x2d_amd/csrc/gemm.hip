@@ -1,22 +1,28 @@
-// Fused fp32 GEMM on CDNA4 matrix cores for the node-update MLP.
+// Fused fp32 GEMM on CDNA4 matrix cores for the node-update MLP and the dense projections.
 //
 // Reference: ShellConvolutionLayer.forward, src/models/layers.py:82-106 (nn.Linear = addmm,
-// SiLU, Dropout, residual adds) and its autograd backward. Every contraction there is fp32, so
-// the MFMA is v_mfma_f32_16x16x4_f32: exact f32 products accumulated as a k-ordered fmaf chain,
-// at the f32 matrix rate (64 FLOP/clk/SIMD, ~157 TF/s chip). There is no xf32 path on gfx950.
+// SiLU, Dropout, residual adds), the projections in gnn.py:224-258 and their autograd backward.
+// Every contraction is fp32, so the MFMA is v_mfma_f32_16x16x4_f32: exact f32 products
+// accumulated as a k-ordered fmaf chain at the f32 matrix rate (~157 TF/s chip); gfx950 has no
+// xf32 path.
 //
-// Tiling: 256 threads = 4 waves in a 2x2 grid over a BM x BN block tile, each wave owning a
-// (BM/2) x (BN/2) sub-tile as (BM/32) x (BN/32) 16x16 accumulators. K advances in BK = 16
-// slices staged in LDS as k-major [BK][BM+16] / [BK][BN+16] images (row stride = 16 mod 32 banks
-// so the two k rows a 32-lane group reads land on disjoint banks). The next slice is prefetched
-// into registers while the MFMAs of the current slice run. The staging loop picks the
-// coalesced direction from the operand strides (row- or column-major, both occur: Y = X W^T
-// forward, dX = dY W and dW = dY^T X backward).
+// Shapes on this path are small and latency-bound (M = atoms ~1e4, N, K = 38..2150), so the
+// design goal is few dependent round trips per block and enough blocks per CU:
+//  * 256 threads = 4 waves in a 2x2 grid over a BM x BN tile (64x64, 64x32 or 32x32, chosen so the
+//    grid covers the chip), each wave (BM/2) x (BN/2) as 16x16 accumulators;
+//  * K advances in 64-deep slices; the next slice's global loads are issued into registers before
+//    the 16 MFMA k-steps of the current slice run from LDS (one exposed round trip per 64 of K);
+//  * the LDS image follows the coalesced direction of each operand: k-contiguous operands
+//    (row-major X, W of Y = X W^T) are stored row-major with a 66-float row stride (the two k
+//    columns a 32-lane group reads fall on disjoint banks: bank = 2*row + k), m/n-contiguous
+//    operands (dY^T of the weight gradient) are stored k-major with a (BM+16)-float stride;
+//  * long-K / small-MN products (weight gradients, K = atoms) split K across workgroups; the
+//    partial slabs are reduced IN the launch by the last-arriving workgroup of each tile
+//    (agent-scope release/acquire + a self-resetting arrival counter, MI355X_MICROARCH.md
+//    §visibility), in slab order: deterministic, no atomics on the data, no extra launch.
 // Epilogue (fused, see include/aimx.h): bias, residuals, pre-activation store, activation,
 // hash-dropout with mask store, mask/act' multiplication for the backward, and an implicit ones
-// column that turns the weight-gradient GEMM's last column into the bias gradient.
-// Long-K / small-MN products (weight gradients, K = atoms) run split-K with fp32 partial slabs
-// and an ordered reduce: deterministic, no atomics.
+// column that turns a weight-gradient GEMM's last column into the bias gradient.
 #include <algorithm>
 
 #include "aimx_common.h"
@@ -26,54 +32,150 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBK = 16;
+constexpr int kBK = 32;
 
-__device__ __forceinline__ void epilogue(const AimxGemmArgs& a, int64_t m, int64_t n, float v) {
-  if (a.ones_col && n == a.N - 1) {
-    a.col_out[m] = v;
-    return;
-  }
-  float* cp = a.C + m * a.ldc + n;
-  if (a.beta != 0.f) v += a.beta * *cp;
-  if (a.bias) v += a.bias[n];
+// Batched epilogue over the NE outputs a thread owns: every global load it needs (C for beta,
+// bias, residuals, dropout mask, act' pre-activation) is issued before any store, so the loads
+// of all NE elements are in flight together instead of one memory round trip per element.
+template <int NE>
+__device__ __forceinline__ void epilogue_n(const AimxGemmArgs& a, const int (&m)[NE], const int (&n)[NE],
+                                           float (&v)[NE]) {
+  // Every load below is unconditional from a clamped address (selects, not branches), and every
+  // optional operand is tested once outside its element loop, so all NE elements' loads are in
+  // flight together before the first store.
+  bool ok[NE], ones[NE];
+  int64_t mc[NE];
+  int nc[NE];
 #pragma unroll
-  for (int r = 0; r < 3; ++r)
-    if (a.res[r]) v += a.res[r][m * a.ldres[r] + n];
-  if (n < a.act_ncols) {
-    if (a.pre) a.pre[m * a.ldpre + n] = v;
-    if (a.act >= 0) v = act_fwd(a.act, v);
+  for (int e = 0; e < NE; ++e) {
+    ones[e] = (a.ones_col != 0) & (n[e] == a.N - 1);
+    ok[e] = (m[e] < a.M) & (n[e] < a.N);
+    const bool in = ok[e] & !ones[e];
+    mc[e] = in ? m[e] : 0;
+    nc[e] = in ? n[e] : 0;
+  }
+  float add[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) add[e] = 0.f;
+  if (a.beta != 0.f) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) add[e] += a.beta * a.C[mc[e] * a.ldc + nc[e]];
+  }
+  if (a.bias) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) add[e] += a.bias[nc[e]];
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    if (a.res[r]) {
+      const float* __restrict__ rp = a.res[r];
+      const int64_t ld = a.ldres[r];
+#pragma unroll
+      for (int e = 0; e < NE; ++e) add[e] += rp[mc[e] * ld + nc[e]];
+    }
+  }
+  float dg[NE];
+  if (a.dact_pre) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) dg[e] = act_grad(a.dact_kind, a.dact_pre[mc[e] * a.lddact + nc[e]]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) dg[e] = 1.f;
+  }
+  const float scale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+  if (a.mask_in) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) dg[e] *= a.mask_in[mc[e] * a.ldmask + nc[e]] ? scale : 0.f;
+  }
+  float x[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) x[e] = v[e] + add[e];
+  if (a.act_ncols > 0) {
+    if (a.pre) {
+#pragma unroll
+      for (int e = 0; e < NE; ++e)
+        if (ok[e] & !ones[e] & (n[e] < a.act_ncols)) a.pre[m[e] * a.ldpre + n[e]] = x[e];
+    }
+    if (a.act >= 0) {
+#pragma unroll
+      for (int e = 0; e < NE; ++e)
+        if (n[e] < a.act_ncols) x[e] = act_fwd(a.act, x[e]);
+    }
   }
   if (a.mask_out) {
-    const float scale = 1.f / (1.f - a.drop_p);
-    const bool keep = hash_uniform((uint64_t)*a.drop_seed, a.drop_salt, (uint64_t)m * (uint64_t)a.N + (uint64_t)n) >= a.drop_p;
-    v = keep ? v * scale : 0.f;
-    a.mask_out[m * a.ldmask + n] = keep ? 1 : 0;
+    const uint64_t seed = (uint64_t)*a.drop_seed;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const bool keep = hash_uniform(seed, a.drop_salt, (uint64_t)m[e] * (uint64_t)a.N + (uint64_t)n[e]) >= a.drop_p;
+      x[e] = keep ? x[e] * scale : 0.f;
+      if (ok[e] & !ones[e]) a.mask_out[m[e] * a.ldmask + n[e]] = keep ? 1 : 0;
+    }
   }
-  if (a.mask_in) {
-    const float scale = 1.f / (1.f - a.drop_p);
-    v = a.mask_in[m * a.ldmask + n] ? v * scale : 0.f;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    if (!ok[e]) continue;
+    if (ones[e])
+      a.col_out[m[e]] = v[e];
+    else
+      a.C[m[e] * a.ldc + n[e]] = x[e] * dg[e];
   }
-  if (a.dact_pre) v *= act_grad(a.dact_kind, a.dact_pre[m * a.lddact + n]);
-  *cp = v;
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int64_t kchunk) {
+// Buffer descriptor over [p, p + bytes): out-of-range loads return 0 (used as the M/N/K edge
+// padding), 32-bit byte offsets (fewer VGPRs than 64-bit flat addresses). Inputs are made
+// provably wave-uniform with readfirstlane so hipcc does not waterfall the loads (guide T8/T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* q = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  // the b32 builtin returns the raw bits as an integer: reinterpret, never convert
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// AK: A is k-contiguous (sak == 1) -> row-major LDS image (row stride BK+2: bank = 2*row + k,
+// conflict-free for the 16x16x4 fragment reads); else A is m-contiguous (sam == 1) -> k-major
+// image (stride BM+16). BKC: the same for B with n in place of m.
+template <int BM, int BN, bool AK, bool BKC>
+__global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
+  constexpr int BK = kBK;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int SA = BM + 16, SB = BN + 16;
-  constexpr int NA = BM * kBK / 256, NB = BN * kBK / 256;  // staged elements per thread
-  __shared__ float As[kBK * SA];
-  __shared__ float Bs[kBK * SB];
+  constexpr int SA = AK ? BK + 2 : BM + 16;
+  constexpr int SB = BKC ? BK + 2 : BN + 16;
+  constexpr int LA = AK ? BM * SA : BK * SA;
+  constexpr int LB = BKC ? BN * SB : BK * SB;
+  constexpr int NA = BM * BK / 256, NB = BN * BK / 256;
+  __shared__ __attribute__((aligned(16))) float smem[LA + LB + 4];
+  float* As = smem;
+  float* Bs = smem + LA;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
-  const int64_t kbeg = (int64_t)blockIdx.z * kchunk;
-  const int64_t kend = min(a.K, kbeg + kchunk);
-  const bool a_mfast = (a.sam == 1 && a.sak != 1);
-  const bool b_nfast = (a.sbn == 1 && a.sbk != 1);
-  const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
+  const int M = (int)a.M, N = (int)a.N;
+  const int Nreal = a.ones_col ? N - 1 : N;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min((int)a.K, kbeg + kchunk);
+  const __amdgpu_buffer_rsrc_t ra_ = make_rsrc(a.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb_ = make_rsrc(a.B, b_bytes);
+  const uint32_t sam = (uint32_t)a.sam, sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
+
+  // Per-thread fixed coordinates of the staging pattern.
+  //  AK : mm = tid / BK + i*(256/BK), kk = tid % BK    |  !AK : mm = tid % BM, kk = tid / BM + i*(256/BM)
+  const int a_m = AK ? tid / BK : tid % BM;
+  const int a_k = AK ? tid % BK : tid / BM;
+  const int b_n = BKC ? tid / BK : tid % BN;
+  const int b_k = BKC ? tid % BK : tid / BN;
+  constexpr int A_STEP = AK ? 256 / BK : 256 / BM;  // rows (AK) or k (!AK) advanced per i
+  constexpr int B_STEP = BKC ? 256 / BK : 256 / BN;
+  const bool a_m_ok = AK ? true : (m0 + a_m < M);
+  const bool b_n_ok = BKC ? true : (n0 + b_n < Nreal);
+  const bool b_n_one = !BKC && a.ones_col && (n0 + b_n == N - 1);
 
   floatx4 acc[TM][TN];
 #pragma unroll
@@ -82,62 +184,82 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int64_t kchu
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   float ra[NA], rb[NB];
-  auto load_tile = [&](int64_t k0) {
+  auto load_slice = [&](int k0, bool tail) {
+    // A
+    if (AK) {
+      const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) * sam + (uint32_t)(k0 + a_k));
+      const bool kok = !tail || (k0 + a_k < kend);
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * 256;
-      const int mm = a_mfast ? (idx % BM) : (idx / kBK);
-      const int kk = a_mfast ? (idx / BM) : (idx % kBK);
-      const int64_t m = m0 + mm, k = k0 + kk;
-      ra[i] = (m < a.M && k < kend) ? a.A[m * a.sam + k * a.sak] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int idx = tid + i * 256;
-      const int nn = b_nfast ? (idx % BN) : (idx / kBK);
-      const int kk = b_nfast ? (idx / BN) : (idx % kBK);
-      const int64_t n = n0 + nn, k = k0 + kk;
-      float v = 0.f;
-      if (k < kend) {
-        if (n < Nreal)
-          v = a.B[k * a.sbk + n * a.sbn];
-        else if (a.ones_col && n == a.N - 1)
-          v = 1.f;
+      for (int i = 0; i < NA; ++i) {
+        const float v = bload(ra_, voff, 4u * (uint32_t)(i * A_STEP) * sam);
+        ra[i] = kok ? v : 0.f;
       }
-      rb[i] = v;
+    } else {
+      const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) + (uint32_t)(k0 + a_k) * sak);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const float v = bload(ra_, voff, 4u * (uint32_t)(i * A_STEP) * sak);
+        const bool ok = a_m_ok && (!tail || (k0 + a_k + i * A_STEP < kend));
+        ra[i] = ok ? v : 0.f;
+      }
+    }
+    // B
+    if (BKC) {
+      const uint32_t voff = 4u * ((uint32_t)(n0 + b_n) * sbn + (uint32_t)(k0 + b_k));
+      const bool kok = !tail || (k0 + b_k < kend);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const float v = bload(rb_, voff, 4u * (uint32_t)(i * B_STEP) * sbn);
+        const int n = n0 + b_n + i * B_STEP;
+        const bool one = a.ones_col && (n == N - 1);
+        rb[i] = kok ? (one ? 1.f : v) : 0.f;
+      }
+    } else {
+      const uint32_t voff = 4u * ((uint32_t)(n0 + b_n) + (uint32_t)(k0 + b_k) * sbk);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const float v = bload(rb_, voff, 4u * (uint32_t)(i * B_STEP) * sbk);
+        const bool kok = !tail || (k0 + b_k + i * B_STEP < kend);
+        rb[i] = kok ? (b_n_one ? 1.f : (b_n_ok ? v : 0.f)) : 0.f;
+      }
     }
   };
-  auto store_tile = [&]() {
+  auto store_slice = [&]() {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int idx = tid + i * 256;
-      const int mm = a_mfast ? (idx % BM) : (idx / kBK);
-      const int kk = a_mfast ? (idx / BM) : (idx % kBK);
-      As[kk * SA + mm] = ra[i];
+      const int mm = AK ? a_m + i * A_STEP : a_m;
+      const int kk = AK ? a_k : a_k + i * A_STEP;
+      As[AK ? (mm * SA + kk) : (kk * SA + mm)] = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int idx = tid + i * 256;
-      const int nn = b_nfast ? (idx % BN) : (idx / kBK);
-      const int kk = b_nfast ? (idx / BN) : (idx % kBK);
-      Bs[kk * SB + nn] = rb[i];
+      const int nn = BKC ? b_n + i * B_STEP : b_n;
+      const int kk = BKC ? b_k : b_k + i * B_STEP;
+      Bs[BKC ? (nn * SB + kk) : (kk * SB + nn)] = rb[i];
     }
   };
 
-  if (kbeg < kend) load_tile(kbeg);
-  for (int64_t k0 = kbeg; k0 < kend; k0 += kBK) {
+  if (kbeg < kend) load_slice(kbeg, kbeg + BK > kend);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
-    store_tile();
+    store_slice();
     __syncthreads();
-    if (k0 + kBK < kend) load_tile(k0 + kBK);
+    const int kn = k0 + BK;
+    if (kn < kend) load_slice(kn, kn + BK > kend);
 #pragma unroll
-    for (int s = 0; s < kBK / 4; ++s) {
+    for (int s = 0; s < BK / 4; ++s) {
       const int kr = 4 * s + (lane >> 4);
       float af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = As[kr * SA + wr * WM + i * 16 + (lane & 15)];
+      for (int i = 0; i < TM; ++i) {
+        const int mm = wr * WM + i * 16 + (lane & 15);
+        af[i] = As[AK ? (mm * SA + kr) : (kr * SA + mm)];
+      }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = Bs[kr * SB + wc * WN + j * 16 + (lane & 15)];
+      for (int j = 0; j < TN; ++j) {
+        const int nn = wc * WN + j * 16 + (lane & 15);
+        bf[j] = Bs[BKC ? (nn * SB + kr) : (kr * SB + nn)];
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -145,32 +267,111 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int64_t kchu
     }
   }
 
-  // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
-  const bool partial = gridDim.z > 1;
-  float* ws = a.workspace + (int64_t)blockIdx.z * a.M * a.N;
+  // C/D layout of the 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg. The tile is
+  // transposed through LDS so the epilogue walks rows with consecutive lanes on consecutive
+  // columns: coalesced residual/bias/mask loads and C/pre stores (4 elements per thread per pass).
+  if (gridDim.z == 1) {
+    constexpr int CS = BN + 1;
+    static_assert(BM * CS <= LA + LB, "C tile must fit the staging LDS");
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          smem[(wr * WM + i * 16 + (lane >> 4) * 4 + r) * CS + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int q0 = 0; q0 < BM * BN / 256; q0 += 4) {
+      int em[4], en[4];
+      float ev[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = tid + (q0 + u) * 256;
+        em[u] = m0 + e / BN;
+        en[u] = n0 + e % BN;
+        ev[u] = smem[(e / BN) * CS + e % BN];
+      }
+      epilogue_n<4>(a, em, en, ev);
+    }
+    return;
+  }
+  // ---- split-K: write this slice's partial slab ----
+  float* slab = a.workspace + (int64_t)blockIdx.z * M * N;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int64_t n = n0 + wc * WN + j * 16 + (lane & 15);
-        if (m < a.M && n < a.N) {
-          if (partial)
-            ws[m * a.N + n] = acc[i][j][r];
-          else
-            epilogue(a, m, n, acc[i][j][r]);
-        }
+        const int m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wc * WN + j * 16 + (lane & 15);
+        if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
       }
+  if (!a.counters) return;  // reduced by k_splitk_reduce
+  // ---- in-launch ordered reduce by the last arriver (release -> ticket -> acquire) ----
+  int* flag = reinterpret_cast<int*>(smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int tile = blockIdx.x * gridDim.y + blockIdx.y;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (old == (int)gridDim.z - 1);
+    if (last) {
+      __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  const int64_t total = (int64_t)M * N;
+  const int S = (int)gridDim.z;
+#pragma unroll 1
+  for (int q0 = 0; q0 < BM * BN / 256; q0 += 4) {
+    int em[4], en[4];
+    int64_t off[4];
+    float ev[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + (q0 + u) * 256;
+      em[u] = m0 + e / BN;
+      en[u] = n0 + e % BN;
+      off[u] = (em[u] < M && en[u] < N) ? (int64_t)em[u] * N + en[u] : 0;
+      ev[u] = 0.f;
+    }
+    // slabs summed in slice order, 8 slices' loads in flight per element at a time
+    for (int z0 = 0; z0 < S; z0 += 8) {
+      float t[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          const bool okz = z0 + w < S;
+          const float x = a.workspace[okz ? (int64_t)(z0 + w) * total + off[u] : 0];
+          t[u][w] = okz ? x : 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+          if (z0 + w < S) ev[u] += t[u][w];
+    }
+    epilogue_n<4>(a, em, en, ev);
+  }
 }
 
 __global__ void k_splitk_reduce(const AimxGemmArgs a, int splits) {
   const int64_t total = a.M * a.N;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += a.workspace[(int64_t)z * total + t];
-    epilogue(a, t / a.N, t % a.N, v);
+    float v[1] = {0.f};
+    for (int z = 0; z < splits; ++z) v[0] += a.workspace[(int64_t)z * total + t];
+    const int m[1] = {(int)(t / a.N)}, n[1] = {(int)(t % a.N)};
+    epilogue_n<1>(a, m, n, v);
   }
 }
 
@@ -181,19 +382,44 @@ struct Plan {
 
 Plan plan_gemm(const AimxGemmArgs& a) {
   Plan p;
-  p.bm = 64;
-  p.bn = a.N <= 32 ? 32 : 64;
-  const int64_t tiles = cdiv(a.M, p.bm) * cdiv(a.N, p.bn);
+  auto tiles = [&](int bm, int bn) { return cdiv(a.M, bm) * cdiv(a.N, bn); };
+  // Prefer the largest tile that still gives >= ~1 block per CU; else the smallest tile.
+  if (a.N <= 32) {
+    p.bm = 64, p.bn = 32;
+    if (tiles(64, 32) < 256) p.bm = 32, p.bn = 32;
+  } else {
+    p.bm = 64, p.bn = 64;
+    if (tiles(64, 64) < 256) {
+      p.bm = 64, p.bn = 32;
+      if (tiles(64, 32) < 256) p.bm = 32, p.bn = 32;
+    }
+  }
+  const int64_t t = tiles(p.bm, p.bn);
   int64_t splits = a.splits;
   if (splits <= 0) {
     splits = 1;
-    if (tiles < 192 && a.K >= 512) splits = std::min<int64_t>(cdiv(384, tiles), a.K / 256);
+    // Split K while the grid is short of ~2 blocks per CU and every slice keeps >= 2 BK steps.
+    // Split K only for starved grids with long K (weight gradients: K = atoms).
+    if (t < 128 && a.K >= 1024) splits = std::min<int64_t>(cdiv(384, t), a.K / (4 * kBK));
   }
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, 64));
   p.kchunk = cdiv(cdiv(a.K, splits), kBK) * kBK;
-  p.splits = (int)cdiv(a.K, p.kchunk);
-  if (p.splits < 1) p.splits = 1;
+  p.splits = (int)std::max<int64_t>(1, cdiv(a.K, p.kchunk));
   return p;
+}
+
+template <int BM, int BN>
+void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
+  const bool ak = (a.sak == 1), bk = (a.sbk == 1);
+  const int kc = (int)p.kchunk;
+  if (ak && bk)
+    hipLaunchKernelGGL((k_gemm<BM, BN, true, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
+  else if (ak)
+    hipLaunchKernelGGL((k_gemm<BM, BN, true, false>), grid, dim3(256), 0, s, a, kc, ab, bb);
+  else if (bk)
+    hipLaunchKernelGGL((k_gemm<BM, BN, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
+  else
+    hipLaunchKernelGGL((k_gemm<BM, BN, false, false>), grid, dim3(256), 0, s, a, kc, ab, bb);
 }
 
 }  // namespace
@@ -210,6 +436,18 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   if (a.ones_col && (!a.col_out || a.N < 1)) return AIMX_EARG;
   if ((a.mask_out || a.mask_in) && !(a.drop_p < 1.f)) return AIMX_EARG;
   if (a.mask_out && !a.drop_seed) return AIMX_EARG;
+  // operand layouts: each operand must be contiguous along k or along m/n; byte extents < 2 GiB
+  if (!(a.sak == 1 || a.sam == 1) || !(a.sbk == 1 || a.sbn == 1)) return AIMX_EARG;
+  const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
+  const int64_t a_ext = 4 * ((a.M - 1) * a.sam + (a.K - 1) * a.sak + 1);
+  const int64_t b_ext = Nreal > 0 ? 4 * ((a.K - 1) * a.sbk + (Nreal - 1) * a.sbn + 1) : 4;
+  if (a.K > 0 && (a_ext >= (1ll << 31) || b_ext >= (1ll << 31))) return AIMX_EARG;
+  if (a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31)) return AIMX_EARG;
+  // descriptor byte counts = the operand's true extent: every in-range element is readable, loads
+  // past the end return 0; rows/columns beyond M/N that still fall inside the extent only feed
+  // output rows/columns that are never stored, and k beyond the slice end is zeroed by a select
+  const uint32_t a_bytes = (uint32_t)std::max<int64_t>(a_ext, 4);
+  const uint32_t b_bytes = (uint32_t)std::max<int64_t>(b_ext, 4);
   Plan p = plan_gemm(a);
   if (p.splits > 1 && (!a.workspace || a.workspace_bytes < sizeof(float) * (size_t)p.splits * a.M * a.N)) {
     p.splits = 1;
@@ -217,12 +455,16 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   }
   if (a.K == 0) p.splits = 1, p.kchunk = kBK;
   dim3 grid((unsigned)cdiv(a.M, p.bm), (unsigned)cdiv(a.N, p.bn), (unsigned)p.splits);
-  if (p.bn == 32)
-    hipLaunchKernelGGL((k_gemm<64, 32>), grid, dim3(256), 0, s, a, p.kchunk);
+  if (p.splits > 1 && a.counters && (int64_t)grid.x * grid.y > a.n_counters) a.counters = nullptr;
+  if (p.splits == 1) a.counters = nullptr;
+  if (p.bm == 64 && p.bn == 64)
+    launch_tile<64, 64>(a, p, grid, s, a_bytes, b_bytes);
+  else if (p.bm == 64)
+    launch_tile<64, 32>(a, p, grid, s, a_bytes, b_bytes);
   else
-    hipLaunchKernelGGL((k_gemm<64, 64>), grid, dim3(256), 0, s, a, p.kchunk);
+    launch_tile<32, 32>(a, p, grid, s, a_bytes, b_bytes);
   AIMX_CHECK_LAUNCH();
-  if (p.splits > 1) {
+  if (p.splits > 1 && !a.counters) {
     const int64_t blocks = std::min<int64_t>(cdiv(a.M * a.N, 256), 2048);
     hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, a, p.splits);
     AIMX_CHECK_LAUNCH();

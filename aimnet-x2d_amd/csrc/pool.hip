@@ -274,22 +274,31 @@ __global__ __launch_bounds__(kThreads) void k_attn_bwd(const float* __restrict__
                          db_part, dtau_part, Slot<false, double>{ds_glob, N}, red);
 }
 
+// One wave per output value (dW[h,c], db[h], dtau): lanes take molecules g = lane, lane+64, ... and
+// the 64 partial sums are combined by a fixed butterfly — deterministic and latency-parallel.
 __global__ void k_attn_reduce(int64_t G, int H, int64_t C, const float* __restrict__ dW_part,
                               const float* __restrict__ db_part, const float* __restrict__ dtau_part,
                               float* __restrict__ dW, float* __restrict__ db, float* __restrict__ dtau) {
   const int64_t nw = (int64_t)H * C;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nw + H + 1; t += (int64_t)gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t t = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6); t < nw + H + 1; t += waves) {
     double s = 0.0;
     if (t < nw) {
-      for (int64_t g = 0; g < G; ++g) s += dW_part[g * nw + t];
-      dW[t] = (float)s;
+      for (int64_t g = lane; g < G; g += 64) s += dW_part[g * nw + t];
     } else if (t < nw + H) {
-      const int64_t h = t - nw;
-      for (int64_t g = 0; g < G; ++g) s += db_part[g * H + h];
-      db[h] = (float)s;
+      for (int64_t g = lane; g < G; g += 64) s += db_part[g * H + (t - nw)];
     } else {
-      for (int64_t g = 0; g < G; ++g) s += dtau_part[g];
-      *dtau = (float)s;
+      for (int64_t g = lane; g < G; g += 64) s += dtau_part[g];
+    }
+    s = wave_sum_d(s);
+    if (lane == 0) {
+      if (t < nw)
+        dW[t] = (float)s;
+      else if (t < nw + H)
+        db[t - nw] = (float)s;
+      else
+        *dtau = (float)s;
     }
   }
 }
@@ -387,7 +396,7 @@ extern "C" int aimx_attn_pool_backward(const float* x, int64_t ldx, int64_t N, i
     AIMX_CHECK_LAUNCH();
   }
   const int64_t tot = H * C + H + 1;
-  hipLaunchKernelGGL(k_attn_reduce, dim3((unsigned)std::min<int64_t>(cdiv(tot, 256), 1024)), dim3(256), 0, s, G,
+  hipLaunchKernelGGL(k_attn_reduce, dim3((unsigned)std::min<int64_t>(cdiv(tot, 4), 4096)), dim3(256), 0, s, G,
                      (int)H, C, dW_part, db_part, dtau_part, dW, db, dtau);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;

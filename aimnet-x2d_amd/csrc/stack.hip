@@ -83,11 +83,15 @@ AimxGemmArgs linear_dw(int64_t rows, int64_t in, int64_t out, const float* dY, i
 struct Ws {
   float* p;
   size_t bytes;
+  int32_t* counters;
+  int64_t n_counters;
 };
 
 int run(AimxGemmArgs a, const Ws& ws, hipStream_t s) {
   a.workspace = ws.p;
   a.workspace_bytes = ws.bytes;
+  a.counters = ws.counters;
+  a.n_counters = ws.n_counters;
   return launch_gemm(a, s);
 }
 
@@ -138,7 +142,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
   if (N == 0) return AIMX_OK;
-  const Ws ws{s->workspace, s->workspace_bytes};
+  const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters};
   const bool drop = s->training && s->drop_p > 0.f;
   for (int64_t l = 0; l < L; ++l) {
     float* F = s->F[l];
@@ -226,7 +230,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
   if (N == 0) return AIMX_OK;
-  const Ws ws{s->workspace, s->workspace_bytes};
+  const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters};
   const bool drop = s->training && s->drop_p > 0.f;
   float* T[3] = {g->dT1, g->dT2, g->dT3};
   float* dV = g->dT0;

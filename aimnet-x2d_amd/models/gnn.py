@@ -25,8 +25,11 @@ from aimx import _lib, ops
 from aimx.plan import GraphPlan
 from utils.activation import activation_name, get_activation_function
 
-from .layers import MultiLayerPerceptron, ShellConvolutionLayer
+from .layers import AimxLinear, MultiLayerPerceptron, ShellConvolutionLayer
 from .pooling import create_pooling_layer
+
+
+_FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
 
 
 class GNN(nn.Module):
@@ -51,7 +54,7 @@ class GNN(nn.Module):
             ffn_hidden_dim = hidden_dim
 
         self._create_embeddings(feature_sizes, embedding_dim)
-        self.embedding_projection = nn.Linear(embedding_dim * len(feature_sizes), hidden_dim)
+        self.embedding_projection = AimxLinear(embedding_dim * len(feature_sizes), hidden_dim)
         self.activation = get_activation_function(activation_type)
 
         self.x_other_dim = int(0.3 * hidden_dim)
@@ -63,15 +66,15 @@ class GNN(nn.Module):
                                             initial_temperature=attention_temperature)
         self._create_processing_layers(hidden_dim, activation_type)
 
-        self.post_pooling_projection = nn.Linear(hidden_dim, ffn_hidden_dim)
+        self.post_pooling_projection = AimxLinear(hidden_dim, ffn_hidden_dim)
         self.ffn = MultiLayerPerceptron(input_dim=ffn_hidden_dim, hidden_dim=ffn_hidden_dim, output_dim=ffn_hidden_dim,
                                         num_layers=ffn_num_layers, activation_type=activation_type,
                                         dropout=ffn_dropout, use_skip=True)
-        self.skip_transform = nn.Linear(ffn_hidden_dim, ffn_hidden_dim)
+        self.skip_transform = AimxLinear(ffn_hidden_dim, ffn_hidden_dim)
         final_output_dim = output_dim * 4 if loss_function == "evidential" else output_dim
-        self.output_layer = nn.Linear(ffn_hidden_dim * 2, final_output_dim)
+        self.output_layer = AimxLinear(ffn_hidden_dim * 2, final_output_dim)
         # constructed by the reference (gnn.py:146) but never used in forward
-        self.long_range_projection = nn.Linear(hidden_dim, ffn_hidden_dim)
+        self.long_range_projection = AimxLinear(hidden_dim, ffn_hidden_dim)
         self.init_weights()
 
     def _create_embeddings(self, feature_sizes: Dict[str, int], embedding_dim: int):
@@ -88,10 +91,10 @@ class GNN(nn.Module):
             for _ in range(num_layers)])
 
     def _create_processing_layers(self, hidden_dim: int, activation_type: str):
-        self.concat_self_other = nn.Linear(hidden_dim, hidden_dim)
+        self.concat_self_other = AimxLinear(hidden_dim, hidden_dim)
         if self.use_stereochemistry:
-            self.stereochemical_embedding = nn.Linear(hidden_dim * 3, hidden_dim)
-            self.stereochemical_embedding_2 = nn.Linear(self.x_other_dim * 3, self.x_other_dim)
+            self.stereochemical_embedding = AimxLinear(hidden_dim * 3, hidden_dim)
+            self.stereochemical_embedding_2 = AimxLinear(self.x_other_dim * 3, self.x_other_dim)
 
     # ------------------------------------------------------------------------------------------
     def forward(self, atom_features: Dict[str, torch.Tensor], multi_hop_edge_indices: torch.Tensor,
@@ -99,8 +102,12 @@ class GNN(nn.Module):
                 cis_indices: torch.Tensor, trans_indices: torch.Tensor
                 ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
         _lib.require_device(multi_hop_edge_indices, batch_indices, total_charges)
-        atom_embeddings = self._embed_atomic_features(atom_features)
-        atom_embeddings = self.activation(self.embedding_projection(atom_embeddings))
+        # gnn.py:221-225: four lookups + cat + projection + activation, fused on the device
+        atom_embeddings = ops.embed_project(
+            [atom_features[k] for k in _FEATURE_KEYS],
+            [self.atom_type_embedding.weight, self.hydrogen_count_embedding.weight, self.degree_embedding.weight,
+             self.hybridization_embedding.weight],
+            self.embedding_projection.weight, self.embedding_projection.bias, act=activation_name(self.activation))
         x_self, x_other = torch.split(atom_embeddings, [self.x_self_dim, self.x_other_dim], dim=-1)
 
         plan = GraphPlan(atom_embeddings.shape[0], self.num_shells, edges=multi_hop_edge_indices,

@@ -87,6 +87,15 @@ class ShellConvolutionLayer(nn.Module):
         return list(torch.split(agg, n, dim=0))
 
 
+class AimxLinear(nn.Linear):
+    """nn.Linear whose forward runs on the fused fp32 MFMA GEMM (aimx.ops.linear): same parameters,
+    state_dict keys, isinstance and hook behaviour as nn.Linear; the weight/bias gradients come from
+    one split-K GEMM with the bias column fused (deterministic)."""
+
+    def forward(self, x: torch.Tensor, act: str = None) -> torch.Tensor:
+        return ops.linear(x, self.weight, self.bias, act)
+
+
 class LinearBlock(nn.Module):
     """Linear -> activation -> dropout -> linear with an optional identity skip (layers.py:170-219)."""
 
@@ -94,15 +103,16 @@ class LinearBlock(nn.Module):
                  use_skip: bool = True):
         super().__init__()
         self.use_skip = use_skip and (input_dim == output_dim)
-        self.linear1 = nn.Linear(input_dim, output_dim)
+        self.linear1 = AimxLinear(input_dim, output_dim)
         self.activation = get_activation_function(activation_type)
         self.dropout = nn.Dropout(dropout)
-        self.linear2 = nn.Linear(output_dim, output_dim)
+        self.linear2 = AimxLinear(output_dim, output_dim)
         # the reference's projection branch is unreachable (use_skip implies equal widths)
         self.skip_proj = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = self.linear2(self.dropout(self.activation(self.linear1(x))))
+        # activation fused into linear1's GEMM epilogue (stateless module, same math)
+        out = self.linear2(self.dropout(self.linear1(x, act=activation_name(self.activation))))
         if self.use_skip:
             out = out + (self.skip_proj(x) if self.skip_proj is not None else x)
         return out

@@ -88,7 +88,8 @@ int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rows_p
  * mask written to mask_out) (v *= mask_in ? 1/(1-p) : 0) (v *= act'(dact_pre)) -> C.
  * ones_col != 0: B gets an implicit all-ones column at n == N-1 and column N-1 of the result is
  * written to col_out[m] instead of C (bias gradient fused into the weight-gradient GEMM).
- * splits > 1: split-K with partial slabs in `workspace` and a deterministic ordered reduce.
+ * splits > 1 (0 = automatic): split-K with partial slabs in `workspace`, reduced in slab order
+ * (deterministic) inside the launch when `counters` is given.
  * ------------------------------------------------------------------------------------------ */
 typedef struct AimxGemmArgs {
   int64_t M, N, K;
@@ -105,6 +106,10 @@ typedef struct AimxGemmArgs {
   uint8_t* mask_out; const uint8_t* mask_in; int64_t ldmask;
   int32_t ones_col; float* col_out;
   int32_t splits; float* workspace; size_t workspace_bytes;
+  /* split-K tile arrival counters: zero-initialised, persistent, self-resetting (the last
+   * arriving slice of a tile reduces the slabs in order and rezeroes its counter). NULL: a
+   * separate ordered reduce kernel is launched instead. */
+  int32_t* counters; int64_t n_counters;
 } AimxGemmArgs;
 
 size_t aimx_gemm_workspace_bytes(const AimxGemmArgs* args);
@@ -139,6 +144,7 @@ typedef struct AimxShellStack {
   const float* x_in; int64_t x_in_ld;
   float* out; int64_t out_ld;
   float* workspace; size_t workspace_bytes;
+  int32_t* counters; int64_t n_counters; /* as in AimxGemmArgs */
 } AimxShellStack;
 
 typedef struct AimxShellStackGrad {
@@ -202,6 +208,32 @@ int aimx_segment_pool_backward(int32_t kind, const float* d_out, int64_t N, int6
                                const int32_t* gptr, const int32_t* gperm, int64_t G,
                                const int32_t* argmax, float* dx, int64_t lddx,
                                aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Atom-feature embeddings (reference src/models/gnn.py:262-274, nn.Embedding x4 + cat) and the
+ * elementwise activation backward used around the dense projections.
+ * gather:   out[j, t*dim + c] = table[t][index[t][j], c]            (out [N, n_tables*dim])
+ * backward: grad[t] = sum over atoms j of dE[j, t*dim:(t+1)*dim] into row index[t][j]
+ *           (deterministic: per-chunk partial tables in LDS, then an ordered reduce).
+ * Indices are int64 (the reference's dtype); out-of-range indices contribute nothing.
+ * ------------------------------------------------------------------------------------------ */
+#define AIMX_MAX_TABLES 8
+typedef struct AimxEmbeddingTables {
+  int32_t n_tables; int64_t dim;
+  const float* table[AIMX_MAX_TABLES];
+  const int64_t* index[AIMX_MAX_TABLES];
+  int64_t rows[AIMX_MAX_TABLES];
+  float* grad[AIMX_MAX_TABLES];
+} AimxEmbeddingTables;
+
+int aimx_embedding_gather(const AimxEmbeddingTables* t, int64_t N, float* out, int64_t ldo,
+                          aimx_stream_t stream);
+size_t aimx_embedding_backward_workspace_bytes(const AimxEmbeddingTables* t, int64_t N);
+int aimx_embedding_backward(const AimxEmbeddingTables* t, int64_t N, const float* dE, int64_t ldd,
+                            void* workspace, size_t workspace_bytes, aimx_stream_t stream);
+/* out[m,n] = dy[m,n] * act'(pre[m,n]) */
+int aimx_act_backward(int32_t kind, const float* dy, int64_t ldy, const float* pre, int64_t ldp,
+                      int64_t M, int64_t N, float* out, int64_t ldo, aimx_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,62 @@
+"""Microbenchmark of aimx_gemm vs torch (hipBLASLt) on the hot path's GEMM shapes."""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aimnet-x2d_amd")]
+from aimx import _lib  # noqa: E402
+
+lib = _lib.load()
+dev = "cuda"
+
+
+def bench(fn, it=50):
+    for _ in range(5):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / it * 1e3
+
+
+def run(M, N, K, layout, label):
+    A = torch.randn(M, K, device=dev) if layout[0] == "N" else torch.randn(K, M, device=dev)
+    B = torch.randn(K, N, device=dev) if layout[1] == "N" else torch.randn(N, K, device=dev)
+    C = torch.empty(M, N, device=dev)
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.A = A.data_ptr()
+    a.sam, a.sak = (K, 1) if layout[0] == "N" else (1, M)
+    a.B = B.data_ptr()
+    a.sbk, a.sbn = (N, 1) if layout[1] == "N" else (1, K)
+    a.C, a.ldc = C.data_ptr(), N
+    a.act, a.dact_kind = -1, -1
+    a.counters, a.n_counters = _lib.counters(dev).data_ptr(), _lib.N_COUNTERS
+    wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
+    ws = torch.empty(wsb // 4 + 1, device=dev)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), wsb
+    st = torch.cuda.current_stream().cuda_stream
+    t_ours = bench(lambda: lib.aimx_gemm(ctypes.byref(a), st))
+    Am = A if layout[0] == "N" else A.t()
+    Bm = B if layout[1] == "N" else B.t()
+    t_torch = bench(lambda: torch.mm(Am, Bm, out=C))
+    fl = 2 * M * N * K
+    print(f"{label:28s} M={M:6d} N={N:5d} K={K:6d} {layout}: ours {t_ours:7.1f} us ({fl / t_ours / 1e6:6.1f} TF/s)"
+          f"  torch {t_torch:7.1f} us ({fl / t_torch / 1e6:6.1f} TF/s)")
+
+
+for args in [(9170, 152, 304, "NT", "c2 fwd [u|g]"), (9170, 76, 76, "NT", "c2 fwd mlp"),
+             (9170, 304, 152, "NN", "c2 bwd dF"), (9170, 76, 76, "NN", "c2 bwd dx mlp"),
+             (152, 305, 9170, "TN", "c2 dW_ig"), (76, 77, 9170, "TN", "c2 dW mlp"),
+             (512, 256, 256, "NT", "c2 ffn fwd"), (256, 257, 512, "TN", "c2 ffn dW"),
+             (9170, 256, 256, "NT", "c2 concat fwd"), (256, 257, 9170, "TN", "c2 concat dW"),
+             (20480, 306, 612, "NT", "c4 fwd [u|g]"), (10240, 614, 2149, "NT", "c5 fwd [u|g]"),
+             (4096, 4096, 4096, "NT", "square 4k")]:
+    run(*args)
