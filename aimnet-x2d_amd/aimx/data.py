@@ -89,6 +89,50 @@ class DeviceBatch:
         self.cis = torch.empty(0, 2, dtype=torch.long, device=device)
         self.trans = torch.empty(0, 2, dtype=torch.long, device=device)
 
+    def copy_(self, other):
+        """In-place copy of another batch of identical shapes (static graph inputs)."""
+        for k in self.atom_features:
+            self.atom_features[k].copy_(other.atom_features[k], non_blocking=True)
+        self.edges.copy_(other.edges, non_blocking=True)
+        self.batch.copy_(other.batch, non_blocking=True)
+        self.total_charges.copy_(other.total_charges, non_blocking=True)
+        self.targets.copy_(other.targets, non_blocking=True)
+
+    def clone(self):
+        import copy
+        b = copy.copy(self)
+        b.atom_features = {k: v.clone() for k, v in self.atom_features.items()}
+        for k in ("edges", "batch", "total_charges", "targets"):
+            setattr(b, k, getattr(self, k).clone())
+        return b
+
     def model_args(self):
         return (self.atom_features, self.edges, self.batch, self.total_charges, self.tetrahedral, self.cis,
                 self.trans)
+
+
+def pad_collated(col, n_max, e_max, g_real):
+    """Pad a collated batch to static shapes for graph replay (SURVEY.md §8d "padded batches").
+
+    The slack atoms form ONE extra padding molecule (index g_real) and the slack edges are
+    self-pairs inside it, so every real molecule's values are untouched (molecules never
+    interact); callers drop row g_real of the per-molecule outputs from the loss.
+    Requires n_max > N (at least one padding atom) and e_max >= E.
+    """
+    n = col["batch"].shape[0]
+    e = col["edges"].shape[0]
+    if n_max <= n or e_max < e:
+        raise ValueError(f"padding too small: atoms {n}/{n_max}, edges {e}/{e_max}")
+    n_pad = n_max - n
+    feats = np.zeros((n_max, col["feats"].shape[1]), np.int64)
+    feats[:n] = col["feats"]
+    batch = np.full(n_max, g_real, np.int64)
+    batch[:n] = col["batch"]
+    edges = np.empty((e_max, 2), np.int64)
+    edges[:e] = col["edges"]
+    # slack edges: self-pairs spread over the padding atoms (no long CSR row)
+    pad = n + (np.arange(e_max - e, dtype=np.int64) % n_pad)
+    edges[e:, 0] = pad
+    edges[e:, 1] = pad
+    n_atoms = np.concatenate([col["n_atoms"], [n_max - n]])
+    return {"edges": edges, "feats": feats, "batch": batch, "n_atoms": n_atoms, "real_atoms": n, "real_edges": e}

@@ -67,7 +67,6 @@ class _MPStack(torch.autograd.Function):
         iV = [ar.add(n, d) for _ in range(nl * nm)]
         iR = [ar.add(n, d) for _ in range(nl * nm)]
         iA = [ar.add(n, d) if (j % nm) != nm - 1 else None for j in range(nl * nm)]
-        iOut = ar.add(n, d)
         buf, views = ar.alloc()
         F = [views[i] for i in iF]
         X = [views[i] if i is not None else None for i in iX]
@@ -76,7 +75,8 @@ class _MPStack(torch.autograd.Function):
         V = [views[i] for i in iV]
         R = [views[i] for i in iR]
         A = [views[i] if i is not None else None for i in iA]
-        out = views[iOut]
+        # tensors handed to autograd are standalone allocations, never views of the arena
+        out = torch.empty(n, d, dtype=_F32, device=dev)
         drop = bool(spec["training"]) and spec["drop_p"] > 0
         M = [torch.empty(n, d, dtype=torch.uint8, device=dev) for _ in range(nl * nm)] if drop else []
         w_ig = [params[l * (2 + 4 * nm)] for l in range(nl)]
@@ -112,30 +112,39 @@ class _MPStack(torch.autograd.Function):
         s.counters, s.n_counters = ptr(_lib.counters(dev)), _lib.N_COUNTERS
         check(lib.aimx_shell_stack_forward(s, stream_ptr(dev)), "shell_stack_forward")
         ctx.spec, ctx.plan = spec, plan
-        ctx.state = dict(buf=buf, M=M, F=F, X=X, UG=UG, U=U, V=V, R=R, A=A, w_ig=w_ig, b_ig=b_ig, w1=w1, b1=b1,
-                         w2=w2, b2=b2, x_in=x_in, x_ld=x_ld, tc=total_charges, seed=drop_seed, ws=ws, drop=drop)
-        ctx.param_shapes = [p.shape for p in params]
+        # inputs go through save_for_backward; only forward-internal buffers live on ctx
+        ctx.save_for_backward(x_in, total_charges, drop_seed, *params)
+        ctx.state = dict(buf=buf, M=M, F=F, X=X, UG=UG, U=U, V=V, R=R, A=A, x_ld=x_ld, ws=ws, drop=drop)
         return out
 
     @staticmethod
     def backward(ctx, d_out):
         lib = _lib.load()
-        st, spec, plan = ctx.state, ctx.spec, ctx.plan
+        st, spec, plan = dict(ctx.state), ctx.spec, ctx.plan
+        x_in, tc, seed, *params = ctx.saved_tensors
+        nm_ = spec["num_mlp"]
+        st["x_in"], st["tc"], st["seed"] = x_in, tc, seed
+        st["w_ig"] = [params[l * (2 + 4 * nm_)] for l in range(spec["num_layers"])]
+        st["b_ig"] = [params[l * (2 + 4 * nm_) + 1] for l in range(spec["num_layers"])]
+        for j, key in enumerate(("w1", "b1", "w2", "b2")):
+            st[key] = [params[l * (2 + 4 * nm_) + 2 + 4 * q + j] for l in range(spec["num_layers"]) for q in range(nm_)]
         dev = d_out.device
         n, d, h, nl, nm = spec["N"], spec["D"], spec["num_hops"], spec["num_layers"], spec["num_mlp"]
         k = d * (h + 1)
         d_out, d_ld = _rows(d_out)
         ar = Arena(dev)
-        i_dx = ar.add(n, d)
-        i_wig = [ar.add(2 * d, k) for _ in range(nl)]
-        i_big = [ar.add(2 * d) for _ in range(nl)]
-        i_w1 = [ar.add(d, d) for _ in range(nl * nm)]
-        i_b1 = [ar.add(d) for _ in range(nl * nm)]
-        i_w2 = [ar.add(d, d) for _ in range(nl * nm)]
-        i_b2 = [ar.add(d) for _ in range(nl * nm)]
         i_dF, i_dUG = ar.add(n, k), ar.add(n, 2 * d)
         i_T = [ar.add(n, d) for _ in range(4)]
         buf, v = ar.alloc()
+        # gradients handed to autograd are standalone allocations, never views of the arena
+        new = lambda *shape: torch.empty(*shape, dtype=_F32, device=dev)  # noqa: E731
+        dx_t = new(n, d)
+        dw_ig = [new(2 * d, k) for _ in range(nl)]
+        db_ig = [new(2 * d) for _ in range(nl)]
+        dw1 = [new(d, d) for _ in range(nl * nm)]
+        db1 = [new(d) for _ in range(nl * nm)]
+        dw2 = [new(d, d) for _ in range(nl * nm)]
+        db2 = [new(d) for _ in range(nl * nm)]
         s = ShellStack()
         s.N, s.D, s.num_hops, s.num_layers, s.num_mlp = n, d, h, nl, nm
         s.act, s.use_pc, s.training, s.mode_single = spec["act"], int(spec["use_pc"]), int(st["drop"]), int(spec["single"])
@@ -155,13 +164,7 @@ class _MPStack(torch.autograd.Function):
         s.counters, s.n_counters = ptr(_lib.counters(dev)), _lib.N_COUNTERS
         g = ShellStackGrad()
         g.d_out, g.d_out_ld = ptr(d_out), d_ld
-        g.d_x_in, g.d_x_in_ld = ptr(v[i_dx]), d
-        dw_ig = [v[i] for i in i_wig]
-        db_ig = [v[i] for i in i_big]
-        dw1 = [v[i] for i in i_w1]
-        db1 = [v[i] for i in i_b1]
-        dw2 = [v[i] for i in i_w2]
-        db2 = [v[i] for i in i_b2]
+        g.d_x_in, g.d_x_in_ld = ptr(dx_t), d
         gkeep = [ptr_array(x) for x in (dw_ig, db_ig, dw1, db1, dw2, db2)]
         g.d_w_ig, g.d_b_ig, g.d_w1, g.d_b1, g.d_w2, g.d_b2 = [_ct_addr(a) for a in gkeep]
         g.dF, g.dUG = ptr(v[i_dF]), ptr(v[i_dUG])
@@ -174,7 +177,7 @@ class _MPStack(torch.autograd.Function):
                 idx = l * nm + j
                 grads += [dw1[idx], db1[idx], dw2[idx], db2[idx]]
         del keep, gkeep, buf
-        return (None, None, v[i_dx], None, None, *grads)
+        return (None, None, dx_t, None, None, *grads)
 
 
 def _ct_addr(arr):

@@ -9,12 +9,19 @@
 // weight/bias gradients as split-K GEMMs with an implicit ones column, and the hop backward as
 // the same segmented gather-sum over the src-keyed CSR with the two residual terms fused.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "aimx_common.h"
 
 namespace aimx {
 namespace {
+
+#define RUN(expr)                 \
+  do {                            \
+    int _r = (expr);              \
+    if (_r != AIMX_OK) return _r; \
+  } while (0)
 
 AimxGemmArgs gemm0() {
   AimxGemmArgs a;
@@ -80,6 +87,25 @@ AimxGemmArgs linear_dw(int64_t rows, int64_t in, int64_t out, const float* dY, i
   return a;
 }
 
+// Strided 2-D copy as a kernel: dst[r*ldd + c] = src[r*lds + c]. (hipMemcpy2DAsync D2D nodes
+// crashed the HIP runtime at stream-capture end on ROCm 7.2; a kernel node is also cheaper.)
+__global__ void k_copy2d(const float* __restrict__ src, int64_t lds, float* __restrict__ dst, int64_t ldd,
+                         int64_t rows, int64_t cols) {
+  const int64_t total = rows * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols, c = i - r * cols;
+    dst[r * ldd + c] = src[r * lds + c];
+  }
+}
+
+int copy2d(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int64_t cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return AIMX_OK;
+  const int64_t blocks = std::min<int64_t>(cdiv(rows * cols, 256), 4096);
+  hipLaunchKernelGGL(k_copy2d, dim3((unsigned)blocks), dim3(256), 0, s, src, lds, dst, ldd, rows, cols);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
 struct Ws {
   float* p;
   size_t bytes;
@@ -109,11 +135,6 @@ bool valid(const AimxShellStack* s) {
   return true;
 }
 
-#define RUN(expr)                 \
-  do {                            \
-    int _r = (expr);              \
-    if (_r != AIMX_OK) return _r; \
-  } while (0)
 
 }  // namespace
 }  // namespace aimx
@@ -152,8 +173,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
       const int64_t ldr = (l == 0) ? s->x_in_ld : D;
       RUN(launch_charge_fwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, F, K, st));
     } else if (l == 0) {
-      AIMX_CHECK_HIP(hipMemcpy2DAsync(F, sizeof(float) * K, s->x_in, sizeof(float) * s->x_in_ld, sizeof(float) * D, N,
-                                      hipMemcpyDeviceToDevice, st));
+      RUN(copy2d(s->x_in, s->x_in_ld, F, K, N, D, st));
     }
     // 2) hop: chunks 1..h of F = scatter_add(x[src % N], target) in edge order
     RUN(gather(F, K, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, K, N, D, nullptr, 0, nullptr, 0, st));
@@ -226,6 +246,14 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
 
 extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShellStackGrad* g, aimx_stream_t stream_) {
   hipStream_t st = (hipStream_t)stream_;
+  // debug aid: AIMX_DEBUG_BWD_OPS=n enqueues only the first n operations of the backward
+  const char* dbg = getenv("AIMX_DEBUG_BWD_OPS");
+  int budget = dbg ? atoi(dbg) : -1;
+#define BUDGET()                           \
+  do {                                     \
+    if (budget == 0) return AIMX_OK;       \
+    if (budget > 0) --budget;              \
+  } while (0)
   if (!valid(s) || !g) return AIMX_EARG;
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
@@ -260,10 +288,15 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
         a.dact_pre = s->V[idx];
         a.lddact = D;
         a.dact_kind = s->act;
+        BUDGET();
         RUN(run(a, ws, st));
       }
-      RUN(run(linear_dw(N, D, D, da_out, ld_out, s->R[idx], D, g->d_w2[idx], g->d_b2[idx]), ws, st));
-      RUN(run(linear_dw(N, D, D, dV, D, in, ldin, g->d_w1[idx], g->d_b1[idx]), ws, st));
+      BUDGET();
+      BUDGET();
+    RUN(run(linear_dw(N, D, D, da_out, ld_out, s->R[idx], D, g->d_w2[idx], g->d_b2[idx]), ws, st));
+      BUDGET();
+      BUDGET();
+    RUN(run(linear_dw(N, D, D, dV, D, in, ldin, g->d_w1[idx], g->d_b1[idx]), ws, st));
       {  // da_in = da_out + dV W1 ; for k == 0 also * act'(u) -> du into dUG[:, :D]
         float* dst;
         int64_t ldd;
@@ -282,6 +315,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
           a.lddact = D;
           a.dact_kind = s->act;
         }
+        BUDGET();
         RUN(run(a, ws, st));
         if (k != 0) {
           da_out = dst;
@@ -291,9 +325,11 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       }
     }
     // dg = dY -> dUG[:, D:]
-    AIMX_CHECK_HIP(hipMemcpy2DAsync(g->dUG + D, sizeof(float) * D2, dY, sizeof(float) * ldy, sizeof(float) * D, N,
-                                    hipMemcpyDeviceToDevice, st));
+    BUDGET();
+    RUN(copy2d(dY, ldy, g->dUG + D, D2, N, D, st));
+    BUDGET();
     RUN(run(linear_dw(N, K, D2, g->dUG, D2, F, K, g->d_w_ig[l], g->d_b_ig[l]), ws, st));
+    BUDGET();
     RUN(run(linear_dx(N, K, D2, g->dUG, D2, s->w_ig[l], g->dF, K), ws, st));
     // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]
     const bool first = (l == 0);
@@ -309,6 +345,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       dst = T[free_slots[1]];
       ldd = D;
     }
+    BUDGET();
     RUN(gather(g->dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, g->dF, K,
                s->mode_single ? nullptr : dY, ldy, st));
     int new_slot = s->use_pc ? -1 : (first ? -1 : free_slots[1]);

@@ -43,7 +43,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FS = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
 
 
-def make_batches(cfg, n_batches, seed, device):
+def make_collated(cfg, n_batches, seed):
+    """Host-collated batches (aimx.data) with targets and total charges."""
     rng = np.random.default_rng(seed)
     out = []
     if cfg["source"] == "qm9":
@@ -53,13 +54,32 @@ def make_batches(cfg, n_batches, seed, device):
             col = adata.collate(asset.molecules(idx), cfg["hops"])
             tg = asset.targets[idx][:, : cfg["tasks"]].astype(np.float32)
             tg = (tg - tg.mean(0)) / (tg.std(0) + 1e-6)
-            out.append(adata.DeviceBatch(col, device, targets=tg, total_charges=asset.total_charge[idx]))
+            out.append((col, tg, asset.total_charge[idx].astype(np.float32)))
     else:
-        for b in range(n_batches):
+        for _ in range(n_batches):
             mols = synth_molecules(cfg["batch"], seed=int(rng.integers(1 << 30)))
             col = adata.collate(mols, cfg["hops"])
             tg = rng.standard_normal((cfg["batch"], cfg["tasks"])).astype(np.float32)
-            out.append(adata.DeviceBatch(col, device, targets=tg))
+            out.append((col, tg, np.zeros(cfg["batch"], np.float32)))
+    return out
+
+
+def make_batches(cfg, n_batches, seed, device, pad=False):
+    """Device-resident batches. pad=True: static shapes for graph replay (one padding molecule)."""
+    cols = make_collated(cfg, n_batches, seed)
+    if not pad:
+        return [adata.DeviceBatch(c, device, targets=t, total_charges=q) for c, t, q in cols]
+    n_max = max(c["batch"].shape[0] for c, _, _ in cols) + 64
+    e_max = max(c["edges"].shape[0] for c, _, _ in cols) + 256
+    out = []
+    for c, t, q in cols:
+        real_atoms, real_edges = c["batch"].shape[0], c["edges"].shape[0]
+        pc = adata.pad_collated(c, n_max, e_max, cfg["batch"])
+        tg = np.concatenate([t, np.zeros((1, t.shape[1]), np.float32)])
+        qq = np.concatenate([q, np.zeros(1, np.float32)])
+        b = adata.DeviceBatch(pc, device, targets=tg, total_charges=qq)
+        b.real_atoms, b.real_edges = real_atoms, real_edges
+        out.append(b)
     return out
 
 
@@ -69,13 +89,13 @@ def build_model(cfg, device):
     return m.to(device).train()
 
 
-def hop_roofline(batch, hops, device, target_atoms=4_000_000, launches=20):
+def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launches=20):
     """Time the hop kernel alone on a QM9-shaped graph of ~target_atoms atoms (tiled copies of a
     real collated batch), with HIP events on the stream it is launched on."""
     from aimx import ops
     from aimx.plan import GraphPlan
     n0 = batch.num_atoms
-    d = int(0.3 * 256)
+    d = int(0.3 * hidden)
     reps = max(1, target_atoms // n0)
     e0 = batch.edges
     off = (torch.arange(reps, device=device, dtype=torch.int64) * n0).view(reps, 1, 1)
@@ -124,7 +144,7 @@ def cpu_baseline(cfg, seconds=10.0, max_steps=40):
                              use_partial_charges=cfg["pc"])
     params = {k: v.requires_grad_() for k, v in om.seeded_params(mcfg, 0).items()}
     opt = torch.optim.Adam(params.values(), lr=2.5e-4)
-    b = make_batches(cfg, 1, 4321, "cpu")[0]
+    b = make_batches(cfg, 1, 4321, "cpu", pad=False)[0]
     af, edges, batch, tc, _, _, _ = b.model_args()
 
     def step():
@@ -156,6 +176,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true", help="only run the hop roofline launches (profiling)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="capture the whole train step in a HIP graph (static padded batches; default)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager execution")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,28 +191,78 @@ def main():
     cfg = CONFIGS[args.config]
     torch.manual_seed(1234 + rank)
 
-    batches = make_batches(cfg, args.pool, 1234 + rank, device)
+    batches = make_batches(cfg, args.pool, 1234 + rank, device, pad=args.graph)
     if args.roofline_only:
-        print(json.dumps(hop_roofline(batches[0], cfg["hops"], device)))
+        print(json.dumps(hop_roofline(make_batches(cfg, 1, 99, device)[0], cfg["hops"], device, cfg["hidden"])))
         return
 
     from utils.distributed import GradientSync
     model = build_model(cfg, device)
-    opt = torch.optim.Adam(model.parameters(), lr=2.5e-4)
-    sync = GradientSync(model.parameters()) if world > 1 else None
+    B = cfg["batch"]
     loss_fn = torch.nn.L1Loss()
 
-    def step(i):
-        b = batches[i % len(batches)]
+    if args.graph:
+        # Whole-step HIP-graph capture on static padded inputs: the captured step is the full
+        # forward + backward (+ RCCL all-reduce, eager, between two graphs when world > 1)
+        # + grad-norm clip + Adam; each timed step copies a fresh resident batch into the static
+        # inputs and replays.
+        opt = torch.optim.Adam(model.parameters(), lr=2.5e-4, capturable=True)
+        sync = GradientSync(model.parameters(), overlap=False) if world > 1 else None
+        static = batches[0].clone()
+
+        def fwd_bwd():
+            out, _, _ = model(*static.model_args())
+            loss = loss_fn(out[:B], static.targets[:B])
+            loss.backward()
+            return loss
+
+        def clip_step():
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                opt.zero_grad(set_to_none=True)
+                fwd_bwd()
+                if sync is not None:
+                    sync.finish()
+                clip_step()
+        torch.cuda.current_stream().wait_stream(side)
         opt.zero_grad(set_to_none=True)
-        out, _, _ = model(*b.model_args())
-        loss = loss_fn(out, b.targets)
-        loss.backward()
-        if sync is not None:
-            sync.finish()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
-        return loss
+        g1, g2 = torch.cuda.CUDAGraph(), None
+        if sync is None:
+            with torch.cuda.graph(g1):
+                fwd_bwd()
+                clip_step()
+        else:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                fwd_bwd()
+            with torch.cuda.graph(g2):
+                clip_step()
+
+        def step(i):
+            static.copy_(batches[i % len(batches)])
+            g1.replay()
+            if g2 is not None:
+                sync.finish()
+                g2.replay()
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=2.5e-4)
+        sync = GradientSync(model.parameters()) if world > 1 else None
+
+        def step(i):
+            b = batches[i % len(batches)]
+            opt.zero_grad(set_to_none=True)
+            out, _, _ = model(*b.model_args())
+            loss = loss_fn(out[:B], b.targets[:B])
+            loss.backward()
+            if sync is not None:
+                sync.finish()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
 
     for i in range(args.warmup):
         step(i)
@@ -207,18 +280,20 @@ def main():
         t = torch.tensor([dt], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    atoms = sum(getattr(b, "real_atoms", b.num_atoms) for b in batches) / len(batches)
+    edges = sum(getattr(b, "real_edges", b.edges.shape[0]) for b in batches) / len(batches)
     mol = cfg["batch"] * world * args.steps
     value = mol / dt
 
     roof = None
     if rank == 0 and not args.no_roofline:
-        roof = hop_roofline(batches[0], cfg["hops"], device)
+        del batches
+        torch.cuda.empty_cache()
+        roof = hop_roofline(make_batches(cfg, 1, 99, device)[0], cfg["hops"], device, cfg["hidden"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
     if rank == 0:
-        atoms = sum(b.num_atoms for b in batches) / len(batches)
-        edges = sum(b.edges.shape[0] for b in batches) / len(batches)
         line = {
             "metric": "molecules/sec fwd+bwd on QM9-shaped batches; achieved HBM GB/s on scatter-add hop",
             "value": round(value, 1), "unit": "molecules/s", "n_gpus": world, "steps": args.steps,
@@ -226,7 +301,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": f"{args.config}: " + ("QM9-shaped" if cfg["source"] == "qm9" else "40-atom synthetic")
                        + f", hidden {cfg['hidden']}, {cfg['hops']} hops, {cfg['tasks']} task(s), attention pool, "
-                       "train step fwd+bwd+clip+Adam, dropout 0.05",
+                       "train step fwd+bwd+clip+Adam, dropout 0.05"
+                       + (", HIP-graph replay of padded static batches (+1 padding molecule, excluded from"
+                          " the loss)" if args.graph else ", eager"),
                        "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
                        "mean_atoms_per_batch": round(atoms, 1), "mean_edges_per_batch": round(edges, 1),
                        "parallelism": f"dp{world}"},

@@ -1,0 +1,109 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of utils/distributed.py: the reference helper API
+(rank-0 return conventions) and GradientSync's DDP-equivalent averaging, with and without the
+backward-overlapped bucket hooks."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn_name, q):
+    import sys
+    sys.path[:0] = [ROOT, PKG, os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, globals()[fn_name](rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn_name, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, v = q.get(timeout=120)
+        out[r] = v
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def _helpers(rank, world):
+    from utils import distributed as D
+    arr = np.arange(3 + rank, dtype=np.float32).reshape(-1, 1) + 10 * rank
+    g = D.gather_ndarray_to_rank0(arr)
+    s = D.gather_strings_to_rank0([f"r{rank}a", f"r{rank}b"])
+    b = D.broadcast_object({"best": 1.5, "stop": rank == 0} if rank == 0 else None)
+    t = D.all_reduce_tensor(torch.tensor([float(rank + 1)]), "mean")
+    m = D.all_reduce_tensor(torch.tensor([float(rank + 1)]), "max")
+    D.barrier()
+    return dict(g=g.tolist(), s=s, b=b, t=t.item(), m=m.item(), rank=D.safe_get_rank(), ws=D.get_world_size(),
+                main=D.is_main_process())
+
+
+def test_reference_helpers():
+    out = _run("_helpers")
+    assert out[0]["g"] == [[0.0], [1.0], [2.0], [10.0], [11.0], [12.0], [13.0]] and out[1]["g"] == []
+    assert out[0]["s"] == ["r0a", "r0b", "r1a", "r1b"] and out[1]["s"] == []
+    assert out[0]["b"] == out[1]["b"] == {"best": 1.5, "stop": True}
+    assert out[0]["t"] == out[1]["t"] == 1.5 and out[0]["m"] == 2.0
+    assert out[0]["main"] and not out[1]["main"] and out[1]["rank"] == 1 and out[0]["ws"] == 2
+
+
+def _grad_sync(rank, world):
+    from utils.distributed import GradientSync
+    res = {}
+    for overlap in (True, False):
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.SiLU(), torch.nn.Linear(5, 3),
+                                  torch.nn.Linear(3, 3))  # last layer unused below -> grad None
+        sync = GradientSync(net.parameters(), bucket_mb=0.0001, overlap=overlap)
+        g = torch.Generator().manual_seed(100 + rank)
+        x = torch.randn(4, 7, generator=g)
+        net[2](net[1](net[0](x))).pow(2).sum().backward()
+        sync.finish()
+        res[overlap] = {n: (p.grad.clone().tolist() if p.grad is not None else None)
+                        for n, p in net.named_parameters()}
+        sync.remove()
+    return res
+
+
+def test_gradient_sync_equals_mean_of_rank_gradients():
+    out = _run("_grad_sync")
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.SiLU(), torch.nn.Linear(5, 3), torch.nn.Linear(3, 3))
+    grads = []
+    for rank in range(2):
+        net.zero_grad()
+        x = torch.randn(4, 7, generator=torch.Generator().manual_seed(100 + rank))
+        net[2](net[1](net[0](x))).pow(2).sum().backward()
+        grads.append({n: (p.grad.clone() if p.grad is not None else None) for n, p in net.named_parameters()})
+    for overlap in (True, False):
+        for n, _ in net.named_parameters():
+            if grads[0][n] is None:
+                assert out[0][overlap][n] is None and out[1][overlap][n] is None
+                continue
+            want = (grads[0][n] + grads[1][n]) / 2
+            for r in range(2):
+                assert torch.allclose(torch.tensor(out[r][overlap][n]), want, atol=1e-6), (n, overlap)
