@@ -72,37 +72,53 @@ __device__ __forceinline__ int64_t row_off(uint32_t r, int64_t ld, const FastDiv
   return (int64_t)(r - q * rpc.d) * ld + (int64_t)q * cstride;
 }
 
-template <int VEC>
-__global__ __launch_bounds__(256) void k_gather_sum(const float* __restrict__ src, int64_t src_ld, FastDiv src_rpc,
-                                                     int64_t src_cs, FastDiv units_per_row,
-                                                     const int32_t* __restrict__ rowptr,
-                                                     const int32_t* __restrict__ col, uint32_t rows,
-                                                     float* __restrict__ out, int64_t out_ld, FastDiv out_rpc,
-                                                     int64_t out_cs, const float* __restrict__ add0, int64_t add0_ld,
-                                                     const float* __restrict__ add1, int64_t add1_ld) {
+// Row tiles: a workgroup owns `tile_rows` consecutive output rows. It stages their rowptr slice and
+// (when it fits) their whole col slice in LDS with two coalesced loads, so the per-output-element
+// dependency chain is LDS -> gathered source row -> store instead of rowptr -> col -> row in HBM.
+// A tile whose rows hold no edges (the reference's hop chunks >= 1 are all-empty, layers.py:154)
+// becomes a pure streaming store. Gathers are issued 8 at a time with clamped (always valid)
+// indices and summed with selects, so the sum is the ordered edge-order sum bit for bit.
+constexpr int kMaxTileRows = 64;
+constexpr int kColCap = 4096;  // staged col entries per tile (16 KiB)
+constexpr int kGroup = 8;      // gathers in flight per thread
+
+template <bool CHUNKED>
+__device__ __forceinline__ int64_t src_off(uint32_t c, int64_t ld, const FastDiv& rpc, int64_t cs) {
+  if (!CHUNKED) return (int64_t)c * ld;
+  const uint32_t q = fdiv(c, rpc);
+  return (int64_t)(c - q * rpc.d) * ld + (int64_t)q * cs;
+}
+
+template <int VEC, bool LDS_COL, bool SRC_CHUNKED>
+__device__ __forceinline__ void tile_body(const float* __restrict__ src, int64_t src_ld, const FastDiv& src_rpc,
+                                          int64_t src_cs, const FastDiv& upr, const int32_t* s_ptr,
+                                          const int32_t* cols, int32_t base, uint32_t r0, uint32_t nr,
+                                          float* __restrict__ out, int64_t out_ld, const FastDiv& out_rpc,
+                                          int64_t out_cs, const float* __restrict__ add0, int64_t add0_ld,
+                                          const float* __restrict__ add1, int64_t add1_ld, bool any_edges) {
   using T = typename VecT<VEC>::T;
-  const uint32_t total = rows * units_per_row.d;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const uint32_t r = fdiv(t, units_per_row);
-    const uint32_t u = (t - r * units_per_row.d) * VEC;
-    const int32_t b = rowptr[r], e = rowptr[r + 1];
+  const uint32_t units = nr * upr.d;
+  for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
+    const uint32_t rl = fdiv(t, upr);
+    const uint32_t u = (t - rl * upr.d) * VEC;
+    const uint32_t r = r0 + rl;
     T acc = vzero<T>();
-    int32_t k = b;
-    // 4 independent gathers in flight, summed in edge order.
-    for (; k + 4 <= e; k += 4) {
-      const int32_t c0 = col[k], c1 = col[k + 1], c2 = col[k + 2], c3 = col[k + 3];
-      const T v0 = *reinterpret_cast<const T*>(src + row_off(c0, src_ld, src_rpc, src_cs) + u);
-      const T v1 = *reinterpret_cast<const T*>(src + row_off(c1, src_ld, src_rpc, src_cs) + u);
-      const T v2 = *reinterpret_cast<const T*>(src + row_off(c2, src_ld, src_rpc, src_cs) + u);
-      const T v3 = *reinterpret_cast<const T*>(src + row_off(c3, src_ld, src_rpc, src_cs) + u);
-      vadd(acc, v0);
-      vadd(acc, v1);
-      vadd(acc, v2);
-      vadd(acc, v3);
-    }
-    for (; k < e; ++k) {
-      const int32_t c0 = col[k];
-      vadd(acc, *reinterpret_cast<const T*>(src + row_off(c0, src_ld, src_rpc, src_cs) + u));
+    if (any_edges) {
+      const int32_t b = s_ptr[rl] - (LDS_COL ? base : 0), e = s_ptr[rl + 1] - (LDS_COL ? base : 0);
+      for (int32_t k = b; k < e; k += kGroup) {
+        T v[kGroup];
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+          const int32_t c = cols[min(k + j, e - 1)];
+          v[j] = *reinterpret_cast<const T*>(src + src_off<SRC_CHUNKED>((uint32_t)c, src_ld, src_rpc, src_cs) + u);
+        }
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+          T s = acc;
+          vadd(s, v[j]);
+          if (k + j < e) acc = s;
+        }
+      }
     }
     if (add0) {
       T s = *reinterpret_cast<const T*>(add0 + (int64_t)r * add0_ld + u);
@@ -111,6 +127,32 @@ __global__ __launch_bounds__(256) void k_gather_sum(const float* __restrict__ sr
     }
     if (add1) vadd(acc, *reinterpret_cast<const T*>(add1 + (int64_t)r * add1_ld + u));
     *reinterpret_cast<T*>(out + row_off(r, out_ld, out_rpc, out_cs) + u) = acc;
+  }
+}
+
+template <int VEC, bool SRC_CHUNKED>
+__global__ __launch_bounds__(256) void k_gather_sum(const float* __restrict__ src, int64_t src_ld, FastDiv src_rpc,
+                                                     int64_t src_cs, FastDiv upr, const int32_t* __restrict__ rowptr,
+                                                     const int32_t* __restrict__ col, uint32_t rows, uint32_t tile_rows,
+                                                     float* __restrict__ out, int64_t out_ld, FastDiv out_rpc,
+                                                     int64_t out_cs, const float* __restrict__ add0, int64_t add0_ld,
+                                                     const float* __restrict__ add1, int64_t add1_ld) {
+  __shared__ int32_t s_ptr[kMaxTileRows + 1];
+  __shared__ int32_t s_col[kColCap];
+  const uint32_t r0 = blockIdx.x * tile_rows;
+  const uint32_t nr = min(tile_rows, rows - r0);
+  if (threadIdx.x <= nr) s_ptr[threadIdx.x] = rowptr[r0 + threadIdx.x];
+  __syncthreads();
+  const int32_t base = s_ptr[0];
+  const int32_t ncols = s_ptr[nr] - base;
+  if (ncols <= kColCap) {
+    for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) s_col[i] = col[base + i];
+    __syncthreads();
+    tile_body<VEC, true, SRC_CHUNKED>(src, src_ld, src_rpc, src_cs, upr, s_ptr, s_col, base, r0, nr, out, out_ld, out_rpc, out_cs,
+                         add0, add0_ld, add1, add1_ld, ncols > 0);
+  } else {
+    tile_body<VEC, false, SRC_CHUNKED>(src, src_ld, src_rpc, src_cs, upr, s_ptr, col, base, r0, nr, out, out_ld, out_rpc, out_cs,
+                          add0, add0_ld, add1, add1_ld, true);
   }
 }
 
@@ -145,16 +187,18 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   const FastDiv srpc = make_fastdiv(src_rpc > 0 ? (uint32_t)src_rpc : 0);
   const FastDiv orpc = make_fastdiv(out_rpc > 0 ? (uint32_t)out_rpc : 0);
   const int threads = 256;
-  const int64_t blocks = std::min<int64_t>(cdiv(rows * upr_i, threads), 256 * 32);
-  if (vec == 4)
-    hipLaunchKernelGGL(k_gather_sum<4>, dim3((unsigned)blocks), dim3(threads), 0, stream, src, src_ld, srpc,
-                       src_cs, upr, rowptr, col, (uint32_t)rows, out, out_ld, orpc, out_cs, add0, add0_ld, add1, add1_ld);
-  else if (vec == 2)
-    hipLaunchKernelGGL(k_gather_sum<2>, dim3((unsigned)blocks), dim3(threads), 0, stream, src, src_ld, srpc,
-                       src_cs, upr, rowptr, col, (uint32_t)rows, out, out_ld, orpc, out_cs, add0, add0_ld, add1, add1_ld);
-  else
-    hipLaunchKernelGGL(k_gather_sum<1>, dim3((unsigned)blocks), dim3(threads), 0, stream, src, src_ld, srpc,
-                       src_cs, upr, rowptr, col, (uint32_t)rows, out, out_ld, orpc, out_cs, add0, add0_ld, add1, add1_ld);
+  // tile height: 64 rows when that still gives >= 2048 workgroups (8 per CU), else fewer rows
+  int64_t tr = kMaxTileRows;
+  while (tr > 4 && cdiv(rows, tr) < 2048) tr >>= 1;
+  const int64_t blocks = cdiv(rows, tr);
+  using KFn = void (*)(const float*, int64_t, FastDiv, int64_t, FastDiv, const int32_t*, const int32_t*, uint32_t,
+                      uint32_t, float*, int64_t, FastDiv, int64_t, const float*, int64_t, const float*, int64_t);
+  const bool chunked = src_rpc > 0;
+  KFn fn = vec == 4 ? (chunked ? k_gather_sum<4, true> : k_gather_sum<4, false>)
+           : vec == 2 ? (chunked ? k_gather_sum<2, true> : k_gather_sum<2, false>)
+                      : (chunked ? k_gather_sum<1, true> : k_gather_sum<1, false>);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(threads), 0, stream, src, src_ld, srpc, src_cs, upr, rowptr, col,
+                     (uint32_t)rows, (uint32_t)tr, out, out_ld, orpc, out_cs, add0, add0_ld, add1, add1_ld);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }

@@ -115,6 +115,34 @@ def test_hop_forward_bit_exact_widths(d):
     assert torch.equal(out.cpu(), ref)
 
 
+@pytest.mark.parametrize("hub_degree", [9, 300, 20_000])
+def test_hop_forward_bit_exact_hubs(hub_degree):
+    """Ragged degrees: rows longer than one 8-gather group and row tiles whose edge list exceeds the
+    LDS staging capacity (global col path); empty rows and empty tiles in between; backward too."""
+    from aimx.plan import GraphPlan
+    from aimx import ops
+    _, om = _oracle()
+    rng = np.random.default_rng(hub_degree)
+    n, h = 3000, 3
+    base_t = rng.integers(0, n, 20_000)
+    hubs = rng.choice(n, 5, replace=False)
+    t = np.concatenate([base_t, np.repeat(hubs, hub_degree)])
+    s = rng.integers(-n, 2 * n, t.shape[0])
+    perm = rng.permutation(t.shape[0])
+    t, s = torch.from_numpy(t[perm]), torch.from_numpy(s[perm])
+    x = torch.randn(n, 76, generator=torch.Generator().manual_seed(3))
+    ref = torch.cat(om.message_passing(x, t, s, h), 0)
+    plan = GraphPlan(n, h, target=t.to(DEV), src=s.to(DEV))
+    xg = x.to(DEV).requires_grad_()
+    out = ops.hop(plan, xg)
+    assert torch.equal(out.detach().cpu(), ref)
+    w = torch.randn(ref.shape, generator=torch.Generator().manual_seed(4))
+    (out * w.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_()
+    (torch.cat(om.message_passing(x64, t, s, h), 0) * w.double()).sum().backward()
+    assert norm_rel(xg.grad.cpu().numpy(), x64.grad.numpy()) < 1e-6
+
+
 def test_hop_backward():
     from aimx.plan import GraphPlan
     from aimx import ops

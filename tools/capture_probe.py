@@ -5,6 +5,10 @@ import time
 
 import torch
 
+if os.environ.get("CRASHTRACE"):
+    import ctypes
+    ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_crashtrace.so")).crashtrace_install()
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "aimnet-x2d_amd")]
 import bench  # noqa: E402
@@ -82,11 +86,15 @@ if "gemm_b" in which:
 if "stack_b" in which:
     from models import GNN
     m = GNN(bench.FS, 128, 1).to(dev)
-    params = []
-    for l in m.message_passing_layers:
-        params += l._aimx_params()
-    cap("stack_b", lambda: ops.message_passing_stack(plan, xr, params, num_hops=3, num_layers=3, num_mlp=2,
-                                                     act="silu").sum().backward())
+
+    def stack_b():
+        # params are built inside the captured region: autograd nodes created on another stream
+        # (e.g. the legacy default stream) must not be part of a captured backward
+        params = []
+        for l in m.message_passing_layers:
+            params += l._aimx_params()
+        ops.message_passing_stack(plan, xr, params, num_hops=3, num_layers=3, num_mlp=2, act="silu").sum().backward()
+    cap("stack_b", stack_b)
 if "pool_b" in which:
     xp = torch.randn(n, 128, device=dev, requires_grad=True)
     Wp = torch.randn(4, 128, device=dev, requires_grad=True)

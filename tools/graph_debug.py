@@ -39,15 +39,16 @@ def clip_step():
     opt.step()
 
 
-opt.zero_grad(set_to_none=True)
-l = fwd_bwd()
-clip_step()
-torch.cuda.synchronize()
-log("eager padded step ok, loss", float(l))
-if stage == "eager":
-    sys.exit(0)
 side = torch.cuda.Stream()
 side.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(side):
+    opt.zero_grad(set_to_none=True)
+    lv = float(fwd_bwd())  # keep no reference to the eager autograd graph
+    clip_step()
+torch.cuda.synchronize()
+log("eager padded step ok, loss", lv)
+if stage == "eager":
+    sys.exit(0)
 with torch.cuda.stream(side):
     for _ in range(2):
         opt.zero_grad(set_to_none=True)
