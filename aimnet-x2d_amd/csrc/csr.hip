@@ -6,7 +6,8 @@
 // summation order (no float atomics). Pipeline (all on `stream`, no host sync):
 //   1. count   : deg[key(i)]++                      (int atomics)
 //   2. scan    : rowptr = exclusive_scan(deg)        (3-phase block scan)
-//   3. fill    : slot via cursor atomics            (unstable placement, plus key and item id)
+//   3. fill    : slot via cursor atomics            (unstable placement, plus key and item id;
+//                the cursor is the degree array, re-zeroed by the scan's last phase)
 //   4. order   : each item's rank among equal keys = #smaller item ids -> stable final position
 #include "aimx_common.h"
 
@@ -103,13 +104,23 @@ __global__ __launch_bounds__(1024) void k_scan_sums(int32_t* __restrict__ sums, 
   if (threadIdx.x == 0) *total = carry;
 }
 
+// Adds the block offsets and re-zeroes the degree array, which k_fill then uses as the per-row
+// insertion cursor (no separate memset: runtime memset nodes are avoided in captured graphs).
 __global__ __launch_bounds__(kScanThreads) void k_scan_add(int32_t* __restrict__ out, int64_t n,
-                                                           const int32_t* __restrict__ block_offs) {
+                                                           const int32_t* __restrict__ block_offs,
+                                                           int32_t* __restrict__ deg) {
   const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
   const int32_t off = block_offs[blockIdx.x];
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j)
-    if (base + j < n) out[base + j] += off;
+    if (base + j < n) {
+      out[base + j] += off;
+      deg[base + j] = 0;
+    }
+}
+
+__global__ void k_zero_i32(int32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
 }
 
 __global__ void k_fill(const int64_t* __restrict__ key, int64_t kstride, int64_t kmod,
@@ -181,8 +192,11 @@ extern "C" int aimx_csr_build(const int64_t* key, int64_t key_stride, int64_t ke
   ws += align256(sizeof(int32_t) * (size_t)(n_items + 1));
   int32_t* t_id = (int32_t*)ws;
 
-  AIMX_CHECK_HIP(hipMemsetAsync(deg, 0, sizeof(int32_t) * (size_t)(n_rows + 1), stream));
   const int threads = 256;
+  // zero-fill by kernel: hipMemsetAsync nodes misbehaved on graph replay (ROCm 7.2)
+  hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>(cdiv(n_rows + 1, threads), 4096)), dim3(threads),
+                     0, stream, deg, n_rows + 1);
+  AIMX_CHECK_LAUNCH();
   const int64_t grid_items = std::min<int64_t>(cdiv(n_items > 0 ? n_items : 1, threads), 8192);
   if (n_items > 0) {
     hipLaunchKernelGGL(k_count, dim3((unsigned)grid_items), dim3(threads), 0, stream, key, key_stride, key_mod,
@@ -195,13 +209,13 @@ extern "C" int aimx_csr_build(const int64_t* key, int64_t key_stride, int64_t ke
     AIMX_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, stream, bsum, nb, rowptr + n_rows);
     AIMX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kScanThreads), 0, stream, rowptr, n_rows, bsum);
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kScanThreads), 0, stream, rowptr, n_rows, bsum, deg);
     AIMX_CHECK_LAUNCH();
   } else {
-    AIMX_CHECK_HIP(hipMemsetAsync(rowptr, 0, sizeof(int32_t), stream));
+    hipLaunchKernelGGL(k_zero_i32, dim3(1), dim3(64), 0, stream, rowptr, (int64_t)1);
+    AIMX_CHECK_LAUNCH();
   }
   if (n_items == 0 || n_rows == 0) return AIMX_OK;
-  AIMX_CHECK_HIP(hipMemsetAsync(deg, 0, sizeof(int32_t) * (size_t)n_rows, stream));
   hipLaunchKernelGGL(k_fill, dim3((unsigned)grid_items), dim3(threads), 0, stream, key, key_stride, key_mod, val,
                      val_stride, val_mod, n_items, n_rows, rowptr, deg, t_key, t_val, t_id);
   AIMX_CHECK_LAUNCH();

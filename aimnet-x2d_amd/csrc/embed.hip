@@ -6,9 +6,10 @@
 // Backward (deterministic, no float atomics): the tables are tiny (119/9/7/7 rows x 64), so each
 // workgroup accumulates a chunk of atoms into a private copy of ALL tables in LDS — thread (t, c)
 // owns column c of table t, so it is the only writer of those LDS words and adds its chunk's
-// rows in atom order — then writes the partial tables; a second kernel sums the partials in
-// chunk order. PyTorch's embedding backward instead sorts the indices (radix sort + segment
-// offsets, several launches per table).
+// rows in atom order — then writes the partial tables; a second kernel sums the partials in a
+// fixed order (4 interleaved in-order wave sums, then wave order), so results are identical run to
+// run. PyTorch's embedding backward instead sorts the indices (radix sort + segment offsets,
+// several launches per table).
 #include <algorithm>
 
 #include "aimx_common.h"
@@ -16,7 +17,11 @@
 namespace aimx {
 namespace {
 
-constexpr int kChunk = 256;  // atoms per workgroup in the backward
+constexpr int kChunk = 64;   // min atoms per workgroup in the backward (>= 2 workgroups per CU at c2)
+constexpr int64_t kMaxChunks = 2048;  // bounds the partial-table workspace for very large batches
+inline int64_t chunk_of(int64_t N) { return std::max<int64_t>(kChunk, cdiv(std::max<int64_t>(N, 1), kMaxChunks)); }
+constexpr int kUnroll = 8;   // atoms whose index + gradient loads are in flight together
+constexpr int kReduceCols = 64, kReduceWaves = 4;
 
 __global__ void k_embed_gather(AimxEmbeddingTables t, int64_t N, float* __restrict__ out, int64_t ldo) {
   const int64_t width = (int64_t)t.n_tables * t.dim;
@@ -31,8 +36,8 @@ __global__ void k_embed_gather(AimxEmbeddingTables t, int64_t N, float* __restri
 }
 
 // blockDim.x == n_tables * dim (<= 1024); dynamic LDS = total_rows * dim floats.
-__global__ void k_embed_bwd_partial(AimxEmbeddingTables t, int64_t N, const float* __restrict__ dE, int64_t ldd,
-                                    float* __restrict__ partial, int64_t total_rows) {
+__global__ void k_embed_bwd_partial(AimxEmbeddingTables t, int64_t N, int64_t chunk, const float* __restrict__ dE,
+                                    int64_t ldd, float* __restrict__ partial, int64_t total_rows) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tb = threadIdx.x / (int)t.dim;
   const int c = threadIdx.x - tb * (int)t.dim;
@@ -40,30 +45,72 @@ __global__ void k_embed_bwd_partial(AimxEmbeddingTables t, int64_t N, const floa
   for (int i = 0; i < tb; ++i) row0 += t.rows[i];
   for (int64_t i = threadIdx.x; i < total_rows * t.dim; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
-  const int64_t j0 = (int64_t)blockIdx.x * kChunk, j1 = min(N, j0 + kChunk);
+  const int64_t j0 = (int64_t)blockIdx.x * chunk, j1 = min(N, j0 + chunk);
   const int64_t rows_tb = t.rows[tb];
   const int64_t* __restrict__ idx = t.index[tb];
-  for (int64_t j = j0; j < j1; ++j) {
-    const int64_t r = idx[j];
-    if (r >= 0 && r < rows_tb) lds[(row0 + r) * t.dim + c] += dE[j * ldd + (int64_t)tb * t.dim + c];
+  const float* __restrict__ g = dE + (int64_t)tb * t.dim + c;
+  // Loads are unconditional (clamped atom, clamped row) so 2*kUnroll of them are in flight; the
+  // LDS adds then run in atom order with a select, which keeps the sum sequential per column.
+  for (int64_t j = j0; j < j1; j += kUnroll) {
+    int64_t r[kUnroll];
+    float v[kUnroll];
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      const int64_t jj = min(j + q, j1 - 1);
+      r[q] = idx[jj];
+      v[q] = g[jj * ldd];
+    }
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      const bool ok = (j + q < j1) && r[q] >= 0 && r[q] < rows_tb;
+      const int64_t rr = ok ? r[q] : 0;
+      float* cell = &lds[(row0 + rr) * t.dim + c];
+      const float cur = *cell;
+      *cell = ok ? cur + v[q] : cur;
+    }
   }
   __syncthreads();
   float* out = partial + (int64_t)blockIdx.x * total_rows * t.dim;
   for (int64_t i = threadIdx.x; i < total_rows * t.dim; i += blockDim.x) out[i] = lds[i];
 }
 
-__global__ void k_embed_bwd_reduce(AimxEmbeddingTables t, const float* __restrict__ partial, int64_t nblk,
-                                   int64_t total_rows) {
+// Column sums over the per-chunk partial tables: a workgroup owns kReduceCols consecutive table
+// words; wave w sums chunks w, w+4, ... in order, then the 4 wave sums are added in wave order
+// (a fixed order: deterministic run to run).
+__global__ __launch_bounds__(kReduceCols * kReduceWaves) void k_embed_bwd_reduce(AimxEmbeddingTables t,
+                                                                               const float* __restrict__ partial,
+                                                                               int64_t nblk, int64_t total_rows) {
+  __shared__ float part[kReduceWaves][kReduceCols];
   const int64_t total = total_rows * t.dim;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int64_t b = 0; b < nblk; ++b) s += partial[b * total + i];
+  const int lane = threadIdx.x % kReduceCols, w = threadIdx.x / kReduceCols;
+  const int64_t i = (int64_t)blockIdx.x * kReduceCols + lane;
+  const int64_t ic = min(i, total - 1);
+  float s = 0.f;
+  int64_t b = w;
+  for (; b + 3 * kReduceWaves < nblk; b += 4 * kReduceWaves) {
+    const float a0 = partial[b * total + ic], a1 = partial[(b + kReduceWaves) * total + ic];
+    const float a2 = partial[(b + 2 * kReduceWaves) * total + ic], a3 = partial[(b + 3 * kReduceWaves) * total + ic];
+    s += a0;
+    s += a1;
+    s += a2;
+    s += a3;
+  }
+  for (; b < nblk; b += kReduceWaves) s += partial[b * total + ic];
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i < total) {
+    float acc = part[0][lane];
+    for (int q = 1; q < kReduceWaves; ++q) acc += part[q][lane];
     int64_t r = i / t.dim;
     const int64_t c = i - r * t.dim;
     int tb = 0;
     while (r >= t.rows[tb]) r -= t.rows[tb++];
-    t.grad[tb][r * t.dim + c] = s;
+    t.grad[tb][r * t.dim + c] = acc;
   }
+}
+
+__global__ void k_zero_f32(float* __restrict__ p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0.f;
 }
 
 __global__ void k_act_bwd(int kind, const float* __restrict__ dy, int64_t ldy, const float* __restrict__ pre,
@@ -107,7 +154,7 @@ extern "C" int aimx_embedding_gather(const AimxEmbeddingTables* t, int64_t N, fl
 
 extern "C" size_t aimx_embedding_backward_workspace_bytes(const AimxEmbeddingTables* t, int64_t N) {
   if (!tables_ok(t)) return 0;
-  return sizeof(float) * (size_t)(cdiv(std::max<int64_t>(N, 1), kChunk) * total_rows_of(t) * t->dim);
+  return sizeof(float) * (size_t)(cdiv(std::max<int64_t>(N, 1), chunk_of(N)) * total_rows_of(t) * t->dim);
 }
 
 extern "C" int aimx_embedding_backward(const AimxEmbeddingTables* t, int64_t N, const float* dE, int64_t ldd,
@@ -117,18 +164,24 @@ extern "C" int aimx_embedding_backward(const AimxEmbeddingTables* t, int64_t N, 
   for (int i = 0; i < t->n_tables; ++i)
     if (!t->grad[i]) return AIMX_EARG;
   const int64_t tr = total_rows_of(t);
-  if (N == 0) {
-    for (int i = 0; i < t->n_tables; ++i)
-      AIMX_CHECK_HIP(hipMemsetAsync(t->grad[i], 0, sizeof(float) * t->rows[i] * t->dim, s));
+  if (N == 0) {  // no atoms: zero gradients (by kernel; no runtime memset nodes in captured graphs)
+    for (int i = 0; i < t->n_tables; ++i) {
+      const int64_t cnt = t->rows[i] * t->dim;
+      hipLaunchKernelGGL(k_zero_f32, dim3((unsigned)std::min<int64_t>(cdiv(cnt, 256), 1024)), dim3(256), 0, s,
+                         t->grad[i], cnt);
+      AIMX_CHECK_LAUNCH();
+    }
     return AIMX_OK;
   }
   if (ws_bytes < aimx_embedding_backward_workspace_bytes(t, N) || !ws) return AIMX_EARG;
-  const int64_t nblk = cdiv(N, kChunk);
+  const int64_t chunk = chunk_of(N);
+  const int64_t nblk = cdiv(N, chunk);
   const size_t lds = sizeof(float) * (size_t)(tr * t->dim);
   hipLaunchKernelGGL(k_embed_bwd_partial, dim3((unsigned)nblk), dim3((unsigned)(t->n_tables * t->dim)), lds, s, *t, N,
-                     dE, ldd, (float*)ws, tr);
+                     chunk, dE, ldd, (float*)ws, tr);
   AIMX_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_embed_bwd_reduce, dim3((unsigned)cdiv(tr * t->dim, 256)), dim3(256), 0, s, *t,
+  hipLaunchKernelGGL(k_embed_bwd_reduce, dim3((unsigned)cdiv(tr * t->dim, kReduceCols)),
+                     dim3(kReduceCols * kReduceWaves), 0, s, *t,
                      (const float*)ws, nblk, tr);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;

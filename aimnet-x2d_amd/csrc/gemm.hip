@@ -150,9 +150,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   constexpr int LA = AK ? BM * SA : BK * SA;
   constexpr int LB = BKC ? BN * SB : BK * SB;
   constexpr int NA = BM * BK / 256, NB = BN * BK / 256;
-  __shared__ __attribute__((aligned(16))) float smem[LA + LB + 4];
-  float* As = smem;
-  float* Bs = smem + LA;
+  // two LDS stages (slice s computes from one while slice s+1 is stored into the other)
+  __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB) + 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -183,8 +182,7 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  float ra[NA], rb[NB];
-  auto load_slice = [&](int k0, bool tail) {
+  auto load_slice = [&](int k0, bool tail, float (&ra)[NA], float (&rb)[NB]) {
     // A
     if (AK) {
       const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) * sam + (uint32_t)(k0 + a_k));
@@ -224,7 +222,9 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       }
     }
   };
-  auto store_slice = [&]() {
+  auto store_slice = [&](const float (&ra)[NA], const float (&rb)[NB], int stage) {
+    float* As = smem + stage * (LA + LB);
+    float* Bs = As + LA;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int mm = AK ? a_m + i * A_STEP : a_m;
@@ -238,14 +238,9 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       Bs[BKC ? (nn * SB + kk) : (kk * SB + nn)] = rb[i];
     }
   };
-
-  if (kbeg < kend) load_slice(kbeg, kbeg + BK > kend);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    store_slice();
-    __syncthreads();
-    const int kn = k0 + BK;
-    if (kn < kend) load_slice(kn, kn + BK > kend);
+  auto compute_slice = [&](int stage) {
+    const float* As = smem + stage * (LA + LB);
+    const float* Bs = As + LA;
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       const int kr = 4 * s + (lane >> 4);
@@ -265,14 +260,94 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+  // Software pipeline: two register sets and two LDS stages. While slice s is multiplied from
+  // LDS, slice s+1 waits in registers (its loads were issued one slice earlier) and slice s+2's
+  // loads are in flight, so each global load has two slices of MFMA work to land behind.
+  const int nsl = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  float ra0[NA], rb0[NB], ra1[NA], rb1[NB];
+  if (nsl > 0) load_slice(kbeg, kbeg + BK > kend, ra0, rb0);
+  if (nsl > 1) load_slice(kbeg + BK, kbeg + 2 * BK > kend, ra1, rb1);
+  if (nsl > 0) store_slice(ra0, rb0, 0);
+  __syncthreads();
+  for (int sl = 0; sl < nsl; sl += 2) {
+    if (sl + 2 < nsl) {
+      const int k2 = kbeg + (sl + 2) * BK;
+      load_slice(k2, k2 + BK > kend, ra0, rb0);
+    }
+    compute_slice(0);
+    if (sl + 1 < nsl) store_slice(ra1, rb1, 1);
+    __syncthreads();
+    if (sl + 1 >= nsl) break;
+    if (sl + 3 < nsl) {
+      const int k3 = kbeg + (sl + 3) * BK;
+      load_slice(k3, k3 + BK > kend, ra1, rb1);
+    }
+    compute_slice(1);
+    if (sl + 2 < nsl) store_slice(ra0, rb0, 0);
+    __syncthreads();
+  }
+
+  if (gridDim.z > 1) {
+    // ---- split-K: this slice's partial tile goes to a slab in ACCUMULATOR order (thread tid's
+    // float4 for fragment (i, j) at ((i*TN + j)*256 + tid)*4), so slab writes and the reducer's
+    // reads are contiguous 16-B-per-lane streams ----
+    const int tile = blockIdx.x * gridDim.y + blockIdx.y;
+    const int64_t ntiles = (int64_t)gridDim.x * gridDim.y;
+    constexpr int TILE = BM * BN;
+    floatx4* slab = reinterpret_cast<floatx4*>(a.workspace + ((int64_t)blockIdx.z * ntiles + tile) * TILE);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) slab[(i * TN + j) * 256 + tid] = acc[i][j];
+    if (!a.counters) return;  // reduced by k_splitk_reduce
+    // ---- in-launch ordered reduce by the last arriver (release -> ticket -> acquire) ----
+    int* flag = reinterpret_cast<int*>(smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == (int)gridDim.z - 1);
+      if (last) {
+        __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    // slabs summed in slice order (deterministic), 8 slices' float4 loads in flight per fragment
+    const int S = (int)gridDim.z;
+    const floatx4* base = reinterpret_cast<const floatx4*>(a.workspace + (int64_t)tile * TILE);
+    const int64_t zstride = ntiles * TILE / 4;  // floatx4 per slice
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t off = (i * TN + j) * 256 + tid;
+        floatx4 s = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int z0 = 0; z0 < S; z0 += 8) {
+          floatx4 t[8];
+#pragma unroll
+          for (int w = 0; w < 8; ++w) t[w] = __builtin_nontemporal_load(&base[min(z0 + w, S - 1) * zstride + off]);
+#pragma unroll
+          for (int w = 0; w < 8; ++w)
+            if (z0 + w < S) s += t[w];
+        }
+        acc[i][j] = s;
+      }
   }
 
   // C/D layout of the 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg. The tile is
   // transposed through LDS so the epilogue walks rows with consecutive lanes on consecutive
   // columns: coalesced residual/bias/mask loads and C/pre stores (4 elements per thread per pass).
-  if (gridDim.z == 1) {
+  {
     constexpr int CS = BN + 1;
-    static_assert(BM * CS <= LA + LB, "C tile must fit the staging LDS");
+    static_assert(BM * CS <= 2 * (LA + LB), "C tile must fit the staging LDS");
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -295,83 +370,29 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       }
       epilogue_n<4>(a, em, en, ev);
     }
-    return;
-  }
-  // ---- split-K: write this slice's partial slab ----
-  float* slab = a.workspace + (int64_t)blockIdx.z * M * N;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wc * WN + j * 16 + (lane & 15);
-        if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
-      }
-  if (!a.counters) return;  // reduced by k_splitk_reduce
-  // ---- in-launch ordered reduce by the last arriver (release -> ticket -> acquire) ----
-  int* flag = reinterpret_cast<int*>(smem);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int tile = blockIdx.x * gridDim.y + blockIdx.y;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (old == (int)gridDim.z - 1);
-    if (last) {
-      __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  const int64_t total = (int64_t)M * N;
-  const int S = (int)gridDim.z;
-#pragma unroll 1
-  for (int q0 = 0; q0 < BM * BN / 256; q0 += 4) {
-    int em[4], en[4];
-    int64_t off[4];
-    float ev[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + (q0 + u) * 256;
-      em[u] = m0 + e / BN;
-      en[u] = n0 + e % BN;
-      off[u] = (em[u] < M && en[u] < N) ? (int64_t)em[u] * N + en[u] : 0;
-      ev[u] = 0.f;
-    }
-    // slabs summed in slice order, 8 slices' loads in flight per element at a time
-    for (int z0 = 0; z0 < S; z0 += 8) {
-      float t[4][8];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-          const bool okz = z0 + w < S;
-          const float x = a.workspace[okz ? (int64_t)(z0 + w) * total + off[u] : 0];
-          t[u][w] = okz ? x : 0.f;
-        }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int w = 0; w < 8; ++w)
-          if (z0 + w < S) ev[u] += t[u][w];
-    }
-    epilogue_n<4>(a, em, en, ev);
   }
 }
 
-__global__ void k_splitk_reduce(const AimxGemmArgs a, int splits) {
+// Fallback when no counter array is supplied: one thread per output element sums the slabs in
+// slice order. Slab element (m, n) of tile (tm, tn) sits where thread tid's accumulator fragment
+// put it (see the split-K branch of k_gemm).
+template <int BM, int BN>
+__global__ void k_splitk_reduce(const AimxGemmArgs a, int splits, int tiles_n) {
+  constexpr int WM = BM / 2, WN = BN / 2, TN = WN / 16;
   const int64_t total = a.M * a.N;
+  const int64_t ntiles = (int64_t)((a.M + BM - 1) / BM) * tiles_n;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(t / a.N), n = (int)(t % a.N);
+    const int tile = (m / BM) * tiles_n + n / BN;
+    const int lm = m % BM, ln = n % BN;
+    const int wr = lm / WM, wc = ln / WN, i = (lm % WM) / 16, j = (ln % WN) / 16;
+    const int r = lm % 4, lane = ((lm % 16) / 4) * 16 + (ln % 16);
+    const int tid = (wr * 2 + wc) * 64 + lane;
+    const int64_t off = ((int64_t)((i * TN + j) * 256 + tid)) * 4 + r;
     float v[1] = {0.f};
-    for (int z = 0; z < splits; ++z) v[0] += a.workspace[(int64_t)z * total + t];
-    const int m[1] = {(int)(t / a.N)}, n[1] = {(int)(t % a.N)};
-    epilogue_n<1>(a, m, n, v);
+    for (int z = 0; z < splits; ++z) v[0] += a.workspace[((int64_t)z * ntiles + tile) * (BM * BN) + off];
+    const int mm[1] = {m}, nn[1] = {n};
+    epilogue_n<1>(a, mm, nn, v);
   }
 }
 
@@ -426,7 +447,7 @@ void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s,
 
 size_t gemm_workspace_floats(const AimxGemmArgs& a) {
   const Plan p = plan_gemm(a);
-  return p.splits > 1 ? (size_t)p.splits * (size_t)a.M * (size_t)a.N : 0;
+  return p.splits > 1 ? (size_t)p.splits * (size_t)(cdiv(a.M, p.bm) * cdiv(a.N, p.bn)) * p.bm * p.bn : 0;
 }
 
 int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
@@ -449,7 +470,7 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   const uint32_t a_bytes = (uint32_t)std::max<int64_t>(a_ext, 4);
   const uint32_t b_bytes = (uint32_t)std::max<int64_t>(b_ext, 4);
   Plan p = plan_gemm(a);
-  if (p.splits > 1 && (!a.workspace || a.workspace_bytes < sizeof(float) * (size_t)p.splits * a.M * a.N)) {
+  if (p.splits > 1 && (!a.workspace || a.workspace_bytes < sizeof(float) * gemm_workspace_floats(a))) {
     p.splits = 1;
     p.kchunk = std::max<int64_t>(cdiv(a.K, kBK) * kBK, kBK);
   }
@@ -466,7 +487,13 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   AIMX_CHECK_LAUNCH();
   if (p.splits > 1 && !a.counters) {
     const int64_t blocks = std::min<int64_t>(cdiv(a.M * a.N, 256), 2048);
-    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, a, p.splits);
+    const int tn = (int)grid.y;
+    if (p.bm == 64 && p.bn == 64)
+      hipLaunchKernelGGL((k_splitk_reduce<64, 64>), dim3((unsigned)blocks), dim3(256), 0, s, a, p.splits, tn);
+    else if (p.bm == 64)
+      hipLaunchKernelGGL((k_splitk_reduce<64, 32>), dim3((unsigned)blocks), dim3(256), 0, s, a, p.splits, tn);
+    else
+      hipLaunchKernelGGL((k_splitk_reduce<32, 32>), dim3((unsigned)blocks), dim3(256), 0, s, a, p.splits, tn);
     AIMX_CHECK_LAUNCH();
   }
   return AIMX_OK;

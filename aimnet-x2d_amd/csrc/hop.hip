@@ -6,8 +6,9 @@
 // (edges with target t, ascending edge id) and sums the source rows in that order starting from
 // +0.0f, which reproduces CPU ATen scatter_add_ bit for bit. Lanes run along the feature dim with
 // VEC-wide (16/8/4-byte) loads; a 64-lane wave covers 64*VEC consecutive floats of the flattened
-// [rows, D] output, so the stores and the gathered source rows are coalesced, and the index loads
-// (rowptr/col, int32) are broadcast within a row. Source rows of one molecule sit together in
+// [rows, D] output, so the stores and the gathered source rows are coalesced. A workgroup owns a
+// tile of consecutive rows and stages the tile's rowptr/col slices in LDS first (see k_gather_sum
+// below). Source rows of one molecule sit together in
 // HBM, so neighbour re-reads hit L2; the only compulsory HBM traffic is x once, the CSR once and
 // the output once (SURVEY.md §8d algorithmic bytes).
 #include <algorithm>
@@ -187,9 +188,10 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   const FastDiv srpc = make_fastdiv(src_rpc > 0 ? (uint32_t)src_rpc : 0);
   const FastDiv orpc = make_fastdiv(out_rpc > 0 ? (uint32_t)out_rpc : 0);
   const int threads = 256;
-  // tile height: 64 rows when that still gives >= 2048 workgroups (8 per CU), else fewer rows
-  int64_t tr = kMaxTileRows;
-  while (tr > 4 && cdiv(rows, tr) < 2048) tr >>= 1;
+  // tile height: ~2 vector units per thread, then shorter tiles while the grid is under 4
+  // workgroups per CU (small batches are latency-bound: more workgroups hide more latency)
+  int64_t tr = std::min<int64_t>(kMaxTileRows, std::max<int64_t>(1, 2 * threads / upr_i));
+  while (tr > 1 && cdiv(rows, tr) < 1024) tr = std::max<int64_t>(1, tr / 2);
   const int64_t blocks = cdiv(rows, tr);
   using KFn = void (*)(const float*, int64_t, FastDiv, int64_t, FastDiv, const int32_t*, const int32_t*, uint32_t,
                       uint32_t, float*, int64_t, FastDiv, int64_t, const float*, int64_t, const float*, int64_t);
