@@ -404,15 +404,17 @@ struct Plan {
 Plan plan_gemm(const AimxGemmArgs& a) {
   Plan p;
   auto tiles = [&](int bm, int bn) { return cdiv(a.M, bm) * cdiv(a.N, bn); };
-  // Prefer the largest tile that still gives >= ~1 block per CU; else the smallest tile.
-  if (a.N <= 32) {
-    p.bm = 64, p.bn = 32;
-    if (tiles(64, 32) < 256) p.bm = 32, p.bn = 32;
-  } else {
-    p.bm = 64, p.bn = 64;
-    if (tiles(64, 64) < 256) {
-      p.bm = 64, p.bn = 32;
-      if (tiles(64, 32) < 256) p.bm = 32, p.bn = 32;
+  // Pick the tile that minimises the busiest CU's MFMA work, ceil(tiles / CUs) * BM * BN (edge
+  // tiles count in full: N = 152 runs 5 x 32 columns rather than 3 x 64); ties go to the larger
+  // tile (fewer operand re-reads).
+  const int cand[3][2] = {{64, 64}, {64, 32}, {32, 32}};
+  int64_t best = -1;
+  for (const auto& c : cand) {
+    const int64_t w = cdiv(tiles(c[0], c[1]), 256) * c[0] * c[1];
+    if (best < 0 || w < best) {
+      best = w;
+      p.bm = c[0];
+      p.bn = c[1];
     }
   }
   const int64_t t = tiles(p.bm, p.bn);
