@@ -80,6 +80,15 @@ class EmbeddingTables(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", c_ptr), ("grad", c_ptr), ("exp_avg", c_ptr), ("exp_avg_sq", c_ptr), ("numel", c_i64),
+                ("group", c_i32)]
+
+
+class AdamHyper(ctypes.Structure):
+    _fields_ = [("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("weight_decay", c_f32), ("max_grad_norm", c_f32)]
+
+
 _SIGS = {
     "aimx_version": (ctypes.c_char_p, []),
     "aimx_csr_workspace_bytes": (c_size, [c_i64, c_i64]),
@@ -109,6 +118,9 @@ _SIGS = {
     "aimx_embedding_backward_workspace_bytes": (c_size, [ctypes.POINTER(EmbeddingTables), c_i64]),
     "aimx_embedding_backward": (c_i32, [ctypes.POINTER(EmbeddingTables), c_i64, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "aimx_act_backward": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_fused_adam_workspace_bytes": (c_size, [ctypes.POINTER(AdamTensor), c_i32]),
+    "aimx_fused_adam": (c_i32, [ctypes.POINTER(AdamTensor), c_i32, ctypes.POINTER(AdamHyper), c_ptr, c_ptr, c_ptr,
+                                c_ptr, c_size, c_ptr]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

@@ -111,28 +111,33 @@ class DeviceBatch:
                 self.trans)
 
 
-def pad_collated(col, n_max, e_max, g_real):
+def pad_collated(col, n_max, e_max, g_real, n_pad_mols=8):
     """Pad a collated batch to static shapes for graph replay (SURVEY.md §8d "padded batches").
 
-    The slack atoms form ONE extra padding molecule (index g_real) and the slack edges are
-    self-pairs inside it, so every real molecule's values are untouched (molecules never
-    interact); callers drop row g_real of the per-molecule outputs from the loss.
-    Requires n_max > N (at least one padding atom) and e_max >= E.
+    The slack atoms form `n_pad_mols` extra padding molecules (indices g_real .. g_real+n_pad_mols-1,
+    sizes as equal as possible; some may be empty) and the slack edges are self-pairs spread over
+    the padding atoms, so every real molecule's values are untouched (molecules never interact);
+    callers drop rows >= g_real of the per-molecule outputs from the loss. Several small padding
+    molecules instead of one large one keep the per-molecule kernels (one workgroup per molecule)
+    free of a long serial tail. Requires n_max > N (at least one padding atom) and e_max >= E.
     """
     n = col["batch"].shape[0]
     e = col["edges"].shape[0]
-    if n_max <= n or e_max < e:
-        raise ValueError(f"padding too small: atoms {n}/{n_max}, edges {e}/{e_max}")
+    if n_max <= n or e_max < e or n_pad_mols < 1:
+        raise ValueError(f"padding too small: atoms {n}/{n_max}, edges {e}/{e_max}, molecules {n_pad_mols}")
     n_pad = n_max - n
     feats = np.zeros((n_max, col["feats"].shape[1]), np.int64)
     feats[:n] = col["feats"]
-    batch = np.full(n_max, g_real, np.int64)
+    sizes = np.full(n_pad_mols, n_pad // n_pad_mols, np.int64)
+    sizes[: n_pad % n_pad_mols] += 1
+    batch = np.empty(n_max, np.int64)
     batch[:n] = col["batch"]
+    batch[n:] = g_real + np.repeat(np.arange(n_pad_mols, dtype=np.int64), sizes)
     edges = np.empty((e_max, 2), np.int64)
     edges[:e] = col["edges"]
     # slack edges: self-pairs spread over the padding atoms (no long CSR row)
     pad = n + (np.arange(e_max - e, dtype=np.int64) % n_pad)
     edges[e:, 0] = pad
     edges[e:, 1] = pad
-    n_atoms = np.concatenate([col["n_atoms"], [n_max - n]])
+    n_atoms = np.concatenate([col["n_atoms"], sizes])
     return {"edges": edges, "feats": feats, "batch": batch, "n_atoms": n_atoms, "real_atoms": n, "real_edges": e}

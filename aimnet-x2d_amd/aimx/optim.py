@@ -1,0 +1,116 @@
+"""Fused gradient clipping + Adam on the device (aimx_fused_adam, include/aimx.h).
+
+Drop-in for the reference trainer's step (src/training/trainer.py:163-164, 221-223):
+
+    torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+    optimizer.step()                      # optimizer = torch.optim.Adam(params, lr=...)
+
+becomes
+
+    optimizer = FusedAdam(params, lr=..., max_grad_norm=1.0)
+    optimizer.step()
+
+Same update as torch.optim.Adam (amsgrad=False, maximize=False), with the same param_groups /
+state layout ('step', 'exp_avg', 'exp_avg_sq' per parameter), and the same in-place gradient
+scaling clip_grad_norm_ performs. The whole step is three kernel launches independent of the
+number of parameters, and it is graph-capturable: the step counter and the per-group learning
+rates are device tensors. A scheduler that changes group['lr'] takes effect at the next eager
+step; a captured graph reads the device copy, so call sync_lr() (outside the capture) after
+changing lr when replaying a graph.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import AdamHyper, AdamTensor, AimxError, check, stream_ptr
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_grad_norm=None):
+        if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1) or weight_decay < 0:
+            raise ValueError("FusedAdam: invalid hyper-parameter")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        self.max_grad_norm = max_grad_norm
+        self._step_t = None
+        self._lr_t = None
+        self._lr_host = None
+        self._norm = None
+        self._ws = None
+
+    def _shared_hyper(self):
+        g0 = self.param_groups[0]
+        for g in self.param_groups[1:]:
+            if g["betas"] != g0["betas"] or g["eps"] != g0["eps"] or g["weight_decay"] != g0["weight_decay"]:
+                raise AimxError("FusedAdam: parameter groups may differ in lr only")
+        return g0
+
+    def _device_state(self, dev):
+        if self._step_t is None:
+            self._step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+            self._norm = torch.zeros(1, dtype=torch.float32, device=dev)
+            self._lr_t = torch.zeros(len(self.param_groups), dtype=torch.float32, device=dev)
+        lrs = [float(g["lr"]) for g in self.param_groups]
+        if lrs != self._lr_host and not torch.cuda.is_current_stream_capturing():
+            self._lr_t.copy_(torch.tensor(lrs, dtype=torch.float32))
+            self._lr_host = lrs
+
+    def sync_lr(self):
+        """Push group['lr'] values to the device copy (call outside graph capture)."""
+        if self._lr_t is not None:
+            self._lr_host = None
+            self._device_state(self._lr_t.device)
+
+    @property
+    def last_grad_norm(self):
+        """Device tensor holding the total gradient norm of the last step (clip_grad_norm_'s value)."""
+        return self._norm
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        hyper_g = self._shared_hyper()
+        rows = []
+        dev = None
+        for gi, group in enumerate(self.param_groups):
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad
+                if not p.is_cuda or p.dtype != torch.float32 or g.dtype != torch.float32:
+                    raise AimxError("FusedAdam: fp32 parameters on the HIP device only (no CPU path)")
+                if not (p.is_contiguous() and g.is_contiguous()):
+                    raise AimxError("FusedAdam: parameters and gradients must be contiguous")
+                st = self.state[p]
+                if not st:
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                dev = p.device
+                rows.append((p, g, st["exp_avg"], st["exp_avg_sq"], gi))
+        if not rows:
+            return loss
+        self._device_state(dev)
+        for p, *_ in rows:
+            self.state[p]["step"] = self._step_t
+        arr = (AdamTensor * len(rows))()
+        for i, (p, g, m, v, gi) in enumerate(rows):
+            arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
+            arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
+            arr[i].numel, arr[i].group = p.numel(), gi
+        lib = _lib.load()
+        wsb = lib.aimx_fused_adam_workspace_bytes(arr, len(rows))
+        if self._ws is None or self._ws.numel() * 8 < wsb:
+            self._ws = torch.empty((wsb + 7) // 8, dtype=torch.float64, device=dev)
+        h = AdamHyper()
+        h.beta1, h.beta2 = hyper_g["betas"]
+        h.eps, h.weight_decay = hyper_g["eps"], hyper_g["weight_decay"]
+        h.max_grad_norm = float(self.max_grad_norm) if self.max_grad_norm else 0.0
+        check(lib.aimx_fused_adam(arr, len(rows), ctypes.byref(h), self._step_t.data_ptr(), self._lr_t.data_ptr(),
+                                  self._norm.data_ptr(), self._ws.data_ptr(), self._ws.numel() * 8,
+                                  stream_ptr(dev)), "fused_adam")
+        return loss

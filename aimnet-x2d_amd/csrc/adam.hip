@@ -1,0 +1,187 @@
+// Fused global-norm gradient clipping + Adam over a list of tensors (three launches per step).
+//
+// Reference: the trainer's step, src/training/trainer.py:163-164
+//   torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0); optimizer.step()
+// with optimizer = torch.optim.Adam(model.parameters(), lr) (trainer.py:221-223). PyTorch runs
+// these as ~2 elementwise launches per parameter tensor (plus foreach norm kernels): hundreds of
+// 3-5 us launches per step for this model. Here:
+//   1. k_adam_sumsq   : per-(tensor, slice) partial sums of g^2 (fp64)  -> workspace
+//   2. k_adam_scalars : one wave: total norm, clip coefficient, step += 1, bias corrections
+//   3. k_adam_update  : g *= coef (in place, as clip_grad_norm_ leaves it), [g += wd * p],
+//                       m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
+//                       p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// The tensor table travels in the kernel arguments (chunks of kAdamChunk tensors), so nothing is
+// copied host->device and the three launches capture into a HIP graph as plain kernel nodes. The
+// step counter and the per-group learning rates live in device memory (capturable).
+#include <algorithm>
+#include <cmath>
+
+#include "aimx_common.h"
+
+namespace aimx {
+namespace {
+
+constexpr int kAdamChunk = 48;        // tensors per launch (kernel-argument table)
+constexpr int kAdamThreads = 256;
+constexpr int64_t kSliceElems = 8192; // elements per workgroup slice
+
+struct AdamTable {
+  int32_t n;
+  int32_t blk0[kAdamChunk + 1];  // first workgroup of each tensor (relative to the chunk)
+  int32_t group[kAdamChunk];
+  int64_t numel[kAdamChunk];
+  float* param[kAdamChunk];
+  float* grad[kAdamChunk];
+  float* m[kAdamChunk];
+  float* v[kAdamChunk];
+};
+
+__device__ __forceinline__ int find_tensor(const AdamTable& t, int b) {
+  int i = 0;
+  while (i + 1 < t.n && t.blk0[i + 1] <= b) ++i;
+  return i;
+}
+
+__global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, double* __restrict__ partial) {
+  const int i = find_tensor(t, blockIdx.x);
+  const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
+  const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
+  const float* __restrict__ g = t.grad[i];
+  double acc = 0.0;
+  for (int64_t j = s0 + threadIdx.x; j < s1; j += kAdamThreads) {
+    const double x = g[j];
+    acc += x * x;
+  }
+  __shared__ double red[kAdamThreads / kWave];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int w = 0; w < kAdamThreads / kWave; ++w) s += red[w];
+    partial[blockIdx.x] = s;
+  }
+}
+
+// scal[0] = clip coefficient, scal[1] = 1 / bias_correction1, scal[2] = sqrt(bias_correction2),
+// scal[3] = total gradient norm (the value clip_grad_norm_ returns)
+__global__ void k_adam_scalars(const double* __restrict__ partial, int n_partial, float max_norm, float beta1,
+                               float beta2, float* __restrict__ step, float* __restrict__ scal,
+                               float* __restrict__ norm_out) {
+  double s = 0.0;
+  for (int j = threadIdx.x; j < n_partial; j += 64) s += partial[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (threadIdx.x == 0) {
+    const float total = (float)sqrt(s);
+    float coef = 1.f;
+    if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
+    const float st = *step + 1.f;
+    *step = st;
+    const float bc1 = 1.f - powf(beta1, st);
+    const float bc2 = 1.f - powf(beta2, st);
+    scal[0] = coef;
+    scal[1] = 1.f / bc1;
+    scal[2] = sqrtf(bc2);
+    scal[3] = total;
+    if (norm_out) *norm_out = total;
+  }
+}
+
+__global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t, const float* __restrict__ scal,
+                                                              const float* __restrict__ lr, float beta1, float beta2,
+                                                              float eps, float wd) {
+  const int i = find_tensor(t, blockIdx.x);
+  const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
+  const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
+  const float coef = scal[0], inv_bc1 = scal[1], bc2s = scal[2];
+  const float step_size = lr[t.group[i]] * inv_bc1;
+  float* __restrict__ p = t.param[i];
+  float* __restrict__ g = t.grad[i];
+  float* __restrict__ m = t.m[i];
+  float* __restrict__ v = t.v[i];
+  for (int64_t j = s0 + threadIdx.x; j < s1; j += kAdamThreads) {
+    float gj = g[j] * coef;
+    g[j] = gj;
+    const float pj = p[j];
+    if (wd != 0.f) gj += wd * pj;
+    const float mj = m[j] + (1.f - beta1) * (gj - m[j]);
+    const float vj = beta2 * v[j] + (1.f - beta2) * gj * gj;
+    m[j] = mj;
+    v[j] = vj;
+    p[j] = pj - step_size * (mj / (sqrtf(vj) / bc2s + eps));
+  }
+}
+
+int64_t blocks_of(int64_t numel) { return std::max<int64_t>(1, cdiv(numel, kSliceElems)); }
+
+}  // namespace
+}  // namespace aimx
+
+using namespace aimx;
+
+extern "C" size_t aimx_fused_adam_workspace_bytes(const AimxAdamTensor* tensors, int32_t n) {
+  if (!tensors || n < 0) return 0;
+  int64_t blocks = 0;
+  for (int32_t i = 0; i < n; ++i) blocks += blocks_of(tensors[i].numel);
+  return sizeof(double) * (size_t)(blocks + 1) + sizeof(float) * 8;
+}
+
+extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const AimxAdamHyper* h, float* step,
+                               const float* lr, float* norm_out, void* workspace, size_t workspace_bytes,
+                               aimx_stream_t stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (!tensors || n < 0 || !h || !step || !lr) return AIMX_EARG;
+  if (n == 0) return AIMX_OK;
+  if (!workspace || workspace_bytes < aimx_fused_adam_workspace_bytes(tensors, n)) return AIMX_EARG;
+  for (int32_t i = 0; i < n; ++i) {
+    const AimxAdamTensor& x = tensors[i];
+    if (x.numel < 0 || (x.numel > 0 && (!x.param || !x.grad || !x.exp_avg || !x.exp_avg_sq)) || x.group < 0)
+      return AIMX_EARG;
+  }
+  double* partial = (double*)workspace;
+  int64_t total_blocks = 0;
+  for (int32_t i = 0; i < n; ++i) total_blocks += blocks_of(tensors[i].numel);
+  float* scal = (float*)(partial + total_blocks + 1);
+  // chunk tables (host, by value into the kernel arguments)
+  auto for_chunks = [&](auto&& launch) -> int {
+    int64_t blk = 0;
+    for (int32_t c0 = 0; c0 < n; c0 += kAdamChunk) {
+      AdamTable t{};
+      t.n = std::min<int32_t>(kAdamChunk, n - c0);
+      int32_t b = 0;
+      for (int32_t k = 0; k < t.n; ++k) {
+        const AimxAdamTensor& x = tensors[c0 + k];
+        t.blk0[k] = b;
+        t.group[k] = x.group;
+        t.numel[k] = x.numel;
+        t.param[k] = x.param;
+        t.grad[k] = x.grad;
+        t.m[k] = x.exp_avg;
+        t.v[k] = x.exp_avg_sq;
+        b += (int32_t)blocks_of(x.numel);
+      }
+      t.blk0[t.n] = b;
+      const int rc = launch(t, b, blk);
+      if (rc) return rc;
+      blk += b;
+    }
+    return AIMX_OK;
+  };
+  int rc = for_chunks([&](const AdamTable& t, int32_t nb, int64_t blk) -> int {
+    hipLaunchKernelGGL(k_adam_sumsq, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, partial + blk);
+    AIMX_CHECK_LAUNCH();
+    return AIMX_OK;
+  });
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_adam_scalars, dim3(1), dim3(64), 0, s, (const double*)partial, (int)total_blocks,
+                     h->max_grad_norm, h->beta1, h->beta2, step, scal, norm_out);
+  AIMX_CHECK_LAUNCH();
+  return for_chunks([&](const AdamTable& t, int32_t nb, int64_t) -> int {
+    hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal, lr, h->beta1,
+                       h->beta2, h->eps, h->weight_decay);
+    AIMX_CHECK_LAUNCH();
+    return AIMX_OK;
+  });
+}

@@ -407,9 +407,11 @@ Plan plan_gemm(const AimxGemmArgs& a) {
   // Pick the tile that minimises the busiest CU's MFMA work, ceil(tiles / CUs) * BM * BN (edge
   // tiles count in full: N = 152 runs 5 x 32 columns rather than 3 x 64); ties go to the larger
   // tile (fewer operand re-reads).
+  // Grids of >= 2 full 64x64 waves over the chip keep 64x64 (operand reuse wins there).
   const int cand[3][2] = {{64, 64}, {64, 32}, {32, 32}};
   int64_t best = -1;
   for (const auto& c : cand) {
+    if (best >= 0 && tiles(64, 64) >= 512) break;
     const int64_t w = cdiv(tiles(c[0], c[1]), 256) * c[0] * c[1];
     if (best < 0 || w < best) {
       best = w;

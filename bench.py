@@ -64,6 +64,9 @@ def make_collated(cfg, n_batches, seed):
     return out
 
 
+PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from the loss)
+
+
 def make_batches(cfg, n_batches, seed, device, pad=False):
     """Device-resident batches. pad=True: static shapes for graph replay (one padding molecule)."""
     cols = make_collated(cfg, n_batches, seed)
@@ -74,9 +77,9 @@ def make_batches(cfg, n_batches, seed, device, pad=False):
     out = []
     for c, t, q in cols:
         real_atoms, real_edges = c["batch"].shape[0], c["edges"].shape[0]
-        pc = adata.pad_collated(c, n_max, e_max, cfg["batch"])
-        tg = np.concatenate([t, np.zeros((1, t.shape[1]), np.float32)])
-        qq = np.concatenate([q, np.zeros(1, np.float32)])
+        pc = adata.pad_collated(c, n_max, e_max, cfg["batch"], PAD_MOLS)
+        tg = np.concatenate([t, np.zeros((PAD_MOLS, t.shape[1]), np.float32)])
+        qq = np.concatenate([q, np.zeros(PAD_MOLS, np.float32)])
         b = adata.DeviceBatch(pc, device, targets=tg, total_charges=qq)
         b.real_atoms, b.real_edges = real_atoms, real_edges
         out.append(b)
@@ -196,6 +199,7 @@ def main():
         print(json.dumps(hop_roofline(make_batches(cfg, 1, 99, device)[0], cfg["hops"], device, cfg["hidden"])))
         return
 
+    from aimx.optim import FusedAdam
     from utils.distributed import GradientSync
     model = build_model(cfg, device)
     B = cfg["batch"]
@@ -206,7 +210,8 @@ def main():
         # forward + backward (+ RCCL all-reduce, eager, between two graphs when world > 1)
         # + grad-norm clip + Adam; each timed step copies a fresh resident batch into the static
         # inputs and replays.
-        opt = torch.optim.Adam(model.parameters(), lr=2.5e-4, capturable=True)
+        # reference step: clip_grad_norm_(1.0) + Adam (trainer.py:163-164), fused on the device
+        opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
         sync = GradientSync(model.parameters(), overlap=False) if world > 1 else None
         static = batches[0].clone()
 
@@ -217,7 +222,6 @@ def main():
             return loss
 
         def clip_step():
-            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
             opt.step()
 
         side = torch.cuda.Stream()
@@ -250,7 +254,7 @@ def main():
                 sync.finish()
                 g2.replay()
     else:
-        opt = torch.optim.Adam(model.parameters(), lr=2.5e-4)
+        opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
         sync = GradientSync(model.parameters()) if world > 1 else None
 
         def step(i):
@@ -261,7 +265,6 @@ def main():
             loss.backward()
             if sync is not None:
                 sync.finish()
-            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
             opt.step()
 
     for i in range(args.warmup):
@@ -302,8 +305,8 @@ def main():
             "config": {"workload": f"{args.config}: " + ("QM9-shaped" if cfg["source"] == "qm9" else "40-atom synthetic")
                        + f", hidden {cfg['hidden']}, {cfg['hops']} hops, {cfg['tasks']} task(s), attention pool, "
                        "train step fwd+bwd+clip+Adam, dropout 0.05"
-                       + (", HIP-graph replay of padded static batches (+1 padding molecule, excluded from"
-                          " the loss)" if args.graph else ", eager"),
+                       + (", HIP-graph replay of padded static batches (+8 padding molecules, excluded"
+                          " from the loss)" if args.graph else ", eager"),
                        "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
                        "mean_atoms_per_batch": round(atoms, 1), "mean_edges_per_batch": round(edges, 1),
                        "parallelism": f"dp{world}"},

@@ -235,6 +235,37 @@ int aimx_embedding_backward(const AimxEmbeddingTables* t, int64_t N, const float
 int aimx_act_backward(int32_t kind, const float* dy, int64_t ldy, const float* pre, int64_t ldp,
                       int64_t M, int64_t N, float* out, int64_t ldo, aimx_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Fused global-norm gradient clip + Adam step over a list of fp32 tensors (three launches).
+ * Replaces the trainer's  torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0);
+ * optimizer.step()  with optimizer = torch.optim.Adam(...) (reference
+ * src/training/trainer.py:163-164 and 221-223):
+ *   total = ||all grads||_2; coef = min(max_norm / (total + 1e-6), 1) (max_norm <= 0: no clip);
+ *   grad *= coef (in place); step += 1; [grad += weight_decay * param];
+ *   exp_avg = lerp(exp_avg, grad, 1 - beta1); exp_avg_sq = beta2*exp_avg_sq + (1-beta2)*grad^2;
+ *   param -= lr[group] / (1 - beta1^step) * exp_avg / (sqrt(exp_avg_sq) / sqrt(1 - beta2^step) + eps)
+ * `step` (one float) and `lr` (one float per parameter group) are device memory, so the call is
+ * graph-capturable and schedulers update lr without re-capture. *norm_out (nullable, device)
+ * receives the total norm clip_grad_norm_ returns.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+  int32_t group;
+} AimxAdamTensor;
+
+typedef struct {
+  float beta1, beta2, eps, weight_decay, max_grad_norm;
+} AimxAdamHyper;
+
+size_t aimx_fused_adam_workspace_bytes(const AimxAdamTensor* tensors, int32_t n);
+int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const AimxAdamHyper* hyper, float* step,
+                    const float* lr, float* norm_out, void* workspace, size_t workspace_bytes,
+                    aimx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -388,3 +388,37 @@ def test_train_mode_dropout_statistics_and_determinism():
     assert not torch.equal(y1, y3)
     y0 = ops.message_passing_stack(plan, x, params, **dict(kw, training=False))
     assert not torch.equal(y0, y1)
+
+
+# ------------------------------------------------------------------------------------ optimizer
+@pytest.mark.parametrize("max_norm,wd", [(1.0, 0.0), (None, 0.0), (0.05, 0.01)])
+def test_fused_adam_matches_torch_clip_and_adam(max_norm, wd):
+    """aimx_fused_adam == clip_grad_norm_(max_norm) + torch.optim.Adam (trainer.py:163-164, 221-223),
+    two parameter groups with different lr, several steps (fp32 rounding only)."""
+    from aimx.optim import FusedAdam
+    g = torch.Generator().manual_seed(7)
+    shapes = [(76, 304), (152,), (256, 256), (3,), (70000,)]
+    p0 = [torch.randn(s, generator=g) for s in shapes]
+    ours = [x.clone().to(DEV).requires_grad_() for x in p0]
+    ref = [x.clone().to(DEV).requires_grad_() for x in p0]
+    groups = lambda ps: [{"params": ps[:3], "lr": 1e-3}, {"params": ps[3:], "lr": 3e-4}]  # noqa: E731
+    opt = FusedAdam(groups(ours), weight_decay=wd, max_grad_norm=max_norm)
+    topt = torch.optim.Adam(groups(ref), weight_decay=wd)
+    for step in range(5):
+        grads = [torch.randn(s, generator=g) * (0.01 + step) for s in shapes]
+        for a, b, gr in zip(ours, ref, grads):
+            a.grad = gr.to(DEV).clone()
+            b.grad = gr.to(DEV).clone()
+        opt.step()
+        if max_norm:
+            tn = torch.nn.utils.clip_grad_norm_(ref, max_norm)
+            assert abs(float(opt.last_grad_norm) - float(tn)) <= 1e-5 * float(tn)
+        topt.step()
+        for a, b in zip(ours, ref):
+            assert torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-9)
+    for a, b in zip(ours, ref):
+        assert norm_rel(a.detach().cpu().numpy(), b.detach().cpu().numpy()) < 1e-6
+        st_a, st_b = opt.state[a], topt.state[b]
+        assert norm_rel(st_a["exp_avg"].cpu().numpy(), st_b["exp_avg"].cpu().numpy()) < 1e-6
+        assert norm_rel(st_a["exp_avg_sq"].cpu().numpy(), st_b["exp_avg_sq"].cpu().numpy()) < 1e-6
+        assert float(st_a["step"]) == float(st_b["step"]) == 5.0

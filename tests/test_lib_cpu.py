@@ -94,7 +94,20 @@ def test_pad_collated_keeps_real_molecules():
     from aimx.synth import QM9Asset
     col = adata.collate(QM9Asset().molecules(range(8)), 3)
     n, e = col["batch"].shape[0], col["edges"].shape[0]
-    pc = adata.pad_collated(col, n + 10, e + 25, 8)
+    pc = adata.pad_collated(col, n + 10, e + 25, 8, n_pad_mols=4)
     assert np.array_equal(pc["edges"][:e], col["edges"]) and np.array_equal(pc["batch"][:n], col["batch"])
-    assert (pc["batch"][n:] == 8).all() and pc["n_atoms"].sum() == n + 10
+    assert (pc["batch"][n:] >= 8).all() and (pc["batch"][n:] < 12).all() and pc["n_atoms"].sum() == n + 10
+    assert list(pc["n_atoms"][8:]) == [3, 3, 2, 2] and (np.diff(pc["batch"]) >= 0).all()
     assert (pc["edges"][e:] >= n).all() and (pc["edges"][e:] < n + 10).all()
+
+
+def test_fused_adam_has_no_cpu_path():
+    import pytest
+    import torch
+
+    from aimx import AimxError
+    from aimx.optim import FusedAdam
+    p = torch.zeros(4, requires_grad=True)
+    p.grad = torch.ones(4)
+    with pytest.raises(AimxError):
+        FusedAdam([p], lr=1e-3, max_grad_norm=1.0).step()
