@@ -86,7 +86,8 @@ class AdamTensor(ctypes.Structure):
 
 
 class AdamHyper(ctypes.Structure):
-    _fields_ = [("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("weight_decay", c_f32), ("max_grad_norm", c_f32)]
+    _fields_ = [("beta1", c_f32), ("beta2", c_f32), ("one_minus_beta1", c_f32), ("one_minus_beta2", c_f32),
+                ("eps", c_f32), ("weight_decay", c_f32), ("max_grad_norm", c_f32)]
 
 
 _SIGS = {

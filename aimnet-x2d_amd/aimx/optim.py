@@ -108,6 +108,7 @@ class FusedAdam(torch.optim.Optimizer):
             self._ws = torch.empty((wsb + 7) // 8, dtype=torch.float64, device=dev)
         h = AdamHyper()
         h.beta1, h.beta2 = hyper_g["betas"]
+        h.one_minus_beta1, h.one_minus_beta2 = 1.0 - hyper_g["betas"][0], 1.0 - hyper_g["betas"][1]
         h.eps, h.weight_decay = hyper_g["eps"], hyper_g["weight_decay"]
         h.max_grad_norm = float(self.max_grad_norm) if self.max_grad_norm else 0.0
         check(lib.aimx_fused_adam(arr, len(rows), ctypes.byref(h), self._step_t.data_ptr(), self._lr_t.data_ptr(),

@@ -23,7 +23,7 @@ namespace {
 
 constexpr int kAdamChunk = 48;        // tensors per launch (kernel-argument table)
 constexpr int kAdamThreads = 256;
-constexpr int64_t kSliceElems = 8192; // elements per workgroup slice
+constexpr int64_t kSliceElems = 2048; // elements per workgroup slice (8 per thread, loads unrolled)
 
 struct AdamTable {
   int32_t n;
@@ -48,6 +48,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, 
   const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
   const float* __restrict__ g = t.grad[i];
   double acc = 0.0;
+#pragma unroll 8
   for (int64_t j = s0 + threadIdx.x; j < s1; j += kAdamThreads) {
     const double x = g[j];
     acc += x * x;
@@ -90,8 +91,8 @@ __global__ void k_adam_scalars(const double* __restrict__ partial, int n_partial
 }
 
 __global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t, const float* __restrict__ scal,
-                                                              const float* __restrict__ lr, float beta1, float beta2,
-                                                              float eps, float wd) {
+                                                              const float* __restrict__ lr, float omb1, float beta2,
+                                                              float omb2, float eps, float wd) {
   const int i = find_tensor(t, blockIdx.x);
   const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
   const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
@@ -101,13 +102,14 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t,
   float* __restrict__ g = t.grad[i];
   float* __restrict__ m = t.m[i];
   float* __restrict__ v = t.v[i];
+#pragma unroll 8
   for (int64_t j = s0 + threadIdx.x; j < s1; j += kAdamThreads) {
     float gj = g[j] * coef;
     g[j] = gj;
     const float pj = p[j];
     if (wd != 0.f) gj += wd * pj;
-    const float mj = m[j] + (1.f - beta1) * (gj - m[j]);
-    const float vj = beta2 * v[j] + (1.f - beta2) * gj * gj;
+    const float mj = m[j] + omb1 * (gj - m[j]);       // exp_avg.lerp_(grad, 1 - beta1)
+    const float vj = beta2 * v[j] + omb2 * gj * gj;   // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
     m[j] = mj;
     v[j] = vj;
     p[j] = pj - step_size * (mj / (sqrtf(vj) / bc2s + eps));
@@ -179,8 +181,8 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
                      h->max_grad_norm, h->beta1, h->beta2, step, scal, norm_out);
   AIMX_CHECK_LAUNCH();
   return for_chunks([&](const AdamTable& t, int32_t nb, int64_t) -> int {
-    hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal, lr, h->beta1,
-                       h->beta2, h->eps, h->weight_decay);
+    hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal, lr,
+                       h->one_minus_beta1, h->beta2, h->one_minus_beta2, h->eps, h->weight_decay);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   });

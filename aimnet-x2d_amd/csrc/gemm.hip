@@ -373,6 +373,193 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   }
 }
 
+// ---- Weight-gradient GEMM (K = atoms, small M x N): MFMA fragments straight from L2 ----------
+// dW = dY^T X: A = dY^T is m-contiguous (sam == 1), B = X is n-contiguous (sbn == 1), K is the atom
+// count. In that layout the 16x16x4 MFMA fragments ARE coalesced global rows (lane l reads A[k0 +
+// l/16][m0 + l%16], 16 consecutive floats per k), so each wave loads its own fragments with no
+// LDS staging and no barriers, keeping kWgU k-steps (8 x 4 fragment loads per lane) in flight.
+// A workgroup owns one 32x32 output tile; its 4 waves split the workgroup's K range in 4 and are
+// summed through LDS in wave order; workgroups split K further (split-K slabs + ordered
+// last-arriver reduce, as in k_gemm). Deterministic throughout.
+constexpr int kWgU = 8;
+
+__global__ __launch_bounds__(256) void k_wgrad(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
+  __shared__ __attribute__((aligned(16))) float red[3 * 1024];
+  // the wave index is made provably uniform so the k-dependent buffer offsets stay scalar (SGPR
+  // soffset); otherwise hipcc waterfalls every fragment load
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = (int)a.M, N = (int)a.N;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  const int kb = blockIdx.z * kchunk;
+  const int kend = min((int)a.K, kb + kchunk);
+  const int kw = kchunk / 4;  // multiple of 4
+  const int k0 = min(kend, kb + w * kw), k1 = min(kend, kb + (w + 1) * kw);
+  const __amdgpu_buffer_rsrc_t ra_ = make_rsrc(a.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb_ = make_rsrc(a.B, b_bytes);
+  const uint32_t sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk;
+  const int lm = lane & 15, lk = lane >> 4;
+  uint32_t va[2], vb[2];
+  bool one[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    va[i] = 4u * ((uint32_t)(m0 + i * 16 + lm) + (uint32_t)lk * sak);
+    vb[i] = 4u * ((uint32_t)(n0 + i * 16 + lm) + (uint32_t)lk * sbk);
+    one[i] = a.ones_col && (n0 + i * 16 + lm == N - 1);
+  }
+  floatx4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // k beyond the wave's range: the per-lane offset is moved past the descriptor's extent, so the
+  // (unconditional) load returns 0 — a select on the address, never on the loaded value, keeps
+  // every load of the group in flight (a value select lets hipcc sink loads under a branch)
+  auto load_group = [&](int kg, float (&fa)[kWgU][2], float (&fb)[kWgU][2]) {
+#pragma unroll
+    for (int u = 0; u < kWgU; ++u) {
+      const int kk = kg + 4 * u;
+      const bool kok = kk + lk < k1;
+      const uint32_t sa = __builtin_amdgcn_readfirstlane(4u * (uint32_t)kk * sak);
+      const uint32_t sb = __builtin_amdgcn_readfirstlane(4u * (uint32_t)kk * sbk);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        fa[u][i] = bload(ra_, kok ? va[i] : a_bytes, sa);
+        const float y = bload(rb_, kok ? vb[i] : b_bytes, sb);
+        fb[u][i] = one[i] ? 1.f : y;
+      }
+    }
+  };
+  auto mma_group = [&](const float (&fa)[kWgU][2], const float (&fb)[kWgU][2]) {
+#pragma unroll
+    for (int u = 0; u < kWgU; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[u][i], fb[u][j], acc[i][j], 0, 0, 0);
+  };
+  constexpr int KG = 4 * kWgU;
+  const int ng = k1 > k0 ? (k1 - k0 + KG - 1) / KG : 0;
+  float fa0[kWgU][2], fb0[kWgU][2], fa1[kWgU][2], fb1[kWgU][2];
+  if (ng > 0) load_group(k0, fa0, fb0);
+  for (int g = 0; g < ng; g += 2) {
+    if (g + 1 < ng) load_group(k0 + (g + 1) * KG, fa1, fb1);
+    mma_group(fa0, fb0);
+    if (g + 1 >= ng) break;
+    if (g + 2 < ng) load_group(k0 + (g + 2) * KG, fa0, fb0);
+    mma_group(fa1, fb1);
+  }
+  // intra-workgroup K reduction, wave order 0,1,2,3 (deterministic)
+  if (w > 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<floatx4*>(&red[(w - 1) * 1024 + ((i * 2 + j) * 64 + lane) * 4]) = acc[i][j];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] += *reinterpret_cast<const floatx4*>(&red[q * 1024 + ((i * 2 + j) * 64 + lane) * 4]);
+  }
+  if (gridDim.z > 1) {
+    const int tile = blockIdx.x * gridDim.y + blockIdx.y;
+    const int64_t ntiles = (int64_t)gridDim.x * gridDim.y;
+    floatx4* slab = reinterpret_cast<floatx4*>(a.workspace + ((int64_t)blockIdx.z * ntiles + tile) * 1024);
+    if (w == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) slab[(i * 2 + j) * 64 + lane] = acc[i][j];
+    }
+    if (!a.counters) return;
+    int* flag = reinterpret_cast<int*>(red);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == (int)gridDim.z - 1);
+      if (last) {
+        __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    // ordered slab sum: wave q sums slices q, q+4, ... ; the 4 partial sums are added in wave order
+    const int S = (int)gridDim.z;
+    const floatx4* base = reinterpret_cast<const floatx4*>(a.workspace + (int64_t)tile * 1024);
+    const int64_t zs = ntiles * 256;  // floatx4 per slice
+    floatx4 part[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int off = (i * 2 + j) * 64 + lane;
+        floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int z0 = w; z0 < S; z0 += 16) {
+          floatx4 t[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t[q] = __builtin_nontemporal_load(&base[min(z0 + 4 * q, S - 1) * zs + off]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (z0 + 4 * q < S) sum += t[q];
+        }
+        part[i][j] = sum;
+      }
+    __syncthreads();
+    if (w > 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<floatx4*>(&red[(w - 1) * 1024 + ((i * 2 + j) * 64 + lane) * 4]) = part[i][j];
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = part[i][j];
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            acc[i][j] += *reinterpret_cast<const floatx4*>(&red[q * 1024 + ((i * 2 + j) * 64 + lane) * 4]);
+        }
+    }
+  }
+  // epilogue: wave 0's tile -> LDS (row-major, stride 33) -> all 256 threads, 4 elements each
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(i * 16 + lk * 4 + r) * 33 + j * 16 + lm] = acc[i][j][r];
+  }
+  __syncthreads();
+  int em[4], en[4];
+  float ev[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + u * 256;
+    em[u] = m0 + e / 32;
+    en[u] = n0 + e % 32;
+    ev[u] = red[(e / 32) * 33 + e % 32];
+  }
+  (void)M;
+  epilogue_n<4>(a, em, en, ev);
+}
+
 // Fallback when no counter array is supplied: one thread per output element sums the slabs in
 // slice order. Slab element (m, n) of tile (tm, tn) sits where thread tid's accumulator fragment
 // put it (see the split-K branch of k_gemm).
@@ -399,10 +586,26 @@ __global__ void k_splitk_reduce(const AimxGemmArgs a, int splits, int tiles_n) {
 struct Plan {
   int bm, bn, splits;
   int64_t kchunk;
+  bool wgrad;
 };
+
+// Weight-gradient layout (A m-contiguous, B n-contiguous) with a long K: k_wgrad.
+inline bool is_wgrad(const AimxGemmArgs& a) { return a.sam == 1 && a.sbn == 1 && a.sak != 1 && a.K >= 512; }
 
 Plan plan_gemm(const AimxGemmArgs& a) {
   Plan p;
+  p.wgrad = false;
+  if (is_wgrad(a)) {
+    // ~1536 waves in flight chip-wide, every wave keeping >= 2 load groups (2 x 32 k) of work
+    p.wgrad = true;
+    p.bm = p.bn = 32;
+    const int64_t t = cdiv(a.M, 32) * cdiv(a.N, 32);
+    int64_t splits = a.splits > 0 ? a.splits : cdiv(384, t);
+    splits = std::max<int64_t>(1, std::min<int64_t>({splits, 64, a.K / 256}));
+    p.kchunk = cdiv(cdiv(a.K, splits), 16) * 16;
+    p.splits = (int)std::max<int64_t>(1, cdiv(a.K, p.kchunk));
+    return p;
+  }
   auto tiles = [&](int bm, int bn) { return cdiv(a.M, bm) * cdiv(a.N, bn); };
   // Pick the tile that minimises the busiest CU's MFMA work, ceil(tiles / CUs) * BM * BN (edge
   // tiles count in full: N = 152 runs 5 x 32 columns rather than 3 x 64); ties go to the larger
@@ -478,11 +681,14 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
     p.splits = 1;
     p.kchunk = std::max<int64_t>(cdiv(a.K, kBK) * kBK, kBK);
   }
+  if (p.splits == 1 && p.wgrad) p.kchunk = cdiv(a.K, 16) * 16;
   if (a.K == 0) p.splits = 1, p.kchunk = kBK;
   dim3 grid((unsigned)cdiv(a.M, p.bm), (unsigned)cdiv(a.N, p.bn), (unsigned)p.splits);
   if (p.splits > 1 && a.counters && (int64_t)grid.x * grid.y > a.n_counters) a.counters = nullptr;
   if (p.splits == 1) a.counters = nullptr;
-  if (p.bm == 64 && p.bn == 64)
+  if (p.wgrad && a.K > 0)
+    hipLaunchKernelGGL(k_wgrad, grid, dim3(256), 0, s, a, (int)p.kchunk, a_bytes, b_bytes);
+  else if (p.bm == 64 && p.bn == 64)
     launch_tile<64, 64>(a, p, grid, s, a_bytes, b_bytes);
   else if (p.bm == 64)
     launch_tile<64, 32>(a, p, grid, s, a_bytes, b_bytes);

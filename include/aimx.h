@@ -257,8 +257,10 @@ typedef struct {
   int32_t group;
 } AimxAdamTensor;
 
+/* one_minus_beta1/2 are passed separately because torch forms 1 - beta in double precision
+ * (1 - 0.999f in fp32 is 1.3e-5 relative away from fp32(1 - 0.999)). */
 typedef struct {
-  float beta1, beta2, eps, weight_decay, max_grad_norm;
+  float beta1, beta2, one_minus_beta1, one_minus_beta2, eps, weight_decay, max_grad_norm;
 } AimxAdamHyper;
 
 size_t aimx_fused_adam_workspace_bytes(const AimxAdamTensor* tensors, int32_t n);

@@ -214,11 +214,22 @@ def _gemm(M, N, K, layout, **epi):
 @pytest.mark.parametrize("M,N,K,layout", [
     (9170, 152, 304, "NT"), (9170, 76, 76, "NT"), (1000, 304, 152, "NN"), (153, 613, 2000, "TN"),
     (17, 5, 3, "NT"), (64, 64, 16, "NN"), (307, 307, 10240, "TN"), (100, 2149, 614, "NN"),
-    (1, 513, 512, "TN"), (512, 1, 512, "NT"), (3, 7, 1, "NN")])
+    (1, 513, 512, "TN"), (512, 1, 512, "NT"), (3, 7, 1, "NN"),
+    (76, 78, 9170, "TN"), (33, 65, 701, "TN"), (5, 3, 515, "TN"), (256, 257, 9186, "TN")])
 def test_gemm_layouts(M, N, K, layout):
     C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True)
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-6, err
+
+
+@pytest.mark.parametrize("splits", [1, 3, 64])
+def test_gemm_weight_grad_forced_splits(splits):
+    """The weight-gradient kernel (A m-contiguous, B n-contiguous, long K) at forced split counts,
+    including one workgroup per tile and more splits than a slice can fill."""
+    C, col, _, ref, Am = _gemm(76, 77, 4099, "TN", ones=True, splits=splits)
+    assert (C.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    rs = Am.double().sum(1)
+    assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
 
 
 @pytest.mark.parametrize("fused", [True, False])

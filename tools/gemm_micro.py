@@ -26,7 +26,7 @@ def bench(fn, it=50):
     return s.elapsed_time(e) / it * 1e3
 
 
-def run(M, N, K, layout, label):
+def run(M, N, K, layout, label, splits=0, torch_ref=True):
     A = torch.randn(M, K, device=dev) if layout[0] == "N" else torch.randn(K, M, device=dev)
     B = torch.randn(K, N, device=dev) if layout[1] == "N" else torch.randn(N, K, device=dev)
     C = torch.empty(M, N, device=dev)
@@ -38,6 +38,7 @@ def run(M, N, K, layout, label):
     a.sbk, a.sbn = (N, 1) if layout[1] == "N" else (1, K)
     a.C, a.ldc = C.data_ptr(), N
     a.act, a.dact_kind = -1, -1
+    a.splits = splits
     a.counters, a.n_counters = _lib.counters(dev).data_ptr(), _lib.N_COUNTERS
     wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
     ws = torch.empty(wsb // 4 + 1, device=dev)
@@ -46,11 +47,17 @@ def run(M, N, K, layout, label):
     t_ours = bench(lambda: lib.aimx_gemm(ctypes.byref(a), st))
     Am = A if layout[0] == "N" else A.t()
     Bm = B if layout[1] == "N" else B.t()
-    t_torch = bench(lambda: torch.mm(Am, Bm, out=C))
+    t_torch = bench(lambda: torch.mm(Am, Bm, out=C)) if torch_ref else float("nan")
     fl = 2 * M * N * K
     print(f"{label:28s} M={M:6d} N={N:5d} K={K:6d} {layout}: ours {t_ours:7.1f} us ({fl / t_ours / 1e6:6.1f} TF/s)"
           f"  torch {t_torch:7.1f} us ({fl / t_torch / 1e6:6.1f} TF/s)")
 
+
+if len(sys.argv) > 1 and sys.argv[1] == "splits":
+    for M, N, K, lab in [(76, 77, 9170, "c2 dW mlp"), (152, 305, 9170, "c2 dW_ig"), (256, 257, 9170, "c2 concat dW")]:
+        for sp in (0, 4, 8, 12, 16, 24, 32, 48, 64):
+            run(M, N, K, "TN", f"{lab} splits={sp}", splits=sp, torch_ref=False)
+    sys.exit(0)
 
 for args in [(9170, 152, 304, "NT", "c2 fwd [u|g]"), (9170, 76, 76, "NT", "c2 fwd mlp"),
              (9170, 304, 152, "NN", "c2 bwd dF"), (9170, 76, 76, "NN", "c2 bwd dx mlp"),
