@@ -69,7 +69,7 @@ class ShellStackGrad(ctypes.Structure):
         ("d_out", c_ptr), ("d_out_ld", c_i64),
         ("d_x_in", c_ptr), ("d_x_in_ld", c_i64),
         ("d_w_ig", c_ptr), ("d_b_ig", c_ptr), ("d_w1", c_ptr), ("d_b1", c_ptr), ("d_w2", c_ptr), ("d_b2", c_ptr),
-        ("dF", c_ptr), ("dUG", c_ptr), ("dT0", c_ptr), ("dT1", c_ptr), ("dT2", c_ptr), ("dT3", c_ptr),
+        ("workspace", c_ptr), ("workspace_bytes", c_size),
     ]
 
 
@@ -78,6 +78,11 @@ class EmbeddingTables(ctypes.Structure):
         ("n_tables", c_i32), ("dim", c_i64),
         ("table", c_ptr * 8), ("index", c_ptr * 8), ("rows", c_i64 * 8), ("grad", c_ptr * 8),
     ]
+
+
+class WgradProblem(ctypes.Structure):
+    _fields_ = [("dY", c_ptr), ("ld_dy", c_i64), ("X", c_ptr), ("ld_x", c_i64), ("dW", c_ptr), ("ld_dw", c_i64),
+                ("col_out", c_ptr), ("M", c_i64), ("N", c_i64), ("K", c_i64)]
 
 
 class AdamTensor(ctypes.Structure):
@@ -102,6 +107,7 @@ _SIGS = {
     "aimx_shell_stack_workspace_bytes": (c_size, [ctypes.POINTER(ShellStack)]),
     "aimx_shell_stack_forward": (c_i32, [ctypes.POINTER(ShellStack), c_ptr]),
     "aimx_shell_stack_backward": (c_i32, [ctypes.POINTER(ShellStack), ctypes.POINTER(ShellStackGrad), c_ptr]),
+    "aimx_shell_stack_backward_workspace_bytes": (c_size, [ctypes.POINTER(ShellStack)]),
     "aimx_partial_charge_forward": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                                             c_ptr]),
     "aimx_partial_charge_backward": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
@@ -119,6 +125,8 @@ _SIGS = {
     "aimx_embedding_backward_workspace_bytes": (c_size, [ctypes.POINTER(EmbeddingTables), c_i64]),
     "aimx_embedding_backward": (c_i32, [ctypes.POINTER(EmbeddingTables), c_i64, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "aimx_act_backward": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_wgrad_grouped_workspace_bytes": (c_size, [ctypes.POINTER(WgradProblem), c_i32]),
+    "aimx_wgrad_grouped": (c_i32, [ctypes.POINTER(WgradProblem), c_i32, c_ptr, c_size, c_ptr, c_i64, c_ptr]),
     "aimx_fused_adam_workspace_bytes": (c_size, [ctypes.POINTER(AdamTensor), c_i32]),
     "aimx_fused_adam": (c_i32, [ctypes.POINTER(AdamTensor), c_i32, ctypes.POINTER(AdamHyper), c_ptr, c_ptr, c_ptr,
                                 c_ptr, c_size, c_ptr]),

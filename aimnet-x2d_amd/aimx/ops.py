@@ -132,11 +132,7 @@ class _MPStack(torch.autograd.Function):
         n, d, h, nl, nm = spec["N"], spec["D"], spec["num_hops"], spec["num_layers"], spec["num_mlp"]
         k = d * (h + 1)
         d_out, d_ld = _rows(d_out)
-        ar = Arena(dev)
-        i_dF, i_dUG = ar.add(n, k), ar.add(n, 2 * d)
-        i_T = [ar.add(n, d) for _ in range(4)]
-        buf, v = ar.alloc()
-        # gradients handed to autograd are standalone allocations, never views of the arena
+        # gradients handed to autograd are standalone allocations; the scratch is one buffer
         new = lambda *shape: torch.empty(*shape, dtype=_F32, device=dev)  # noqa: E731
         dx_t = new(n, d)
         dw_ig = [new(2 * d, k) for _ in range(nl)]
@@ -167,8 +163,9 @@ class _MPStack(torch.autograd.Function):
         g.d_x_in, g.d_x_in_ld = ptr(dx_t), d
         gkeep = [ptr_array(x) for x in (dw_ig, db_ig, dw1, db1, dw2, db2)]
         g.d_w_ig, g.d_b_ig, g.d_w1, g.d_b1, g.d_w2, g.d_b2 = [_ct_addr(a) for a in gkeep]
-        g.dF, g.dUG = ptr(v[i_dF]), ptr(v[i_dUG])
-        g.dT0, g.dT1, g.dT2, g.dT3 = [ptr(v[i]) for i in i_T]
+        gwsb = lib.aimx_shell_stack_backward_workspace_bytes(s)
+        buf = torch.empty(max(gwsb // 4, 1), dtype=_F32, device=dev)
+        g.workspace, g.workspace_bytes = ptr(buf), buf.numel() * 4
         check(lib.aimx_shell_stack_backward(s, g, stream_ptr(dev)), "shell_stack_backward")
         grads = []
         for l in range(nl):

@@ -24,6 +24,7 @@
 // hash-dropout with mask store, mask/act' multiplication for the backward, and an implicit ones
 // column that turns a weight-gradient GEMM's last column into the bias gradient.
 #include <algorithm>
+#include <cstdlib>
 
 #include "aimx_common.h"
 
@@ -140,7 +141,16 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
 // AK: A is k-contiguous (sak == 1) -> row-major LDS image (row stride BK+2: bank = 2*row + k,
 // conflict-free for the 16x16x4 fragment reads); else A is m-contiguous (sam == 1) -> k-major
 // image (stride BM+16). BKC: the same for B with n in place of m.
-template <int BM, int BN, bool AK, bool BKC>
+__device__ __forceinline__ floatx4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// V4: both operands staged with 16-byte buffer loads (one dwordx4 moves 1 KiB per wave; dword
+// loads are address-rate bound at a quarter of that). Requires the contiguous extent of each
+// operand to be a multiple of 4 floats and 16-byte aligned rows (checked by the host), so a float4
+// is wholly valid or wholly outside: invalid ones are pointed past the descriptor's extent and
+// read as zeros (an address select — no value select for hipcc to turn into a branch).
+template <int BM, int BN, bool AK, bool BKC, bool V4>
 __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
   constexpr int BK = kBK;
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -182,7 +192,40 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  constexpr int NA4 = V4 ? BM * BK / 1024 : 1, NB4 = V4 ? BN * BK / 1024 : 1;
   auto load_slice = [&](int k0, bool tail, float (&ra)[NA], float (&rb)[NB]) {
+    if constexpr (V4) {
+#pragma unroll
+      for (int i = 0; i < NA4; ++i) {
+        const int q = tid + i * 256;
+        const int mm = AK ? q / (BK / 4) : (q % (BM / 4)) * 4;
+        const int kk = AK ? (q % (BK / 4)) * 4 : q / (BM / 4);
+        const bool ok = (k0 + kk < kend) && (AK || m0 + mm < M);
+        const uint32_t off = AK ? 4u * ((uint32_t)(m0 + mm) * sam + (uint32_t)(k0 + kk))
+                                : 4u * ((uint32_t)(m0 + mm) + (uint32_t)(k0 + kk) * sak);
+        const floatx4 v = bload4(ra_, ok ? off : a_bytes, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ra[4 * i + e] = v[e];
+      }
+#pragma unroll
+      for (int i = 0; i < NB4; ++i) {
+        const int q = tid + i * 256;
+        const int nn = BKC ? q / (BK / 4) : (q % (BN / 4)) * 4;
+        const int kk = BKC ? (q % (BK / 4)) * 4 : q / (BN / 4);
+        const bool kok = k0 + kk < kend;
+        const bool ok = kok && (n0 + nn < Nreal);
+        const uint32_t off = BKC ? 4u * ((uint32_t)(n0 + nn) * sbn + (uint32_t)(k0 + kk))
+                                 : 4u * ((uint32_t)(n0 + nn) + (uint32_t)(k0 + kk) * sbk);
+        const floatx4 v = bload4(rb_, ok ? off : b_bytes, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool one = a.ones_col && kok && ((BKC ? n0 + nn : n0 + nn + e) == N - 1);
+          rb[4 * i + e] = one ? 1.f : v[e];
+        }
+      }
+      return;
+    }
+    (void)tail;
     // A
     if (AK) {
       const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) * sam + (uint32_t)(k0 + a_k));
@@ -225,6 +268,35 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   auto store_slice = [&](const float (&ra)[NA], const float (&rb)[NB], int stage) {
     float* As = smem + stage * (LA + LB);
     float* Bs = As + LA;
+    if constexpr (V4) {
+#pragma unroll
+      for (int i = 0; i < NA4; ++i) {
+        const int q = tid + i * 256;
+        const int mm = AK ? q / (BK / 4) : (q % (BM / 4)) * 4;
+        const int kk = AK ? (q % (BK / 4)) * 4 : q / (BM / 4);
+        if (AK) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) As[mm * SA + kk + e] = ra[4 * i + e];
+        } else {
+          *reinterpret_cast<floatx4*>(&As[kk * SA + mm]) =
+              floatx4{ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NB4; ++i) {
+        const int q = tid + i * 256;
+        const int nn = BKC ? q / (BK / 4) : (q % (BN / 4)) * 4;
+        const int kk = BKC ? (q % (BK / 4)) * 4 : q / (BN / 4);
+        if (BKC) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) Bs[nn * SB + kk + e] = rb[4 * i + e];
+        } else {
+          *reinterpret_cast<floatx4*>(&Bs[kk * SB + nn]) =
+              floatx4{rb[4 * i], rb[4 * i + 1], rb[4 * i + 2], rb[4 * i + 3]};
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int mm = AK ? a_m + i * A_STEP : a_m;
@@ -383,14 +455,17 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
 // last-arriver reduce, as in k_gemm). Deterministic throughout.
 constexpr int kWgU = 8;
 
-__global__ __launch_bounds__(256) void k_wgrad(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
-  __shared__ __attribute__((aligned(16))) float red[3 * 1024];
+// One 32x32 output tile, K slice bz of S (of width kchunk): the body shared by the single-problem
+// kernel and the grouped one. Slabs of this problem live at ws + (z * ntiles + tile) * 1024.
+__device__ __forceinline__ void wgrad_block(const AimxGemmArgs& a, int kchunk, uint32_t a_bytes, uint32_t b_bytes,
+                                            int bx, int by, int bz, int S, int tile, int ntiles, float* ws,
+                                            int32_t* counters, float* red) {
   // the wave index is made provably uniform so the k-dependent buffer offsets stay scalar (SGPR
   // soffset); otherwise hipcc waterfalls every fragment load
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = (int)a.M, N = (int)a.N;
-  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
-  const int kb = blockIdx.z * kchunk;
+  const int m0 = bx * 32, n0 = by * 32;
+  const int kb = bz * kchunk;
   const int kend = min((int)a.K, kb + kchunk);
   const int kw = kchunk / 4;  // multiple of 4
   const int k0 = min(kend, kb + w * kw), k1 = min(kend, kb + (w + 1) * kw);
@@ -466,27 +541,25 @@ __global__ __launch_bounds__(256) void k_wgrad(const AimxGemmArgs a, int kchunk,
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] += *reinterpret_cast<const floatx4*>(&red[q * 1024 + ((i * 2 + j) * 64 + lane) * 4]);
   }
-  if (gridDim.z > 1) {
-    const int tile = blockIdx.x * gridDim.y + blockIdx.y;
-    const int64_t ntiles = (int64_t)gridDim.x * gridDim.y;
-    floatx4* slab = reinterpret_cast<floatx4*>(a.workspace + ((int64_t)blockIdx.z * ntiles + tile) * 1024);
+  if (S > 1) {
+    floatx4* slab = reinterpret_cast<floatx4*>(ws + ((int64_t)bz * ntiles + tile) * 1024);
     if (w == 0) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) slab[(i * 2 + j) * 64 + lane] = acc[i][j];
     }
-    if (!a.counters) return;
+    if (!counters) return;
     int* flag = reinterpret_cast<int*>(red);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == (int)gridDim.z - 1);
+      const int old = __hip_atomic_fetch_add(&counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == S - 1);
       if (last) {
-        __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+        __hip_atomic_store(&counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -495,8 +568,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const AimxGemmArgs a, int kchunk,
     __syncthreads();
     if (!flag[0]) return;
     // ordered slab sum: wave q sums slices q, q+4, ... ; the 4 partial sums are added in wave order
-    const int S = (int)gridDim.z;
-    const floatx4* base = reinterpret_cast<const floatx4*>(a.workspace + (int64_t)tile * 1024);
+    const floatx4* base = reinterpret_cast<const floatx4*>(ws + (int64_t)tile * 1024);
     const int64_t zs = ntiles * 256;  // floatx4 per slice
     floatx4 part[2][2];
 #pragma unroll
@@ -560,6 +632,53 @@ __global__ __launch_bounds__(256) void k_wgrad(const AimxGemmArgs a, int kchunk,
   epilogue_n<4>(a, em, en, ev);
 }
 
+__global__ __launch_bounds__(256) void k_wgrad(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
+  __shared__ __attribute__((aligned(16))) float red[3 * 1024];
+  wgrad_block(a, kchunk, a_bytes, b_bytes, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z,
+              blockIdx.x * gridDim.y + blockIdx.y, gridDim.x * gridDim.y, a.workspace, a.counters, red);
+}
+
+// Grouped weight gradients: up to kWgMaxProb independent dW = dY^T X problems in one launch (the
+// whole message-passing stack's weight gradients, deferred to the end of its backward), so the
+// per-launch latency of ~15 small long-K GEMMs is paid once and their workgroups fill the chip.
+constexpr int kWgMaxProb = 16;
+struct WgradTable {
+  int32_t n;
+  int32_t blk0[kWgMaxProb + 1];  // first workgroup of each problem
+  int32_t tiles_y[kWgMaxProb], ntiles[kWgMaxProb], splits[kWgMaxProb], kchunk[kWgMaxProb];
+  uint32_t a_bytes[kWgMaxProb], b_bytes[kWgMaxProb];
+  int64_t ws_off[kWgMaxProb], cnt_off[kWgMaxProb];
+  AimxWgradProblem p[kWgMaxProb];
+};
+
+__global__ __launch_bounds__(256) void k_wgrad_grouped(const WgradTable t, float* ws, int32_t* counters) {
+  __shared__ __attribute__((aligned(16))) float red[3 * 1024];
+  int q = 0;
+  while (q + 1 < t.n && t.blk0[q + 1] <= (int)blockIdx.x) ++q;
+  const int local = blockIdx.x - t.blk0[q];
+  const int nt = t.ntiles[q];
+  const int z = local / nt, tile = local - z * nt;
+  const AimxWgradProblem& pr = t.p[q];
+  AimxGemmArgs a = {};
+  a.M = pr.M;
+  a.N = pr.col_out ? pr.N + 1 : pr.N;
+  a.K = pr.K;
+  a.A = pr.dY;
+  a.sam = 1;
+  a.sak = pr.ld_dy;
+  a.B = pr.X;
+  a.sbk = pr.ld_x;
+  a.sbn = 1;
+  a.C = pr.dW;
+  a.ldc = pr.ld_dw;
+  a.act = -1;
+  a.dact_kind = -1;
+  a.ones_col = pr.col_out ? 1 : 0;
+  a.col_out = pr.col_out;
+  wgrad_block(a, t.kchunk[q], t.a_bytes[q], t.b_bytes[q], tile / t.tiles_y[q], tile % t.tiles_y[q], z, t.splits[q],
+              tile, nt, ws + t.ws_off[q], counters ? counters + t.cnt_off[q] : nullptr, red);
+}
+
 // Fallback when no counter array is supplied: one thread per output element sums the slabs in
 // slice order. Slab element (m, n) of tile (tm, tn) sits where thread tid's accumulator fragment
 // put it (see the split-K branch of k_gemm).
@@ -590,7 +709,10 @@ struct Plan {
 };
 
 // Weight-gradient layout (A m-contiguous, B n-contiguous) with a long K: k_wgrad.
-inline bool is_wgrad(const AimxGemmArgs& a) { return a.sam == 1 && a.sbn == 1 && a.sak != 1 && a.K >= 512; }
+inline bool is_wgrad(const AimxGemmArgs& a) {
+  static const bool off = getenv("AIMX_GEMM_NO_WGRAD") != nullptr;  // A/B experiments only
+  return !off && a.sam == 1 && a.sbn == 1 && a.sak != 1 && a.K >= 512;
+}
 
 Plan plan_gemm(const AimxGemmArgs& a) {
   Plan p;
@@ -636,18 +758,38 @@ Plan plan_gemm(const AimxGemmArgs& a) {
   return p;
 }
 
-template <int BM, int BN>
-void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
+// 16-byte staging is legal when each operand's contiguous extent is a multiple of 4 floats and
+// every row starts 16-byte aligned.
+bool v4_ok(const AimxGemmArgs& a) {
+  const bool ak = (a.sak == 1), bk = (a.sbk == 1);
+  const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al(a.A) || !al(a.B) || a.K % 4) return false;
+  if (ak ? (a.sam % 4) : (a.sak % 4 || a.M % 4)) return false;
+  if (bk ? (a.sbn % 4) : (a.sbk % 4 || Nreal % 4)) return false;
+  return true;
+}
+
+template <int BM, int BN, bool V4>
+void launch_tile_v(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
   const bool ak = (a.sak == 1), bk = (a.sbk == 1);
   const int kc = (int)p.kchunk;
   if (ak && bk)
-    hipLaunchKernelGGL((k_gemm<BM, BN, true, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, true, true, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
   else if (ak)
-    hipLaunchKernelGGL((k_gemm<BM, BN, true, false>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, true, false, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
   else if (bk)
-    hipLaunchKernelGGL((k_gemm<BM, BN, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, false, true, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
   else
-    hipLaunchKernelGGL((k_gemm<BM, BN, false, false>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, false, false, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
+}
+
+template <int BM, int BN>
+void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
+  if (v4_ok(a))
+    launch_tile_v<BM, BN, true>(a, p, grid, s, ab, bb);
+  else
+    launch_tile_v<BM, BN, false>(a, p, grid, s, ab, bb);
 }
 
 }  // namespace
@@ -710,6 +852,85 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
 }
 
 }  // namespace aimx
+
+namespace aimx {
+namespace {
+struct WgPlan {
+  int tiles_x, tiles_y, splits, kchunk;
+};
+WgPlan wg_plan(const AimxWgradProblem& p) {
+  WgPlan w;
+  w.tiles_x = (int)cdiv(p.M, 32);
+  w.tiles_y = (int)cdiv(p.col_out ? p.N + 1 : p.N, 32);
+  // ~1k atoms of K per workgroup: enough MFMA work per wave to amortise the fragment pipeline
+  int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / 1024));
+  w.kchunk = (int)(cdiv(cdiv(std::max<int64_t>(p.K, 1), sp), 16) * 16);
+  w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
+  return w;
+}
+bool wg_valid(const AimxWgradProblem& p) {
+  if (p.M < 1 || p.N < 1 || p.K < 0 || !p.dY || !p.X || !p.dW) return false;
+  if (p.ld_dy < p.M || p.ld_x < p.N || p.ld_dw < p.N) return false;
+  const int64_t a_ext = 4 * ((p.K - 1) * p.ld_dy + p.M), b_ext = 4 * ((p.K - 1) * p.ld_x + p.N);
+  return p.K == 0 || (a_ext < (1ll << 31) && b_ext < (1ll << 31));
+}
+}  // namespace
+}  // namespace aimx
+
+extern "C" size_t aimx_wgrad_grouped_workspace_bytes(const AimxWgradProblem* p, int32_t n) {
+  if (!p || n < 0) return 0;
+  size_t f = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const aimx::WgPlan w = aimx::wg_plan(p[i]);
+    if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * 1024;
+  }
+  return sizeof(float) * f;
+}
+
+extern "C" int aimx_wgrad_grouped(const AimxWgradProblem* p, int32_t n, void* workspace, size_t workspace_bytes,
+                                  int32_t* counters, int64_t n_counters, aimx_stream_t stream) {
+  using namespace aimx;
+  if (!p || n < 0) return AIMX_EARG;
+  for (int32_t i = 0; i < n; ++i)
+    if (!wg_valid(p[i])) return AIMX_EARG;
+  if (workspace_bytes < aimx_wgrad_grouped_workspace_bytes(p, n) || (workspace_bytes && !workspace)) return AIMX_EARG;
+  int64_t ctiles = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const WgPlan w = wg_plan(p[i]);
+    ctiles += (int64_t)w.tiles_x * w.tiles_y;
+  }
+  if (!counters || ctiles > n_counters) return AIMX_EARG;
+  int64_t ws_off = 0, cnt_off = 0;
+  for (int32_t c0 = 0; c0 < n; c0 += kWgMaxProb) {
+    WgradTable t{};
+    t.n = std::min<int32_t>(kWgMaxProb, n - c0);
+    int32_t blk = 0;
+    for (int32_t k = 0; k < t.n; ++k) {
+      const AimxWgradProblem& pr = p[c0 + k];
+      const WgPlan w = wg_plan(pr);
+      t.p[k] = pr;
+      t.blk0[k] = blk;
+      t.tiles_y[k] = w.tiles_y;
+      t.ntiles[k] = w.tiles_x * w.tiles_y;
+      t.splits[k] = w.splits;
+      t.kchunk[k] = w.kchunk;
+      t.a_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * ((std::max<int64_t>(pr.K, 1) - 1) * pr.ld_dy + pr.M));
+      t.b_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * ((std::max<int64_t>(pr.K, 1) - 1) * pr.ld_x + pr.N));
+      t.ws_off[k] = ws_off;
+      t.cnt_off[k] = cnt_off;
+      if (w.splits > 1) ws_off += (int64_t)w.splits * t.ntiles[k] * 1024;
+      cnt_off += t.ntiles[k];
+      blk += w.splits * t.ntiles[k];
+    }
+    t.blk0[t.n] = blk;
+    if (blk > 0) {
+      hipLaunchKernelGGL(k_wgrad_grouped, dim3((unsigned)blk), dim3(256), 0, (hipStream_t)stream, t, (float*)workspace,
+                         counters);
+      AIMX_CHECK_LAUNCH();
+    }
+  }
+  return AIMX_OK;
+}
 
 extern "C" size_t aimx_gemm_workspace_bytes(const AimxGemmArgs* a) {
   return a ? sizeof(float) * aimx::gemm_workspace_floats(*a) : 0;

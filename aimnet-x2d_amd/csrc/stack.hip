@@ -5,12 +5,14 @@
 // (layers.py:82-106) as five fused MFMA GEMMs whose epilogues carry bias, activation, dropout,
 // the per-block residual, the global skip and the outer residual (gnn.py:302-306). The next
 // layer's input is written by the last GEMM directly into chunk 0 of the next layer's F.
-// The backward replays the same structure in reverse with fused act'/dropout epilogues, the
-// weight/bias gradients as split-K GEMMs with an implicit ones column, and the hop backward as
-// the same segmented gather-sum over the src-keyed CSR with the two residual terms fused.
+// The backward replays the same structure in reverse with fused act'/dropout epilogues and the
+// hop backward as the same segmented gather-sum over the src-keyed CSR with the two residual
+// terms fused; the activation gradients every weight gradient needs are kept, and all weight and
+// bias gradients of the stack run at the end as ONE grouped launch (aimx_wgrad_grouped).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "aimx_common.h"
 
@@ -244,40 +246,103 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
   return AIMX_OK;
 }
 
+namespace aimx {
+namespace {
+
+// Backward scratch layout (floats, 64-aligned regions); every gradient a weight gradient needs
+// stays live until the grouped launch at the end.
+struct BwdLayout {
+  int64_t dF, dUG, dV, dA, dY, T0, wg, total;  // offsets (floats); wg: grouped-wgrad workspace
+  int64_t nA, nY;
+};
+
+int64_t al64(int64_t x) { return (x + 63) / 64 * 64; }
+
+// one AimxWgradProblem per weight gradient of the stack, in launch order
+int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, const float* base, const BwdLayout* L_,
+                         AimxWgradProblem* out) {
+  const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
+  const int64_t K = D * (h + 1), D2 = 2 * D;
+  int n = 0;
+  for (int64_t l = L - 1; l >= 0; --l) {
+    const float* dYl = nullptr;
+    int64_t ldy = D;
+    if (base) {
+      dYl = (l == L - 1) ? g->d_out : base + L_->dY + (l * N * D);
+      ldy = (l == L - 1) ? g->d_out_ld : D;
+    }
+    for (int64_t k = nm - 1; k >= 0; --k) {
+      const int64_t idx = l * nm + k;
+      const float* da = (k == nm - 1) ? dYl : (base ? base + L_->dA + (l * (nm - 1) + k) * N * D : nullptr);
+      const int64_t lda = (k == nm - 1) ? ldy : D;
+      AimxWgradProblem w2 = {da, lda, base ? s->R[idx] : nullptr, D, g ? g->d_w2[idx] : nullptr, D,
+                             g ? g->d_b2[idx] : nullptr, D, D, N};
+      const float* in = base ? ((k == 0) ? s->UG[l] : s->A[idx - 1]) : nullptr;
+      AimxWgradProblem w1 = {base ? base + L_->dV + idx * N * D : nullptr, D, in, (k == 0) ? D2 : D,
+                             g ? g->d_w1[idx] : nullptr, D, g ? g->d_b1[idx] : nullptr, D, D, N};
+      out[n++] = w2;
+      out[n++] = w1;
+    }
+    AimxWgradProblem wig = {base ? base + L_->dUG + l * N * D2 : nullptr, D2, base ? s->F[l] : nullptr, K,
+                            g ? g->d_w_ig[l] : nullptr, K, g ? g->d_b_ig[l] : nullptr, D2, K, N};
+    out[n++] = wig;
+  }
+  return n;
+}
+
+BwdLayout bwd_layout(const AimxShellStack* s) {
+  const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
+  const int64_t K = D * (h + 1);
+  BwdLayout b;
+  b.nA = L * (nm - 1);
+  b.nY = std::max<int64_t>(L - 1, 0);
+  int64_t o = 0;
+  b.dF = o, o += al64(N * K);
+  b.dUG = o, o += al64(L * N * 2 * D);
+  b.dV = o, o += al64(L * nm * N * D);
+  b.dA = o, o += al64(std::max<int64_t>(b.nA, 1) * N * D);
+  b.dY = o, o += al64(std::max<int64_t>(b.nY, 1) * N * D);
+  b.T0 = o, o += al64(N * D);
+  b.wg = o;
+  // problem shapes only (null pointers, non-null col_out flags) for the grouped workspace size
+  std::vector<AimxWgradProblem> pr(L * (2 * nm + 1));
+  const int n = stack_wgrad_problems(s, nullptr, nullptr, &b, pr.data());
+  for (int i = 0; i < n; ++i) pr[i].col_out = reinterpret_cast<float*>(16);
+  o += al64((int64_t)(aimx_wgrad_grouped_workspace_bytes(pr.data(), n) / sizeof(float)));
+  b.total = o;
+  return b;
+}
+
+}  // namespace
+}  // namespace aimx
+
+extern "C" size_t aimx_shell_stack_backward_workspace_bytes(const AimxShellStack* s) {
+  if (!valid(s)) return 0;
+  return sizeof(float) * (size_t)bwd_layout(s).total + 256;
+}
+
 extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShellStackGrad* g, aimx_stream_t stream_) {
   hipStream_t st = (hipStream_t)stream_;
-  // debug aid: AIMX_DEBUG_BWD_OPS=n enqueues only the first n operations of the backward
-  const char* dbg = getenv("AIMX_DEBUG_BWD_OPS");
-  int budget = dbg ? atoi(dbg) : -1;
-#define BUDGET()                           \
-  do {                                     \
-    if (budget == 0) return AIMX_OK;       \
-    if (budget > 0) --budget;              \
-  } while (0)
   if (!valid(s) || !g) return AIMX_EARG;
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
   if (N == 0) return AIMX_OK;
+  const BwdLayout lay = bwd_layout(s);
+  if (!g->workspace || g->workspace_bytes < sizeof(float) * (size_t)lay.total) return AIMX_EARG;
+  float* base = (float*)g->workspace;
+  float* dF = base + lay.dF;
   const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters};
   const bool drop = s->training && s->drop_p > 0.f;
-  float* T[3] = {g->dT1, g->dT2, g->dT3};
-  float* dV = g->dT0;
-  const float* dY = g->d_out;
-  int64_t ldy = g->d_out_ld;
-  int y_slot = -1;  // which T holds dY (-1: caller's d_out)
   for (int64_t l = L - 1; l >= 0; --l) {
-    const float* F = s->F[l];
-    int free_slots[3], nf = 0;
-    for (int i = 0; i < 3; ++i)
-      if (i != y_slot) free_slots[nf++] = i;
-    // MLP blocks, last to first. da_out of the last block is dY.
-    const float* da_out = dY;
-    int64_t ld_out = ldy;
-    int ping = 0;
+    float* dUG = base + lay.dUG + l * N * D2;
+    const float* dY = (l == L - 1) ? g->d_out : base + lay.dY + l * N * D;
+    const int64_t ldy = (l == L - 1) ? g->d_out_ld : D;
+    // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
     for (int64_t k = nm - 1; k >= 0; --k) {
       const int64_t idx = l * nm + k;
-      const float* in = (k == 0) ? s->UG[l] : s->A[idx - 1];
-      const int64_t ldin = (k == 0) ? D2 : D;
+      const float* da_out = (k == nm - 1) ? dY : base + lay.dA + (l * (nm - 1) + k) * N * D;
+      const int64_t ld_out = (k == nm - 1) ? ldy : D;
+      float* dV = base + lay.dV + idx * N * D;
       {  // dV = (da_out W2) * mask/(1-p) * act'(V)
         AimxGemmArgs a = linear_dx(N, D, D, da_out, ld_out, s->w2[idx], dV, D);
         if (drop) {
@@ -288,25 +353,11 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
         a.dact_pre = s->V[idx];
         a.lddact = D;
         a.dact_kind = s->act;
-        BUDGET();
         RUN(run(a, ws, st));
       }
-      BUDGET();
-      BUDGET();
-    RUN(run(linear_dw(N, D, D, da_out, ld_out, s->R[idx], D, g->d_w2[idx], g->d_b2[idx]), ws, st));
-      BUDGET();
-      BUDGET();
-    RUN(run(linear_dw(N, D, D, dV, D, in, ldin, g->d_w1[idx], g->d_b1[idx]), ws, st));
       {  // da_in = da_out + dV W1 ; for k == 0 also * act'(u) -> du into dUG[:, :D]
-        float* dst;
-        int64_t ldd;
-        if (k == 0) {
-          dst = g->dUG;
-          ldd = D2;
-        } else {
-          dst = T[free_slots[ping]];
-          ldd = D;
-        }
+        float* dst = (k == 0) ? dUG : base + lay.dA + (l * (nm - 1) + k - 1) * N * D;
+        const int64_t ldd = (k == 0) ? D2 : D;
         AimxGemmArgs a = linear_dx(N, D, D, dV, D, s->w1[idx], dst, ldd);
         a.res[0] = da_out;
         a.ldres[0] = ld_out;
@@ -315,53 +366,29 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
           a.lddact = D;
           a.dact_kind = s->act;
         }
-        BUDGET();
         RUN(run(a, ws, st));
-        if (k != 0) {
-          da_out = dst;
-          ld_out = D;
-          ping ^= 1;
-        }
       }
     }
     // dg = dY -> dUG[:, D:]
-    BUDGET();
-    RUN(copy2d(dY, ldy, g->dUG + D, D2, N, D, st));
-    BUDGET();
-    RUN(run(linear_dw(N, K, D2, g->dUG, D2, F, K, g->d_w_ig[l], g->d_b_ig[l]), ws, st));
-    BUDGET();
-    RUN(run(linear_dx(N, K, D2, g->dUG, D2, s->w_ig[l], g->dF, K), ws, st));
+    RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
+    RUN(run(linear_dx(N, K, D2, dUG, D2, s->w_ig[l], dF, K), ws, st));
     // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]
     const bool first = (l == 0);
-    float* dst;
-    int64_t ldd;
-    if (s->use_pc) {
-      dst = T[free_slots[0]];
-      ldd = D;
-    } else if (first) {
-      dst = g->d_x_in;
-      ldd = g->d_x_in_ld;
-    } else {
-      dst = T[free_slots[1]];
-      ldd = D;
-    }
-    BUDGET();
-    RUN(gather(g->dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, g->dF, K,
+    float* nxt = first ? g->d_x_in : base + lay.dY + (l - 1) * N * D;
+    const int64_t ldn = first ? g->d_x_in_ld : D;
+    float* dst = s->use_pc ? base + lay.T0 : nxt;
+    const int64_t ldd = s->use_pc ? D : ldn;
+    RUN(gather(dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, dF, K,
                s->mode_single ? nullptr : dY, ldy, st));
-    int new_slot = s->use_pc ? -1 : (first ? -1 : free_slots[1]);
     if (s->use_pc) {
       const float* raw = first ? s->x_in : s->X[l];
       const int64_t ldr = first ? s->x_in_ld : D;
-      float* pdst = first ? g->d_x_in : T[free_slots[1]];
-      const int64_t pld = first ? g->d_x_in_ld : D;
-      RUN(launch_charge_bwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, dst, D, pdst, pld, st));
-      new_slot = first ? -1 : free_slots[1];
-    }
-    if (!first) {
-      y_slot = new_slot;
-      dY = T[y_slot];
-      ldy = D;
+      RUN(launch_charge_bwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, dst, D, nxt, ldn, st));
     }
   }
-  return AIMX_OK;
+  // every weight and bias gradient of the stack in one grouped launch
+  std::vector<AimxWgradProblem> pr(L * (2 * nm + 1));
+  const int n = stack_wgrad_problems(s, g, base, &lay, pr.data());
+  return aimx_wgrad_grouped(pr.data(), n, base + lay.wg, sizeof(float) * (size_t)(lay.total - lay.wg), s->counters,
+                            s->n_counters, stream_);
 }

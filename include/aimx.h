@@ -152,11 +152,14 @@ typedef struct AimxShellStackGrad {
   float* d_x_in; int64_t d_x_in_ld;      /* grad w.r.t. x_in (written) */
   float* const* d_w_ig; float* const* d_b_ig;   /* per layer [2D,K], [2D] (written) */
   float* const* d_w1; float* const* d_b1; float* const* d_w2; float* const* d_b2;
-  /* scratch, caller-owned: dF [N,K], dUG [N,2D], dA, dV [N,D] x2, dX [N,D] x2 */
-  float* dF; float* dUG; float* dT0; float* dT1; float* dT2; float* dT3;
+  /* scratch, caller-owned, aimx_shell_stack_backward_workspace_bytes(s) bytes: the per-layer /
+   * per-block activation gradients are kept until the weight gradients of the whole stack run
+   * as ONE grouped launch at the end (aimx_wgrad_grouped) */
+  void* workspace; size_t workspace_bytes;
 } AimxShellStackGrad;
 
 size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s);
+size_t aimx_shell_stack_backward_workspace_bytes(const AimxShellStack* s);
 int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t stream);
 int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShellStackGrad* g,
                               aimx_stream_t stream);
@@ -234,6 +237,29 @@ int aimx_embedding_backward(const AimxEmbeddingTables* t, int64_t N, const float
 /* out[m,n] = dy[m,n] * act'(pre[m,n]) */
 int aimx_act_backward(int32_t kind, const float* dy, int64_t ldy, const float* pre, int64_t ldp,
                       int64_t M, int64_t N, float* out, int64_t ldo, aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Grouped weight gradients: for each problem, dW[M, N] = dY^T X over K rows (atoms) and, when
+ * col_out is non-NULL, col_out[M] = sum_k dY (the bias gradient) — the backward of nn.Linear's
+ * weight and bias (reference layers.py:82-106 via autograd) for many layers in ONE launch.
+ * dY is [K, M] row-major with row stride ld_dy, X is [K, N] with row stride ld_x. Deterministic
+ * (fixed split-K order). Needs `counters` (>= sum of 32x32 tiles, kept zero by the kernel) and
+ * aimx_wgrad_grouped_workspace_bytes() of workspace.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  const float* dY;
+  int64_t ld_dy;
+  const float* X;
+  int64_t ld_x;
+  float* dW;
+  int64_t ld_dw;
+  float* col_out;
+  int64_t M, N, K;
+} AimxWgradProblem;
+
+size_t aimx_wgrad_grouped_workspace_bytes(const AimxWgradProblem* problems, int32_t n);
+int aimx_wgrad_grouped(const AimxWgradProblem* problems, int32_t n, void* workspace, size_t workspace_bytes,
+                       int32_t* counters, int64_t n_counters, aimx_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused global-norm gradient clip + Adam step over a list of fp32 tensors (three launches).

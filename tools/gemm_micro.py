@@ -26,7 +26,7 @@ def bench(fn, it=50):
     return s.elapsed_time(e) / it * 1e3
 
 
-def run(M, N, K, layout, label, splits=0, torch_ref=True):
+def run(M, N, K, layout, label, splits=0, torch_ref=True, counters=True):
     A = torch.randn(M, K, device=dev) if layout[0] == "N" else torch.randn(K, M, device=dev)
     B = torch.randn(K, N, device=dev) if layout[1] == "N" else torch.randn(N, K, device=dev)
     C = torch.empty(M, N, device=dev)
@@ -39,7 +39,8 @@ def run(M, N, K, layout, label, splits=0, torch_ref=True):
     a.C, a.ldc = C.data_ptr(), N
     a.act, a.dact_kind = -1, -1
     a.splits = splits
-    a.counters, a.n_counters = _lib.counters(dev).data_ptr(), _lib.N_COUNTERS
+    if counters:
+        a.counters, a.n_counters = _lib.counters(dev).data_ptr(), _lib.N_COUNTERS
     wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
     ws = torch.empty(wsb // 4 + 1, device=dev)
     a.workspace, a.workspace_bytes = ws.data_ptr(), wsb
@@ -53,10 +54,26 @@ def run(M, N, K, layout, label, splits=0, torch_ref=True):
           f"  torch {t_torch:7.1f} us ({fl / t_torch / 1e6:6.1f} TF/s)")
 
 
+if len(sys.argv) > 1 and sys.argv[1] == "slices":
+    # per-slice latency: one split, few tiles, K swept (no reduction, idle chip)
+    for K in (512, 1024, 2048, 4096, 8192):
+        run(76, 77, K, "TN", f"dW mlp S=1 K={K}", splits=1, torch_ref=False)
+    for K in (512, 1024, 2048, 4096, 8192):
+        run(64, 64, K, "NT", f"NT 64x64 S=1 K={K}", splits=1, torch_ref=False)
+    sys.exit(0)
+
+if len(sys.argv) > 1 and sys.argv[1] == "dw":
+    for M, N, K, lab in [(76, 77, 9170, "c2 dW mlp"), (152, 305, 9170, "c2 dW_ig"), (256, 257, 9170, "c2 concat dW"),
+                         (256, 257, 520, "c2 ffn dW")]:
+        for sp in (0, 4, 8, 16, 32):
+            run(M, N, K, "TN", f"{lab} splits={sp}", splits=sp, torch_ref=False)
+    sys.exit(0)
+
 if len(sys.argv) > 1 and sys.argv[1] == "splits":
     for M, N, K, lab in [(76, 77, 9170, "c2 dW mlp"), (152, 305, 9170, "c2 dW_ig"), (256, 257, 9170, "c2 concat dW")]:
         for sp in (0, 4, 8, 12, 16, 24, 32, 48, 64):
             run(M, N, K, "TN", f"{lab} splits={sp}", splits=sp, torch_ref=False)
+            run(M, N, K, "TN", f"{lab} splits={sp} 2-kernel", splits=sp, torch_ref=False, counters=False)
     sys.exit(0)
 
 for args in [(9170, 152, 304, "NT", "c2 fwd [u|g]"), (9170, 76, 76, "NT", "c2 fwd mlp"),
