@@ -18,8 +18,9 @@
 //    operands (dY^T of the weight gradient) are stored k-major with a (BM+16)-float stride;
 //  * long-K / small-MN products (weight gradients, K = atoms) split K across workgroups; the
 //    partial slabs are reduced IN the launch by the last-arriving workgroup of each tile
-//    (agent-scope release/acquire + a self-resetting arrival counter, MI355X_MICROARCH.md
-//    §visibility), in slab order: deterministic, no atomics on the data, no extra launch.
+//    (sc1 slab stores/loads + a self-resetting agent-scope arrival counter, MI355X_MICROARCH.md
+//    §visibility "Valid forms"), in slab order: deterministic, no atomics on the data, no extra
+//    launch.
 // Epilogue (fused, see include/aimx.h): bias, residuals, pre-activation store, activation,
 // hash-dropout with mask store, mask/act' multiplication for the backward, and an implicit ones
 // column that turns a weight-gradient GEMM's last column into the bias gradient.
@@ -136,6 +137,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   // the b32 builtin returns the raw bits as an integer: reinterpret, never convert
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// Split-K slab hand-off between workgroups without fences (MI355X_MICROARCH.md "Valid forms",
+// row 1): every slab byte is stored and loaded with 16-byte `sc1` (device-coherent) buffer
+// accesses; each storing wave drains (vmcnt 0) before the workgroup barrier, one lane then adds
+// to the tile's agent-scope counter, and the workgroup whose add returns S-1 reduces. An agent
+// release per workgroup (an XCD-wide L2 write-back, serialised per XCD) cost ~0.7 us per block.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSC1 = 16;  // buffer cache-policy bit 4 = sc1
+__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, uint32_t voff, floatx4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, kSC1);
+}
+__device__ __forceinline__ floatx4 load_sc1(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, kSC1));
 }
 
 // AK: A is k-contiguous (sak == 1) -> row-major LDS image (row stride BK+2: bank = 2*row + k,
@@ -368,44 +383,39 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     const int tile = blockIdx.x * gridDim.y + blockIdx.y;
     const int64_t ntiles = (int64_t)gridDim.x * gridDim.y;
     constexpr int TILE = BM * BN;
-    floatx4* slab = reinterpret_cast<floatx4*>(a.workspace + ((int64_t)blockIdx.z * ntiles + tile) * TILE);
+    const int S = (int)gridDim.z;
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(a.workspace, (uint32_t)(4 * (int64_t)S * ntiles * TILE));
+    const uint32_t slab0 = (uint32_t)(4 * (((int64_t)blockIdx.z * ntiles + tile) * TILE));
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) slab[(i * TN + j) * 256 + tid] = acc[i][j];
+      for (int j = 0; j < TN; ++j) store_sc1(rws, slab0 + 16u * (uint32_t)((i * TN + j) * 256 + tid), acc[i][j]);
     if (!a.counters) return;  // reduced by k_splitk_reduce
-    // ---- in-launch ordered reduce by the last arriver (release -> ticket -> acquire) ----
+    // ---- in-launch ordered reduce by the last arriver (sc1 hand-off, see store_sc1) ----
     int* flag = reinterpret_cast<int*>(smem);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == (int)gridDim.z - 1);
-      if (last) {
-        __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      const int last = (old == S - 1);
+      if (last) __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
       flag[0] = last;
     }
     __syncthreads();
     if (!flag[0]) return;
     // slabs summed in slice order (deterministic), 8 slices' float4 loads in flight per fragment
-    const int S = (int)gridDim.z;
-    const floatx4* base = reinterpret_cast<const floatx4*>(a.workspace + (int64_t)tile * TILE);
-    const int64_t zstride = ntiles * TILE / 4;  // floatx4 per slice
+    const uint32_t zstride = (uint32_t)(4 * ntiles * TILE);  // bytes per slice
+    const uint32_t tile0 = (uint32_t)(4 * (int64_t)tile * TILE);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int64_t off = (i * TN + j) * 256 + tid;
+        const uint32_t off = tile0 + 16u * (uint32_t)((i * TN + j) * 256 + tid);
         floatx4 s = floatx4{0.f, 0.f, 0.f, 0.f};
         for (int z0 = 0; z0 < S; z0 += 8) {
           floatx4 t[8];
 #pragma unroll
-          for (int w = 0; w < 8; ++w) t[w] = __builtin_nontemporal_load(&base[min(z0 + w, S - 1) * zstride + off]);
+          for (int w = 0; w < 8; ++w) t[w] = load_sc1(rws, (uint32_t)min(z0 + w, S - 1) * zstride + off);
 #pragma unroll
           for (int w = 0; w < 8; ++w)
             if (z0 + w < S) s += t[w];
@@ -542,45 +552,41 @@ __device__ __forceinline__ void wgrad_block(const AimxGemmArgs& a, int kchunk, u
         for (int j = 0; j < 2; ++j) acc[i][j] += *reinterpret_cast<const floatx4*>(&red[q * 1024 + ((i * 2 + j) * 64 + lane) * 4]);
   }
   if (S > 1) {
-    floatx4* slab = reinterpret_cast<floatx4*>(ws + ((int64_t)bz * ntiles + tile) * 1024);
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(ws, (uint32_t)(4 * (int64_t)S * ntiles * 1024));
+    const uint32_t slab0 = (uint32_t)(4 * (((int64_t)bz * ntiles + tile) * 1024));
     if (w == 0) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) slab[(i * 2 + j) * 64 + lane] = acc[i][j];
+        for (int j = 0; j < 2; ++j) store_sc1(rws, slab0 + 16u * (uint32_t)((i * 2 + j) * 64 + lane), acc[i][j]);
     }
     if (!counters) return;
+    // sc1 hand-off (see store_sc1): drained stores -> barrier -> one agent add; last adder reduces
     int* flag = reinterpret_cast<int*>(red);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int old = __hip_atomic_fetch_add(&counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = (old == S - 1);
-      if (last) {
-        __hip_atomic_store(&counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(&counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
       flag[0] = last;
     }
     __syncthreads();
     if (!flag[0]) return;
     // ordered slab sum: wave q sums slices q, q+4, ... ; the 4 partial sums are added in wave order
-    const floatx4* base = reinterpret_cast<const floatx4*>(ws + (int64_t)tile * 1024);
-    const int64_t zs = ntiles * 256;  // floatx4 per slice
+    const uint32_t zs = (uint32_t)(4 * ntiles * 1024);  // bytes per slice
+    const uint32_t tile0 = (uint32_t)(4 * (int64_t)tile * 1024);
     floatx4 part[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int off = (i * 2 + j) * 64 + lane;
+        const uint32_t off = tile0 + 16u * (uint32_t)((i * 2 + j) * 64 + lane);
         floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
         for (int z0 = w; z0 < S; z0 += 16) {
           floatx4 t[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) t[q] = __builtin_nontemporal_load(&base[min(z0 + 4 * q, S - 1) * zs + off]);
+          for (int q = 0; q < 4; ++q) t[q] = load_sc1(rws, (uint32_t)min(z0 + 4 * q, S - 1) * zs + off);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             if (z0 + 4 * q < S) sum += t[q];
