@@ -71,39 +71,56 @@ def collate(mols, max_hops, hops=None):
 
 
 class DeviceBatch:
-    """A collated batch resident in HBM, in the reference trainer's argument layout."""
+    """A collated batch resident in HBM, in the reference trainer's argument layout.
+
+    All fields are typed views into ONE device byte buffer, so re-filling a static (graph-captured)
+    batch is a single copy (copy_) instead of one per tensor."""
+
+    _FIELDS = ("feat0", "feat1", "feat2", "feat3", "edges", "batch", "total_charges", "targets")
 
     def __init__(self, col, device, targets=None, total_charges=None):
-        self.atom_features = {k: torch.from_numpy(np.ascontiguousarray(col["feats"][:, i])).to(device)
-                              for i, k in enumerate(FEATURE_KEYS)}
-        self.edges = torch.from_numpy(col["edges"]).to(device)
-        self.batch = torch.from_numpy(col["batch"]).to(device)
         g = len(col["n_atoms"])
         self.num_graphs = g
         self.num_atoms = int(col["batch"].shape[0])
         tc = total_charges if total_charges is not None else np.zeros(g, np.float32)
-        self.total_charges = torch.from_numpy(np.asarray(tc, np.float32)).to(device)
         tg = targets if targets is not None else np.zeros((g, 1), np.float32)
-        self.targets = torch.from_numpy(np.asarray(tg, np.float32)).to(device)
+        parts = [np.ascontiguousarray(col["feats"][:, i]).astype(np.int64) for i in range(len(FEATURE_KEYS))]
+        parts += [np.ascontiguousarray(col["edges"], np.int64), np.ascontiguousarray(col["batch"], np.int64),
+                  np.ascontiguousarray(tc, np.float32), np.ascontiguousarray(tg, np.float32)]
+        self._layout = []
+        off = 0
+        for a in parts:
+            self._layout.append((off, a.dtype, a.shape))
+            off += (a.nbytes + 255) // 256 * 256
+        host = np.zeros(max(off, 256), np.uint8)
+        for (o, _, _), a in zip(self._layout, parts):
+            host[o:o + a.nbytes] = a.view(np.uint8).reshape(-1)
+        self._blob = torch.from_numpy(host).to(device)
+        self._bind()
         self.tetrahedral = torch.empty(0, 4, dtype=torch.long, device=device)
         self.cis = torch.empty(0, 2, dtype=torch.long, device=device)
         self.trans = torch.empty(0, 2, dtype=torch.long, device=device)
 
+    def _bind(self):
+        views = []
+        for o, dt, shape in self._layout:
+            tdt = torch.int64 if dt == np.int64 else torch.float32
+            n = int(np.prod(shape)) if len(shape) else 1
+            views.append(self._blob[o:o + n * (8 if tdt == torch.int64 else 4)].view(tdt).view(*shape))
+        self.atom_features = {k: views[i] for i, k in enumerate(FEATURE_KEYS)}
+        self.edges, self.batch, self.total_charges, self.targets = views[len(FEATURE_KEYS):]
+
     def copy_(self, other):
-        """In-place copy of another batch of identical shapes (static graph inputs)."""
-        for k in self.atom_features:
-            self.atom_features[k].copy_(other.atom_features[k], non_blocking=True)
-        self.edges.copy_(other.edges, non_blocking=True)
-        self.batch.copy_(other.batch, non_blocking=True)
-        self.total_charges.copy_(other.total_charges, non_blocking=True)
-        self.targets.copy_(other.targets, non_blocking=True)
+        """In-place copy of another batch of identical layout (static graph inputs): one copy."""
+        if other._layout != self._layout:
+            raise ValueError("DeviceBatch.copy_: layouts differ")
+        self._blob.copy_(other._blob, non_blocking=True)
 
     def clone(self):
         import copy
         b = copy.copy(self)
-        b.atom_features = {k: v.clone() for k, v in self.atom_features.items()}
-        for k in ("edges", "batch", "total_charges", "targets"):
-            setattr(b, k, getattr(self, k).clone())
+        b._blob = self._blob.clone()
+        b._bind()
         return b
 
     def model_args(self):

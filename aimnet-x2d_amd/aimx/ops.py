@@ -531,3 +531,110 @@ def embed_project(indices, tables, W, b, act=None):
     _lib.require_device(W, *indices)
     kind = -1 if act is None else _lib.ACT_KIND[act]
     return _EmbedProject.apply(list(indices), kind, W, b, *tables)
+
+
+# ---------------------------------------------------------------------------------------------
+# Grouped weight gradients (aimx_wgrad_grouped) and the fused LinearBlock (layers.py:170-219)
+# ---------------------------------------------------------------------------------------------
+def wgrad_grouped(problems):
+    """problems: list of (dY [K, M] (ld), X [K, N] (ld), dW [M, N] out, db [M] out or None), all on one
+    device; every dW = dY^T X (and db = sum_k dY) in one launch."""
+    lib = _lib.load()
+    n = len(problems)
+    arr = (_lib.WgradProblem * n)()
+    dev = problems[0][0].device
+    for i, (dy, x, dw, db) in enumerate(problems):
+        dy, ldy = _rows(dy)
+        x, ldx = _rows(x)
+        arr[i].dY, arr[i].ld_dy = ptr(dy), ldy
+        arr[i].X, arr[i].ld_x = ptr(x), ldx
+        arr[i].dW, arr[i].ld_dw = ptr(dw), dw.shape[1]
+        arr[i].col_out = ptr(db)
+        arr[i].M, arr[i].N, arr[i].K = dy.shape[1], x.shape[1], dy.shape[0]
+    wsb = lib.aimx_wgrad_grouped_workspace_bytes(arr, n)
+    ws = torch.empty(max(wsb // 4, 1), dtype=_F32, device=dev)
+    check(lib.aimx_wgrad_grouped(arr, n, ptr(ws), ws.numel() * 4, ptr(_lib.counters(dev)), _lib.N_COUNTERS,
+                                 stream_ptr(dev)), "wgrad_grouped")
+    return ws
+
+
+class _LinearBlock(torch.autograd.Function):
+    """y = linear2(dropout(act(linear1(x)))) [+ x]: two fused GEMMs forward (bias, activation,
+    pre-activation store and hash dropout in the first epilogue; bias and skip in the second), two
+    input-gradient GEMMs with act'/mask fused, and both weight gradients in one grouped launch."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, act, drop_p, skip, seed):
+        dev = x.device
+        shape = x.shape
+        x2, ldx = _rows(x.reshape(-1, shape[-1]))
+        M, n_in = x2.shape
+        n_out = W1.shape[0]
+        W1, b1, W2, b2 = W1.contiguous(), b1.contiguous(), W2.contiguous(), b2.contiguous()
+        H = torch.empty(M, n_out, dtype=_F32, device=dev)
+        V = torch.empty(M, n_out, dtype=_F32, device=dev)
+        drop = seed is not None and drop_p > 0
+        mask = torch.empty(M, n_out, dtype=torch.uint8, device=dev) if drop else None
+        a = _gemm_args(M, n_out, n_in)
+        a.A, a.sam, a.sak = ptr(x2), ldx, 1
+        a.B, a.sbk, a.sbn = ptr(W1), 1, n_in
+        a.C, a.ldc = ptr(H), n_out
+        a.bias = ptr(b1)
+        a.act, a.act_ncols, a.pre, a.ldpre = act, n_out, ptr(V), n_out
+        if drop:
+            a.drop_p, a.drop_seed, a.drop_salt = float(drop_p), ptr(seed), 0x5EED
+            a.mask_out, a.ldmask = ptr(mask), n_out
+        _run_gemm(a, dev)
+        Y = torch.empty(M, n_out, dtype=_F32, device=dev)
+        a = _gemm_args(M, n_out, n_out)
+        a.A, a.sam, a.sak = ptr(H), n_out, 1
+        a.B, a.sbk, a.sbn = ptr(W2), 1, n_out
+        a.C, a.ldc = ptr(Y), n_out
+        a.bias = ptr(b2)
+        if skip:
+            a.res[0], a.ldres[0] = ptr(x2), ldx
+        _run_gemm(a, dev)
+        ctx.act, ctx.drop_p, ctx.skip, ctx.shape = act, float(drop_p), skip, shape
+        ctx.save_for_backward(x2, W1, W2, H, V, mask)
+        return Y.view(*shape[:-1], n_out)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, W1, W2, H, V, mask = ctx.saved_tensors
+        dev = dy.device
+        M, n_in = x2.shape
+        n_out = W1.shape[0]
+        dY, ldy = _rows(dy.reshape(-1, n_out))
+        dV = torch.empty(M, n_out, dtype=_F32, device=dev)
+        a = _gemm_args(M, n_out, n_out)  # dV = (dY W2) * mask/(1-p) * act'(V)
+        a.A, a.sam, a.sak = ptr(dY), ldy, 1
+        a.B, a.sbk, a.sbn = ptr(W2), n_out, 1
+        a.C, a.ldc = ptr(dV), n_out
+        if mask is not None:
+            a.drop_p, a.mask_in, a.ldmask = ctx.drop_p, ptr(mask), n_out
+        a.dact_pre, a.lddact, a.dact_kind = ptr(V), n_out, ctx.act
+        _run_gemm(a, dev)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, n_in, dtype=_F32, device=dev)
+            a = _gemm_args(M, n_in, n_out)  # dx = dV W1 [+ dY]
+            a.A, a.sam, a.sak = ptr(dV), n_out, 1
+            a.B, a.sbk, a.sbn = ptr(W1), n_in, 1
+            a.C, a.ldc = ptr(dx), n_in
+            if ctx.skip:
+                a.res[0], a.ldres[0] = ptr(dY), ldy
+            _run_gemm(a, dev)
+            dx = dx.view(*ctx.shape[:-1], n_in)
+        dW1, db1 = torch.empty_like(W1), torch.empty(n_out, dtype=_F32, device=dev)
+        dW2, db2 = torch.empty_like(W2), torch.empty(n_out, dtype=_F32, device=dev)
+        wgrad_grouped([(dY, H, dW2, db2), (dV, x2, dW1, db1)])
+        return dx, dW1, db1, dW2, db2, None, None, None, None
+
+
+def linear_block(x, W1, b1, W2, b2, act, drop_p=0.0, training=False, skip=False):
+    """reference LinearBlock.forward (layers.py:204-219) with skip_proj = None."""
+    _lib.require_device(x, W1, W2)
+    kind = _lib.ACT_KIND[act] if isinstance(act, str) else int(act)
+    seed = (torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64)
+            if (training and drop_p > 0) else None)
+    return _LinearBlock.apply(x, W1, b1, W2, b2, kind, float(drop_p), bool(skip), seed)

@@ -111,11 +111,11 @@ class LinearBlock(nn.Module):
         self.skip_proj = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        # activation fused into linear1's GEMM epilogue (stateless module, same math)
-        out = self.linear2(self.dropout(self.linear1(x, act=activation_name(self.activation))))
-        if self.use_skip:
-            out = out + (self.skip_proj(x) if self.skip_proj is not None else x)
-        return out
+        # one fused operator: linear1 + activation + dropout (hash mask, honours self.dropout's
+        # training flag) + linear2 + skip, with a fused backward (aimx.ops.linear_block)
+        return ops.linear_block(x, self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias,
+                                activation_name(self.activation), self.dropout.p, self.dropout.training,
+                                self.use_skip)
 
 
 class MultiLayerPerceptron(nn.Module):
