@@ -80,6 +80,11 @@ class EmbeddingTables(ctypes.Structure):
     ]
 
 
+class CsrSpec(ctypes.Structure):
+    _fields_ = [("key", c_ptr), ("key_stride", c_i64), ("key_mod", c_i64), ("val", c_ptr), ("val_stride", c_i64),
+                ("val_mod", c_i64), ("n_items", c_i64), ("n_rows", c_i64), ("rowptr", c_ptr), ("col", c_ptr)]
+
+
 class WgradProblem(ctypes.Structure):
     _fields_ = [("dY", c_ptr), ("ld_dy", c_i64), ("X", c_ptr), ("ld_x", c_i64), ("dW", c_ptr), ("ld_dw", c_i64),
                 ("col_out", c_ptr), ("M", c_i64), ("N", c_i64), ("K", c_i64)]
@@ -100,6 +105,8 @@ _SIGS = {
     "aimx_csr_workspace_bytes": (c_size, [c_i64, c_i64]),
     "aimx_csr_build": (c_i32, [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_size,
                                c_ptr, c_ptr]),
+    "aimx_csr_build_multi_workspace_bytes": (c_size, [ctypes.POINTER(CsrSpec), c_i32]),
+    "aimx_csr_build_multi": (c_i32, [ctypes.POINTER(CsrSpec), c_i32, c_ptr, c_size, c_ptr, c_ptr]),
     "aimx_segment_gather_sum": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i64,
                                         c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "aimx_gemm_workspace_bytes": (c_size, [ctypes.POINTER(GemmArgs)]),

@@ -50,6 +50,26 @@ def build_csr(key_ptr, key_stride, key_mod, val_ptr, val_stride, val_mod, n_item
     return CSR(rowptr, col, n_rows)
 
 
+def build_csrs(specs, device, status):
+    """All CSRs of a plan in one pass (aimx_csr_build_multi: one launch per phase for all)."""
+    lib = _lib.load()
+    arr = (_lib.CsrSpec * len(specs))()
+    out = []
+    for i, (kp, ks, km, vp, vs, vm, n_items, n_rows, _) in enumerate(specs):
+        rowptr = torch.empty(n_rows + 1, dtype=torch.int32, device=device)
+        col = torch.empty(max(n_items, 1), dtype=torch.int32, device=device)
+        arr[i].key, arr[i].key_stride, arr[i].key_mod = kp, ks, km
+        arr[i].val, arr[i].val_stride, arr[i].val_mod = vp, vs, vm
+        arr[i].n_items, arr[i].n_rows = n_items, n_rows
+        arr[i].rowptr, arr[i].col = rowptr.data_ptr(), col.data_ptr()
+        out.append(CSR(rowptr, col, n_rows))
+    wsb = lib.aimx_csr_build_multi_workspace_bytes(arr, len(specs))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
+    _lib.check(lib.aimx_csr_build_multi(arr, len(specs), ws.data_ptr(), wsb, status.data_ptr(),
+                                        _lib.stream_ptr(device)), "csr_build_multi")
+    return out
+
+
 class GraphPlan:
     """CSR views for one batch. `edges` [E,2] (target, source) or separate target/src vectors."""
 
@@ -76,18 +96,22 @@ class GraphPlan:
             self.E = 0
             e = torch.zeros(0, 2, dtype=torch.int64, device=self.device)
             (t_ptr, t_st), (s_ptr, s_st) = _col(e, 0), _col(e, 1)
-        if self.N > 0:  # E == 0 gives all-empty rows: every hop chunk is zero (layers.py:148-149)
-            n, h = self.N, self.num_hops
-            self.fwd = build_csr(t_ptr, t_st, 0, s_ptr, s_st, n, self.E, h * n, self.device, self.status)
-            self.bwd = build_csr(s_ptr, s_st, n, t_ptr, t_st, 0, self.E, n, self.device, self.status)
         self.batch = batch
         self.G = None
+        specs = []  # (key, key_stride, key_mod, val, val_stride, val_mod, n_items, n_rows, attribute)
+        if self.N > 0:  # E == 0 gives all-empty rows: every hop chunk is zero (layers.py:148-149)
+            n, h = self.N, self.num_hops
+            specs.append((t_ptr, t_st, 0, s_ptr, s_st, n, self.E, h * n, "fwd"))
+            specs.append((s_ptr, s_st, n, t_ptr, t_st, 0, self.E, n, "bwd"))
         if batch is not None:
             b = _as_i64(batch)
             self._keep.append(b)
             g = int(num_graphs) if num_graphs is not None else int(b.max().item()) + 1 if b.numel() else 0
             self.G = g
-            self.graph = build_csr(b.data_ptr(), b.stride(0), 0, None, 0, 0, b.shape[0], g, self.device, self.status)
+            specs.append((b.data_ptr(), b.stride(0), 0, None, 0, 0, b.shape[0], g, "graph"))
+        if specs:
+            for name, c in zip([sp[-1] for sp in specs], build_csrs(specs, self.device, self.status)):
+                setattr(self, name, c)
         if _VALIDATE:
             self.validate()
 

@@ -224,3 +224,172 @@ extern "C" int aimx_csr_build(const int64_t* key, int64_t key_stride, int64_t ke
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Several CSRs in one pass (the plan's fwd / bwd / graph CSRs): one launch per phase for all of
+// them. Rows of all specs are concatenated (spec s owns global rows [row0_s, row0_s + rows_s)),
+// items likewise; one scan over all rows gives global positions, and each spec's rowptr is the
+// scan relative to its first row.
+// ---------------------------------------------------------------------------------------------
+namespace aimx {
+namespace {
+
+constexpr int kMaxSpecs = 4;
+struct MultiTable {
+  int32_t n;
+  int64_t item0[kMaxSpecs + 1], row0[kMaxSpecs + 1];
+  AimxCsrSpec s[kMaxSpecs];
+};
+
+__device__ __forceinline__ int spec_of_item(const MultiTable& t, int64_t i) {
+  int q = 0;
+  while (q + 1 < t.n && t.item0[q + 1] <= i) ++q;
+  return q;
+}
+__device__ __forceinline__ int spec_of_row(const MultiTable& t, int64_t r) {
+  int q = 0;
+  while (q + 1 < t.n && t.row0[q + 1] <= r) ++q;
+  return q;
+}
+
+__global__ void k_count_multi(const MultiTable t, int32_t* __restrict__ deg, int32_t* __restrict__ status) {
+  const int64_t total = t.item0[t.n];
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int q = spec_of_item(t, g);
+    const AimxCsrSpec& sp = t.s[q];
+    const int64_t k = read_key(sp.key, sp.key_stride, sp.key_mod, g - t.item0[q]);
+    if (k >= 0 && k < sp.n_rows) {
+      atomicAdd(&deg[t.row0[q] + k], 1);
+    } else if (status) {
+      atomicOr(status, AIMX_STATUS_KEY_OUT_OF_RANGE);
+    }
+  }
+}
+
+__global__ void k_fill_multi(const MultiTable t, const int32_t* __restrict__ scan, int32_t* __restrict__ cursor,
+                             int32_t* __restrict__ t_key, int32_t* __restrict__ t_val, int32_t* __restrict__ t_id) {
+  const int64_t total = t.item0[t.n];
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int q = spec_of_item(t, g);
+    const AimxCsrSpec& sp = t.s[q];
+    const int64_t i = g - t.item0[q];
+    const int64_t k = read_key(sp.key, sp.key_stride, sp.key_mod, i);
+    if (k < 0 || k >= sp.n_rows) continue;
+    const int64_t row = t.row0[q] + k;
+    const int32_t pos = scan[row] + atomicAdd(&cursor[row], 1);
+    int64_t v = i;
+    if (sp.val) {
+      v = sp.val[i * sp.val_stride];
+      if (sp.val_mod > 0) v = pymod(v, sp.val_mod);
+    }
+    t_key[pos] = (int32_t)row;
+    t_val[pos] = (int32_t)v;
+    t_id[pos] = (int32_t)i;
+  }
+}
+
+// Threads over max(valid items, rows + specs): stable placement of every item, and each spec's
+// rowptr = global scan relative to the spec's first row.
+__global__ void k_order_multi(const MultiTable t, int64_t work, const int32_t* __restrict__ scan,
+                              const int32_t* __restrict__ t_key, const int32_t* __restrict__ t_val,
+                              const int32_t* __restrict__ t_id) {
+  const int64_t R = t.row0[t.n];
+  const int32_t n_valid = scan[R];
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < work; g += (int64_t)gridDim.x * blockDim.x) {
+    if (g < n_valid) {
+      const int32_t row = t_key[g];
+      const int q = spec_of_row(t, row);
+      const int32_t b = scan[row], e = scan[row + 1];
+      const int32_t me = t_id[g];
+      int32_t rank = 0;
+      for (int32_t p = b; p < e; ++p) rank += (t_id[p] < me) ? 1 : 0;
+      t.s[q].col[b - scan[t.row0[q]] + rank] = t_val[g];
+    }
+    // rowptr entries: global row index r in [0, R + n) -> spec q, local i in [0, rows_q]
+    if (g < R + t.n) {
+      int q = 0;
+      while (q + 1 < t.n && g >= t.row0[q + 1] + (q + 1)) ++q;
+      const int64_t i = g - t.row0[q] - q;
+      if (i <= t.s[q].n_rows) t.s[q].rowptr[i] = scan[t.row0[q] + i] - scan[t.row0[q]];
+    }
+  }
+}
+
+}  // namespace
+}  // namespace aimx
+
+extern "C" size_t aimx_csr_build_multi_workspace_bytes(const AimxCsrSpec* specs, int32_t n) {
+  if (!specs || n < 1 || n > aimx::kMaxSpecs) return 0;
+  int64_t R = 0, I = 0;
+  for (int32_t i = 0; i < n; ++i) R += specs[i].n_rows, I += specs[i].n_items;
+  const int64_t nb = cdiv(R > 0 ? R : 1, aimx::kScanTile);
+  return 2 * aimx::align256(sizeof(int32_t) * (size_t)(R + 1)) + aimx::align256(sizeof(int32_t) * (size_t)(nb + 1)) +
+         3 * aimx::align256(sizeof(int32_t) * (size_t)(I + 1));
+}
+
+extern "C" int aimx_csr_build_multi(const AimxCsrSpec* specs, int32_t n, void* workspace, size_t workspace_bytes,
+                                    int32_t* status, aimx_stream_t stream_) {
+  using namespace aimx;
+  hipStream_t stream = (hipStream_t)stream_;
+  if (!specs || n < 1 || n > kMaxSpecs) return AIMX_EARG;
+  MultiTable t{};
+  t.n = n;
+  int64_t R = 0, I = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const AimxCsrSpec& sp = specs[i];
+    if (sp.n_items < 0 || sp.n_rows < 0 || !sp.rowptr || (sp.n_items > 0 && (!sp.key || !sp.col))) return AIMX_EARG;
+    t.s[i] = sp;
+    t.item0[i] = I;
+    t.row0[i] = R;
+    I += sp.n_items;
+    R += sp.n_rows;
+  }
+  t.item0[n] = I;
+  t.row0[n] = R;
+  if (I > INT32_MAX || R >= INT32_MAX) return AIMX_EARG;
+  if (!workspace || workspace_bytes < aimx_csr_build_multi_workspace_bytes(specs, n)) return AIMX_EARG;
+  const int64_t nb = cdiv(R > 0 ? R : 1, kScanTile);
+  char* ws = (char*)workspace;
+  int32_t* deg = (int32_t*)ws;
+  ws += align256(sizeof(int32_t) * (size_t)(R + 1));
+  int32_t* scan = (int32_t*)ws;
+  ws += align256(sizeof(int32_t) * (size_t)(R + 1));
+  int32_t* bsum = (int32_t*)ws;
+  ws += align256(sizeof(int32_t) * (size_t)(nb + 1));
+  int32_t* t_key = (int32_t*)ws;
+  ws += align256(sizeof(int32_t) * (size_t)(I + 1));
+  int32_t* t_val = (int32_t*)ws;
+  ws += align256(sizeof(int32_t) * (size_t)(I + 1));
+  int32_t* t_id = (int32_t*)ws;
+  const int threads = 256;
+  hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>(cdiv(R + 1, threads), 4096)), dim3(threads), 0, stream,
+                     deg, R + 1);
+  AIMX_CHECK_LAUNCH();
+  const int64_t grid_items = std::min<int64_t>(cdiv(I > 0 ? I : 1, threads), 8192);
+  if (I > 0) {
+    hipLaunchKernelGGL(k_count_multi, dim3((unsigned)grid_items), dim3(threads), 0, stream, t, deg, status);
+    AIMX_CHECK_LAUNCH();
+  }
+  // scan[0..R) = exclusive scan(deg); scan[R] = total; deg re-zeroed (the fill cursor)
+  if (R > 0) {
+    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nb), dim3(kScanThreads), 0, stream, deg, R, scan, bsum);
+    AIMX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, stream, bsum, nb, scan + R);
+    AIMX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kScanThreads), 0, stream, scan, R, bsum, deg);
+    AIMX_CHECK_LAUNCH();
+  } else {
+    hipLaunchKernelGGL(k_zero_i32, dim3(1), dim3(64), 0, stream, scan, (int64_t)1);
+    AIMX_CHECK_LAUNCH();
+  }
+  if (I > 0) {
+    hipLaunchKernelGGL(k_fill_multi, dim3((unsigned)grid_items), dim3(threads), 0, stream, t, (const int32_t*)scan, deg,
+                       t_key, t_val, t_id);
+    AIMX_CHECK_LAUNCH();
+  }
+  const int64_t work = std::max<int64_t>(I, R + n);
+  hipLaunchKernelGGL(k_order_multi, dim3((unsigned)std::min<int64_t>(cdiv(work, threads), 8192)), dim3(threads), 0,
+                     stream, t, work, (const int32_t*)scan, t_key, t_val, t_id);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}

@@ -58,6 +58,23 @@ int aimx_csr_build(const int64_t* key, int64_t key_stride, int64_t key_mod,
                    int64_t n_items, int64_t n_rows, int32_t* rowptr, int32_t* col,
                    void* workspace, size_t workspace_bytes, int32_t* status, aimx_stream_t stream);
 
+/* Several CSRs (at most 4) in one pass — one launch per phase for all of them. Each spec is the
+ * argument set of aimx_csr_build; rowptr/col are written per spec exactly as aimx_csr_build
+ * would (bit-identical), keys out of range are flagged in *status. */
+typedef struct {
+  const int64_t* key;
+  int64_t key_stride, key_mod;
+  const int64_t* val;
+  int64_t val_stride, val_mod;
+  int64_t n_items, n_rows;
+  int32_t* rowptr;
+  int32_t* col;
+} AimxCsrSpec;
+
+size_t aimx_csr_build_multi_workspace_bytes(const AimxCsrSpec* specs, int32_t n);
+int aimx_csr_build_multi(const AimxCsrSpec* specs, int32_t n, void* workspace, size_t workspace_bytes,
+                         int32_t* status, aimx_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Multi-hop scatter-add as a segmented gather-sum (the hop).
  * Replaces ShellConvolutionLayer.message_passing (reference src/models/layers.py:133-167):
