@@ -1,0 +1,38 @@
+"""Copy the round's profile summaries from gpurun_out/round/ into profiles/ (tracked).
+
+usage: python tools/collect_profiles.py <round tag, e.g. r01>
+"""
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag = sys.argv[1]
+src = os.path.join(ROOT, "gpurun_out", "round")
+dst = os.path.join(ROOT, "profiles")
+os.makedirs(dst, exist_ok=True)
+
+
+def one(pattern):
+    hits = glob.glob(os.path.join(src, pattern), recursive=True)
+    if not hits:
+        raise SystemExit(f"missing {pattern}")
+    return hits[0]
+
+
+shutil.copy(one("bench/**/*kernel_stats.csv"), os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+shutil.copy(one("roof/**/*kernel_stats.csv"), os.path.join(dst, f"{tag}_hop_roofline_kernel_stats.csv"))
+with open(os.path.join(dst, f"{tag}_step_breakdown.txt"), "w") as f:
+    f.write(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "step_kernels.py"), os.path.join(src, "bench")],
+                           capture_output=True, text=True, check=True).stdout)
+subprocess.run([sys.executable, os.path.join(ROOT, "tools", "hop_traffic.py"), os.path.join(src, "pmc_fetch"),
+                os.path.join(src, "pmc_write"), os.path.join(src, "pmc_fetch.log"),
+                os.path.join(dst, "hop_traffic.json")], check=True)
+for name in ("bench_plain.log", "roof.log"):
+    lines = [ln for ln in open(os.path.join(src, name)) if ln.startswith("{")]
+    with open(os.path.join(dst, f"{tag}_{name.replace('.log', '.json')}"), "w") as f:
+        f.write(lines[-1])
+print(json.dumps(json.load(open(os.path.join(dst, "hop_traffic.json"))), indent=1))
