@@ -143,6 +143,25 @@ def test_hop_forward_bit_exact_hubs(hub_degree):
     assert norm_rel(xg.grad.cpu().numpy(), x64.grad.numpy()) < 1e-6
 
 
+def test_hop_forward_bit_exact_large():
+    """A multi-molecule graph with rows * D >= 2^24 (thousands of row tiles): still bit-exact."""
+    from aimx.plan import GraphPlan
+    from aimx import ops
+    _, om = _oracle()
+    z = load_golden("c2")
+    e0 = torch.from_numpy(z["edges"].astype(np.int64))
+    n0 = z["feats"].shape[0]
+    reps = 9
+    e = torch.cat([e0 + r * n0 for r in range(reps)], 0)
+    n = n0 * reps
+    assert 3 * n * 76 >= 1 << 24
+    x = torch.randn(n, 76, generator=torch.Generator().manual_seed(5))
+    ref = torch.cat(om.message_passing(x, e[:, 0], e[:, 1], 3), 0)
+    plan = GraphPlan(n, 3, edges=e.to(DEV))
+    out = ops.hop(plan, x.to(DEV))
+    assert torch.equal(out.cpu(), ref)
+
+
 def test_hop_backward():
     from aimx.plan import GraphPlan
     from aimx import ops
