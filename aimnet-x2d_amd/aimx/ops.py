@@ -209,8 +209,10 @@ class _Hop(torch.autograd.Function):
         h = plan.num_hops
         x, ldx = _rows(x)
         out = torch.empty(h * n, d, dtype=_F32, device=x.device)
+        # out viewed as h chunks of n rows (same addresses): tells the kernel where chunk 0 ends
         check(lib.aimx_segment_gather_sum(ptr(x), ldx, 0, 0, d, ptr(plan.fwd.rowptr), ptr(plan.fwd.col), h * n,
-                                          ptr(out), d, 0, 0, None, 0, None, 0, stream_ptr(x.device)), "hop_forward")
+                                          ptr(out), d, n, n * d, None, 0, None, 0, stream_ptr(x.device)),
+              "hop_forward")
         ctx.plan = plan
         return out
 

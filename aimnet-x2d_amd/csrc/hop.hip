@@ -6,12 +6,14 @@
 // (edges with target t, ascending edge id) and sums the source rows in that order starting from
 // +0.0f, which reproduces CPU ATen scatter_add_ bit for bit. Lanes run along the feature dim with
 // VEC-wide (16/8/4-byte) loads; a 64-lane wave covers 64*VEC consecutive floats of the flattened
-// [rows, D] output, so the stores and the gathered source rows are coalesced. A workgroup owns a
-// tile of consecutive rows and stages the tile's rowptr/col slices in LDS first (see k_gather_sum
-// below). Source rows of one molecule sit together in
-// HBM, so neighbour re-reads hit L2; the only compulsory HBM traffic is x once, the CSR once and
-// the output once (SURVEY.md §8d algorithmic bytes).
+// [rows, D] output, so the stores are coalesced. A workgroup owns a tile of consecutive rows: it
+// stages the tile's rowptr and col slices in LDS, then (when the tile's sources span few rows, as
+// they do in a molecular batch) the source rows themselves, and sums from LDS; the compulsory HBM
+// traffic is x once, the CSR once and the output once (SURVEY.md §8d algorithmic bytes). Measured
+// at roofline size (tools/hop_micro.py): 1.46 ms -> 1.11 ms per launch for staging the sources.
 #include <algorithm>
+#include <climits>
+#include <cstdlib>
 
 #include "aimx_common.h"
 
@@ -80,8 +82,10 @@ __device__ __forceinline__ int64_t row_off(uint32_t r, int64_t ld, const FastDiv
 // becomes a pure streaming store. Gathers are issued 8 at a time with clamped (always valid)
 // indices and summed with selects, so the sum is the ordered edge-order sum bit for bit.
 constexpr int kMaxTileRows = 64;
-constexpr int kColCap = 4096;  // staged col entries per tile (16 KiB)
 constexpr int kGroup = 8;      // gathers in flight per thread
+constexpr int kColCap = 512;             // default staged col entries per tile (2 KiB)
+constexpr int kStageBytes = 17 * 1024 + 512;  // default LDS for the staged source span
+constexpr int kBigMul = 8;             // small tiles per big tile
 
 template <bool CHUNKED>
 __device__ __forceinline__ int64_t src_off(uint32_t c, int64_t ld, const FastDiv& rpc, int64_t cs) {
@@ -131,33 +135,199 @@ __device__ __forceinline__ void tile_body(const float* __restrict__ src, int64_t
   }
 }
 
-template <int VEC, bool SRC_CHUNKED>
-__global__ __launch_bounds__(256) void k_gather_sum(const float* __restrict__ src, int64_t src_ld, FastDiv src_rpc,
-                                                     int64_t src_cs, FastDiv upr, const int32_t* __restrict__ rowptr,
-                                                     const int32_t* __restrict__ col, uint32_t rows, uint32_t tile_rows,
-                                                     float* __restrict__ out, int64_t out_ld, FastDiv out_rpc,
-                                                     int64_t out_cs, const float* __restrict__ add0, int64_t add0_ld,
-                                                     const float* __restrict__ add1, int64_t add1_ld) {
-  __shared__ int32_t s_ptr[kMaxTileRows + 1];
-  __shared__ int32_t s_col[kColCap];
-  const uint32_t r0 = blockIdx.x * tile_rows;
-  const uint32_t nr = min(tile_rows, rows - r0);
-  if (threadIdx.x <= nr) s_ptr[threadIdx.x] = rowptr[r0 + threadIdx.x];
-  __syncthreads();
-  const int32_t base = s_ptr[0];
-  const int32_t ncols = s_ptr[nr] - base;
-  if (ncols <= kColCap) {
-    for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) s_col[i] = col[base + i];
-    __syncthreads();
-    tile_body<VEC, true, SRC_CHUNKED>(src, src_ld, src_rpc, src_cs, upr, s_ptr, s_col, base, r0, nr, out, out_ld, out_rpc, out_cs,
-                         add0, add0_ld, add1, add1_ld, ncols > 0);
-  } else {
-    tile_body<VEC, false, SRC_CHUNKED>(src, src_ld, src_rpc, src_cs, upr, s_ptr, col, base, r0, nr, out, out_ld, out_rpc, out_cs,
-                          add0, add0_ld, add1, add1_ld, true);
+// Same sum with the tile's source rows staged in LDS. In a molecular batch the sources of a tile's
+// targets are rows of the same few molecules, so the tile's col values span a short row range
+// [lo, hi]; each of those rows is gathered ~deg times (once per edge that names it). Loading the
+// span once with coalesced loads and summing from LDS turns ~10 vector-L1 gathers per source row
+// into one global load plus ds_read_b128s (the L1 tag/fill rate, not HBM, bounds the unstaged
+// gather phase: TCP pending-stall ~55 % of cycles at roofline size).
+// cols[] holds BYTE offsets of the staged rows (precomputed once per tile) and cols[zslot] the
+// offset of an all-zero staged row: slots past a row's segment read the zero row, and adding +0.0f
+// leaves the sum bit-identical (the running sum starts at +0.0f, so it is never -0.0f), so the
+// edge loop needs no data selects, only an index select per edge.
+template <int VEC>
+__device__ __forceinline__ void tile_body_staged(const float* s_x, const FastDiv& upr, const int32_t* s_ptr,
+                                                 const int32_t* cols, int32_t zslot, int32_t base, uint32_t r0,
+                                                 uint32_t nr, float* __restrict__ out, int64_t out_ld,
+                                                 const FastDiv& out_rpc, int64_t out_cs,
+                                                 const float* __restrict__ add0, int64_t add0_ld,
+                                                 const float* __restrict__ add1, int64_t add1_ld) {
+  using T = typename VecT<VEC>::T;
+  constexpr int kU = 4;  // LDS reads in flight per thread (two items in lockstep measured slower)
+  const uint32_t units = nr * upr.d;
+  const char* xb = reinterpret_cast<const char*>(s_x);
+  for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
+    const uint32_t rl = fdiv(t, upr);
+    const uint32_t ub = (t - rl * upr.d) * VEC * 4;
+    const uint32_t r = r0 + rl;
+    const int32_t b = s_ptr[rl] - base, e = s_ptr[rl + 1] - base;
+    T acc = vzero<T>();
+    for (int32_t k = b; k < e; k += kU) {
+      T v[kU];
+#pragma unroll
+      for (int j = 0; j < kU; ++j) {
+        const int32_t off = cols[(k + j < e) ? k + j : zslot];
+        v[j] = *reinterpret_cast<const T*>(xb + off + ub);
+      }
+#pragma unroll
+      for (int j = 0; j < kU; ++j) vadd(acc, v[j]);
+    }
+    const uint32_t u = ub / 4;
+    if (add0) {
+      T s = *reinterpret_cast<const T*>(add0 + (int64_t)r * add0_ld + u);
+      vadd(s, acc);
+      acc = s;
+    }
+    if (add1) vadd(acc, *reinterpret_cast<const T*>(add1 + (int64_t)r * add1_ld + u));
+    *reinterpret_cast<T*>(out + row_off(r, out_ld, out_rpc, out_cs) + u) = acc;
   }
 }
 
+struct HopArgs {
+  const float* src;
+  int64_t src_ld, src_cs;
+  FastDiv src_rpc, upr;
+  const int32_t* rowptr;
+  const int32_t* col;
+  uint32_t rows, tile_rows;
+  uint32_t split_rows;  // rows [0, split) in workgroups of one tile; rows [split, rows) in big tiles
+  uint32_t nsmall;      // workgroups of the small-tile range
+  uint32_t big_rows;    // rows per big tile (a multiple of tile_rows)
+  uint32_t col_cap;     // staged col entries per tile (dynamic LDS)
+  uint32_t xcap_rows;   // staged source rows that fit the dynamic LDS (0: no staging)
+  float* out;
+  int64_t out_ld, out_cs;
+  FastDiv out_rpc;
+  const float* add0;
+  int64_t add0_ld;
+  const float* add1;
+  int64_t add1_ld;
+};
+
+// All LDS is dynamic, carved at 16-byte multiples (MI355X guide: a static __shared__ ahead of the
+// dynamic region shifts its base off 16-B alignment and every ds_read_b128 replays at ~64 cycles).
+struct HopLds {
+  int32_t* ptr;   // [kMaxTileRows + 1]
+  int32_t* lohi;  // [2]
+};
+constexpr int kLdsHead = 80;  // ints ahead of the col slice: ptr (65) + lohi (2), padded to 16 B
+
+// One tile of nr <= tile_rows rows at r0 (called by the whole workgroup; leaves LDS reusable).
+template <int VEC, bool SRC_CHUNKED>
+// s_col / s_x point into the dynamic LDS (col_cap entries, then the staged rows). They are passed
+// down as arguments, never stored in memory: a pointer loaded back from LDS is a generic pointer
+// and its reads become flat loads through the vector-memory pipe instead of ds_reads.
+__device__ __forceinline__ void process_tile(const HopArgs& a, HopLds& L, int32_t* s_col, float* s_x, uint32_t r0,
+                                             uint32_t nr) {
+  using T = typename VecT<VEC>::T;
+  if (threadIdx.x <= nr) L.ptr[threadIdx.x] = a.rowptr[r0 + threadIdx.x];
+  if (threadIdx.x == 0) {
+    L.lohi[0] = INT32_MAX;
+    L.lohi[1] = INT32_MIN;
+  }
+  __syncthreads();
+  const int32_t base = L.ptr[0];
+  const int32_t ncols = L.ptr[nr] - base;
+  if (ncols == 0) {  // no edges: a streaming store of zeros (+ the fused residual terms)
+    tile_body<VEC, true, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, L.ptr, s_col, base, r0, nr, a.out,
+                                      a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, false);
+  } else if ((uint32_t)ncols > a.col_cap) {
+    tile_body<VEC, false, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, L.ptr, a.col, base, r0, nr, a.out,
+                                       a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, true);
+  } else {
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+    for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) {
+      const int32_t c = a.col[base + i];
+      s_col[i] = c;
+      lo = min(lo, c);
+      hi = max(hi, c);
+    }
+    if (a.xcap_rows) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o, 64));
+        hi = max(hi, __shfl_xor(hi, o, 64));
+      }
+      if ((threadIdx.x & 63) == 0) {
+        atomicMin(&L.lohi[0], lo);
+        atomicMax(&L.lohi[1], hi);
+      }
+    }
+    __syncthreads();
+    bool staged = false;
+    if (a.xcap_rows) {
+      lo = L.lohi[0];
+      hi = L.lohi[1];
+      // the span plus one zero row must fit, and one col slot is kept for the zero row's offset
+      if ((uint32_t)(hi - lo) + 1 < a.xcap_rows && (uint32_t)ncols < a.col_cap) {
+        staged = true;
+        const int32_t D = (int32_t)(a.upr.d * VEC);
+        const int32_t span = hi - lo + 1;
+        // each thread rewrites the col entries it staged as byte offsets of the staged rows
+        for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) s_col[i] = (s_col[i] - lo) * D * 4;
+        if (threadIdx.x == 0) s_col[ncols] = span * D * 4;
+        const uint32_t units = (uint32_t)(span + 1) * a.upr.d;
+        for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
+          const uint32_t rl = fdiv(t, a.upr);
+          const uint32_t u = (t - rl * a.upr.d) * VEC;
+          T v = vzero<T>();
+          if (rl < (uint32_t)span)
+            v = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>((uint32_t)lo + rl, a.src_ld, a.src_rpc,
+                                                                         a.src_cs) + u);
+          *reinterpret_cast<T*>(s_x + rl * D + u) = v;
+        }
+        __syncthreads();
+        tile_body_staged<VEC>(s_x, a.upr, L.ptr, s_col, ncols, base, r0, nr, a.out, a.out_ld, a.out_rpc, a.out_cs,
+                              a.add0, a.add0_ld, a.add1, a.add1_ld);
+      }
+    }
+    if (!staged)
+      tile_body<VEC, true, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, L.ptr, s_col, base, r0, nr, a.out,
+                                        a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, true);
+  }
+  __syncthreads();  // LDS is reused by the next tile of a big tile
+}
+
+// Rows [0, split) (the first output chunk) run one tile per workgroup: separate workgroups overlap
+// their load phases better than tiles walked in sequence. Rows [split, rows) (hop chunks >= 1)
+// run in big tiles: a big tile whose rows hold no edges at all (the reference's chunks >= 1 are
+// empty, layers.py:154) is one long streaming store, so the two thirds of the output that are zero
+// cost stores, not workgroup launches; a big tile with edges walks its tiles in order.
+template <int VEC, bool SRC_CHUNKED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_gather_sum(const HopArgs a) {
+  // [ptr | lohi | pad] [col_cap col entries] [xcap_rows x D staged rows]
+  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
+  HopLds L{s_dyn, s_dyn + kMaxTileRows + 1};
+  int32_t* s_col = s_dyn + kLdsHead;
+  float* s_x = reinterpret_cast<float*>(s_dyn + kLdsHead + a.col_cap);
+  if (blockIdx.x < a.nsmall) {
+    const uint32_t r0 = blockIdx.x * a.tile_rows;
+    process_tile<VEC, SRC_CHUNKED>(a, L, s_col, s_x, r0, min(a.tile_rows, a.split_rows - r0));
+    return;
+  }
+  const uint32_t R0 = a.split_rows + (blockIdx.x - a.nsmall) * a.big_rows;
+  const uint32_t NR = min(a.big_rows, a.rows - R0);
+  if (threadIdx.x == 0) {
+    L.lohi[0] = a.rowptr[R0];
+    L.lohi[1] = a.rowptr[R0 + NR];
+  }
+  __syncthreads();
+  if (L.lohi[0] == L.lohi[1]) {
+    tile_body<VEC, true, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, L.ptr, s_col, 0, R0, NR, a.out,
+                                      a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, false);
+    return;
+  }
+  __syncthreads();
+  for (uint32_t r0 = R0; r0 < R0 + NR; r0 += a.tile_rows)
+    process_tile<VEC, SRC_CHUNKED>(a, L, s_col, s_x, r0, min(a.tile_rows, R0 + NR - r0));
+}
+
 inline bool aligned(const void* p, int bytes) { return ((uintptr_t)p % bytes) == 0; }
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  return e ? std::max<int64_t>(0, atoll(e)) : dflt;
+}
 
 }  // namespace
 }  // namespace aimx
@@ -184,23 +354,57 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   const int64_t upr_i = D / vec;
   // 32-bit thread indexing (rows * D / vec < 2^31) and int32 chunked row ids.
   if (rows * upr_i >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;
-  const FastDiv upr = make_fastdiv((uint32_t)upr_i);
-  const FastDiv srpc = make_fastdiv(src_rpc > 0 ? (uint32_t)src_rpc : 0);
-  const FastDiv orpc = make_fastdiv(out_rpc > 0 ? (uint32_t)out_rpc : 0);
   const int threads = 256;
   // tile height: ~2 vector units per thread, then shorter tiles while the grid is under 4
   // workgroups per CU (small batches are latency-bound: more workgroups hide more latency)
-  int64_t tr = std::min<int64_t>(kMaxTileRows, std::max<int64_t>(1, 2 * threads / upr_i));
+  const int64_t tile_units = env_i64("AIMX_HOP_TILE_UNITS", 2 * threads);
+  int64_t tr = std::min<int64_t>(kMaxTileRows, std::max<int64_t>(1, tile_units / upr_i));
   while (tr > 1 && cdiv(rows, tr) < 1024) tr = std::max<int64_t>(1, tr / 2);
-  const int64_t blocks = cdiv(rows, tr);
-  using KFn = void (*)(const float*, int64_t, FastDiv, int64_t, FastDiv, const int32_t*, const int32_t*, uint32_t,
-                      uint32_t, float*, int64_t, FastDiv, int64_t, const float*, int64_t, const float*, int64_t);
+  // output rows past the first chunk (hop chunks >= 1; out_rpc = rows per chunk) go in big tiles
+  // once those rows hold >= 2048 tiles (8 per CU) to spare
+  const int64_t split = (out_rpc > 0 && out_rpc < rows) ? out_rpc : rows;
+  const int64_t big_max = std::max<int64_t>(1, env_i64("AIMX_HOP_BIG_MUL", kBigMul));
+  const int64_t big_mul = std::max<int64_t>(1, std::min<int64_t>(big_max, cdiv(rows - split, tr) / 2048));
+  const int64_t big = tr * big_mul;
+  const int64_t nsmall = cdiv(split, tr);
+  const int64_t blocks = nsmall + cdiv(rows - split, big);
+  // LDS budget for the staged source span (AIMX_HOP_STAGE_BYTES overrides; 0 disables staging)
+  // (the defaults keep 8 workgroups = 32 waves per CU resident: <= 20 KiB of LDS each)
+  const int64_t col_cap = (std::max<int64_t>(64, env_i64("AIMX_HOP_COL_CAP", kColCap)) + 3) / 4 * 4;
+  const int64_t stage_bytes = env_i64("AIMX_HOP_STAGE_BYTES", kStageBytes);
+  int64_t xcap = stage_bytes / (4 * D);
+  if (xcap < 2) xcap = 0;
+  xcap = std::min<int64_t>(xcap, 4096);
+  const size_t dyn = (size_t)((kLdsHead + col_cap) * 4 + xcap * D * 4);
+  HopArgs a;
+  a.src = src;
+  a.src_ld = src_ld;
+  a.src_cs = src_cs;
+  a.src_rpc = make_fastdiv(src_rpc > 0 ? (uint32_t)src_rpc : 0);
+  a.upr = make_fastdiv((uint32_t)upr_i);
+  a.rowptr = rowptr;
+  a.col = col;
+  a.rows = (uint32_t)rows;
+  a.tile_rows = (uint32_t)tr;
+  a.split_rows = (uint32_t)split;
+  a.nsmall = (uint32_t)nsmall;
+  a.big_rows = (uint32_t)big;
+  a.col_cap = (uint32_t)col_cap;
+  a.xcap_rows = (uint32_t)xcap;
+  a.out = out;
+  a.out_ld = out_ld;
+  a.out_cs = out_cs;
+  a.out_rpc = make_fastdiv(out_rpc > 0 ? (uint32_t)out_rpc : 0);
+  a.add0 = add0;
+  a.add0_ld = add0_ld;
+  a.add1 = add1;
+  a.add1_ld = add1_ld;
+  using KFn = void (*)(const HopArgs);
   const bool chunked = src_rpc > 0;
   KFn fn = vec == 4 ? (chunked ? k_gather_sum<4, true> : k_gather_sum<4, false>)
            : vec == 2 ? (chunked ? k_gather_sum<2, true> : k_gather_sum<2, false>)
                       : (chunked ? k_gather_sum<1, true> : k_gather_sum<1, false>);
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(threads), 0, stream, src, src_ld, srpc, src_cs, upr, rowptr, col,
-                     (uint32_t)rows, (uint32_t)tr, out, out_ld, orpc, out_cs, add0, add0_ld, add1, add1_ld);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(threads), dyn, stream, a);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }

@@ -85,7 +85,10 @@ int aimx_csr_build_multi(const AimxCsrSpec* specs, int32_t n, void* workspace, s
  * + (r / rows_per_chunk)*chunk_stride (rows_per_chunk <= 0: base + r*ld), so the output can be
  * written straight into the column chunks of the concatenated [N, D*(h+1)] feature matrix
  * (layers.py:76-79) without a cat. add0/add1 (nullable, indexed by output row, plain ld) are
- * added to each output row (fused residual terms in the backward).
+ * added to each output row (fused residual terms in the backward). Output rows past the first
+ * chunk are expected to be mostly edge-free (the reference's hop chunks >= 1) and are walked in
+ * large tiles; pass out_rows_per_chunk = N, out_chunk_stride = N*out_ld for a plain [h*N, D]
+ * output to get that (same addresses as rows_per_chunk <= 0).
  * ------------------------------------------------------------------------------------------ */
 int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rows_per_chunk,
                             int64_t src_chunk_stride, int64_t D,

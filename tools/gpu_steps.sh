@@ -9,6 +9,7 @@ for spec in "$@"; do
   soft=0
   if [ "${spec:0:1}" = "?" ]; then soft=1; spec="${spec:1}"; fi
   read -r t log cmd <<<"$spec"
+  mkdir -p "$(dirname "gpurun_out/$log")"
   echo "[gpu_steps] $(date +%T) start: $cmd (limit ${t}s) -> $log"
   timeout -k 10 "$t" bash -c "$cmd" >"gpurun_out/$log" 2>&1
   rc=$?
