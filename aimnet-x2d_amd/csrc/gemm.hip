@@ -36,36 +36,41 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 32;
 
-// Batched epilogue over the NE outputs a thread owns: every global load it needs (C for beta,
-// bias, residuals, dropout mask, act' pre-activation) is issued before any store, so the loads
-// of all NE elements are in flight together instead of one memory round trip per element.
+// Epilogue over the NE outputs a thread owns, in two phases. epi_load issues every global load
+// the epilogue needs (C for beta, bias, residuals, act' pre-activation, dropout mask) and folds
+// them into two values per element (the additive term and the gradient factor); it depends only
+// on the element coordinates, so a kernel may run it BEFORE its main loop and let the loads land
+// behind the MFMA work. epi_apply then needs only the accumulators and does the stores.
 template <int NE>
-__device__ __forceinline__ void epilogue_n(const AimxGemmArgs& a, const int (&m)[NE], const int (&n)[NE],
-                                           float (&v)[NE]) {
+struct EpiPre {
+  float add[NE];
+  float dg[NE];
+};
+
+template <int NE>
+__device__ __forceinline__ void epi_load(const AimxGemmArgs& a, const int (&m)[NE], const int (&n)[NE],
+                                         EpiPre<NE>& p) {
   // Every load below is unconditional from a clamped address (selects, not branches), and every
   // optional operand is tested once outside its element loop, so all NE elements' loads are in
-  // flight together before the first store.
-  bool ok[NE], ones[NE];
+  // flight together.
   int64_t mc[NE];
   int nc[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
-    ones[e] = (a.ones_col != 0) & (n[e] == a.N - 1);
-    ok[e] = (m[e] < a.M) & (n[e] < a.N);
-    const bool in = ok[e] & !ones[e];
+    const bool ones = (a.ones_col != 0) & (n[e] == a.N - 1);
+    const bool in = (m[e] < a.M) & (n[e] < a.N) & !ones;
     mc[e] = in ? m[e] : 0;
     nc[e] = in ? n[e] : 0;
   }
-  float add[NE];
 #pragma unroll
-  for (int e = 0; e < NE; ++e) add[e] = 0.f;
+  for (int e = 0; e < NE; ++e) p.add[e] = 0.f;
   if (a.beta != 0.f) {
 #pragma unroll
-    for (int e = 0; e < NE; ++e) add[e] += a.beta * a.C[mc[e] * a.ldc + nc[e]];
+    for (int e = 0; e < NE; ++e) p.add[e] += a.beta * a.C[mc[e] * a.ldc + nc[e]];
   }
   if (a.bias) {
 #pragma unroll
-    for (int e = 0; e < NE; ++e) add[e] += a.bias[nc[e]];
+    for (int e = 0; e < NE; ++e) p.add[e] += a.bias[nc[e]];
   }
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
@@ -73,25 +78,36 @@ __device__ __forceinline__ void epilogue_n(const AimxGemmArgs& a, const int (&m)
       const float* __restrict__ rp = a.res[r];
       const int64_t ld = a.ldres[r];
 #pragma unroll
-      for (int e = 0; e < NE; ++e) add[e] += rp[mc[e] * ld + nc[e]];
+      for (int e = 0; e < NE; ++e) p.add[e] += rp[mc[e] * ld + nc[e]];
     }
   }
-  float dg[NE];
   if (a.dact_pre) {
 #pragma unroll
-    for (int e = 0; e < NE; ++e) dg[e] = act_grad(a.dact_kind, a.dact_pre[mc[e] * a.lddact + nc[e]]);
+    for (int e = 0; e < NE; ++e) p.dg[e] = act_grad(a.dact_kind, a.dact_pre[mc[e] * a.lddact + nc[e]]);
   } else {
 #pragma unroll
-    for (int e = 0; e < NE; ++e) dg[e] = 1.f;
+    for (int e = 0; e < NE; ++e) p.dg[e] = 1.f;
   }
   const float scale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
   if (a.mask_in) {
 #pragma unroll
-    for (int e = 0; e < NE; ++e) dg[e] *= a.mask_in[mc[e] * a.ldmask + nc[e]] ? scale : 0.f;
+    for (int e = 0; e < NE; ++e) p.dg[e] *= a.mask_in[mc[e] * a.ldmask + nc[e]] ? scale : 0.f;
   }
+}
+
+template <int NE>
+__device__ __forceinline__ void epi_apply(const AimxGemmArgs& a, const int (&m)[NE], const int (&n)[NE],
+                                          const float (&v)[NE], const EpiPre<NE>& p) {
+  bool ok[NE], ones[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    ones[e] = (a.ones_col != 0) & (n[e] == a.N - 1);
+    ok[e] = (m[e] < a.M) & (n[e] < a.N);
+  }
+  const float scale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
   float x[NE];
 #pragma unroll
-  for (int e = 0; e < NE; ++e) x[e] = v[e] + add[e];
+  for (int e = 0; e < NE; ++e) x[e] = v[e] + p.add[e];
   if (a.act_ncols > 0) {
     if (a.pre) {
 #pragma unroll
@@ -119,8 +135,16 @@ __device__ __forceinline__ void epilogue_n(const AimxGemmArgs& a, const int (&m)
     if (ones[e])
       a.col_out[m[e]] = v[e];
     else
-      a.C[m[e] * a.ldc + n[e]] = x[e] * dg[e];
+      a.C[m[e] * a.ldc + n[e]] = x[e] * p.dg[e];
   }
+}
+
+template <int NE>
+__device__ __forceinline__ void epilogue_n(const AimxGemmArgs& a, const int (&m)[NE], const int (&n)[NE],
+                                           float (&v)[NE]) {
+  EpiPre<NE> p;
+  epi_load<NE>(a, m, n, p);
+  epi_apply<NE>(a, m, n, v, p);
 }
 
 // Buffer descriptor over [p, p + bytes): out-of-range loads return 0 (used as the M/N/K edge
@@ -206,6 +230,24 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // Epilogue coordinates (the C tile is walked row-major, consecutive lanes on consecutive
+  // columns). For tiles with <= 8 outputs per thread, the epilogue operands are loaded NOW so
+  // their round trip overlaps the main loop instead of following it (not for split-K launches,
+  // where only the last-arriving workgroup runs the epilogue).
+  constexpr int NEPI = BM * BN / 256;
+  constexpr bool PRE = NEPI <= 8;
+  int em[NEPI], en[NEPI];
+#pragma unroll
+  for (int u = 0; u < NEPI; ++u) {
+    const int e = tid + u * 256;
+    em[u] = m0 + e / BN;
+    en[u] = n0 + e % BN;
+  }
+  EpiPre<NEPI> epre;
+  if constexpr (PRE) {
+    if (gridDim.z == 1) epi_load<NEPI>(a, em, en, epre);
+  }
 
   constexpr int NA4 = V4 ? BM * BK / 1024 : 1, NB4 = V4 ? BN * BK / 1024 : 1;
   auto load_slice = [&](int k0, bool tail, float (&ra)[NA], float (&rb)[NB]) {
@@ -439,18 +481,29 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
         for (int r = 0; r < 4; ++r)
           smem[(wr * WM + i * 16 + (lane >> 4) * 4 + r) * CS + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r];
     __syncthreads();
+    if constexpr (PRE) {
+      float ev[NEPI];
 #pragma unroll
-    for (int q0 = 0; q0 < BM * BN / 256; q0 += 4) {
-      int em[4], en[4];
-      float ev[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = tid + (q0 + u) * 256;
-        em[u] = m0 + e / BN;
-        en[u] = n0 + e % BN;
+      for (int u = 0; u < NEPI; ++u) {
+        const int e = tid + u * 256;
         ev[u] = smem[(e / BN) * CS + e % BN];
       }
-      epilogue_n<4>(a, em, en, ev);
+      if (gridDim.z > 1) epi_load<NEPI>(a, em, en, epre);
+      epi_apply<NEPI>(a, em, en, ev, epre);
+    } else {
+#pragma unroll
+      for (int q0 = 0; q0 < NEPI; q0 += 4) {
+        int qm[4], qn[4];
+        float ev[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = tid + (q0 + u) * 256;
+          qm[u] = em[q0 + u];
+          qn[u] = en[q0 + u];
+          ev[u] = smem[(e / BN) * CS + e % BN];
+        }
+        epilogue_n<4>(a, qm, qn, ev);
+      }
     }
   }
 }

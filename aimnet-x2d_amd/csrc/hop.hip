@@ -153,20 +153,23 @@ __device__ __forceinline__ void tile_body_staged(const float* s_x, const FastDiv
                                                  const float* __restrict__ add0, int64_t add0_ld,
                                                  const float* __restrict__ add1, int64_t add1_ld) {
   using T = typename VecT<VEC>::T;
-  constexpr int kU = 4;  // LDS reads in flight per thread (two items in lockstep measured slower)
+  constexpr int kU = 4;  // LDS reads in flight per thread (8, or two items in lockstep: slower)
   const uint32_t units = nr * upr.d;
   const char* xb = reinterpret_cast<const char*>(s_x);
+  const char* cb = reinterpret_cast<const char*>(cols);
+  const int32_t zb = zslot * 4;
   for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
     const uint32_t rl = fdiv(t, upr);
     const uint32_t ub = (t - rl * upr.d) * VEC * 4;
     const uint32_t r = r0 + rl;
-    const int32_t b = s_ptr[rl] - base, e = s_ptr[rl + 1] - base;
+    // col slots in bytes: (kb + 4j < eb) ? kb + 4j : zb
+    const int32_t bb = (s_ptr[rl] - base) * 4, eb = (s_ptr[rl + 1] - base) * 4;
     T acc = vzero<T>();
-    for (int32_t k = b; k < e; k += kU) {
+    for (int32_t kb = bb; kb < eb; kb += 4 * kU) {
       T v[kU];
 #pragma unroll
       for (int j = 0; j < kU; ++j) {
-        const int32_t off = cols[(k + j < e) ? k + j : zslot];
+        const int32_t off = *reinterpret_cast<const int32_t*>(cb + ((kb + 4 * j < eb) ? kb + 4 * j : zb));
         v[j] = *reinterpret_cast<const T*>(xb + off + ub);
       }
 #pragma unroll
