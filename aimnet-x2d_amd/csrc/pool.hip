@@ -19,6 +19,7 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
 constexpr int kMaxH = 8;
 constexpr int kCap = 1024;  // atoms per molecule kept in LDS (larger molecules use global scratch)
+constexpr int kCapB = 512;  // the same for the backward's fp64 scratch
 
 __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   v = wave_sum(v);
@@ -46,11 +47,11 @@ __device__ __forceinline__ float block_reduce_max(float v, float* red) {
 
 // Per-(head, atom) scratch for one molecule: LDS image [H][kCap] when the molecule fits, else the
 // global [H][N] arrays. Two inlined instantiations keep every access in one address space.
-template <bool LDS, typename T = float>
+template <bool LDS, typename T = float, int CAP = kCap>
 struct Slot {
   T* p;
   int64_t N;
-  __device__ __forceinline__ T& at(int h, int j, int64_t i) const { return LDS ? p[h * kCap + j] : p[h * N + i]; }
+  __device__ __forceinline__ T& at(int h, int j, int64_t i) const { return LDS ? p[h * CAP + j] : p[h * N + i]; }
 };
 
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -141,19 +142,113 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
   }
 }
 
+// ---- Small-molecule fast path (every QM9 molecule): the molecule's x rows are staged in LDS once
+// with 16-B loads (one round trip), then scores, softmax and the pooled sum run from LDS with no
+// further global loads; the softmax of head h is one wave's job (lanes over atoms, no barriers).
+// Same arithmetic per value as the general body above, except the softmax max/sum reductions,
+// which run as one wave butterfly instead of a block reduction (fp32 reassociation only).
+constexpr int kFastAtoms = 64;             // atoms per molecule (one wave's lanes in the softmax)
+constexpr int kFastXBytes = 32 * 1024;     // LDS for the staged rows
+constexpr int kSmemBytes = kFastXBytes + 8 * 1024;
+static_assert(kMaxH * kCap * 4 <= kSmemBytes && kMaxH * kCapB * 8 <= kSmemBytes, "general-path scratch fits");
+
+__device__ __forceinline__ bool fast_ok(int n, int64_t C, int H) {
+  return n <= kFastAtoms && (int64_t)n * C * 4 <= kFastXBytes && H <= kMaxH && (C % 4) == 0;
+}
+
+// stage rows gperm[b .. b+n) of x into xs[n][C] (16-B loads; ldx % 4 == 0 checked by the host)
+__device__ __forceinline__ void stage_rows(const float* __restrict__ x, int64_t ldx, int64_t C, int32_t b, int n,
+                                           const int32_t* __restrict__ gperm, float* xs) {
+  const int c4 = (int)(C / 4);
+  const int tot = n * c4;
+  for (int q = threadIdx.x; q < tot; q += kThreads) {
+    const int j = q / c4, c = (q - j * c4) * 4;
+    const int64_t i = gperm[b + j];
+    *reinterpret_cast<float4*>(xs + j * C + c) = *reinterpret_cast<const float4*>(x + i * ldx + c);
+  }
+}
+
+__device__ __forceinline__ void attn_fwd_fast(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
+                                              const float* __restrict__ W, const float* __restrict__ bias, float tau,
+                                              int H, int32_t b, int n, const int32_t* __restrict__ gperm, int g,
+                                              float* __restrict__ pooled, float* __restrict__ attn,
+                                              float* __restrict__ scores, char* smem) {
+  float* xs = reinterpret_cast<float*>(smem);                      // [n][C]
+  float* sa = reinterpret_cast<float*>(smem + kFastXBytes);        // [kMaxH][kFastAtoms]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  stage_rows(x, ldx, C, b, n, gperm, xs);
+  __syncthreads();
+  // 1) scores: a wave per atom, lanes over channels (same order as attn_fwd_body)
+  for (int j = w; j < n; j += kWaves) {
+    float acc[kMaxH];
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h) acc[h] = 0.f;
+    for (int64_t c = lane; c < C; c += 64) {
+      const float xv = xs[j * C + c];
+#pragma unroll
+      for (int h = 0; h < kMaxH; ++h)
+        if (h < H) acc[h] += xv * W[h * C + c];
+    }
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h) {
+      if (h < H) {
+        const float sc = (wave_sum(acc[h]) + bias[h]) / tau;
+        if (lane == 0) {
+          scores[h * N + gperm[b + j]] = sc;
+          sa[h * kFastAtoms + j] = sc;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // 2) softmax of head h by wave h % kWaves, lanes over atoms
+  for (int h = w; h < H; h += kWaves) {
+    const float v = lane < n ? sa[h * kFastAtoms + lane] : -INFINITY;
+    const float mx = wave_max(v);
+    const float ex = lane < n ? expf(v - mx) : 0.f;
+    const float sum = wave_sum(ex);
+    if (lane < n) {
+      const float a = expf(v - mx) / sum;
+      attn[h * N + gperm[b + lane]] = a;
+      sa[h * kFastAtoms + lane] = a;
+    }
+  }
+  __syncthreads();
+  // 3) pooled[g,c] = (sum_h sum_i a[h,i] x[i,c]) / H
+  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
+    float acc[kMaxH];
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h) acc[h] = 0.f;
+    for (int j = 0; j < n; ++j) {
+      const float xv = xs[j * C + c];
+#pragma unroll
+      for (int h = 0; h < kMaxH; ++h)
+        if (h < H) acc[h] += sa[h * kFastAtoms + j] * xv;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h)
+      if (h < H) sm += acc[h];
+    pooled[(int64_t)g * C + c] = sm / (float)H;
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_attn_fwd(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
                                                         const float* __restrict__ W, const float* __restrict__ bias,
                                                         const float* __restrict__ tau_p, int H,
                                                         const int32_t* __restrict__ gptr,
                                                         const int32_t* __restrict__ gperm, float* __restrict__ pooled,
                                                         float* __restrict__ attn, float* __restrict__ scores) {
-  __shared__ float sa[kMaxH * kCap];
+  __shared__ __attribute__((aligned(16))) char smem[kSmemBytes];
   __shared__ float red[kWaves];
+  float* sa = reinterpret_cast<float*>(smem);  // general path: [kMaxH][kCap] floats
   const int g = blockIdx.x;
   const int32_t b = gptr[g], e = gptr[g + 1];
   const int n = e - b;
   const float tau = *tau_p;
-  if (n <= kCap)
+  if (fast_ok(n, C, H) && (ldx % 4) == 0 && ((uintptr_t)x & 15) == 0)
+    attn_fwd_fast(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, smem);
+  else if (n <= kCap)
     attn_fwd_body<true>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, Slot<true>{sa, N}, red);
   else
     attn_fwd_body<false>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, Slot<false>{attn, N},
@@ -172,7 +267,7 @@ __device__ __forceinline__ void attn_bwd_body(const float* __restrict__ x, int64
                                               const float* __restrict__ dpool, const float* __restrict__ dattn,
                                               float* __restrict__ dx, int64_t lddx, float* __restrict__ dW_part,
                                               float* __restrict__ db_part, float* __restrict__ dtau_part,
-                                              Slot<LDS, double> sds, double* red) {
+                                              Slot<LDS, double, kCapB> sds, double* red) {
   const double invH = 1.0 / (double)H;
   const double dtau_inv = 1.0 / (double)tau;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -250,6 +345,85 @@ __device__ __forceinline__ void attn_bwd_body(const float* __restrict__ x, int64
   }
 }
 
+__device__ __forceinline__ void attn_bwd_fast(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
+                                              const float* __restrict__ W, float tau, int H, int32_t b, int n,
+                                              const int32_t* __restrict__ gperm, int g,
+                                              const float* __restrict__ attn, const float* __restrict__ scores,
+                                              const float* __restrict__ dpool, const float* __restrict__ dattn,
+                                              float* __restrict__ dx, int64_t lddx, float* __restrict__ dW_part,
+                                              float* __restrict__ db_part, float* __restrict__ dtau_part, char* smem,
+                                              double* red) {
+  float* xs = reinterpret_cast<float*>(smem);                                // [n][C]
+  double* sds = reinterpret_cast<double*>(smem + kFastXBytes);               // [kMaxH][kFastAtoms]
+  float* sa = reinterpret_cast<float*>(smem + kFastXBytes + 8 * kMaxH * kFastAtoms);
+  float* ssc = sa + kMaxH * kFastAtoms;
+  const double invH = 1.0 / (double)H;
+  const double dtau_inv = 1.0 / (double)tau;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float* q = dpool + (int64_t)g * C;
+  stage_rows(x, ldx, C, b, n, gperm, xs);
+  for (int t = threadIdx.x; t < H * n; t += kThreads) {
+    const int h = t / n, j = t - h * n;
+    const int64_t i = gperm[b + j];
+    sa[h * kFastAtoms + j] = attn[h * N + i];
+    ssc[h * kFastAtoms + j] = scores[h * N + i];
+  }
+  __syncthreads();
+  // 1) da[h,i] (a wave per atom, lanes over channels, fp64 as in attn_bwd_body)
+  for (int j = w; j < n; j += kWaves) {
+    double acc = 0.0;
+    for (int64_t c = lane; c < C; c += 64) acc += (double)xs[j * C + c] * (double)q[c];
+    const double d = wave_sum_d(acc) * invH;
+    if (lane < H) sds[lane * kFastAtoms + j] = d + (dattn ? (double)dattn[lane * N + gperm[b + j]] : 0.0);
+  }
+  __syncthreads();
+  // 2) ds = a (da - <a, da> / sum a) per head (wave h % kWaves, lanes over atoms); db, dtau partials
+  double dtau_acc = 0.0;
+  for (int h = w; h < H; h += kWaves) {
+    const bool in = lane < n;
+    const double a = in ? (double)sa[h * kFastAtoms + lane] : 0.0;
+    const double da = in ? sds[h * kFastAtoms + lane] : 0.0;
+    double t = wave_sum_d(a * da);
+    const double asum = wave_sum_d(a);
+    if (asum > 0.0) t /= asum;
+    const double ds = a * (da - t);
+    if (in) sds[h * kFastAtoms + lane] = ds;
+    const double dbs = wave_sum_d(ds);
+    if (lane == 0) db_part[(int64_t)g * H + h] = (float)(dbs * dtau_inv);
+    dtau_acc += ds * (in ? (double)ssc[h * kFastAtoms + lane] : 0.0);
+  }
+  dtau_acc = block_reduce_sum_d(dtau_acc, red);
+  if (threadIdx.x == 0) dtau_part[g] = (float)(-dtau_acc * dtau_inv);
+  __syncthreads();
+  // 3) dx_i = (sum_h a[h,i]) q / H + sum_h ds[h,i] W_h / tau ; dW_part[g,h] = sum_i ds[h,i] x_i / tau
+  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
+    const double qc = (double)q[c] * invH;
+    double wc[kMaxH], dw[kMaxH];
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h) {
+      wc[h] = h < H ? (double)W[h * C + c] : 0.0;
+      dw[h] = 0.0;
+    }
+    for (int j = 0; j < n; ++j) {
+      const double xv = xs[j * C + c];
+      double asum = 0.0, dsw = 0.0;
+#pragma unroll
+      for (int h = 0; h < kMaxH; ++h) {
+        if (h < H) {
+          const double ds = sds[h * kFastAtoms + j];
+          asum += sa[h * kFastAtoms + j];
+          dsw += ds * wc[h];
+          dw[h] += ds * xv;
+        }
+      }
+      dx[gperm[b + j] * lddx + c] = (float)(asum * qc + dsw * dtau_inv);
+    }
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h)
+      if (h < H) dW_part[((int64_t)g * H + h) * C + c] = (float)(dw[h] * dtau_inv);
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_attn_bwd(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
                                                         const float* __restrict__ W, const float* __restrict__ tau_p,
                                                         int H, const int32_t* __restrict__ gptr,
@@ -260,18 +434,22 @@ __global__ __launch_bounds__(kThreads) void k_attn_bwd(const float* __restrict__
                                                         int64_t lddx, float* __restrict__ dW_part,
                                                         float* __restrict__ db_part, float* __restrict__ dtau_part,
                                                         double* __restrict__ ds_glob) {
-  __shared__ double sds[kMaxH * kCap];
+  __shared__ __attribute__((aligned(16))) char smem[kSmemBytes];
   __shared__ double red[kWaves];
+  double* sds = reinterpret_cast<double*>(smem);  // general path: [kMaxH][kCapB] doubles
   const int g = blockIdx.x;
   const int32_t b = gptr[g], e = gptr[g + 1];
   const int n = e - b;
   const float tau = *tau_p;
-  if (n <= kCap)
+  if (fast_ok(n, C, H) && (ldx % 4) == 0 && ((uintptr_t)x & 15) == 0)
+    attn_bwd_fast(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part, db_part,
+                  dtau_part, smem, red);
+  else if (n <= kCapB)
     attn_bwd_body<true>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part, db_part,
-                        dtau_part, Slot<true, double>{sds, N}, red);
+                        dtau_part, Slot<true, double, kCapB>{sds, N}, red);
   else
     attn_bwd_body<false>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part,
-                         db_part, dtau_part, Slot<false, double>{ds_glob, N}, red);
+                         db_part, dtau_part, Slot<false, double, kCapB>{ds_glob, N}, red);
 }
 
 // One wave per output value (dW[h,c], db[h], dtau): lanes take molecules g = lane, lane+64, ... and

@@ -14,16 +14,26 @@ dev = "cuda"
 
 
 def bench(fn, it=50):
-    for _ in range(5):
-        fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    """us per launch, measured on a HIP graph of `it` back-to-back launches (device time incl. the
+    ~1.6 us graph-node floor; eager Python launches would measure the host instead)."""
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
     torch.cuda.synchronize()
-    s.record()
-    for _ in range(it):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / it * 1e3
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(it):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(5):
+        g.replay()
+    t1.record()
+    t1.synchronize()
+    return t0.elapsed_time(t1) / (5 * it) * 1e3
 
 
 def run(M, N, K, layout, label, splits=0, torch_ref=True, counters=True):
@@ -44,8 +54,7 @@ def run(M, N, K, layout, label, splits=0, torch_ref=True, counters=True):
     wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
     ws = torch.empty(wsb // 4 + 1, device=dev)
     a.workspace, a.workspace_bytes = ws.data_ptr(), wsb
-    st = torch.cuda.current_stream().cuda_stream
-    t_ours = bench(lambda: lib.aimx_gemm(ctypes.byref(a), st))
+    t_ours = bench(lambda: lib.aimx_gemm(ctypes.byref(a), torch.cuda.current_stream().cuda_stream))
     Am = A if layout[0] == "N" else A.t()
     Bm = B if layout[1] == "N" else B.t()
     t_torch = bench(lambda: torch.mm(Am, Bm, out=C)) if torch_ref else float("nan")

@@ -1,0 +1,75 @@
+"""Device time of the c2 train step's sections, each captured as its own HIP graph (no profiler):
+forward(+loss), forward+backward, and the full step with clip+Adam. Differences give the backward
+and optimizer shares without the per-kernel inflation a kernel trace adds.
+
+usage: python tools/step_sections.py [--config c2] [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aimnet-x2d_amd")]
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    from aimx.optim import FusedAdam
+    dev = torch.device("cuda:0")
+    cfg = bench.CONFIGS[a.config]
+    batches = bench.make_batches(cfg, 2, 1234, dev, pad=True)
+    model = bench.build_model(cfg, dev)
+    B = cfg["batch"]
+    loss_fn = torch.nn.L1Loss()
+    opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
+    static = batches[0].clone()
+
+    def fwd():
+        out, _, _ = model(*static.model_args())
+        return loss_fn(out[:B], static.targets[:B])
+
+    sections = {
+        "forward+loss": lambda: fwd(),
+        "forward+backward": lambda: fwd().backward(),
+        "full step": lambda: (fwd().backward(), opt.step()),
+    }
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            fwd().backward()
+            opt.step()
+    torch.cuda.current_stream().wait_stream(side)
+    res = {}
+    for name, fn in sections.items():
+        opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(a.reps):
+            g.replay()
+        t1.record()
+        t1.synchronize()
+        res[name] = round(t0.elapsed_time(t1) / a.reps * 1e3, 1)
+        del g
+    res["backward"] = round(res["forward+backward"] - res["forward+loss"], 1)
+    res["clip+adam"] = round(res["full step"] - res["forward+backward"], 1)
+    print(json.dumps({"unit": "us", **res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
