@@ -251,6 +251,35 @@ def test_gemm_weight_grad_forced_splits(splits):
     assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
 
 
+def test_wgrad_grouped_matches_fp64():
+    """aimx_wgrad_grouped over the stack's shapes (76 x 76 / 152 x 304 with the bias column, long
+    K), a short-K FFN shape, K = 1 and odd widths: dW = dY^T X and db = sum_k dY against fp64,
+    deterministic, counters left at zero."""
+    from aimx import ops, _lib
+    g = torch.Generator().manual_seed(11)
+    shapes = [(76, 76, 9170, True), (152, 304, 9170, True), (76, 76, 4099, False), (256, 256, 520, True),
+              (36, 36, 1, True), (38, 38, 777, True), (8, 12, 64, False)]
+    probs, refs = [], []
+    for M, N, K, bias in shapes:
+        dy = torch.randn(K, M, generator=g)
+        x = torch.randn(K, N, generator=g)
+        dw = torch.full((M, N), float("nan"), device=DEV)
+        db = torch.full((M,), float("nan"), device=DEV) if bias else None
+        probs.append((dy.to(DEV), x.to(DEV), dw, db))
+        refs.append((dy.double().t() @ x.double(), dy.double().sum(0) if bias else None))
+    ops.wgrad_grouped(probs)
+    outs = [(p[2].clone(), None if p[3] is None else p[3].clone()) for p in probs]
+    for (dw, db), (rw, rb) in zip(outs, refs):
+        assert torch.isfinite(dw).all()
+        assert (dw.cpu().double() - rw).abs().max().item() / rw.abs().max().item() < 2e-6
+        if rb is not None:
+            assert (db.cpu().double() - rb).abs().max().item() / rb.abs().max().item() < 2e-6
+    ops.wgrad_grouped(probs)
+    for p, (dw, db) in zip(probs, outs):
+        assert torch.equal(p[2], dw) and (db is None or torch.equal(p[3], db))
+    assert int(_lib.counters(DEV).abs().sum().item()) == 0
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_gemm_ones_column_bias_grad_and_splitk(fused):
     C, col, _, ref, Am = _gemm(76, 304, 9170, "TN", ones=True, splits=24, fused_reduce=fused)

@@ -2,7 +2,10 @@
 forward(+loss), forward+backward, and the full step with clip+Adam. Differences give the backward
 and optimizer shares without the per-kernel inflation a kernel trace adds.
 
-usage: python tools/step_sections.py [--config c2] [--reps 20]
+usage: python tools/step_sections.py [--config c2] [--reps 20] [--env "A=1 B=2" ...]
+With --env, the whole-step graph is also captured under each environment setting (AIMX_* knobs
+are read at launch/capture time) and all variants are replayed interleaved, so an A/B between
+code paths runs on one box in one process.
 """
 import argparse
 import json
@@ -21,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--env", action="append", default=[])
     a = ap.parse_args()
     from aimx.optim import FusedAdam
     dev = torch.device("cuda:0")
@@ -69,6 +73,40 @@ def main():
     res["backward"] = round(res["forward+backward"] - res["forward+loss"], 1)
     res["clip+adam"] = round(res["full step"] - res["forward+backward"], 1)
     print(json.dumps({"unit": "us", **res}), flush=True)
+    if a.env:
+        variants = [""] + a.env
+        graphs = []
+        for ev in variants:
+            kv = [x.split("=") for x in ev.split()]
+            for k, v in kv:
+                os.environ[k] = v
+            with torch.cuda.stream(side):
+                opt.zero_grad(set_to_none=True)
+                fwd().backward()
+                opt.step()
+            torch.cuda.current_stream().wait_stream(side)
+            opt.zero_grad(set_to_none=True)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fwd().backward()
+                opt.step()
+            for k, _ in kv:
+                os.environ.pop(k, None)
+            graphs.append(g)
+        tot = [0.0] * len(graphs)
+        for rnd in range(5):
+            for gi, g in enumerate(graphs):
+                g.replay()
+                torch.cuda.synchronize()
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
+                for _ in range(a.reps):
+                    g.replay()
+                t1.record()
+                t1.synchronize()
+                tot[gi] += t0.elapsed_time(t1) / a.reps * 1e3 / 5
+        print(json.dumps({"unit": "us", "ab_full_step": {v or "baseline": round(t, 1) for v, t in zip(variants, tot)}}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,59 @@
+"""Graph-timed aimx_wgrad_grouped on the c2 stack's 15 weight-gradient problems (3 layers x
+[dW_ig 152 x 304 + bias, 4 x dW_mlp 76 x 76 + bias], K = 9170)."""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "aimnet-x2d_amd")]
+from aimx import _lib  # noqa: E402
+
+
+def main():
+    lib = _lib.load()
+    dev = torch.device("cuda")
+    K = 9170
+    shapes = [(152, 304)] + [(76, 76)] * 4
+    shapes = shapes * 3
+    bufs = []
+    arr = (_lib.WgradProblem * len(shapes))()
+    for i, (M, N) in enumerate(shapes):
+        dy, x = torch.randn(K, M, device=dev), torch.randn(K, N, device=dev)
+        dw, db = torch.empty(M, N, device=dev), torch.empty(M, device=dev)
+        bufs += [dy, x, dw, db]
+        arr[i].dY, arr[i].ld_dy, arr[i].X, arr[i].ld_x = dy.data_ptr(), M, x.data_ptr(), N
+        arr[i].dW, arr[i].ld_dw, arr[i].col_out = dw.data_ptr(), N, db.data_ptr()
+        arr[i].M, arr[i].N, arr[i].K = M, N, K
+    n = len(shapes)
+    ws = torch.empty(lib.aimx_wgrad_grouped_workspace_bytes(arr, n) // 4 + 1, device=dev)
+    cnt = _lib.counters(dev)
+    res = {}
+    for path in ("current",):
+        fn = lambda: lib.aimx_wgrad_grouped(arr, n, ws.data_ptr(), ws.numel() * 4, cnt.data_ptr(), _lib.N_COUNTERS,
+                                            torch.cuda.current_stream().cuda_stream)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(10):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(5):
+            g.replay()
+        t1.record()
+        t1.synchronize()
+        res[path + "_us"] = round(t0.elapsed_time(t1) / 50 * 1e3, 1)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
