@@ -70,6 +70,22 @@ def collate(mols, max_hops, hops=None):
     return {"edges": edges, "feats": feats, "batch": batch, "n_atoms": n_atoms}
 
 
+def blob_layout(fields):
+    """Byte layout of DeviceBatch fields [(dtype, shape)]: 256-byte aligned offsets.
+    Returns ([(offset, dtype, shape)], total bytes)."""
+    out, off = [], 0
+    for dt, shape in fields:
+        out.append((off, np.dtype(dt), tuple(shape)))
+        off += (int(np.prod(shape)) * np.dtype(dt).itemsize + 255) // 256 * 256
+    return out, max(off, 256)
+
+
+def batch_fields(n_rows, e_rows, g_rows, n_tasks):
+    """DeviceBatch field (dtype, shape) list: 4 feature columns, edges, batch, charges, targets."""
+    return ([(np.int64, (n_rows,))] * len(FEATURE_KEYS) + [(np.int64, (e_rows, 2)), (np.int64, (n_rows,)),
+                                                           (np.float32, (g_rows,)), (np.float32, (g_rows, n_tasks))])
+
+
 class DeviceBatch:
     """A collated batch resident in HBM, in the reference trainer's argument layout.
 
@@ -87,12 +103,8 @@ class DeviceBatch:
         parts = [np.ascontiguousarray(col["feats"][:, i]).astype(np.int64) for i in range(len(FEATURE_KEYS))]
         parts += [np.ascontiguousarray(col["edges"], np.int64), np.ascontiguousarray(col["batch"], np.int64),
                   np.ascontiguousarray(tc, np.float32), np.ascontiguousarray(tg, np.float32)]
-        self._layout = []
-        off = 0
-        for a in parts:
-            self._layout.append((off, a.dtype, a.shape))
-            off += (a.nbytes + 255) // 256 * 256
-        host = np.zeros(max(off, 256), np.uint8)
+        self._layout, off = blob_layout([(a.dtype, a.shape) for a in parts])
+        host = np.zeros(off, np.uint8)
         for (o, _, _), a in zip(self._layout, parts):
             host[o:o + a.nbytes] = a.view(np.uint8).reshape(-1)
         self._blob = torch.from_numpy(host).to(device)
@@ -100,6 +112,19 @@ class DeviceBatch:
         self.tetrahedral = torch.empty(0, 4, dtype=torch.long, device=device)
         self.cis = torch.empty(0, 2, dtype=torch.long, device=device)
         self.trans = torch.empty(0, 2, dtype=torch.long, device=device)
+
+    @classmethod
+    def from_blob(cls, blob, layout, num_graphs, num_atoms):
+        """Wrap a device byte buffer already holding the fields at `layout` (blob_layout())."""
+        b = cls.__new__(cls)
+        b.num_graphs, b.num_atoms = int(num_graphs), int(num_atoms)
+        b._layout, b._blob = list(layout), blob
+        b._bind()
+        dev = blob.device
+        b.tetrahedral = torch.empty(0, 4, dtype=torch.long, device=dev)
+        b.cis = torch.empty(0, 2, dtype=torch.long, device=dev)
+        b.trans = torch.empty(0, 2, dtype=torch.long, device=dev)
+        return b
 
     def _bind(self):
         views = []

@@ -1,0 +1,300 @@
+"""Native batch feed: the C++ batch builder (libaimx_host.so, include/aimx_host.h) behind Python.
+
+Replaces the reference's host input path for the hot path:
+  * src/datasets/features.py:82-150  multi-hop BFS pair lists (per molecule)
+  * src/datasets/molecular.py:339-458 MyBatch.from_data_list (collate)
+  * trainer.py:123-131 per-tensor `.to(device)` copies
+with one native plan+write per batch straight into a pinned host blob in DeviceBatch layout and ONE
+async host->device copy of that blob on a copy stream. `BatchFeeder` keeps `depth` batches in
+flight from a background thread (ctypes releases the GIL inside the native calls), so collation
+and the PCIe copy overlap the GPU step.
+
+Everything here is bit-identical to aimx.data (the Python restatement) and to the reference's own
+BFS + collate fixtures (tests/test_host_collate.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import queue
+import threading
+
+import numpy as np
+import torch
+
+from . import data as adata
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+HOST_LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libaimx_host.so")
+
+c_i64, c_i32, c_ptr = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+_ERR = {-1: "invalid argument", -2: "capacity too small", -3: "out of host memory", -4: "write without a plan"}
+
+
+class HostError(RuntimeError):
+    pass
+
+
+class CollateOut(ctypes.Structure):
+    _fields_ = [("feat", c_ptr * 8), ("edges", c_ptr), ("batch", c_ptr), ("total_charges", c_ptr),
+                ("targets", c_ptr), ("n_atoms", c_ptr), ("n_max", c_i64), ("e_max", c_i64), ("pad_mols", c_i32)]
+
+
+_lib = None
+
+
+def load_host():
+    """Load libaimx_host.so (built by `make -C aimnet-x2d_amd/csrc`); raises HostError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(HOST_LIB_PATH):
+        raise HostError(f"{HOST_LIB_PATH} not built (run make -C aimnet-x2d_amd/csrc)")
+    lib = ctypes.CDLL(HOST_LIB_PATH)
+    lib.aimx_host_version.restype = ctypes.c_char_p
+    lib.aimx_bfs_multi_hop.restype = c_i64
+    lib.aimx_bfs_multi_hop.argtypes = [c_i32, c_ptr, c_i64, c_i32, c_ptr, c_i64, c_ptr]
+    lib.aimx_store_create.restype = c_i32
+    lib.aimx_store_create.argtypes = [c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_i32, c_ptr, c_i32, c_i32,
+                                      ctypes.POINTER(c_ptr)]
+    lib.aimx_store_destroy.argtypes = [c_ptr]
+    lib.aimx_store_num_molecules.restype = c_i64
+    lib.aimx_store_num_molecules.argtypes = [c_ptr]
+    lib.aimx_store_num_atoms.restype = c_i64
+    lib.aimx_store_num_atoms.argtypes = [c_ptr, c_i64]
+    lib.aimx_collator_create.restype = c_i32
+    lib.aimx_collator_create.argtypes = [c_i32, c_i32, ctypes.POINTER(c_ptr)]
+    lib.aimx_collator_destroy.argtypes = [c_ptr]
+    lib.aimx_collate_plan.restype = c_i32
+    lib.aimx_collate_plan.argtypes = [c_ptr, c_ptr, c_ptr, c_i64, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]
+    lib.aimx_collate_write.restype = c_i32
+    lib.aimx_collate_write.argtypes = [c_ptr, ctypes.POINTER(CollateOut)]
+    _lib = lib
+    return lib
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise HostError(f"aimx_host {what}: {_ERR.get(int(rc), rc)}")
+    return rc
+
+
+def _p(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+def bfs_multi_hop(n_atoms, bonds, max_hops):
+    """Native restatement of features.py:97-150; same return shape as aimx.data.bfs_multi_hop."""
+    lib = load_host()
+    b = np.ascontiguousarray(np.asarray(bonds).reshape(-1, 2), np.int32)
+    counts = np.zeros(max(max_hops, 1), np.int64)
+    cap = max(64, 4 * n_atoms * max(max_hops, 1))
+    while True:
+        pairs = np.empty((cap, 2), np.int32)
+        tot = _check(lib.aimx_bfs_multi_hop(n_atoms, _p(b), b.shape[0], max_hops, pairs.ctypes.data, cap,
+                                            counts.ctypes.data), "bfs")
+        if tot <= cap:
+            break
+        cap = tot
+    out, o = [], 0
+    for h in range(max_hops):
+        c = int(counts[h])
+        out.append(pairs[o:o + c].T.copy())
+        o += c
+    return out
+
+
+class HostStore:
+    """Molecule records in native memory (the fields collate reads from each reference Data object).
+
+    precompute_hops > 0 caches every molecule's hop pairs at creation (the reference stores
+    multi_hop_edges in its datasets, features.py:416-431); 0 runs the BFS inside each collate."""
+
+    def __init__(self, n_atoms, bonds_per_mol, feats, targets=None, total_charge=None, precompute_hops=0,
+                 threads=4):
+        lib = load_host()
+        n_atoms = np.asarray(n_atoms, np.int64)
+        nb = np.array([len(b) for b in bonds_per_mol], np.int64)
+        self._atom_ptr = np.concatenate([[0], np.cumsum(n_atoms)]).astype(np.int64)
+        self._bond_ptr = np.concatenate([[0], np.cumsum(nb)]).astype(np.int64)
+        bonds = (np.concatenate([np.asarray(b, np.int32).reshape(-1, 2) for b in bonds_per_mol])
+                 if len(bonds_per_mol) else np.zeros((0, 2), np.int32))
+        self._init(lib, n_atoms.shape[0], bonds, feats, targets, total_charge, precompute_hops, threads)
+
+    @classmethod
+    def from_arrays(cls, atom_ptr, bond_ptr, bonds, feats, targets=None, total_charge=None, precompute_hops=0,
+                    threads=4):
+        s = cls.__new__(cls)
+        s._atom_ptr = np.ascontiguousarray(atom_ptr, np.int64)
+        s._bond_ptr = np.ascontiguousarray(bond_ptr, np.int64)
+        s._init(load_host(), s._atom_ptr.shape[0] - 1, bonds, feats, targets, total_charge, precompute_hops, threads)
+        return s
+
+    @classmethod
+    def from_qm9_asset(cls, asset, precompute_hops=0, threads=4):
+        bonds = np.stack([asset.bi, asset.bj], 1)
+        return cls.from_arrays(asset.atom_off, asset.bond_off, bonds, asset.feats, asset.targets,
+                               asset.total_charge, precompute_hops, threads)
+
+    @classmethod
+    def from_molecules(cls, mols, targets=None, total_charge=None, precompute_hops=0, threads=4):
+        """mols: list of (n_atoms, bonds [B,2], feats [n,F]) as produced by aimx.synth."""
+        feats = (np.concatenate([np.asarray(m[2]).reshape(m[0], -1) for m in mols])
+                 if mols else np.zeros((0, len(adata.FEATURE_KEYS)), np.int32))
+        return cls([m[0] for m in mols], [m[1] for m in mols], feats, targets, total_charge, precompute_hops, threads)
+
+    def _init(self, lib, n_mols, bonds, feats, targets, total_charge, precompute_hops, threads):
+        self._lib = lib
+        bonds = np.ascontiguousarray(np.asarray(bonds).reshape(-1, 2), np.int32)
+        feats = np.ascontiguousarray(feats, np.int32)
+        self.n_feat = feats.shape[1] if feats.ndim == 2 else len(adata.FEATURE_KEYS)
+        tg = None if targets is None else np.ascontiguousarray(np.asarray(targets, np.float32).reshape(n_mols, -1))
+        self.n_tasks = 0 if tg is None else tg.shape[1]
+        tc = None if total_charge is None else np.ascontiguousarray(total_charge, np.float32)
+        h = c_ptr()
+        _check(lib.aimx_store_create(n_mols, self._atom_ptr.ctypes.data, self._bond_ptr.ctypes.data, _p(bonds),
+                                     _p(feats), self.n_feat, _p(tg), self.n_tasks, _p(tc), int(precompute_hops),
+                                     int(threads), ctypes.byref(h)), "store_create")
+        self._h = h
+        self.n_mols = int(n_mols)
+        self.n_atoms = np.diff(self._atom_ptr)
+
+    def __len__(self):
+        return self.n_mols
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.aimx_store_destroy(h)
+            self._h = None
+
+
+class HostCollator:
+    """One native collator (persistent worker pool). Not thread-safe: one batch at a time."""
+
+    def __init__(self, max_hops, threads=4):
+        self._lib = load_host()
+        h = c_ptr()
+        _check(self._lib.aimx_collator_create(int(max_hops), int(threads), ctypes.byref(h)), "collator_create")
+        self._h = h
+        self.max_hops = int(max_hops)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.aimx_collator_destroy(h)
+            self._h = None
+
+    def plan(self, store, idx):
+        self._idx = np.ascontiguousarray(idx, np.int64)
+        n, e = c_i64(), c_i64()
+        _check(self._lib.aimx_collate_plan(self._h, store._h, _p(self._idx), self._idx.shape[0], ctypes.byref(n),
+                                           ctypes.byref(e)), "collate_plan")
+        self._store = store
+        return int(n.value), int(e.value)
+
+    def write(self, feat_ptrs, edges, batch, total_charges=None, targets=None, n_atoms=None, n_max=0, e_max=0,
+              pad_mols=0):
+        o = CollateOut()
+        for k, p in enumerate(feat_ptrs):
+            o.feat[k] = p
+        o.edges, o.batch, o.total_charges, o.targets, o.n_atoms = edges, batch, total_charges, targets, n_atoms
+        o.n_max, o.e_max, o.pad_mols = int(n_max), int(e_max), int(pad_mols)
+        _check(self._lib.aimx_collate_write(self._h, ctypes.byref(o)), "collate_write")
+
+    def collate(self, store, idx):
+        """Numpy arrays in aimx.data.collate's format (plus targets / total charges)."""
+        n, e = self.plan(store, idx)
+        g = self._idx.shape[0]
+        feats = np.empty((store.n_feat, n), np.int64)
+        edges = np.empty((e, 2), np.int64)
+        batch = np.empty(n, np.int64)
+        tc = np.empty(g, np.float32)
+        tg = np.empty((g, max(store.n_tasks, 1)), np.float32)
+        na = np.empty(g, np.int64)
+        self.write([feats[k].ctypes.data for k in range(store.n_feat)], edges.ctypes.data, batch.ctypes.data,
+                   tc.ctypes.data, tg.ctypes.data if store.n_tasks else None, na.ctypes.data)
+        return {"edges": edges, "feats": feats.T.copy(), "batch": batch, "n_atoms": na, "total_charges": tc,
+                "targets": tg[:, :store.n_tasks]}
+
+    def collate_blob(self, store, idx, pinned=True, n_max=0, e_max=0, pad_mols=0, n_tasks=None):
+        """Plan + write one batch into a (pinned) host byte tensor in DeviceBatch layout.
+        Returns (blob uint8 tensor, layout, G_rows, N_rows, real (G, N, E))."""
+        n, e = self.plan(store, idx)
+        g = self._idx.shape[0]
+        pad = n_max > 0
+        nr, er, gr = (n_max, e_max, g + pad_mols) if pad else (n, e, g)
+        t = store.n_tasks if n_tasks is None else n_tasks
+        layout, nbytes = adata.blob_layout(adata.batch_fields(nr, er, gr, max(t, 1)))
+        blob = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
+        base = blob.data_ptr()
+        ptr = [base + o for o, _, _ in layout]
+        if t == 0:  # no targets in the store: zero the target field
+            o, dt, shape = layout[-1]
+            blob[o:o + int(np.prod(shape)) * 4].zero_()
+        self.write(ptr[:4], ptr[4], ptr[5], ptr[6], ptr[7] if t else None, None, n_max if pad else 0,
+                   e_max if pad else 0, pad_mols if pad else 0)
+        return blob, layout, gr, nr, (g, n, e)
+
+
+class BatchFeeder:
+    """Background native collation + async H2D copies, `depth` batches ahead of the consumer.
+
+    batches: iterable of molecule-index arrays. Yields DeviceBatch objects whose copy has been
+    enqueued on the feeder's copy stream; the consumer's current stream waits on it (event), so
+    the step never reads a half-copied batch and never blocks the host on the copy. Padding to
+    static shapes (n_max/e_max/pad_mols) makes the batches replayable by one captured HIP graph.
+    """
+
+    def __init__(self, store, index_batches, max_hops, device, depth=3, threads=4, n_max=0, e_max=0, pad_mols=0):
+        self.store, self.device = store, torch.device(device)
+        self.collator = HostCollator(max_hops, threads)
+        self.pad = (n_max, e_max, pad_mols)
+        self.stream = torch.cuda.Stream(self.device)
+        self._q = queue.Queue(maxsize=depth)
+        self._it = iter(index_batches)
+        self._stop = False
+        self._err = None
+        self._th = threading.Thread(target=self._run, daemon=True)
+        self._th.start()
+
+    def _run(self):
+        try:
+            for idx in self._it:
+                if self._stop:
+                    break
+                blob, layout, gr, nr, real = self.collator.collate_blob(self.store, idx, True, *self.pad)
+                with torch.cuda.stream(self.stream):
+                    dev = blob.to(self.device, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                b = adata.DeviceBatch.from_blob(dev, layout, gr, nr)
+                b.real_graphs, b.real_atoms, b.real_edges = real
+                self._q.put((b, ev, blob))
+        except Exception as exc:  # surfaced to the consumer
+            self._err = exc
+        self._q.put(None)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        item = self._q.get()
+        if item is None:
+            if self._err is not None:
+                raise self._err
+            raise StopIteration
+        b, ev, blob = item
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        b._host_blob = blob  # keep the pinned source alive until the copy has been consumed
+        # the consumer's stream must not reuse the device blob before its own work is done
+        b._blob.record_stream(torch.cuda.current_stream(self.device))
+        return b
+
+    def close(self):
+        self._stop = True
+        while self._th.is_alive():
+            try:
+                self._q.get(timeout=0.1)
+            except queue.Empty:
+                pass
