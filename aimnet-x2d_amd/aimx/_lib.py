@@ -44,6 +44,7 @@ class GemmArgs(ctypes.Structure):
         ("ones_col", c_i32), ("col_out", c_ptr),
         ("splits", c_i32), ("workspace", c_ptr), ("workspace_bytes", c_size),
         ("counters", c_ptr), ("n_counters", c_i64),
+        ("zc_rowptr", c_ptr), ("zc_rows", c_i64), ("zc_chunks", c_i32), ("zc_width", c_i64), ("zc_dim", c_i32),
     ]
 
 
@@ -87,7 +88,8 @@ class CsrSpec(ctypes.Structure):
 
 class WgradProblem(ctypes.Structure):
     _fields_ = [("dY", c_ptr), ("ld_dy", c_i64), ("X", c_ptr), ("ld_x", c_i64), ("dW", c_ptr), ("ld_dw", c_i64),
-                ("col_out", c_ptr), ("M", c_i64), ("N", c_i64), ("K", c_i64)]
+                ("col_out", c_ptr), ("M", c_i64), ("N", c_i64), ("K", c_i64),
+                ("zc_rowptr", c_ptr), ("zc_rows", c_i64), ("zc_chunks", c_i32), ("zc_width", c_i64)]
 
 
 class AdamTensor(ctypes.Structure):

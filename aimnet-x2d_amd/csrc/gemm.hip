@@ -184,6 +184,24 @@ __device__ __forceinline__ floatx4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t vof
   return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+// Extent of the non-empty hop chunks (AimxGemmArgs.zc_*): E = width * (1 + c), c = 1 + the last
+// chunk holding an edge. The row pointers are wave-uniform, so these are a handful of scalar loads.
+__device__ __forceinline__ int zc_extent(const int32_t* rp, int64_t rows, int chunks, int64_t width) {
+  int c = 0;
+  for (int j = 0; j < chunks; ++j)
+    if (rp[(int64_t)(j + 1) * rows] > rp[(int64_t)j * rows]) c = j + 1;
+  return (int)(width * (1 + c));
+}
+
+// Plain zero store of one BM x BN output tile (zc_dim 1: a tile wholly inside the empty chunks).
+template <int BM, int BN>
+__device__ __forceinline__ void zero_tile(const AimxGemmArgs& a, int m0, int n0, int M, int Nreal) {
+  for (int e = threadIdx.x; e < BM * BN; e += 256) {
+    const int m = m0 + e / BN, n = n0 + e % BN;
+    if (m < M && n < Nreal) a.C[(int64_t)m * a.ldc + n] = 0.f;
+  }
+}
+
 // V4: both operands staged with 16-byte buffer loads (one dwordx4 moves 1 KiB per wave; dword
 // loads are address-rate bound at a quarter of that). Requires the contiguous extent of each
 // operand to be a multiple of 4 floats and 16-byte aligned rows (checked by the host), so a float4
@@ -208,7 +226,16 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   const int Nreal = a.ones_col ? N - 1 : N;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * kchunk;
-  const int kend = min((int)a.K, kbeg + kchunk);
+  int kend = min((int)a.K, kbeg + kchunk);
+  if (a.zc_rowptr) {  // empty hop chunks: stop the k loop at their start, or skip whole zero tiles
+    const int zE = zc_extent(a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width);
+    if (a.zc_dim == 0) {
+      kend = min(kend, zE);
+    } else if (n0 >= zE && !(a.ones_col && n0 + BN > Nreal)) {  // never the tile of the ones column
+      if (blockIdx.z == 0) zero_tile<BM, BN>(a, m0, n0, M, Nreal);
+      return;
+    }
+  }
   const __amdgpu_buffer_rsrc_t ra_ = make_rsrc(a.A, a_bytes);
   const __amdgpu_buffer_rsrc_t rb_ = make_rsrc(a.B, b_bytes);
   const uint32_t sam = (uint32_t)a.sam, sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
@@ -528,6 +555,13 @@ __device__ __forceinline__ void wgrad_block(const AimxGemmArgs& a, int kchunk, u
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = (int)a.M, N = (int)a.N;
   const int m0 = bx * 32, n0 = by * 32;
+  if (a.zc_rowptr) {  // a tile wholly inside the empty hop chunks: zero gradient, no work
+    const int Nreal = a.ones_col ? N - 1 : N;
+    if (n0 >= zc_extent(a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width) && !(a.ones_col && n0 + 32 > Nreal)) {
+      if (bz == 0) zero_tile<32, 32>(a, m0, n0, M, Nreal);
+      return;
+    }
+  }
   const int kb = bz * kchunk;
   const int kend = min((int)a.K, kb + kchunk);
   const int kw = kchunk / 4;  // multiple of 4
@@ -734,6 +768,11 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const WgradTable t, float
   a.dact_kind = -1;
   a.ones_col = pr.col_out ? 1 : 0;
   a.col_out = pr.col_out;
+  a.zc_rowptr = pr.zc_rowptr;
+  a.zc_rows = pr.zc_rows;
+  a.zc_chunks = pr.zc_chunks;
+  a.zc_width = pr.zc_width;
+  a.zc_dim = 1;
   wgrad_block(a, t.kchunk[q], t.a_bytes[q], t.b_bytes[q], tile / t.tiles_y[q], tile % t.tiles_y[q], z, t.splits[q],
               tile, nt, ws + t.ws_off[q], counters ? counters + t.cnt_off[q] : nullptr, red);
 }
@@ -865,6 +904,13 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   if (a.ones_col && (!a.col_out || a.N < 1)) return AIMX_EARG;
   if ((a.mask_out || a.mask_in) && !(a.drop_p < 1.f)) return AIMX_EARG;
   if (a.mask_out && !a.drop_seed) return AIMX_EARG;
+  if (a.zc_rowptr) {  // trimming: sane chunk geometry; zc_dim 1 only with a plain-store epilogue
+    if (a.zc_chunks < 0 || a.zc_rows < 0 || a.zc_width < 0 || (a.zc_dim != 0 && a.zc_dim != 1)) return AIMX_EARG;
+    if (a.zc_width * (a.zc_chunks + 1) >= (1ll << 31)) return AIMX_EARG;
+    if (a.zc_dim == 1 && (a.beta != 0.f || a.bias || a.res[0] || a.res[1] || a.res[2] || a.act_ncols > 0 ||
+                          a.pre || a.dact_pre || a.mask_in || a.mask_out))
+      return AIMX_EARG;
+  }
   // operand layouts: each operand must be contiguous along k or along m/n; byte extents < 2 GiB
   if (!(a.sak == 1 || a.sam == 1) || !(a.sbk == 1 || a.sbn == 1)) return AIMX_EARG;
   const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
@@ -930,6 +976,7 @@ WgPlan wg_plan(const AimxWgradProblem& p) {
 bool wg_valid(const AimxWgradProblem& p) {
   if (p.M < 1 || p.N < 1 || p.K < 0 || !p.dY || !p.X || !p.dW) return false;
   if (p.ld_dy < p.M || p.ld_x < p.N || p.ld_dw < p.N) return false;
+  if (p.zc_rowptr && (p.zc_chunks < 0 || p.zc_rows < 0 || p.zc_width < 0)) return false;
   const int64_t a_ext = 4 * ((p.K - 1) * p.ld_dy + p.M), b_ext = 4 * ((p.K - 1) * p.ld_x + p.N);
   return p.K == 0 || (a_ext < (1ll << 31) && b_ext < (1ll << 31));
 }

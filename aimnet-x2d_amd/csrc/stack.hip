@@ -130,6 +130,23 @@ int gather(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, in
                                  add0_ld, add1, add1_ld, (aimx_stream_t)s);
 }
 
+// Empty hop chunks (AimxGemmArgs.zc_*): every GEMM over F's columns trims the all-zero chunks the
+// reference's hop leaves (layers.py:154), detected on the device from the forward CSR row pointers.
+// AIMX_NO_ZC=1 disables it (A/B experiments).
+bool zc_on() {
+  static const bool off = getenv("AIMX_NO_ZC") != nullptr;
+  return !off;
+}
+
+void set_zc(AimxGemmArgs& a, const AimxShellStack* s, int dim) {
+  if (!zc_on() || !s->fwd_rowptr) return;
+  a.zc_rowptr = s->fwd_rowptr;
+  a.zc_rows = s->N;
+  a.zc_chunks = (int32_t)s->num_hops;
+  a.zc_width = s->D;
+  a.zc_dim = dim;
+}
+
 bool valid(const AimxShellStack* s) {
   if (!s || s->N < 0 || s->D < 1 || s->num_hops < 1 || s->num_layers < 1 || s->num_mlp < 1) return false;
   if (s->mode_single && (s->num_layers != 1 || s->use_pc)) return false;
@@ -182,6 +199,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
     // 3) [u | g] = F [Wi ; Wg]^T + [bi ; bg], a0 = act(u)
     {
       AimxGemmArgs a = linear_fwd(N, K, D2, F, K, s->w_ig[l], s->UG[l], D2);
+      set_zc(a, s, 0);
       a.bias = s->b_ig[l];
       a.act = s->act;
       a.act_ncols = D;
@@ -285,6 +303,12 @@ int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, c
     }
     AimxWgradProblem wig = {base ? base + L_->dUG + l * N * D2 : nullptr, D2, base ? s->F[l] : nullptr, K,
                             g ? g->d_w_ig[l] : nullptr, K, g ? g->d_b_ig[l] : nullptr, D2, K, N};
+    if (zc_on() && s->fwd_rowptr) {  // weight columns of empty chunks get an exact zero gradient
+      wig.zc_rowptr = s->fwd_rowptr;
+      wig.zc_rows = N;
+      wig.zc_chunks = (int32_t)h;
+      wig.zc_width = D;
+    }
     out[n++] = wig;
   }
   return n;
@@ -371,7 +395,11 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     }
     // dg = dY -> dUG[:, D:]
     RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
-    RUN(run(linear_dx(N, K, D2, dUG, D2, s->w_ig[l], dF, K), ws, st));
+    {  // dF = dUG [Wi ; Wg]; the columns of empty chunks are zero (never read by the hop backward)
+      AimxGemmArgs a = linear_dx(N, K, D2, dUG, D2, s->w_ig[l], dF, K);
+      set_zc(a, s, 1);
+      RUN(run(a, ws, st));
+    }
     // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]
     const bool first = (l == 0);
     float* nxt = first ? g->d_x_in : base + lay.dY + (l - 1) * N * D;

@@ -130,6 +130,16 @@ typedef struct AimxGemmArgs {
    * arriving slice of a tile reduces the slabs in order and rezeroes its counter). NULL: a
    * separate ordered reduce kernel is launched instead. */
   int32_t* counters; int64_t n_counters;
+  /* Empty hop chunks. The reference's hop adds every hop's pairs to chunk 0 (targets < N,
+   * layers.py:154), so chunks 1..h-1 of message_passing's output are all-zero for reference
+   * inputs. When zc_rowptr != NULL (the hop's forward CSR row pointers) the kernel reads, on the
+   * device, E = zc_width * (1 + c) with c = 1 + the last chunk j in [0, zc_chunks) that holds an
+   * edge (zc_rowptr[(j+1)*zc_rows] > zc_rowptr[j*zc_rows]; c = 0 if none):
+   *   zc_dim 0: operand entries with k >= E are zero, so the k loop stops at E;
+   *   zc_dim 1: output columns >= E (ones column excluded) are zero: whole tiles there are
+   *             written as 0 without loads or MFMA work (plain-store epilogue only).
+   * Results are identical to the untrimmed product (only exact zeros are skipped). */
+  const int32_t* zc_rowptr; int64_t zc_rows; int32_t zc_chunks; int64_t zc_width; int32_t zc_dim;
 } AimxGemmArgs;
 
 size_t aimx_gemm_workspace_bytes(const AimxGemmArgs* args);
@@ -275,6 +285,8 @@ typedef struct {
   int64_t ld_dw;
   float* col_out;
   int64_t M, N, K;
+  /* optional empty-chunk trimming of the N (= X column) dimension, as zc_dim 1 of AimxGemmArgs */
+  const int32_t* zc_rowptr; int64_t zc_rows; int32_t zc_chunks; int64_t zc_width;
 } AimxWgradProblem;
 
 size_t aimx_wgrad_grouped_workspace_bytes(const AimxWgradProblem* problems, int32_t n);

@@ -188,6 +188,10 @@ def _gemm(M, N, K, layout, **epi):
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
     A = torch.randn(M, K, generator=g) if layout[0] == "N" else torch.randn(K, M, generator=g)
     B = torch.randn(K, N, generator=g) if layout[1] == "N" else torch.randn(N, K, generator=g)
+    if "A" in epi:
+        A = epi["A"]
+    if "B" in epi:
+        B = epi["B"]
     Ad, Bd = A.to(DEV), B.to(DEV)
     ones = epi.get("ones", False)
     Nt = N + 1 if ones else N
@@ -213,6 +217,9 @@ def _gemm(M, N, K, layout, **epi):
     if ones:
         a.ones_col, a.col_out = 1, col.data_ptr()
     a.splits = epi.get("splits", 0)
+    if epi.get("zc") is not None:
+        rp, rows, chunks, width, dim = epi["zc"]
+        a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width, a.zc_dim = rp.data_ptr(), rows, chunks, width, dim
     if epi.get("fused_reduce", True):
         a.counters, a.n_counters = _lib.counters(DEV).data_ptr(), _lib.N_COUNTERS
     wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
@@ -239,6 +246,44 @@ def test_gemm_layouts(M, N, K, layout):
     C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True)
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-6, err
+
+
+@pytest.mark.parametrize("nonempty", [(True, False, False), (False, False, False), (True, True, False),
+                                      (False, True, False), (True, False, True)])
+def test_gemm_empty_hop_chunk_trimming(nonempty):
+    """zc_* trimming (the reference's all-zero hop chunks, layers.py:154): F = [x | c0 | c1 | c2]
+    with the empty chunks zero. Forward (k loop stops at E) and weight gradient (zero tiles) equal
+    the untrimmed products; the input gradient matches on every column < E and stores whole tiles
+    at n >= E as 0."""
+    n, d, h = 1500, 76, 3
+    K = d * (h + 1)
+    counts = torch.zeros(h * n, dtype=torch.int32)
+    for j, ne in enumerate(nonempty):
+        if ne:
+            counts[j * n:(j + 1) * n:7] = 2
+    rowptr = torch.cat([torch.zeros(1, dtype=torch.int32), counts.cumsum(0).to(torch.int32)]).to(DEV)
+    c = max([j + 1 for j, ne in enumerate(nonempty) if ne], default=0)
+    E = d * (1 + c)
+    g = torch.Generator().manual_seed(5)
+    F = torch.randn(n, K, generator=g)
+    F[:, E:] = 0
+    zc = lambda dim: (rowptr, n, h, d, dim)  # noqa: E731
+    W = torch.randn(2 * d, K, generator=g)
+    full, _, _, ref, _ = _gemm(n, 2 * d, K, "NT", A=F, B=W)
+    trim, _, _, _, _ = _gemm(n, 2 * d, K, "NT", A=F, B=W, zc=zc(0))
+    assert torch.equal(full, trim)
+    assert (trim.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    dUG = torch.randn(n, 2 * d, generator=g)  # dF = dUG W
+    full, _, _, _, _ = _gemm(n, K, 2 * d, "NN", A=dUG, B=W)
+    trim, _, _, _, _ = _gemm(n, K, 2 * d, "NN", A=dUG, B=W, zc=zc(1))
+    assert torch.equal(full[:, :E], trim[:, :E])
+    past = -(-E // 64) * 64  # past the tile (32 or 64 columns wide) that holds column E-1
+    assert not trim[:, past:].any()
+    dY = torch.randn(n, 2 * d, generator=g)  # dW = dY^T F (+ bias column)
+    full, fcol, _, ref, _ = _gemm(2 * d, K, n, "TN", A=dY, B=F, ones=True)
+    trim, tcol, _, _, _ = _gemm(2 * d, K, n, "TN", A=dY, B=F, ones=True, zc=zc(1))
+    assert torch.equal(full, trim) and torch.equal(fcol, tcol)
+    assert not trim[:, E:].any()
 
 
 @pytest.mark.parametrize("splits", [1, 3, 64])
