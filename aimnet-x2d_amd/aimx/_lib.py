@@ -71,6 +71,7 @@ class ShellStackGrad(ctypes.Structure):
         ("d_x_in", c_ptr), ("d_x_in_ld", c_i64),
         ("d_w_ig", c_ptr), ("d_b_ig", c_ptr), ("d_w1", c_ptr), ("d_b1", c_ptr), ("d_w2", c_ptr), ("d_b2", c_ptr),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
+        ("aux_stream", c_ptr), ("events", c_ptr), ("n_events", c_i32),
     ]
 
 
@@ -134,6 +135,8 @@ _SIGS = {
     "aimx_embedding_backward_workspace_bytes": (c_size, [ctypes.POINTER(EmbeddingTables), c_i64]),
     "aimx_embedding_backward": (c_i32, [ctypes.POINTER(EmbeddingTables), c_i64, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "aimx_act_backward": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_events_create": (c_i32, [c_i32, c_ptr]),
+    "aimx_events_destroy": (c_i32, [c_i32, c_ptr]),
     "aimx_wgrad_grouped_workspace_bytes": (c_size, [ctypes.POINTER(WgradProblem), c_i32]),
     "aimx_wgrad_grouped": (c_i32, [ctypes.POINTER(WgradProblem), c_i32, c_ptr, c_size, c_ptr, c_i64, c_ptr]),
     "aimx_fused_adam_workspace_bytes": (c_size, [ctypes.POINTER(AdamTensor), c_i32]),
@@ -182,6 +185,30 @@ def require_device(*tensors):
 
 def stream_ptr(device=None):
     return torch.cuda.current_stream(device).cuda_stream
+
+
+_AUX = {}
+N_EVENTS = 64
+
+
+def aux_stream(device):
+    """Per-device auxiliary stream + event handles for the fork/join of independent work (weight
+    gradients beside the activation-gradient chain). Returns (torch stream, ctypes event array).
+    Opt-in (AIMX_AUX=1): measured on MI355X at c2 the forked weight gradients made the captured
+    train step slower (1389 vs 1216 us; c4 3886 vs 3781 us) — the latency-bound activation-gradient
+    chain loses more to the co-running work than the weight gradients gain — so by default
+    (None, None) is returned and the stack runs its single grouped weight-gradient launch."""
+    if os.environ.get("AIMX_AUX", "0") != "1":
+        return None, None
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    hit = _AUX.get(key)
+    if hit is None:
+        lib = load()
+        ev = (c_ptr * N_EVENTS)()
+        check(lib.aimx_events_create(N_EVENTS, ev), "events_create")
+        hit = (torch.cuda.Stream(device=torch.device("cuda", key)), ev)
+        _AUX[key] = hit
+    return hit
 
 
 _COUNTERS = {}

@@ -166,6 +166,9 @@ class _MPStack(torch.autograd.Function):
         gwsb = lib.aimx_shell_stack_backward_workspace_bytes(s)
         buf = torch.empty(max(gwsb // 4, 1), dtype=_F32, device=dev)
         g.workspace, g.workspace_bytes = ptr(buf), buf.numel() * 4
+        aux, events = _lib.aux_stream(dev)
+        if aux is not None and nl + 1 <= _lib.N_EVENTS:
+            g.aux_stream, g.events, g.n_events = aux.cuda_stream, _ct_addr(events), _lib.N_EVENTS
         check(lib.aimx_shell_stack_backward(s, g, stream_ptr(dev)), "shell_stack_backward")
         grads = []
         for l in range(nl):

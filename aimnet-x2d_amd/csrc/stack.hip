@@ -355,7 +355,20 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   if (!g->workspace || g->workspace_bytes < sizeof(float) * (size_t)lay.total) return AIMX_EARG;
   float* base = (float*)g->workspace;
   float* dF = base + lay.dF;
-  const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters};
+  // weight-gradient problems of the whole stack (layer L-1 first, 2*nm+1 per layer)
+  const int per_layer = (int)(2 * nm + 1);
+  std::vector<AimxWgradProblem> pr(L * per_layer);
+  const int n_pr = stack_wgrad_problems(s, g, base, &lay, pr.data());
+  // with an auxiliary stream, each layer's weight gradients fork off as soon as its activation
+  // gradients exist; the two streams split the counter array so their split-K tickets never meet
+  const bool aux = g->aux_stream && g->events && g->n_events >= L + 1 && s->counters && s->n_counters >= 2;
+  hipStream_t ast = (hipStream_t)g->aux_stream;
+  const int64_t main_counters = aux ? s->n_counters / 2 : s->n_counters;
+  const Ws ws{s->workspace, s->workspace_bytes, s->counters, main_counters};
+  int32_t* aux_cnt = aux ? s->counters + main_counters : nullptr;
+  const int64_t aux_ncnt = aux ? s->n_counters - main_counters : 0;
+  float* wg_ws = base + lay.wg;
+  const size_t wg_bytes = sizeof(float) * (size_t)(lay.total - lay.wg);
   const bool drop = s->training && s->drop_p > 0.f;
   for (int64_t l = L - 1; l >= 0; --l) {
     float* dUG = base + lay.dUG + l * N * D2;
@@ -395,6 +408,13 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     }
     // dg = dY -> dUG[:, D:]
     RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
+    if (aux) {  // fork: this layer's weight gradients run beside the rest of the chain
+      hipEvent_t ev = (hipEvent_t)g->events[l];
+      AIMX_CHECK_HIP(hipEventRecord(ev, st));
+      AIMX_CHECK_HIP(hipStreamWaitEvent(ast, ev, 0));
+      RUN(aimx_wgrad_grouped(pr.data() + (L - 1 - l) * per_layer, per_layer, wg_ws, wg_bytes, aux_cnt, aux_ncnt,
+                             (aimx_stream_t)ast));
+    }
     {  // dF = dUG [Wi ; Wg]; the columns of empty chunks are zero (never read by the hop backward)
       AimxGemmArgs a = linear_dx(N, K, D2, dUG, D2, s->w_ig[l], dF, K);
       set_zc(a, s, 1);
@@ -414,9 +434,12 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       RUN(launch_charge_bwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, dst, D, nxt, ldn, st));
     }
   }
+  if (aux) {  // join
+    hipEvent_t ev = (hipEvent_t)g->events[L];
+    AIMX_CHECK_HIP(hipEventRecord(ev, ast));
+    AIMX_CHECK_HIP(hipStreamWaitEvent(st, ev, 0));
+    return AIMX_OK;
+  }
   // every weight and bias gradient of the stack in one grouped launch
-  std::vector<AimxWgradProblem> pr(L * (2 * nm + 1));
-  const int n = stack_wgrad_problems(s, g, base, &lay, pr.data());
-  return aimx_wgrad_grouped(pr.data(), n, base + lay.wg, sizeof(float) * (size_t)(lay.total - lay.wg), s->counters,
-                            s->n_counters, stream_);
+  return aimx_wgrad_grouped(pr.data(), n_pr, wg_ws, wg_bytes, s->counters, s->n_counters, stream_);
 }

@@ -159,10 +159,15 @@ class GradientSync:
         self._handles = [None] * len(self.buckets)
 
     def _launch(self, i):
+        # one persistent flat buffer per bucket: the gradients are packed by ONE cat kernel into it,
+        # all-reduced in place, then scattered back by one multi-tensor copy (finish)
         bucket = self.buckets[i]
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        self._flat[i] = flat
+        flat = self._flat[i]
+        if flat is None or flat.device != bucket[0].device:
+            flat = torch.empty(sum(p.numel() for p in bucket), dtype=bucket[0].dtype, device=bucket[0].device)
+            self._flat[i] = flat
+        grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket]
+        torch.cat(grads, out=flat)
         self._handles[i] = dist.all_reduce(flat, group=self.group, async_op=True)
 
     def _on_grad(self, p):
@@ -182,13 +187,15 @@ class GradientSync:
         for i, bucket in enumerate(self.buckets):
             self._handles[i].wait()
             flat = self._flat[i].div_(self.world)
-            off = 0
+            dst, src, off = [], [], 0
             for p in bucket:
                 n = p.numel()
                 if p.grad is not None:
-                    p.grad.copy_(flat[off:off + n].view_as(p))
+                    dst.append(p.grad)
+                    src.append(flat[off:off + n].view_as(p))
                 off += n
-            self._flat[i] = None
+            if dst:
+                torch._foreach_copy_(dst, src)
         self._reset()
 
     def remove(self):

@@ -215,15 +215,23 @@ def main():
                          "step's batch is collated by the C++ batch builder from the molecule store and "
                          "copied host->device inside the timed region (PCIe-inclusive rate)")
     ap.add_argument("--feed-threads", type=int, default=4)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:  # rehearsal only (more ranks than GPUs): ranks share the box's GPUs
+        local = local % ndev
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
     cfg = CONFIGS[args.config]
     torch.manual_seed(1234 + rank)
 
@@ -285,12 +293,32 @@ def main():
             with torch.cuda.graph(g2):
                 clip_step()
 
+        # diagnostic: AIMX_BENCH_PHASES=1 synchronising per-phase times, =2 host-side call times only
+        phases = int(os.environ.get("AIMX_BENCH_PHASES", "0"))
+        hsync = torch.cuda.synchronize if phases == 1 else (lambda: None)
+
         def step(i):
             static.copy_(next(feeder) if feeder is not None else batches[i % len(batches)])
+            if phases:
+                hsync()
+                t0 = time.perf_counter()
             g1.replay()
+            if phases:
+                hsync()
+                t1 = time.perf_counter()
             if g2 is not None:
                 sync.finish()
+                if phases:
+                    hsync()
+                    t2 = time.perf_counter()
                 g2.replay()
+            if phases:
+                hsync()
+                t3 = time.perf_counter()
+                if rank == 0:
+                    print(json.dumps({"step": i, "fwd_bwd_ms": round((t1 - t0) * 1e3, 3),
+                                      "sync_ms": round((t2 - t1) * 1e3, 3) if g2 is not None else None,
+                                      "opt_ms": round((t3 - (t2 if g2 is not None else t1)) * 1e3, 3)}), flush=True)
     else:
         opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
         sync = GradientSync(model.parameters()) if world > 1 else None

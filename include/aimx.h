@@ -41,6 +41,11 @@ typedef void* aimx_stream_t; /* hipStream_t */
 /* Library identity (for load checks): returns "aimx/<version>/gfx950". */
 const char* aimx_version(void);
 
+/* Event handles (hipEvent_t, timing disabled) for the fork/join of auxiliary streams
+ * (AimxShellStackGrad.aux_stream). Created once by the caller and reused across calls. */
+int aimx_events_create(int32_t n, void** events);
+int aimx_events_destroy(int32_t n, void** events);
+
 /* ------------------------------------------------------------------------------------------
  * Stable CSR build (device): rows sorted by key, ties kept in ascending item order — exactly the
  * order in which CPU ATen scatter_add_ visits edges (reference layers.py:158 via torch_scatter
@@ -186,6 +191,13 @@ typedef struct AimxShellStackGrad {
    * per-block activation gradients are kept until the weight gradients of the whole stack run
    * as ONE grouped launch at the end (aimx_wgrad_grouped) */
   void* workspace; size_t workspace_bytes;
+  /* optional concurrency: when aux_stream != NULL and n_events >= num_layers + 1, each layer's
+   * weight gradients are launched on aux_stream as soon as that layer's activation gradients
+   * exist (event fork), overlapping the rest of the activation-gradient chain on `stream`; the
+   * call returns with `stream` joined on aux_stream (event join), so graph capture and eager
+   * execution see the same dependencies. aux_stream uses the upper half of the counter array.
+   * events: hipEvent_t handles from aimx_events_create. */
+  aimx_stream_t aux_stream; void* const* events; int32_t n_events;
 } AimxShellStackGrad;
 
 size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s);

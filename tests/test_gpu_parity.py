@@ -526,3 +526,25 @@ def test_fused_adam_matches_torch_clip_and_adam(max_norm, wd):
         assert norm_rel(st_a["exp_avg"].cpu().numpy(), st_b["exp_avg"].cpu().numpy()) < 1e-6
         assert norm_rel(st_a["exp_avg_sq"].cpu().numpy(), st_b["exp_avg_sq"].cpu().numpy()) < 1e-6
         assert float(st_a["step"]) == float(st_b["step"]) == 5.0
+
+
+def test_aux_stream_weight_gradients_identical(monkeypatch):
+    """AIMX_AUX=1 (weight gradients forked onto an auxiliary stream, event fork/join) gives the
+    same gradients bit for bit as the single grouped launch (eager execution)."""
+    z, cfg, _ = load_case("c2")
+    af, edges, batch, tc = load_case("c2", DEV)[2]
+    e_empty = torch.empty(0, 2, dtype=torch.long, device=DEV)
+    w = torch.from_numpy(z["loss_w"]).to(DEV)
+
+    def grads(aux):
+        monkeypatch.setenv("AIMX_AUX", "1" if aux else "0")
+        model = _build_model(cfg, int(z["seed"]))
+        out, _, _ = model(af, edges, batch, tc, torch.empty(0, 4, dtype=torch.long, device=DEV), e_empty, e_empty)
+        (out * w).sum().backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
+
+    a, b = grads(False), grads(True)
+    assert a.keys() == b.keys()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
