@@ -55,6 +55,7 @@ class ShellStack(ctypes.Structure):
         ("drop_p", c_f32), ("drop_seed", c_ptr),
         ("fwd_rowptr", c_ptr), ("fwd_col", c_ptr), ("bwd_rowptr", c_ptr), ("bwd_col", c_ptr),
         ("gptr", c_ptr), ("gperm", c_ptr), ("G", c_i64), ("total_charges", c_ptr),
+        ("row_seg", c_ptr), ("row_seg_stride", c_i64),
         ("w_ig", c_ptr), ("b_ig", c_ptr), ("w1", c_ptr), ("b1", c_ptr), ("w2", c_ptr), ("b2", c_ptr),
         ("F", c_ptr), ("X", c_ptr), ("UG", c_ptr), ("U", c_ptr),
         ("V", c_ptr), ("R", c_ptr), ("A", c_ptr), ("M", c_ptr),
@@ -111,7 +112,7 @@ _SIGS = {
     "aimx_csr_build_multi_workspace_bytes": (c_size, [ctypes.POINTER(CsrSpec), c_i32]),
     "aimx_csr_build_multi": (c_i32, [ctypes.POINTER(CsrSpec), c_i32, c_ptr, c_size, c_ptr, c_ptr]),
     "aimx_segment_gather_sum": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i64,
-                                        c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+                                        c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "aimx_gemm_workspace_bytes": (c_size, [ctypes.POINTER(GemmArgs)]),
     "aimx_gemm": (c_i32, [ctypes.POINTER(GemmArgs), c_ptr]),
     "aimx_shell_stack_workspace_bytes": (c_size, [ctypes.POINTER(ShellStack)]),

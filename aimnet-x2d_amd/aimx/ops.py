@@ -99,6 +99,7 @@ class _MPStack(torch.autograd.Function):
         if plan.graph is not None:
             s.gptr, s.gperm, s.G = ptr(plan.graph.rowptr), ptr(plan.graph.col), plan.G
         s.total_charges = ptr(total_charges)
+        s.row_seg, s.row_seg_stride = plan.row_seg()
         keep = [ptr_array(w_ig), ptr_array(b_ig), ptr_array(w1), ptr_array(b1), ptr_array(w2), ptr_array(b2),
                 ptr_array(F), ptr_array(X), ptr_array(UG), ptr_array(U), ptr_array(V), ptr_array(R), ptr_array(A),
                 ptr_array(M)]
@@ -151,6 +152,7 @@ class _MPStack(torch.autograd.Function):
         if plan.graph is not None:
             s.gptr, s.gperm, s.G = ptr(plan.graph.rowptr), ptr(plan.graph.col), plan.G
         s.total_charges = ptr(st["tc"])
+        s.row_seg, s.row_seg_stride = plan.row_seg()
         keep = [ptr_array(st[nm_]) for nm_ in ("w_ig", "b_ig", "w1", "b1", "w2", "b2", "F", "X", "UG", "U", "V", "R",
                                                "A", "M")]
         (s.w_ig, s.b_ig, s.w1, s.b1, s.w2, s.b2, s.F, s.X, s.UG, s.U, s.V, s.R, s.A, s.M) = [
@@ -213,9 +215,10 @@ class _Hop(torch.autograd.Function):
         x, ldx = _rows(x)
         out = torch.empty(h * n, d, dtype=_F32, device=x.device)
         # out viewed as h chunks of n rows (same addresses): tells the kernel where chunk 0 ends
+        seg, seg_st = plan.row_seg()
         check(lib.aimx_segment_gather_sum(ptr(x), ldx, 0, 0, d, ptr(plan.fwd.rowptr), ptr(plan.fwd.col), h * n,
-                                          ptr(out), d, n, n * d, None, 0, None, 0, stream_ptr(x.device)),
-              "hop_forward")
+                                          ptr(out), d, n, n * d, None, 0, None, 0, seg, seg_st,
+                                          stream_ptr(x.device)), "hop_forward")
         ctx.plan = plan
         return out
 
@@ -227,8 +230,9 @@ class _Hop(torch.autograd.Function):
         g = g.contiguous()
         d = g.shape[1]
         dx = torch.empty(n, d, dtype=_F32, device=g.device)
+        seg, seg_st = plan.row_seg()
         check(lib.aimx_segment_gather_sum(ptr(g), d, 0, 0, d, ptr(plan.bwd.rowptr), ptr(plan.bwd.col), n, ptr(dx), d,
-                                          0, 0, None, 0, None, 0, stream_ptr(g.device)), "hop_backward")
+                                          0, 0, None, 0, None, 0, seg, seg_st, stream_ptr(g.device)), "hop_backward")
         return None, dx
 
 

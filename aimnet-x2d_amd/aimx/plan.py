@@ -115,6 +115,14 @@ class GraphPlan:
         if _VALIDATE:
             self.validate()
 
+    def row_seg(self):
+        """(pointer, stride) of the molecule id per atom (the batch indices) for segment-aligned
+        hop tiles, or (None, 0) when the plan has no batch (the result never depends on it)."""
+        if self.batch is None or self.batch.dim() != 1 or self.batch.shape[0] != self.N:
+            return None, 0
+        b = self._keep[-1]  # the int64 batch tensor kept alive by the plan
+        return b.data_ptr(), b.stride(0)
+
     def validate(self):
         """Synchronising check (opt-in via AIMX_VALIDATE=1): the reference raises on bad indices."""
         if int(self.status.item()) != 0:

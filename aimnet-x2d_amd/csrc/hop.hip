@@ -81,11 +81,13 @@ __device__ __forceinline__ int64_t row_off(uint32_t r, int64_t ld, const FastDiv
 // A tile whose rows hold no edges (the reference's hop chunks >= 1 are all-empty, layers.py:154)
 // becomes a pure streaming store. Gathers are issued 8 at a time with clamped (always valid)
 // indices and summed with selects, so the sum is the ordered edge-order sum bit for bit.
-constexpr int kMaxTileRows = 64;
+constexpr int kMaxTileRows = 64;   // nominal rows per tile
+constexpr int kAlignWin = 64;      // a segment-aligned tile cut moves at most this many rows
+constexpr int kMaxRows = kMaxTileRows + kAlignWin;  // rows of one (aligned) tile
 constexpr int kGroup = 8;      // gathers in flight per thread
 constexpr int kColCap = 512;             // default staged col entries per tile (2 KiB)
 constexpr int kStageBytes = 17 * 1024 + 512;  // default LDS for the staged source span
-constexpr int kBigMul = 8;             // small tiles per big tile
+constexpr int kBigMul = 16;            // small tiles per big tile (measured: 8 -> 16 with interleave, -1.2 %)
 
 template <bool CHUNKED>
 __device__ __forceinline__ int64_t src_off(uint32_t c, int64_t ld, const FastDiv& rpc, int64_t cs) {
@@ -205,15 +207,20 @@ struct HopArgs {
   int64_t add0_ld;
   const float* add1;
   int64_t add1_ld;
+  const int64_t* seg;  // optional segment (molecule) id per row of [0, split_rows)
+  int64_t seg_stride;
+  int32_t flat_zero;    // rows past split are one contiguous [rows - split, D] region, no adds
+  int32_t nt_store;     // nontemporal stores for that fill
+  int32_t interleave;   // spread the big tiles among the small ones (block order)
 };
 
 // All LDS is dynamic, carved at 16-byte multiples (MI355X guide: a static __shared__ ahead of the
 // dynamic region shifts its base off 16-B alignment and every ds_read_b128 replays at ~64 cycles).
 struct HopLds {
-  int32_t* ptr;   // [kMaxTileRows + 1]
-  int32_t* lohi;  // [2]
+  int32_t* ptr;   // [kMaxRows + 1]
+  int32_t* lohi;  // [2] (also the two aligned cuts of a segment-aligned tile)
 };
-constexpr int kLdsHead = 80;  // ints ahead of the col slice: ptr (65) + lohi (2), padded to 16 B
+constexpr int kLdsHead = 136;  // ints ahead of the col slice: ptr (129) + lohi (2), padded to 16 B
 
 // One tile of nr <= tile_rows rows at r0 (called by the whole workgroup; leaves LDS reusable).
 template <int VEC, bool SRC_CHUNKED>
@@ -300,15 +307,53 @@ template <int VEC, bool SRC_CHUNKED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_gather_sum(const HopArgs a) {
   // [ptr | lohi | pad] [col_cap col entries] [xcap_rows x D staged rows]
   extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
-  HopLds L{s_dyn, s_dyn + kMaxTileRows + 1};
+  HopLds L{s_dyn, s_dyn + kMaxRows + 1};
   int32_t* s_col = s_dyn + kLdsHead;
   float* s_x = reinterpret_cast<float*>(s_dyn + kLdsHead + a.col_cap);
-  if (blockIdx.x < a.nsmall) {
-    const uint32_t r0 = blockIdx.x * a.tile_rows;
-    process_tile<VEC, SRC_CHUNKED>(a, L, s_col, s_x, r0, min(a.tile_rows, a.split_rows - r0));
+  // Block order: with `interleave`, the big (mostly zero-fill) tiles are spread evenly among the
+  // gather tiles, so the chip runs the write-bound fill beside the latency-bound gathers instead
+  // of one phase after the other. big(b) = # big blocks among 0..b = floor((b+1) nbig / total).
+  uint32_t bsmall = blockIdx.x, bbig = 0;
+  bool is_small = blockIdx.x < a.nsmall;
+  if (a.interleave) {
+    const uint64_t total = (uint64_t)gridDim.x, nbig = total - a.nsmall;
+    const uint32_t c1 = (uint32_t)(((uint64_t)blockIdx.x + 1) * nbig / total);
+    const uint32_t c0 = (uint32_t)((uint64_t)blockIdx.x * nbig / total);
+    is_small = (c1 == c0);
+    bsmall = blockIdx.x - c1;
+    bbig = c1 - 1;
+  } else if (!is_small) {
+    bbig = blockIdx.x - a.nsmall;
+  }
+  if (is_small) {
+    uint32_t r0 = bsmall * a.tile_rows;
+    uint32_t r1 = min(r0 + a.tile_rows, a.split_rows);
+    if (a.seg) {
+      // Segment-aligned cuts: each nominal cut c moves to the first segment (molecule) start in
+      // [c, c + 64) (c itself if none), so a tile holds whole molecules and its source rows are
+      // exactly its own rows: x is staged once instead of once per straddling tile. Both cuts
+      // are the same function of c, so consecutive tiles still partition the rows exactly.
+      const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+      if (w < 2) {
+        const uint32_t c = w ? r1 : r0;
+        uint32_t cut = c;
+        if (c > 0 && c < a.split_rows) {
+          const uint32_t q = min(c + lane, a.split_rows - 1);
+          const int64_t sq = a.seg[(int64_t)q * a.seg_stride], sp = a.seg[(int64_t)(q - 1) * a.seg_stride];
+          const unsigned long long m = __ballot((c + lane < a.split_rows) && sq != sp);
+          if (m) cut = c + (uint32_t)__builtin_ctzll(m);
+        }
+        if (lane == 0) L.lohi[w] = (int32_t)cut;
+      }
+      __syncthreads();
+      r0 = (uint32_t)L.lohi[0];
+      r1 = (uint32_t)L.lohi[1];
+      __syncthreads();
+    }
+    if (r1 > r0) process_tile<VEC, SRC_CHUNKED>(a, L, s_col, s_x, r0, r1 - r0);
     return;
   }
-  const uint32_t R0 = a.split_rows + (blockIdx.x - a.nsmall) * a.big_rows;
+  const uint32_t R0 = a.split_rows + bbig * a.big_rows;
   const uint32_t NR = min(a.big_rows, a.rows - R0);
   if (threadIdx.x == 0) {
     L.lohi[0] = a.rowptr[R0];
@@ -316,6 +361,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
   __syncthreads();
   if (L.lohi[0] == L.lohi[1]) {
+    if (a.flat_zero) {
+      // the big tile's rows are one contiguous [NR, D] region and there is nothing to add: a flat
+      // streaming fill (16-byte stores, no per-element row arithmetic; nontemporal when asked)
+      typedef float V __attribute__((ext_vector_type(VEC)));
+      V* o = reinterpret_cast<V*>(a.out + (int64_t)R0 * a.out_ld);
+      const uint32_t n = NR * a.upr.d;
+      const V z = (V)(0.f);
+      if (a.nt_store) {
+        for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) __builtin_nontemporal_store(z, o + t);
+      } else {
+        for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) o[t] = z;
+      }
+      return;
+    }
     tile_body<VEC, true, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, L.ptr, s_col, 0, R0, NR, a.out,
                                       a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, false);
     return;
@@ -340,7 +399,8 @@ using namespace aimx;
 extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
                                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out,
                                        int64_t out_ld, int64_t out_rpc, int64_t out_cs, const float* add0,
-                                       int64_t add0_ld, const float* add1, int64_t add1_ld, aimx_stream_t stream_) {
+                                       int64_t add0_ld, const float* add1, int64_t add1_ld, const int64_t* row_seg,
+                                       int64_t row_seg_stride, aimx_stream_t stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (rows < 0 || D < 0) return AIMX_EARG;
   if (rows == 0 || D == 0) return AIMX_OK;
@@ -402,6 +462,17 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   a.add0_ld = add0_ld;
   a.add1 = add1;
   a.add1_ld = add1_ld;
+  // segment-aligned tiles: only for the one-tile-per-workgroup range, and only when the staged
+  // source span is in use (the alignment is what makes the span equal the tile)
+  // (tiles of >= 16 rows only: moving a cut of a 3-row tile up to a 40-atom molecule start turns
+  // most tiles empty and the rest too tall to stage — c4/c5 measured 6-20 % slower)
+  a.seg = (row_seg && xcap > 0 && tr >= 16 && getenv("AIMX_HOP_NO_SEG") == nullptr) ? row_seg : nullptr;
+  a.seg_stride = row_seg_stride;
+  // chunks >= 1 contiguous after chunk 0 (a plain [h*N, D] output, as the hop op writes it)
+  const bool contiguous = out_ld == D && (out_rpc <= 0 || out_cs == out_rpc * out_ld);
+  a.flat_zero = (contiguous && !add0 && !add1 && env_i64("AIMX_HOP_FLAT", 1) != 0) ? 1 : 0;
+  a.nt_store = env_i64("AIMX_HOP_NT", 0) != 0 ? 1 : 0;
+  a.interleave = env_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
   using KFn = void (*)(const HopArgs);
   const bool chunked = src_rpc > 0;
   KFn fn = vec == 4 ? (chunked ? k_gather_sum<4, true> : k_gather_sum<4, false>)

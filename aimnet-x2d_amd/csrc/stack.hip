@@ -123,11 +123,11 @@ int run(AimxGemmArgs a, const Ws& ws, hipStream_t s) {
   return launch_gemm(a, s);
 }
 
-int gather(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D, const int32_t* rowptr,
-           const int32_t* col, int64_t rows, float* out, int64_t out_ld, int64_t out_rpc, int64_t out_cs,
-           const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld, hipStream_t s) {
+int gather(const AimxShellStack* st, const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
+           const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld, int64_t out_rpc,
+           int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld, hipStream_t s) {
   return aimx_segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
-                                 add0_ld, add1, add1_ld, (aimx_stream_t)s);
+                                 add0_ld, add1, add1_ld, st->row_seg, st->row_seg_stride, (aimx_stream_t)s);
 }
 
 // Empty hop chunks (AimxGemmArgs.zc_*): every GEMM over F's columns trims the all-zero chunks the
@@ -195,7 +195,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
       RUN(copy2d(s->x_in, s->x_in_ld, F, K, N, D, st));
     }
     // 2) hop: chunks 1..h of F = scatter_add(x[src % N], target) in edge order
-    RUN(gather(F, K, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, K, N, D, nullptr, 0, nullptr, 0, st));
+    RUN(gather(s, F, K, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, K, N, D, nullptr, 0, nullptr, 0, st));
     // 3) [u | g] = F [Wi ; Wg]^T + [bi ; bg], a0 = act(u)
     {
       AimxGemmArgs a = linear_fwd(N, K, D2, F, K, s->w_ig[l], s->UG[l], D2);
@@ -426,7 +426,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     const int64_t ldn = first ? g->d_x_in_ld : D;
     float* dst = s->use_pc ? base + lay.T0 : nxt;
     const int64_t ldd = s->use_pc ? D : ldn;
-    RUN(gather(dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, dF, K,
+    RUN(gather(s, dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, dF, K,
                s->mode_single ? nullptr : dY, ldy, st));
     if (s->use_pc) {
       const float* raw = first ? s->x_in : s->X[l];

@@ -133,7 +133,10 @@ def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launch
     edges = (e0.unsqueeze(0) + off).reshape(-1, 2)
     n = n0 * reps
     e = edges.shape[0]
-    plan = GraphPlan(n, hops, edges=edges)
+    # molecule ids of the tiled graph: the model's plans always carry them (segment-aligned tiles)
+    g0 = batch.num_graphs
+    mol = (batch.batch.unsqueeze(0) + torch.arange(reps, device=device, dtype=torch.int64).view(reps, 1) * g0)
+    plan = GraphPlan(n, hops, edges=edges, batch=mol.reshape(-1), num_graphs=g0 * reps)
     x = torch.randn(n, d, device=device)
     del edges
     torch.cuda.synchronize()

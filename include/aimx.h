@@ -94,6 +94,11 @@ int aimx_csr_build_multi(const AimxCsrSpec* specs, int32_t n, void* workspace, s
  * chunk are expected to be mostly edge-free (the reference's hop chunks >= 1) and are walked in
  * large tiles; pass out_rows_per_chunk = N, out_chunk_stride = N*out_ld for a plain [h*N, D]
  * output to get that (same addresses as rows_per_chunk <= 0).
+ * row_seg (nullable, stride row_seg_stride): segment id per row of the first output chunk —
+ * the molecule index (batch_indices) for the hop and its backward, whose rows are atoms. Rows
+ * of one segment are consecutive and edges stay inside a segment, so row tiles cut at segment
+ * starts (when one lies within 64 rows of the nominal cut) stage their source rows exactly once.
+ * The result does not depend on row_seg (it only moves tile boundaries).
  * ------------------------------------------------------------------------------------------ */
 int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rows_per_chunk,
                             int64_t src_chunk_stride, int64_t D,
@@ -101,7 +106,7 @@ int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rows_p
                             float* out, int64_t out_ld, int64_t out_rows_per_chunk,
                             int64_t out_chunk_stride,
                             const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld,
-                            aimx_stream_t stream);
+                            const int64_t* row_seg, int64_t row_seg_stride, aimx_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused fp32 GEMM on the matrix cores (v_mfma_f32_16x16x4_f32; exact f32 fmaf chains), the
@@ -172,6 +177,7 @@ typedef struct AimxShellStack {
   const int32_t* fwd_rowptr; const int32_t* fwd_col; /* rows N*num_hops, col = src % N */
   const int32_t* bwd_rowptr; const int32_t* bwd_col; /* rows N, col = target */
   const int32_t* gptr; const int32_t* gperm; int64_t G; const float* total_charges;
+  const int64_t* row_seg; int64_t row_seg_stride; /* molecule id per atom (nullable): hop tiles */
   const float* const* w_ig; const float* const* b_ig;
   const float* const* w1; const float* const* b1; const float* const* w2; const float* const* b2;
   float* const* F; float* const* X; float* const* UG; float* const* U;

@@ -17,10 +17,11 @@ os.makedirs(dst, exist_ok=True)
 
 
 def one(pattern):
+    """The newest match (gpurun_out/ accumulates the run directories of earlier calls)."""
     hits = glob.glob(os.path.join(src, pattern), recursive=True)
     if not hits:
         raise SystemExit(f"missing {pattern}")
-    return hits[0]
+    return max(hits, key=os.path.getmtime)
 
 
 shutil.copy(one("bench/**/*kernel_stats.csv"), os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))

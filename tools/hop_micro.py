@@ -51,11 +51,13 @@ def main():
     n, e = n0 * reps, edges.shape[0]
     x = torch.randn(n, d, device=dev)
     out = []
-    plans = {h: GraphPlan(n, h, edges=edges) for h in (3, 1)}
+    g0 = batch.num_graphs
+    mol = (batch.batch.unsqueeze(0) + torch.arange(reps, device=dev, dtype=torch.int64).view(reps, 1) * g0).reshape(-1)
+    plans = {h: GraphPlan(n, h, edges=edges, batch=mol, num_graphs=g0 * reps) for h in (3, 1)}
     envs = a.env or [""]
     for rnd in range(a.rounds):
         for ev in envs:
-            for kv in ev.split():
+            for kv in ev.replace(",", " ").split():
                 k, v = kv.split("=")
                 os.environ[k] = v
             for h in (3, 1):
@@ -64,7 +66,7 @@ def main():
                 b = 4 * (n * d + e + (h * n + 1) + h * n * d)
                 out.append({"case": f"hop h={h} [{ev}] r{rnd}", "ms": ms, "alg_GBs": b / ms / 1e6})
                 print(json.dumps(out[-1]), flush=True)
-            for kv in ev.split():
+            for kv in ev.replace(",", " ").split():
                 os.environ.pop(kv.split("=")[0], None)
     del plans
     plan = GraphPlan(n, 2, edges=edges[:0])

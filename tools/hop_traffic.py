@@ -19,10 +19,8 @@ def rows(d):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
-    out = []
-    for f in files:
-        out += list(csv.DictReader(open(f)))
-    return out
+    # the newest run only (gpurun_out/ keeps the run directories of earlier calls)
+    return list(csv.DictReader(open(max(files, key=os.path.getmtime))))
 
 
 def per_dispatch(rs, counter):

@@ -23,7 +23,7 @@ XCD = 8
 def main():
     d = sys.argv[1]
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 15
-    path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    path = max(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True), key=os.path.getmtime)
     per = defaultdict(dict)
     names = {}
     for r in csv.DictReader(open(path)):

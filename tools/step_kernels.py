@@ -3,11 +3,12 @@ consecutive k_embed_gather dispatches, i.e. one forward start to the next)."""
 import collections
 import csv
 import glob
+import os
 import re
 import sys
 
 d = sys.argv[1]
-f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
+f = max(glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True), key=os.path.getmtime)
 tr = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(tr) if "k_embed_gather" in r["Kernel_Name"]]
 a, b = starts[-3], starts[-2]
