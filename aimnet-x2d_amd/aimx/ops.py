@@ -7,6 +7,7 @@ Each operator corresponds to a reference interface:
   attention_pool         <- MultiHeadAttentionPoolingLayer.forward (pooling.py:122-172)
   segment_pool           <- Mean/Max/SumPoolingLayer.forward (pooling.py:15-80)
   partial_charges        <- GNN._partial_charge_calculation (gnn.py:622-658)
+  l1_loss                <- nn.L1Loss / WeightedL1Loss (trainer.py:24-35, models/losses.py:14-48)
 """
 from __future__ import annotations
 
@@ -79,11 +80,12 @@ class _MPStack(torch.autograd.Function):
         out = torch.empty(n, d, dtype=_F32, device=dev)
         drop = bool(spec["training"]) and spec["drop_p"] > 0
         M = [torch.empty(n, d, dtype=torch.uint8, device=dev) for _ in range(nl * nm)] if drop else []
-        w_ig = [params[l * (2 + 4 * nm)] for l in range(nl)]
-        b_ig = [params[l * (2 + 4 * nm) + 1] for l in range(nl)]
+        # [input_proj.W ; global_skip_proj.W] and their biases of every layer, packed by ONE cat
+        # kernel (layer blocks padded to 64 floats: 16-byte aligned GEMM operands)
+        packed, w_ig, b_ig = _pack_ig(params, nl, nm, d, k)
         w1, b1, w2, b2 = [], [], [], []
         for l in range(nl):
-            base = l * (2 + 4 * nm) + 2
+            base = l * (4 + 4 * nm) + 4
             for j in range(nm):
                 w1.append(params[base + 4 * j])
                 b1.append(params[base + 4 * j + 1])
@@ -115,7 +117,8 @@ class _MPStack(torch.autograd.Function):
         ctx.spec, ctx.plan = spec, plan
         # inputs go through save_for_backward; only forward-internal buffers live on ctx
         ctx.save_for_backward(x_in, total_charges, drop_seed, *params)
-        ctx.state = dict(buf=buf, M=M, F=F, X=X, UG=UG, U=U, V=V, R=R, A=A, x_ld=x_ld, ws=ws, drop=drop)
+        ctx.state = dict(buf=buf, M=M, F=F, X=X, UG=UG, U=U, V=V, R=R, A=A, x_ld=x_ld, ws=ws, drop=drop,
+                         packed=packed, w_ig=w_ig, b_ig=b_ig)
         return out
 
     @staticmethod
@@ -125,10 +128,8 @@ class _MPStack(torch.autograd.Function):
         x_in, tc, seed, *params = ctx.saved_tensors
         nm_ = spec["num_mlp"]
         st["x_in"], st["tc"], st["seed"] = x_in, tc, seed
-        st["w_ig"] = [params[l * (2 + 4 * nm_)] for l in range(spec["num_layers"])]
-        st["b_ig"] = [params[l * (2 + 4 * nm_) + 1] for l in range(spec["num_layers"])]
         for j, key in enumerate(("w1", "b1", "w2", "b2")):
-            st[key] = [params[l * (2 + 4 * nm_) + 2 + 4 * q + j] for l in range(spec["num_layers"]) for q in range(nm_)]
+            st[key] = [params[l * (4 + 4 * nm_) + 4 + 4 * q + j] for l in range(spec["num_layers"]) for q in range(nm_)]
         dev = d_out.device
         n, d, h, nl, nm = spec["N"], spec["D"], spec["num_hops"], spec["num_layers"], spec["num_mlp"]
         k = d * (h + 1)
@@ -136,8 +137,10 @@ class _MPStack(torch.autograd.Function):
         # gradients handed to autograd are standalone allocations; the scratch is one buffer
         new = lambda *shape: torch.empty(*shape, dtype=_F32, device=dev)  # noqa: E731
         dx_t = new(n, d)
-        dw_ig = [new(2 * d, k) for _ in range(nl)]
-        db_ig = [new(2 * d) for _ in range(nl)]
+        d_packed = torch.empty_like(st["packed"])
+        blk = st["packed"].numel() // nl
+        dw_ig = [d_packed[l * blk:l * blk + 2 * d * k].view(2 * d, k) for l in range(nl)]
+        db_ig = [d_packed[l * blk + 2 * d * k:l * blk + 2 * d * k + 2 * d] for l in range(nl)]
         dw1 = [new(d, d) for _ in range(nl * nm)]
         db1 = [new(d) for _ in range(nl * nm)]
         dw2 = [new(d, d) for _ in range(nl * nm)]
@@ -174,12 +177,40 @@ class _MPStack(torch.autograd.Function):
         check(lib.aimx_shell_stack_backward(s, g, stream_ptr(dev)), "shell_stack_backward")
         grads = []
         for l in range(nl):
-            grads += [dw_ig[l], db_ig[l]]
+            # input_proj / global_skip_proj weight and bias gradients: views of the packed gradient
+            grads += [dw_ig[l][:d], dw_ig[l][d:], db_ig[l][:d], db_ig[l][d:]]
             for j in range(nm):
                 idx = l * nm + j
                 grads += [dw1[idx], db1[idx], dw2[idx], db2[idx]]
         del keep, gkeep, buf
         return (None, None, dx_t, None, None, *grads)
+
+
+_PAD = {}
+
+
+def _pack_ig(params, nl, nm, d, k):
+    """One cat of every layer's [Wi ; Wg] (each [D, K]) and [bi ; bg]: returns (packed, w_ig views
+    [2D, K], b_ig views [2D]); per-layer blocks are padded to a multiple of 64 floats."""
+    per = 2 * d * k + 2 * d
+    blk = (per + 63) // 64 * 64
+    dev = params[0].device
+    parts = []
+    pad = None
+    if blk > per:
+        pad = _PAD.get((dev, blk - per))
+        if pad is None:
+            pad = torch.zeros(blk - per, dtype=_F32, device=dev)
+            _PAD[(dev, blk - per)] = pad
+    for l in range(nl):
+        wi, wg, bi, bg = params[l * (4 + 4 * nm):l * (4 + 4 * nm) + 4]
+        parts += [wi.detach().reshape(-1), wg.detach().reshape(-1), bi.detach().reshape(-1), bg.detach().reshape(-1)]
+        if pad is not None:
+            parts.append(pad)
+    packed = torch.cat(parts)
+    w_ig = [packed[l * blk:l * blk + 2 * d * k].view(2 * d, k) for l in range(nl)]
+    b_ig = [packed[l * blk + 2 * d * k:l * blk + per] for l in range(nl)]
+    return packed, w_ig, b_ig
 
 
 def _ct_addr(arr):
@@ -189,7 +220,8 @@ def _ct_addr(arr):
 
 def message_passing_stack(plan, x, params, *, num_hops, num_layers, num_mlp, act, use_pc=False, total_charges=None,
                           training=False, drop_p=0.0, drop_seed=None, single=False):
-    """params: per layer [w_ig (2D,K), b_ig (2D), then per MLP block w1, b1, w2, b2]."""
+    """params: per layer [input_proj.W (D,K), global_skip_proj.W (D,K), input_proj.b, global_skip_proj.b,
+    then per MLP block w1, b1, w2, b2] (ShellConvolutionLayer._aimx_params())."""
     _lib.require_device(x)
     if x.dtype != _F32:
         raise _lib.AimxError("aimx: message passing runs in fp32 (the reference dtype)")
@@ -640,10 +672,53 @@ class _LinearBlock(torch.autograd.Function):
         return dx, dW1, db1, dW2, db2, None, None, None, None
 
 
-def linear_block(x, W1, b1, W2, b2, act, drop_p=0.0, training=False, skip=False):
-    """reference LinearBlock.forward (layers.py:204-219) with skip_proj = None."""
+def linear_block(x, W1, b1, W2, b2, act, drop_p=0.0, training=False, skip=False, seed=None):
+    """reference LinearBlock.forward (layers.py:204-219) with skip_proj = None. seed: optional
+    int64 [1] device tensor for the dropout hash (drawn here when None and dropout is active)."""
     _lib.require_device(x, W1, W2)
     kind = _lib.ACT_KIND[act] if isinstance(act, str) else int(act)
-    seed = (torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64)
-            if (training and drop_p > 0) else None)
+    if not (training and drop_p > 0):
+        seed = None
+    elif seed is None:
+        seed = torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64)
     return _LinearBlock.apply(x, W1, b1, W2, b2, kind, float(drop_p), bool(skip), seed)
+
+
+# ---------------------------------------------------------------------------------------------
+# L1 losses (trainer.py:24-35: nn.L1Loss; models/losses.py:14-48: WeightedL1Loss)
+# ---------------------------------------------------------------------------------------------
+class _L1Loss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target, weights, per_sample):
+        lib = _lib.load()
+        p, ldp = _rows(pred.reshape(pred.shape[0], -1) if pred.dim() != 2 else pred)
+        t, ldt = _rows(target.reshape(target.shape[0], -1) if target.dim() != 2 else target)
+        rows, cols = p.shape
+        w = weights.contiguous().float() if weights is not None else None
+        loss = torch.empty((), dtype=_F32, device=pred.device)
+        check(lib.aimx_l1_loss_forward(ptr(p), ldp, ptr(t), ldt, rows, cols, ptr(w), int(per_sample), ptr(loss),
+                                       stream_ptr(pred.device)), "l1_loss_forward")
+        ctx.save_for_backward(p, t, w)
+        ctx.meta = (ldp, ldt, int(per_sample), pred.shape)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        p, t, w = ctx.saved_tensors
+        ldp, ldt, per_sample, shape = ctx.meta
+        rows, cols = p.shape
+        g = g.contiguous()
+        dp = torch.empty(rows, cols, dtype=_F32, device=p.device)
+        check(lib.aimx_l1_loss_backward(ptr(p), ldp, ptr(t), ldt, rows, cols, ptr(w), per_sample, ptr(g), ptr(dp),
+                                        cols, stream_ptr(p.device)), "l1_loss_backward")
+        return dp.view(shape), None, None, None
+
+
+def l1_loss(pred, target, weights=None, per_sample=False):
+    """mean |pred - target| (per_sample=False, weights None: nn.L1Loss) or
+    mean over samples of sum_t w_t |pred - target| (per_sample=True: WeightedL1Loss)."""
+    _lib.require_device(pred, target)
+    if pred.shape != target.shape or pred.dtype != _F32 or target.dtype != _F32:
+        raise _lib.AimxError("aimx.l1_loss: pred and target must be fp32 tensors of one shape")
+    return _L1Loss.apply(pred, target, weights, bool(per_sample))

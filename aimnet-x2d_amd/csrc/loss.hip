@@ -1,0 +1,77 @@
+// Fused L1 losses of the train step (one launch forward, one launch backward).
+//
+// Reference: trainer._setup_loss_function, src/training/trainer.py:24-35 — nn.L1Loss() for a
+// single task (mean |y_pred - y_true| over all elements) and WeightedL1Loss for multitask,
+// src/models/losses.py:14-48 (sum over tasks of w_t |y_pred - y_true|, mean over samples). Both are
+//   loss = (1 / div) * sum_{i,t} w_t |p_it - y_it|   (w = 1, div = rows*cols | w, div = rows)
+// and d p_it = sign(p_it - y_it) * w_t * dloss / div (sign(0) = 0, as ATen's l1_loss backward).
+// The forward is one workgroup (the loss is per molecule: rows*cols is a few thousand) with a
+// fixed reduction order, so it is deterministic.
+#include <algorithm>
+
+#include "aimx_common.h"
+
+namespace aimx {
+namespace {
+
+__global__ __launch_bounds__(256) void k_l1_fwd(const float* __restrict__ p, int64_t ldp, const float* __restrict__ y,
+                                                int64_t ldy, int64_t rows, int64_t cols,
+                                                const float* __restrict__ w, float inv_div, float* __restrict__ loss) {
+  __shared__ float part[4];
+  float s = 0.f;
+  const int64_t n = rows * cols;
+  for (int64_t e = threadIdx.x; e < n; e += 256) {
+    const int64_t i = e / cols, t = e - i * cols;
+    const float d = fabsf(p[i * ldp + t] - y[i * ldy + t]);
+    s += w ? d * w[t] : d;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = ((part[0] + part[1]) + (part[2] + part[3])) * inv_div;
+}
+
+__global__ void k_l1_bwd(const float* __restrict__ p, int64_t ldp, const float* __restrict__ y, int64_t ldy,
+                         int64_t rows, int64_t cols, const float* __restrict__ w, float inv_div,
+                         const float* __restrict__ dloss, float* __restrict__ dp, int64_t ldd) {
+  const int64_t n = rows * cols;
+  const float g = dloss[0] * inv_div;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / cols, t = e - i * cols;
+    const float d = p[i * ldp + t] - y[i * ldy + t];
+    const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+    dp[i * ldd + t] = sg * (w ? w[t] : 1.f) * g;
+  }
+}
+
+}  // namespace
+}  // namespace aimx
+
+using namespace aimx;
+
+extern "C" int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
+                                    int64_t cols, const float* weights, int32_t per_sample, float* loss,
+                                    aimx_stream_t stream) {
+  if (rows < 0 || cols < 0 || !loss || ldp < cols || ldt < cols) return AIMX_EARG;
+  if (rows * cols > 0 && (!pred || !target)) return AIMX_EARG;
+  const double div = per_sample ? (double)rows : (double)rows * (double)cols;
+  const float inv = div > 0 ? (float)(1.0 / div) : __builtin_nanf("");  // mean of nothing: NaN, as ATen
+  hipLaunchKernelGGL(k_l1_fwd, dim3(1), dim3(256), 0, (hipStream_t)stream, pred, ldp, target, ldt, rows, cols, weights,
+                     inv, loss);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
+extern "C" int aimx_l1_loss_backward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
+                                     int64_t cols, const float* weights, int32_t per_sample, const float* d_loss,
+                                     float* d_pred, int64_t ldd, aimx_stream_t stream) {
+  if (rows < 0 || cols < 0 || ldp < cols || ldt < cols || ldd < cols || !d_loss) return AIMX_EARG;
+  if (rows * cols == 0) return AIMX_OK;
+  if (!pred || !target || !d_pred) return AIMX_EARG;
+  const double div = per_sample ? (double)rows : (double)rows * (double)cols;
+  const int64_t blocks = std::min<int64_t>(cdiv(rows * cols, 256), 1024);
+  hipLaunchKernelGGL(k_l1_bwd, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, pred, ldp, target, ldt, rows,
+                     cols, weights, (float)(1.0 / div), d_loss, d_pred, ldd);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}

@@ -112,9 +112,21 @@ class GNN(nn.Module):
 
         plan = GraphPlan(atom_embeddings.shape[0], self.num_shells, edges=multi_hop_edge_indices,
                          batch=batch_indices, num_graphs=total_charges.shape[0])
-        x_other_updated = self._message_passing_forward(x_other, multi_hop_edge_indices, batch_indices,
-                                                        total_charges, tetrahedral_indices, cis_indices,
-                                                        trans_indices, plan=plan)
+        # every dropout seed of this forward (message-passing stack + FFN blocks) from ONE draw
+        blocks = list(self.ffn.layers)
+        need = (self.message_passing_layers[0]._aimx_dropout()[0] if len(self.message_passing_layers) else False) or \
+            any(b.dropout.training and b.dropout.p > 0 for b in blocks)
+        if need:  # (MC-dropout may switch single Dropout modules on in eval mode: follow their flags)
+            seeds = torch.randint(0, 2 ** 62, (1 + len(blocks),), device=atom_embeddings.device, dtype=torch.int64)
+            self._aimx_stack_seed = seeds[0:1]
+            for i, blk in enumerate(blocks):
+                blk._aimx_seed = seeds[1 + i:2 + i]
+        try:
+            x_other_updated = self._message_passing_forward(x_other, multi_hop_edge_indices, batch_indices,
+                                                            total_charges, tetrahedral_indices, cis_indices,
+                                                            trans_indices, plan=plan)
+        finally:
+            self._aimx_stack_seed = None
         partial_charges = None
         if self.use_partial_charges and x_other_updated.shape[-1] >= 2:
             partial_charges = x_other_updated[:, 0].clone()
@@ -126,7 +138,11 @@ class GNN(nn.Module):
         finally:
             self.pooling._aimx_plan = None
 
-        x = self.ffn(self.post_pooling_projection(x_pooled))
+        try:
+            x = self.ffn(self.post_pooling_projection(x_pooled))
+        finally:
+            for blk in blocks:
+                blk._aimx_seed = None
         skip_connection = self.skip_transform(x)
         output = self.output_layer(torch.cat([x, skip_connection], dim=-1))
         return output, attention_weights, partial_charges
@@ -150,7 +166,9 @@ class GNN(nn.Module):
         layers = self.message_passing_layers
         first = layers[0]
         training, p = first._aimx_dropout()
-        seed = torch.randint(0, 2 ** 62, (1,), device=x_other.device, dtype=torch.int64) if training else None
+        seed = getattr(self, "_aimx_stack_seed", None)
+        if training and seed is None:
+            seed = torch.randint(0, 2 ** 62, (1,), device=x_other.device, dtype=torch.int64)
         if not self.use_stereochemistry:
             params = []
             for layer in layers:

@@ -46,12 +46,12 @@ class ShellConvolutionLayer(nn.Module):
 
     # -- kernel plumbing -------------------------------------------------------------------
     def _aimx_params(self):
-        """[w_ig, b_ig, (w1, b1, w2, b2) per block] with w_ig = [input_proj.W ; global_skip_proj.W]."""
+        """[input_proj.W, global_skip_proj.W, input_proj.b, global_skip_proj.b, (w1, b1, w2, b2) per
+        block]; the operator packs [Wi ; Wg] of all layers with one cat kernel."""
         if self.global_skip_proj is None or self._atom_input_dim != self._output_dim or len(self.mlp_blocks) == 0:
             raise NotImplementedError("aimx: ShellConvolutionLayer needs global_skip_proj, equal in/out width and "
                                       ">= 1 MLP block (every reference configuration does)")
-        p = [torch.cat([self.input_proj.weight, self.global_skip_proj.weight], 0),
-             torch.cat([self.input_proj.bias, self.global_skip_proj.bias], 0)]
+        p = [self.input_proj.weight, self.global_skip_proj.weight, self.input_proj.bias, self.global_skip_proj.bias]
         for b in self.mlp_blocks:
             p += [b["linear_1"].weight, b["linear_1"].bias, b["linear_2"].weight, b["linear_2"].bias]
         return p
@@ -113,9 +113,10 @@ class LinearBlock(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # one fused operator: linear1 + activation + dropout (hash mask, honours self.dropout's
         # training flag) + linear2 + skip, with a fused backward (aimx.ops.linear_block)
+        # (GNN.forward may hand every block its dropout seed from one draw: _aimx_seed)
         return ops.linear_block(x, self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias,
                                 activation_name(self.activation), self.dropout.p, self.dropout.training,
-                                self.use_skip)
+                                self.use_skip, seed=getattr(self, "_aimx_seed", None))
 
 
 class MultiLayerPerceptron(nn.Module):

@@ -252,7 +252,8 @@ def main():
     from utils.distributed import GradientSync
     model = build_model(cfg, device)
     B = cfg["batch"]
-    loss_fn = torch.nn.L1Loss()
+    from models import L1Loss
+    loss_fn = L1Loss()  # the reference criterion (nn.L1Loss, trainer.py:34) as one fused launch each way
 
     if args.graph:
         # Whole-step HIP-graph capture on static padded inputs: the captured step is the full

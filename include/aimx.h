@@ -344,6 +344,22 @@ int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const AimxAdamHype
                     const float* lr, float* norm_out, void* workspace, size_t workspace_bytes,
                     aimx_stream_t stream);
 
+/* ------------------------------------------------------------------------------------------
+ * L1 losses of the train step (reference trainer.py:24-35: nn.L1Loss for one task,
+ * WeightedL1Loss src/models/losses.py:14-48 for multitask):
+ *   loss = (1/div) * sum_{i<rows, t<cols} w_t |pred[i,t] - target[i,t]|
+ *   div = rows (per_sample != 0: sum over tasks, mean over samples) or rows*cols (mean);
+ *   weights NULL = all ones. loss is one device float. Backward:
+ *   d_pred[i,t] = sign(pred - target) * w_t * d_loss[0] / div  (sign(0) = 0).
+ * One deterministic workgroup for the forward (rows*cols is per molecule: a few thousand).
+ * ------------------------------------------------------------------------------------------ */
+int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
+                         int64_t cols, const float* weights, int32_t per_sample, float* loss,
+                         aimx_stream_t stream);
+int aimx_l1_loss_backward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
+                          int64_t cols, const float* weights, int32_t per_sample, const float* d_loss,
+                          float* d_pred, int64_t ldd, aimx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -583,3 +583,26 @@ def test_hop_segment_aligned_tiles_bit_exact():
         grads.append(xg.grad.cpu())
     assert torch.equal(outs[0], ref) and torch.equal(outs[1], ref)
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("rows,cols,weighted", [(520, 1, False), (512, 12, False), (512, 12, True), (3, 5, True)])
+def test_l1_losses_match_reference_criteria(rows, cols, weighted):
+    """models.L1Loss == nn.L1Loss and models.WeightedL1Loss == the reference's WeightedL1Loss
+    (losses.py:14-48: sum over tasks of w |p - y|, mean over samples): values and gradients,
+    including exact ties (sign(0) = 0)."""
+    from models import L1Loss, WeightedL1Loss
+    g = torch.Generator().manual_seed(rows + cols)
+    p = torch.randn(rows, cols, generator=g)
+    y = torch.randn(rows, cols, generator=g)
+    y[0, 0] = p[0, 0]  # a tie
+    w = torch.rand(cols, generator=g) + 0.5
+    pg = p.to(DEV).requires_grad_()
+    crit = WeightedL1Loss(w).to(DEV) if weighted else L1Loss()
+    loss = crit(pg, y.to(DEV))
+    loss.backward()
+    p64 = p.double().requires_grad_()
+    ref = ((p64 - y.double()).abs() * w.double()).sum(1).mean() if weighted else (p64 - y.double()).abs().mean()
+    ref.backward()
+    assert abs(loss.item() - ref.item()) <= 1e-6 * max(1.0, abs(ref.item()))
+    assert (pg.grad.cpu().double() - p64.grad).abs().max().item() <= 1e-7
+    assert pg.grad[0, 0].item() == 0.0

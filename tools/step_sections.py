@@ -32,7 +32,8 @@ def main():
     batches = bench.make_batches(cfg, 2, 1234, dev, pad=True)
     model = bench.build_model(cfg, dev)
     B = cfg["batch"]
-    loss_fn = torch.nn.L1Loss()
+    from models import L1Loss
+    loss_fn = L1Loss()
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
     static = batches[0].clone()
 
