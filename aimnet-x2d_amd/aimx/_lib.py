@@ -76,6 +76,35 @@ class ShellStackGrad(ctypes.Structure):
     ]
 
 
+HEAD_MAX_BLOCKS = 8
+
+
+class Head(ctypes.Structure):
+    _fields_ = [
+        ("G", c_i64), ("F", c_i64), ("H_in", c_i64), ("T", c_i64),
+        ("nb", c_i32), ("act", c_i32), ("training", c_i32),
+        ("drop_p", c_f32), ("seed", c_ptr),
+        ("x0", c_ptr), ("ldx0", c_i64),
+        ("wp", c_ptr), ("bp", c_ptr),
+        ("w1", c_ptr * HEAD_MAX_BLOCKS), ("b1", c_ptr * HEAD_MAX_BLOCKS),
+        ("w2", c_ptr * HEAD_MAX_BLOCKS), ("b2", c_ptr * HEAD_MAX_BLOCKS),
+        ("skip", c_i32 * HEAD_MAX_BLOCKS),
+        ("ws", c_ptr), ("bs", c_ptr), ("wo", c_ptr), ("bo", c_ptr),
+        ("y0", c_ptr), ("v", c_ptr * HEAD_MAX_BLOCKS), ("hid", c_ptr * HEAD_MAX_BLOCKS),
+        ("mask", c_ptr * HEAD_MAX_BLOCKS), ("z", c_ptr * HEAD_MAX_BLOCKS), ("cat", c_ptr),
+        ("out", c_ptr), ("ldo", c_i64),
+    ]
+
+
+class HeadGrad(ctypes.Structure):
+    _fields_ = [
+        ("d_out", c_ptr), ("ld_dout", c_i64),
+        ("d_x0", c_ptr), ("ld_dx0", c_i64),
+        ("ds", c_ptr), ("dz", c_ptr * HEAD_MAX_BLOCKS), ("dv", c_ptr * HEAD_MAX_BLOCKS), ("dy0", c_ptr),
+        ("workspace", c_ptr), ("workspace_bytes", c_size),
+    ]
+
+
 class EmbeddingTables(ctypes.Structure):
     _fields_ = [
         ("n_tables", c_i32), ("dim", c_i64),
@@ -136,6 +165,9 @@ _SIGS = {
     "aimx_embedding_backward_workspace_bytes": (c_size, [ctypes.POINTER(EmbeddingTables), c_i64]),
     "aimx_embedding_backward": (c_i32, [ctypes.POINTER(EmbeddingTables), c_i64, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "aimx_act_backward": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_head_forward": (c_i32, [ctypes.POINTER(Head), c_ptr]),
+    "aimx_head_backward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
+    "aimx_head_backward": (c_i32, [ctypes.POINTER(Head), ctypes.POINTER(HeadGrad), c_ptr]),
     "aimx_l1_loss_forward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr]),
     "aimx_l1_loss_backward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_i64,
                                       c_ptr]),

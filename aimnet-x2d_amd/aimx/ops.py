@@ -722,3 +722,134 @@ def l1_loss(pred, target, weights=None, per_sample=False):
     if pred.shape != target.shape or pred.dtype != _F32 or target.dtype != _F32:
         raise _lib.AimxError("aimx.l1_loss: pred and target must be fp32 tensors of one shape")
     return _L1Loss.apply(pred, target, weights, bool(per_sample))
+
+
+# ---------------------------------------------------------------------------------------------
+# Fused post-pool head (gnn.py:252-258; MultiLayerPerceptron / LinearBlock layers.py:170-267)
+# ---------------------------------------------------------------------------------------------
+HEAD_MAX_F = 256
+
+
+class _Head(torch.autograd.Function):
+    """Forward: one launch (aimx_head_forward). Backward: one launch for the input-gradient chain
+    (aimx_head_backward) + one grouped launch for every weight and bias gradient."""
+
+    @staticmethod
+    def forward(ctx, spec, seed, x0, wp, bp, *rest):
+        lib = _lib.load()
+        dev = x0.device
+        nb = spec["nb"]
+        blocks = [rest[4 * i:4 * i + 4] for i in range(nb)]
+        ws_, bs_, wo, bo = rest[4 * nb:4 * nb + 4]
+        x0, ldx0 = _rows(x0)
+        G, Hin = x0.shape
+        F, T = wp.shape[0], wo.shape[0]
+        drop = bool(spec["training"]) and spec["drop_p"] > 0 and seed is not None
+        ar = Arena(dev)
+        iy0 = ar.add(G, F)
+        iv = [ar.add(G, F) for _ in range(nb)]
+        ih = [ar.add(G, F) for _ in range(nb)]
+        iz = [ar.add(G, F) for _ in range(nb)]
+        icat = ar.add(G, 2 * F)
+        buf, views = ar.alloc()
+        masks = [torch.empty(G, F, dtype=torch.uint8, device=dev) for _ in range(nb)] if drop else []
+        out = torch.empty(G, T, dtype=_F32, device=dev)
+        h = _lib.Head()
+        h.G, h.F, h.H_in, h.T = G, F, Hin, T
+        h.nb, h.act, h.training = nb, spec["act"], int(drop)
+        h.drop_p, h.seed = float(spec["drop_p"]) if drop else 0.0, ptr(seed) if drop else None
+        h.x0, h.ldx0 = ptr(x0), ldx0
+        wts = [wp.contiguous(), bp.contiguous()] + [t.contiguous() for t in rest]
+        h.wp, h.bp = ptr(wts[0]), ptr(wts[1])
+        for i in range(nb):
+            w1, b1, w2, b2 = wts[2 + 4 * i:6 + 4 * i]
+            h.w1[i], h.b1[i], h.w2[i], h.b2[i] = ptr(w1), ptr(b1), ptr(w2), ptr(b2)
+            h.skip[i] = int(spec["skip"][i])
+            h.v[i], h.hid[i], h.z[i] = ptr(views[iv[i]]), ptr(views[ih[i]]), ptr(views[iz[i]])
+            h.mask[i] = ptr(masks[i]) if drop else None
+        h.ws, h.bs, h.wo, h.bo = [ptr(t) for t in wts[2 + 4 * nb:6 + 4 * nb]]
+        h.y0, h.cat = ptr(views[iy0]), ptr(views[icat])
+        h.out, h.ldo = ptr(out), T
+        check(lib.aimx_head_forward(h, stream_ptr(dev)), "head_forward")
+        ctx.spec, ctx.drop = spec, drop
+        ctx.save_for_backward(x0, seed if drop else None, *wts)
+        ctx.state = dict(buf=buf, views=views, iy0=iy0, iv=iv, ih=ih, iz=iz, icat=icat, masks=masks)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        lib = _lib.load()
+        spec, st = ctx.spec, ctx.state
+        x0, seed, *wts = ctx.saved_tensors
+        nb = spec["nb"]
+        dev = x0.device
+        G, Hin = x0.shape
+        F, T = wts[0].shape[0], wts[-2].shape[0]
+        views = st["views"]
+        d_out = d_out.contiguous()
+        ar = Arena(dev)
+        ids = ar.add(G, F)
+        idz = [ar.add(G, F) for _ in range(nb)]
+        idv = [ar.add(G, F) for _ in range(nb)]
+        idy0 = ar.add(G, F)
+        gbuf, gv = ar.alloc()
+        d_x0 = torch.empty(G, Hin, dtype=_F32, device=dev)
+        h = _lib.Head()
+        h.G, h.F, h.H_in, h.T = G, F, Hin, T
+        h.nb, h.act, h.training = nb, spec["act"], int(ctx.drop)
+        h.drop_p, h.seed = float(spec["drop_p"]) if ctx.drop else 0.0, ptr(seed) if ctx.drop else None
+        h.x0, h.ldx0 = ptr(x0), x0.stride(0)
+        h.wp, h.bp = ptr(wts[0]), ptr(wts[1])
+        for i in range(nb):
+            w1, b1, w2, b2 = wts[2 + 4 * i:6 + 4 * i]
+            h.w1[i], h.b1[i], h.w2[i], h.b2[i] = ptr(w1), ptr(b1), ptr(w2), ptr(b2)
+            h.skip[i] = int(spec["skip"][i])
+            h.v[i], h.hid[i], h.z[i] = ptr(views[st["iv"][i]]), ptr(views[st["ih"][i]]), ptr(views[st["iz"][i]])
+            h.mask[i] = ptr(st["masks"][i]) if ctx.drop else None
+        h.ws, h.bs, h.wo, h.bo = [ptr(t) for t in wts[2 + 4 * nb:6 + 4 * nb]]
+        h.y0, h.cat = ptr(views[st["iy0"]]), ptr(views[st["icat"]])
+        h.out, h.ldo = ptr(d_out), T  # unused by the backward (validity only)
+        dg = _lib.HeadGrad()
+        dg.d_out, dg.ld_dout = ptr(d_out), T
+        dg.d_x0, dg.ld_dx0 = ptr(d_x0), Hin
+        dg.ds, dg.dy0 = ptr(gv[ids]), ptr(gv[idy0])
+        for i in range(nb):
+            dg.dz[i], dg.dv[i] = ptr(gv[idz[i]]), ptr(gv[idv[i]])
+        wsb = lib.aimx_head_backward_workspace_bytes(h)
+        hws = torch.empty(max(wsb // 4, 1), dtype=_F32, device=dev)
+        dg.workspace, dg.workspace_bytes = ptr(hws), wsb
+        check(lib.aimx_head_backward(h, dg, stream_ptr(dev)), "head_backward")
+        # every weight / bias gradient: dW = dY^T X over the G molecules, one grouped launch
+        new = lambda *shape: torch.empty(*shape, dtype=_F32, device=dev)  # noqa: E731
+        grads = [new(*t.shape) for t in wts]
+        y = [views[st["iy0"]]] + [views[st["iz"][i]] for i in range(nb - 1)]
+        probs = [(gv[idy0], x0, grads[0], grads[1])]
+        for i in range(nb):
+            probs.append((gv[idv[i]], y[i], grads[2 + 4 * i], grads[3 + 4 * i]))
+            probs.append((gv[idz[i]], views[st["ih"][i]], grads[4 + 4 * i], grads[5 + 4 * i]))
+        cat = views[st["icat"]]
+        probs.append((gv[ids], views[st["iz"][nb - 1]], grads[2 + 4 * nb], grads[3 + 4 * nb]))
+        probs.append((d_out, cat, grads[4 + 4 * nb], grads[5 + 4 * nb]))
+        ws = wgrad_grouped(probs)
+        del ws, gbuf, hws
+        return (None, None, d_x0, *grads)
+
+
+def head(x_pooled, wp, bp, blocks, ws, bs, wo, bo, *, act, drop_p=0.0, training=False, seed=None, skips=None):
+    """out = output_layer([z | skip_transform(z)]), z = ffn(post_pooling_projection(x_pooled)) as the
+    fused head (reference gnn.py:252-258). blocks: [(W1, b1, W2, b2)] of the LinearBlocks, skips:
+    their use_skip flags. seed: int64 [1] device tensor when dropout is active."""
+    _lib.require_device(x_pooled, wp, wo)
+    nb = len(blocks)
+    if not (1 <= nb <= _lib.HEAD_MAX_BLOCKS):
+        raise _lib.AimxError("aimx.head: 1..8 LinearBlocks")
+    kind = _lib.ACT_KIND[act] if isinstance(act, str) else int(act)
+    drop = bool(training) and drop_p > 0
+    if drop and seed is None:
+        seed = torch.randint(0, 2 ** 62, (1,), device=x_pooled.device, dtype=torch.int64)
+    spec = dict(nb=nb, act=kind, training=bool(training), drop_p=float(drop_p),
+                skip=tuple(bool(s) for s in (skips or [False] * nb)))
+    flat = []
+    for b in blocks:
+        flat += list(b)
+    return _Head.apply(spec, seed if drop else None, x_pooled, wp, bp, *flat, ws, bs, wo, bo)

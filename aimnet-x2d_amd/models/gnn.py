@@ -15,6 +15,7 @@ Embedding lookups, the embedding/concat projections (N x hidden, hipBLASLt) and 
 FFN stay on PyTorch. Stereochemistry (off in every BASELINE config) is plain PyTorch around the
 per-layer HIP operators, as the reference computes it (gnn.py:310-509).
 """
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -139,13 +140,45 @@ class GNN(nn.Module):
             self.pooling._aimx_plan = None
 
         try:
-            x = self.ffn(self.post_pooling_projection(x_pooled))
+            if self._aimx_head_ok():
+                # gnn.py:252-258 as one fused operator forward and backward (aimx.ops.head)
+                b0 = blocks[0]
+                output = ops.head(
+                    x_pooled, self.post_pooling_projection.weight, self.post_pooling_projection.bias,
+                    [(b.linear1.weight, b.linear1.bias, b.linear2.weight, b.linear2.bias) for b in blocks],
+                    self.skip_transform.weight, self.skip_transform.bias, self.output_layer.weight,
+                    self.output_layer.bias, act=activation_name(b0.activation), drop_p=b0.dropout.p,
+                    training=b0.dropout.training, seed=getattr(b0, "_aimx_seed", None),
+                    skips=[b.use_skip for b in blocks])
+            else:
+                x = self.ffn(self.post_pooling_projection(x_pooled))
+                skip_connection = self.skip_transform(x)
+                output = self.output_layer(torch.cat([x, skip_connection], dim=-1))
         finally:
             for blk in blocks:
                 blk._aimx_seed = None
-        skip_connection = self.skip_transform(x)
-        output = self.output_layer(torch.cat([x, skip_connection], dim=-1))
         return output, attention_weights, partial_charges
+
+    def _aimx_head_ok(self) -> bool:
+        """The fused head covers the reference's post-pool chain when every LinearBlock is F -> F
+        with one activation and one dropout setting, F <= 256, F and the input width multiples of 32
+        (AIMX_NO_FUSED_HEAD=1 disables)."""
+        if os.environ.get("AIMX_NO_FUSED_HEAD", "0") == "1":
+            return False
+        pp, blocks = self.post_pooling_projection, list(self.ffn.layers)
+        F = pp.out_features
+        if not (32 <= F <= ops.HEAD_MAX_F and F % 32 == 0 and pp.in_features % 32 == 0 and 1 <= len(blocks) <= 8):
+            return False
+        if self.skip_transform.in_features != F or self.skip_transform.out_features != F or \
+                self.output_layer.in_features != 2 * F:
+            return False
+        b0 = blocks[0]
+        for b in blocks:
+            if b.skip_proj is not None or b.linear1.in_features != F or b.linear1.out_features != F or \
+                    b.linear2.out_features != F or type(b.activation) is not type(b0.activation) or \
+                    b.dropout.p != b0.dropout.p or b.dropout.training != b0.dropout.training:
+                return False
+        return True
 
     def _embed_atomic_features(self, atom_features: Dict[str, torch.Tensor]) -> torch.Tensor:
         return torch.cat([

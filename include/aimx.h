@@ -345,6 +345,51 @@ int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const AimxAdamHype
                     aimx_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Fused post-pool head (reference gnn.py:252-258 with MultiLayerPerceptron / LinearBlock,
+ * layers.py:170-267):
+ *   y0 = x0 Wp^T + bp
+ *   per block i < nb: v_i = y_i W1_i^T + b1_i ; h_i = dropout(act(v_i)) ;
+ *                     z_i = h_i W2_i^T + b2_i (+ y_i when skip[i]) ; y_{i+1} = z_i
+ *   s = z Ws^T + bs ; cat = [z | s] ; out = cat Wo^T + bo          (z = z_{nb-1})
+ * G rows (molecules), F = ffn width (32 <= F <= 256, F % 32 == 0), H_in = input width (% 32 == 0),
+ * T outputs. Weights row-major [out, in] (nn.Linear), 16-byte aligned. Dropout: hash mask of
+ * (seed, salt 0x4EAD + i, row * F + col), p = drop_p, active when training != 0 and seed != NULL.
+ * The forward saves (caller-owned, [G, F] row-major unless noted): y0, v[i], hid[i] (= h_i),
+ * mask[i] (uint8, when dropout is active), z[i], cat [G, 2F]; it writes out [G, T] (ld ldo).
+ * The backward (AimxHeadGrad) runs the input-gradient chain given d_out: it writes d_x0 and the
+ * activation gradients the weight gradients need: ds (= d s), dz[i] (= d z_i), dv[i] (= d v_i),
+ * dy0 (= d y0). The weight gradients are then plain dW = dY^T X products (aimx_wgrad_grouped):
+ *   Wo: (d_out, cat)  Ws: (ds, z)  W2_i: (dz[i], hid[i])  W1_i: (dv[i], y_i = i ? z[i-1] : y0)
+ *   Wp: (dy0, x0)
+ * ------------------------------------------------------------------------------------------ */
+#define AIMX_HEAD_MAX_BLOCKS 8
+typedef struct AimxHead {
+  int64_t G, F, H_in, T;
+  int32_t nb, act, training;
+  float drop_p; const int64_t* seed;
+  const float* x0; int64_t ldx0;
+  const float* wp; const float* bp;
+  const float* w1[AIMX_HEAD_MAX_BLOCKS]; const float* b1[AIMX_HEAD_MAX_BLOCKS];
+  const float* w2[AIMX_HEAD_MAX_BLOCKS]; const float* b2[AIMX_HEAD_MAX_BLOCKS];
+  int32_t skip[AIMX_HEAD_MAX_BLOCKS];
+  const float* ws; const float* bs; const float* wo; const float* bo;
+  float* y0; float* v[AIMX_HEAD_MAX_BLOCKS]; float* hid[AIMX_HEAD_MAX_BLOCKS];
+  uint8_t* mask[AIMX_HEAD_MAX_BLOCKS]; float* z[AIMX_HEAD_MAX_BLOCKS]; float* cat;
+  float* out; int64_t ldo;
+} AimxHead;
+
+typedef struct AimxHeadGrad {
+  const float* d_out; int64_t ld_dout;
+  float* d_x0; int64_t ld_dx0;
+  float* ds; float* dz[AIMX_HEAD_MAX_BLOCKS]; float* dv[AIMX_HEAD_MAX_BLOCKS]; float* dy0;
+  void* workspace; size_t workspace_bytes;  /* aimx_head_backward_workspace_bytes(h), 16-B aligned */
+} AimxHeadGrad;
+
+int aimx_head_forward(const AimxHead* h, aimx_stream_t stream);
+size_t aimx_head_backward_workspace_bytes(const AimxHead* h);
+int aimx_head_backward(const AimxHead* h, const AimxHeadGrad* d, aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
  * L1 losses of the train step (reference trainer.py:24-35: nn.L1Loss for one task,
  * WeightedL1Loss src/models/losses.py:14-48 for multitask):
  *   loss = (1/div) * sum_{i<rows, t<cols} w_t |pred[i,t] - target[i,t]|

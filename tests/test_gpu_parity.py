@@ -606,3 +606,52 @@ def test_l1_losses_match_reference_criteria(rows, cols, weighted):
     assert abs(loss.item() - ref.item()) <= 1e-6 * max(1.0, abs(ref.item()))
     assert (pg.grad.cpu().double() - p64.grad).abs().max().item() <= 1e-7
     assert pg.grad[0, 0].item() == 0.0
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+def test_fused_head_matches_module_path(name, monkeypatch):
+    """The fused post-pool head (one launch forward, one + a grouped weight-gradient launch
+    backward) against the per-module path (post_pooling_projection -> ffn -> skip_transform ->
+    output_layer on the fused GEMM ops): outputs and every gradient, eval mode."""
+    z, cfg, _ = load_case(name)
+    af, edges, batch, tc = load_case(name, DEV)[2]
+    e_empty = torch.empty(0, 2, dtype=torch.long, device=DEV)
+    w = torch.from_numpy(z["loss_w"]).to(DEV)
+    res = []
+    for off in ("0", "1"):
+        monkeypatch.setenv("AIMX_NO_FUSED_HEAD", off)
+        model = _build_model(cfg, int(z["seed"]))
+        assert model._aimx_head_ok() == (off == "0")
+        out, _, _ = model(af, edges, batch, tc, torch.empty(0, 4, dtype=torch.long, device=DEV), e_empty, e_empty)
+        (out * w).sum().backward()
+        g = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+        res.append((out.detach().clone(), g))
+    (o1, g1), (o2, g2) = res
+    assert norm_rel(o1.cpu().numpy(), o2.cpu().numpy()) < 2e-6
+    assert g1.keys() == g2.keys()
+    for k in g1:
+        if "attention_weights" in k and k.endswith("bias"):
+            continue  # exactly 0 in exact arithmetic (softmax shift invariance): both are ~1e-19 noise
+        assert norm_rel(g1[k].cpu().numpy(), g2[k].cpu().numpy()) < 2e-5, k
+
+
+def test_fused_head_dropout():
+    """Train mode: ~p of the head's hidden units dropped, a fixed seed is deterministic, another
+    seed differs, and the backward runs (finite gradients)."""
+    from aimx import ops
+    g = torch.Generator().manual_seed(0)
+    F, G = 256, 300
+    mk = lambda *s: (torch.randn(*s, generator=g) * 0.1).to(DEV).requires_grad_()  # noqa: E731
+    x = mk(G, F)
+    wp, bp = mk(F, F), mk(F)
+    blocks = [(mk(F, F), mk(F), mk(F, F), mk(F)) for _ in range(3)]
+    ws, bs, wo, bo = mk(F, F), mk(F), mk(3, 2 * F), mk(3)
+    kw = dict(act="silu", drop_p=0.2, training=True, skips=[False, True, False])
+    s1 = torch.tensor([7], device=DEV)
+    y1 = ops.head(x, wp, bp, blocks, ws, bs, wo, bo, seed=s1, **kw)
+    y2 = ops.head(x, wp, bp, blocks, ws, bs, wo, bo, seed=s1.clone(), **kw)
+    y3 = ops.head(x, wp, bp, blocks, ws, bs, wo, bo, seed=torch.tensor([8], device=DEV), **kw)
+    y0 = ops.head(x, wp, bp, blocks, ws, bs, wo, bo, **dict(kw, training=False))
+    assert torch.equal(y1, y2) and not torch.equal(y1, y3) and not torch.equal(y0, y1)
+    y1.sum().backward()
+    assert all(torch.isfinite(t.grad).all() for t in [x, wp, bp, ws, bs, wo, bo] + [p for b in blocks for p in b])
