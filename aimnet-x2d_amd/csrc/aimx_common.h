@@ -83,4 +83,11 @@ int launch_charge_bwd(const float* x, int64_t ldx, int64_t N, int64_t D, const i
                       int64_t G, const float* tc, const float* dout, int64_t ldd, float* dx, int64_t lddx,
                       hipStream_t s);
 
+// Fused node-update MLP of one shell layer (mlp.hip): all MLP blocks in one launch each way.
+bool mlp_fused_ok(int64_t D, int64_t nm);
+int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64_t ldx, float* out, int64_t ldo,
+                   hipStream_t st);
+int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t lddy, float* const* dV,
+                   float* const* dA, float* dug, hipStream_t st);
+
 }  // namespace aimx

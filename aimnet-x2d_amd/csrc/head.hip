@@ -183,9 +183,20 @@ __global__ __launch_bounds__(kThreads) void k_head_fwd(const AimxHead h) {
   const int F = (int)h.F, Hin = (int)h.H_in, T = (int)h.T;
   const int64_t G = h.G;
   // input rows (x_pooled) -> Cb (as a staging buffer for the first GEMM's A operand)
-  for (int e = threadIdx.x; e < kR * Hin; e += blockDim.x) {
-    const int r = e / Hin, c = e - r * Hin;
-    Cb[r * kS2 + c] = (g0 + r < G) ? h.x0[(g0 + r) * h.ldx0 + c] : 0.f;
+  for (int e0 = 0; e0 < kR * Hin; e0 += 8 * kThreads) {  // 8 loads in flight per thread
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * kThreads + threadIdx.x, r = e / Hin, c = e - r * Hin;
+      const bool ok = e < kR * Hin && g0 + r < G;
+      v[u] = h.x0[ok ? (g0 + r) * h.ldx0 + c : 0];
+      v[u] = ok ? v[u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * kThreads + threadIdx.x, r = e / Hin, c = e - r * Hin;
+      if (e < kR * Hin) Cb[r * kS2 + c] = v[u];
+    }
   }
   __syncthreads();
   // y0 = x0 Wp^T + bp

@@ -207,7 +207,23 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
       a.ldpre = D;
       RUN(run(a, ws, st));
     }
-    // 4) MLP blocks
+    // 4) MLP blocks: one fused launch for all of them (mlp.hip), or one GEMM per linear
+    if (mlp_fused_ok(D, nm)) {
+      float* dst;
+      int64_t ldd;
+      if (l == L - 1) {
+        dst = s->out;
+        ldd = s->out_ld;
+      } else if (s->use_pc) {
+        dst = s->X[l + 1];
+        ldd = D;
+      } else {
+        dst = s->F[l + 1];
+        ldd = K;
+      }
+      RUN(launch_mlp_fwd(s, l, s->mode_single ? nullptr : F, K, dst, ldd, st));
+      continue;
+    }
     for (int64_t k = 0; k < nm; ++k) {
       const int64_t idx = l * nm + k;
       const float* in = (k == 0) ? s->UG[l] : s->A[idx - 1];
@@ -375,7 +391,17 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     const float* dY = (l == L - 1) ? g->d_out : base + lay.dY + l * N * D;
     const int64_t ldy = (l == L - 1) ? g->d_out_ld : D;
     // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
-    for (int64_t k = nm - 1; k >= 0; --k) {
+    const bool fused = mlp_fused_ok(D, nm);
+    if (fused) {  // the whole chain + dUG = [du | dY] in one launch (mlp.hip)
+      float* dVs[8];
+      float* dAs[8];
+      for (int64_t k = 0; k < nm; ++k) {
+        dVs[k] = base + lay.dV + (l * nm + k) * N * D;
+        dAs[k] = (k < nm - 1) ? base + lay.dA + (l * (nm - 1) + k) * N * D : nullptr;
+      }
+      RUN(launch_mlp_bwd(s, l, dY, ldy, dVs, dAs, dUG, st));
+    }
+    for (int64_t k = nm - 1; k >= 0 && !fused; --k) {
       const int64_t idx = l * nm + k;
       const float* da_out = (k == nm - 1) ? dY : base + lay.dA + (l * (nm - 1) + k) * N * D;
       const int64_t ld_out = (k == nm - 1) ? ldy : D;
@@ -406,8 +432,8 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
         RUN(run(a, ws, st));
       }
     }
-    // dg = dY -> dUG[:, D:]
-    RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
+    // dg = dY -> dUG[:, D:] (the fused chain writes it itself)
+    if (!fused) RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
     if (aux) {  // fork: this layer's weight gradients run beside the rest of the chain
       hipEvent_t ev = (hipEvent_t)g->events[l];
       AIMX_CHECK_HIP(hipEventRecord(ev, st));
