@@ -68,7 +68,7 @@ PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from t
 
 
 def make_batches(cfg, n_batches, seed, device, pad=False):
-    """Device-resident batches. pad=True: static shapes for graph replay (one padding molecule)."""
+    """Device-resident batches. pad=True: static shapes for graph replay (PAD_MOLS padding molecules)."""
     cols = make_collated(cfg, n_batches, seed)
     if not pad:
         return [adata.DeviceBatch(c, device, targets=t, total_charges=q) for c, t, q in cols]
