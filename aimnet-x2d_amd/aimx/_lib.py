@@ -77,6 +77,7 @@ class ShellStackGrad(ctypes.Structure):
 
 
 HEAD_MAX_BLOCKS = 8
+HEAD_SYNC_WORDS = 68
 
 
 class Head(ctypes.Structure):
@@ -93,6 +94,7 @@ class Head(ctypes.Structure):
         ("y0", c_ptr), ("v", c_ptr * HEAD_MAX_BLOCKS), ("hid", c_ptr * HEAD_MAX_BLOCKS),
         ("mask", c_ptr * HEAD_MAX_BLOCKS), ("z", c_ptr * HEAD_MAX_BLOCKS), ("cat", c_ptr),
         ("out", c_ptr), ("ldo", c_i64),
+        ("sync", c_ptr), ("cluster", c_i32),
     ]
 
 
@@ -259,6 +261,25 @@ def counters(device):
         buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=device)
         _COUNTERS[key] = buf
     return buf
+
+
+_HEAD_SYNC = {}
+
+
+def head_sync(device):
+    """Per-device sync words of the clustered head kernels: zeroed once, kept zero by the kernels
+    (word 0 is the sticky timeout flag, see include/aimx.h AimxHead)."""
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    buf = _HEAD_SYNC.get(key)
+    if buf is None:
+        buf = torch.zeros(HEAD_SYNC_WORDS, dtype=torch.int32, device=device)
+        _HEAD_SYNC[key] = buf
+    return buf
+
+
+def head_cluster():
+    """Workgroups per 16-molecule tile of the fused head (AIMX_HEAD_CLUSTER, default 2)."""
+    return int(os.environ.get("AIMX_HEAD_CLUSTER", "2"))
 
 
 def ptr(t):

@@ -770,6 +770,7 @@ class _Head(torch.autograd.Function):
         h.ws, h.bs, h.wo, h.bo = [ptr(t) for t in wts[2 + 4 * nb:6 + 4 * nb]]
         h.y0, h.cat = ptr(views[iy0]), ptr(views[icat])
         h.out, h.ldo = ptr(out), T
+        h.sync, h.cluster = ptr(_lib.head_sync(dev)), spec["cluster"]
         check(lib.aimx_head_forward(h, stream_ptr(dev)), "head_forward")
         ctx.spec, ctx.drop = spec, drop
         ctx.save_for_backward(x0, seed if drop else None, *wts)
@@ -809,6 +810,7 @@ class _Head(torch.autograd.Function):
         h.ws, h.bs, h.wo, h.bo = [ptr(t) for t in wts[2 + 4 * nb:6 + 4 * nb]]
         h.y0, h.cat = ptr(views[st["iy0"]]), ptr(views[st["icat"]])
         h.out, h.ldo = ptr(d_out), T  # unused by the backward (validity only)
+        h.sync, h.cluster = ptr(_lib.head_sync(dev)), spec["cluster"]
         dg = _lib.HeadGrad()
         dg.d_out, dg.ld_dout = ptr(d_out), T
         dg.d_x0, dg.ld_dx0 = ptr(d_x0), Hin
@@ -848,7 +850,7 @@ def head(x_pooled, wp, bp, blocks, ws, bs, wo, bo, *, act, drop_p=0.0, training=
     if drop and seed is None:
         seed = torch.randint(0, 2 ** 62, (1,), device=x_pooled.device, dtype=torch.int64)
     spec = dict(nb=nb, act=kind, training=bool(training), drop_p=float(drop_p),
-                skip=tuple(bool(s) for s in (skips or [False] * nb)))
+                skip=tuple(bool(s) for s in (skips or [False] * nb)), cluster=_lib.head_cluster())
     flat = []
     for b in blocks:
         flat += list(b)

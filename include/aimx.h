@@ -363,6 +363,7 @@ int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const AimxAdamHype
  *   Wp: (dy0, x0)
  * ------------------------------------------------------------------------------------------ */
 #define AIMX_HEAD_MAX_BLOCKS 8
+#define AIMX_HEAD_SYNC_WORDS 68
 typedef struct AimxHead {
   int64_t G, F, H_in, T;
   int32_t nb, act, training;
@@ -376,6 +377,11 @@ typedef struct AimxHead {
   float* y0; float* v[AIMX_HEAD_MAX_BLOCKS]; float* hid[AIMX_HEAD_MAX_BLOCKS];
   uint8_t* mask[AIMX_HEAD_MAX_BLOCKS]; float* z[AIMX_HEAD_MAX_BLOCKS]; float* cat;
   float* out; int64_t ldo;
+  /* Clustered launch: `cluster` (0/1 = off, 2, 4 or 8) workgroups share each 16-molecule tile and
+   * exchange activations through HBM inside the launch; `sync` = AIMX_HEAD_SYNC_WORDS int32
+   * words, zeroed once by the caller and kept zero by the kernels (word 0 becomes non-zero if a
+   * cluster wait ever timed out: results of that call are invalid). */
+  int32_t* sync; int32_t cluster;
 } AimxHead;
 
 typedef struct AimxHeadGrad {

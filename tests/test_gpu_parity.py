@@ -657,6 +657,42 @@ def test_fused_head_dropout():
     assert all(torch.isfinite(t.grad).all() for t in [x, wp, bp, ws, bs, wo, bo] + [p for b in blocks for p in b])
 
 
+@pytest.mark.parametrize("G", [5, 300, 2100])
+def test_fused_head_clusters_bit_identical(G, monkeypatch):
+    """Clustered head launches (2, 4 or 8 workgroups per 16-molecule tile exchanging activations
+    through HBM inside the launch; 2100 molecules = 132 tiles make the clusters loop over tiles)
+    give bit-identical outputs and gradients to the one-workgroup-per-tile launch, with dropout,
+    and never set the timeout word."""
+    from aimx import _lib, ops
+    g = torch.Generator().manual_seed(G)
+    F, Hin = 256, 512
+    base = [torch.randn(G, Hin, generator=g) * 0.1, torch.randn(F, Hin, generator=g) * 0.05,
+            torch.randn(F, generator=g) * 0.1]
+    for _ in range(2):
+        base += [torch.randn(F, F, generator=g) * 0.06, torch.randn(F, generator=g) * 0.1,
+                 torch.randn(F, F, generator=g) * 0.06, torch.randn(F, generator=g) * 0.1]
+    base += [torch.randn(F, F, generator=g) * 0.06, torch.randn(F, generator=g) * 0.1,
+             torch.randn(2, 2 * F, generator=g) * 0.05, torch.randn(2, generator=g) * 0.1]
+    seed = torch.tensor([11], device=DEV)
+    res = {}
+    for S in ("1", "2", "4", "8"):
+        monkeypatch.setenv("AIMX_HEAD_CLUSTER", S)
+        t = [b.to(DEV).requires_grad_() for b in base]
+        x, wp, bp = t[:3]
+        blocks = [tuple(t[3 + 4 * i:7 + 4 * i]) for i in range(2)]
+        ws, bs, wo, bo = t[11:15]
+        y = ops.head(x, wp, bp, blocks, ws, bs, wo, bo, act="silu", drop_p=0.1, training=True, seed=seed,
+                     skips=[False, True])
+        (y * torch.linspace(-1, 1, 2 * G, device=DEV).view(G, 2)).sum().backward()
+        torch.cuda.synchronize()
+        res[S] = [y.detach()] + [p.grad.detach() for p in t]
+    assert int(_lib.head_sync(DEV)[0]) == 0, "a cluster wait timed out"
+    assert int(_lib.head_sync(DEV)[1:].abs().sum()) == 0, "sync words not reset"
+    for S in ("2", "4", "8"):
+        for i, (a, b) in enumerate(zip(res["1"], res[S])):
+            assert torch.equal(a, b), (S, i, (a - b).abs().max().item())
+
+
 @pytest.mark.parametrize("name", ["c2", "c3"])
 def test_fused_mlp_opt_in_parity(name, monkeypatch):
     """AIMX_FUSED_MLP=1 (all MLP blocks of a shell layer in one launch each way, mlp.hip) keeps

@@ -69,8 +69,17 @@ def main():
     def ffwdbwd():
         fused().backward()
 
-    print(json.dumps({"head_fwd_us": timed(fwd), "head_fwd_bwd_us": timed(fwdbwd),
-                      "fused_fwd_us": timed(ffwd), "fused_fwd_bwd_us": timed(ffwdbwd)}), flush=True)
+    res = {"head_fwd_us": timed(fwd), "head_fwd_bwd_us": timed(fwdbwd)}
+    for cfg in os.environ.get("HEAD_CLUSTERS", "1,2,4").split(","):
+        S, _, W = cfg.partition("w")  # "4" or "4w8": cluster 4, 8 waves
+        os.environ["AIMX_HEAD_CLUSTER"] = S
+        if W:
+            os.environ["AIMX_HEAD_WAVES"] = W
+        else:
+            os.environ.pop("AIMX_HEAD_WAVES", None)
+        res[f"fused_fwd_us[{cfg}]"] = timed(ffwd)
+        res[f"fused_fwd_bwd_us[{cfg}]"] = timed(ffwdbwd)
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
