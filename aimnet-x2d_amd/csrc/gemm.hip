@@ -777,6 +777,181 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const WgradTable t, float
               tile, nt, ws + t.ws_off[q], counters ? counters + t.cnt_off[q] : nullptr, red);
 }
 
+// ---- Long-K weight gradients through LDS: 80 x 80 output blocks ----------------------------------
+// k_wgrad_grouped's waves load their MFMA fragments straight from global memory: one dword load
+// per MFMA, re-read by every 32 x 32 tile of the output, which leaves that kernel address-rate
+// bound (~30 % MFMA issue). Here a workgroup owns an 80 x 80 block (a whole 76 x 76 + bias MLP
+// weight of c2, or a quarter of its input projection) and a K slice: 32 k rows of dY and X are
+// staged in LDS by 16-byte loads (each element read once per block), prefetched into registers
+// while the previous rows compute; wave w (of 5) owns fragment row w and runs its 5 MFMAs per k
+// step from LDS (A read once, reused across the row). The LDS row stride of 80 floats puts the 4
+// k rows of a fragment read on bank offsets 0/16/32/48: conflict-free. Split-K slices are summed
+// as in k_wgrad_grouped (sc1 slabs, last arriver adds them in slice order): deterministic.
+constexpr int kWbB = 80;                             // block edge
+constexpr int kWbF = kWbB / 16;                      // fragments per edge = waves per workgroup
+constexpr int kWbK = 32;                             // k rows per LDS fill
+constexpr int kWbT = 64 * kWbF;                      // threads per workgroup
+constexpr int kWbSlab = kWbB * kWbB;                 // floats per split-K slab
+constexpr int kWbQ = kWbK * kWbB / 4;                // float4 per operand per fill
+constexpr int kWbV = 2 * kWbQ / kWbT;                // float4 per thread per fill
+static_assert(kWbQ % kWbT == 0, "each thread's float4s belong to one operand");
+
+struct WbTable {
+  int32_t n;
+  int32_t blk0[kWgMaxProb + 1];
+  int32_t bn[kWgMaxProb], nblk[kWgMaxProb], splits[kWgMaxProb], kchunk[kWgMaxProb], v4[kWgMaxProb];
+  uint32_t a_bytes[kWgMaxProb], b_bytes[kWgMaxProb];
+  int64_t ws_off[kWgMaxProb], cnt_off[kWgMaxProb];
+  AimxWgradProblem p[kWgMaxProb];
+};
+
+__global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
+  __shared__ __attribute__((aligned(16))) float sA[kWbK * kWbB];
+  __shared__ __attribute__((aligned(16))) float sB[kWbK * kWbB];
+  __shared__ int flag;
+  int q = 0;
+  while (q + 1 < t.n && t.blk0[q + 1] <= (int)blockIdx.x) ++q;
+  const int nb = t.nblk[q];
+  const int local = blockIdx.x - t.blk0[q];
+  const int z = local / nb, blk = local - z * nb;
+  const AimxWgradProblem& pr = t.p[q];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lm = lane & 15, lk = lane >> 4;
+  const int M = (int)pr.M, Nreal = (int)pr.N, ones = pr.col_out != nullptr;
+  const int N = Nreal + ones;
+  const int m0 = (blk / t.bn[q]) * kWbB, n0 = (blk % t.bn[q]) * kWbB;
+  const int S = t.splits[q];
+  AimxGemmArgs a = {};
+  a.M = M;
+  a.N = N;
+  a.K = pr.K;
+  a.C = pr.dW;
+  a.ldc = pr.ld_dw;
+  a.act = -1;
+  a.dact_kind = -1;
+  a.ones_col = ones;
+  a.col_out = pr.col_out;
+  if (pr.zc_rowptr && n0 >= zc_extent(pr.zc_rowptr, pr.zc_rows, pr.zc_chunks, pr.zc_width) &&
+      !(ones && n0 + kWbB > Nreal)) {  // a block wholly inside the empty hop chunks: zero, no work
+    if (z == 0)
+      for (int e = tid; e < kWbSlab; e += kWbT) {
+        const int m = m0 + e / kWbB, n = n0 + e % kWbB;
+        if (m < M && n < Nreal) pr.dW[(int64_t)m * pr.ld_dw + n] = 0.f;
+      }
+    return;
+  }
+  const int kb = z * t.kchunk[q];
+  const int kend = min((int)pr.K, kb + t.kchunk[q]);
+  const int nsub = kend > kb ? (kend - kb + kWbK - 1) / kWbK : 0;
+  const uint32_t ab = t.a_bytes[q], bb = t.b_bytes[q];
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(pr.dY, ab);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(pr.X, bb);
+  const uint32_t lda = (uint32_t)pr.ld_dy, ldb = (uint32_t)pr.ld_x;
+  const bool v4 = t.v4[q] != 0;
+
+  floatx4 stage[kWbV];
+  // rows k0.. of both operands -> registers. Invalid rows/columns read 0 (address moved past the
+  // descriptor's extent, or a component select for a float4 straddling the edge); X's implicit
+  // ones column (the bias gradient) reads 1 on valid rows.
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < kWbV; ++u) {
+      const bool isb = u >= kWbV / 2;
+      const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
+      const int row = f / (kWbB / 4), c = 4 * (f % (kWbB / 4));
+      const int k = k0 + row;
+      const int col = (isb ? n0 : m0) + c, lim = isb ? Nreal : M;
+      const uint32_t ld = isb ? ldb : lda, bytes = isb ? bb : ab;
+      const __amdgpu_buffer_rsrc_t r = isb ? rb : ra;
+      const bool kok = k < kend;
+      floatx4 v;
+      if (v4) {
+        v = bload4(r, kok && col < lim ? 4u * ((uint32_t)k * ld + (uint32_t)col) : bytes, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (col + i >= lim) v[i] = 0.f;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          v[i] = bload(r, kok && col + i < lim ? 4u * ((uint32_t)k * ld + (uint32_t)(col + i)) : bytes, 0);
+      }
+      if (isb && ones) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (kok && col + i == Nreal) v[i] = 1.f;
+      }
+      stage[u] = v;
+    }
+  };
+
+  floatx4 acc[kWbF];
+#pragma unroll
+  for (int j = 0; j < kWbF; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (nsub > 0) fetch(kb);
+  for (int s = 0; s < nsub; ++s) {
+    __syncthreads();  // the previous rows' MFMA reads are done
+#pragma unroll
+    for (int u = 0; u < kWbV; ++u) {
+      const bool isb = u >= kWbV / 2;
+      const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
+      *reinterpret_cast<floatx4*>((isb ? sB : sA) + 4 * f) = stage[u];
+    }
+    __syncthreads();
+    if (s + 1 < nsub) fetch(kb + (s + 1) * kWbK);
+#pragma unroll
+    for (int k4 = 0; k4 < kWbK / 4; ++k4) {
+      const int r = (k4 * 4 + lk) * kWbB + lm;
+      const float av = sA[r + w * 16];
+      float bv[kWbF];
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j) bv[j] = sB[r + j * 16];
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
+    }
+  }
+
+  if (S > 1) {
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(ws + t.ws_off[q], (uint32_t)(4 * (int64_t)S * nb * kWbSlab));
+    const uint32_t own = 16u * (uint32_t)((w * kWbF) * 64 + lane);
+#pragma unroll
+    for (int j = 0; j < kWbF; ++j)
+      store_sc1(rws, 4u * (uint32_t)((z * nb + blk) * kWbSlab) + own + 16u * 64u * (uint32_t)j, acc[j]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      int32_t* cnt = counters + t.cnt_off[q] + blk;
+      const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == S - 1);
+      if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+      flag = last;
+    }
+    __syncthreads();
+    if (!flag) return;
+#pragma unroll
+    for (int j = 0; j < kWbF; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int zz = 0; zz < S; ++zz) {  // slice order
+      floatx4 v[kWbF];
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j)
+        v[j] = load_sc1(rws, 4u * (uint32_t)((zz * nb + blk) * kWbSlab) + own + 16u * 64u * (uint32_t)j);
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kWbF; ++j) {
+    int em[4], en[4];
+    float ev[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      em[r] = m0 + w * 16 + lk * 4 + r;
+      en[r] = n0 + j * 16 + lm;
+      ev[r] = acc[j][r];
+    }
+    epilogue_n<4>(a, em, en, ev);
+  }
+}
+
 // Fallback when no counter array is supplied: one thread per output element sums the slabs in
 // slice order. Slab element (m, n) of tile (tm, tn) sits where thread tid's accumulator fragment
 // put it (see the split-K branch of k_gemm).
@@ -962,11 +1137,29 @@ namespace aimx {
 namespace {
 struct WgPlan {
   int tiles_x, tiles_y, splits, kchunk;
+  bool lds;    // k_wgrad_lds (80 x 80 blocks) instead of k_wgrad_grouped (32 x 32 tiles)
+  int64_t slab;  // floats per split-K slab
 };
 WgPlan wg_plan(const AimxWgradProblem& p) {
+  const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
+  const bool no_lds = e && atoi(e) == 0;
   WgPlan w;
+  const int64_t N = p.col_out ? p.N + 1 : p.N;
+  if (!no_lds && p.K >= 2048) {
+    // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks
+    w.lds = true;
+    w.slab = kWbSlab;
+    w.tiles_x = (int)cdiv(p.M, kWbB);
+    w.tiles_y = (int)cdiv(N, kWbB);
+    const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / 512));
+    w.kchunk = (int)(cdiv(cdiv(p.K, sp), kWbK) * kWbK);
+    w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
+    return w;
+  }
+  w.lds = false;
+  w.slab = 1024;
   w.tiles_x = (int)cdiv(p.M, 32);
-  w.tiles_y = (int)cdiv(p.col_out ? p.N + 1 : p.N, 32);
+  w.tiles_y = (int)cdiv(N, 32);
   // ~1k atoms of K per workgroup: enough MFMA work per wave to amortise the fragment pipeline
   int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / 1024));
   w.kchunk = (int)(cdiv(cdiv(std::max<int64_t>(p.K, 1), sp), 16) * 16);
@@ -988,7 +1181,7 @@ extern "C" size_t aimx_wgrad_grouped_workspace_bytes(const AimxWgradProblem* p, 
   size_t f = 0;
   for (int32_t i = 0; i < n; ++i) {
     const aimx::WgPlan w = aimx::wg_plan(p[i]);
-    if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * 1024;
+    if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab;
   }
   return sizeof(float) * f;
 }
@@ -1006,35 +1199,75 @@ extern "C" int aimx_wgrad_grouped(const AimxWgradProblem* p, int32_t n, void* wo
     ctiles += (int64_t)w.tiles_x * w.tiles_y;
   }
   if (!counters || ctiles > n_counters) return AIMX_EARG;
+  // long-K problems -> k_wgrad_lds launches, the rest -> k_wgrad_grouped launches (<= kWgMaxProb
+  // problems per launch each); workspace slabs and counters are laid out in problem order
   int64_t ws_off = 0, cnt_off = 0;
-  for (int32_t c0 = 0; c0 < n; c0 += kWgMaxProb) {
-    WgradTable t{};
-    t.n = std::min<int32_t>(kWgMaxProb, n - c0);
-    int32_t blk = 0;
-    for (int32_t k = 0; k < t.n; ++k) {
-      const AimxWgradProblem& pr = p[c0 + k];
-      const WgPlan w = wg_plan(pr);
+  WgradTable t{};
+  WbTable tb{};
+  int32_t blk = 0, blkb = 0;
+  auto flush = [&](bool lds) {
+    if (lds) {
+      tb.blk0[tb.n] = blkb;
+      if (blkb > 0)
+        hipLaunchKernelGGL(k_wgrad_lds, dim3((unsigned)blkb), dim3(kWbT), 0, (hipStream_t)stream, tb, (float*)workspace,
+                           counters);
+      tb = WbTable{};
+      blkb = 0;
+    } else {
+      t.blk0[t.n] = blk;
+      if (blk > 0)
+        hipLaunchKernelGGL(k_wgrad_grouped, dim3((unsigned)blk), dim3(256), 0, (hipStream_t)stream, t, (float*)workspace,
+                           counters);
+      t = WgradTable{};
+      blk = 0;
+    }
+  };
+  for (int32_t i = 0; i < n; ++i) {
+    const AimxWgradProblem& pr = p[i];
+    const WgPlan w = wg_plan(pr);
+    const int32_t nt = w.tiles_x * w.tiles_y;
+    if (w.lds) {
+      const int k = tb.n++;
+      const int64_t Kr = std::max<int64_t>(pr.K, 1) - 1;
+      const bool v4 = pr.ld_dy % 4 == 0 && pr.ld_x % 4 == 0 && (uintptr_t)pr.dY % 16 == 0 && (uintptr_t)pr.X % 16 == 0;
+      tb.p[k] = pr;
+      tb.blk0[k] = blkb;
+      tb.bn[k] = w.tiles_y;
+      tb.nblk[k] = nt;
+      tb.splits[k] = w.splits;
+      tb.kchunk[k] = w.kchunk;
+      tb.v4[k] = v4;
+      // a float4 straddling the last row's edge stays inside the descriptor (rows are ld >= the
+      // rounded width long), so its valid components are never cut by the range check
+      const int64_t am = v4 ? std::min<int64_t>(pr.ld_dy, cdiv(pr.M, 4) * 4) : pr.M;
+      const int64_t bm = v4 ? std::min<int64_t>(pr.ld_x, cdiv(pr.N, 4) * 4) : pr.N;
+      tb.a_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * (Kr * pr.ld_dy + am));
+      tb.b_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * (Kr * pr.ld_x + bm));
+      tb.ws_off[k] = ws_off;
+      tb.cnt_off[k] = cnt_off;
+      blkb += w.splits * nt;
+      if (tb.n == kWgMaxProb) flush(true);
+    } else {
+      const int k = t.n++;
       t.p[k] = pr;
       t.blk0[k] = blk;
       t.tiles_y[k] = w.tiles_y;
-      t.ntiles[k] = w.tiles_x * w.tiles_y;
+      t.ntiles[k] = nt;
       t.splits[k] = w.splits;
       t.kchunk[k] = w.kchunk;
       t.a_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * ((std::max<int64_t>(pr.K, 1) - 1) * pr.ld_dy + pr.M));
       t.b_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * ((std::max<int64_t>(pr.K, 1) - 1) * pr.ld_x + pr.N));
       t.ws_off[k] = ws_off;
       t.cnt_off[k] = cnt_off;
-      if (w.splits > 1) ws_off += (int64_t)w.splits * t.ntiles[k] * 1024;
-      cnt_off += t.ntiles[k];
-      blk += w.splits * t.ntiles[k];
+      blk += w.splits * nt;
+      if (t.n == kWgMaxProb) flush(false);
     }
-    t.blk0[t.n] = blk;
-    if (blk > 0) {
-      hipLaunchKernelGGL(k_wgrad_grouped, dim3((unsigned)blk), dim3(256), 0, (hipStream_t)stream, t, (float*)workspace,
-                         counters);
-      AIMX_CHECK_LAUNCH();
-    }
+    if (w.splits > 1) ws_off += (int64_t)w.splits * nt * w.slab;
+    cnt_off += nt;
   }
+  if (t.n) flush(false);
+  if (tb.n) flush(true);
+  AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
 

@@ -17,7 +17,11 @@ prev = None
 tot = 0.0
 for r in tr[a:b]:
     n = r["Kernel_Name"].replace("void ", "").replace("aimx::(anonymous namespace)::", "")
-    n = re.sub(r"\(.*", "", n)[:70]
+    if n.startswith("at::native::"):  # keep the kernel and its functor, drop the template noise
+        fn = re.findall(r"(\w+(?:Functor|Op|_kernel|Kernel)\w*)", n)
+        n = "torch:" + " ".join(dict.fromkeys(fn))[:90]
+    else:
+        n = re.sub(r"\(.*", "", n)[:70]
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     gap = (s - prev) / 1e3 if prev else 0.0
     prev = e
