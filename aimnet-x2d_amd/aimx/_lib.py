@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libaimx.so")
+# AIMX_LIB_PATH: a variant build of the same sources (A/B experiments on the GPU box)
+LIB_PATH = os.environ.get("AIMX_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "lib", "libaimx.so")
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32

@@ -790,6 +790,10 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const WgradTable t, float
 constexpr int kWbB = 80;                             // block edge
 constexpr int kWbF = kWbB / 16;                      // fragments per edge = waves per workgroup
 constexpr int kWbK = 32;                             // k rows per LDS fill
+#ifndef AIMX_WBD
+#define AIMX_WBD 2
+#endif
+constexpr int kWbD = AIMX_WBD;                       // LDS fills in flight (register ring)
 constexpr int kWbT = 64 * kWbF;                      // threads per workgroup
 constexpr int kWbSlab = kWbB * kWbB;                 // floats per split-K slab
 constexpr int kWbQ = kWbK * kWbB / 4;                // float4 per operand per fill
@@ -849,11 +853,10 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
   const uint32_t lda = (uint32_t)pr.ld_dy, ldb = (uint32_t)pr.ld_x;
   const bool v4 = t.v4[q] != 0;
 
-  floatx4 stage[kWbV];
   // rows k0.. of both operands -> registers. Invalid rows/columns read 0 (address moved past the
   // descriptor's extent, or a component select for a float4 straddling the edge); X's implicit
   // ones column (the bias gradient) reads 1 on valid rows.
-  auto fetch = [&](int k0) {
+  auto fetch = [&](int k0, floatx4 (&stage)[kWbV]) {
 #pragma unroll
     for (int u = 0; u < kWbV; ++u) {
       const bool isb = u >= kWbV / 2;
@@ -887,26 +890,36 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
   floatx4 acc[kWbF];
 #pragma unroll
   for (int j = 0; j < kWbF; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if (nsub > 0) fetch(kb);
-  for (int s = 0; s < nsub; ++s) {
-    __syncthreads();  // the previous rows' MFMA reads are done
+  // kWbD fills in flight: fill s lands in register slot s % kWbD, is copied to LDS kWbD - 1
+  // compute periods after its loads were issued, and the slot is refilled with fill s + kWbD
+  floatx4 ring[kWbD][kWbV];
 #pragma unroll
-    for (int u = 0; u < kWbV; ++u) {
-      const bool isb = u >= kWbV / 2;
-      const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
-      *reinterpret_cast<floatx4*>((isb ? sB : sA) + 4 * f) = stage[u];
-    }
-    __syncthreads();
-    if (s + 1 < nsub) fetch(kb + (s + 1) * kWbK);
+  for (int d = 0; d < kWbD; ++d)
+    if (d < nsub) fetch(kb + d * kWbK, ring[d]);
+  for (int s0 = 0; s0 < nsub; s0 += kWbD) {
 #pragma unroll
-    for (int k4 = 0; k4 < kWbK / 4; ++k4) {
-      const int r = (k4 * 4 + lk) * kWbB + lm;
-      const float av = sA[r + w * 16];
-      float bv[kWbF];
+    for (int d = 0; d < kWbD; ++d) {
+      const int s = s0 + d;
+      if (s >= nsub) break;
+      __syncthreads();  // the previous rows' MFMA reads are done
 #pragma unroll
-      for (int j = 0; j < kWbF; ++j) bv[j] = sB[r + j * 16];
+      for (int u = 0; u < kWbV; ++u) {
+        const bool isb = u >= kWbV / 2;
+        const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
+        *reinterpret_cast<floatx4*>((isb ? sB : sA) + 4 * f) = ring[d][u];
+      }
+      __syncthreads();
+      if (s + kWbD < nsub) fetch(kb + (s + kWbD) * kWbK, ring[d]);
 #pragma unroll
-      for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
+      for (int k4 = 0; k4 < kWbK / 4; ++k4) {
+        const int r = (k4 * 4 + lk) * kWbB + lm;
+        const float av = sA[r + w * 16];
+        float bv[kWbF];
+#pragma unroll
+        for (int j = 0; j < kWbF; ++j) bv[j] = sB[r + j * 16];
+#pragma unroll
+        for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
+      }
     }
   }
 
@@ -1067,9 +1080,95 @@ void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s,
 
 }  // namespace
 
-size_t gemm_workspace_floats(const AimxGemmArgs& a) {
+namespace {
+struct WgPlan {
+  int tiles_x, tiles_y, splits, kchunk;
+  bool lds;    // k_wgrad_lds (80 x 80 blocks) instead of k_wgrad_grouped (32 x 32 tiles)
+  int64_t slab;  // floats per split-K slab
+};
+WgPlan wg_plan(const AimxWgradProblem& p) {
+  const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
+  const bool no_lds = e && atoi(e) == 0;
+  WgPlan w;
+  const int64_t N = p.col_out ? p.N + 1 : p.N;
+  if (!no_lds && p.K >= 2048) {
+    // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks
+    w.lds = true;
+    w.slab = kWbSlab;
+    w.tiles_x = (int)cdiv(p.M, kWbB);
+    w.tiles_y = (int)cdiv(N, kWbB);
+    const char* kp = getenv("AIMX_WGRAD_KPER");  // atoms per workgroup (tuning experiments)
+    const int64_t kper = kp ? std::max(64, atoi(kp)) : 512;
+    const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
+    w.kchunk = (int)(cdiv(cdiv(p.K, sp), kWbK) * kWbK);
+    w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
+    return w;
+  }
+  w.lds = false;
+  w.slab = 1024;
+  w.tiles_x = (int)cdiv(p.M, 32);
+  w.tiles_y = (int)cdiv(N, 32);
+  // ~1k atoms of K per workgroup: enough MFMA work per wave to amortise the fragment pipeline
+  int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / 1024));
+  w.kchunk = (int)(cdiv(cdiv(std::max<int64_t>(p.K, 1), sp), 16) * 16);
+  w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
+  return w;
+}
+bool wg_valid(const AimxWgradProblem& p) {
+  if (p.M < 1 || p.N < 1 || p.K < 0 || !p.dY || !p.X || !p.dW) return false;
+  if (p.ld_dy < p.M || p.ld_x < p.N || p.ld_dw < p.N) return false;
+  if (p.zc_rowptr && (p.zc_chunks < 0 || p.zc_rows < 0 || p.zc_width < 0)) return false;
+  const int64_t a_ext = 4 * ((p.K - 1) * p.ld_dy + p.M), b_ext = 4 * ((p.K - 1) * p.ld_x + p.N);
+  return p.K == 0 || (a_ext < (1ll << 31) && b_ext < (1ll << 31));
+}
+
+// A long-K weight-gradient GEMM with a plain-store epilogue (dW = dY^T X [+ ones-column bias
+// gradient], optional zc_dim 1 trimming) runs as a one-problem k_wgrad_lds launch.
+bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
+  if (!(a.sam == 1 && a.sbn == 1 && a.sak != 1) || a.K < 1 || a.M < 1) return false;
+  if (a.beta != 0.f || a.bias || a.res[0] || a.res[1] || a.res[2] || a.act_ncols > 0 || a.pre || a.dact_pre ||
+      a.mask_in || a.mask_out || a.act >= 0)
+    return false;
+  if (a.zc_rowptr && a.zc_dim != 1) return false;
+  const char* e = getenv("AIMX_WGRAD_LDS_GEMM");  // single long-K GEMMs too (opt-in: see DESIGN)
+  if (!e || atoi(e) == 0) return false;
+  pr = AimxWgradProblem{};
+  pr.dY = a.A;
+  pr.ld_dy = a.sak;
+  pr.X = a.B;
+  pr.ld_x = a.sbk;
+  pr.dW = a.C;
+  pr.ld_dw = a.ldc;
+  pr.col_out = a.ones_col ? a.col_out : nullptr;
+  pr.M = a.M;
+  pr.N = a.ones_col ? a.N - 1 : a.N;
+  pr.K = a.K;
+  if (a.zc_rowptr) {
+    pr.zc_rowptr = a.zc_rowptr;
+    pr.zc_rows = a.zc_rows;
+    pr.zc_chunks = a.zc_chunks;
+    pr.zc_width = a.zc_width;
+  }
+  return pr.N >= 1 && wg_valid(pr) && wg_plan(pr).lds;
+}
+}  // namespace
+
+// workspace of the tiled kernels' split-K plan
+size_t tiled_workspace_floats(const AimxGemmArgs& a) {
   const Plan p = plan_gemm(a);
   return p.splits > 1 ? (size_t)p.splits * (size_t)(cdiv(a.M, p.bm) * cdiv(a.N, p.bn)) * p.bm * p.bn : 0;
+}
+
+// what the caller allocates: enough for whichever path launch_gemm takes (the k_wgrad_lds route
+// needs counters, so a caller without them falls back to the tiled plan)
+size_t gemm_workspace_floats(const AimxGemmArgs& a) {
+  size_t f = tiled_workspace_floats(a);
+  AimxWgradProblem pr;
+  if (gemm_as_wgrad(a, pr)) {
+    const WgPlan w = wg_plan(pr);
+    if (w.splits > 1) f = std::max(f, (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab);
+  }
+  return f;
 }
 
 int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
@@ -1086,6 +1185,16 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
                           a.pre || a.dact_pre || a.mask_in || a.mask_out))
       return AIMX_EARG;
   }
+  {
+    AimxWgradProblem pr;
+    if (gemm_as_wgrad(a, pr)) {
+      const WgPlan w = wg_plan(pr);
+      const size_t need = w.splits > 1 ? sizeof(float) * w.splits * w.tiles_x * w.tiles_y * w.slab : 0;
+      if ((w.splits == 1 || (a.workspace && a.workspace_bytes >= need)) && a.counters &&
+          (int64_t)w.tiles_x * w.tiles_y <= a.n_counters)
+        return aimx_wgrad_grouped(&pr, 1, a.workspace, a.workspace_bytes, a.counters, a.n_counters, s);
+    }
+  }
   // operand layouts: each operand must be contiguous along k or along m/n; byte extents < 2 GiB
   if (!(a.sak == 1 || a.sam == 1) || !(a.sbk == 1 || a.sbn == 1)) return AIMX_EARG;
   const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
@@ -1099,7 +1208,7 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   const uint32_t a_bytes = (uint32_t)std::max<int64_t>(a_ext, 4);
   const uint32_t b_bytes = (uint32_t)std::max<int64_t>(b_ext, 4);
   Plan p = plan_gemm(a);
-  if (p.splits > 1 && (!a.workspace || a.workspace_bytes < sizeof(float) * gemm_workspace_floats(a))) {
+  if (p.splits > 1 && (!a.workspace || a.workspace_bytes < sizeof(float) * tiled_workspace_floats(a))) {
     p.splits = 1;
     p.kchunk = std::max<int64_t>(cdiv(a.K, kBK) * kBK, kBK);
   }
@@ -1133,48 +1242,6 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
 
 }  // namespace aimx
 
-namespace aimx {
-namespace {
-struct WgPlan {
-  int tiles_x, tiles_y, splits, kchunk;
-  bool lds;    // k_wgrad_lds (80 x 80 blocks) instead of k_wgrad_grouped (32 x 32 tiles)
-  int64_t slab;  // floats per split-K slab
-};
-WgPlan wg_plan(const AimxWgradProblem& p) {
-  const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
-  const bool no_lds = e && atoi(e) == 0;
-  WgPlan w;
-  const int64_t N = p.col_out ? p.N + 1 : p.N;
-  if (!no_lds && p.K >= 2048) {
-    // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks
-    w.lds = true;
-    w.slab = kWbSlab;
-    w.tiles_x = (int)cdiv(p.M, kWbB);
-    w.tiles_y = (int)cdiv(N, kWbB);
-    const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / 512));
-    w.kchunk = (int)(cdiv(cdiv(p.K, sp), kWbK) * kWbK);
-    w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
-    return w;
-  }
-  w.lds = false;
-  w.slab = 1024;
-  w.tiles_x = (int)cdiv(p.M, 32);
-  w.tiles_y = (int)cdiv(N, 32);
-  // ~1k atoms of K per workgroup: enough MFMA work per wave to amortise the fragment pipeline
-  int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / 1024));
-  w.kchunk = (int)(cdiv(cdiv(std::max<int64_t>(p.K, 1), sp), 16) * 16);
-  w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
-  return w;
-}
-bool wg_valid(const AimxWgradProblem& p) {
-  if (p.M < 1 || p.N < 1 || p.K < 0 || !p.dY || !p.X || !p.dW) return false;
-  if (p.ld_dy < p.M || p.ld_x < p.N || p.ld_dw < p.N) return false;
-  if (p.zc_rowptr && (p.zc_chunks < 0 || p.zc_rows < 0 || p.zc_width < 0)) return false;
-  const int64_t a_ext = 4 * ((p.K - 1) * p.ld_dy + p.M), b_ext = 4 * ((p.K - 1) * p.ld_x + p.N);
-  return p.K == 0 || (a_ext < (1ll << 31) && b_ext < (1ll << 31));
-}
-}  // namespace
-}  // namespace aimx
 
 extern "C" size_t aimx_wgrad_grouped_workspace_bytes(const AimxWgradProblem* p, int32_t n) {
   if (!p || n < 0) return 0;
