@@ -174,6 +174,8 @@ _SIGS = {
     "aimx_l1_loss_forward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr]),
     "aimx_l1_loss_backward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_i64,
                                       c_ptr]),
+    "aimx_l1_loss_backward_padded": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr,
+                                             c_ptr, c_i64, c_ptr]),
     "aimx_events_create": (c_i32, [c_i32, c_ptr]),
     "aimx_events_destroy": (c_i32, [c_i32, c_ptr]),
     "aimx_wgrad_grouped_workspace_bytes": (c_size, [ctypes.POINTER(WgradProblem), c_i32]),

@@ -297,6 +297,7 @@ class _AttnPool(torch.autograd.Function):
         ctx.plan = plan
         ctx.ldx = ldx
         ctx.save_for_backward(x, W, tau, attn, scores)
+        ctx.set_materialize_grads(False)  # an unused attention output needs no zero-filled gradient
         return pooled, attn
 
     @staticmethod
@@ -312,7 +313,7 @@ class _AttnPool(torch.autograd.Function):
             d_pooled = torch.zeros(G, c, dtype=_F32, device=dev)
         d_pooled = d_pooled.contiguous()
         d_attn = d_attn.contiguous() if d_attn is not None else None
-        dx = torch.zeros(n, c, dtype=_F32, device=dev)
+        dx = torch.empty(n, c, dtype=_F32, device=dev)  # every atom row is written (its molecule's segment)
         dW = torch.empty(H, c, dtype=_F32, device=dev)
         db = torch.empty(H, dtype=_F32, device=dev)
         dtau = torch.empty(1, dtype=_F32, device=dev)
@@ -689,39 +690,48 @@ def linear_block(x, W1, b1, W2, b2, act, drop_p=0.0, training=False, skip=False,
 # ---------------------------------------------------------------------------------------------
 class _L1Loss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, target, weights, per_sample):
+    def forward(ctx, pred, target, weights, per_sample, rows):
         lib = _lib.load()
         p, ldp = _rows(pred.reshape(pred.shape[0], -1) if pred.dim() != 2 else pred)
         t, ldt = _rows(target.reshape(target.shape[0], -1) if target.dim() != 2 else target)
-        rows, cols = p.shape
+        total, cols = p.shape
+        rows = total if rows is None else rows
         w = weights.contiguous().float() if weights is not None else None
         loss = torch.empty((), dtype=_F32, device=pred.device)
         check(lib.aimx_l1_loss_forward(ptr(p), ldp, ptr(t), ldt, rows, cols, ptr(w), int(per_sample), ptr(loss),
                                        stream_ptr(pred.device)), "l1_loss_forward")
         ctx.save_for_backward(p, t, w)
-        ctx.meta = (ldp, ldt, int(per_sample), pred.shape)
+        ctx.meta = (ldp, ldt, int(per_sample), pred.shape, rows)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         lib = _lib.load()
         p, t, w = ctx.saved_tensors
-        ldp, ldt, per_sample, shape = ctx.meta
-        rows, cols = p.shape
+        ldp, ldt, per_sample, shape, rows = ctx.meta
+        total, cols = p.shape
         g = g.contiguous()
-        dp = torch.empty(rows, cols, dtype=_F32, device=p.device)
-        check(lib.aimx_l1_loss_backward(ptr(p), ldp, ptr(t), ldt, rows, cols, ptr(w), per_sample, ptr(g), ptr(dp),
-                                        cols, stream_ptr(p.device)), "l1_loss_backward")
-        return dp.view(shape), None, None, None
+        dp = torch.empty(total, cols, dtype=_F32, device=p.device)
+        check(lib.aimx_l1_loss_backward_padded(ptr(p), ldp, ptr(t), ldt, rows, total, cols, ptr(w), per_sample, ptr(g),
+                                               ptr(dp), cols, stream_ptr(p.device)), "l1_loss_backward")
+        return dp.view(shape), None, None, None, None
 
 
-def l1_loss(pred, target, weights=None, per_sample=False):
+def l1_loss(pred, target, weights=None, per_sample=False, rows=None):
     """mean |pred - target| (per_sample=False, weights None: nn.L1Loss) or
-    mean over samples of sum_t w_t |pred - target| (per_sample=True: WeightedL1Loss)."""
+    mean over samples of sum_t w_t |pred - target| (per_sample=True: WeightedL1Loss).
+    rows=B: the loss of pred[:B] against target (B rows), with pred's remaining rows (the padding
+    molecules of a static captured batch) getting a zero gradient in the same launch; equal to
+    l1_loss(pred[:B], target) without autograd's slice-backward zero fill and copy."""
     _lib.require_device(pred, target)
-    if pred.shape != target.shape or pred.dtype != _F32 or target.dtype != _F32:
-        raise _lib.AimxError("aimx.l1_loss: pred and target must be fp32 tensors of one shape")
-    return _L1Loss.apply(pred, target, weights, bool(per_sample))
+    if pred.dtype != _F32 or target.dtype != _F32:
+        raise _lib.AimxError("aimx.l1_loss: pred and target must be fp32 tensors")
+    if rows is None:
+        if pred.shape != target.shape:
+            raise _lib.AimxError("aimx.l1_loss: pred and target must have one shape")
+    elif not (0 <= rows <= pred.shape[0] and target.shape[0] == rows and target.shape[1:] == pred.shape[1:]):
+        raise _lib.AimxError("aimx.l1_loss: rows must be <= pred rows and equal target rows")
+    return _L1Loss.apply(pred, target, weights, bool(per_sample), rows)
 
 
 # ---------------------------------------------------------------------------------------------

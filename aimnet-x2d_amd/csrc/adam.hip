@@ -21,7 +21,8 @@
 namespace aimx {
 namespace {
 
-constexpr int kAdamChunk = 48;        // tensors per launch (kernel-argument table)
+constexpr int kAdamChunk = 80;        // tensors per launch (kernel-argument table, < 4 KiB: a
+                                      // reference GNN's ~75 parameters take one launch each way)
 constexpr int kAdamThreads = 256;
 constexpr int64_t kSliceElems = 2048; // elements per workgroup slice (8 per thread, loads unrolled)
 
@@ -35,6 +36,7 @@ struct AdamTable {
   float* m[kAdamChunk];
   float* v[kAdamChunk];
 };
+static_assert(sizeof(AdamTable) <= 4000, "kernel argument table must stay under the 4 KiB limit");
 
 __device__ __forceinline__ int find_tensor(const AdamTable& t, int b) {
   int i = 0;

@@ -33,11 +33,15 @@ __global__ __launch_bounds__(256) void k_l1_fwd(const float* __restrict__ p, int
 
 __global__ void k_l1_bwd(const float* __restrict__ p, int64_t ldp, const float* __restrict__ y, int64_t ldy,
                          int64_t rows, int64_t cols, const float* __restrict__ w, float inv_div,
-                         const float* __restrict__ dloss, float* __restrict__ dp, int64_t ldd) {
-  const int64_t n = rows * cols;
+                         const float* __restrict__ dloss, float* __restrict__ dp, int64_t ldd, int64_t rows_total) {
+  const int64_t n = rows_total * cols;
   const float g = dloss[0] * inv_div;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = e / cols, t = e - i * cols;
+    if (i >= rows) {  // rows past the loss's rows (padding): zero gradient
+      dp[i * ldd + t] = 0.f;
+      continue;
+    }
     const float d = p[i * ldp + t] - y[i * ldy + t];
     const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
     dp[i * ldd + t] = sg * (w ? w[t] : 1.f) * g;
@@ -62,16 +66,24 @@ extern "C" int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float*
   return AIMX_OK;
 }
 
+extern "C" int aimx_l1_loss_backward_padded(const float* pred, int64_t ldp, const float* target, int64_t ldt,
+                                            int64_t rows, int64_t rows_total, int64_t cols, const float* weights,
+                                            int32_t per_sample, const float* d_loss, float* d_pred, int64_t ldd,
+                                            aimx_stream_t stream) {
+  if (rows < 0 || rows_total < rows || cols < 0 || ldp < cols || ldt < cols || ldd < cols || !d_loss) return AIMX_EARG;
+  if (rows_total * cols == 0) return AIMX_OK;
+  if ((rows > 0 && (!pred || !target)) || !d_pred) return AIMX_EARG;
+  const double div = per_sample ? (double)rows : (double)rows * (double)cols;
+  const int64_t blocks = std::min<int64_t>(cdiv(rows_total * cols, 256), 1024);
+  hipLaunchKernelGGL(k_l1_bwd, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, pred, ldp, target, ldt, rows,
+                     cols, weights, (float)(1.0 / div), d_loss, d_pred, ldd, rows_total);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
 extern "C" int aimx_l1_loss_backward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
                                      int64_t cols, const float* weights, int32_t per_sample, const float* d_loss,
                                      float* d_pred, int64_t ldd, aimx_stream_t stream) {
-  if (rows < 0 || cols < 0 || ldp < cols || ldt < cols || ldd < cols || !d_loss) return AIMX_EARG;
-  if (rows * cols == 0) return AIMX_OK;
-  if (!pred || !target || !d_pred) return AIMX_EARG;
-  const double div = per_sample ? (double)rows : (double)rows * (double)cols;
-  const int64_t blocks = std::min<int64_t>(cdiv(rows * cols, 256), 1024);
-  hipLaunchKernelGGL(k_l1_bwd, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, pred, ldp, target, ldt, rows,
-                     cols, weights, (float)(1.0 / div), d_loss, d_pred, ldd);
-  AIMX_CHECK_LAUNCH();
-  return AIMX_OK;
+  return aimx_l1_loss_backward_padded(pred, ldp, target, ldt, rows, rows, cols, weights, per_sample, d_loss, d_pred,
+                                      ldd, stream);
 }

@@ -410,6 +410,13 @@ int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float* target, in
 int aimx_l1_loss_backward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
                           int64_t cols, const float* weights, int32_t per_sample, const float* d_loss,
                           float* d_pred, int64_t ldd, aimx_stream_t stream);
+/* The loss over the first `rows` rows of a [rows_total, cols] prediction (the padded static batch
+ * of a captured train step: rows >= rows are padding molecules excluded from the loss): d_pred
+ * gets the gradient of those rows and 0 for the rest, in one launch (what autograd's
+ * slice-backward would otherwise do with a zero fill and a copy). */
+int aimx_l1_loss_backward_padded(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
+                                 int64_t rows_total, int64_t cols, const float* weights, int32_t per_sample,
+                                 const float* d_loss, float* d_pred, int64_t ldd, aimx_stream_t stream);
 
 #ifdef __cplusplus
 }

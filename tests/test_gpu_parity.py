@@ -610,6 +610,28 @@ def test_l1_losses_match_reference_criteria(rows, cols, weighted):
     assert pg.grad[0, 0].item() == 0.0
 
 
+@pytest.mark.parametrize("weighted", [False, True])
+def test_l1_loss_rows_of_padded_prediction(weighted):
+    """ops.l1_loss(pred, target, rows=B) on a padded [B + 8, T] prediction (the captured train
+    step's static batch) == the loss of pred[:B] through autograd's slice: bit-identical value and
+    gradient, padding rows' gradient exactly 0 (they start as NaN in the buffer)."""
+    from aimx import ops
+    g = torch.Generator().manual_seed(5)
+    B, T = 512, 12
+    p = torch.randn(B + 8, T, generator=g).to(DEV)
+    y = torch.randn(B, T, generator=g).to(DEV)
+    w = (torch.rand(T, generator=g) + 0.5).to(DEV) if weighted else None
+    a = p.clone().requires_grad_()
+    la = ops.l1_loss(a, y, weights=w, per_sample=weighted, rows=B)
+    la.backward()
+    b = p.clone().requires_grad_()
+    lb = ops.l1_loss(b[:B], y, weights=w, per_sample=weighted)
+    lb.backward()
+    assert torch.equal(la, lb)
+    assert torch.equal(a.grad, b.grad)
+    assert torch.equal(a.grad[B:], torch.zeros(8, T, device=DEV))
+
+
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 def test_fused_head_matches_module_path(name, monkeypatch):
     """The fused post-pool head (one launch forward, one + a grouped weight-gradient launch
