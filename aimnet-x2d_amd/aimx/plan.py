@@ -79,7 +79,7 @@ class GraphPlan:
         ref = edges if edges is not None else (target if target is not None else batch)
         self.device = ref.device
         _lib.require_device(ref)
-        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.status = torch.empty(1, dtype=torch.int32, device=self.device)  # zeroed by the CSR build
         self.fwd = self.bwd = self.graph = None
         if edges is not None:
             e = _as_i64(edges)
@@ -112,6 +112,8 @@ class GraphPlan:
         if specs:
             for name, c in zip([sp[-1] for sp in specs], build_csrs(specs, self.device, self.status)):
                 setattr(self, name, c)
+        else:
+            self.status.zero_()
         if _VALIDATE:
             self.validate()
 

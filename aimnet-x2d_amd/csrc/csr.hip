@@ -123,6 +123,12 @@ __global__ void k_zero_i32(int32_t* __restrict__ p, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
 }
 
+// p[0..n) = 0 and, when q is non-null, *q = 0 (the multi build's status word) in the same launch
+__global__ void k_zero_i32_and(int32_t* __restrict__ p, int64_t n, int32_t* __restrict__ q) {
+  if (q && blockIdx.x == 0 && threadIdx.x == 0) *q = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
+}
+
 __global__ void k_fill(const int64_t* __restrict__ key, int64_t kstride, int64_t kmod,
                        const int64_t* __restrict__ val, int64_t vstride, int64_t vmod, int64_t n_items,
                        int64_t n_rows, const int32_t* __restrict__ rowptr, int32_t* __restrict__ cursor,
@@ -362,8 +368,8 @@ extern "C" int aimx_csr_build_multi(const AimxCsrSpec* specs, int32_t n, void* w
   ws += align256(sizeof(int32_t) * (size_t)(I + 1));
   int32_t* t_id = (int32_t*)ws;
   const int threads = 256;
-  hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>(cdiv(R + 1, threads), 4096)), dim3(threads), 0, stream,
-                     deg, R + 1);
+  hipLaunchKernelGGL(k_zero_i32_and, dim3((unsigned)std::min<int64_t>(cdiv(R + 1, threads), 4096)), dim3(threads), 0,
+                     stream, deg, R + 1, status);
   AIMX_CHECK_LAUNCH();
   const int64_t grid_items = std::min<int64_t>(cdiv(I > 0 ? I : 1, threads), 8192);
   if (I > 0) {

@@ -65,7 +65,8 @@ int aimx_csr_build(const int64_t* key, int64_t key_stride, int64_t key_mod,
 
 /* Several CSRs (at most 4) in one pass — one launch per phase for all of them. Each spec is the
  * argument set of aimx_csr_build; rowptr/col are written per spec exactly as aimx_csr_build
- * would (bit-identical), keys out of range are flagged in *status. */
+ * would (bit-identical), keys out of range are flagged in *status. *status is set to 0 first
+ * (by the call's own zero-fill launch: the caller need not zero it; a status word is per call). */
 typedef struct {
   const int64_t* key;
   int64_t key_stride, key_mod;

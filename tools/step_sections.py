@@ -37,6 +37,7 @@ def main():
     loss_fn = L1Loss()
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
     static = batches[0].clone()
+    one = torch.ones((), dtype=torch.float32, device=dev)
 
     def fwd():
         out, _, _ = model(*static.model_args())
@@ -44,15 +45,15 @@ def main():
 
     sections = {
         "forward+loss": lambda: fwd(),
-        "forward+backward": lambda: fwd().backward(),
-        "full step": lambda: (fwd().backward(), opt.step()),
+        "forward+backward": lambda: fwd().backward(one),
+        "full step": lambda: (fwd().backward(one), opt.step()),
     }
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         for _ in range(3):
             opt.zero_grad(set_to_none=True)
-            fwd().backward()
+            fwd().backward(one)
             opt.step()
     torch.cuda.current_stream().wait_stream(side)
     res = {}
@@ -84,13 +85,13 @@ def main():
                 os.environ[k] = v
             with torch.cuda.stream(side):
                 opt.zero_grad(set_to_none=True)
-                fwd().backward()
+                fwd().backward(one)
                 opt.step()
             torch.cuda.current_stream().wait_stream(side)
             opt.zero_grad(set_to_none=True)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                fwd().backward()
+                fwd().backward(one)
                 opt.step()
             for k, _ in kv:
                 os.environ.pop(k, None)
