@@ -301,9 +301,9 @@ int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, c
   for (int64_t l = L - 1; l >= 0; --l) {
     const float* dYl = nullptr;
     int64_t ldy = D;
-    if (base) {
-      dYl = (l == L - 1) ? g->d_out : base + L_->dY + (l * N * D);
-      ldy = (l == L - 1) ? g->d_out_ld : D;
+    if (base) {  // below the top layer, dY lives in the upper half of the layer's dUG (see backward)
+      dYl = (l == L - 1) ? g->d_out : base + L_->dUG + l * N * D2 + D;
+      ldy = (l == L - 1) ? g->d_out_ld : D2;
     }
     for (int64_t k = nm - 1; k >= 0; --k) {
       const int64_t idx = l * nm + k;
@@ -387,9 +387,11 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   const size_t wg_bytes = sizeof(float) * (size_t)(lay.total - lay.wg);
   const bool drop = s->training && s->drop_p > 0.f;
   for (int64_t l = L - 1; l >= 0; --l) {
+    // dUG = [du | dg] with dg = dY: below the top layer the hop backward of layer l + 1 already
+    // wrote dY into dUG's upper half (ld 2D), so only the top layer copies its upstream gradient
     float* dUG = base + lay.dUG + l * N * D2;
-    const float* dY = (l == L - 1) ? g->d_out : base + lay.dY + l * N * D;
-    const int64_t ldy = (l == L - 1) ? g->d_out_ld : D;
+    const float* dY = (l == L - 1) ? g->d_out : dUG + D;
+    const int64_t ldy = (l == L - 1) ? g->d_out_ld : D2;
     // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
     const bool fused = mlp_fused_ok(D, nm);
     if (fused) {  // the whole chain + dUG = [du | dY] in one launch (mlp.hip)
@@ -433,7 +435,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       }
     }
     // dg = dY -> dUG[:, D:] (the fused chain writes it itself)
-    if (!fused) RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
+    if (!fused && dY != dUG + D) RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
     if (aux) {  // fork: this layer's weight gradients run beside the rest of the chain
       hipEvent_t ev = (hipEvent_t)g->events[l];
       AIMX_CHECK_HIP(hipEventRecord(ev, st));
@@ -448,8 +450,8 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     }
     // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]
     const bool first = (l == 0);
-    float* nxt = first ? g->d_x_in : base + lay.dY + (l - 1) * N * D;
-    const int64_t ldn = first ? g->d_x_in_ld : D;
+    float* nxt = first ? g->d_x_in : base + lay.dUG + (l - 1) * N * D2 + D;  // layer l-1's dY slot
+    const int64_t ldn = first ? g->d_x_in_ld : D2;
     float* dst = s->use_pc ? base + lay.T0 : nxt;
     const int64_t ldd = s->use_pc ? D : ldn;
     RUN(gather(s, dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, dF, K,
