@@ -212,6 +212,7 @@ struct HopArgs {
   int32_t flat_zero;    // rows past split are one contiguous [rows - split, D] region, no adds
   int32_t nt_store;     // nontemporal stores for that fill
   int32_t interleave;   // spread the big tiles among the small ones (block order)
+  int32_t spec_stage;   // segment-aligned tiles in two round trips (process_tile_seg)
 };
 
 // All LDS is dynamic, carved at 16-byte multiples (MI355X guide: a static __shared__ ahead of the
@@ -298,6 +299,112 @@ __device__ __forceinline__ void process_tile(const HopArgs& a, HopLds& L, int32_
   __syncthreads();  // LDS is reused by the next tile of a big tile
 }
 
+// A segment-aligned tile (rows [0, split) with molecule ids) in two dependent global round trips
+// instead of four: (1) the segment cuts together with the row pointers of every row the tile can
+// span (the nominal range plus the 64-row cut window), (2) the tile's col slice together with a
+// speculative stage of the tile's own source rows [r0, r0 + nr) -- in a molecular batch a
+// molecule-aligned tile's sources are exactly its own rows. If the col range confirms it, the sum
+// runs from that stage; otherwise the span is restaged as in process_tile (same result either way).
+template <int VEC, bool SRC_CHUNKED>
+__device__ __forceinline__ void process_tile_seg(const HopArgs& a, HopLds& L, int32_t* s_col, float* s_x,
+                                                 uint32_t c0, uint32_t c1) {
+  using T = typename VecT<VEC>::T;
+  int32_t* spec = L.lohi + 2;  // [lo, hi] of the col slice (LDS head padding, see kLdsHead)
+  {
+    const uint32_t pend = min(c1 + (uint32_t)kAlignWin, a.split_rows);  // last possible cut
+    for (uint32_t t = threadIdx.x; t <= pend - c0; t += blockDim.x) L.ptr[t] = a.rowptr[c0 + t];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {
+      const uint32_t c = w ? c1 : c0;
+      uint32_t cut = c;
+      if (c > 0 && c < a.split_rows) {
+        const uint32_t q = min(c + lane, a.split_rows - 1);
+        const int64_t sq = a.seg[(int64_t)q * a.seg_stride], sp = a.seg[(int64_t)(q - 1) * a.seg_stride];
+        const unsigned long long m = __ballot((c + lane < a.split_rows) && sq != sp);
+        if (m) cut = c + (uint32_t)__builtin_ctzll(m);
+      }
+      if (lane == 0) L.lohi[w] = (int32_t)cut;
+    }
+    if (threadIdx.x == 128) {
+      spec[0] = INT32_MAX;
+      spec[1] = INT32_MIN;
+    }
+  }
+  __syncthreads();
+  const uint32_t r0 = (uint32_t)L.lohi[0], r1 = (uint32_t)L.lohi[1];
+  if (r1 <= r0) return;
+  const uint32_t nr = r1 - r0;
+  const int32_t* P = L.ptr + (r0 - c0);  // the tile's row pointers
+  const int32_t base = P[0];
+  const int32_t ncols = P[nr] - base;
+  if (ncols == 0) {
+    tile_body<VEC, true, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, P, s_col, base, r0, nr, a.out,
+                                      a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, false);
+    return;
+  }
+  if ((uint32_t)ncols >= a.col_cap || !a.xcap_rows || nr + 1 >= a.xcap_rows) {
+    tile_body<VEC, false, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, P, a.col, base, r0, nr, a.out,
+                                       a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, true);
+    return;
+  }
+  const int32_t D = (int32_t)(a.upr.d * VEC);
+  int32_t lo = INT32_MAX, hi = INT32_MIN;
+  for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) {
+    const int32_t c = a.col[base + i];
+    s_col[i] = c;
+    lo = min(lo, c);
+    hi = max(hi, c);
+  }
+  {  // speculative stage of rows [r0, r0 + nr) plus the zero row, loads in flight with the cols'
+    const uint32_t units = (nr + 1) * a.upr.d;
+    for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
+      const uint32_t rl = fdiv(t, a.upr);
+      const uint32_t u = (t - rl * a.upr.d) * VEC;
+      T v = vzero<T>();
+      if (rl < nr) v = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>(r0 + rl, a.src_ld, a.src_rpc, a.src_cs) + u);
+      *reinterpret_cast<T*>(s_x + rl * D + u) = v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o, 64));
+    hi = max(hi, __shfl_xor(hi, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&spec[0], lo);
+    atomicMax(&spec[1], hi);
+  }
+  __syncthreads();
+  lo = spec[0];
+  hi = spec[1];
+  uint32_t first = r0, span = nr;  // the staged rows
+  bool staged = lo >= (int32_t)r0 && hi < (int32_t)(r0 + nr);
+  if (!staged && (uint32_t)(hi - lo) + 1 < a.xcap_rows) {  // the guess missed: stage [lo, hi]
+    __syncthreads();
+    first = (uint32_t)lo;
+    span = (uint32_t)(hi - lo + 1);
+    const uint32_t units = (span + 1) * a.upr.d;
+    for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
+      const uint32_t rl = fdiv(t, a.upr);
+      const uint32_t u = (t - rl * a.upr.d) * VEC;
+      T v = vzero<T>();
+      if (rl < span) v = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>(first + rl, a.src_ld, a.src_rpc, a.src_cs) + u);
+      *reinterpret_cast<T*>(s_x + rl * D + u) = v;
+    }
+    staged = true;
+  }
+  if (staged) {
+    for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) s_col[i] = (s_col[i] - (int32_t)first) * D * 4;
+    if (threadIdx.x == 0) s_col[ncols] = (int32_t)span * D * 4;
+    __syncthreads();
+    tile_body_staged<VEC>(s_x, a.upr, P, s_col, ncols, base, r0, nr, a.out, a.out_ld, a.out_rpc, a.out_cs, a.add0,
+                          a.add0_ld, a.add1, a.add1_ld);
+  } else {
+    tile_body<VEC, true, SRC_CHUNKED>(a.src, a.src_ld, a.src_rpc, a.src_cs, a.upr, P, s_col, base, r0, nr, a.out,
+                                      a.out_ld, a.out_rpc, a.out_cs, a.add0, a.add0_ld, a.add1, a.add1_ld, true);
+  }
+}
+
 // Rows [0, split) (the first output chunk) run one tile per workgroup: separate workgroups overlap
 // their load phases better than tiles walked in sequence. Rows [split, rows) (hop chunks >= 1)
 // run in big tiles: a big tile whose rows hold no edges at all (the reference's chunks >= 1 are
@@ -328,6 +435,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   if (is_small) {
     uint32_t r0 = bsmall * a.tile_rows;
     uint32_t r1 = min(r0 + a.tile_rows, a.split_rows);
+    if (a.seg && a.spec_stage) {
+      process_tile_seg<VEC, SRC_CHUNKED>(a, L, s_col, s_x, r0, r1);
+      return;
+    }
     if (a.seg) {
       // Segment-aligned cuts: each nominal cut c moves to the first segment (molecule) start in
       // [c, c + 64) (c itself if none), so a tile holds whole molecules and its source rows are
@@ -473,6 +584,7 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   a.flat_zero = (contiguous && !add0 && !add1 && env_i64("AIMX_HOP_FLAT", 1) != 0) ? 1 : 0;
   a.nt_store = env_i64("AIMX_HOP_NT", 0) != 0 ? 1 : 0;
   a.interleave = env_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
+  a.spec_stage = env_i64("AIMX_HOP_SPEC", 1) != 0 ? 1 : 0;
   using KFn = void (*)(const HopArgs);
   const bool chunked = src_rpc > 0;
   KFn fn = vec == 4 ? (chunked ? k_gather_sum<4, true> : k_gather_sum<4, false>)
