@@ -156,6 +156,11 @@ __device__ __forceinline__ bool fast_ok(int n, int64_t C, int H) {
   return n <= kFastAtoms && (int64_t)n * C * 4 <= kFastXBytes && H <= kMaxH && (C % 4) == 0;
 }
 
+// head weights [H][C] staged after the fast path's sa scratch (16-B aligned: W 16-B aligned too)
+__device__ __forceinline__ bool wlds_ok(int64_t C, int H) {
+  return (int64_t)H * C * 4 + kMaxH * kFastAtoms * 4 <= kSmemBytes - kFastXBytes && (C % 4) == 0;
+}
+
 // stage rows gperm[b .. b+n) of x into xs[n][C] (16-B loads; ldx % 4 == 0 checked by the host)
 __device__ __forceinline__ void stage_rows(const float* __restrict__ x, int64_t ldx, int64_t C, int32_t b, int n,
                                            const int32_t* __restrict__ gperm, float* xs) {
@@ -175,9 +180,17 @@ __device__ __forceinline__ void attn_fwd_fast(const float* __restrict__ x, int64
                                               float* __restrict__ scores, char* smem) {
   float* xs = reinterpret_cast<float*>(smem);                      // [n][C]
   float* sa = reinterpret_cast<float*>(smem + kFastXBytes);        // [kMaxH][kFastAtoms]
+  float* ws = sa + kMaxH * kFastAtoms;                             // [H][C] when it fits
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the head weights are read once per atom by every wave: stage them beside the rows (one
+  // round trip for both) when they fit the scratch after sa, else read them from global memory
+  const bool wlds = wlds_ok(C, H) && ((uintptr_t)W & 15) == 0;
+  if (wlds)
+    for (int q = threadIdx.x; q < H * (int)C / 4; q += kThreads)
+      *reinterpret_cast<float4*>(ws + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
   stage_rows(x, ldx, C, b, n, gperm, xs);
   __syncthreads();
+  const float* Wr = wlds ? ws : W;
   // 1) scores: a wave per atom, lanes over channels (same order as attn_fwd_body)
   for (int j = w; j < n; j += kWaves) {
     float acc[kMaxH];
@@ -187,7 +200,7 @@ __device__ __forceinline__ void attn_fwd_fast(const float* __restrict__ x, int64
       const float xv = xs[j * C + c];
 #pragma unroll
       for (int h = 0; h < kMaxH; ++h)
-        if (h < H) acc[h] += xv * W[h * C + c];
+        if (h < H) acc[h] += xv * Wr[h * C + c];
     }
 #pragma unroll
     for (int h = 0; h < kMaxH; ++h) {
