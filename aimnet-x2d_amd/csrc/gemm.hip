@@ -1080,13 +1080,19 @@ void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s,
 
 }  // namespace
 
+int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, size_t workspace_bytes,
+                      int32_t* counters, int64_t n_counters, hipStream_t stream, int64_t min_wgs);
+constexpr int64_t kLoneWgs = 1024;  // workgroups a lone long-K GEMM's LDS launch aims for
+
 namespace {
 struct WgPlan {
   int tiles_x, tiles_y, splits, kchunk;
   bool lds;    // k_wgrad_lds (80 x 80 blocks) instead of k_wgrad_grouped (32 x 32 tiles)
   int64_t slab;  // floats per split-K slab
 };
-WgPlan wg_plan(const AimxWgradProblem& p) {
+// min_wgs > 0 (a lone long-K GEMM routed here): split K further until the launch has about that
+// many workgroups, so the LDS fills of a few blocks are spread over the whole chip
+WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
   const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
   const bool no_lds = e && atoi(e) == 0;
   WgPlan w;
@@ -1099,7 +1105,9 @@ WgPlan wg_plan(const AimxWgradProblem& p) {
     w.tiles_y = (int)cdiv(N, kWbB);
     const char* kp = getenv("AIMX_WGRAD_KPER");  // atoms per workgroup (tuning experiments)
     const int64_t kper = kp ? std::max(64, atoi(kp)) : 512;
-    const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
+    int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
+    if (min_wgs > 0)
+      sp = std::max(sp, std::min<int64_t>({64, p.K / 128, cdiv(min_wgs, (int64_t)w.tiles_x * w.tiles_y)}));
     w.kchunk = (int)(cdiv(cdiv(p.K, sp), kWbK) * kWbK);
     w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
     return w;
@@ -1165,7 +1173,7 @@ size_t gemm_workspace_floats(const AimxGemmArgs& a) {
   size_t f = tiled_workspace_floats(a);
   AimxWgradProblem pr;
   if (gemm_as_wgrad(a, pr)) {
-    const WgPlan w = wg_plan(pr);
+    const WgPlan w = wg_plan(pr, kLoneWgs);
     if (w.splits > 1) f = std::max(f, (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab);
   }
   return f;
@@ -1188,11 +1196,11 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   {
     AimxWgradProblem pr;
     if (gemm_as_wgrad(a, pr)) {
-      const WgPlan w = wg_plan(pr);
+      const WgPlan w = wg_plan(pr, kLoneWgs);
       const size_t need = w.splits > 1 ? sizeof(float) * w.splits * w.tiles_x * w.tiles_y * w.slab : 0;
       if ((w.splits == 1 || (a.workspace && a.workspace_bytes >= need)) && a.counters &&
           (int64_t)w.tiles_x * w.tiles_y <= a.n_counters)
-        return aimx_wgrad_grouped(&pr, 1, a.workspace, a.workspace_bytes, a.counters, a.n_counters, s);
+        return wgrad_grouped_run(&pr, 1, a.workspace, a.workspace_bytes, a.counters, a.n_counters, s, kLoneWgs);
     }
   }
   // operand layouts: each operand must be contiguous along k or along m/n; byte extents < 2 GiB
@@ -1243,26 +1251,26 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
 }  // namespace aimx
 
 
-extern "C" size_t aimx_wgrad_grouped_workspace_bytes(const AimxWgradProblem* p, int32_t n) {
+namespace aimx {
+size_t wgrad_ws_bytes(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
   if (!p || n < 0) return 0;
   size_t f = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const aimx::WgPlan w = aimx::wg_plan(p[i]);
+    const WgPlan w = wg_plan(p[i], min_wgs);
     if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab;
   }
   return sizeof(float) * f;
 }
 
-extern "C" int aimx_wgrad_grouped(const AimxWgradProblem* p, int32_t n, void* workspace, size_t workspace_bytes,
-                                  int32_t* counters, int64_t n_counters, aimx_stream_t stream) {
-  using namespace aimx;
+int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, size_t workspace_bytes,
+                      int32_t* counters, int64_t n_counters, hipStream_t stream, int64_t min_wgs) {
   if (!p || n < 0) return AIMX_EARG;
   for (int32_t i = 0; i < n; ++i)
     if (!wg_valid(p[i])) return AIMX_EARG;
-  if (workspace_bytes < aimx_wgrad_grouped_workspace_bytes(p, n) || (workspace_bytes && !workspace)) return AIMX_EARG;
+  if (workspace_bytes < wgrad_ws_bytes(p, n, min_wgs) || (workspace_bytes && !workspace)) return AIMX_EARG;
   int64_t ctiles = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i]);
+    const WgPlan w = wg_plan(p[i], min_wgs);
     ctiles += (int64_t)w.tiles_x * w.tiles_y;
   }
   if (!counters || ctiles > n_counters) return AIMX_EARG;
@@ -1291,7 +1299,7 @@ extern "C" int aimx_wgrad_grouped(const AimxWgradProblem* p, int32_t n, void* wo
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
-    const WgPlan w = wg_plan(pr);
+    const WgPlan w = wg_plan(pr, min_wgs);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {
       const int k = tb.n++;
@@ -1336,6 +1344,16 @@ extern "C" int aimx_wgrad_grouped(const AimxWgradProblem* p, int32_t n, void* wo
   if (tb.n) flush(true);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
+}
+}  // namespace aimx
+
+extern "C" size_t aimx_wgrad_grouped_workspace_bytes(const AimxWgradProblem* p, int32_t n) {
+  return aimx::wgrad_ws_bytes(p, n, 0);
+}
+
+extern "C" int aimx_wgrad_grouped(const AimxWgradProblem* p, int32_t n, void* workspace, size_t workspace_bytes,
+                                  int32_t* counters, int64_t n_counters, aimx_stream_t stream) {
+  return aimx::wgrad_grouped_run(p, n, workspace, workspace_bytes, counters, n_counters, (hipStream_t)stream, 0);
 }
 
 extern "C" size_t aimx_gemm_workspace_bytes(const AimxGemmArgs* a) {
