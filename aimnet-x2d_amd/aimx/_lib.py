@@ -280,6 +280,13 @@ def head_sync(device):
     return buf
 
 
+def head_sync_timed_out(device):
+    """True if a clustered head launch on `device` ever gave up waiting (host read: synchronises)."""
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    buf = _HEAD_SYNC.get(key)
+    return buf is not None and int(buf[0].item()) != 0
+
+
 def head_cluster():
     """Workgroups per 16-molecule tile of the fused head (AIMX_HEAD_CLUSTER, default 2)."""
     return int(os.environ.get("AIMX_HEAD_CLUSTER", "2"))

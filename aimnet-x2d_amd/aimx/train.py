@@ -20,6 +20,8 @@ from typing import Iterable, Optional
 import torch
 import torch.distributed as dist
 
+from . import _lib
+
 
 def _real_rows(batch):
     """Real (non-padding) molecules of a batch: padded batches carry real_graphs."""
@@ -134,6 +136,11 @@ def train_epoch(model, batches: Iterable, criterion, optimizer, device, sync=Non
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t)
     s, c, n = t.tolist()
+    # the clustered head's sticky timeout word (include/aimx.h AimxHead.sync): read once per epoch,
+    # after the sync above, so a cluster wait that ever gave up cannot pass silently
+    if _lib.head_sync_timed_out(dev):
+        raise RuntimeError("aimx: a clustered head launch timed out waiting for its cluster this epoch "
+                           "(results invalid; set AIMX_HEAD_CLUSTER=1)")
     return (s / c if c > 0 else 0.0), int(n)
 
 
