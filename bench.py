@@ -359,6 +359,10 @@ def main():
         dt = float(t.item())
     if feeder is not None:
         feeder.close()
+    from aimx import _lib as alib
+    head_timeout = alib.head_sync_timed_out(device)  # a clustered head wait gave up: run invalid
+    if head_timeout:
+        print("bench: a clustered head launch timed out (AIMX_HEAD_CLUSTER); results invalid", file=sys.stderr)
     atoms = sum(getattr(b, "real_atoms", b.num_atoms) for b in batches) / len(batches)
     edges = sum(getattr(b, "real_edges", b.edges.shape[0]) for b in batches) / len(batches)
     mol = cfg["batch"] * world * args.steps
@@ -392,6 +396,8 @@ def main():
         }
         if cpu is not None:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if head_timeout:
+            line["invalid"] = "clustered head wait timed out"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
