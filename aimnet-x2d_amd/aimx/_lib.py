@@ -280,6 +280,16 @@ def head_sync(device):
     return buf
 
 
+def head_sync_flag(device):
+    """The sticky timeout word of the clustered head as a float64 device scalar (0 when no
+    clustered head ran on `device`): no host synchronisation, so it can ride along in a collective."""
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    buf = _HEAD_SYNC.get(key)
+    if buf is None:
+        return torch.zeros((), dtype=torch.float64, device=device)
+    return buf[0].to(torch.float64)
+
+
 def head_sync_timed_out(device):
     """True if a clustered head launch on `device` ever gave up waiting (host read: synchronises)."""
     key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
@@ -288,8 +298,24 @@ def head_sync_timed_out(device):
 
 
 def head_cluster():
-    """Workgroups per 16-molecule tile of the fused head (AIMX_HEAD_CLUSTER, default 2)."""
-    return int(os.environ.get("AIMX_HEAD_CLUSTER", "2"))
+    """Workgroups per 16-molecule tile of the fused head.
+
+    The clustered head (2 workgroups per tile, about 3 % of the c2 step) relies on both workgroups
+    of a cluster running at once. Nothing guarantees that while other kernels share the CUs: RCCL
+    collectives under DDP, another process on the same GPU, or the auxiliary stream. So the default
+    is 2 only for a lone process (torch.distributed not initialised with world > 1, AIMX_AUX off);
+    otherwise 1, which has no inter-workgroup wait at all. AIMX_HEAD_CLUSTER overrides both. A wait
+    that still gives up poisons that launch's outputs with NaN (head.hip cluster_poisoned), so the
+    per-step NaN count of the train loop sees it on the step it happens."""
+    env = os.environ.get("AIMX_HEAD_CLUSTER")
+    if env is not None:
+        return int(env)
+    if os.environ.get("AIMX_AUX", "0") == "1":
+        return 1
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return 1
+    return 2
 
 
 def ptr(t):

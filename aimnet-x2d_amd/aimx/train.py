@@ -7,9 +7,9 @@ and, under DDP, one all-reduce of (loss sum, count) per epoch.
 
 Here the same step runs either eagerly (`train_step`) or as captured HIP graphs (`GraphedTrainStep`)
 over static padded batches (aimx.data.pad_collated / the native BatchFeeder padding): the first
-call captures forward + loss + backward (+ the RCCL gradient all-reduce, eager, between two
-graphs when world > 1) + fused clip + Adam; every later batch is copied into the static inputs
-and replayed. The per-step `loss.item()` and the NaN check of the reference are kept on the
+call captures forward + loss + backward (+ the bucketed RCCL gradient all-reduce overlapped with
+the backward when world > 1) + fused clip + Adam; every later batch is copied into the static
+inputs and replayed. The per-step `loss.item()` and the NaN check of the reference are kept on the
 device (a running loss sum and a NaN counter) and read once per epoch, so the loop never
 synchronises the host per step.
 """
@@ -48,9 +48,21 @@ class GraphedTrainStep:
     Every replayed batch must have the static batch's layout (same padded atom / edge / molecule
     counts and task count) and the same number of real molecules B (rows >= B of the per-molecule
     outputs are padding and excluded from the loss). optimizer must be capturable (FusedAdam).
+
+    Data-parallel modes (`sync`: a utils.distributed.GradientSync; `ddp_graph` or the
+    AIMX_DDP_GRAPH environment variable picks one):
+      "capture" (default over RCCL): ONE graph holds forward, backward, the bucketed RCCL
+          all-reduces (issued by the gradient hooks as their buckets fill, on RCCL's stream, so they
+          overlap the rest of the backward — DDP's reducer, reference runner.py:703-707), the
+          averaging, clip and Adam. Needs sync.capturable (overlap on, nccl backend). If the
+          capture raises on any rank, every rank falls back to "split".
+      "split": forward+backward graph, then the all-reduce eagerly, then a clip+Adam graph (the
+          only choice for gloo, whose collectives run on the host).
     """
 
-    def __init__(self, model, criterion, optimizer, example_batch, n_real=None, sync=None, warmup=3):
+    def __init__(self, model, criterion, optimizer, example_batch, n_real=None, sync=None, warmup=3,
+                 ddp_graph=None):
+        import os
         self.model, self.criterion, self.optimizer, self.sync = model, criterion, optimizer, sync
         self.B = _real_rows(example_batch) if n_real is None else int(n_real)
         self.static = example_batch.clone()
@@ -58,19 +70,32 @@ class GraphedTrainStep:
         self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
         self.nan_count = torch.zeros((), dtype=torch.int32, device=dev)
         self.steps = torch.zeros((), dtype=torch.int64, device=dev)
+        one = torch.ones((), dtype=torch.float32, device=dev)
+        padded = getattr(criterion, "padded", None)
+        B = self.B
 
         def fwd_bwd():
             out, _, _ = model(*self.static.model_args())
-            loss = criterion(out[:self.B], self.static.targets[:self.B])
-            loss.backward()
-            self.loss_sum.add_(loss.detach() * self.B)
-            self.nan_count.add_(torch.isnan(out[:self.B]).any().to(torch.int32))
+            if padded is not None:  # fused L1: padding rows' zero gradient in the loss's own launch
+                loss = padded(out, self.static.targets[:B], B)
+            else:
+                loss = criterion(out[:B], self.static.targets[:B])
+            loss.backward(one)  # d loss = 1 from a resident tensor (no per-step fill launch)
+            self.loss_sum.add_(loss.detach() * B)
+            self.nan_count.add_(torch.isnan(out[:B]).any().to(torch.int32))
             self.steps.add_(1)
 
         self._fwd_bwd = fwd_bwd
+        mode = ddp_graph or os.environ.get("AIMX_DDP_GRAPH") or "capture"
+        if mode not in ("capture", "split"):
+            raise ValueError(f"ddp_graph must be 'capture' or 'split', not {mode!r}")
+        if sync is None or not sync.active:
+            mode = "single"
+        elif mode == "capture" and not sync.capturable:
+            mode = "split"
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):  # warm-up: allocator pools, plans, optimizer state, lazy loads
+        with torch.cuda.stream(side):  # warm-up: allocator pools, plans, optimizer state, RCCL comms
             for _ in range(warmup):
                 optimizer.zero_grad(set_to_none=True)
                 fwd_bwd()
@@ -78,19 +103,48 @@ class GraphedTrainStep:
                     sync.finish()
                 optimizer.step()
         torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
         optimizer.zero_grad(set_to_none=True)
         self.g1 = torch.cuda.CUDAGraph()
         self.g2 = None
-        if sync is None:
+        if mode == "single":
             with torch.cuda.graph(self.g1):
                 fwd_bwd()
                 optimizer.step()
-        else:
+        elif mode == "capture":
+            ok = True
+            err = None
+            if dist.is_initialized():
+                dist.barrier()
+                torch.cuda.synchronize(dev)
+            try:
+                # thread_local: RCCL's watchdog thread may query events while this thread captures
+                with torch.cuda.graph(self.g1, capture_error_mode="thread_local"):
+                    fwd_bwd()
+                    sync.finish()
+                    optimizer.step()
+            except RuntimeError as e:  # pragma: no cover (depends on the RCCL build)
+                ok, err = False, e
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                import sys
+                print(f"aimx.train: RCCL all-reduce capture failed ({err}); using split graphs", file=sys.stderr)
+                sync._reset()
+                optimizer.zero_grad(set_to_none=True)
+                self.g1 = torch.cuda.CUDAGraph()
+                mode = "split"
+        if mode == "split":
             self.g2 = torch.cuda.CUDAGraph()
+            hooks, sync._hooks = sync._hooks, []  # the eager all-reduce runs between the graphs
+            for h in hooks:
+                h.remove()
+            sync.overlap = False
             with torch.cuda.graph(self.g1):
                 fwd_bwd()
             with torch.cuda.graph(self.g2):
                 optimizer.step()
+        self.mode = mode
         self.reset_stats()
 
     def reset_stats(self):
@@ -101,6 +155,10 @@ class GraphedTrainStep:
     def __call__(self, batch=None):
         """Copy `batch` (a DeviceBatch of the static layout) into the static inputs and replay."""
         if batch is not None:
+            n_real = _real_rows(batch)
+            if n_real != self.B:  # e.g. a trailing partial batch: padding rows would enter the loss
+                raise ValueError(f"GraphedTrainStep: batch has {n_real} real molecules, the captured step "
+                                 f"takes exactly {self.B} (run partial batches through train_step)")
             self.static.copy_(batch)
         self.g1.replay()
         if self.g2 is not None:
@@ -132,13 +190,15 @@ def train_epoch(model, batches: Iterable, criterion, optimizer, device, sync=Non
     if graphed is not None:
         loss_sum = graphed.loss_sum.double()
         nans = graphed.nan_count.to(torch.int64)
-    t = torch.stack([loss_sum, torch.tensor(float(count), dtype=torch.float64, device=dev), nans.double()])
+    # the clustered head's sticky timeout word (include/aimx.h AimxHead.sync) rides along in the
+    # epoch's one collective, so every rank sees any rank's timeout and all of them raise together
+    # (a rank raising alone would leave the others blocked in the next collective)
+    t = torch.stack([loss_sum, torch.tensor(float(count), dtype=torch.float64, device=dev), nans.double(),
+                     _lib.head_sync_flag(dev)])
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t)
-    s, c, n = t.tolist()
-    # the clustered head's sticky timeout word (include/aimx.h AimxHead.sync): read once per epoch,
-    # after the sync above, so a cluster wait that ever gave up cannot pass silently
-    if _lib.head_sync_timed_out(dev):
+    s, c, n, tmo = t.tolist()
+    if tmo != 0:
         raise RuntimeError("aimx: a clustered head launch timed out waiting for its cluster this epoch "
                            "(results invalid; set AIMX_HEAD_CLUSTER=1)")
     return (s / c if c > 0 else 0.0), int(n)
@@ -196,7 +256,7 @@ def main(argv=None):
     model = GNN(fs, a.hidden, 1, num_shells=a.hops).to(dev).train()
     crit = L1Loss()
     opt = FusedAdam(model.parameters(), lr=a.lr, max_grad_norm=1.0)
-    sync = GradientSync(model.parameters(), overlap=a.eager) if world > 1 else None
+    sync = GradientSync(model.parameters(), unused=model.unused_parameters()) if world > 1 else None
     B = a.batch
     shard = tr_idx[rank::world]  # disjoint per rank (DistributedSampler semantics)
     steps = len(shard) // B

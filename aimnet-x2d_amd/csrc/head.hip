@@ -314,10 +314,23 @@ __device__ __forceinline__ void cluster_done(const Cluster& cl, const AimxHead& 
   }
 }
 
+// Clustered: has any wait of this launch (or an earlier one: the word is sticky) given up? Read
+// once per tile before the final GEMM; the tile's outputs are then written as NaN, so the per-step
+// NaN count of the train loop (aimx.train) catches a lost hand-off on the step it happens instead
+// of letting stale rows reach the optimizer. A workgroup that timed out stored the word before its
+// next arrival, so a partner released by that arrival reads it too.
+__device__ __forceinline__ bool cluster_poisoned(const Cluster& cl, int* s_flag) {
+  if (cl.S == 1) return false;
+  if (threadIdx.x == 0) *s_flag = __hip_atomic_load((gi32*)cl.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // Forward. A cluster (or a lone workgroup) walks the 16-molecule tiles tile, tile + #clusters, ...
 template <int W>
 __global__ __launch_bounds__(64 * W) void k_head_fwd(const AimxHead h) {
   __shared__ __attribute__((aligned(16))) float lds[kHeadLdsFloats];
+  __shared__ int s_poison;
   constexpr int NT = 64 * W;
   float* X = lds;                    // current block input y (then z)   [16][kS1]
   float* Hb = X + kR * kS1;          // block hidden h                  [16][kS1]
@@ -419,8 +432,9 @@ __global__ __launch_bounds__(64 * W) void k_head_fwd(const AimxHead h) {
     exchange<W>(cl, h.cat + g0 * 2 * F + F, 2 * F, nvalid, F, Cb + F, kS2);
     HEAD_STAMP(0 + st++);
     // out = [z | s] Wo^T + bo
+    const bool bad = cluster_poisoned(cl, &s_poison);
     chain_gemm<W>(cl, Cb, kS2, jo, jp, R, bias(h.bo), [&](int r, int c, float acc, float2 p) {
-      if (g0 + r < G) h.out[(g0 + r) * h.ldo + c] = acc + p.x;
+      if (g0 + r < G) h.out[(g0 + r) * h.ldo + c] = bad ? __builtin_nanf("") : acc + p.x;
     });
     HEAD_STAMP(0 + st++);
     __syncthreads();  // the next tile overwrites Cb
@@ -434,6 +448,7 @@ __global__ __launch_bounds__(64 * W) void k_head_fwd(const AimxHead h) {
 template <int W>
 __global__ __launch_bounds__(64 * W) void k_head_bwd(const AimxHead h, const AimxHeadGrad d) {
   __shared__ __attribute__((aligned(16))) float lds[kHeadLdsFloats];
+  __shared__ int s_poison;
   constexpr int NT = 64 * W;
   float* DZ = lds;                    // gradient w.r.t. the current block output  [16][kS1]
   float* DV = DZ + kR * kS1;          // ds, then dv of each block                [16][kS1]
@@ -524,8 +539,9 @@ __global__ __launch_bounds__(64 * W) void k_head_bwd(const AimxHead h, const Aim
       HEAD_STAMP(32 + st++);
     }
     // d x_pooled = dy0 Wp
+    const bool bad = cluster_poisoned(cl, &s_poison);
     chain_gemm<W>(cl, DZ, kS1, jp, jo, R, none, [&](int r, int c, float acc, float2) {
-      if (g0 + r < G) d.d_x0[(g0 + r) * d.ld_dx0 + c] = acc;
+      if (g0 + r < G) d.d_x0[(g0 + r) * d.ld_dx0 + c] = bad ? __builtin_nanf("") : acc;
     });
     HEAD_STAMP(32 + st++);
     __syncthreads();  // the next tile overwrites DO

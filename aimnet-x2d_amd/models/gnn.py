@@ -298,6 +298,11 @@ class GNN(nn.Module):
                 if head.bias is not None:
                     nn.init.zeros_(head.bias)
 
+    def unused_parameters(self):
+        """Parameters the forward never touches: long_range_projection (constructed by the reference,
+        gnn.py:146, never called in forward). Data-parallel sync leaves them out (GradientSync(unused=))."""
+        return list(self.long_range_projection.parameters())
+
     def get_model_info(self) -> Dict[str, object]:
         total = sum(p.numel() for p in self.parameters())
         trainable = sum(p.numel() for p in self.parameters() if p.requires_grad)

@@ -18,6 +18,11 @@ class L1Loss(nn.Module):
     def forward(self, y_pred: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:
         return ops.l1_loss(y_pred, y_true)
 
+    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int) -> torch.Tensor:
+        """forward(y_pred[:rows], y_true) for a static padded batch, the padding rows' zero gradient
+        written by the same backward launch (no slice-backward fill + copy)."""
+        return ops.l1_loss(y_pred, y_true, rows=rows)
+
 
 class WeightedL1Loss(nn.Module):
     """sum over tasks of w_t |y_pred - y_true|, averaged over samples (reference losses.py:14-48)."""
@@ -28,3 +33,6 @@ class WeightedL1Loss(nn.Module):
 
     def forward(self, y_pred: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:
         return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True)
+
+    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int) -> torch.Tensor:
+        return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True, rows=rows)

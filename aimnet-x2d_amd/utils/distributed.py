@@ -126,18 +126,39 @@ class GradientSync:
 
     usage:  sync = GradientSync(model.parameters())
             loss.backward(); sync.finish(); clip; optimizer.step()
+
+    Buckets follow DDP's reducer (reference runner.py:703-707 wraps the model in DDP with its
+    defaults): reverse registration order, a small first bucket (first_bucket_mb, DDP's 1 MiB) so
+    the collectives start early in the backward, then bucket_mb (DDP's 25 MiB) buckets.
+
+    `unused`: parameters the model never uses in forward (GNN.long_range_projection, reference
+    gnn.py:146): they take no part in the sync and keep grad None, as DDP(find_unused_parameters)
+    leaves them; without this their bucket could only start at finish(). Every rank must pass the
+    same set.
+
+    Graph capture: with overlap, each bucket's pack + RCCL all-reduce is issued from the
+    post-accumulate-grad hook of its last gradient; inside torch.cuda.graph capture those calls
+    are recorded as graph nodes on RCCL's stream, forked from and joined back (finish()) to the
+    capturing stream, so a replay runs them concurrently with the rest of the backward
+    (aimx.train.GraphedTrainStep "capture" mode). `always=True` runs the bucket path even at world
+    size 1 (tests of that mechanism on a one-GPU box).
     """
 
-    def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True):
-        self.params = [p for p in params if p.requires_grad]
+    def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True,
+                 first_bucket_mb: float = 1.0, unused=(), always: bool = False):
+        skip = {id(p) for p in unused}
+        self.params = [p for p in params if p.requires_grad and id(p) not in skip]
         self.group = process_group
         self.world = dist.get_world_size(process_group) if _ready() else 1
-        self.overlap = overlap and self.world > 1
+        self.active = self.world > 1 or (always and _ready())
+        self.overlap = overlap and self.active
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        cap0 = max(1, int(min(first_bucket_mb, bucket_mb) * 1024 * 1024 / 4))
         self.buckets: List[List[torch.nn.Parameter]] = []
         cur, size = [], 0
         for p in reversed(self.params):  # backward produces late layers first
-            if cur and size + p.numel() > cap:
+            limit = cap0 if not self.buckets else cap
+            if cur and size + p.numel() > limit:
                 self.buckets.append(cur)
                 cur, size = [], 0
             cur.append(p)
@@ -153,6 +174,15 @@ class GradientSync:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self._reset()
+
+    @property
+    def backend(self) -> str:
+        return dist.get_backend(self.group) if _ready() else ""
+
+    @property
+    def capturable(self) -> bool:
+        """True when the collectives can be recorded into a HIP graph (RCCL; gloo runs on the host)."""
+        return self.overlap and self.backend == "nccl"
 
     def _reset(self):
         self._pending = [len(b) for b in self.buckets]
@@ -178,7 +208,7 @@ class GradientSync:
 
     def finish(self):
         """Complete every bucket's all-reduce and write averaged gradients back into .grad."""
-        if self.world == 1:
+        if not self.active:
             self._reset()
             return
         for i in range(len(self.buckets)):
@@ -186,7 +216,9 @@ class GradientSync:
                 self._launch(i)
         for i, bucket in enumerate(self.buckets):
             self._handles[i].wait()
-            flat = self._flat[i].div_(self.world)
+            flat = self._flat[i]
+            if self.world > 1:
+                flat.div_(self.world)
             dst, src, off = [], [], 0
             for p in bucket:
                 n = p.numel()

@@ -82,7 +82,7 @@ def make_batches(cfg, n_batches, seed, device, pad=False):
         tg = np.concatenate([t, np.zeros((PAD_MOLS, t.shape[1]), np.float32)])
         qq = np.concatenate([q, np.zeros(PAD_MOLS, np.float32)])
         b = adata.DeviceBatch(pc, device, targets=tg, total_charges=qq)
-        b.real_atoms, b.real_edges = real_atoms, real_edges
+        b.real_atoms, b.real_edges, b.real_graphs = real_atoms, real_edges, cfg["batch"]
         out.append(b)
     return out
 
@@ -256,81 +256,23 @@ def main():
     from models import L1Loss
     loss_fn = L1Loss()  # the reference criterion (nn.L1Loss, trainer.py:34) as one fused launch each way
 
+    sync = None
+    if world > 1:
+        # DDP-equivalent bucketed all-reduce (reference runner.py:703-707); the unused
+        # long_range_projection (gnn.py:146) takes no part, as under find_unused_parameters
+        sync = GradientSync(model.parameters(), unused=model.unused_parameters())
+    opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)  # clip(1.0) + Adam, trainer.py:163-164
+    graphed = None
     if args.graph:
-        # Whole-step HIP-graph capture on static padded inputs: the captured step is the full
-        # forward + backward (+ RCCL all-reduce, eager, between two graphs when world > 1)
-        # + grad-norm clip + Adam; each timed step copies a fresh resident batch into the static
-        # inputs and replays.
-        # reference step: clip_grad_norm_(1.0) + Adam (trainer.py:163-164), fused on the device
-        opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
-        sync = GradientSync(model.parameters(), overlap=False) if world > 1 else None
-        static = batches[0].clone()
-        one = torch.ones((), dtype=torch.float32, device=device)
-
-        def fwd_bwd():
-            out, _, _ = model(*static.model_args())
-            # nn.L1Loss of the B real molecules; the padding rows' zero gradient comes from the
-            # same backward launch (ops.l1_loss rows=B) instead of a slice-backward fill + copy
-            loss = ops.l1_loss(out, static.targets[:B], rows=B)
-            loss.backward(one)  # d loss = 1 from a resident tensor (no per-step fill launch)
-            return loss
-
-        def clip_step():
-            opt.step()
-
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(3):
-                opt.zero_grad(set_to_none=True)
-                fwd_bwd()
-                if sync is not None:
-                    sync.finish()
-                clip_step()
-        torch.cuda.current_stream().wait_stream(side)
-        opt.zero_grad(set_to_none=True)
-        g1, g2 = torch.cuda.CUDAGraph(), None
-        if sync is None:
-            with torch.cuda.graph(g1):
-                fwd_bwd()
-                clip_step()
-        else:
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                fwd_bwd()
-            with torch.cuda.graph(g2):
-                clip_step()
-
-        # diagnostic: AIMX_BENCH_PHASES=1 synchronising per-phase times, =2 host-side call times only
-        phases = int(os.environ.get("AIMX_BENCH_PHASES", "0"))
-        hsync = torch.cuda.synchronize if phases == 1 else (lambda: None)
+        # Whole-step HIP-graph capture on static padded inputs (aimx.train.GraphedTrainStep): forward,
+        # backward, the bucketed RCCL all-reduces overlapped with the backward (world > 1), clip and
+        # Adam; each timed step copies a fresh resident batch into the static inputs and replays.
+        from aimx.train import GraphedTrainStep
+        graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync)
 
         def step(i):
-            static.copy_(next(feeder) if feeder is not None else batches[i % len(batches)])
-            if phases:
-                hsync()
-                t0 = time.perf_counter()
-            g1.replay()
-            if phases:
-                hsync()
-                t1 = time.perf_counter()
-            if g2 is not None:
-                sync.finish()
-                if phases:
-                    hsync()
-                    t2 = time.perf_counter()
-                g2.replay()
-            if phases:
-                hsync()
-                t3 = time.perf_counter()
-                if rank == 0:
-                    print(json.dumps({"step": i, "fwd_bwd_ms": round((t1 - t0) * 1e3, 3),
-                                      "sync_ms": round((t2 - t1) * 1e3, 3) if g2 is not None else None,
-                                      "opt_ms": round((t3 - (t2 if g2 is not None else t1)) * 1e3, 3)}), flush=True)
+            graphed(next(feeder) if feeder is not None else batches[i % len(batches)])
     else:
-        opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
-        sync = GradientSync(model.parameters()) if world > 1 else None
-
         def step(i):
             b = next(feeder) if feeder is not None else batches[i % len(batches)]
             opt.zero_grad(set_to_none=True)
@@ -360,7 +302,11 @@ def main():
     if feeder is not None:
         feeder.close()
     from aimx import _lib as alib
-    head_timeout = alib.head_sync_timed_out(device)  # a clustered head wait gave up: run invalid
+    # a clustered head wait gave up on ANY rank: the run is invalid (max over ranks)
+    tmo = alib.head_sync_flag(device).reshape(1)
+    if world > 1:
+        dist.all_reduce(tmo, op=dist.ReduceOp.MAX)
+    head_timeout = bool(tmo.item() != 0)
     if head_timeout:
         print("bench: a clustered head launch timed out (AIMX_HEAD_CLUSTER); results invalid", file=sys.stderr)
     atoms = sum(getattr(b, "real_atoms", b.num_atoms) for b in batches) / len(batches)
@@ -394,6 +340,13 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if world > 1:
+            line["ddp"] = {"world_size_reported": dist.get_world_size(), "backend": dist.get_backend(),
+                           "graph_mode": graphed.mode if graphed is not None else "eager",
+                           "buckets": len(sync.buckets),
+                           "bucket_mb": [round(sum(p.numel() for p in bk) * 4 / 2 ** 20, 3) for bk in sync.buckets]}
+            if args.gpus != world:
+                line["ddp"]["note"] = f"--gpus {args.gpus} but WORLD_SIZE {world}"
         if cpu is not None:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         if head_timeout:

@@ -107,3 +107,20 @@ def test_gradient_sync_equals_mean_of_rank_gradients():
             want = (grads[0][n] + grads[1][n]) / 2
             for r in range(2):
                 assert torch.allclose(torch.tensor(out[r][overlap][n]), want, atol=1e-6), (n, overlap)
+
+
+def test_gradient_sync_bucket_layout():
+    """DDP's reducer layout: reverse registration order, a small first bucket, unused params out."""
+    from utils.distributed import GradientSync
+    net = torch.nn.Sequential(torch.nn.Linear(512, 512), torch.nn.Linear(512, 512), torch.nn.Linear(512, 512),
+                              torch.nn.Linear(512, 4))
+    sync = GradientSync(net.parameters(), bucket_mb=2.0, first_bucket_mb=1.0, unused=list(net[1].parameters()))
+    names = {id(p): n for n, p in net.named_parameters()}
+    layout = [[names[id(p)] for p in b] for b in sync.buckets]
+    assert layout[0] == ["3.bias", "3.weight", "2.bias"]  # 2.weight (1 MiB) would overflow the 1 MiB first bucket
+    assert all("1." not in n for b in layout for n in b)
+    assert sum(len(b) for b in layout) == 6
+    for b in sync.buckets[1:]:
+        assert sum(p.numel() for p in b) * 4 <= 2 * 2 ** 20 or len(b) == 1
+    assert not sync.active and not sync.capturable  # no process group: finish() is a no-op
+    sync.finish()

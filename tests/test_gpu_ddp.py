@@ -1,0 +1,225 @@
+"""GPU: data-parallel training of the GNN (reference runner.py:703-707 DDP + utils/distributed.py).
+
+* Two ranks, each on half of a batch, synced by GradientSync, give the full-batch gradients of
+  one process (DDP's defining property), with and without the backward-overlapped bucket hooks.
+  The ranks share the box's one GPU over gloo (RCCL refuses two ranks on one device).
+* The split-graph data-parallel step (captured forward+backward, eager all-reduce, captured
+  clip+Adam) keeps both replicas identical and equals the eager data-parallel step.
+* The captured RCCL all-reduce ("capture" mode: one graph with the bucket all-reduces on RCCL's
+  stream, overlapping the backward) at world size 1 over the real RCCL backend: the capture
+  succeeds and the replayed step equals the eager step.
+Every rank is a fresh spawned process (no fork of an initialised HIP context).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG, ROOT
+
+pytestmark = pytest.mark.gpu
+HOPS = 3
+B_HALF = 32
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, backend, fn_name, q):
+    import sys
+    sys.path[:0] = [ROOT, PKG, os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    try:
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        import test_gpu_ddp as T
+        q.put((rank, getattr(T, fn_name)(rank, world)))
+    except BaseException as e:  # report, do not hang the parent
+        import traceback
+        q.put((rank, {"error": f"{type(e).__name__}: {e}\n{traceback.format_exc()}"}))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(fn_name, world=2, backend="gloo"):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, backend, fn_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, v = q.get(timeout=100)
+            out[r] = v
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r, v in out.items():
+        assert "error" not in v, f"rank {r}: {v['error']}"
+    return out
+
+
+def _model(seed=0):
+    from models import GNN
+    torch.manual_seed(seed)
+    fs = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+    # dropout off: the ranks' and the full batch's gradients are then deterministic functions of the data
+    return GNN(fs, 128, 1, num_shells=HOPS, shell_conv_dropout=0.0, ffn_dropout=0.0).to("cuda").train()
+
+
+def _qm9_batch(idx):
+    from aimx import data as adata
+    from aimx.synth import QM9Asset
+    asset = QM9Asset()
+    col = adata.collate(asset.molecules(idx), HOPS)
+    y = asset.targets[idx][:, :1].astype(np.float32)
+    y = (y - 2.7) / 1.5
+    return adata.DeviceBatch(col, "cuda", targets=y, total_charges=asset.total_charge[idx].astype(np.float32))
+
+
+def _grads(model):
+    return {n: p.grad.detach().cpu().numpy().copy() for n, p in model.named_parameters() if p.grad is not None}
+
+
+def ddp_grads(rank, world):
+    """Each rank: half of molecules [0, 2*B_HALF); GradientSync with and without overlap."""
+    from models import L1Loss
+    from utils.distributed import GradientSync
+    res = {}
+    b = _qm9_batch(np.arange(rank * B_HALF, (rank + 1) * B_HALF))
+    for overlap in (True, False):
+        m = _model()
+        sync = GradientSync(m.parameters(), overlap=overlap, unused=m.unused_parameters(), bucket_mb=0.25,
+                            first_bucket_mb=0.05)
+        out, _, _ = m(*b.model_args())
+        L1Loss()(out, b.targets).backward()
+        sync.finish()
+        torch.cuda.synchronize()
+        res[overlap] = _grads(m)
+        res[f"buckets{overlap}"] = len(sync.buckets)
+        sync.remove()
+    return res
+
+
+def test_two_ranks_equal_full_batch_gradients():
+    from models import L1Loss
+    out = _run("ddp_grads")
+    m = _model()
+    b = _qm9_batch(np.arange(2 * B_HALF))
+    o, _, _ = m(*b.model_args())
+    L1Loss()(o, b.targets).backward()
+    full = _grads(m)
+    assert "long_range_projection.weight" not in full
+    for overlap in (True, False):
+        assert out[0][f"buckets{overlap}"] > 2  # several buckets: the hooks path really overlaps
+        for r in range(2):
+            got = out[r][overlap]
+            assert set(got) == set(full), (overlap, r)
+            for k, want in full.items():
+                den = max(np.abs(want).max(), 1e-12)
+                err = np.abs(got[k] - want).max() / den
+                # 1e-5 norm-relative (north star); the attention bias gradient is exactly 0 in exact
+                # arithmetic (softmax shift invariance): judge it against its weight's scale
+                if ".attention_weights." in k and k.endswith(".bias"):
+                    err = np.abs(got[k] - want).max() / max(np.abs(full[k[:-4] + "weight"]).max(), 1e-12)
+                assert err <= 1e-5, (k, overlap, r, err)
+
+
+def _padded_batches(rank, n_steps):
+    from aimx import feed
+    from aimx.synth import QM9Asset
+    asset = QM9Asset()
+    y = asset.targets[:, :1]
+    store = feed.HostStore.from_arrays(asset.atom_off, asset.bond_off, np.stack([asset.bi, asset.bj], 1), asset.feats,
+                                       ((y - y.mean()) / y.std()).astype(np.float32), asset.total_charge,
+                                       precompute_hops=HOPS)
+    rng = np.random.default_rng(7)
+    idx = [rng.integers(0, len(store), 2 * B_HALF)[rank * B_HALF:(rank + 1) * B_HALF] for _ in range(n_steps)]
+    return list(feed.BatchFeeder(store, iter(idx), HOPS, "cuda", depth=2, n_max=1400, e_max=14000, pad_mols=8))
+
+
+def ddp_split_graph(rank, world):
+    """Split-graph data-parallel steps (gloo) vs the eager data-parallel steps on the same batches."""
+    from aimx.optim import FusedAdam
+    from aimx.train import GraphedTrainStep, train_step
+    from models import L1Loss
+    from utils.distributed import GradientSync
+    bs = _padded_batches(rank, 4)
+    res = {}
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    sync = GradientSync(m.parameters(), unused=m.unused_parameters())
+    g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1)
+    for b in bs[1:]:
+        g(b)
+    torch.cuda.synchronize()
+    res["mode"] = g.mode
+    res["graph"] = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    sync.remove()
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    sync = GradientSync(m.parameters(), unused=m.unused_parameters())
+    for b in bs:  # eager: the graph's warm-up step on bs[0] included
+        train_step(m, b, L1Loss(), opt, sync=sync, n_real=B_HALF)
+    torch.cuda.synchronize()
+    res["eager"] = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    return res
+
+
+def test_split_graph_ddp_replicas_agree_and_equal_eager():
+    out = _run("ddp_split_graph")
+    assert out[0]["mode"] == out[1]["mode"] == "split"  # gloo collectives cannot be captured
+    np.testing.assert_array_equal(out[0]["graph"], out[1]["graph"])  # replicas stay identical
+    np.testing.assert_array_equal(out[0]["eager"], out[1]["eager"])
+    scale = np.abs(out[0]["eager"]).max()
+    assert np.abs(out[0]["graph"] - out[0]["eager"]).max() <= 1e-5 * scale
+
+
+def rccl_capture_world1(rank, world):
+    """One RCCL rank: the bucket all-reduces are recorded inside the step's single graph."""
+    from aimx.optim import FusedAdam
+    from aimx.train import GraphedTrainStep, train_step
+    from models import L1Loss
+    from utils.distributed import GradientSync
+    bs = _padded_batches(0, 4)
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    sync = GradientSync(m.parameters(), unused=m.unused_parameters(), always=True, bucket_mb=0.25,
+                        first_bucket_mb=0.05)
+    g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1)
+    for b in bs[1:]:
+        g(b)
+    torch.cuda.synchronize()
+    got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    for b in bs:
+        train_step(m, b, L1Loss(), opt, n_real=B_HALF)
+    torch.cuda.synchronize()
+    want = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    return {"mode": g.mode, "buckets": len(sync.buckets), "err": float(np.abs(got - want).max()),
+            "scale": float(np.abs(want).max())}
+
+
+def test_rccl_allreduce_captured_in_step_graph():
+    out = _run("rccl_capture_world1", world=1, backend="nccl")[0]
+    assert out["mode"] == "capture", out
+    assert out["buckets"] > 2
+    assert out["err"] <= 1e-5 * out["scale"], out
