@@ -299,9 +299,13 @@ class GNN(nn.Module):
                     nn.init.zeros_(head.bias)
 
     def unused_parameters(self):
-        """Parameters the forward never touches: long_range_projection (constructed by the reference,
-        gnn.py:146, never called in forward). Data-parallel sync leaves them out (GradientSync(unused=))."""
-        return list(self.long_range_projection.parameters())
+        """Parameters the forward never touches: long_range_projection (gnn.py:146) and, with
+        stereochemistry, stereochemical_embedding (gnn.py:194) — the reference constructs both and
+        never calls them. Data-parallel sync leaves them out (GradientSync(unused=))."""
+        out = list(self.long_range_projection.parameters())
+        if hasattr(self, "stereochemical_embedding"):
+            out += list(self.stereochemical_embedding.parameters())
+        return out
 
     def get_model_info(self) -> Dict[str, object]:
         total = sum(p.numel() for p in self.parameters())

@@ -219,6 +219,9 @@ def main():
                          "step's batch is collated by the C++ batch builder from the molecule store and "
                          "copied host->device inside the timed region (PCIe-inclusive rate)")
     ap.add_argument("--feed-threads", type=int, default=4)
+    ap.add_argument("--ddp-world1", action="store_true",
+                    help="A/B of the data-parallel step on one GPU: a world-size-1 RCCL group with the bucket "
+                         "all-reduces kept (GradientSync always=True); AIMX_DDP_GRAPH=capture|split picks the mode")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
@@ -261,6 +264,15 @@ def main():
         # DDP-equivalent bucketed all-reduce (reference runner.py:703-707); the unused
         # long_range_projection (gnn.py:146) takes no part, as under find_unused_parameters
         sync = GradientSync(model.parameters(), unused=model.unused_parameters())
+    elif args.ddp_world1:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=device)
+        sync = GradientSync(model.parameters(), unused=model.unused_parameters(), always=True)
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)  # clip(1.0) + Adam, trainer.py:163-164
     graphed = None
     if args.graph:
@@ -340,7 +352,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu,
         }
-        if world > 1:
+        if sync is not None:
             line["ddp"] = {"world_size_reported": dist.get_world_size(), "backend": dist.get_backend(),
                            "graph_mode": graphed.mode if graphed is not None else "eager",
                            "buckets": len(sync.buckets),
@@ -352,7 +364,7 @@ def main():
         if head_timeout:
             line["invalid"] = "clustered head wait timed out"
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

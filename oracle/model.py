@@ -142,13 +142,58 @@ def mlp(p, pre, x, cfg, training):
     return x
 
 
+def cis_trans(x, cis, trans):
+    """gnn.py:452-497 (_cis_trans_calculation): rows 0 and 1 of the collated [M, 2] cis / trans
+    tensors are the source and target atom lists (as the reference indexes them); cis sources are
+    subtracted, trans sources added, by one scatter_add onto a copy of x."""
+    if cis.numel() == 0 and trans.numel() == 0:
+        return x
+    tg, sv = [], []
+    if cis.numel() > 0:
+        tg.append(cis[1])
+        sv.append(-x[cis[0]])
+    if trans.numel() > 0:
+        tg.append(trans[1])
+        sv.append(x[trans[0]])
+    t = torch.cat(tg)
+    return x.scatter_add(0, t.unsqueeze(1).expand(-1, x.shape[1]), torch.cat(sv))
+
+
+def tetrahedral(x, tet):
+    """gnn.py:376-450 (_tetrahedral_feature_calculation_physics_inspired): for every chiral centre's
+    4 neighbour rows e (unit-normalised, eps 1e-8), chi = e1^2 (e2 - e3) + e2^2 (e3 - e1) +
+    e3^2 (e1 - e2) with e_k = roll(e, -k) over the 4 neighbours, scaled by tanh(mean |row| / 3),
+    index_add_-ed onto a copy of x at the neighbour rows; rows named by no centre become 0."""
+    if tet.numel() == 0:
+        return x
+    out = x.clone()
+    raw = out[tet]
+    mag = torch.norm(raw, dim=-1, keepdim=True)
+    e = F.normalize(raw, dim=-1, eps=1e-8)
+    sq = e ** 2
+    r = lambda t, k: torch.roll(t, shifts=-k, dims=1)  # noqa: E731
+    chi = r(sq, 1) * (r(e, 2) - r(e, 3)) + r(sq, 2) * (r(e, 3) - r(e, 1)) + r(sq, 3) * (r(e, 1) - r(e, 2))
+    chi = chi * torch.tanh(torch.mean(mag, dim=1, keepdim=True) / 3.0)
+    idx = tet.reshape(-1)
+    out.index_add_(0, idx, chi.reshape(-1, out.shape[-1]))
+    keep = torch.zeros(out.shape[0], dtype=torch.bool, device=out.device)
+    keep[torch.unique(idx)] = True
+    out[~keep] = 0.0
+    return out
+
+
+def stereo(p, x, tet, cis, trans):
+    """gnn.py:310-326 (_apply_stereochemistry): Linear(3D -> D) of [x | cis_trans(x) | tetrahedral(x)]."""
+    return linear(p, "stereochemical_embedding_2", torch.cat([x, cis_trans(x, cis, trans), tetrahedral(x, tet)], -1))
+
+
 def default_config(**kw):
     """GNN.__init__ defaults (gnn.py:50-70)."""
     cfg = dict(hidden_dim=512, output_dim=1, num_shells=3, num_message_passing_layers=3,
                ffn_hidden_dim=None, ffn_num_layers=3, pooling_type="attention", embedding_dim=64,
                use_partial_charges=False, ffn_dropout=0.05, activation="silu",
                shell_conv_num_mlp_layers=2, shell_conv_dropout=0.05, attention_num_heads=4,
-               attention_temperature=1.0, loss_function="l1")
+               attention_temperature=1.0, loss_function="l1", use_stereochemistry=False)
     cfg.update(kw)
     if cfg["ffn_hidden_dim"] is None:
         cfg["ffn_hidden_dim"] = cfg["hidden_dim"]
@@ -156,8 +201,10 @@ def default_config(**kw):
     return cfg
 
 
-def gnn_forward(p, cfg, atom_features, edges, batch, total_charges, training=False, capture=None):
-    """gnn.py:197-260 (GNN.forward) without stereochemistry (off in every BASELINE config).
+def gnn_forward(p, cfg, atom_features, edges, batch, total_charges, training=False, capture=None, tet=None, cis=None,
+                trans=None):
+    """gnn.py:197-260 (GNN.forward); stereochemistry (gnn.py:297-300) when cfg['use_stereochemistry'],
+    from the collated tetrahedral [M, 4] / cis [C, 2] / trans [T, 2] tensors.
 
     Returns (output [G, T or 4T], attention [H, N] or None, partial_charges [N] or None).
     `capture` (dict) receives intermediate tensors: 'x_other_in', 'layer{l}', 'chunks0', 'pre_pool'.
@@ -177,6 +224,10 @@ def gnn_forward(p, cfg, atom_features, edges, batch, total_charges, training=Fal
         for l in range(cfg["num_message_passing_layers"]):
             if cfg["use_partial_charges"]:
                 x_other = partial_charges(x_other, batch, total_charges)
+            if cfg.get("use_stereochemistry"):
+                e0 = torch.empty(0, 2, dtype=torch.long)
+                x_other = stereo(p, x_other, tet if tet is not None else torch.empty(0, 4, dtype=torch.long),
+                                 cis if cis is not None else e0, trans if trans is not None else e0)
             if capture is not None and l == 0:
                 capture["chunks0"] = message_passing(x_other, edges[:, 0], edges[:, 1], cfg["num_shells"])
             x_other = shell_layer(p, f"message_passing_layers.{l}.", x_other, edges[:, 0], edges[:, 1],
@@ -221,6 +272,9 @@ def param_shapes(cfg, feature_sizes=None):
         for i in range(cfg["attention_num_heads"]):
             s += [(f"pooling.attention_weights.{i}.weight", (1, hd)), (f"pooling.attention_weights.{i}.bias", (1,))]
     s += [("concat_self_other.weight", (hd, hd)), ("concat_self_other.bias", (hd,))]
+    if cfg.get("use_stereochemistry"):  # gnn.py:192-195
+        s += [("stereochemical_embedding.weight", (hd, 3 * hd)), ("stereochemical_embedding.bias", (hd,)),
+              ("stereochemical_embedding_2.weight", (d, 3 * d)), ("stereochemical_embedding_2.bias", (d,))]
     s += [("post_pooling_projection.weight", (fh, hd)), ("post_pooling_projection.bias", (fh,))]
     for i in range(cfg["ffn_num_layers"]):
         for nm in ("linear1", "linear2"):
@@ -247,7 +301,7 @@ def seeded_params(cfg, seed, dtype=torch.float32):
     import numpy as np
 
     top = ("embedding_projection.", "concat_self_other.", "post_pooling_projection.", "skip_transform.",
-           "output_layer.", "long_range_projection.", "pooling.attention_weights.")
+           "output_layer.", "long_range_projection.", "pooling.attention_weights.", "stereochemical_embedding")
     out = {}
     for name, shape in param_shapes(cfg):
         rng = np.random.default_rng([seed, zlib.crc32(name.encode())])

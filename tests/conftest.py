@@ -73,3 +73,28 @@ def parity_failures(ours, ref32, ref64, atol_rel=1e-5, factor=3.0):
         if not err <= tol:
             bad.append((k, err, tol))
     return bad
+
+
+SKETCH_K = 32
+
+
+def sketch(key, g):
+    """g @ P, P a seeded Gaussian [cols, 32] keyed by the tensor name — the same summary
+    tests/golden/make_golden.py stores (as 'sketch.<key>') for gradients too large to commit."""
+    import zlib
+    rng = np.random.default_rng([77, zlib.crc32(key.encode())])
+    P = rng.standard_normal((np.asarray(g).shape[1], SKETCH_K))
+    return np.asarray(g, np.float64) @ P
+
+
+def add_sketches(res, z):
+    """For every 'sketch.<key>' in fixture z, add res['sketch.<key>'] = sketch(key, res[key])."""
+    for k in z.files:
+        if k.startswith("sketch.") and k[len("sketch."):] in res:
+            res[k] = sketch(k[len("sketch."):], res[k[len("sketch."):]])
+    return res
+
+
+def fixture_refs(z):
+    """The reference fp32 tensors a model-case fixture stores (outputs, gradients, sketches)."""
+    return {k: z[k] for k in z.files if k in ("out", "attn", "q") or k.startswith("grad.") or k.startswith("sketch.")}

@@ -17,6 +17,7 @@ featuriser over the reference's sample split) and synthetic 40-atom molecules (a
 Weights: oracle.model.seeded_params(cfg, seed) loaded into the reference with load_state_dict.
 
 Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.npz)
+        python tests/golden/make_golden.py init_weights stereo large   (only those groups)
 """
 import ast
 import os
@@ -32,14 +33,19 @@ import torch  # noqa: E402
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference/src"
-sys.path.insert(0, os.path.join(HERE, "_shim"))
-sys.path.insert(0, REF)
-sys.path.insert(0, os.path.join(ROOT, "aimnet-x2d_amd"))
+# the reference's `models` / `utils` packages must win over the same-named packages of the build
+# (aimnet-x2d_amd/models, .../utils), so the build's directory goes LAST on the path
 sys.path.insert(0, ROOT)
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(HERE, "_shim"))
+sys.path.append(os.path.join(ROOT, "aimnet-x2d_amd"))
 
 from models.gnn import GNN  # noqa: E402  (reference)
 from models.layers import ShellConvolutionLayer  # noqa: E402  (reference)
 from models.pooling import MultiHeadAttentionPoolingLayer  # noqa: E402  (reference)
+
+assert os.path.realpath(sys.modules[GNN.__module__].__file__).startswith(os.path.realpath(REF)), \
+    "fixtures must come from the reference's GNN, not the build's"
 
 from oracle.model import default_config, seeded_params  # noqa: E402
 from aimx.synth import QM9Asset, adjacency, synth_molecules  # noqa: E402
@@ -87,7 +93,37 @@ def ref_hops(n, bonds, hops):
     return BFS["compute_multi_hop_edges_bfs_numba"](al, hops)
 
 
-def ref_batch(mols, hops, targets=None, charges=None):
+def synth_stereo(n, bonds):
+    """Stereo annotations of one molecule in the featuriser's per-molecule format
+    (features.py:213-283): chiral tensors = the 4 neighbours of every 4-connected atom (sorted),
+    cis/trans pairs = the 4 directed substituent pairs of every bond between two 3-connected atoms
+    (higher / lower neighbour index standing in for the CIP ranks; the bond parity alternates
+    between the 'trans' and 'cis' branches). RDKit is absent, so the annotations are synthetic;
+    the collate and the model that consume them are the reference's own."""
+    nbr = [[] for _ in range(n)]
+    for a, b in np.asarray(bonds).reshape(-1, 2).tolist():
+        nbr[a].append(b)
+        nbr[b].append(a)
+    chiral = [np.array(sorted(v), np.int64) for v in nbr if len(v) == 4]
+    cis, trans = [], []
+    for k, (s_, e_) in enumerate(np.asarray(bonds).reshape(-1, 2).tolist()):
+        if len(nbr[s_]) != 3 or len(nbr[e_]) != 3:
+            continue
+        so = sorted(x for x in nbr[s_] if x != e_)
+        eo = sorted(x for x in nbr[e_] if x != s_)
+        s_lo, s_hi, e_lo, e_hi = so[0], so[-1], eo[0], eo[-1]
+        same = [[s_hi, e_hi], [s_lo, e_lo], [e_hi, s_hi], [e_lo, s_lo]]
+        cross = [[s_hi, e_lo], [s_lo, e_hi], [e_lo, s_hi], [e_hi, s_lo]]
+        if k % 2 == 0:  # "E": same-rank pairs trans, cross pairs cis (features.py:261-271)
+            trans += same
+            cis += cross
+        else:           # "Z": same-rank pairs cis, cross pairs trans (features.py:273-283)
+            cis += same
+            trans += cross
+    return chiral, [np.array(c, np.int64) for c in cis], [np.array(t, np.int64) for t in trans]
+
+
+def ref_batch(mols, hops, targets=None, charges=None, stereo=False):
     """Run the reference collate on per-molecule data objects."""
     data = []
     for k, (n, bonds, feats) in enumerate(mols):
@@ -102,6 +138,11 @@ def ref_batch(mols, hops, targets=None, charges=None):
             "hybridization": torch.from_numpy(feats[:, 3]).long(),
         }
         d.chiral_tensors, d.cis_bonds_tensors, d.trans_bonds_tensors = [], [], []
+        if stereo:
+            ch, ci, tr = synth_stereo(n, bonds)
+            d.chiral_tensors = [torch.from_numpy(c) for c in ch]
+            d.cis_bonds_tensors = [torch.from_numpy(c) for c in ci]
+            d.trans_bonds_tensors = [torch.from_numpy(c) for c in tr]
         d.target = torch.tensor(targets[k] if targets is not None else [0.0], dtype=torch.float)
         d.total_charge = torch.tensor([charges[k] if charges is not None else 0.0], dtype=torch.float)
         d.smiles = ""
@@ -118,13 +159,29 @@ def build_ref_model(cfg):
             pooling_type=cfg["pooling_type"], embedding_dim=cfg["embedding_dim"],
             use_partial_charges=cfg["use_partial_charges"], activation_type=cfg["activation"],
             shell_conv_num_mlp_layers=cfg["shell_conv_num_mlp_layers"], attention_num_heads=cfg["attention_num_heads"],
-            loss_function=cfg["loss_function"])
+            loss_function=cfg["loss_function"], use_stereochemistry=cfg.get("use_stereochemistry", False))
     return m
 
 
-def run_case(name, cfg, mols, seed, grads="all", targets=None, charges=None, extra=None, intermediates=False):
+SKETCH_K = 32
+
+
+def sketch(name, g):
+    """Size-independent summary of a large gradient: g @ P with P a seeded Gaussian [cols, SKETCH_K]
+    (P regenerated by the tests from the key); the tests compare the same sketch of their own
+    gradient, so no 1.3 M-float tensor has to be committed."""
+    import zlib
+    rng = np.random.default_rng([77, zlib.crc32(name.encode())])
+    P = rng.standard_normal((g.shape[1], SKETCH_K))
+    return (g.astype(np.float64) @ P).astype(np.float64)
+
+
+def run_case(name, cfg, mols, seed, grads="all", targets=None, charges=None, extra=None, intermediates=False,
+             sketch_over=None):
+    """sketch_over: gradients with more elements than this are stored as sketch(key, grad)."""
     torch.manual_seed(0)
-    b, per_mol = ref_batch(mols, cfg["num_shells"], targets, charges)
+    stereo = bool(cfg.get("use_stereochemistry"))
+    b, per_mol = ref_batch(mols, cfg["num_shells"], targets, charges, stereo=stereo)
     model = build_ref_model(cfg)
     params = seeded_params(cfg, seed)
     sd = model.state_dict()
@@ -173,8 +230,16 @@ def run_case(name, cfg, mols, seed, grads="all", targets=None, charges=None, ext
         if p.grad is None:
             continue
         if grads == "all" or any(k.startswith(s) for s in grads):
-            rec["grad." + k] = p.grad.numpy()
+            g = p.grad.numpy()
+            if sketch_over is not None and g.ndim == 2 and g.size > sketch_over:
+                rec["sketch.grad." + k] = sketch("grad." + k, g)
+            else:
+                rec["grad." + k] = g
     rec["n_mol_atoms"] = np.array([m[0] for m in mols], np.int32)
+    if stereo:
+        rec["tet"] = b.final_tetrahedral_chiral_tensor.numpy().astype(np.int32)
+        rec["cis"] = b.final_cis_tensor.numpy().astype(np.int32)
+        rec["trans"] = b.final_trans_tensor.numpy().astype(np.int32)
     if extra:
         rec.update(extra)
     path = os.path.join(HERE, f"{name}.npz")
@@ -262,8 +327,49 @@ def case_attn_pool():
     print("attn_pool:", os.path.getsize(path))
 
 
+def case_init_weights():
+    """GNN.__init__ + init_weights (gnn.py:50-149, 660-703) under torch.manual_seed: the state_dict
+    a seeded construction produces (the builder must consume the RNG in the same order)."""
+    rec = {}
+    for tag, kw in (("a", dict(hidden_dim=64)),
+                    ("b", dict(hidden_dim=40, num_shells=4, use_partial_charges=True, use_stereochemistry=True,
+                               pooling_type="mean", ffn_num_layers=2, output_dim=3))):
+        cfg = default_config(**kw)
+        torch.manual_seed(1234)
+        m = build_ref_model(cfg)
+        rec[f"{tag}.cfg_json"] = np.array(repr(sorted(cfg.items())))
+        for k, v in m.state_dict().items():
+            rec[f"{tag}.{k}"] = v.numpy()
+    path = os.path.join(HERE, "init_weights.npz")
+    np.savez_compressed(path, **rec)
+    print("init_weights:", os.path.getsize(path))
+
+
+def case_stereo():
+    asset = QM9Asset()
+    cfg = default_config(hidden_dim=128, num_shells=3, use_stereochemistry=True)
+    run_case("stereo", cfg, asset.molecules(range(96, 128)), seed=12)
+    cfg = default_config(hidden_dim=128, num_shells=3, use_stereochemistry=True, use_partial_charges=True)
+    run_case("stereo_pc", cfg, asset.molecules(range(128, 144)), seed=13, charges=asset.total_charge[128:144],
+             grads=("message_passing_layers.", "stereochemical_embedding_2.", "embedding_projection."))
+
+
+def case_large():
+    c4 = default_config(hidden_dim=512, num_shells=3)
+    run_case("c4s", c4, synth_molecules(64, seed=4), seed=4,
+             grads=("message_passing_layers.", "pooling.", "concat_self_other."))
+    c5 = default_config(hidden_dim=1024, num_shells=6)
+    run_case("c5s", c5, synth_molecules(32, seed=5), seed=5,
+             grads=("message_passing_layers.", "pooling."), sketch_over=100_000)
+
+
 def main():
     torch.set_num_threads(8)
+    only = sys.argv[1:]
+    if only:
+        for nm in only:
+            {"init_weights": case_init_weights, "stereo": case_stereo, "large": case_large}[nm]()
+        return
     asset = QM9Asset()
     case_edges()
     case_mp_general()
@@ -276,11 +382,9 @@ def main():
     idx = np.arange(512, 1024)
     run_case("c3", c3, asset.molecules(idx), seed=3, targets=asset.targets[idx],
              charges=asset.total_charge[idx])
-    c4 = default_config(hidden_dim=512, num_shells=3)
-    run_case("c4s", c4, synth_molecules(16, seed=4), seed=4,
-             grads=("message_passing_layers.0.", "pooling.", "concat_self_other."))
-    c5 = default_config(hidden_dim=1024, num_shells=6)
-    run_case("c5s", c5, synth_molecules(4, seed=5), seed=5, grads=("pooling.",))
+    case_large()
+    case_init_weights()
+    case_stereo()
     for kind in ("mean", "max", "sum"):
         cfg = default_config(hidden_dim=128, num_shells=3, pooling_type=kind)
         run_case(f"pool_{kind}", cfg, asset.molecules(range(32, 64)), seed=6,

@@ -7,7 +7,7 @@ import torch
 from conftest import load_golden
 
 CASES = ["c1", "c2", "c3", "c4s", "c5s", "pool_mean", "pool_max", "pool_sum",
-         "act_relu", "act_leakyrelu", "act_elu", "act_gelu", "evidential", "noedges"]
+         "act_relu", "act_leakyrelu", "act_elu", "act_gelu", "evidential", "noedges", "stereo", "stereo_pc"]
 FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
 
 
@@ -23,6 +23,15 @@ def case_inputs(z, device="cpu"):
     batch = torch.from_numpy(z["batch"].astype(np.int64)).to(device)
     tc = torch.from_numpy(z["total_charges"]).to(device)
     return af, edges, batch, tc
+
+
+def case_stereo(z, device="cpu"):
+    """The collated (tetrahedral [M,4], cis [C,2], trans [T,2]) tensors of a case (empty if none)."""
+    def get(k, w):
+        if k in z.files:
+            return torch.from_numpy(z[k].astype(np.int64)).reshape(-1, w).to(device)
+        return torch.empty(0, w, dtype=torch.long, device=device)
+    return get("tet", 4), get("cis", 2), get("trans", 2)
 
 
 def load_case(name, device="cpu"):

@@ -8,8 +8,8 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden, norm_rel, parity_failures
-from golden_cases import CASES, load_case
+from conftest import add_sketches, fixture_refs, load_golden, norm_rel, parity_failures
+from golden_cases import CASES, case_stereo, load_case
 
 pytestmark = pytest.mark.gpu
 
@@ -404,7 +404,7 @@ def _build_model(cfg, seed):
             pooling_type=cfg["pooling_type"], embedding_dim=cfg["embedding_dim"],
             use_partial_charges=cfg["use_partial_charges"], activation_type=cfg["activation"],
             shell_conv_num_mlp_layers=cfg["shell_conv_num_mlp_layers"], attention_num_heads=cfg["attention_num_heads"],
-            loss_function=cfg["loss_function"])
+            loss_function=cfg["loss_function"], use_stereochemistry=cfg.get("use_stereochemistry", False))
     m.load_state_dict(om.seeded_params(cfg, seed))
     return m.to(DEV).eval()
 
@@ -413,7 +413,8 @@ def _oracle_run(z, cfg, inputs, dtype):
     _, om = _oracle()
     af, edges, batch, tc = inputs
     p = {k: v.to(dtype).requires_grad_() for k, v in om.seeded_params(cfg, int(z["seed"])).items()}
-    out, attn, q = om.gnn_forward(p, cfg, af, edges, batch, tc.to(dtype))
+    tet, cis, trans = case_stereo(z)
+    out, attn, q = om.gnn_forward(p, cfg, af, edges, batch, tc.to(dtype), tet=tet, cis=cis, trans=trans)
     (out * torch.from_numpy(z["loss_w"]).to(dtype)).sum().backward()
     res = {"out": out.detach().numpy()}
     if attn is not None:
@@ -423,7 +424,7 @@ def _oracle_run(z, cfg, inputs, dtype):
     for k, v in p.items():
         if v.grad is not None:
             res["grad." + k] = v.grad.numpy()
-    return res
+    return add_sketches(res, z)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -431,7 +432,7 @@ def test_model_case(name):
     z, cfg, inputs = load_case(name)
     torch.set_num_threads(8)
     ref64 = _oracle_run(z, cfg, inputs, torch.float64)
-    ref32 = {k: z[k] for k in z.files if k in ("out", "attn", "q") or k.startswith("grad.")}
+    ref32 = fixture_refs(z)
     must = set(ref32)
     # tensors the fixture did not store: the oracle's fp32 CPU run (the reference's own ATen ops,
     # pinned by tests/test_oracle_golden.py) stands in for the reference's fp32 error floor
@@ -439,8 +440,7 @@ def test_model_case(name):
         ref32.setdefault(k, v)
     model = _build_model(cfg, int(z["seed"]))
     af, edges, batch, tc = load_case(name, DEV)[2]
-    e_empty = torch.empty(0, 2, dtype=torch.long, device=DEV)
-    out, attn, q = model(af, edges, batch, tc, torch.empty(0, 4, dtype=torch.long, device=DEV), e_empty, e_empty)
+    out, attn, q = model(af, edges, batch, tc, *case_stereo(z, DEV))
     (out * torch.from_numpy(z["loss_w"]).to(DEV)).sum().backward()
     ours = {"out": out.detach().cpu().numpy()}
     if attn is not None:
@@ -450,6 +450,7 @@ def test_model_case(name):
     for k, p in model.named_parameters():
         if p.grad is not None:
             ours["grad." + k] = p.grad.cpu().numpy()
+    add_sketches(ours, z)
     # every gradient the reference produced must be produced here too
     for k in must:
         assert k in ours, k

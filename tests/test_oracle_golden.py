@@ -6,8 +6,8 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden, norm_rel, parity_failures
-from golden_cases import CASES, load_case
+from conftest import add_sketches, fixture_refs, load_golden, norm_rel, parity_failures
+from golden_cases import CASES, case_stereo, load_case
 from oracle import graph as og
 from oracle import model as om
 from aimx.synth import QM9Asset
@@ -105,7 +105,8 @@ def oracle_run(name, dtype):
     z, cfg, (af, edges, batch, tc) = load_case(name)
     p = {k: v.to(dtype).requires_grad_() for k, v in om.seeded_params(cfg, int(z["seed"])).items()}
     cap = {}
-    out, attn, q = om.gnn_forward(p, cfg, af, edges, batch, tc.to(dtype), capture=cap)
+    tet, cis, trans = case_stereo(z)
+    out, attn, q = om.gnn_forward(p, cfg, af, edges, batch, tc.to(dtype), capture=cap, tet=tet, cis=cis, trans=trans)
     (out * torch.from_numpy(z["loss_w"]).to(dtype)).sum().backward()
     res = {"out": out.detach().numpy()}
     if attn is not None:
@@ -115,7 +116,7 @@ def oracle_run(name, dtype):
     for k, v in p.items():
         if v.grad is not None:
             res["grad." + k] = v.grad.numpy()
-    return z, res, cap
+    return z, add_sketches(res, z), cap
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -124,7 +125,7 @@ def test_model_case(name):
     torch.set_num_threads(4)
     z, r32, cap = oracle_run(name, torch.float32)
     _, r64, _ = oracle_run(name, torch.float64)
-    ref = {k: z[k] for k in z.files if k in ("out", "attn", "q") or k.startswith("grad.")}
+    ref = fixture_refs(z)
     assert len([k for k in ref if k.startswith("grad.")]) > 0
     for k in ref:
         assert k in r32, k
@@ -134,3 +135,24 @@ def test_model_case(name):
     assert not parity_failures(r32, ref, r64), parity_failures(r32, ref, r64)
     if "chunks0" in z.files:
         assert np.array_equal(torch.cat(cap["chunks0"], 0).detach().numpy(), z["chunks0"])
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_init_weights_matches_reference(tag):
+    """GNN(...) under torch.manual_seed gives the reference's state_dict bit for bit: same
+    submodule construction order (default nn.Linear / nn.Embedding init) and the same
+    GNN.init_weights (gnn.py:660-703) xavier / zero calls in the same order."""
+    import ast
+    from models import GNN
+    z = load_golden("init_weights")
+    cfg = dict(ast.literal_eval(str(z[f"{tag}.cfg_json"])))
+    torch.manual_seed(1234)
+    m = GNN({"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}, cfg["hidden_dim"],
+            cfg["output_dim"], num_shells=cfg["num_shells"], pooling_type=cfg["pooling_type"],
+            ffn_num_layers=cfg["ffn_num_layers"], use_partial_charges=cfg["use_partial_charges"],
+            use_stereochemistry=cfg["use_stereochemistry"])
+    sd = m.state_dict()
+    keys = [k[len(tag) + 1:] for k in z.files if k.startswith(tag + ".") and k != f"{tag}.cfg_json"]
+    assert list(sd.keys()) == keys
+    for k in keys:
+        assert np.array_equal(sd[k].numpy(), z[f"{tag}.{k}"]), k
