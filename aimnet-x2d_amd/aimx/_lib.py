@@ -115,6 +115,10 @@ class EmbeddingTables(ctypes.Structure):
     ]
 
 
+class CopyItem(ctypes.Structure):
+    _fields_ = [("src", c_ptr), ("dst", c_ptr), ("n", c_i64)]
+
+
 class CsrSpec(ctypes.Structure):
     _fields_ = [("key", c_ptr), ("key_stride", c_i64), ("key_mod", c_i64), ("val", c_ptr), ("val_stride", c_i64),
                 ("val_mod", c_i64), ("n_items", c_i64), ("n_rows", c_i64), ("rowptr", c_ptr), ("col", c_ptr)]
@@ -181,6 +185,12 @@ _SIGS = {
     "aimx_wgrad_grouped_workspace_bytes": (c_size, [ctypes.POINTER(WgradProblem), c_i32]),
     "aimx_wgrad_grouped": (c_i32, [ctypes.POINTER(WgradProblem), c_i32, c_ptr, c_size, c_ptr, c_i64, c_ptr]),
     "aimx_fused_adam_workspace_bytes": (c_size, [ctypes.POINTER(AdamTensor), c_i32]),
+    "aimx_multi_copy": (c_i32, [ctypes.POINTER(CopyItem), c_i32, c_ptr]),
+    "aimx_comm_load": (c_i32, [ctypes.c_char_p]),
+    "aimx_comm_unique_id": (c_i32, [c_ptr, c_size]),
+    "aimx_comm_init": (c_i32, [ctypes.POINTER(c_ptr), c_ptr, c_size, c_i32, c_i32]),
+    "aimx_comm_allreduce": (c_i32, [c_ptr, c_ptr, c_i64, c_i32, c_ptr]),
+    "aimx_comm_destroy": (c_i32, [c_ptr]),
     "aimx_fused_adam": (c_i32, [ctypes.POINTER(AdamTensor), c_i32, ctypes.POINTER(AdamHyper), c_ptr, c_ptr, c_ptr,
                                 c_ptr, c_size, c_ptr]),
 }
@@ -325,3 +335,67 @@ def ptr(t):
 def ptr_array(tensors):
     arr = (c_ptr * max(1, len(tensors)))(*[ptr(t) for t in tensors])
     return arr
+
+
+COMM_ID_BYTES = 128
+
+
+def rccl_path():
+    """The RCCL this process uses: PyTorch's bundled librccl.so (what torch.distributed's "nccl"
+    backend runs on), else the system one."""
+    cand = [os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"), "/opt/rocm/lib/librccl.so.1",
+            "/opt/rocm/lib/librccl.so"]
+    for c in cand:
+        if os.path.exists(c):
+            return c
+    raise AimxError("aimx: no librccl found")
+
+
+class Comm:
+    """An RCCL communicator of our own (include/aimx.h aimx_comm_*), built over an initialised
+    torch.distributed group: rank 0's ncclUniqueId is broadcast through that group. Its all-reduce
+    is enqueued on any stream the caller picks and captures into HIP graphs as a plain node."""
+
+    def __init__(self, group=None, device=None):
+        import torch.distributed as dist
+        lib = load()
+        check(lib.aimx_comm_load(rccl_path().encode()), "comm_load")
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        uid = (ctypes.c_uint8 * COMM_ID_BYTES)()
+        if self.rank == 0:
+            check(lib.aimx_comm_unique_id(uid, COMM_ID_BYTES), "comm_unique_id")
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8,
+                         device=dev if dist.get_backend(group) == "nccl" else "cpu")
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = (ctypes.c_uint8 * COMM_ID_BYTES)(*t.cpu().tolist())
+        h = c_ptr()
+        with torch.cuda.device(dev):
+            check(lib.aimx_comm_init(ctypes.byref(h), uid, COMM_ID_BYTES, self.world, self.rank), "comm_init")
+        self.handle = h
+
+    def all_reduce(self, buf, average=True, stream=None):
+        """In-place fp32 all-reduce of `buf` on `stream` (default: the current stream)."""
+        if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
+            raise AimxError("aimx.Comm.all_reduce: contiguous fp32 device tensor")
+        s = (stream or torch.cuda.current_stream(buf.device)).cuda_stream
+        check(load().aimx_comm_allreduce(self.handle, buf.data_ptr(), buf.numel(), 1 if average else 0, s),
+              "comm_allreduce")
+
+    def close(self):
+        if self.handle:
+            load().aimx_comm_destroy(self.handle)
+            self.handle = None
+
+
+def multi_copy(pairs, device):
+    """pairs: [(src tensor or None, dst tensor)] of fp32 contiguous tensors: dst <- src (None: 0),
+    one launch (aimx_multi_copy) on the current stream."""
+    if not pairs:
+        return
+    arr = (CopyItem * len(pairs))()
+    for i, (src, dst) in enumerate(pairs):
+        arr[i].src = None if src is None else src.data_ptr()
+        arr[i].dst = dst.data_ptr()
+        arr[i].n = dst.numel()
+    check(load().aimx_multi_copy(arr, len(pairs), stream_ptr(device)), "multi_copy")

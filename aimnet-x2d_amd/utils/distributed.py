@@ -136,12 +136,19 @@ class GradientSync:
     leaves them; without this their bucket could only start at finish(). Every rank must pass the
     same set.
 
-    Graph capture: with overlap, each bucket's pack + RCCL all-reduce is issued from the
-    post-accumulate-grad hook of its last gradient; inside torch.cuda.graph capture those calls
-    are recorded as graph nodes on RCCL's stream, forked from and joined back (finish()) to the
-    capturing stream, so a replay runs them concurrently with the rest of the backward
-    (aimx.train.GraphedTrainStep "capture" mode). `always=True` runs the bucket path even at world
-    size 1 (tests of that mechanism on a one-GPU box).
+    Transport: over the "nccl" backend (RCCL) the buckets go through an RCCL communicator of the
+    library's own (aimx._lib.Comm, include/aimx.h aimx_comm_*): one ncclAllReduce(ncclAvg) per
+    bucket — the average in the collective's own kernel — on a side stream forked from the
+    backward's stream by an event and joined back in finish(). torch.distributed's own
+    ProcessGroupNCCL is not used for them because its watchdog thread queries every collective's
+    event, and events recorded during graph capture may not be queried (the process aborts).
+    Over gloo (CPU rehearsal) the buckets use dist.all_reduce.
+
+    Graph capture: with overlap, each bucket's pack + all-reduce is issued from the
+    post-accumulate-grad hook of its last gradient; inside torch.cuda.graph capture they become
+    graph nodes on the side stream, so a replay runs them concurrently with the rest of the
+    backward (aimx.train.GraphedTrainStep "capture" mode). `always=True` runs the bucket path
+    even at world size 1 (tests of that mechanism on a one-GPU box).
     """
 
     def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True,
@@ -170,6 +177,24 @@ class GradientSync:
         self._pending = [0] * len(self.buckets)
         self._handles = [None] * len(self.buckets)
         self._hooks = []
+        import os
+        # Side stream (overlap with the backward) only for large gradient sets: measured on one
+        # MI355X with a world-size-1 RCCL group (profiles/r02_ddp_ab.txt), the forked graph costs
+        # ~20 us per c2 step (3.3 MB of gradients: an 8-GPU all-reduce of them is only tens of us)
+        # and nothing at c5 (63 MB, where an 8-GPU all-reduce takes ~0.3 ms and overlap pays).
+        # AIMX_DDP_SIDE=1 / 0 forces it on / off.
+        total = sum(p.numel() for p in self.params) * 4
+        env = os.environ.get("AIMX_DDP_SIDE")
+        self.side_stream = (env == "1") if env is not None else total >= 16 * 2 ** 20
+        self.comm = None
+        self._stream = None
+        self._events = []
+        if self.active and self.backend == "nccl" and self.params and self.params[0].is_cuda:
+            from aimx import _lib
+            dev = self.params[0].device
+            self.comm = _lib.Comm(process_group, dev)
+            self._stream = torch.cuda.Stream(device=dev)
+            self._events = [(torch.cuda.Event(), torch.cuda.Event()) for _ in self.buckets]
         if self.overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -181,8 +206,9 @@ class GradientSync:
 
     @property
     def capturable(self) -> bool:
-        """True when the collectives can be recorded into a HIP graph (RCCL; gloo runs on the host)."""
-        return self.overlap and self.backend == "nccl"
+        """True when the collectives can be recorded into a HIP graph (our RCCL communicator;
+        gloo runs on the host)."""
+        return self.overlap and self.comm is not None
 
     def _reset(self):
         self._pending = [len(b) for b in self.buckets]
@@ -196,9 +222,32 @@ class GradientSync:
         if flat is None or flat.device != bucket[0].device:
             flat = torch.empty(sum(p.numel() for p in bucket), dtype=bucket[0].dtype, device=bucket[0].device)
             self._flat[i] = flat
-        grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket]
-        torch.cat(grads, out=flat)
-        self._handles[i] = dist.all_reduce(flat, group=self.group, async_op=True)
+        if self.comm is not None:
+            # pack every gradient (zeros for a missing one) into the flat buffer: one launch
+            from aimx import _lib
+            pairs, off = [], 0
+            for p in bucket:
+                n = p.numel()
+                g = p.grad
+                pairs.append((g if g is not None and g.is_contiguous() else
+                              (g.contiguous() if g is not None else None), flat[off:off + n]))
+                off += n
+            _lib.multi_copy(pairs, flat.device)
+        else:
+            grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket]
+            torch.cat(grads, out=flat)
+        if self.comm is not None:
+            ready, done = self._events[i]
+            cur = torch.cuda.current_stream(flat.device)
+            side = self._stream if self.side_stream else cur
+            if side is not cur:
+                ready.record(cur)
+                side.wait_event(ready)
+            self.comm.all_reduce(flat, average=True, stream=side)
+            done.record(side)
+            self._handles[i] = done
+        else:
+            self._handles[i] = dist.all_reduce(flat, group=self.group, async_op=True)
 
     def _on_grad(self, p):
         i = self._bucket_of[id(p)]
@@ -215,10 +264,13 @@ class GradientSync:
             if self._handles[i] is None:
                 self._launch(i)
         for i, bucket in enumerate(self.buckets):
-            self._handles[i].wait()
             flat = self._flat[i]
-            if self.world > 1:
-                flat.div_(self.world)
+            if self.comm is not None:  # averaged by the collective (ncclAvg); join its stream
+                torch.cuda.current_stream(flat.device).wait_event(self._handles[i])
+            else:
+                self._handles[i].wait()
+                if self.world > 1:
+                    flat.div_(self.world)
             dst, src, off = [], [], 0
             for p in bucket:
                 n = p.numel()
@@ -226,7 +278,10 @@ class GradientSync:
                     dst.append(p.grad)
                     src.append(flat[off:off + n].view_as(p))
                 off += n
-            if dst:
+            if dst and self.comm is not None and all(d.is_contiguous() for d in dst):
+                from aimx import _lib
+                _lib.multi_copy(list(zip(src, dst)), flat.device)  # one launch for the bucket
+            elif dst:
                 torch._foreach_copy_(dst, src)
         self._reset()
 
@@ -234,3 +289,6 @@ class GradientSync:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None

@@ -223,3 +223,25 @@ def test_rccl_allreduce_captured_in_step_graph():
     assert out["mode"] == "capture", out
     assert out["buckets"] > 2
     assert out["err"] <= 1e-5 * out["scale"], out
+
+
+def test_multi_copy_exact():
+    """aimx_multi_copy (the bucket pack / unpack of the gradient sync): exact copies, zero fill for
+    a missing source, aligned and unaligned views, several slices per item and > 64 items."""
+    from aimx import _lib
+    torch.manual_seed(0)
+    sizes = [1, 3, 77, 4096, 4097, 9000, 0, 513] * 10
+    flat = torch.full((sum(sizes) + 5,), 7.0, device="cuda")
+    srcs = [torch.randn(n, device="cuda") if i % 9 != 4 else None for i, n in enumerate(sizes)]
+    pairs, off = [], 1  # offset 1: unaligned destinations
+    for s, n in zip(srcs, sizes):
+        pairs.append((s, flat[off:off + n]))
+        off += n
+    _lib.multi_copy(pairs, flat.device)
+    back = [torch.empty(n, device="cuda") for n in sizes]
+    _lib.multi_copy([(d, b) for (_, d), b in zip(pairs, back)], flat.device)
+    torch.cuda.synchronize()
+    for s, (_, d), b in zip(srcs, pairs, back):
+        want = s if s is not None else torch.zeros_like(d)
+        assert torch.equal(d, want) and torch.equal(b, want)
+    assert flat[0].item() == 7.0 and flat[-4:].eq(7.0).all()
