@@ -132,7 +132,7 @@ class WgradProblem(ctypes.Structure):
 
 class AdamTensor(ctypes.Structure):
     _fields_ = [("param", c_ptr), ("grad", c_ptr), ("exp_avg", c_ptr), ("exp_avg_sq", c_ptr), ("numel", c_i64),
-                ("group", c_i32)]
+                ("group", c_i32), ("step_slot", c_i32)]
 
 
 class AdamHyper(ctypes.Structure):

@@ -49,7 +49,10 @@ class FusedAdam(torch.optim.Optimizer):
 
     def _device_state(self, dev):
         if self._step_t is None:
-            self._step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+            # one step counter per parameter (torch.optim.Adam's state['step']), advanced on the
+            # device only for parameters that have a gradient in that step
+            n = sum(len(g["params"]) for g in self.param_groups)
+            self._step_t = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
             self._norm = torch.zeros(1, dtype=torch.float32, device=dev)
             self._lr_t = torch.zeros(len(self.param_groups), dtype=torch.float32, device=dev)
         lrs = [float(g["lr"]) for g in self.param_groups]
@@ -77,8 +80,10 @@ class FusedAdam(torch.optim.Optimizer):
         hyper_g = self._shared_hyper()
         rows = []
         dev = None
+        slot = -1
         for gi, group in enumerate(self.param_groups):
             for p in group["params"]:
+                slot += 1
                 if p.grad is None:
                     continue
                 g = p.grad
@@ -91,17 +96,17 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 dev = p.device
-                rows.append((p, g, st["exp_avg"], st["exp_avg_sq"], gi))
+                rows.append((p, g, st["exp_avg"], st["exp_avg_sq"], gi, slot))
         if not rows:
             return loss
         self._device_state(dev)
-        for p, *_ in rows:
-            self.state[p]["step"] = self._step_t
+        for p, *_, k in rows:
+            self.state[p]["step"] = self._step_t[k]  # 0-dim view of this parameter's device counter
         arr = (AdamTensor * len(rows))()
-        for i, (p, g, m, v, gi) in enumerate(rows):
+        for i, (p, g, m, v, gi, k) in enumerate(rows):
             arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
             arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
-            arr[i].numel, arr[i].group = p.numel(), gi
+            arr[i].numel, arr[i].group, arr[i].step_slot = p.numel(), gi, k
         lib = _lib.load()
         wsb = lib.aimx_fused_adam_workspace_bytes(arr, len(rows))
         if self._ws is None or self._ws.numel() * 8 < wsb:

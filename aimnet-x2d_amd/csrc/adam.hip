@@ -6,7 +6,10 @@
 // these as ~2 elementwise launches per parameter tensor (plus foreach norm kernels): hundreds of
 // 3-5 us launches per step for this model. Here:
 //   1. k_adam_sumsq   : per-(tensor, slice) partial sums of g^2 (fp64)  -> workspace
-//   2. k_adam_scalars : one wave: total norm, clip coefficient, step += 1, bias corrections
+//   2. k_adam_scalars : one wave: total norm, clip coefficient
+// (each tensor's own step counter, torch.optim.Adam's per-parameter state['step'], is advanced by
+// the first workgroup of that tensor in launch 1 and read by launch 3 for its bias corrections:
+// a parameter without a gradient in a step keeps its count, as in torch)
 //   3. k_adam_update  : g *= coef (in place, as clip_grad_norm_ leaves it), [g += wd * p],
 //                       m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
 //                       p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
@@ -29,7 +32,7 @@ constexpr int64_t kSliceElems = 2048; // elements per workgroup slice (8 per thr
 struct AdamTable {
   int32_t n;
   int32_t blk0[kAdamChunk + 1];  // first workgroup of each tensor (relative to the chunk)
-  int32_t group[kAdamChunk];
+  int32_t gs[kAdamChunk];        // parameter group | step slot << 8
   int64_t numel[kAdamChunk];
   float* param[kAdamChunk];
   float* grad[kAdamChunk];
@@ -44,8 +47,10 @@ __device__ __forceinline__ int find_tensor(const AdamTable& t, int b) {
   return i;
 }
 
-__global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, double* __restrict__ partial) {
+__global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, double* __restrict__ partial,
+                                                             float* __restrict__ steps) {
   const int i = find_tensor(t, blockIdx.x);
+  if (blockIdx.x == t.blk0[i] && threadIdx.x == 0) steps[t.gs[i] >> 8] += 1.f;
   const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
   const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
   const float* __restrict__ g = t.grad[i];
@@ -67,11 +72,9 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, 
   }
 }
 
-// scal[0] = clip coefficient, scal[1] = 1 / bias_correction1, scal[2] = sqrt(bias_correction2),
-// scal[3] = total gradient norm (the value clip_grad_norm_ returns)
-__global__ void k_adam_scalars(const double* __restrict__ partial, int n_partial, float max_norm, float beta1,
-                               float beta2, float* __restrict__ step, float* __restrict__ scal,
-                               float* __restrict__ norm_out) {
+// scal[0] = clip coefficient, scal[3] = total gradient norm (the value clip_grad_norm_ returns)
+__global__ void k_adam_scalars(const double* __restrict__ partial, int n_partial, float max_norm,
+                               float* __restrict__ scal, float* __restrict__ norm_out) {
   double s = 0.0;
   for (int j = threadIdx.x; j < n_partial; j += 64) s += partial[j];
 #pragma unroll
@@ -80,26 +83,22 @@ __global__ void k_adam_scalars(const double* __restrict__ partial, int n_partial
     const float total = (float)sqrt(s);
     float coef = 1.f;
     if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
-    const float st = *step + 1.f;
-    *step = st;
-    const float bc1 = 1.f - powf(beta1, st);
-    const float bc2 = 1.f - powf(beta2, st);
     scal[0] = coef;
-    scal[1] = 1.f / bc1;
-    scal[2] = sqrtf(bc2);
     scal[3] = total;
     if (norm_out) *norm_out = total;
   }
 }
 
 __global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t, const float* __restrict__ scal,
-                                                              const float* __restrict__ lr, float omb1, float beta2,
-                                                              float omb2, float eps, float wd) {
+                                                              const float* __restrict__ steps,
+                                                              const float* __restrict__ lr, float beta1, float omb1,
+                                                              float beta2, float omb2, float eps, float wd) {
   const int i = find_tensor(t, blockIdx.x);
   const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
   const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
-  const float coef = scal[0], inv_bc1 = scal[1], bc2s = scal[2];
-  const float step_size = lr[t.group[i]] * inv_bc1;
+  const float st = steps[t.gs[i] >> 8];
+  const float coef = scal[0], inv_bc1 = 1.f / (1.f - powf(beta1, st)), bc2s = sqrtf(1.f - powf(beta2, st));
+  const float step_size = lr[t.gs[i] & 255] * inv_bc1;
   float* __restrict__ p = t.param[i];
   float* __restrict__ g = t.grad[i];
   float* __restrict__ m = t.m[i];
@@ -141,8 +140,11 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
   if (!workspace || workspace_bytes < aimx_fused_adam_workspace_bytes(tensors, n)) return AIMX_EARG;
   for (int32_t i = 0; i < n; ++i) {
     const AimxAdamTensor& x = tensors[i];
-    if (x.numel < 0 || (x.numel > 0 && (!x.param || !x.grad || !x.exp_avg || !x.exp_avg_sq)) || x.group < 0)
+    if (x.numel < 0 || (x.numel > 0 && (!x.param || !x.grad || !x.exp_avg || !x.exp_avg_sq)) || x.group < 0 ||
+        x.group > 255 || x.step_slot < 0 || x.step_slot >= (1 << 23))
       return AIMX_EARG;
+    for (int32_t k = 0; k < i; ++k)  // each counter advanced once per call
+      if (tensors[k].step_slot == x.step_slot) return AIMX_EARG;
   }
   double* partial = (double*)workspace;
   int64_t total_blocks = 0;
@@ -158,7 +160,7 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
       for (int32_t k = 0; k < t.n; ++k) {
         const AimxAdamTensor& x = tensors[c0 + k];
         t.blk0[k] = b;
-        t.group[k] = x.group;
+        t.gs[k] = x.group | (x.step_slot << 8);
         t.numel[k] = x.numel;
         t.param[k] = x.param;
         t.grad[k] = x.grad;
@@ -174,17 +176,18 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
     return AIMX_OK;
   };
   int rc = for_chunks([&](const AdamTable& t, int32_t nb, int64_t blk) -> int {
-    hipLaunchKernelGGL(k_adam_sumsq, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, partial + blk);
+    hipLaunchKernelGGL(k_adam_sumsq, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, partial + blk, step);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   });
   if (rc) return rc;
   hipLaunchKernelGGL(k_adam_scalars, dim3(1), dim3(64), 0, s, (const double*)partial, (int)total_blocks,
-                     h->max_grad_norm, h->beta1, h->beta2, step, scal, norm_out);
+                     h->max_grad_norm, scal, norm_out);
   AIMX_CHECK_LAUNCH();
   return for_chunks([&](const AdamTable& t, int32_t nb, int64_t) -> int {
-    hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal, lr,
-                       h->one_minus_beta1, h->beta2, h->one_minus_beta2, h->eps, h->weight_decay);
+    hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal,
+                       (const float*)step, lr, h->beta1, h->one_minus_beta1, h->beta2, h->one_minus_beta2, h->eps,
+                       h->weight_decay);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   });

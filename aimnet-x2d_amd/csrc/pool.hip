@@ -3,11 +3,20 @@
 // Reference: MultiHeadAttentionPoolingLayer.forward, src/models/pooling.py:122-172, and
 // Mean/Max/SumPoolingLayer, pooling.py:15-80 (torch_scatter scatter_softmax / scatter_sum /
 // scatter_mean / scatter_max). The reference materialises [H, N, hidden] (x expanded per head,
-// pooling.py:150-159); here x rows are read once for the H score dot-products (a wave per atom,
-// lanes over channels, butterfly reduction) and once more (L2-resident, same molecule) for the
-// head-weighted segment sum. Softmax statistics live in LDS. Molecules never span workgroups, so
-// there are no atomics; weight gradients are per-molecule partial slabs reduced in molecule order
-// by a second kernel (deterministic).
+// pooling.py:150-159). Here each x row is read from HBM once per direction:
+//
+// * Row-resident path (every molecule up to 4·R atoms with C <= 1024, C % 4 == 0): a workgroup
+//   of S·4 waves owns one molecule. Wave (s, p) holds channel slice s (256 channels, one float4 per
+//   lane) of the molecule's atoms p, p+4, p+8, ... in registers, loaded in one burst. Score dot
+//   products are reduced across lanes by a reduce-scatter butterfly (R·H values in ~R·H shuffles,
+//   not 6·R·H) and across slices in LDS; the softmax of head h is one wave (lanes over atoms); the
+//   pooled sum and, in the backward, dx and the weight-gradient partials are formed from the same
+//   registers, so the backward reads x once and writes dx once.
+// * General path (larger molecules, odd widths or alignment): per-molecule three-pass body that
+//   re-reads x rows (L2-resident), softmax statistics in LDS or, beyond kCap atoms, global scratch.
+//
+// Molecules never span workgroups, so there are no atomics; weight gradients are per-molecule
+// partial slabs reduced in molecule order by a second kernel (deterministic).
 #include <algorithm>
 
 #include "aimx_common.h"
@@ -15,12 +24,14 @@
 namespace aimx {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / kWave;
 constexpr int kMaxH = 8;
-constexpr int kCap = 1024;  // atoms per molecule kept in LDS (larger molecules use global scratch)
-constexpr int kCapB = 512;  // the same for the backward's fp64 scratch
+constexpr int kCap = 512;   // atoms per molecule kept in LDS on the general path (beyond: global scratch)
+constexpr int kCapB = 128;  // the same for the backward's two fp64 scratch arrays
+constexpr int kSegThreads = 256;
+constexpr int kGeneralSmem = 16 * 1024;
+static_assert(kMaxH * kCap * 4 <= kGeneralSmem && 2 * kMaxH * kCapB * 8 <= kGeneralSmem, "general-path scratch fits");
 
+template <int NW>
 __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -29,10 +40,11 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   __syncthreads();
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < kWaves; ++i) s += red[i];
+  for (int i = 0; i < NW; ++i) s += red[i];
   return s;
 }
 
+template <int NW>
 __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   v = wave_max(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -41,8 +53,64 @@ __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   __syncthreads();
   float s = red[0];
 #pragma unroll
-  for (int i = 1; i < kWaves; ++i) s = fmaxf(s, red[i]);
+  for (int i = 1; i < NW; ++i) s = fmaxf(s, red[i]);
   return s;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int NW>
+__device__ __forceinline__ double block_reduce_sum_d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += red[i];
+  return s;
+}
+
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
+constexpr int pow2ceil(int v) { return v <= 1 ? 1 : 2 * pow2ceil((v + 1) / 2); }
+
+// Sum NV per-lane values over the wave's 64 lanes. Each butterfly step sends half of the values a
+// lane still holds to its partner and keeps the other half, so the whole reduction costs
+// NV - 1 + log2(64 / NV) shuffles instead of 6·NV. On return each lane holds the wave total of
+// value index lane >> (6 - log2 NV) (lanes of one group of 64 / NV hold the same total).
+// (Template recursion keeps every step's trip count a constant, so v stays in registers.)
+template <int M, int O, typename T>
+struct RsStep {
+  static __device__ __forceinline__ void run(T* v, int lane) {
+    const bool up = (lane & O) != 0;
+#pragma unroll
+    for (int i = 0; i < M / 2; ++i) {
+      const T send = up ? v[i] : v[i + M / 2];
+      const T keep = up ? v[i + M / 2] : v[i];
+      v[i] = keep + __shfl_xor(send, O, 64);
+    }
+    RsStep<M / 2, O / 2, T>::run(v, lane);
+  }
+};
+template <int O, typename T>
+struct RsStep<1, O, T> {
+  static __device__ __forceinline__ void run(T*, int) {}
+};
+
+template <int NV, typename T>
+__device__ __forceinline__ T wave_reduce_scatter(T (&v)[NV]) {
+  static_assert(NV >= 1 && NV <= 64 && (NV & (NV - 1)) == 0, "NV: power of two <= 64");
+  const int lane = threadIdx.x & 63;
+  RsStep<NV, 32, T>::run(v, lane);
+  T r = v[0];
+#pragma unroll
+  for (int o = 32 >> ilog2(NV); o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+  return r;
 }
 
 // Per-(head, atom) scratch for one molecule: LDS image [H][kCap] when the molecule fits, else the
@@ -54,47 +122,33 @@ struct Slot {
   __device__ __forceinline__ T& at(int h, int j, int64_t i) const { return LDS ? p[h * CAP + j] : p[h * N + i]; }
 };
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-__device__ __forceinline__ double block_reduce_sum_d(double v, double* red) {
-  v = wave_sum_d(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  double s = 0.0;
-#pragma unroll
-  for (int i = 0; i < kWaves; ++i) s += red[i];
-  return s;
-}
-
-template <bool LDS>
+// ---------------------------------------------------------------------------------------------
+// General path (any molecule size, width or alignment)
+// ---------------------------------------------------------------------------------------------
+template <bool LDS, int NT>
 __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
                                               const float* __restrict__ W, const float* __restrict__ bias, float tau,
                                               int H, int32_t b, int n, const int32_t* __restrict__ gperm, int g,
                                               float* __restrict__ pooled, float* __restrict__ attn,
                                               float* __restrict__ scores, Slot<LDS> sa, float* red) {
+  constexpr int NW = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // 1) scores s[h,i] = (x_i . W_h + b_h) / tau  (a wave per atom, lanes over channels)
-  for (int j = w; j < n; j += kWaves) {
+  for (int j = w; j < n; j += NW) {
     const int64_t i = gperm[b + j];
-    float acc[kMaxH];
+    double acc[kMaxH];  // fp64 score sums: see attn_fwd_rows
 #pragma unroll
-    for (int h = 0; h < kMaxH; ++h) acc[h] = 0.f;
+    for (int h = 0; h < kMaxH; ++h) acc[h] = 0.0;
     for (int64_t c = lane; c < C; c += 64) {
-      const float xv = x[i * ldx + c];
+      const double xv = x[i * ldx + c];
 #pragma unroll
       for (int h = 0; h < kMaxH; ++h)
-        if (h < H) acc[h] += xv * W[h * C + c];
+        if (h < H) acc[h] += xv * (double)W[h * C + c];
     }
 #pragma unroll
     for (int h = 0; h < kMaxH; ++h) {
       if (h < H) {
-        const float s = (wave_sum(acc[h]) + bias[h]) / tau;
+        const float s = (float)((wave_sum_d(acc[h]) + (double)bias[h]) / (double)tau);
         if (lane == 0) {
           scores[h * N + i] = s;
           if (LDS) sa.at(h, j, i) = s;
@@ -107,13 +161,12 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
   // 2) per-head softmax over the molecule's atoms (torch_scatter.scatter_softmax)
   for (int h = 0; h < H; ++h) {
     float mx = -INFINITY;
-    for (int j = threadIdx.x; j < n; j += kThreads) mx = fmaxf(mx, LDS ? sa.at(h, j, 0) : scores[h * N + gperm[b + j]]);
-    mx = block_reduce_max(mx, red);
+    for (int j = threadIdx.x; j < n; j += NT) mx = fmaxf(mx, LDS ? sa.at(h, j, 0) : scores[h * N + gperm[b + j]]);
+    mx = block_reduce_max<NW>(mx, red);
     float sum = 0.f;
-    for (int j = threadIdx.x; j < n; j += kThreads)
-      sum += expf((LDS ? sa.at(h, j, 0) : scores[h * N + gperm[b + j]]) - mx);
-    sum = block_reduce_sum(sum, red);
-    for (int j = threadIdx.x; j < n; j += kThreads) {
+    for (int j = threadIdx.x; j < n; j += NT) sum += expf((LDS ? sa.at(h, j, 0) : scores[h * N + gperm[b + j]]) - mx);
+    sum = block_reduce_sum<NW>(sum, red);
+    for (int j = threadIdx.x; j < n; j += NT) {
       const int64_t i = gperm[b + j];
       const float a = expf((LDS ? sa.at(h, j, i) : scores[h * N + i]) - mx) / sum;
       attn[h * N + i] = a;
@@ -123,7 +176,7 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
   if (!LDS) __threadfence();
   __syncthreads();
   // 3) pooled[g,c] = (sum_h sum_i a[h,i] x[i,c]) / H  (pooling.py:150-161: per-head sums, head mean)
-  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
+  for (int64_t c = threadIdx.x; c < C; c += NT) {
     float acc[kMaxH];
 #pragma unroll
     for (int h = 0; h < kMaxH; ++h) acc[h] = 0.f;
@@ -142,156 +195,47 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
   }
 }
 
-// ---- Small-molecule fast path (every QM9 molecule): the molecule's x rows are staged in LDS once
-// with 16-B loads (one round trip), then scores, softmax and the pooled sum run from LDS with no
-// further global loads; the softmax of head h is one wave's job (lanes over atoms, no barriers).
-// Same arithmetic per value as the general body above, except the softmax max/sum reductions,
-// which run as one wave butterfly instead of a block reduction (fp32 reassociation only).
-constexpr int kFastAtoms = 64;             // atoms per molecule (one wave's lanes in the softmax)
-constexpr int kFastXBytes = 32 * 1024;     // LDS for the staged rows
-constexpr int kSmemBytes = kFastXBytes + 8 * 1024;
-static_assert(kMaxH * kCap * 4 <= kSmemBytes && kMaxH * kCapB * 8 <= kSmemBytes, "general-path scratch fits");
-
-__device__ __forceinline__ bool fast_ok(int n, int64_t C, int H) {
-  return n <= kFastAtoms && (int64_t)n * C * 4 <= kFastXBytes && H <= kMaxH && (C % 4) == 0;
-}
-
-// head weights [H][C] staged after the fast path's sa scratch (16-B aligned: W 16-B aligned too)
-__device__ __forceinline__ bool wlds_ok(int64_t C, int H) {
-  return (int64_t)H * C * 4 + kMaxH * kFastAtoms * 4 <= kSmemBytes - kFastXBytes && (C % 4) == 0;
-}
-
-// stage rows gperm[b .. b+n) of x into xs[n][C] (16-B loads; ldx % 4 == 0 checked by the host)
-__device__ __forceinline__ void stage_rows(const float* __restrict__ x, int64_t ldx, int64_t C, int32_t b, int n,
-                                           const int32_t* __restrict__ gperm, float* xs) {
-  const int c4 = (int)(C / 4);
-  const int tot = n * c4;
-  for (int q = threadIdx.x; q < tot; q += kThreads) {
-    const int j = q / c4, c = (q - j * c4) * 4;
-    const int64_t i = gperm[b + j];
-    *reinterpret_cast<float4*>(xs + j * C + c) = *reinterpret_cast<const float4*>(x + i * ldx + c);
-  }
-}
-
-__device__ __forceinline__ void attn_fwd_fast(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
-                                              const float* __restrict__ W, const float* __restrict__ bias, float tau,
-                                              int H, int32_t b, int n, const int32_t* __restrict__ gperm, int g,
-                                              float* __restrict__ pooled, float* __restrict__ attn,
-                                              float* __restrict__ scores, char* smem) {
-  float* xs = reinterpret_cast<float*>(smem);                      // [n][C]
-  float* sa = reinterpret_cast<float*>(smem + kFastXBytes);        // [kMaxH][kFastAtoms]
-  float* ws = sa + kMaxH * kFastAtoms;                             // [H][C] when it fits
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // the head weights are read once per atom by every wave: stage them beside the rows (one
-  // round trip for both) when they fit the scratch after sa, else read them from global memory
-  const bool wlds = wlds_ok(C, H) && ((uintptr_t)W & 15) == 0;
-  if (wlds)
-    for (int q = threadIdx.x; q < H * (int)C / 4; q += kThreads)
-      *reinterpret_cast<float4*>(ws + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
-  stage_rows(x, ldx, C, b, n, gperm, xs);
-  __syncthreads();
-  const float* Wr = wlds ? ws : W;
-  // 1) scores: a wave per atom, lanes over channels (same order as attn_fwd_body)
-  for (int j = w; j < n; j += kWaves) {
-    float acc[kMaxH];
-#pragma unroll
-    for (int h = 0; h < kMaxH; ++h) acc[h] = 0.f;
-    for (int64_t c = lane; c < C; c += 64) {
-      const float xv = xs[j * C + c];
-#pragma unroll
-      for (int h = 0; h < kMaxH; ++h)
-        if (h < H) acc[h] += xv * Wr[h * C + c];
-    }
-#pragma unroll
-    for (int h = 0; h < kMaxH; ++h) {
-      if (h < H) {
-        const float sc = (wave_sum(acc[h]) + bias[h]) / tau;
-        if (lane == 0) {
-          scores[h * N + gperm[b + j]] = sc;
-          sa[h * kFastAtoms + j] = sc;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // 2) softmax of head h by wave h % kWaves, lanes over atoms
-  for (int h = w; h < H; h += kWaves) {
-    const float v = lane < n ? sa[h * kFastAtoms + lane] : -INFINITY;
-    const float mx = wave_max(v);
-    const float ex = lane < n ? expf(v - mx) : 0.f;
-    const float sum = wave_sum(ex);
-    if (lane < n) {
-      const float a = expf(v - mx) / sum;
-      attn[h * N + gperm[b + lane]] = a;
-      sa[h * kFastAtoms + lane] = a;
-    }
-  }
-  __syncthreads();
-  // 3) pooled[g,c] = (sum_h sum_i a[h,i] x[i,c]) / H
-  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
-    float acc[kMaxH];
-#pragma unroll
-    for (int h = 0; h < kMaxH; ++h) acc[h] = 0.f;
-    for (int j = 0; j < n; ++j) {
-      const float xv = xs[j * C + c];
-#pragma unroll
-      for (int h = 0; h < kMaxH; ++h)
-        if (h < H) acc[h] += sa[h * kFastAtoms + j] * xv;
-    }
-    float sm = 0.f;
-#pragma unroll
-    for (int h = 0; h < kMaxH; ++h)
-      if (h < H) sm += acc[h];
-    pooled[(int64_t)g * C + c] = sm / (float)H;
-  }
-}
-
-__global__ __launch_bounds__(kThreads) void k_attn_fwd(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
-                                                        const float* __restrict__ W, const float* __restrict__ bias,
-                                                        const float* __restrict__ tau_p, int H,
-                                                        const int32_t* __restrict__ gptr,
-                                                        const int32_t* __restrict__ gperm, float* __restrict__ pooled,
-                                                        float* __restrict__ attn, float* __restrict__ scores) {
-  __shared__ __attribute__((aligned(16))) char smem[kSmemBytes];
-  __shared__ float red[kWaves];
-  float* sa = reinterpret_cast<float*>(smem);  // general path: [kMaxH][kCap] floats
-  const int g = blockIdx.x;
-  const int32_t b = gptr[g], e = gptr[g + 1];
-  const int n = e - b;
-  const float tau = *tau_p;
-  if (fast_ok(n, C, H) && (ldx % 4) == 0 && ((uintptr_t)x & 15) == 0)
-    attn_fwd_fast(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, smem);
-  else if (n <= kCap)
-    attn_fwd_body<true>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, Slot<true>{sa, N}, red);
-  else
-    attn_fwd_body<false>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, Slot<false>{attn, N},
-                         red);
-}
-
 // Backward. ds[h,i] = a (da - sum_j a da), da[h,i] = (x_i . dpooled[g]) / H + d_attn[h,i].
 // The softmax backward cancels (da - <a, da>) when a molecule's attention is peaked, so every
 // reduction here (dots, <a, da>, ds, the dW/db/dtau partial sums) is accumulated in fp64: the
 // kernel is memory/latency-bound and the fp64 VALU rate is not the limit.
-template <bool LDS>
+template <bool LDS, int NT>
 __device__ __forceinline__ void attn_bwd_body(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
                                               const float* __restrict__ W, float tau, int H, int32_t b, int n,
                                               const int32_t* __restrict__ gperm, int g,
                                               const float* __restrict__ attn, const float* __restrict__ scores,
                                               const float* __restrict__ dpool, const float* __restrict__ dattn,
                                               float* __restrict__ dx, int64_t lddx, float* __restrict__ dW_part,
-                                              float* __restrict__ db_part, float* __restrict__ dtau_part,
-                                              Slot<LDS, double, kCapB> sds, double* red) {
+                                              double* __restrict__ db_part, double* __restrict__ dtau_part,
+                                              Slot<LDS, double, kCapB> sds, Slot<LDS, double, kCapB> sxw,
+                                              double* red) {
+  constexpr int NW = NT / kWave;
   const double invH = 1.0 / (double)H;
   const double dtau_inv = 1.0 / (double)tau;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* q = dpool + (int64_t)g * C;
-  // 1) da[h,i]
-  for (int j = w; j < n; j += kWaves) {
+  // 1) da[h,i], and x_i . W_h in fp64 for the temperature gradient (see attn_bwd_rows)
+  for (int j = w; j < n; j += NW) {
     const int64_t i = gperm[b + j];
-    double acc = 0.0;
-    for (int64_t c = lane; c < C; c += 64) acc += (double)x[i * ldx + c] * (double)q[c];
+    double acc = 0.0, aw[kMaxH];
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h) aw[h] = 0.0;
+    for (int64_t c = lane; c < C; c += 64) {
+      const double xv = x[i * ldx + c];
+      acc += xv * (double)q[c];
+#pragma unroll
+      for (int h = 0; h < kMaxH; ++h)
+        if (h < H) aw[h] += xv * (double)W[h * C + c];
+    }
     const double d = wave_sum_d(acc) * invH;
     if (lane < H) sds.at(lane, j, i) = d + (dattn ? (double)dattn[lane * N + i] : 0.0);
+#pragma unroll
+    for (int h = 0; h < kMaxH; ++h) {
+      if (h < H) {
+        const double sw = wave_sum_d(aw[h]);
+        if (lane == 0) sxw.at(h, j, i) = sw;
+      }
+    }
   }
   if (!LDS) __threadfence();
   __syncthreads();
@@ -304,32 +248,32 @@ __device__ __forceinline__ void attn_bwd_body(const float* __restrict__ x, int64
     // share a large mean. (torch's autograd gets the same cancellation by routing the residue
     // through scatter_max's gradient.)
     double t = 0.0, asum = 0.0;
-    for (int j = threadIdx.x; j < n; j += kThreads) {
+    for (int j = threadIdx.x; j < n; j += NT) {
       const int64_t i = gperm[b + j];
       const double a = attn[h * N + i];
       t += a * sds.at(h, j, i);
       asum += a;
     }
-    t = block_reduce_sum_d(t, red);
-    asum = block_reduce_sum_d(asum, red);
+    t = block_reduce_sum_d<NW>(t, red);
+    asum = block_reduce_sum_d<NW>(asum, red);
     if (asum > 0.0) t /= asum;
     double dbs = 0.0;
-    for (int j = threadIdx.x; j < n; j += kThreads) {
+    for (int j = threadIdx.x; j < n; j += NT) {
       const int64_t i = gperm[b + j];
       const double ds = (double)attn[h * N + i] * (sds.at(h, j, i) - t);
       sds.at(h, j, i) = ds;
       dbs += ds;
-      dtau_acc += ds * (double)scores[h * N + i];
+      dtau_acc += ds * sxw.at(h, j, i) * dtau_inv;  // s without the bias: sum_i ds = 0
     }
-    dbs = block_reduce_sum_d(dbs, red);
-    if (threadIdx.x == 0) db_part[(int64_t)g * H + h] = (float)(dbs * dtau_inv);
+    dbs = block_reduce_sum_d<NW>(dbs, red);
+    if (threadIdx.x == 0) db_part[(int64_t)g * H + h] = dbs * dtau_inv;
   }
-  dtau_acc = block_reduce_sum_d(dtau_acc, red);
-  if (threadIdx.x == 0) dtau_part[g] = (float)(-dtau_acc * dtau_inv);
+  dtau_acc = block_reduce_sum_d<NW>(dtau_acc, red);
+  if (threadIdx.x == 0) dtau_part[g] = -dtau_acc * dtau_inv;
   if (!LDS) __threadfence();
   __syncthreads();
   // 3) dx_i = (sum_h a[h,i]) q / H + sum_h ds[h,i] W_h / tau ; dW_part[g,h] = sum_i ds[h,i] x_i / tau
-  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
+  for (int64_t c = threadIdx.x; c < C; c += NT) {
     const double qc = (double)q[c] * invH;
     double wc[kMaxH], dw[kMaxH];
 #pragma unroll
@@ -358,150 +302,467 @@ __device__ __forceinline__ void attn_bwd_body(const float* __restrict__ x, int64
   }
 }
 
-__device__ __forceinline__ void attn_bwd_fast(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
-                                              const float* __restrict__ W, float tau, int H, int32_t b, int n,
-                                              const int32_t* __restrict__ gperm, int g,
-                                              const float* __restrict__ attn, const float* __restrict__ scores,
-                                              const float* __restrict__ dpool, const float* __restrict__ dattn,
-                                              float* __restrict__ dx, int64_t lddx, float* __restrict__ dW_part,
-                                              float* __restrict__ db_part, float* __restrict__ dtau_part, char* smem,
-                                              double* red) {
-  float* xs = reinterpret_cast<float*>(smem);                                // [n][C]
-  double* sds = reinterpret_cast<double*>(smem + kFastXBytes);               // [kMaxH][kFastAtoms]
-  float* sa = reinterpret_cast<float*>(smem + kFastXBytes + 8 * kMaxH * kFastAtoms);
-  float* ssc = sa + kMaxH * kFastAtoms;
-  const double invH = 1.0 / (double)H;
-  const double dtau_inv = 1.0 / (double)tau;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const float* q = dpool + (int64_t)g * C;
-  stage_rows(x, ldx, C, b, n, gperm, xs);
-  for (int t = threadIdx.x; t < H * n; t += kThreads) {
-    const int h = t / n, j = t - h * n;
-    const int64_t i = gperm[b + j];
-    sa[h * kFastAtoms + j] = attn[h * N + i];
-    ssc[h * kFastAtoms + j] = scores[h * N + i];
-  }
-  __syncthreads();
-  // 1) da[h,i] (a wave per atom, lanes over channels, fp64 as in attn_bwd_body)
-  for (int j = w; j < n; j += kWaves) {
-    double acc = 0.0;
-    for (int64_t c = lane; c < C; c += 64) acc += (double)xs[j * C + c] * (double)q[c];
-    const double d = wave_sum_d(acc) * invH;
-    if (lane < H) sds[lane * kFastAtoms + j] = d + (dattn ? (double)dattn[lane * N + gperm[b + j]] : 0.0);
-  }
-  __syncthreads();
-  // 2) ds = a (da - <a, da> / sum a) per head (wave h % kWaves, lanes over atoms); db, dtau partials
-  double dtau_acc = 0.0;
-  for (int h = w; h < H; h += kWaves) {
-    const bool in = lane < n;
-    const double a = in ? (double)sa[h * kFastAtoms + lane] : 0.0;
-    const double da = in ? sds[h * kFastAtoms + lane] : 0.0;
-    double t = wave_sum_d(a * da);
-    const double asum = wave_sum_d(a);
-    if (asum > 0.0) t /= asum;
-    const double ds = a * (da - t);
-    if (in) sds[h * kFastAtoms + lane] = ds;
-    const double dbs = wave_sum_d(ds);
-    if (lane == 0) db_part[(int64_t)g * H + h] = (float)(dbs * dtau_inv);
-    dtau_acc += ds * (in ? (double)ssc[h * kFastAtoms + lane] : 0.0);
-  }
-  dtau_acc = block_reduce_sum_d(dtau_acc, red);
-  if (threadIdx.x == 0) dtau_part[g] = (float)(-dtau_acc * dtau_inv);
-  __syncthreads();
-  // 3) dx_i = (sum_h a[h,i]) q / H + sum_h ds[h,i] W_h / tau ; dW_part[g,h] = sum_i ds[h,i] x_i / tau
-  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
-    const double qc = (double)q[c] * invH;
-    double wc[kMaxH], dw[kMaxH];
+// ---------------------------------------------------------------------------------------------
+// Row-resident path
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxAtomsRows = 128;  // molecules up to this many atoms take the row-resident path
+
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+__device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+__device__ __forceinline__ float4 sub4(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
+__device__ __forceinline__ float4 scale4(float4 a, float k) { return make_float4(a.x * k, a.y * k, a.z * k, a.w * k); }
+
+// k * a + c, per component
+__device__ __forceinline__ float4 fma4(float k, float4 a, float4 c) {
+  return make_float4(fmaf(k, a.x, c.x), fmaf(k, a.y, c.y), fmaf(k, a.z, c.z), fmaf(k, a.w, c.w));
+}
+
+__device__ __forceinline__ double dot4d(float4 a, float4 b) {
+  return (double)a.x * (double)b.x + (double)a.y * (double)b.y + (double)a.z * (double)b.z + (double)a.w * (double)b.w;
+}
+
+__device__ __forceinline__ double wave_max_d(double v) {
 #pragma unroll
-    for (int h = 0; h < kMaxH; ++h) {
-      wc[h] = h < H ? (double)W[h * C + c] : 0.0;
-      dw[h] = 0.0;
-    }
-    for (int j = 0; j < n; ++j) {
-      const double xv = xs[j * C + c];
-      double asum = 0.0, dsw = 0.0;
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// this wave's rows j = base + p + r*P of the molecule, lane channels c..c+3 (one burst)
+template <int P, int R>
+__device__ __forceinline__ void load_rows(float4 (&xr)[R], const float* __restrict__ x, int64_t ldx,
+                                          const int32_t* __restrict__ gperm, int32_t b, int n, int base, int p,
+                                          int c, bool cv) {
 #pragma unroll
-      for (int h = 0; h < kMaxH; ++h) {
-        if (h < H) {
-          const double ds = sds[h * kFastAtoms + j];
-          asum += sa[h * kFastAtoms + j];
-          dsw += ds * wc[h];
-          dw[h] += ds * xv;
-        }
-      }
-      dx[gperm[b + j] * lddx + c] = (float)(asum * qc + dsw * dtau_inv);
-    }
-#pragma unroll
-    for (int h = 0; h < kMaxH; ++h)
-      if (h < H) dW_part[((int64_t)g * H + h) * C + c] = (float)(dw[h] * dtau_inv);
+  for (int r = 0; r < R; ++r) {
+    const int j = base + p + r * P;
+    xr[r] = (cv && j < n) ? ld4(x + (int64_t)gperm[b + j] * ldx + c) : zero4();
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_attn_bwd(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
-                                                        const float* __restrict__ W, const float* __restrict__ tau_p,
-                                                        int H, const int32_t* __restrict__ gptr,
-                                                        const int32_t* __restrict__ gperm,
-                                                        const float* __restrict__ attn, const float* __restrict__ scores,
-                                                        const float* __restrict__ dpool,
-                                                        const float* __restrict__ dattn, float* __restrict__ dx,
-                                                        int64_t lddx, float* __restrict__ dW_part,
-                                                        float* __restrict__ db_part, float* __restrict__ dtau_part,
-                                                        double* __restrict__ ds_glob) {
-  __shared__ __attribute__((aligned(16))) char smem[kSmemBytes];
-  __shared__ double red[kWaves];
-  double* sds = reinterpret_cast<double*>(smem);  // general path: [kMaxH][kCapB] doubles
+// Forward. A molecule of up to P·R atoms is one chunk and stays in registers from the score pass
+// to the pooled sum; larger ones (up to kMaxAtomsRows) run chunk by chunk and reload each chunk
+// for the pooled sum (L2/MALL hits).
+//
+// Centering. The softmax is shift invariant, so the scores enter as d_hj = (x_j - x_0) . W_h / tau
+// (x_0 = the molecule's first row; the bias cancels): fp32 dots of centred rows keep their error
+// relative to the spread of the scores, not to their common level (plain fp32 score sums left
+// 1e-6..6e-5 of the temperature gradient, which cancels the same way, to the summation order).
+// The saved scores are s_0 + d with s_0 = (x_0 . W_h + b_h) / tau.
+//
+// LDS (floats): scp [S][HM][MAXA] per-slice partial dots (+ [S][HM] of x_0 . W_h), sa [HM][MAXA]
+// attention, red [P-1][S*256] pooled partials.
+template <int S, int P, int R, int HM>
+__device__ __forceinline__ void attn_fwd_rows(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
+                                              const float* __restrict__ W, const float* __restrict__ bias, float tau,
+                                              int H, int32_t b, int n, const int32_t* __restrict__ gperm, int g,
+                                              float* __restrict__ pooled, float* __restrict__ attn,
+                                              float* __restrict__ scores, char* smem) {
+  constexpr int CAPN = P * R, NW = S * P, SC = S * 256, MAXA = kMaxAtomsRows;
+  // (R + 1) x HM dot partials (the extra row: x_0 . W_h) reduced in groups of NVC (power of two
+  // <= 32, the last group zero-padded)
+  constexpr int NV = (R + 1) * HM, NVC = NV >= 32 ? 32 : pow2ceil(NV), NCH = (NV + NVC - 1) / NVC,
+                SH = 6 - ilog2(NVC);
+  float* scp = reinterpret_cast<float*>(smem);
+  float* s0p = scp + S * HM * MAXA;
+  float* sa = s0p + S * HM;
+  float* red = sa + HM * MAXA;
+  // wave index made scalar: row indices, gperm reads and LDS offsets below stay in SGPRs
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), s = w % S, p = w / S;
+  const int c = s * 256 + lane * 4;
+  const bool cv = c < C;
+  const int nchunk = (n + CAPN - 1) / CAPN;
+  const float4 x0 = cv ? ld4(x + (int64_t)gperm[b] * ldx + c) : zero4();
+  float4 wv[HM];
+#pragma unroll
+  for (int h = 0; h < HM; ++h) wv[h] = (cv && h < H) ? ld4(W + (int64_t)h * C + c) : zero4();
+  float4 xr[R];
+  // 1) partial dots of this slice, reduced across the wave
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int base = ch * CAPN;
+    load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      float v[NVC];
+#pragma unroll
+      for (int k = 0; k < NVC; ++k) {
+        const int idx = q * NVC + k, r = idx / HM;
+        v[k] = idx >= NV ? 0.f : (r < R ? dot4(sub4(xr[r], x0), wv[idx % HM]) : dot4(x0, wv[idx % HM]));
+      }
+      const float tot = wave_reduce_scatter<NVC>(v);
+      const int idx = q * NVC + (lane >> SH);
+      const int r = idx / HM, h = idx % HM, j = base + p + r * P;
+      if ((lane & ((1 << SH) - 1)) == 0 && idx < NV && h < H) {
+        if (r < R) {
+          if (j < n) scp[(s * HM + h) * MAXA + j] = tot;
+        } else if (ch == 0 && p == 0) {
+          s0p[s * HM + h] = tot;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one group's products live at a time (VGPR budget)
+    }
+  }
+  __syncthreads();
+  // 2) softmax of head h by one wave, lanes over atoms
+  const float inv_tau = 1.f / tau;
+  for (int h = w; h < H; h += NW) {
+    float s0 = 0.f;
+#pragma unroll
+    for (int k = 0; k < S; ++k) s0 += s0p[k * HM + h];
+    s0 = (s0 + bias[h]) * inv_tau;
+    float mx = -INFINITY;
+    for (int j = lane; j < n; j += 64) {
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) d += scp[(k * HM + h) * MAXA + j];
+      d *= inv_tau;
+      sa[h * MAXA + j] = d;
+      mx = fmaxf(mx, d);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < n; j += 64) sum += expf(sa[h * MAXA + j] - mx);
+    sum = wave_sum(sum);
+    for (int j = lane; j < n; j += 64) {
+      const int64_t i = gperm[b + j];
+      const float d = sa[h * MAXA + j];
+      const float a = expf(d - mx) / sum;
+      scores[h * N + i] = s0 + d;
+      attn[h * N + i] = a;
+      sa[h * MAXA + j] = a;
+    }
+  }
+  __syncthreads();
+  // 3) pooled[g] = (1/H) sum_i (sum_h a[h,i]) x_i : this wave's rows, then the row groups in order
+  float4 acc = zero4();
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int base = ch * CAPN;
+    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = base + p + r * P;
+      if (j < n) {
+        float cf = 0.f;
+#pragma unroll
+        for (int h = 0; h < HM; ++h)
+          if (h < H) cf += sa[h * MAXA + j];
+        acc = fma4(cf, xr[r], acc);
+      }
+    }
+  }
+  if (p > 0 && cv) *reinterpret_cast<float4*>(red + (p - 1) * SC + c) = acc;
+  __syncthreads();
+  if (p == 0 && cv) {
+#pragma unroll
+    for (int k = 0; k < P - 1; ++k) acc = add4(acc, *reinterpret_cast<const float4*>(red + k * SC + c));
+    const float invH = 1.f / (float)H;
+    *reinterpret_cast<float4*>(pooled + (int64_t)g * C + c) =
+        make_float4(acc.x * invH, acc.y * invH, acc.z * invH, acc.w * invH);
+  }
+}
+
+// Backward (same chunking and centring: x_j - x_0 in every dot; sum_j ds_hj = 0, so the
+// centred da, score and dW sums equal the plain ones exactly, and fp32 keeps their error relative
+// to the spread of the atoms' features rather than their common level).
+//   da_hj = (x_j - x_0) . q / H + d_attn_hj,  t_h = sum_j a da / sum_j a,  ds = a (da - t)
+//   dx_j = (sum_h a_hj) q / H + sum_h ds_hj W_h / tau
+//   dW_h = sum_j ds_hj (x_j - x_0) / tau,  db_h = sum_j ds_hj / tau,
+//   dtau = -sum_hj ds_hj ((x_j - x_0) . W_h / tau) / tau
+// LDS (floats): dap [S][MAXA] per-slice x.q partials, dsp [S][HM][MAXA] x.W_h partials, sds [HM][MAXA]
+// ds, sa [HM][MAXA] attention, red [P-1][HM][S*256] dW partials; dtp [NW] doubles.
+template <int S, int P, int R, int HM>
+__device__ __forceinline__ void attn_bwd_rows(const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C,
+                                              const float* __restrict__ W, float tau, int H, int32_t b, int n,
+                                              const int32_t* __restrict__ gperm, int g,
+                                              const float* __restrict__ attn, const float* __restrict__ dpool,
+                                              const float* __restrict__ dattn, float* __restrict__ dx, int64_t lddx,
+                                              float* __restrict__ dW_part, double* __restrict__ db_part,
+                                              double* __restrict__ dtau_part, char* smem) {
+  constexpr int CAPN = P * R, NW = S * P, SC = S * 256, MAXA = kMaxAtomsRows;
+  // per row: x.q and the HM x.W_h dots, reduced in groups of NVC (power of two <= 32, zero-padded)
+  constexpr int HC = HM + 1, NV = R * HC, NVC = NV >= 32 ? 32 : pow2ceil(NV), NCH = (NV + NVC - 1) / NVC,
+                SH = 6 - ilog2(NVC);
+  double* dtp = reinterpret_cast<double*>(smem);
+  float* dap = reinterpret_cast<float*>(dtp + NW);
+  float* dsp = dap + S * MAXA;
+  float* sds = dsp + S * HM * MAXA;
+  float* sa = sds + HM * MAXA;
+  float* red = sa + HM * MAXA;
+  // wave index made scalar: row indices, gperm reads and LDS offsets below stay in SGPRs
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), s = w % S, p = w / S;
+  const int c = s * 256 + lane * 4;
+  const bool cv = c < C;
+  const int nchunk = (n + CAPN - 1) / CAPN;
+  const float4 x0 = cv ? ld4(x + (int64_t)gperm[b] * ldx + c) : zero4();
+  const float4 q = cv ? ld4(dpool + (int64_t)g * C + c) : zero4();
+  float4 wv[HM];
+#pragma unroll
+  for (int h = 0; h < HM; ++h) wv[h] = (cv && h < H) ? ld4(W + (int64_t)h * C + c) : zero4();
+  for (int t = threadIdx.x; t < H * n; t += NW * 64) {
+    const int h = t / n, j = t - h * n;
+    sa[h * MAXA + j] = attn[h * N + gperm[b + j]];
+  }
+  float4 xr[R];
+  // 1) centred dots with q and with each W_h for this slice, reduced across the wave
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int base = ch * CAPN;
+    load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+#pragma unroll
+    for (int qq = 0; qq < NCH; ++qq) {
+      float v[NVC];
+#pragma unroll
+      for (int k = 0; k < NVC; ++k) {
+        const int idx = qq * NVC + k;
+        v[k] = idx < NV ? dot4(sub4(xr[idx / HC], x0), (idx % HC) == 0 ? q : wv[(idx % HC + HM - 1) % HM]) : 0.f;
+      }
+      const float tot = wave_reduce_scatter<NVC>(v);
+      const int idx = qq * NVC + (lane >> SH);
+      const int r = idx / HC, comp = idx % HC, j = base + p + r * P;
+      if ((lane & ((1 << SH) - 1)) == 0 && idx < NV && j < n) {
+        if (comp == 0)
+          dap[s * MAXA + j] = tot;
+        else if (comp - 1 < H)
+          dsp[(s * HM + comp - 1) * MAXA + j] = tot;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one group's products live at a time (VGPR budget)
+    }
+  }
+  __syncthreads();
+  // 2) ds = a (da - <a, da> / sum a) per head (one wave per head, lanes over atoms; sums in fp64);
+  //    db, dtau partials (normalising by sum a keeps sum_i ds = 0: see attn_bwd_body)
+  const double invH = 1.0 / (double)H;
+  const double dtau_inv = 1.0 / (double)tau;
+  double dtl = 0.0;
+  for (int h = w; h < H; h += NW) {
+    double t = 0.0, asum = 0.0;
+    for (int j = lane; j < n; j += 64) {
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) d += dap[k * MAXA + j];
+      const double da = (double)d * invH + (dattn ? (double)dattn[h * N + gperm[b + j]] : 0.0);
+      const double a = sa[h * MAXA + j];
+      sds[h * MAXA + j] = (float)da;  // exact up to its fp32 rounding: recomputed below
+      t += a * da;
+      asum += a;
+    }
+    t = wave_sum_d(t);
+    asum = wave_sum_d(asum);
+    if (asum > 0.0) t /= asum;
+    double dbs = 0.0;
+    for (int j = lane; j < n; j += 64) {
+      float d = 0.f, sw = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        d += dap[k * MAXA + j];
+        sw += dsp[(k * HM + h) * MAXA + j];
+      }
+      const double da = (double)d * invH + (dattn ? (double)dattn[h * N + gperm[b + j]] : 0.0);
+      const double ds = (double)sa[h * MAXA + j] * (da - t);
+      sds[h * MAXA + j] = (float)ds;
+      dbs += ds;
+      dtl += ds * (double)sw * dtau_inv;
+    }
+    dbs = wave_sum_d(dbs);
+    if (lane == 0) db_part[(int64_t)g * H + h] = dbs * dtau_inv;
+  }
+  dtl = wave_sum_d(dtl);
+  if (lane == 0) dtp[w] = dtl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) t += dtp[k];
+    dtau_part[g] = -t * dtau_inv;
+  }
+  // 3) dx_j = (sum_h a_hj) q / H + sum_h ds_hj W_h / tau, and dW partials sum_j ds_hj (x_j - x_0)
+  const float qh = 1.f / (float)H, ti = 1.f / tau;
+  const float4 qs = make_float4(q.x * qh, q.y * qh, q.z * qh, q.w * qh);
+  float4 dw[HM];
+#pragma unroll
+  for (int h = 0; h < HM; ++h) dw[h] = zero4();
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int base = ch * CAPN;
+    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = base + p + r * P;
+      if (j < n) {
+        const float4 xc = sub4(xr[r], x0);
+        float as = 0.f;
+        float4 d = zero4();
+#pragma unroll
+        for (int h = 0; h < HM; ++h) {
+          if (h < H) {
+            const float ds = sds[h * MAXA + j];
+            as += sa[h * MAXA + j];
+            d = fma4(ds, wv[h], d);
+            dw[h] = fma4(ds, xc, dw[h]);
+          }
+        }
+        if (cv) *reinterpret_cast<float4*>(dx + (int64_t)gperm[b + j] * lddx + c) = fma4(as, qs, scale4(d, ti));
+      }
+    }
+  }
+  // 4) this molecule's dW partial: the row groups combined in order, all heads at once
+  if (p > 0 && cv) {
+#pragma unroll
+    for (int h = 0; h < HM; ++h)
+      if (h < H) *reinterpret_cast<float4*>(red + ((p - 1) * HM + h) * SC + c) = dw[h];
+  }
+  __syncthreads();
+  if (p == 0 && cv) {
+#pragma unroll
+    for (int h = 0; h < HM; ++h) {
+      if (h < H) {
+        float4 t = dw[h];
+#pragma unroll
+        for (int k = 0; k < P - 1; ++k) t = add4(t, *reinterpret_cast<const float4*>(red + (k * HM + h) * SC + c));
+        *reinterpret_cast<float4*>(dW_part + ((int64_t)g * H + h) * C + c) = scale4(t, ti);
+      }
+    }
+  }
+}
+
+template <int S, int P, int HM>
+constexpr int rows_fwd_bytes() {
+  return 4 * (S * HM * kMaxAtomsRows + S * HM + HM * kMaxAtomsRows + (P - 1) * S * 256);
+}
+template <int S, int P, int HM>
+constexpr int rows_bwd_bytes() {
+  return 8 * S * P + 4 * (S * kMaxAtomsRows + S * HM * kMaxAtomsRows + 2 * HM * kMaxAtomsRows + (P - 1) * HM * S * 256);
+}
+template <int S, int P, int HM>
+constexpr int smem_bytes() {
+  return std::max(kGeneralSmem, std::max(rows_fwd_bytes<S, P, HM>(), rows_bwd_bytes<S, P, HM>()));
+}
+
+// One molecule per workgroup of S*P waves. The row-resident body runs when the molecule and the
+// operand layout fit it (a per-block uniform choice); the general body otherwise.
+template <int S, int P, int R, int HM>
+__global__ __launch_bounds__(S * P * 64) void k_attn_fwd(
+    const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C, const float* __restrict__ W,
+    const float* __restrict__ bias, const float* __restrict__ tau_p, int H, const int32_t* __restrict__ gptr,
+    const int32_t* __restrict__ gperm, float* __restrict__ pooled, float* __restrict__ attn,
+    float* __restrict__ scores) {
+  constexpr int NT = S * P * 64;
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<S, P, HM>()];
+  __shared__ float red[NT / 64];
   const int g = blockIdx.x;
   const int32_t b = gptr[g], e = gptr[g + 1];
   const int n = e - b;
   const float tau = *tau_p;
-  if (fast_ok(n, C, H) && (ldx % 4) == 0 && ((uintptr_t)x & 15) == 0)
-    attn_bwd_fast(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part, db_part,
-                  dtau_part, smem, red);
-  else if (n <= kCapB)
-    attn_bwd_body<true>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part, db_part,
-                        dtau_part, Slot<true, double, kCapB>{sds, N}, red);
+  const bool rows = n <= kMaxAtomsRows && H <= HM && C <= S * 256 && (C % 4) == 0 &&
+                    (ldx % 4) == 0 && al16(x) && al16(W) && al16(pooled);
+  if (rows)
+    attn_fwd_rows<S, P, R, HM>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, smem);
+  else if (n <= kCap)
+    attn_fwd_body<true, NT>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores,
+                            Slot<true>{reinterpret_cast<float*>(smem), N}, red);
   else
-    attn_bwd_body<false>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part,
-                         db_part, dtau_part, Slot<false, double, kCapB>{ds_glob, N}, red);
+    attn_fwd_body<false, NT>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, Slot<false>{attn, N},
+                             red);
 }
 
-// One wave per output value (dW[h,c], db[h], dtau): lanes take molecules g = lane, lane+64, ... and
-// the 64 partial sums are combined by a fixed butterfly — deterministic and latency-parallel.
-__global__ void k_attn_reduce(int64_t G, int H, int64_t C, const float* __restrict__ dW_part,
-                              const float* __restrict__ db_part, const float* __restrict__ dtau_part,
-                              float* __restrict__ dW, float* __restrict__ db, float* __restrict__ dtau) {
+template <int S, int P, int R, int HM>
+__global__ __launch_bounds__(S * P * 64) void k_attn_bwd(
+    const float* __restrict__ x, int64_t ldx, int64_t N, int64_t C, const float* __restrict__ W,
+    const float* __restrict__ tau_p, int H, const int32_t* __restrict__ gptr, const int32_t* __restrict__ gperm,
+    const float* __restrict__ attn, const float* __restrict__ scores, const float* __restrict__ dpool,
+    const float* __restrict__ dattn, float* __restrict__ dx, int64_t lddx, float* __restrict__ dW_part,
+    double* __restrict__ db_part, double* __restrict__ dtau_part, double* __restrict__ ds_glob) {
+  constexpr int NT = S * P * 64;
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<S, P, HM>()];
+  __shared__ double red[NT / 64];
+  const int g = blockIdx.x;
+  const int32_t b = gptr[g], e = gptr[g + 1];
+  const int n = e - b;
+  const float tau = *tau_p;
+  const bool rows = n <= kMaxAtomsRows && H <= HM && C <= S * 256 && (C % 4) == 0 &&
+                    (ldx % 4) == 0 && (lddx % 4) == 0 && al16(x) && al16(W) && al16(dx) && al16(dpool) &&
+                    al16(dW_part);
+  if (rows)
+    attn_bwd_rows<S, P, R, HM>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, dpool, dattn, dx, lddx, dW_part, db_part,
+                            dtau_part, smem);
+  else if (n <= kCapB)
+    attn_bwd_body<true, NT>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part,
+                            db_part, dtau_part, Slot<true, double, kCapB>{reinterpret_cast<double*>(smem), N},
+                            Slot<true, double, kCapB>{reinterpret_cast<double*>(smem) + kMaxH * kCapB, N}, red);
+  else
+    attn_bwd_body<false, NT>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, scores, dpool, dattn, dx, lddx, dW_part,
+                             db_part, dtau_part, Slot<false, double, kCapB>{ds_glob, N},
+                             Slot<false, double, kCapB>{ds_glob + (int64_t)H * N, N}, red);
+}
+
+// Deterministic reduction of the per-molecule partials: column t of [dW (H*C) | db (H) | dtau]
+// is summed over molecules by lane t % 64 of a 16-wave block (coalesced rows of the partial slab),
+// wave k taking molecules g = k, k+16, ... in fp64 (16 loads in flight), then the 16 wave sums in
+// order.
+constexpr int kRedWaves = 16;
+
+template <typename T>
+__device__ __forceinline__ double sum_column(const T* __restrict__ src, int64_t stride, int64_t G, int w) {
+  double s = 0.0;
+  for (int64_t g0 = w; g0 < G; g0 += 16 * kRedWaves) {
+    T v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int64_t g = g0 + (int64_t)k * kRedWaves;
+      v[k] = g < G ? src[g * stride] : T(0);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += (double)v[k];
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(kRedWaves * 64) void k_attn_reduce(int64_t G, int H, int64_t C,
+                                                                const float* __restrict__ dW_part,
+                                                                const double* __restrict__ db_part,
+                                                                const double* __restrict__ dtau_part,
+                                                                float* __restrict__ dW, float* __restrict__ db,
+                                                                float* __restrict__ dtau) {
+  __shared__ double red[kRedWaves][64];
   const int64_t nw = (int64_t)H * C;
-  const int lane = threadIdx.x & 63;
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
-  for (int64_t t = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6); t < nw + H + 1; t += waves) {
-    double s = 0.0;
-    if (t < nw) {
-      for (int64_t g = lane; g < G; g += 64) s += dW_part[g * nw + t];
-    } else if (t < nw + H) {
-      for (int64_t g = lane; g < G; g += 64) s += db_part[g * H + (t - nw)];
-    } else {
-      for (int64_t g = lane; g < G; g += 64) s += dtau_part[g];
-    }
-    s = wave_sum_d(s);
-    if (lane == 0) {
-      if (t < nw)
-        dW[t] = (float)s;
-      else if (t < nw + H)
-        db[t - nw] = (float)s;
-      else
-        *dtau = (float)s;
-    }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (t < nw)
+    s = sum_column(dW_part + t, nw, G, w);
+  else if (t < nw + H)
+    s = sum_column(db_part + (t - nw), H, G, w);
+  else if (t == nw + H)
+    s = sum_column(dtau_part, 1, G, w);
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && t <= nw + H) {
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRedWaves; ++k) tot += red[k][lane];
+    if (t < nw)
+      dW[t] = (float)tot;
+    else if (t < nw + H)
+      db[t - nw] = (float)tot;
+    else
+      *dtau = (float)tot;
   }
 }
 
 // kind: 0 mean, 1 max, 2 sum
-__global__ __launch_bounds__(kThreads) void k_segpool_fwd(int kind, const float* __restrict__ x, int64_t ldx, int64_t C,
-                                                           const int32_t* __restrict__ gptr,
-                                                           const int32_t* __restrict__ gperm, float* __restrict__ out,
-                                                           int32_t* __restrict__ argmax) {
+__global__ __launch_bounds__(kSegThreads) void k_segpool_fwd(int kind, const float* __restrict__ x, int64_t ldx,
+                                                              int64_t C, const int32_t* __restrict__ gptr,
+                                                              const int32_t* __restrict__ gperm,
+                                                              float* __restrict__ out, int32_t* __restrict__ argmax) {
   const int g = blockIdx.x;
   const int32_t b = gptr[g], e = gptr[g + 1];
-  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
+  for (int64_t c = threadIdx.x; c < C; c += kSegThreads) {
     if (kind == 1) {
       // torch_scatter 2.1.2 CPU scatter_max: running max initialised to lowest(), strict '>'
       // (first arg-max wins), untouched outputs filled with 0.
@@ -526,15 +787,15 @@ __global__ __launch_bounds__(kThreads) void k_segpool_fwd(int kind, const float*
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_segpool_bwd(int kind, const float* __restrict__ dout, int64_t C,
-                                                           const int32_t* __restrict__ gptr,
-                                                           const int32_t* __restrict__ gperm,
-                                                           const int32_t* __restrict__ argmax, float* __restrict__ dx,
-                                                           int64_t lddx) {
+__global__ __launch_bounds__(kSegThreads) void k_segpool_bwd(int kind, const float* __restrict__ dout, int64_t C,
+                                                              const int32_t* __restrict__ gptr,
+                                                              const int32_t* __restrict__ gperm,
+                                                              const int32_t* __restrict__ argmax,
+                                                              float* __restrict__ dx, int64_t lddx) {
   const int g = blockIdx.x;
   const int32_t b = gptr[g], e = gptr[g + 1];
   const float inv = kind == 0 ? 1.f / (float)max(e - b, 1) : 1.f;
-  for (int64_t c = threadIdx.x; c < C; c += kThreads) {
+  for (int64_t c = threadIdx.x; c < C; c += kSegThreads) {
     const float d = dout[(int64_t)g * C + c];
     const int32_t am = kind == 1 ? argmax[(int64_t)g * C + c] : -1;
     for (int32_t j = b; j < e; ++j) {
@@ -549,13 +810,47 @@ __global__ __launch_bounds__(kThreads) void k_segpool_bwd(int kind, const float*
   }
 }
 
+// Channel slices per workgroup (S) and register rows per wave (R) for a width: C <= 256 -> one
+// slice, 8 rows per wave (32-atom chunks: all of QM9 in one); C <= 512 -> 2 slices, 16 rows per
+// wave (64-atom chunks); C <= 1024 -> 4 slices (1024 threads, 128 VGPRs), 12 rows per wave (48-atom
+// chunks: the synthetic 40-atom molecules in one).
+// C > 1024 runs the general body inside the S = 4 instantiation.
+int pool_slices(int64_t C) { return C <= 256 ? 1 : (C <= 512 ? 2 : 4); }
+
+template <int S, int P, int R>
+void launch_attn_fwd(int H, unsigned G, hipStream_t st, const float* x, int64_t ldx, int64_t N, int64_t C,
+                     const float* W, const float* b, const float* tau, const int32_t* gptr, const int32_t* gperm,
+                     float* pooled, float* attn, float* scores) {
+  const dim3 block(S * P * 64);
+  if (H <= 4)
+    hipLaunchKernelGGL((k_attn_fwd<S, P, R, 4>), dim3(G), block, 0, st, x, ldx, N, C, W, b, tau, H, gptr, gperm, pooled,
+                       attn, scores);
+  else
+    hipLaunchKernelGGL((k_attn_fwd<S, P, R, 8>), dim3(G), block, 0, st, x, ldx, N, C, W, b, tau, H, gptr, gperm, pooled,
+                       attn, scores);
+}
+
+template <int S, int P, int R>
+void launch_attn_bwd(int H, unsigned G, hipStream_t st, const float* x, int64_t ldx, int64_t N, int64_t C,
+                     const float* W, const float* tau, const int32_t* gptr, const int32_t* gperm, const float* attn,
+                     const float* scores, const float* dpool, const float* dattn, float* dx, int64_t lddx,
+                     float* dW_part, double* db_part, double* dtau_part, double* ds_glob) {
+  const dim3 block(S * P * 64);
+  if (H <= 4)
+    hipLaunchKernelGGL((k_attn_bwd<S, P, R, 4>), dim3(G), block, 0, st, x, ldx, N, C, W, tau, H, gptr, gperm, attn,
+                       scores, dpool, dattn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+  else
+    hipLaunchKernelGGL((k_attn_bwd<S, P, R, 8>), dim3(G), block, 0, st, x, ldx, N, C, W, tau, H, gptr, gperm, attn,
+                       scores, dpool, dattn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+}
+
 }  // namespace
 }  // namespace aimx
 
 using namespace aimx;
 
 extern "C" size_t aimx_attn_pool_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t G) {
-  return sizeof(float) * (size_t)(G * H * C + G * H + G + 64) + sizeof(double) * (size_t)(H * N + 8);
+  return sizeof(float) * (size_t)(G * H * C + 32) + sizeof(double) * (size_t)(G * H + G + 2 * H * N + 24);
 }
 
 extern "C" int aimx_attn_pool_forward(const float* x, int64_t ldx, int64_t N, int64_t C, const float* W, const float* b,
@@ -563,8 +858,12 @@ extern "C" int aimx_attn_pool_forward(const float* x, int64_t ldx, int64_t N, in
                                       float* pooled, float* attn, float* scores, aimx_stream_t s) {
   if (H < 1 || H > kMaxH || C < 0 || N < 0 || G < 0) return AIMX_EARG;
   if (G == 0) return AIMX_OK;
-  hipLaunchKernelGGL(k_attn_fwd, dim3((unsigned)G), dim3(kThreads), 0, (hipStream_t)s, x, ldx, N, C, W, b, tau, (int)H,
-                     gptr, gperm, pooled, attn, scores);
+  hipStream_t st = (hipStream_t)s;
+  switch (pool_slices(C)) {
+    case 1: launch_attn_fwd<1, 4, 8>((int)H, (unsigned)G, st, x, ldx, N, C, W, b, tau, gptr, gperm, pooled, attn, scores); break;
+    case 2: launch_attn_fwd<2, 4, 12>((int)H, (unsigned)G, st, x, ldx, N, C, W, b, tau, gptr, gperm, pooled, attn, scores); break;
+    default: launch_attn_fwd<4, 2, 24>((int)H, (unsigned)G, st, x, ldx, N, C, W, b, tau, gptr, gperm, pooled, attn, scores);
+  }
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
@@ -578,17 +877,30 @@ extern "C" int aimx_attn_pool_backward(const float* x, int64_t ldx, int64_t N, i
   if (H < 1 || H > kMaxH || C < 0 || N < 0 || G < 0) return AIMX_EARG;
   if (ws_bytes < aimx_attn_pool_workspace_bytes(N, C, H, G) || !ws) return AIMX_EARG;
   float* dW_part = (float*)ws;
-  float* db_part = dW_part + G * H * C;
-  float* dtau_part = db_part + G * H;
+  // per-molecule db / dtau partials in fp64: these scalars sum contributions of both signs over
+  // all molecules, and fp32 partials left their rounding amplified in the total
+  double* db_part = (double*)(((uintptr_t)(dW_part + G * H * C) + 63) & ~(uintptr_t)63);
+  double* dtau_part = db_part + G * H;
   double* ds_glob = (double*)(((uintptr_t)(dtau_part + G) + 63) & ~(uintptr_t)63);
   if (G > 0) {
-    hipLaunchKernelGGL(k_attn_bwd, dim3((unsigned)G), dim3(kThreads), 0, s, x, ldx, N, C, W, tau, (int)H, gptr,
-                       gperm, attn, scores, d_pooled, d_attn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+    switch (pool_slices(C)) {
+      case 1:
+        launch_attn_bwd<1, 4, 8>((int)H, (unsigned)G, s, x, ldx, N, C, W, tau, gptr, gperm, attn, scores, d_pooled, d_attn,
+                              dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+        break;
+      case 2:
+        launch_attn_bwd<2, 4, 12>((int)H, (unsigned)G, s, x, ldx, N, C, W, tau, gptr, gperm, attn, scores, d_pooled,
+                               d_attn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+        break;
+      default:
+        launch_attn_bwd<4, 2, 24>((int)H, (unsigned)G, s, x, ldx, N, C, W, tau, gptr, gperm, attn, scores, d_pooled,
+                               d_attn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+    }
     AIMX_CHECK_LAUNCH();
   }
   const int64_t tot = H * C + H + 1;
-  hipLaunchKernelGGL(k_attn_reduce, dim3((unsigned)std::min<int64_t>(cdiv(tot, 4), 4096)), dim3(256), 0, s, G,
-                     (int)H, C, dW_part, db_part, dtau_part, dW, db, dtau);
+  hipLaunchKernelGGL(k_attn_reduce, dim3((unsigned)cdiv(tot, 64)), dim3(kRedWaves * 64), 0, s, G, (int)H, C, dW_part,
+                     db_part, dtau_part, dW, db, dtau);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
@@ -598,8 +910,8 @@ extern "C" int aimx_segment_pool_forward(int32_t kind, const float* x, int64_t l
                                          int32_t* argmax, aimx_stream_t s) {
   if (kind < 0 || kind > 2 || (kind == 1 && !argmax) || G < 0 || C < 0) return AIMX_EARG;
   if (G == 0 || C == 0) return AIMX_OK;
-  hipLaunchKernelGGL(k_segpool_fwd, dim3((unsigned)G), dim3(kThreads), 0, (hipStream_t)s, (int)kind, x, ldx, C, gptr,
-                     gperm, out, argmax);
+  hipLaunchKernelGGL(k_segpool_fwd, dim3((unsigned)G), dim3(kSegThreads), 0, (hipStream_t)s, (int)kind, x, ldx, C,
+                     gptr, gperm, out, argmax);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
@@ -609,7 +921,7 @@ extern "C" int aimx_segment_pool_backward(int32_t kind, const float* dout, int64
                                           int64_t lddx, aimx_stream_t s) {
   if (kind < 0 || kind > 2 || (kind == 1 && !argmax) || G < 0 || C < 0) return AIMX_EARG;
   if (G == 0 || C == 0) return AIMX_OK;
-  hipLaunchKernelGGL(k_segpool_bwd, dim3((unsigned)G), dim3(kThreads), 0, (hipStream_t)s, (int)kind, dout, C, gptr,
+  hipLaunchKernelGGL(k_segpool_bwd, dim3((unsigned)G), dim3(kSegThreads), 0, (hipStream_t)s, (int)kind, dout, C, gptr,
                      gperm, argmax, dx, lddx);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;

@@ -318,12 +318,16 @@ int aimx_wgrad_grouped(const AimxWgradProblem* problems, int32_t n, void* worksp
  * optimizer.step()  with optimizer = torch.optim.Adam(...) (reference
  * src/training/trainer.py:163-164 and 221-223):
  *   total = ||all grads||_2; coef = min(max_norm / (total + 1e-6), 1) (max_norm <= 0: no clip);
- *   grad *= coef (in place); step += 1; [grad += weight_decay * param];
+ *   grad *= coef (in place); step[slot] += 1; [grad += weight_decay * param];
  *   exp_avg = lerp(exp_avg, grad, 1 - beta1); exp_avg_sq = beta2*exp_avg_sq + (1-beta2)*grad^2;
- *   param -= lr[group] / (1 - beta1^step) * exp_avg / (sqrt(exp_avg_sq) / sqrt(1 - beta2^step) + eps)
- * `step` (one float) and `lr` (one float per parameter group) are device memory, so the call is
- * graph-capturable and schedulers update lr without re-capture. *norm_out (nullable, device)
- * receives the total norm clip_grad_norm_ returns.
+ *   param -= lr[group] / (1 - beta1^s) * exp_avg / (sqrt(exp_avg_sq) / sqrt(1 - beta2^s) + eps),
+ *   s = step[slot]
+ * `step` is an array of per-parameter step counters (torch.optim.Adam's state['step']): tensor i
+ * advances and uses step[tensors[i].step_slot] (slots distinct within a call, < 2^23), so a
+ * parameter left out of a step (no gradient) keeps its count, as in torch. `step` and `lr` (one
+ * float per parameter group, group < 256) are device memory, so the call is graph-capturable and
+ * schedulers update lr without re-capture. *norm_out (nullable, device) receives the total norm
+ * clip_grad_norm_ returns.
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
   float* param;
@@ -332,6 +336,7 @@ typedef struct {
   float* exp_avg_sq;
   int64_t numel;
   int32_t group;
+  int32_t step_slot;
 } AimxAdamTensor;
 
 /* one_minus_beta1/2 are passed separately because torch forms 1 - beta in double precision

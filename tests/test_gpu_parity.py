@@ -394,6 +394,50 @@ def test_attention_pool_standalone():
     assert not bad, bad
 
 
+@pytest.mark.parametrize("C,H,strided", [(128, 4, False), (256, 4, True), (256, 1, False), (300, 3, False),
+                                           (512, 4, False), (512, 8, True), (1024, 4, False), (1024, 8, False),
+                                           (76, 4, False), (1100, 2, False)])
+def test_attention_pool_shapes(C, H, strided):
+    """Row-resident path (one chunk, several chunks), general path (odd widths, > 128 atoms, > 512
+    atoms: global scratch), strided x, 1..8 heads, an upstream attention gradient, and features
+    with a large common mean (the softmax-backward cancellation case) vs the fp64 oracle."""
+    from models.pooling import MultiHeadAttentionPoolingLayer
+    _, om = _oracle()
+    g = torch.Generator().manual_seed(C * 10 + H)
+    sizes = [1, 2, 7, 18, 29, 31, 32, 33, 40, 47, 48, 49, 64, 65, 100, 128, 129, 300, 600, 3]
+    batch = torch.cat([torch.full((s,), i, dtype=torch.long) for i, s in enumerate(sizes)])
+    n = batch.numel()
+    x = 3.0 + torch.randn(n, C + (4 if strided else 0), generator=g)
+    pool = MultiHeadAttentionPoolingLayer(C, num_heads=H, initial_temperature=0.7)
+    with torch.no_grad():
+        for lin in pool.attention_weights:
+            lin.weight.copy_(torch.randn(1, C, generator=g) * 0.1)
+            lin.bias.copy_(torch.randn(1, generator=g))
+    params = {k: v.detach().clone() for k, v in pool.state_dict().items()}
+    wp = torch.randn(len(sizes), C, generator=g)
+    wa = torch.randn(H, n, generator=g)
+    pool = pool.to(DEV)
+    xd = x.to(DEV)[:, :C].requires_grad_() if not strided else x.to(DEV).requires_grad_()
+    xin = xd[:, :C] if strided else xd
+    pooled, attn = pool(xin, batch.to(DEV))
+    ((pooled * wp.to(DEV)).sum() + (attn * wa.to(DEV)).sum()).backward()
+    ours = {"pooled": pooled.detach().cpu().numpy(), "attn": attn.detach().cpu().numpy(),
+            "grad_x": xd.grad[:, :C].cpu().numpy()}
+    for k, p in pool.named_parameters():
+        ours["grad." + k] = p.grad.cpu().numpy()
+    refs = {}
+    for dt in (torch.float32, torch.float64):  # the reference's fp32 algorithm (its noise floor) and fp64
+        pd = {"pool." + k: v.detach().to(dt).requires_grad_() for k, v in params.items()}
+        xr = x[:, :C].detach().to(dt).requires_grad_()
+        pp, aa = om.attention_pool(pd, "pool.", xr, batch, H, len(sizes))
+        ((pp * wp.to(dt)).sum() + (aa * wa.to(dt)).sum()).backward()
+        ref = {"pooled": pp.detach().numpy(), "attn": aa.detach().numpy(), "grad_x": xr.grad.numpy()}
+        ref.update({"grad." + k[5:]: v.grad.numpy() for k, v in pd.items()})
+        refs[dt] = ref
+    bad = parity_failures(ours, refs[torch.float32], refs[torch.float64])
+    assert not bad, bad
+
+
 # ----------------------------------------------------------------------------------- full model
 def _build_model(cfg, seed):
     from models import GNN
@@ -529,6 +573,35 @@ def test_fused_adam_matches_torch_clip_and_adam(max_norm, wd):
         assert norm_rel(st_a["exp_avg"].cpu().numpy(), st_b["exp_avg"].cpu().numpy()) < 1e-6
         assert norm_rel(st_a["exp_avg_sq"].cpu().numpy(), st_b["exp_avg_sq"].cpu().numpy()) < 1e-6
         assert float(st_a["step"]) == float(st_b["step"]) == 5.0
+
+
+def test_fused_adam_missing_gradients_keep_per_parameter_steps():
+    """Steps where some parameters have no gradient (e.g. a batch without edges skips message
+    passing, gnn.py:287): torch.optim.Adam advances only the stepped parameters' state['step'];
+    the fused step must too (per-parameter bias corrections)."""
+    from aimx.optim import FusedAdam
+    g = torch.Generator().manual_seed(11)
+    shapes = [(64, 32), (32,), (1000,), (5,)]
+    p0 = [torch.randn(s, generator=g) for s in shapes]
+    ours = [x.clone().to(DEV).requires_grad_() for x in p0]
+    ref = [x.clone().to(DEV).requires_grad_() for x in p0]
+    opt = FusedAdam(ours, lr=1e-2, max_grad_norm=1.0)
+    topt = torch.optim.Adam(ref, lr=1e-2)
+    present = [[0, 1, 2, 3], [0, 2], [1, 3], [0, 1, 2, 3], [2], [0, 1, 2, 3]]
+    for have in present:
+        for i, (a, b) in enumerate(zip(ours, ref)):
+            if i in have:
+                gr = torch.randn(shapes[i], generator=g)
+                a.grad, b.grad = gr.to(DEV).clone(), gr.to(DEV).clone()
+            else:
+                a.grad = b.grad = None
+        opt.step()
+        torch.nn.utils.clip_grad_norm_([b for b in ref if b.grad is not None], 1.0)
+        topt.step()
+    for a, b in zip(ours, ref):
+        assert float(opt.state[a]["step"]) == float(topt.state[b]["step"])
+        assert norm_rel(a.detach().cpu().numpy(), b.detach().cpu().numpy()) < 1e-6
+        assert norm_rel(opt.state[a]["exp_avg_sq"].cpu().numpy(), topt.state[b]["exp_avg_sq"].cpu().numpy()) < 1e-6
 
 
 def test_aux_stream_weight_gradients_identical(monkeypatch):

@@ -37,8 +37,9 @@ def test_struct_layouts_match_header():
     src = open(os.path.join(ROOT, "include", "aimx.h")).read()
     for cname, py in (("AimxGemmArgs", _lib.GemmArgs), ("AimxShellStack", _lib.ShellStack),
                       ("AimxShellStackGrad", _lib.ShellStackGrad), ("AimxEmbeddingTables", _lib.EmbeddingTables),
-                      ("AimxHead", _lib.Head), ("AimxHeadGrad", _lib.HeadGrad)):
-        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
+                      ("AimxHead", _lib.Head), ("AimxHeadGrad", _lib.HeadGrad), ("AimxAdamTensor", _lib.AdamTensor),
+                      ("AimxAdamHyper", _lib.AdamHyper)):
+        body = re.search(r"typedef struct (?:%s )?\{([^{}]*)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = re.findall(r"\**\s*(\w+)\s*(?:\[[^\]]*\])?\s*[;,]", body)
         assert names == [f[0] for f in py._fields_], (cname, names)
