@@ -57,6 +57,9 @@ def load_host():
     lib.aimx_store_create.restype = c_i32
     lib.aimx_store_create.argtypes = [c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_i32, c_ptr, c_i32, c_i32,
                                       ctypes.POINTER(c_ptr)]
+    lib.aimx_store_create_hops.restype = c_i32
+    lib.aimx_store_create_hops.argtypes = [c_i64, c_ptr, c_ptr, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i32, c_ptr,
+                                           ctypes.POINTER(c_ptr)]
     lib.aimx_store_destroy.argtypes = [c_ptr]
     lib.aimx_store_num_molecules.restype = c_i64
     lib.aimx_store_num_molecules.argtypes = [c_ptr]
@@ -142,6 +145,42 @@ class HostStore:
         feats = (np.concatenate([np.asarray(m[2]).reshape(m[0], -1) for m in mols])
                  if mols else np.zeros((0, len(adata.FEATURE_KEYS)), np.int32))
         return cls([m[0] for m in mols], [m[1] for m in mols], feats, targets, total_charge, precompute_hops, threads)
+
+    @classmethod
+    def from_handle(cls, handle, n_feat, n_tasks):
+        """Adopt a native store created elsewhere (e.g. aimx_h5_read_store); destroyed with this object."""
+        lib = load_host()
+        s = cls.__new__(cls)
+        s._lib, s._h = lib, handle
+        s.n_feat, s.n_tasks = int(n_feat), int(n_tasks)
+        s.n_mols = int(lib.aimx_store_num_molecules(handle))
+        s.n_atoms = np.array([lib.aimx_store_num_atoms(handle, m) for m in range(s.n_mols)], np.int64)
+        return s
+
+    @classmethod
+    def from_hop_lists(cls, n_atoms, hops_per_mol, feats, targets=None, total_charge=None):
+        """A store from precomputed hop arrays (the reference's multi_hop_edges: per molecule a list
+        of int [2, E_h] arrays, one per hop) instead of bonds."""
+        lib = load_host()
+        n_atoms = np.asarray(n_atoms, np.int64)
+        n_mols = n_atoms.shape[0]
+        H = len(hops_per_mol[0]) if n_mols else 1
+        lens = np.array([[np.asarray(e).reshape(2, -1).shape[1] for e in hops] for hops in hops_per_mol],
+                        np.int64).reshape(n_mols, H)
+        hop_ptr = np.concatenate([[0], np.cumsum(lens.reshape(-1))]).astype(np.int64)
+        pairs = (np.concatenate([np.asarray(e).reshape(2, -1).T for hops in hops_per_mol for e in hops])
+                 if n_mols else np.zeros((0, 2)))
+        pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        atom_ptr = np.concatenate([[0], np.cumsum(n_atoms)]).astype(np.int64)
+        feats = np.ascontiguousarray(feats, np.int32)
+        n_feat = feats.shape[1] if feats.ndim == 2 else len(adata.FEATURE_KEYS)
+        tg = None if targets is None else np.ascontiguousarray(np.asarray(targets, np.float32).reshape(n_mols, -1))
+        tc = None if total_charge is None else np.ascontiguousarray(total_charge, np.float32)
+        h = c_ptr()
+        _check(lib.aimx_store_create_hops(n_mols, atom_ptr.ctypes.data, _p(feats), n_feat, H, hop_ptr.ctypes.data,
+                                          _p(pairs), _p(tg), 0 if tg is None else tg.shape[1], _p(tc),
+                                          ctypes.byref(h)), "store_create_hops")
+        return cls.from_handle(h, n_feat, 0 if tg is None else tg.shape[1])
 
     def _init(self, lib, n_mols, bonds, feats, targets, total_charge, precompute_hops, threads):
         self._lib = lib
@@ -240,7 +279,9 @@ class HostCollator:
 class BatchFeeder:
     """Background native collation + async H2D copies, `depth` batches ahead of the consumer.
 
-    batches: iterable of molecule-index arrays. Yields DeviceBatch objects whose copy has been
+    batches: iterable of molecule-index arrays into `store`, or of (store, index array) pairs (a
+    stream whose chunks are separate stores, aimx.h5.HDF5MolecularStream.batches; `store` may then
+    be None). Yields DeviceBatch objects whose copy has been
     enqueued on the feeder's copy stream; the consumer's current stream waits on it (event), so
     the step never reads a half-copied batch and never blocks the host on the copy. Padding to
     static shapes (n_max/e_max/pad_mols) makes the batches replayable by one captured HIP graph.
@@ -260,10 +301,11 @@ class BatchFeeder:
 
     def _run(self):
         try:
-            for idx in self._it:
+            for item in self._it:
                 if self._stop:
                     break
-                blob, layout, gr, nr, real = self.collator.collate_blob(self.store, idx, True, *self.pad)
+                store, idx = item if isinstance(item, tuple) else (self.store, item)
+                blob, layout, gr, nr, real = self.collator.collate_blob(store, idx, True, *self.pad)
                 with torch.cuda.stream(self.stream):
                     dev = blob.to(self.device, non_blocking=True)
                     ev = torch.cuda.Event()

@@ -306,6 +306,56 @@ int aimx_store_create(int64_t n_mols, const int64_t* atom_ptr, const int64_t* bo
   return AIMX_HOST_OK;
 }
 
+int aimx_store_create_hops(int64_t n_mols, const int64_t* atom_ptr, const int32_t* feats, int32_t n_feat,
+                           int32_t n_hops, const int64_t* hop_ptr, const int32_t* pairs, const float* targets,
+                           int32_t n_tasks, const float* total_charge, aimx_mol_store** out) {
+  if (!out || n_mols < 0 || !atom_ptr || n_feat < 0 || n_feat > 8 || n_tasks < 0 || n_hops < 1 || !hop_ptr)
+    return AIMX_HOST_EARG;
+  *out = nullptr;
+  if (atom_ptr[0] != 0 || hop_ptr[0] != 0) return AIMX_HOST_EARG;
+  const int64_t NH = n_mols * n_hops;
+  for (int64_t m = 0; m < n_mols; ++m) {
+    const int64_t na = atom_ptr[m + 1] - atom_ptr[m];
+    if (na < 0 || na > 65535) return AIMX_HOST_EARG;
+  }
+  for (int64_t k = 0; k < NH; ++k)
+    if (hop_ptr[k + 1] < hop_ptr[k]) return AIMX_HOST_EARG;
+  const int64_t NA = atom_ptr[n_mols], NP = hop_ptr[NH];
+  if ((NP > 0 && !pairs) || (NA > 0 && n_feat > 0 && !feats)) return AIMX_HOST_EARG;
+  for (int64_t m = 0; m < n_mols; ++m) {  // local indices in range (the stored form is uint16)
+    const int64_t na = atom_ptr[m + 1] - atom_ptr[m];
+    for (int64_t q = hop_ptr[m * n_hops]; q < hop_ptr[(m + 1) * n_hops]; ++q)
+      if (pairs[2 * q] < 0 || pairs[2 * q] >= na || pairs[2 * q + 1] < 0 || pairs[2 * q + 1] >= na)
+        return AIMX_HOST_EARG;
+  }
+  aimx_mol_store* s = nullptr;
+  try {
+    s = new aimx_mol_store();
+    s->n_mols = n_mols;
+    s->n_feat = n_feat;
+    s->n_tasks = n_tasks;
+    s->atom_ptr.assign(atom_ptr, atom_ptr + n_mols + 1);
+    s->bond_ptr.assign(n_mols + 1, 0);
+    if (NA && n_feat) s->feats.assign(feats, feats + NA * n_feat);
+    s->targets.assign(size_t(n_mols) * n_tasks, 0.f);
+    if (targets && n_tasks) std::memcpy(s->targets.data(), targets, sizeof(float) * s->targets.size());
+    s->charge.assign(n_mols, 0.f);
+    if (total_charge) std::memcpy(s->charge.data(), total_charge, sizeof(float) * n_mols);
+    s->cached_hops = n_hops;
+    s->hop_len.resize(size_t(NH));
+    for (int64_t k = 0; k < NH; ++k) s->hop_len[k] = int32_t(hop_ptr[k + 1] - hop_ptr[k]);
+    s->pair_ptr.assign(n_mols + 1, 0);
+    for (int64_t m = 0; m < n_mols; ++m) s->pair_ptr[m + 1] = hop_ptr[(m + 1) * n_hops];
+    s->pairs.resize(size_t(2 * NP));
+    for (int64_t q = 0; q < 2 * NP; ++q) s->pairs[q] = uint16_t(pairs[q]);
+  } catch (const std::bad_alloc&) {
+    delete s;
+    return AIMX_HOST_ENOMEM;
+  }
+  *out = s;
+  return AIMX_HOST_OK;
+}
+
 void aimx_store_destroy(aimx_mol_store* store) { delete store; }
 
 int64_t aimx_store_num_molecules(const aimx_mol_store* s) { return s ? s->n_mols : AIMX_HOST_EARG; }

@@ -133,14 +133,17 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
                                               float* __restrict__ scores, Slot<LDS> sa, float* red) {
   constexpr int NW = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // 1) scores s[h,i] = (x_i . W_h + b_h) / tau  (a wave per atom, lanes over channels)
+  // 1) scores, centred on the first atom (fp64 dots; the softmax is shift invariant and the bias
+  //    cancels: d_hj = (x_j - x_0) . W_h / tau, see attn_fwd_rows), a wave per atom, lanes over
+  //    channels; d is kept in LDS or, for the largest molecules, in the scores array itself
+  const int64_t i0 = gperm[b];
   for (int j = w; j < n; j += NW) {
     const int64_t i = gperm[b + j];
-    double acc[kMaxH];  // fp64 score sums: see attn_fwd_rows
+    double acc[kMaxH];
 #pragma unroll
     for (int h = 0; h < kMaxH; ++h) acc[h] = 0.0;
     for (int64_t c = lane; c < C; c += 64) {
-      const double xv = x[i * ldx + c];
+      const double xv = (double)x[i * ldx + c] - (double)x[i0 * ldx + c];
 #pragma unroll
       for (int h = 0; h < kMaxH; ++h)
         if (h < H) acc[h] += xv * (double)W[h * C + c];
@@ -148,18 +151,24 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
 #pragma unroll
     for (int h = 0; h < kMaxH; ++h) {
       if (h < H) {
-        const float s = (float)((wave_sum_d(acc[h]) + (double)bias[h]) / (double)tau);
+        const float d = (float)(wave_sum_d(acc[h]) / (double)tau);
         if (lane == 0) {
-          scores[h * N + i] = s;
-          if (LDS) sa.at(h, j, i) = s;
+          if (LDS)
+            sa.at(h, j, i) = d;
+          else
+            scores[h * N + i] = d;
         }
       }
     }
   }
   if (!LDS) __threadfence();
   __syncthreads();
-  // 2) per-head softmax over the molecule's atoms (torch_scatter.scatter_softmax)
+  // 2) per-head softmax over the molecule's atoms (torch_scatter.scatter_softmax); the saved
+  //    scores are s_0 + d with s_0 = (x_0 . W_h + b_h) / tau
   for (int h = 0; h < H; ++h) {
+    double s0 = 0.0;
+    for (int64_t c = lane; c < C; c += 64) s0 += (double)x[i0 * ldx + c] * (double)W[h * C + c];
+    s0 = (wave_sum_d(s0) + (double)bias[h]) / (double)tau;
     float mx = -INFINITY;
     for (int j = threadIdx.x; j < n; j += NT) mx = fmaxf(mx, LDS ? sa.at(h, j, 0) : scores[h * N + gperm[b + j]]);
     mx = block_reduce_max<NW>(mx, red);
@@ -168,13 +177,15 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
     sum = block_reduce_sum<NW>(sum, red);
     for (int j = threadIdx.x; j < n; j += NT) {
       const int64_t i = gperm[b + j];
-      const float a = expf((LDS ? sa.at(h, j, i) : scores[h * N + i]) - mx) / sum;
+      const float d = LDS ? sa.at(h, j, i) : scores[h * N + i];
+      const float a = expf(d - mx) / sum;
       attn[h * N + i] = a;
+      scores[h * N + i] = (float)(s0 + (double)d);
       if (LDS) sa.at(h, j, i) = a;
     }
+    if (!LDS) __threadfence();
+    __syncthreads();  // this head's d values are consumed before the next head's reads start
   }
-  if (!LDS) __threadfence();
-  __syncthreads();
   // 3) pooled[g,c] = (sum_h sum_i a[h,i] x[i,c]) / H  (pooling.py:150-161: per-head sums, head mean)
   for (int64_t c = threadIdx.x; c < C; c += NT) {
     float acc[kMaxH];
@@ -703,22 +714,23 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_bwd(
 
 // Deterministic reduction of the per-molecule partials: column t of [dW (H*C) | db (H) | dtau]
 // is summed over molecules by lane t % 64 of a 16-wave block (coalesced rows of the partial slab),
-// wave k taking molecules g = k, k+16, ... in fp64 (16 loads in flight), then the 16 wave sums in
+// wave k taking molecules g = k, k+16, ... in fp64 (32 loads in flight), then the 16 wave sums in
 // order.
 constexpr int kRedWaves = 16;
 
 template <typename T>
 __device__ __forceinline__ double sum_column(const T* __restrict__ src, int64_t stride, int64_t G, int w) {
+  constexpr int kB = 32;  // loads in flight per lane: G <= 512 molecules in one round trip
   double s = 0.0;
-  for (int64_t g0 = w; g0 < G; g0 += 16 * kRedWaves) {
-    T v[16];
+  for (int64_t g0 = w; g0 < G; g0 += kB * kRedWaves) {
+    T v[kB];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < kB; ++k) {
       const int64_t g = g0 + (int64_t)k * kRedWaves;
       v[k] = g < G ? src[g * stride] : T(0);
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s += (double)v[k];
+    for (int k = 0; k < kB; ++k) s += (double)v[k];
   }
   return s;
 }

@@ -63,6 +63,14 @@ int aimx_store_create(int64_t n_mols, const int64_t* atom_ptr, const int64_t* bo
                       const int32_t* bonds, const int32_t* feats, int32_t n_feat,
                       const float* targets, int32_t n_tasks, const float* total_charge,
                       int32_t precompute_hops, int32_t n_threads, aimx_mol_store** out);
+/* A store from precomputed hop pair lists (the reference's stored multi_hop_edges,
+ * features.py:318-334 / molecular.py:307-309, e.g. decoded from an HDF5 stream by
+ * libaimx_h5.so): molecule m's hop h pairs are pairs[hop_ptr[m*n_hops+h] .. hop_ptr[m*n_hops+h+1])
+ * as (u, w) rows of local atom indices, in the reference's stored order. hop_ptr has
+ * n_mols*n_hops+1 entries starting at 0; collate with the same max_hops = n_hops. */
+int aimx_store_create_hops(int64_t n_mols, const int64_t* atom_ptr, const int32_t* feats, int32_t n_feat,
+                           int32_t n_hops, const int64_t* hop_ptr, const int32_t* pairs, const float* targets,
+                           int32_t n_tasks, const float* total_charge, aimx_mol_store** out);
 void aimx_store_destroy(aimx_mol_store* store);
 int64_t aimx_store_num_molecules(const aimx_mol_store* store);
 int64_t aimx_store_num_atoms(const aimx_mol_store* store, int64_t mol);
