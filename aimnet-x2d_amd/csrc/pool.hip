@@ -712,59 +712,57 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_bwd(
                              Slot<false, double, kCapB>{ds_glob + (int64_t)H * N, N}, red);
 }
 
-// Deterministic reduction of the per-molecule partials: column t of [dW (H*C) | db (H) | dtau]
-// is summed over molecules by lane t % 64 of a 16-wave block (coalesced rows of the partial slab),
-// wave k taking molecules g = k, k+16, ... in fp64 (32 loads in flight), then the 16 wave sums in
-// order.
-constexpr int kRedWaves = 16;
+// Deterministic reduction of the per-molecule partials, column t of [dW (H*C) | db (H) | dtau],
+// in two launches so that enough CUs share the reads (one 64-column block per CU was bound by the
+// CU's outstanding-request limit at ~10 GB/s): k_attn_reduce1 sums slices of kRedSlice molecules
+// (a 64-column x 64-molecule tile per workgroup: 4 waves x 16 molecules, 16 loads in flight per
+// lane, then the 4 wave sums in order) into a slice slab; k_attn_reduce2 sums the slices in order.
+constexpr int kRedSlice = 64;
 
-template <typename T>
-__device__ __forceinline__ double sum_column(const T* __restrict__ src, int64_t stride, int64_t G, int w) {
-  constexpr int kB = 32;  // loads in flight per lane: G <= 512 molecules in one round trip
-  double s = 0.0;
-  for (int64_t g0 = w; g0 < G; g0 += kB * kRedWaves) {
-    T v[kB];
-#pragma unroll
-    for (int k = 0; k < kB; ++k) {
-      const int64_t g = g0 + (int64_t)k * kRedWaves;
-      v[k] = g < G ? src[g * stride] : T(0);
-    }
-#pragma unroll
-    for (int k = 0; k < kB; ++k) s += (double)v[k];
-  }
-  return s;
+__device__ __forceinline__ double partial_at(int64_t t, int64_t g, int64_t nw, int H, const float* __restrict__ dW_part,
+                                             const double* __restrict__ db_part,
+                                             const double* __restrict__ dtau_part) {
+  if (t < nw) return (double)dW_part[g * nw + t];
+  if (t < nw + H) return db_part[g * H + (t - nw)];
+  return dtau_part[g];
 }
 
-__global__ __launch_bounds__(kRedWaves * 64) void k_attn_reduce(int64_t G, int H, int64_t C,
-                                                                const float* __restrict__ dW_part,
-                                                                const double* __restrict__ db_part,
-                                                                const double* __restrict__ dtau_part,
-                                                                float* __restrict__ dW, float* __restrict__ db,
-                                                                float* __restrict__ dtau) {
-  __shared__ double red[kRedWaves][64];
-  const int64_t nw = (int64_t)H * C;
+__global__ __launch_bounds__(256) void k_attn_reduce1(int64_t G, int H, int64_t C, const float* __restrict__ dW_part,
+                                                      const double* __restrict__ db_part,
+                                                      const double* __restrict__ dtau_part, double* __restrict__ slab) {
+  __shared__ double red[4][64];
+  const int64_t nw = (int64_t)H * C, tot = nw + H + 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t t = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t g0 = (int64_t)blockIdx.y * kRedSlice + w * (kRedSlice / 4);
   double s = 0.0;
-  if (t < nw)
-    s = sum_column(dW_part + t, nw, G, w);
-  else if (t < nw + H)
-    s = sum_column(db_part + (t - nw), H, G, w);
-  else if (t == nw + H)
-    s = sum_column(dtau_part, 1, G, w);
+  if (t < tot) {
+    double v[kRedSlice / 4];
+#pragma unroll
+    for (int k = 0; k < kRedSlice / 4; ++k)
+      v[k] = g0 + k < G ? partial_at(t, g0 + k, nw, H, dW_part, db_part, dtau_part) : 0.0;
+#pragma unroll
+    for (int k = 0; k < kRedSlice / 4; ++k) s += v[k];
+  }
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && t <= nw + H) {
-    double tot = 0.0;
-#pragma unroll
-    for (int k = 0; k < kRedWaves; ++k) tot += red[k][lane];
-    if (t < nw)
-      dW[t] = (float)tot;
-    else if (t < nw + H)
-      db[t - nw] = (float)tot;
-    else
-      *dtau = (float)tot;
-  }
+  if (w == 0 && t < tot) slab[(int64_t)blockIdx.y * tot + t] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ __launch_bounds__(256) void k_attn_reduce2(int64_t n_slices, int H, int64_t C, const double* __restrict__ slab,
+                                                      float* __restrict__ dW, float* __restrict__ db,
+                                                      float* __restrict__ dtau) {
+  const int64_t nw = (int64_t)H * C, tot = nw + H + 1;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= tot) return;
+  double s = 0.0;
+  for (int64_t k = 0; k < n_slices; ++k) s += slab[k * tot + t];
+  if (t < nw)
+    dW[t] = (float)s;
+  else if (t < nw + H)
+    db[t - nw] = (float)s;
+  else
+    *dtau = (float)s;
 }
 
 // kind: 0 mean, 1 max, 2 sum
@@ -862,7 +860,8 @@ void launch_attn_bwd(int H, unsigned G, hipStream_t st, const float* x, int64_t 
 using namespace aimx;
 
 extern "C" size_t aimx_attn_pool_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t G) {
-  return sizeof(float) * (size_t)(G * H * C + 32) + sizeof(double) * (size_t)(G * H + G + 2 * H * N + 24);
+  return sizeof(float) * (size_t)(G * H * C + 32) +
+         sizeof(double) * (size_t)(G * H + G + 2 * H * N + cdiv(G, kRedSlice) * (H * C + H + 1) + 40);
 }
 
 extern "C" int aimx_attn_pool_forward(const float* x, int64_t ldx, int64_t N, int64_t C, const float* W, const float* b,
@@ -894,6 +893,7 @@ extern "C" int aimx_attn_pool_backward(const float* x, int64_t ldx, int64_t N, i
   double* db_part = (double*)(((uintptr_t)(dW_part + G * H * C) + 63) & ~(uintptr_t)63);
   double* dtau_part = db_part + G * H;
   double* ds_glob = (double*)(((uintptr_t)(dtau_part + G) + 63) & ~(uintptr_t)63);
+  double* slab = (double*)(((uintptr_t)(ds_glob + 2 * H * N) + 63) & ~(uintptr_t)63);
   if (G > 0) {
     switch (pool_slices(C)) {
       case 1:
@@ -910,9 +910,12 @@ extern "C" int aimx_attn_pool_backward(const float* x, int64_t ldx, int64_t N, i
     }
     AIMX_CHECK_LAUNCH();
   }
-  const int64_t tot = H * C + H + 1;
-  hipLaunchKernelGGL(k_attn_reduce, dim3((unsigned)cdiv(tot, 64)), dim3(kRedWaves * 64), 0, s, G, (int)H, C, dW_part,
-                     db_part, dtau_part, dW, db, dtau);
+  const int64_t tot = H * C + H + 1, n_slices = std::max<int64_t>(1, cdiv(G, kRedSlice));
+  hipLaunchKernelGGL(k_attn_reduce1, dim3((unsigned)cdiv(tot, 64), (unsigned)n_slices), dim3(256), 0, s, G, (int)H, C,
+                     dW_part, db_part, dtau_part, slab);
+  AIMX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_attn_reduce2, dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, s, n_slices, (int)H, C, slab, dW,
+                     db, dtau);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }

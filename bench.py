@@ -115,6 +115,44 @@ def native_feeder(cfg, seed, device, threads, pad):
                                  n_max=n_max, e_max=e_max, pad_mols=PAD_MOLS if pad else 0))
 
 
+def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None):
+    """Endless BatchFeeder over an HDF5 molecule stream in the reference's dataset format
+    (features.py:381-431 / molecular.py:102-329): a synthetic file of n_mols molecules (made once
+    on this host by rank 0), this rank's equal shard read in chunks by the C++ reader (HDF5 C
+    library + non-executing record decoder) on a prefetch thread, collated by the C++ batch
+    builder and copied host->device by BatchFeeder (aimx/h5.py, aimx/feed.py)."""
+    from aimx import feed, h5
+    path = path or os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                f"aimx_stream_{cfg['source']}_{cfg['hops']}h_{cfg['tasks']}t_{n_mols}.h5")
+    if rank == 0 and not os.path.exists(path):
+        t0 = time.perf_counter()
+        tmp = path + f".part{os.getpid()}"
+        h5.make_synthetic_stream(tmp, n_mols, cfg["source"], cfg["hops"], cfg["tasks"], seed=0,
+                                 workers=min(16, os.cpu_count() or 4))
+        os.replace(tmp, path)
+        print(f"bench: wrote {n_mols}-molecule stream {path} in {time.perf_counter() - t0:.1f} s", file=sys.stderr)
+    if world > 1:
+        dist.barrier()
+    stream = h5.HDF5MolecularStream(path, shuffle=True, ddp_enabled=world > 1, rank=rank, world_size=world,
+                                    n_hops=cfg["hops"], n_tasks=cfg["tasks"], threads=threads)
+    B = cfg["batch"]
+    n_max = e_max = 0
+    if pad:  # static capacity from the first chunk's batches + margin (an overflow raises HostError)
+        store, _ = stream.file.read_store(stream.positions(0)[:16384], cfg["hops"], cfg["tasks"], threads)
+        probe = feed.HostCollator(cfg["hops"], threads)
+        rng = np.random.default_rng(rank)
+        sizes = np.array([probe.plan(store, rng.integers(0, len(store), B)) for _ in range(256)])
+        n_max, e_max = int(sizes[:, 0].max() * 1.08) + 64, int(sizes[:, 1].max() * 1.08) + 256
+
+    def batches():
+        epoch = 0
+        while True:
+            yield from stream.batches(B, chunk_size=16384, epoch_seed=epoch)
+            epoch += 1
+    return iter(feed.BatchFeeder(None, batches(), cfg["hops"], device, depth=4, threads=threads,
+                                 n_max=n_max, e_max=e_max, pad_mols=PAD_MOLS if pad else 0))
+
+
 def build_model(cfg, device):
     from models import GNN
     m = GNN(FS, cfg["hidden"], cfg["tasks"], num_shells=cfg["hops"], use_partial_charges=cfg["pc"])
@@ -214,10 +252,14 @@ def main():
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="capture the whole train step in a HIP graph (static padded batches; default)")
     ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager execution")
-    ap.add_argument("--feed", default="resident", choices=["resident", "native"],
+    ap.add_argument("--feed", default="resident", choices=["resident", "native", "stream"],
                     help="resident: a pool of batches already in HBM (the metric's `value`); native: every "
                          "step's batch is collated by the C++ batch builder from the molecule store and "
-                         "copied host->device inside the timed region (PCIe-inclusive rate)")
+                         "copied host->device inside the timed region (PCIe-inclusive rate); stream: the same "
+                         "from an HDF5 file in the reference's dataset format, read and decoded in C++ on a "
+                         "prefetch thread (this rank's equal shard)")
+    ap.add_argument("--stream-mols", type=int, default=200_000, help="molecules in the --feed stream file")
+    ap.add_argument("--stream-path", default=None, help="--feed stream file (default: generated under $TMPDIR)")
     ap.add_argument("--feed-threads", type=int, default=4)
     ap.add_argument("--ddp-world1", action="store_true",
                     help="A/B of the data-parallel step on one GPU: a world-size-1 RCCL group with the bucket "
@@ -245,6 +287,10 @@ def main():
     feeder = None
     if args.feed == "native":
         feeder = native_feeder(cfg, 1234 + rank, device, args.feed_threads, args.graph)
+        batches = [next(feeder)]
+    elif args.feed == "stream":
+        feeder = stream_feeder(cfg, rank, world, device, args.feed_threads, args.graph, args.stream_mols,
+                               args.stream_path)
         batches = [next(feeder)]
     else:
         batches = make_batches(cfg, args.pool, 1234 + rank, device, pad=args.graph)
@@ -346,7 +392,10 @@ def main():
                        + (", HIP-graph replay of padded static batches (+8 padding molecules, excluded"
                           " from the loss)" if args.graph else ", eager"),
                        "feed": ("resident pool of %d batches in HBM" % args.pool if feeder is None else
-                                "native C++ collate + pinned H2D per step (PCIe-inclusive; not the metric value)"),
+                                "native C++ collate + pinned H2D per step (PCIe-inclusive; not the metric value)"
+                                if args.feed == "native" else
+                                f"HDF5 stream of {args.stream_mols} molecules (reference format), C++ read + "
+                                "decode + collate + pinned H2D per step (PCIe-inclusive; not the metric value)"),
                        "global_batch": cfg["batch"] * world, "per_gpu_batch": cfg["batch"],
                        "mean_atoms_per_batch": round(atoms, 1), "mean_edges_per_batch": round(edges, 1),
                        "parallelism": f"dp{world}"},
