@@ -234,7 +234,20 @@ def require_device(*tensors):
             raise AimxError("aimx: tensors must live on the HIP device (MI355X); there is no CPU path")
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None):
+    """The current HIP stream of `device` as an integer handle (hot path: one C call, no Stream
+    object; torch.cuda.current_stream builds a Python Stream per call)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

@@ -39,6 +39,53 @@ class FusedAdam(torch.optim.Optimizer):
         self._lr_host = None
         self._norm = None
         self._ws = None
+        self._table_key = None
+        self._arr = None
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._table_key = None  # state tensors replaced: rebuild the table on the next step
+
+    def _build_table(self):
+        """AdamTensor table of the parameters that have a gradient (torch.optim.Adam skips the
+        others), with their state tensors and per-parameter step slots."""
+        rows = []
+        dev = None
+        slot = -1
+        for gi, group in enumerate(self.param_groups):
+            for p in group["params"]:
+                slot += 1
+                if p.grad is None:
+                    continue
+                g = p.grad
+                if not p.is_cuda or p.dtype != torch.float32 or g.dtype != torch.float32:
+                    raise AimxError("FusedAdam: fp32 parameters on the HIP device only (no CPU path)")
+                if not (p.is_contiguous() and g.is_contiguous()):
+                    raise AimxError("FusedAdam: parameters and gradients must be contiguous")
+                st = self.state[p]
+                if "exp_avg" not in st:
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                dev = p.device
+                rows.append((p, g, st["exp_avg"], st["exp_avg_sq"], gi, slot))
+        self._rows, self._dev = rows, dev
+        if not rows:
+            self._arr = None
+            return
+        self._device_state(dev)
+        for p, *_, k in rows:
+            st, view = self.state[p], self._step_t[k]  # 0-dim view of this parameter's device counter
+            old = st.get("step")
+            if old is not None and (not torch.is_tensor(old) or old.data_ptr() != view.data_ptr()):
+                view.fill_(float(old))  # a step count from load_state_dict
+            st["step"] = view
+        arr = (AdamTensor * len(rows))()
+        for i, (p, g, m, v, gi, k) in enumerate(rows):
+            arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
+            arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
+            arr[i].numel, arr[i].group, arr[i].step_slot = p.numel(), gi, k
+        self._arr = arr
+        self._wsb = _lib.load().aimx_fused_adam_workspace_bytes(arr, len(rows))
 
     def _shared_hyper(self):
         g0 = self.param_groups[0]
@@ -78,37 +125,24 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         hyper_g = self._shared_hyper()
-        rows = []
-        dev = None
-        slot = -1
-        for gi, group in enumerate(self.param_groups):
+        # the tensor table is rebuilt only when the set of stepped parameters or a gradient's
+        # address changed (steady state: the caching allocator hands autograd the same blocks)
+        key = []
+        for group in self.param_groups:
             for p in group["params"]:
-                slot += 1
-                if p.grad is None:
-                    continue
                 g = p.grad
-                if not p.is_cuda or p.dtype != torch.float32 or g.dtype != torch.float32:
-                    raise AimxError("FusedAdam: fp32 parameters on the HIP device only (no CPU path)")
-                if not (p.is_contiguous() and g.is_contiguous()):
-                    raise AimxError("FusedAdam: parameters and gradients must be contiguous")
-                st = self.state[p]
-                if not st:
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                dev = p.device
-                rows.append((p, g, st["exp_avg"], st["exp_avg_sq"], gi, slot))
-        if not rows:
+                key.append(p.data_ptr())
+                key.append(0 if g is None else g.data_ptr())
+        key = tuple(key)
+        if key != self._table_key:
+            self._build_table()
+            self._table_key = key
+        if self._arr is None:
             return loss
-        self._device_state(dev)
-        for p, *_, k in rows:
-            self.state[p]["step"] = self._step_t[k]  # 0-dim view of this parameter's device counter
-        arr = (AdamTensor * len(rows))()
-        for i, (p, g, m, v, gi, k) in enumerate(rows):
-            arr[i].param, arr[i].grad = p.data_ptr(), g.data_ptr()
-            arr[i].exp_avg, arr[i].exp_avg_sq = m.data_ptr(), v.data_ptr()
-            arr[i].numel, arr[i].group, arr[i].step_slot = p.numel(), gi, k
+        rows, arr, dev = self._rows, self._arr, self._dev
+        self._device_state(dev)  # group lr changes (schedulers)
         lib = _lib.load()
-        wsb = lib.aimx_fused_adam_workspace_bytes(arr, len(rows))
+        wsb = self._wsb
         if self._ws is None or self._ws.numel() * 8 < wsb:
             self._ws = torch.empty((wsb + 7) // 8, dtype=torch.float64, device=dev)
         h = AdamHyper()

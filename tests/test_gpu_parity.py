@@ -248,6 +248,46 @@ def test_gemm_layouts(M, N, K, layout):
     assert err < 2e-6, err
 
 
+@pytest.mark.parametrize("M,N,K,layout,off", [(2049, 153, 153, "NT", 1), (2049, 307, 153, "NN", 3),
+                                               (153, 307, 4099, "TN", 2), (1027, 77, 301, "TT", 1),
+                                               (5, 3, 7, "NT", 3)])
+def test_gemm_unaligned_rows_and_bases(M, N, K, layout, off):
+    """16-byte staging at any float alignment: operands are views starting `off` floats into their
+    buffers with odd row strides (the c4/c5 widths D = 153 / 307), so rows, bases and the extent's
+    last float4 are all misaligned."""
+    import ctypes
+    from aimx import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K)
+    rA, cA = (M, K) if layout[0] == "N" else (K, M)
+    rB, cB = (K, N) if layout[1] == "N" else (N, K)
+    la, lb = cA + 3, cB + 1
+    bufA = torch.randn(off + rA * la, generator=g)
+    bufB = torch.randn(off + rB * lb, generator=g)
+    A = bufA[off:].view(rA, la)[:, :cA]
+    B = bufB[off:].view(rB, lb)[:, :cB]
+    dA, dB = bufA.to(DEV), bufB.to(DEV)
+    C = torch.zeros(M, N, device=DEV)
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.A = dA.data_ptr() + 4 * off
+    a.sam, a.sak = (la, 1) if layout[0] == "N" else (1, la)
+    a.B = dB.data_ptr() + 4 * off
+    a.sbk, a.sbn = (lb, 1) if layout[1] == "N" else (1, lb)
+    a.C, a.ldc = C.data_ptr(), N
+    a.act, a.dact_kind = -1, -1
+    a.counters, a.n_counters = _lib.counters(DEV).data_ptr(), _lib.N_COUNTERS
+    wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
+    ws = torch.empty(max(wsb // 4, 1) + 64 * 1024, device=DEV)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    assert lib.aimx_gemm(ctypes.byref(a), torch.cuda.current_stream().cuda_stream) == 0
+    Am = A if layout[0] == "N" else A.t()
+    Bm = B if layout[1] == "N" else B.t()
+    ref = Am.double() @ Bm.double()
+    err = (C.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+
+
 @pytest.mark.parametrize("nonempty", [(True, False, False), (False, False, False), (True, True, False),
                                       (False, True, False), (True, False, True)])
 def test_gemm_empty_hop_chunk_trimming(nonempty):
