@@ -200,18 +200,224 @@ def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launch
                 traffic = rec.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    bwd = hop_bwd_roofline(plan, n, d, hops, device)
     del plan, x
     torch.cuda.empty_cache()
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": ("profiles/hop_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same "
+                               "command (bench.py --roofline-only), per launch, gfx950 corrections applied; not "
+                               "measured inside this run") if traffic is not None else None,
+            "bwd": bwd,
             "kernel": "k_gather_sum (hop fwd)", "atoms": n, "edges": e, "D": d, "hops": hops,
             "algorithmic_bytes_per_launch": alg_bytes, "ms_per_launch": round(ms, 4)}
 
 
-def cpu_baseline(cfg, seconds=10.0, max_steps=40):
-    """Oracle CPU restatement of the reference train step (fwd+bwd+clip+Adam, dropout on)."""
-    from oracle import model as om
+def graph_time_us(fn, launches=20, replays=5):
+    """Device time per launch of fn(): `launches` back-to-back launches captured in one HIP graph on
+    a side stream, replayed `replays` times between HIP events recorded on that same stream (eager
+    Python launches of a ~10 us kernel would time the host instead). Includes the ~1.5 us boundary
+    between dependent kernels."""
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(launches):
+            fn()
+    with torch.cuda.stream(s):
+        g.replay()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record(s)
+        for _ in range(replays):
+            g.replay()
+        t1.record(s)
+    t1.synchronize()
+    us = t0.elapsed_time(t1) / (replays * launches) * 1e3
+    del g
+    return us
+
+
+def _bw(name, bytes_, us, **kw):
+    gbs = bytes_ / (us * 1e-6) / 1e9
+    return {"kernel": name, "bound": "hbm", "algorithmic_bytes": int(bytes_), "us_per_launch": round(us, 2),
+            "achieved": round(gbs, 1), "unit": "GB/s", "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), **kw}
+
+
+def hop_in_step(batch, hops, hidden, device):
+    """The hop forward and backward at the config's own batch size (what one train step runs per
+    layer), timed by graph_time_us through the C ABI. Backward bytes: the gathered gradient rows
+    (every target row is < N for reference inputs, layers.py:154, so chunk 0 only), the src-keyed
+    CSR and the written dx — the minimal traffic, not SURVEY §8d's all-chunks upper bound."""
+    from aimx import _lib
+    from aimx.plan import GraphPlan
+    lib = _lib.load()
+    P = _lib.ptr
+    n, d = batch.num_atoms, int(0.3 * hidden)
+    plan = GraphPlan(n, hops, edges=batch.edges, batch=batch.batch, num_graphs=batch.num_graphs)
+    e = plan.E
+    x = torch.randn(n, d, device=device)
+    out = torch.empty(hops * n, d, device=device)
+    g = torch.randn(hops * n, d, device=device)
+    dx = torch.empty(n, d, device=device)
+    seg, seg_st = plan.row_seg()
+    torch.cuda.synchronize()
+
+    def fwd():
+        assert lib.aimx_segment_gather_sum(P(x), d, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n, P(out), d,
+                                           n, n * d, None, 0, None, 0, seg, seg_st, _lib.stream_ptr(device)) == 0
+
+    def bwd():
+        assert lib.aimx_segment_gather_sum(P(g), d, 0, 0, d, P(plan.bwd.rowptr), P(plan.bwd.col), n, P(dx), d, 0, 0,
+                                           None, 0, None, 0, seg, seg_st, _lib.stream_ptr(device)) == 0
+    tf, tb = graph_time_us(fwd), graph_time_us(bwd)
+    bf = 4 * (n * d + e + (hops * n + 1) + hops * n * d)
+    bb = 4 * (n * d + e + (n + 1) + n * d)
+    return {"atoms": n, "edges": e, "D": d, "hops": hops,
+            "fwd": _bw("k_gather_sum (hop fwd)", bf, tf), "bwd": _bw("k_gather_sum (hop bwd)", bb, tb)}
+
+
+def hop_bwd_roofline(plan, n, d, hops, device, launches=20):
+    """Hop backward at the roofline size (HIP events on the launch stream, like hop_roofline)."""
+    from aimx import _lib
+    lib = _lib.load()
+    P = _lib.ptr
+    g = torch.randn(hops * n, d, device=device)
+    dx = torch.empty(n, d, device=device)
+    seg, seg_st = plan.row_seg()
+    s = _lib.stream_ptr(device)
+
+    def bwd():
+        assert lib.aimx_segment_gather_sum(P(g), d, 0, 0, d, P(plan.bwd.rowptr), P(plan.bwd.col), n, P(dx), d, 0, 0,
+                                           None, 0, None, 0, seg, seg_st, s) == 0
+    for _ in range(3):
+        bwd()
+    stream = torch.cuda.current_stream()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record(stream)
+    for _ in range(launches):
+        bwd()
+    t1.record(stream)
+    t1.synchronize()
+    us = t0.elapsed_time(t1) / launches * 1e3
+    return _bw("k_gather_sum (hop bwd)", 4 * (n * d + plan.E + (n + 1) + n * d), us)
+
+
+def attn_in_step(batch, hidden, device, heads=4):
+    """Attention pool forward/backward (pool.hip) at the config's batch, through the C ABI.
+    Algorithmic bytes (fp32): fwd = read x, W; write attn, scores, pooled; bwd = read x, attn,
+    scores, dpooled, W; write dx, dW."""
+    from aimx import _lib
+    from aimx.plan import GraphPlan
+    lib = _lib.load()
+    P = _lib.ptr
+    n, C, G, H = batch.num_atoms, hidden, batch.num_graphs, heads
+    plan = GraphPlan(n, 1, batch=batch.batch, num_graphs=G)
+    x = torch.randn(n, C, device=device)
+    W, b = torch.randn(H, C, device=device) * C ** -0.5, torch.zeros(H, device=device)
+    tau = torch.ones(1, device=device)
+    pooled, attn, scores = (torch.empty(G, C, device=device), torch.empty(H, n, device=device),
+                            torch.empty(H, n, device=device))
+    dpool, dx = torch.randn(G, C, device=device), torch.empty(n, C, device=device)
+    dW, db, dtau = torch.empty(H, C, device=device), torch.empty(H, device=device), torch.empty(1, device=device)
+    wsb = lib.aimx_attn_pool_workspace_bytes(n, C, H, G)
+    ws = torch.empty(wsb // 4 + 1, device=device)
+    rp, col = P(plan.graph.rowptr), P(plan.graph.col)
+
+    def fwd():
+        assert lib.aimx_attn_pool_forward(P(x), C, n, C, P(W), P(b), P(tau), H, rp, col, G, P(pooled), P(attn),
+                                          P(scores), _lib.stream_ptr(device)) == 0
+
+    def bwd():
+        assert lib.aimx_attn_pool_backward(P(x), C, n, C, P(W), P(tau), H, rp, col, G, P(attn), P(scores), P(dpool),
+                                           None, P(dx), C, P(dW), P(db), P(dtau), P(ws), wsb,
+                                           _lib.stream_ptr(device)) == 0
+    fwd()
+    tf, tb = graph_time_us(fwd), graph_time_us(bwd)
+    bf = 4 * (n * C + 2 * H * n + G * C + H * C)
+    bb = 4 * (2 * n * C + 2 * H * n + G * C + 2 * H * C)
+    return {"atoms": n, "molecules": G, "C": C, "heads": H,
+            "fwd": _bw("k_attn_fwd", bf, tf), "bwd": _bw("k_attn_bwd + partial reduce", bb, tb)}
+
+
+MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_16x16x4_f32), MI355X_MICROARCH.md chip table
+
+
+def step_flops(cfg, n_atoms, n_mols, emb=64, n_feat=4, mlp_blocks=2, ffn_blocks=3, heads=4):
+    """fp32 GEMM flops of one train step (forward x 3 for forward + input and weight gradients).
+    algorithmic: SURVEY §8d's count (the input projection over all h+1 chunks of F);
+    executed: what the kernels multiply — the hop chunks >= 2 of F are exact zeros for reference
+    inputs (targets never hop-offset, layers.py:154) and are skipped (DESIGN.md §3 'Empty hop
+    chunks'), so the input projection contracts over 2·D."""
+    H, h, D, T, L = cfg["hidden"], cfg["hops"], int(0.3 * cfg["hidden"]), cfg["tasks"], 3
+    N, G = n_atoms, n_mols
+    common = 2 * N * emb * n_feat * H + 2 * N * H * H + 2 * 2 * N * H * heads  # embed proj, concat, attn scores+sum
+    head = 2 * G * (H * H + ffn_blocks * 2 * H * H + H * H + 2 * H * T)
+    mlp = mlp_blocks * 2 * 2 * N * D * D
+    alg = common + head + L * (2 * N * D * (h + 1) * 2 * D + mlp)
+    exe = common + head + L * (2 * N * 2 * D * 2 * D + mlp)
+    return 3 * alg, 3 * exe
+
+
+def concat_gemm(n_atoms, hidden, device):
+    """The largest single GEMM of the step, concat_self_other forward ([N, hidden] x [hidden, hidden]
+    + bias, gnn.py:245-246), alone through the C ABI."""
+    from aimx import ops
+    x = torch.randn(n_atoms, hidden, device=device)
+    W = torch.randn(hidden, hidden, device=device) * hidden ** -0.5
+    b = torch.zeros(hidden, device=device)
+    out = torch.empty(n_atoms, hidden, device=device)
+    us = graph_time_us(lambda: ops.gemm_linear_fwd(x, hidden, W, b, out, hidden))
+    fl = 2 * n_atoms * hidden * hidden
+    tfs = fl / (us * 1e-6) / 1e12
+    return {"kernel": "k_gemm (concat_self_other fwd)", "M": n_atoms, "N": hidden, "K": hidden, "flops": fl,
+            "us_per_launch": round(us, 2), "achieved": round(tfs, 2), "unit": "TFLOP/s", "peak": MFMA_F32_PEAK_TFS,
+            "frac": round(tfs / MFMA_F32_PEAK_TFS, 4)}
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return model, os.cpu_count(), affinity
+
+
+def cpu_baseline(cfg, seconds=10.0, max_steps=40, one_thread_seconds=6.0):
+    """Oracle CPU restatement of the reference train step (fwd+bwd+clip+Adam, dropout on): on the
+    box's CPU share (min(16, cpu_count) threads) and on 1 thread (BASELINE.md CPU-baseline plan);
+    the port/reference ratio comes from profiles/port_vs_reference.json (the reference itself only
+    runs in the development container)."""
     threads = min(16, os.cpu_count() or 1)
+    res = _cpu_rate(cfg, threads, seconds, max_steps)
+    res1 = _cpu_rate(cfg, 1, one_thread_seconds, 8)
+    model, count, affinity = cpu_info()
+    res.update({"value_1thread": res1["value"], "sample_1thread": res1["sample"], "cpu_model": model,
+                "cpu_count": count, "cpu_affinity": affinity})
+    pvr = os.path.join(ROOT, "profiles", "port_vs_reference.json")
+    if os.path.exists(pvr):
+        try:
+            rec = json.load(open(pvr))
+            res["port_vs_reference"] = {k: rec.get(k) for k in ("ratio_port_over_reference", "oracle_mol_per_s",
+                                                                 "reference_mol_per_s", "threads", "cpu_model",
+                                                                 "measured", "script")}
+        except (OSError, ValueError):
+            pass
+    return res
+
+
+def _cpu_rate(cfg, threads, seconds, max_steps):
+    from oracle import model as om
     torch.set_num_threads(threads)
     mcfg = om.default_config(hidden_dim=cfg["hidden"], num_shells=cfg["hops"], output_dim=cfg["tasks"],
                              use_partial_charges=cfg["pc"])
@@ -239,6 +445,37 @@ def cpu_baseline(cfg, seconds=10.0, max_steps=40):
                       f"{cfg['hops']} hops), oracle/model.py fp32 torch-CPU, {threads} threads"}
 
 
+def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5):
+    """The drop-in (unchanged reference trainer) rate: a fresh model trained eagerly on unpadded
+    resident batches — forward, L1 loss, backward, clip + Adam, one Python call per op as
+    trainer.py:151-164 runs it (no graph). A side measurement; never the metric `value`."""
+    from aimx.optim import FusedAdam
+    from models import L1Loss
+    model = build_model(cfg, device)
+    opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
+    loss_fn = L1Loss()
+    bs = make_batches(cfg, batches_eager, 777, device, pad=False)
+
+    def step(i):
+        b = bs[i % len(bs)]
+        opt.zero_grad(set_to_none=True)
+        out, _, _ = model(*b.model_args())
+        loss_fn(out, b.targets).backward()
+        opt.step()
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del model, opt, bs
+    torch.cuda.empty_cache()
+    return {"value": round(cfg["batch"] * steps / dt, 1), "unit": "molecules/s", "ms_per_step": round(dt / steps * 1e3, 4),
+            "steps": steps, "warmup": warmup, "mode": "eager (no HIP graph), unpadded batches, same step"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -261,6 +498,8 @@ def main():
     ap.add_argument("--stream-mols", type=int, default=200_000, help="molecules in the --feed stream file")
     ap.add_argument("--stream-path", default=None, help="--feed stream file (default: generated under $TMPDIR)")
     ap.add_argument("--feed-threads", type=int, default=4)
+    ap.add_argument("--no-eager", action="store_true", help="skip the eager (no-graph) side measurement")
+    ap.add_argument("--eager-steps", type=int, default=20)
     ap.add_argument("--ddp-world1", action="store_true",
                     help="A/B of the data-parallel step on one GPU: a world-size-1 RCCL group with the bucket "
                          "all-reduces kept (GradientSync always=True); AIMX_DDP_GRAPH=capture|split picks the mode")
@@ -372,11 +611,29 @@ def main():
     mol = cfg["batch"] * world * args.steps
     value = mol / dt
 
-    roof = None
+    eager = None
+    if rank == 0 and world == 1 and args.graph and feeder is None and not args.no_eager:
+        eager = eager_rate(cfg, device, batches_eager=4, steps=args.eager_steps)
+    roof = extra = None
     if rank == 0 and not args.no_roofline:
         del batches
         torch.cuda.empty_cache()
-        roof = hop_roofline(make_batches(cfg, 1, 99, device)[0], cfg["hops"], device, cfg["hidden"])
+        probe = make_batches(cfg, 1, 99, device)[0]
+        roof = hop_roofline(probe, cfg["hops"], device, cfg["hidden"])
+        fl_alg, fl_exe = step_flops(cfg, atoms, cfg["batch"])
+        step_s = dt / args.steps
+        extra = {
+            "hop_in_step": hop_in_step(probe, cfg["hops"], cfg["hidden"], device),
+            "attn_in_step": attn_in_step(probe, cfg["hidden"], device),
+            "mfma": {"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_F32_PEAK_TFS,
+                     "step_flops_algorithmic": fl_alg, "step_flops_executed": fl_exe,
+                     "achieved_step_executed": round(fl_exe / step_s / 1e12, 2),
+                     "frac_step_executed": round(fl_exe / step_s / 1e12 / MFMA_F32_PEAK_TFS, 4),
+                     "achieved_step_algorithmic": round(fl_alg / step_s / 1e12, 2),
+                     "note": "whole-step rate over the whole step time (GEMMs + every HBM-bound kernel); "
+                             "executed skips the exact-zero hop chunks (step_flops)",
+                     "largest_gemm": concat_gemm(int(atoms), cfg["hidden"], device)},
+        }
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
@@ -401,6 +658,10 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if extra is not None:
+            line.update(extra)
+        if eager is not None:
+            line["eager"] = eager
         if sync is not None:
             line["ddp"] = {"world_size_reported": dist.get_world_size(), "backend": dist.get_backend(),
                            "graph_mode": graphed.mode if graphed is not None else "eager",
