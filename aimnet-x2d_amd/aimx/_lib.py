@@ -28,6 +28,12 @@ class AimxError(RuntimeError):
     pass
 
 
+class LossAccum(ctypes.Structure):
+    """AimxLossAccum (include/aimx.h): the train step's device-side loss / NaN / step bookkeeping."""
+    _fields_ = [("loss_sum", ctypes.c_void_p), ("nan_count", ctypes.c_void_p), ("steps", ctypes.c_void_p),
+                ("scale", ctypes.c_float)]
+
+
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ("M", c_i64), ("N", c_i64), ("K", c_i64),
@@ -176,6 +182,8 @@ _SIGS = {
     "aimx_head_backward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
     "aimx_head_backward": (c_i32, [ctypes.POINTER(Head), ctypes.POINTER(HeadGrad), c_ptr]),
     "aimx_l1_loss_forward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr]),
+    "aimx_l1_loss_forward_accum": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr,
+                                           ctypes.c_void_p, c_ptr]),
     "aimx_l1_loss_backward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_i64,
                                       c_ptr]),
     "aimx_l1_loss_backward_padded": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr,

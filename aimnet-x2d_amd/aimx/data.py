@@ -80,10 +80,43 @@ def blob_layout(fields):
     return out, max(off, 256)
 
 
-def batch_fields(n_rows, e_rows, g_rows, n_tasks):
-    """DeviceBatch field (dtype, shape) list: 4 feature columns, edges, batch, charges, targets."""
-    return ([(np.int64, (n_rows,))] * len(FEATURE_KEYS) + [(np.int64, (e_rows, 2)), (np.int64, (n_rows,)),
-                                                           (np.float32, (g_rows,)), (np.float32, (g_rows, n_tasks))])
+def batch_fields(n_rows, e_rows, g_rows, n_tasks, csr_hops=0):
+    """DeviceBatch field (dtype, shape) list: 4 feature columns, edges, batch, charges, targets, and
+    with csr_hops > 0 the host-built CSR views (fwd / bwd / graph rowptr + col, int32;
+    aimx_csr_host_build) for a model of that many hops."""
+    f = ([(np.int64, (n_rows,))] * len(FEATURE_KEYS) + [(np.int64, (e_rows, 2)), (np.int64, (n_rows,)),
+                                                        (np.float32, (g_rows,)), (np.float32, (g_rows, n_tasks))])
+    if csr_hops > 0:
+        f += [(np.int32, (csr_hops * n_rows + 1,)), (np.int32, (max(e_rows, 1),)), (np.int32, (n_rows + 1,)),
+              (np.int32, (max(e_rows, 1),)), (np.int32, (g_rows + 1,)), (np.int32, (max(n_rows, 1),))]
+    return f
+
+
+class HostCSR:
+    """The CSR views a DeviceBatch carries (host-built, aimx_csr_host_build), attached to its edges
+    tensor as `_aimx_csr`; aimx.plan.GraphPlan uses them instead of building on the device when
+    the plan's (hops, N, E, G, batch tensor) match."""
+    __slots__ = ("hops", "N", "E", "G", "batch", "fwd_rowptr", "fwd_col", "bwd_rowptr", "bwd_col",
+                 "graph_rowptr", "graph_col")
+
+    def __init__(self, hops, N, E, G, batch, views):
+        self.hops, self.N, self.E, self.G, self.batch = hops, N, E, G, batch
+        (self.fwd_rowptr, self.fwd_col, self.bwd_rowptr, self.bwd_col, self.graph_rowptr, self.graph_col) = views
+
+
+def host_csr_into(views, edges, batch, n_graphs, hops):
+    """Run aimx_csr_host_build on host arrays / pinned views (numpy or CPU tensors) in place."""
+    from .feed import _check, load_host
+    lib = load_host()
+
+    def p(a):
+        if isinstance(a, torch.Tensor):
+            return a.data_ptr() if a.numel() else None
+        return a.ctypes.data if a.size else None
+    n = int(batch.shape[0])
+    e = int(edges.shape[0])
+    _check(lib.aimx_csr_host_build(p(edges), e, p(batch), n, int(n_graphs), int(hops), *[p(v) for v in views]),
+           "csr_host_build (index out of range: target >= hops*N or batch index >= G)")
 
 
 class DeviceBatch:
@@ -94,7 +127,7 @@ class DeviceBatch:
 
     _FIELDS = ("feat0", "feat1", "feat2", "feat3", "edges", "batch", "total_charges", "targets")
 
-    def __init__(self, col, device, targets=None, total_charges=None):
+    def __init__(self, col, device, targets=None, total_charges=None, csr_hops=0):
         g = len(col["n_atoms"])
         self.num_graphs = g
         self.num_atoms = int(col["batch"].shape[0])
@@ -103,10 +136,17 @@ class DeviceBatch:
         parts = [np.ascontiguousarray(col["feats"][:, i]).astype(np.int64) for i in range(len(FEATURE_KEYS))]
         parts += [np.ascontiguousarray(col["edges"], np.int64), np.ascontiguousarray(col["batch"], np.int64),
                   np.ascontiguousarray(tc, np.float32), np.ascontiguousarray(tg, np.float32)]
-        self._layout, off = blob_layout([(a.dtype, a.shape) for a in parts])
+        fields = [(a.dtype, a.shape) for a in parts]
+        self.csr_hops = int(csr_hops)
+        if self.csr_hops > 0:
+            fields = batch_fields(self.num_atoms, parts[len(FEATURE_KEYS)].shape[0], g, tg.shape[1], self.csr_hops)
+        self._layout, off = blob_layout(fields)
         host = np.zeros(off, np.uint8)
         for (o, _, _), a in zip(self._layout, parts):
             host[o:o + a.nbytes] = a.view(np.uint8).reshape(-1)
+        if self.csr_hops > 0:
+            views = [host[o:o + int(np.prod(sh)) * 4].view(np.int32) for o, _, sh in self._layout[len(parts):]]
+            host_csr_into(views, parts[len(FEATURE_KEYS)], parts[len(FEATURE_KEYS) + 1], g, self.csr_hops)
         self._blob = torch.from_numpy(host).to(device)
         self._bind()
         self.tetrahedral = torch.empty(0, 4, dtype=torch.long, device=device)
@@ -114,10 +154,11 @@ class DeviceBatch:
         self.trans = torch.empty(0, 2, dtype=torch.long, device=device)
 
     @classmethod
-    def from_blob(cls, blob, layout, num_graphs, num_atoms):
+    def from_blob(cls, blob, layout, num_graphs, num_atoms, csr_hops=0):
         """Wrap a device byte buffer already holding the fields at `layout` (blob_layout())."""
         b = cls.__new__(cls)
         b.num_graphs, b.num_atoms = int(num_graphs), int(num_atoms)
+        b.csr_hops = int(csr_hops)
         b._layout, b._blob = list(layout), blob
         b._bind()
         dev = blob.device
@@ -129,11 +170,17 @@ class DeviceBatch:
     def _bind(self):
         views = []
         for o, dt, shape in self._layout:
-            tdt = torch.int64 if dt == np.int64 else torch.float32
+            tdt = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32}.get(np.dtype(dt), torch.float32)
             n = int(np.prod(shape)) if len(shape) else 1
             views.append(self._blob[o:o + n * (8 if tdt == torch.int64 else 4)].view(tdt).view(*shape))
+        nf = len(FEATURE_KEYS)
         self.atom_features = {k: views[i] for i, k in enumerate(FEATURE_KEYS)}
-        self.edges, self.batch, self.total_charges, self.targets = views[len(FEATURE_KEYS):]
+        self.edges, self.batch, self.total_charges, self.targets = views[nf:nf + 4]
+        if getattr(self, "csr_hops", 0) > 0:
+            csr = views[nf + 4:nf + 10]
+            csr[1], csr[3], csr[5] = csr[1][:self.edges.shape[0]], csr[3][:self.edges.shape[0]], csr[5][:self.num_atoms]
+            self.edges._aimx_csr = HostCSR(self.csr_hops, self.num_atoms, self.edges.shape[0], self.num_graphs,
+                                           self.batch, csr)
 
     def copy_(self, other):
         """In-place copy of another batch of identical layout (static graph inputs): one copy."""

@@ -72,6 +72,8 @@ def load_host():
     lib.aimx_collate_plan.argtypes = [c_ptr, c_ptr, c_ptr, c_i64, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]
     lib.aimx_collate_write.restype = c_i32
     lib.aimx_collate_write.argtypes = [c_ptr, ctypes.POINTER(CollateOut)]
+    lib.aimx_csr_host_build.restype = c_i32
+    lib.aimx_csr_host_build.argtypes = [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32] + [c_ptr] * 6
     _lib = lib
     return lib
 
@@ -211,12 +213,14 @@ class HostStore:
 class HostCollator:
     """One native collator (persistent worker pool). Not thread-safe: one batch at a time."""
 
-    def __init__(self, max_hops, threads=4):
+    def __init__(self, max_hops, threads=4, csr=True):
         self._lib = load_host()
         h = c_ptr()
         _check(self._lib.aimx_collator_create(int(max_hops), int(threads), ctypes.byref(h)), "collator_create")
         self._h = h
         self.max_hops = int(max_hops)
+        # collate_blob also builds the batch's CSR views for a model of max_hops hops (csr=False: not)
+        self.csr_hops = self.max_hops if csr else 0
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -264,7 +268,7 @@ class HostCollator:
         pad = n_max > 0
         nr, er, gr = (n_max, e_max, g + pad_mols) if pad else (n, e, g)
         t = store.n_tasks if n_tasks is None else n_tasks
-        layout, nbytes = adata.blob_layout(adata.batch_fields(nr, er, gr, max(t, 1)))
+        layout, nbytes = adata.blob_layout(adata.batch_fields(nr, er, gr, max(t, 1), self.csr_hops))
         blob = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
         base = blob.data_ptr()
         ptr = [base + o for o, _, _ in layout]
@@ -273,6 +277,9 @@ class HostCollator:
             blob[o:o + int(np.prod(shape)) * 4].zero_()
         self.write(ptr[:4], ptr[4], ptr[5], ptr[6], ptr[7] if t else None, None, n_max if pad else 0,
                    e_max if pad else 0, pad_mols if pad else 0)
+        if self.csr_hops > 0:  # the step's CSR views ride in the same blob (one H2D copy)
+            _check(self._lib.aimx_csr_host_build(ptr[4], er, ptr[5], nr, gr, self.csr_hops, *ptr[8:14]),
+                   "csr_host_build")
         return blob, layout, gr, nr, (g, n, e)
 
 
@@ -310,7 +317,7 @@ class BatchFeeder:
                     dev = blob.to(self.device, non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(self.stream)
-                b = adata.DeviceBatch.from_blob(dev, layout, gr, nr)
+                b = adata.DeviceBatch.from_blob(dev, layout, gr, nr, self.collator.csr_hops)
                 b.real_graphs, b.real_atoms, b.real_edges = real
                 self._q.put((b, ev, blob))
         except Exception as exc:  # surfaced to the consumer

@@ -331,6 +331,49 @@ def attention_pool(plan, x, W, b, tau):
     return _AttnPool.apply(plan, x, W, b, tau)
 
 
+def _packed_rows(ts):
+    """The [len(ts), k] tensor the row tensors ts (each k elements) already form in memory (one
+    contiguous storage, consecutive, in order), or None."""
+    t0 = ts[0]
+    k = t0.numel()
+    base = t0.data_ptr()
+    for i, t in enumerate(ts):
+        if t.numel() != k or not t.is_contiguous() or t.data_ptr() != base + i * k * t.element_size() or \
+                t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() or t.dtype != t0.dtype:
+            return None
+    return t0.detach().as_strided((len(ts), k), (k, 1))
+
+
+class _AttnPoolHeads(torch.autograd.Function):
+    """Attention pool over per-head Linear(C, 1) parameters (pooling.py:122-172's ModuleList) laid out
+    as one [H, C] / [H] block (MultiHeadAttentionPoolingLayer packs them): the kernels read that
+    block in place and the gradients come back as row views of one [H, C] / [H] result, so neither
+    direction launches a cat or a split."""
+
+    @staticmethod
+    def forward(ctx, plan, x, W, b, tau, *heads):
+        pooled, attn = _AttnPool.forward(ctx, plan, x, W, b, tau)
+        ctx.H = len(heads) // 2
+        return pooled, attn
+
+    @staticmethod
+    def backward(ctx, d_pooled, d_attn):
+        _, dx, dW, db, dtau = _AttnPool.backward(ctx, d_pooled, d_attn)
+        H = ctx.H
+        return (None, dx, None, None, dtau) + tuple(dW[i:i + 1] for i in range(H)) + \
+            tuple(db[i:i + 1] for i in range(H))
+
+
+def attention_pool_heads(plan, x, weights, biases, tau):
+    """attention_pool with the H head weights [1, C] and biases [1] given separately (the
+    reference's nn.Linear per head); no concatenation when they are packed (_packed_rows)."""
+    W, b = _packed_rows(weights), _packed_rows(biases)
+    if W is None or b is None:
+        return attention_pool(plan, x, torch.cat(list(weights), 0), torch.cat(list(biases), 0), tau)
+    _lib.require_device(x, W, b, tau)
+    return _AttnPoolHeads.apply(plan, x, W, b.view(-1), tau, *weights, *biases)
+
+
 # ---------------------------------------------------------------------------------------------
 # Mean / max / sum pooling
 # ---------------------------------------------------------------------------------------------
@@ -690,7 +733,8 @@ def linear_block(x, W1, b1, W2, b2, act, drop_p=0.0, training=False, skip=False,
 # ---------------------------------------------------------------------------------------------
 class _L1Loss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, target, weights, per_sample, rows):
+    def forward(ctx, pred, target, weights, per_sample, rows, accum):
+        import ctypes
         lib = _lib.load()
         p, ldp = _rows(pred.reshape(pred.shape[0], -1) if pred.dim() != 2 else pred)
         t, ldt = _rows(target.reshape(target.shape[0], -1) if target.dim() != 2 else target)
@@ -698,8 +742,13 @@ class _L1Loss(torch.autograd.Function):
         rows = total if rows is None else rows
         w = weights.contiguous().float() if weights is not None else None
         loss = torch.empty((), dtype=_F32, device=pred.device)
-        check(lib.aimx_l1_loss_forward(ptr(p), ldp, ptr(t), ldt, rows, cols, ptr(w), int(per_sample), ptr(loss),
-                                       stream_ptr(pred.device)), "l1_loss_forward")
+        acc = None
+        if accum is not None:
+            loss_sum, nan_count, steps, scale = accum
+            acc = _lib.LossAccum(ptr(loss_sum), ptr(nan_count), ptr(steps), float(scale))
+        check(lib.aimx_l1_loss_forward_accum(ptr(p), ldp, ptr(t), ldt, rows, cols, ptr(w), int(per_sample), ptr(loss),
+                                             ctypes.byref(acc) if acc is not None else None,
+                                             stream_ptr(pred.device)), "l1_loss_forward")
         ctx.save_for_backward(p, t, w)
         ctx.meta = (ldp, ldt, int(per_sample), pred.shape, rows)
         return loss
@@ -714,15 +763,23 @@ class _L1Loss(torch.autograd.Function):
         dp = torch.empty(total, cols, dtype=_F32, device=p.device)
         check(lib.aimx_l1_loss_backward_padded(ptr(p), ldp, ptr(t), ldt, rows, total, cols, ptr(w), per_sample, ptr(g),
                                                ptr(dp), cols, stream_ptr(p.device)), "l1_loss_backward")
-        return dp.view(shape), None, None, None, None
+        return dp.view(shape), None, None, None, None, None
 
 
-def l1_loss(pred, target, weights=None, per_sample=False, rows=None):
+def l1_loss(pred, target, weights=None, per_sample=False, rows=None, accum=None):
     """mean |pred - target| (per_sample=False, weights None: nn.L1Loss) or
     mean over samples of sum_t w_t |pred - target| (per_sample=True: WeightedL1Loss).
     rows=B: the loss of pred[:B] against target (B rows), with pred's remaining rows (the padding
     molecules of a static captured batch) getting a zero gradient in the same launch; equal to
-    l1_loss(pred[:B], target) without autograd's slice-backward zero fill and copy."""
+    l1_loss(pred[:B], target) without autograd's slice-backward zero fill and copy.
+    accum=(loss_sum f32[], nan_count i32[], steps i64[], scale): the train step's device-side
+    bookkeeping in the same launch (loss_sum += loss * scale, nan_count += any(isnan(pred[:rows])),
+    steps += 1; aimx_l1_loss_forward_accum)."""
+    if accum is not None:
+        ls, nc, st, _ = accum
+        if ls.dtype != _F32 or nc.dtype != torch.int32 or st.dtype != torch.int64 or \
+                ls.numel() != 1 or nc.numel() != 1 or st.numel() != 1:
+            raise _lib.AimxError("aimx.l1_loss: accum = (f32 scalar, int32 scalar, int64 scalar, scale)")
     _lib.require_device(pred, target)
     if pred.dtype != _F32 or target.dtype != _F32:
         raise _lib.AimxError("aimx.l1_loss: pred and target must be fp32 tensors")
@@ -731,7 +788,7 @@ def l1_loss(pred, target, weights=None, per_sample=False, rows=None):
             raise _lib.AimxError("aimx.l1_loss: pred and target must have one shape")
     elif not (0 <= rows <= pred.shape[0] and target.shape[0] == rows and target.shape[1:] == pred.shape[1:]):
         raise _lib.AimxError("aimx.l1_loss: rows must be <= pred rows and equal target rows")
-    return _L1Loss.apply(pred, target, weights, bool(per_sample), rows)
+    return _L1Loss.apply(pred, target, weights, bool(per_sample), rows, accum)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -19,6 +19,17 @@ import torch
 from . import _lib
 
 _VALIDATE = os.environ.get("AIMX_VALIDATE", "0") == "1"
+# use the CSR views a DeviceBatch carries from the batch builder (AIMX_HOST_CSR=0: always build)
+_HOST_CSR = os.environ.get("AIMX_HOST_CSR", "1") != "0"
+_ZERO = {}
+
+
+def _zero_status(device):
+    """A status word that stays 0 (plans whose indices were checked on the host)."""
+    z = _ZERO.get(device)
+    if z is None:
+        z = _ZERO[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return z
 
 
 def _col(t2d, j):
@@ -98,6 +109,21 @@ class GraphPlan:
             (t_ptr, t_st), (s_ptr, s_st) = _col(e, 0), _col(e, 1)
         self.batch = batch
         self.G = None
+        hc = getattr(edges, "_aimx_csr", None) if edges is not None and _HOST_CSR else None
+        if hc is not None and batch is not None and hc.hops == self.num_hops and hc.N == self.N and \
+                hc.E == self.E and (num_graphs is None or int(num_graphs) == hc.G) and \
+                batch.data_ptr() == hc.batch.data_ptr() and tuple(batch.shape) == tuple(hc.batch.shape) and \
+                batch.dtype == torch.int64:
+            # the batch builder already made this batch's CSRs (aimx.data.HostCSR, in the batch blob)
+            self._keep.append(batch)
+            self.G = hc.G
+            self.fwd = CSR(hc.fwd_rowptr, hc.fwd_col, self.num_hops * self.N)
+            self.bwd = CSR(hc.bwd_rowptr, hc.bwd_col, self.N)
+            self.graph = CSR(hc.graph_rowptr, hc.graph_col, hc.G)
+            self.status = _zero_status(self.device)  # validated on the host (aimx_csr_host_build)
+            self.host_csr = True
+            return
+        self.host_csr = False
         specs = []  # (key, key_stride, key_mod, val, val_stride, val_mod, n_items, n_rows, attribute)
         if self.N > 0:  # E == 0 gives all-empty rows: every hop chunk is zero (layers.py:148-149)
             n, h = self.N, self.num_hops

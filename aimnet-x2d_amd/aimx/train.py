@@ -76,14 +76,18 @@ class GraphedTrainStep:
 
         def fwd_bwd():
             out, _, _ = model(*self.static.model_args())
-            if padded is not None:  # fused L1: padding rows' zero gradient in the loss's own launch
-                loss = padded(out, self.static.targets[:B], B)
+            if padded is not None:
+                # fused L1: the padding rows' zero gradient in the loss's backward launch, and the
+                # step's loss sum / NaN flag / step count in its forward launch
+                loss = padded(out, self.static.targets[:B], B,
+                              accum=(self.loss_sum, self.nan_count, self.steps, float(B)))
             else:
                 loss = criterion(out[:B], self.static.targets[:B])
             loss.backward(one)  # d loss = 1 from a resident tensor (no per-step fill launch)
-            self.loss_sum.add_(loss.detach() * B)
-            self.nan_count.add_(torch.isnan(out[:B]).any().to(torch.int32))
-            self.steps.add_(1)
+            if padded is None:
+                self.loss_sum.add_(loss.detach() * B)
+                self.nan_count.add_(torch.isnan(out[:B]).any().to(torch.int32))
+                self.steps.add_(1)
 
         self._fwd_bwd = fwd_bwd
         mode = ddp_graph or os.environ.get("AIMX_DDP_GRAPH") or "capture"

@@ -523,3 +523,46 @@ int aimx_collate_write(aimx_collator* c, const AimxCollateOut* o) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Host CSR views (include/aimx_host.h): stable counting sorts, the host twin of csr.hip.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+// rowptr[rows+1] and col[n] of the stable sort of items 0..n-1 by key(i) in [0, rows)
+template <class Key, class Val>
+void counting_csr(int64_t n, int64_t rows, Key key, Val val, int32_t* rowptr, int32_t* col) {
+  std::fill(rowptr, rowptr + rows + 1, 0);
+  for (int64_t i = 0; i < n; ++i) ++rowptr[key(i) + 1];
+  for (int64_t r = 0; r < rows; ++r) rowptr[r + 1] += rowptr[r];
+  std::vector<int32_t> next(rowptr, rowptr + rows);
+  for (int64_t i = 0; i < n; ++i) col[next[key(i)]++] = val(i);
+}
+
+}  // namespace
+
+extern "C" int aimx_csr_host_build(const int64_t* edges, int64_t E, const int64_t* batch, int64_t N, int64_t G,
+                                   int32_t hops, int32_t* fwd_rowptr, int32_t* fwd_col, int32_t* bwd_rowptr,
+                                   int32_t* bwd_col, int32_t* graph_rowptr, int32_t* graph_col) {
+  const int64_t lim = int64_t(1) << 31;
+  if (E < 0 || N < 0 || G < 0 || hops < 1 || E >= lim || G >= lim || int64_t(hops) * N >= lim) return AIMX_HOST_EARG;
+  if (!fwd_rowptr || !bwd_rowptr || !graph_rowptr || (E > 0 && (!edges || !fwd_col || !bwd_col)) ||
+      (N > 0 && (!batch || !graph_col)))
+    return AIMX_HOST_EARG;
+  if (E > 0 && N == 0) return AIMX_HOST_EARG;
+  const int64_t HN = int64_t(hops) * N;
+  for (int64_t i = 0; i < E; ++i)
+    if (edges[2 * i] < 0 || edges[2 * i] >= HN) return AIMX_HOST_EARG;
+  for (int64_t i = 0; i < N; ++i)
+    if (batch[i] < 0 || batch[i] >= G) return AIMX_HOST_EARG;
+  try {
+    auto src = [&](int64_t i) { return int32_t(((edges[2 * i + 1] % N) + N) % N); };
+    counting_csr(E, HN, [&](int64_t i) { return edges[2 * i]; }, src, fwd_rowptr, fwd_col);
+    counting_csr(E, N, src, [&](int64_t i) { return int32_t(edges[2 * i]); }, bwd_rowptr, bwd_col);
+    counting_csr(N, G, [&](int64_t i) { return batch[i]; }, [](int64_t i) { return int32_t(i); }, graph_rowptr,
+                 graph_col);
+  } catch (const std::bad_alloc&) {
+    return AIMX_HOST_ENOMEM;
+  }
+  return AIMX_HOST_OK;
+}

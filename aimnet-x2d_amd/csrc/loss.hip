@@ -14,21 +14,39 @@
 namespace aimx {
 namespace {
 
+// acc != NULL: also the train step's device-side bookkeeping (aimx_l1_loss_forward_accum):
+// acc->loss_sum += loss * acc_scale (two roundings, as torch's mul then add_), acc->nan_count += any
+// element of pred[:rows] is NaN, acc->steps += 1.
 __global__ __launch_bounds__(256) void k_l1_fwd(const float* __restrict__ p, int64_t ldp, const float* __restrict__ y,
                                                 int64_t ldy, int64_t rows, int64_t cols,
-                                                const float* __restrict__ w, float inv_div, float* __restrict__ loss) {
-  __shared__ float part[4];
-  float s = 0.f;
+                                                const float* __restrict__ w, float inv_div, float* __restrict__ loss,
+                                                AimxLossAccum acc) {
+  __shared__ float part[4], nanp[4];
+  float s = 0.f, nn = 0.f;
   const int64_t n = rows * cols;
   for (int64_t e = threadIdx.x; e < n; e += 256) {
     const int64_t i = e / cols, t = e - i * cols;
-    const float d = fabsf(p[i * ldp + t] - y[i * ldy + t]);
+    const float pv = p[i * ldp + t];
+    const float d = fabsf(pv - y[i * ldy + t]);
     s += w ? d * w[t] : d;
+    nn += (pv != pv) ? 1.f : 0.f;
   }
   s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  nn = wave_sum(nn);
+  if ((threadIdx.x & 63) == 0) {
+    part[threadIdx.x >> 6] = s;
+    nanp[threadIdx.x >> 6] = nn;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) loss[0] = ((part[0] + part[1]) + (part[2] + part[3])) * inv_div;
+  if (threadIdx.x == 0) {
+    const float l = ((part[0] + part[1]) + (part[2] + part[3])) * inv_div;
+    loss[0] = l;
+    if (acc.loss_sum) {
+      acc.loss_sum[0] = __fadd_rn(acc.loss_sum[0], __fmul_rn(l, acc.scale));
+      acc.nan_count[0] += ((nanp[0] + nanp[1]) + (nanp[2] + nanp[3])) > 0.f ? 1 : 0;
+      acc.steps[0] += 1;
+    }
+  }
 }
 
 __global__ void k_l1_bwd(const float* __restrict__ p, int64_t ldp, const float* __restrict__ y, int64_t ldy,
@@ -53,17 +71,28 @@ __global__ void k_l1_bwd(const float* __restrict__ p, int64_t ldp, const float* 
 
 using namespace aimx;
 
-extern "C" int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
-                                    int64_t cols, const float* weights, int32_t per_sample, float* loss,
-                                    aimx_stream_t stream) {
+extern "C" int aimx_l1_loss_forward_accum(const float* pred, int64_t ldp, const float* target, int64_t ldt,
+                                          int64_t rows, int64_t cols, const float* weights, int32_t per_sample,
+                                          float* loss, const AimxLossAccum* accum, aimx_stream_t stream) {
   if (rows < 0 || cols < 0 || !loss || ldp < cols || ldt < cols) return AIMX_EARG;
   if (rows * cols > 0 && (!pred || !target)) return AIMX_EARG;
+  AimxLossAccum acc{};
+  if (accum) {
+    if (!accum->loss_sum || !accum->nan_count || !accum->steps) return AIMX_EARG;
+    acc = *accum;
+  }
   const double div = per_sample ? (double)rows : (double)rows * (double)cols;
   const float inv = div > 0 ? (float)(1.0 / div) : __builtin_nanf("");  // mean of nothing: NaN, as ATen
   hipLaunchKernelGGL(k_l1_fwd, dim3(1), dim3(256), 0, (hipStream_t)stream, pred, ldp, target, ldt, rows, cols, weights,
-                     inv, loss);
+                     inv, loss, acc);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
+}
+
+extern "C" int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
+                                    int64_t cols, const float* weights, int32_t per_sample, float* loss,
+                                    aimx_stream_t stream) {
+  return aimx_l1_loss_forward_accum(pred, ldp, target, ldt, rows, cols, weights, per_sample, loss, nullptr, stream);
 }
 
 extern "C" int aimx_l1_loss_backward_padded(const float* pred, int64_t ldp, const float* target, int64_t ldt,

@@ -18,10 +18,10 @@ class L1Loss(nn.Module):
     def forward(self, y_pred: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:
         return ops.l1_loss(y_pred, y_true)
 
-    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int) -> torch.Tensor:
+    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int, accum=None) -> torch.Tensor:
         """forward(y_pred[:rows], y_true) for a static padded batch, the padding rows' zero gradient
-        written by the same backward launch (no slice-backward fill + copy)."""
-        return ops.l1_loss(y_pred, y_true, rows=rows)
+        written by the same backward launch (no slice-backward fill + copy); accum: ops.l1_loss."""
+        return ops.l1_loss(y_pred, y_true, rows=rows, accum=accum)
 
 
 class WeightedL1Loss(nn.Module):
@@ -34,5 +34,5 @@ class WeightedL1Loss(nn.Module):
     def forward(self, y_pred: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:
         return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True)
 
-    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int) -> torch.Tensor:
-        return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True, rows=rows)
+    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int, accum=None) -> torch.Tensor:
+        return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True, rows=rows, accum=accum)

@@ -66,14 +66,35 @@ class MultiHeadAttentionPoolingLayer(nn.Module):
         else:
             self.register_buffer("temperature", torch.tensor(initial_temperature))
         self.dropout = nn.Dropout(dropout_prob)
+        self._pack_heads()
+
+    def _pack_heads(self):
+        """Lay the heads' weights [1, C] and biases [1] out as consecutive rows of one [H, C] / [H]
+        block (same Parameters, same state_dict; values unchanged), so the kernels read them in
+        place (ops.attention_pool_heads). Re-done after .to() / .cuda() (_apply)."""
+        lins = list(self.attention_weights)
+        if not lins:
+            return
+        with torch.no_grad():
+            for name in ("weight", "bias"):
+                ps = [getattr(lin, name) for lin in lins]
+                if ops._packed_rows(ps) is not None:
+                    continue
+                block = torch.cat([p.detach().reshape(1, -1) for p in ps], 0)
+                for i, p in enumerate(ps):
+                    p.data = block[i].view(p.shape)
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._pack_heads()
+        return out
 
     def forward(self, x: torch.Tensor, batch_indices: Optional[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
         if batch_indices is None:  # whole input is one graph (pooling.py:146-147, 163-166)
             batch_indices = torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
         plan = _plan_for(self, x, batch_indices)
-        W = torch.cat([lin.weight for lin in self.attention_weights], 0)
-        b = torch.cat([lin.bias for lin in self.attention_weights], 0)
-        pooled, attn = ops.attention_pool(plan, x, W, b, self.temperature)
+        pooled, attn = ops.attention_pool_heads(plan, x, [lin.weight for lin in self.attention_weights],
+                                                [lin.bias for lin in self.attention_weights], self.temperature)
         if self.dropout.p > 0:
             pooled = self.dropout(pooled)
         return pooled, attn

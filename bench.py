@@ -72,7 +72,7 @@ def make_batches(cfg, n_batches, seed, device, pad=False):
     """Device-resident batches. pad=True: static shapes for graph replay (PAD_MOLS padding molecules)."""
     cols = make_collated(cfg, n_batches, seed)
     if not pad:
-        return [adata.DeviceBatch(c, device, targets=t, total_charges=q) for c, t, q in cols]
+        return [adata.DeviceBatch(c, device, targets=t, total_charges=q, csr_hops=cfg["hops"]) for c, t, q in cols]
     n_max = max(c["batch"].shape[0] for c, _, _ in cols) + 64
     e_max = max(c["edges"].shape[0] for c, _, _ in cols) + 256
     out = []
@@ -81,7 +81,7 @@ def make_batches(cfg, n_batches, seed, device, pad=False):
         pc = adata.pad_collated(c, n_max, e_max, cfg["batch"], PAD_MOLS)
         tg = np.concatenate([t, np.zeros((PAD_MOLS, t.shape[1]), np.float32)])
         qq = np.concatenate([q, np.zeros(PAD_MOLS, np.float32)])
-        b = adata.DeviceBatch(pc, device, targets=tg, total_charges=qq)
+        b = adata.DeviceBatch(pc, device, targets=tg, total_charges=qq, csr_hops=cfg["hops"])
         b.real_atoms, b.real_edges, b.real_graphs = real_atoms, real_edges, cfg["batch"]
         out.append(b)
     return out

@@ -413,6 +413,20 @@ int aimx_head_backward(const AimxHead* h, const AimxHeadGrad* d, aimx_stream_t s
 int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
                          int64_t cols, const float* weights, int32_t per_sample, float* loss,
                          aimx_stream_t stream);
+/* The same forward plus the train step's per-step bookkeeping (reference trainer.py:160-171:
+ * `torch.isnan(outputs).any()` and `loss.item() * batch_size`, kept on the device so the loop never
+ * synchronises), in the loss's own launch:
+ *   *loss_sum += loss * scale (fp32 multiply, then fp32 add), *nan_count += any(isnan(pred[:rows])),
+ *   *steps += 1.  accum NULL: aimx_l1_loss_forward. */
+typedef struct AimxLossAccum {
+  float* loss_sum;
+  int32_t* nan_count;
+  int64_t* steps;
+  float scale;
+} AimxLossAccum;
+int aimx_l1_loss_forward_accum(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
+                               int64_t cols, const float* weights, int32_t per_sample, float* loss,
+                               const AimxLossAccum* accum, aimx_stream_t stream);
 int aimx_l1_loss_backward(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
                           int64_t cols, const float* weights, int32_t per_sample, const float* d_loss,
                           float* d_pred, int64_t ldd, aimx_stream_t stream);

@@ -104,6 +104,23 @@ int aimx_collate_plan(aimx_collator* c, const aimx_mol_store* store, const int64
 /* Write the planned batch (same store; the plan stays valid until the next plan). */
 int aimx_collate_write(aimx_collator* c, const AimxCollateOut* out);
 
+/* ------------------------------------------------------------------------------------------
+ * Host-built CSR views of a collated batch: the same three stable CSRs the device builder
+ * aimx_csr_build_multi (include/aimx.h) makes at the start of every forward, computed here by the
+ * batch builder and shipped inside the batch blob, so a train step starts with its CSRs already
+ * in HBM (no per-step count / scan / fill / order launches).
+ *   edges int64 [E, 2] (column 0 target, column 1 source: multi_hop_edge_indices), batch int64 [N]
+ *   fwd:   rows hops*N keyed by target,  col = source mod N (Python-style), fwd_rowptr[hops*N+1]
+ *   bwd:   rows N keyed by source mod N, col = target,                      bwd_rowptr[N+1]
+ *   graph: rows G keyed by batch[i],     col = i,                           graph_rowptr[G+1]
+ * Items keep ascending order inside a row (the reference's summation order). Returns AIMX_HOST_EARG
+ * when a target is outside [0, hops*N), a batch index outside [0, G), or N == 0 with E > 0 (the
+ * device builder's status word cases), and for E, N, G, hops sizes that do not fit int32 CSRs.
+ * ------------------------------------------------------------------------------------------ */
+int aimx_csr_host_build(const int64_t* edges, int64_t E, const int64_t* batch, int64_t N, int64_t G, int32_t hops,
+                        int32_t* fwd_rowptr, int32_t* fwd_col, int32_t* bwd_rowptr, int32_t* bwd_col,
+                        int32_t* graph_rowptr, int32_t* graph_col);
+
 #ifdef __cplusplus
 }
 #endif

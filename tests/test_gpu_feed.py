@@ -22,7 +22,9 @@ def _gpu():
 
 
 def _fields(b):
-    return [b.edges, b.batch, b.total_charges, b.targets] + [b.atom_features[k] for k in adata.FEATURE_KEYS]
+    c = b.edges._aimx_csr
+    return [b.edges, b.batch, b.total_charges, b.targets] + [b.atom_features[k] for k in adata.FEATURE_KEYS] + \
+        [c.fwd_rowptr, c.fwd_col, c.bwd_rowptr, c.bwd_col, c.graph_rowptr, c.graph_col]
 
 
 @pytest.mark.parametrize("pad", [False, True])
@@ -46,7 +48,7 @@ def test_feeder_batches_bit_exact_and_ordered(pad):
             col = adata.pad_collated(col, n_max, e_max, len(idx), pm)
             tg = np.concatenate([tg, np.zeros((pm, tg.shape[1]), np.float32)])
             tc = np.concatenate([tc, np.zeros(pm, np.float32)])
-        ref = adata.DeviceBatch(col, DEV, targets=tg, total_charges=tc)
+        ref = adata.DeviceBatch(col, DEV, targets=tg, total_charges=tc, csr_hops=3)
         assert b._layout == ref._layout
         for x, y in zip(_fields(b), _fields(ref)):
             assert torch.equal(x, y)
@@ -64,9 +66,12 @@ def test_fed_batch_drives_model_identically():
     b = next(iter(feed.BatchFeeder(store, iter([idx]), 3, DEV, depth=1, threads=2)))
     ref = adata.DeviceBatch(adata.collate(asset.molecules(idx), 3), DEV, targets=asset.targets[idx],
                             total_charges=asset.total_charge[idx])
+    from aimx.plan import GraphPlan
+    assert GraphPlan(b.num_atoms, 3, edges=b.edges, batch=b.batch, num_graphs=b.num_graphs).host_csr
+    assert not GraphPlan(ref.num_atoms, 3, edges=ref.edges, batch=ref.batch, num_graphs=ref.num_graphs).host_csr
     with torch.no_grad():
-        o1 = m(*b.model_args())[0]
-        o2 = m(*ref.model_args())[0]
+        o1 = m(*b.model_args())[0]  # CSR views built by the batch builder
+        o2 = m(*ref.model_args())[0]  # CSR views built on the device
     assert torch.equal(o1, o2)
 
 

@@ -746,6 +746,33 @@ def test_l1_loss_rows_of_padded_prediction(weighted):
     assert torch.equal(a.grad[B:], torch.zeros(8, T, device=DEV))
 
 
+def test_l1_loss_accum_bookkeeping():
+    """ops.l1_loss(..., accum=...) == the captured step's former torch bookkeeping
+    (loss_sum.add_(loss * B), nan_count.add_(isnan(pred[:B]).any()), steps.add_(1)): bit-identical
+    loss sums over several steps, NaN rows counted only inside the loss rows."""
+    from aimx import ops
+    g = torch.Generator().manual_seed(9)
+    B, T = 512, 3
+    ls, nc, st = (torch.zeros((), device=DEV), torch.zeros((), dtype=torch.int32, device=DEV),
+                  torch.zeros((), dtype=torch.int64, device=DEV))
+    ref_ls, ref_nc = torch.zeros((), device=DEV), torch.zeros((), dtype=torch.int32, device=DEV)
+    for k in range(5):
+        p = torch.randn(B + 8, T, generator=g).to(DEV)
+        y = torch.randn(B, T, generator=g).to(DEV)
+        if k == 2:
+            p[7, 1] = float("nan")  # inside the loss rows: counted
+        if k == 3:
+            p[B + 2, 0] = float("nan")  # a padding row: not counted (not an output of the batch)
+        loss = ops.l1_loss(p, y, rows=B, accum=(ls, nc, st, float(B)))
+        ref = ops.l1_loss(p, y, rows=B)
+        assert torch.equal(loss, ref) or (torch.isnan(loss).item() and torch.isnan(ref).item())
+        ref_ls.add_(ref.detach() * B)
+        ref_nc.add_(torch.isnan(p[:B]).any().to(torch.int32))
+    torch.testing.assert_close(ls, ref_ls, rtol=0, atol=0, equal_nan=True)
+    assert int(nc.item()) == int(ref_nc.item()) == 1
+    assert int(st.item()) == 5
+
+
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 def test_fused_head_matches_module_path(name, monkeypatch):
     """The fused post-pool head (one launch forward, one + a grouped weight-gradient launch

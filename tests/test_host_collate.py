@@ -119,7 +119,7 @@ def test_blob_matches_device_batch_layout(asset):
     store = feed.HostStore.from_qm9_asset(asset)
     blob, layout, gr, nr, _ = feed.HostCollator(3, 2).collate_blob(store, idx, pinned=False)
     col = adata.collate(asset.molecules(idx), 3)
-    ref = adata.DeviceBatch(col, "cpu", targets=asset.targets[idx], total_charges=asset.total_charge[idx])
+    ref = adata.DeviceBatch(col, "cpu", targets=asset.targets[idx], total_charges=asset.total_charge[idx], csr_hops=3)
     assert layout == ref._layout
     for o, dt, shape in layout:  # field bytes (alignment gaps are never read)
         nb = int(np.prod(shape)) * dt.itemsize
@@ -154,3 +154,75 @@ def test_host_library_exports_every_header_symbol_and_struct_layout():
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     names = re.findall(r"\**\s*(\w+)\s*(?:\[[^\]]*\])?\s*[;,]", body)
     assert names == [f[0] for f in feed.CollateOut._fields_]
+
+
+# ------------------------------------------------------------------------------- host CSR views
+def _oracle_graph():
+    import importlib
+    return importlib.import_module("oracle.graph")
+
+
+@pytest.mark.parametrize("case,h", [("c1", 3), ("c2", 3), ("c3", 4), ("c5s", 6)])
+def test_host_csr_matches_oracle_stable_sort(case, h):
+    """aimx_csr_host_build == the oracle's stable CSR (the reference's scatter order) on the
+    golden batches, for all three views; and the DeviceBatch carries them on its edges tensor."""
+    og = _oracle_graph()
+    z = load_golden(case)
+    e = z["edges"].astype(np.int64)
+    b = z["batch"].astype(np.int64)
+    n, g = b.shape[0], len(z["n_mol_atoms"])
+    col = {"edges": e, "feats": z["feats"].astype(np.int64), "batch": b, "n_atoms": z["n_mol_atoms"]}
+    db = adata.DeviceBatch(col, "cpu", csr_hops=h)
+    hc = db.edges._aimx_csr
+    assert (hc.hops, hc.N, hc.E, hc.G) == (h, n, e.shape[0], g)
+    for (rp, cl), (keys, vals, rows) in zip(
+            [(hc.fwd_rowptr, hc.fwd_col), (hc.bwd_rowptr, hc.bwd_col), (hc.graph_rowptr, hc.graph_col)],
+            [(e[:, 0], np.mod(e[:, 1], n), h * n), (np.mod(e[:, 1], n), e[:, 0], n), (b, np.arange(n), g)]):
+        rref, cref = og.stable_csr(keys, vals, rows)
+        assert np.array_equal(rp.numpy(), rref)
+        assert np.array_equal(cl.numpy(), cref)
+
+
+def test_host_csr_general_contract_and_errors():
+    """Hop-offset targets, negative and >= N sources (Python-style mod); out-of-range target or
+    batch index -> HostError (the device builder's status word)."""
+    og = _oracle_graph()
+    rng = np.random.default_rng(5)
+    n, h, e, g = 300, 4, 20000, 7
+    t = rng.integers(0, h * n, e)
+    s = rng.integers(-5 * n, 5 * n, e)
+    edges = np.stack([t, s], 1).astype(np.int64)
+    batch = np.sort(rng.integers(0, g, n)).astype(np.int64)
+    views = [np.empty(h * n + 1, np.int32), np.empty(e, np.int32), np.empty(n + 1, np.int32), np.empty(e, np.int32),
+             np.empty(g + 1, np.int32), np.empty(n, np.int32)]
+    adata.host_csr_into(views, edges, batch, g, h)
+    rp, col = og.stable_csr(t, np.mod(s, n), h * n)
+    assert np.array_equal(views[0], rp) and np.array_equal(views[1], col)
+    rp, col = og.stable_csr(np.mod(s, n), t, n)
+    assert np.array_equal(views[2], rp) and np.array_equal(views[3], col)
+    bad = edges.copy()
+    bad[11, 0] = h * n
+    with pytest.raises(feed.HostError):
+        adata.host_csr_into(views, bad, batch, g, h)
+    bb = batch.copy()
+    bb[3] = g
+    with pytest.raises(feed.HostError):
+        adata.host_csr_into(views, edges, bb, g, h)
+    # no edges: empty fwd/bwd rows, graph CSR still built
+    adata.host_csr_into(views, np.zeros((0, 2), np.int64), batch, g, h)
+    assert views[0][-1] == 0 and views[2][-1] == 0 and views[4][-1] == n
+
+
+def test_feeder_blob_carries_host_csr(asset):
+    idx = np.arange(40, 104)
+    store = feed.HostStore.from_qm9_asset(asset, precompute_hops=3)
+    c = feed.HostCollator(3, 2)
+    n, e = c.plan(store, idx)
+    blob, layout, gr, nr, _ = c.collate_blob(store, idx, pinned=False, n_max=n + 20, e_max=e + 50, pad_mols=8)
+    b = adata.DeviceBatch.from_blob(blob, layout, gr, nr, 3)
+    col = adata.pad_collated(adata.collate(asset.molecules(idx), 3), n + 20, e + 50, 64, 8)
+    ref = adata.DeviceBatch(col, "cpu", targets=np.zeros((72, 12), np.float32), csr_hops=3)
+    assert layout == ref._layout
+    a, r = b.edges._aimx_csr, ref.edges._aimx_csr
+    for k in ("fwd_rowptr", "fwd_col", "bwd_rowptr", "bwd_col", "graph_rowptr", "graph_col"):
+        assert torch.equal(getattr(a, k), getattr(r, k)), k
