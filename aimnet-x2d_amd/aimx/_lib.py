@@ -181,6 +181,7 @@ _SIGS = {
     "aimx_head_forward": (c_i32, [ctypes.POINTER(Head), c_ptr]),
     "aimx_head_backward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
     "aimx_head_backward": (c_i32, [ctypes.POINTER(Head), ctypes.POINTER(HeadGrad), c_ptr]),
+    "aimx_dropout_seeds": (c_i32, [c_ptr, c_ptr, c_i32, c_ptr]),
     "aimx_l1_loss_forward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr]),
     "aimx_l1_loss_forward_accum": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr,
                                            ctypes.c_void_p, c_ptr]),

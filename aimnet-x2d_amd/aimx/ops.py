@@ -189,6 +189,41 @@ class _MPStack(torch.autograd.Function):
 _PAD = {}
 
 
+def _ig_in_place(heads, d, k, blk):
+    """The packed [Wi ; Wg ; bi ; bg | pad] x layers block as a view when the parameters already
+    sit at exactly those offsets of one storage (GNN.pack_ig_params), else None."""
+    t0 = heads[0][0]
+    if t0.dtype != _F32 or not t0.is_cuda:
+        return None
+    st = t0.untyped_storage().data_ptr()
+    base = t0.data_ptr()
+    offs = (0, d * k, 2 * d * k, 2 * d * k + d)
+    for l, ps in enumerate(heads):
+        for o, p in zip(offs, ps):
+            if p.dtype != _F32 or not p.is_contiguous() or p.untyped_storage().data_ptr() != st or \
+                    p.data_ptr() != base + 4 * (l * blk + o):
+                return None
+    n = len(heads) * blk
+    if t0.storage_offset() + n > t0.untyped_storage().nbytes() // 4:
+        return None
+    return t0.detach().as_strided((n,), (1,))
+
+
+def pack_ig_params(params, nl, nm, d, k):
+    """Lay every layer's [Wi ; Wg ; bi ; bg] out as _pack_ig's packed block (one storage, padded
+    64-float layer blocks) and point the Parameters at it (same values, same state_dict), so
+    message_passing_stack reads the weights in place instead of a per-step cat."""
+    with torch.no_grad():
+        packed, _, _ = _pack_ig(params, nl, nm, d, k)
+        per = 2 * d * k + 2 * d
+        blk = (per + 63) // 64 * 64
+        packed = packed.clone()
+        offs = (0, d * k, 2 * d * k, 2 * d * k + d)
+        for l in range(nl):
+            for o, p in zip(offs, params[l * (4 + 4 * nm):l * (4 + 4 * nm) + 4]):
+                p.data = packed[l * blk + o:l * blk + o + p.numel()].view(p.shape)
+
+
 def _pack_ig(params, nl, nm, d, k):
     """One cat of every layer's [Wi ; Wg] (each [D, K]) and [bi ; bg]: returns (packed, w_ig views
     [2D, K], b_ig views [2D]); per-layer blocks are padded to a multiple of 64 floats."""
@@ -202,8 +237,13 @@ def _pack_ig(params, nl, nm, d, k):
         if pad is None:
             pad = torch.zeros(blk - per, dtype=_F32, device=dev)
             _PAD[(dev, blk - per)] = pad
-    for l in range(nl):
-        wi, wg, bi, bg = params[l * (4 + 4 * nm):l * (4 + 4 * nm) + 4]
+    heads = [params[l * (4 + 4 * nm):l * (4 + 4 * nm) + 4] for l in range(nl)]
+    packed = _ig_in_place(heads, d, k, blk)
+    if packed is not None:  # GNN.pack_ig_params laid the parameters out this way: no cat
+        w_ig = [packed[l * blk:l * blk + 2 * d * k].view(2 * d, k) for l in range(nl)]
+        b_ig = [packed[l * blk + 2 * d * k:l * blk + per] for l in range(nl)]
+        return packed, w_ig, b_ig
+    for wi, wg, bi, bg in heads:
         parts += [wi.detach().reshape(-1), wg.detach().reshape(-1), bi.detach().reshape(-1), bg.detach().reshape(-1)]
         if pad is not None:
             parts.append(pad)
@@ -211,6 +251,18 @@ def _pack_ig(params, nl, nm, d, k):
     w_ig = [packed[l * blk:l * blk + 2 * d * k].view(2 * d, k) for l in range(nl)]
     b_ig = [packed[l * blk + 2 * d * k:l * blk + per] for l in range(nl)]
     return packed, w_ig, b_ig
+
+
+def dropout_seeds(owner, n, device):
+    """n int64 dropout seeds for one forward, drawn on the device from a counter kept on `owner`
+    (aimx_dropout_seeds; one launch, graph-safe). The counter starts from torch's generator."""
+    st = getattr(owner, "_aimx_seed_state", None)
+    if st is None or st.device != device:
+        st = torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
+        owner._aimx_seed_state = st
+    seeds = torch.empty(n, dtype=torch.int64, device=device)
+    check(_lib.load().aimx_dropout_seeds(ptr(st), ptr(seeds), int(n), stream_ptr(device)), "dropout_seeds")
+    return seeds
 
 
 def _ct_addr(arr):

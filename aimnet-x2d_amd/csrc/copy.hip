@@ -50,6 +50,20 @@ __global__ __launch_bounds__(kThreads) void k_multi_copy(const CopyTable t) {
 
 int64_t slices(int64_t n) { return std::max<int64_t>(1, cdiv(n, kSlice)); }
 
+// Dropout seeds of one forward from a device-resident counter (aimx_dropout_seeds).
+__global__ void k_dropout_seeds(int64_t* __restrict__ state, int64_t* __restrict__ seeds, int32_t n) {
+  if (threadIdx.x != 0) return;
+  const uint64_t s = (uint64_t)state[0];
+  for (int32_t i = 0; i < n; ++i) {
+    uint64_t z = s + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    seeds[i] = (int64_t)(z >> 2);  // [0, 2^62), the range torch.randint(0, 2**62) drew
+  }
+  state[0] = (int64_t)(s + 0x9E3779B97F4A7C15ull * (uint64_t)(n + 1));
+}
+
 }  // namespace
 }  // namespace aimx
 
@@ -75,5 +89,12 @@ extern "C" int aimx_multi_copy(const AimxCopyItem* items, int32_t n_items, aimx_
     hipLaunchKernelGGL(k_multi_copy, dim3((unsigned)b), dim3(kThreads), 0, (hipStream_t)stream, t);
     AIMX_CHECK_LAUNCH();
   }
+  return AIMX_OK;
+}
+
+extern "C" int aimx_dropout_seeds(int64_t* state, int64_t* seeds, int32_t n, aimx_stream_t stream) {
+  if (n < 0 || !state || (n > 0 && !seeds)) return AIMX_EARG;
+  hipLaunchKernelGGL(k_dropout_seeds, dim3(1), dim3(64), 0, (hipStream_t)stream, state, seeds, n);
+  AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }

@@ -77,6 +77,25 @@ class GNN(nn.Module):
         # constructed by the reference (gnn.py:146) but never used in forward
         self.long_range_projection = AimxLinear(hidden_dim, ffn_hidden_dim)
         self.init_weights()
+        self._aimx_pack_ig()
+
+    def _aimx_pack_ig(self):
+        """Input-projection weights of every shell layer laid out as the fused stack's packed block
+        (ops.pack_ig_params): read in place each step instead of one cat per forward."""
+        layers = self.message_passing_layers
+        if len(layers) == 0 or self.use_stereochemistry:
+            return
+        params = []
+        for layer in layers:
+            params += layer._aimx_params()
+        d = layers[0].input_proj.weight.shape[0]
+        k = layers[0].input_proj.weight.shape[1]
+        ops.pack_ig_params(params, len(layers), len(layers[0].mlp_blocks), d, k)
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._aimx_pack_ig()
+        return out
 
     def _create_embeddings(self, feature_sizes: Dict[str, int], embedding_dim: int):
         self.atom_type_embedding = nn.Embedding(feature_sizes["atom_type"], embedding_dim)
@@ -118,7 +137,7 @@ class GNN(nn.Module):
         need = (self.message_passing_layers[0]._aimx_dropout()[0] if len(self.message_passing_layers) else False) or \
             any(b.dropout.training and b.dropout.p > 0 for b in blocks)
         if need:  # (MC-dropout may switch single Dropout modules on in eval mode: follow their flags)
-            seeds = torch.randint(0, 2 ** 62, (1 + len(blocks),), device=atom_embeddings.device, dtype=torch.int64)
+            seeds = ops.dropout_seeds(self, 1 + len(blocks), atom_embeddings.device)
             self._aimx_stack_seed = seeds[0:1]
             for i, blk in enumerate(blocks):
                 blk._aimx_seed = seeds[1 + i:2 + i]
@@ -201,7 +220,7 @@ class GNN(nn.Module):
         training, p = first._aimx_dropout()
         seed = getattr(self, "_aimx_stack_seed", None)
         if training and seed is None:
-            seed = torch.randint(0, 2 ** 62, (1,), device=x_other.device, dtype=torch.int64)
+            seed = ops.dropout_seeds(self, 1, x_other.device)
         if not self.use_stereochemistry:
             params = []
             for layer in layers:

@@ -451,6 +451,12 @@ typedef struct {
 } AimxCopyItem;
 int aimx_multi_copy(const AimxCopyItem* items, int32_t n_items, aimx_stream_t stream);
 
+/* Dropout seeds of one forward: seeds[0..n) in [0, 2^62) from the device-resident counter state[0]
+ * (a splitmix64 sequence), which advances. Replaces the per-forward torch.randint draw, whose
+ * CUDA-graph capture adds two generator-state fill launches to every replay; the model seeds the
+ * state once from torch's generator, so torch.manual_seed still fixes the masks. */
+int aimx_dropout_seeds(int64_t* state, int64_t* seeds, int32_t n, aimx_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Gradient all-reduce over RCCL (xGMI inside an MI355X node) — the DDP reducer's collective
  * (reference runner.py:703-707 wraps the model in DistributedDataParallel over "nccl" = RCCL).

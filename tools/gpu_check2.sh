@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU box: -m gpu suite, bench line, c2 kernel sequence, and the op -> kernel map of one eager step.
+set -o pipefail
+export TMPDIR=/tmp
+R=gpurun_out/check
+mkdir -p $R
+tools/gpu_steps.sh "900 check/tests.log python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
+  "400 check/bench.log python3 bench.py --no-cpu-baseline" \
+  "300 check/opk.log python3 tools/op_kernels.py" \
+  "300 check/c2trace.log rocprofv3 --kernel-trace --output-format csv -d $R/c2 -- python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3" || exit $?
+python3 tools/step_seq.py $R/c2 > $R/c2_seq.txt 2>&1
+rm -rf $R/c2
+tail -1 $R/c2_seq.txt

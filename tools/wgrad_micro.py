@@ -1,5 +1,6 @@
-"""Graph-timed aimx_wgrad_grouped on the c2 stack's 15 weight-gradient problems (3 layers x
-[dW_ig 152 x 304 + bias, 4 x dW_mlp 76 x 76 + bias], K = 9170)."""
+"""Graph-timed aimx_wgrad_grouped on a stack's 15 weight-gradient problems (3 layers x
+[dW_ig 2D x 2D + bias (the trimmed input projection), 4 x dW_mlp D x D + bias]), K = atoms.
+usage: python tools/wgrad_micro.py [c2|c4|c5] [KPER,KPER,...]   (AIMX_WGRAD_KPER sweep)"""
 import ctypes
 import json
 import os
@@ -15,9 +16,12 @@ from aimx import _lib  # noqa: E402
 def main():
     lib = _lib.load()
     dev = torch.device("cuda")
-    K = 9170
-    shapes = [(152, 304)] + [(76, 76)] * 4
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    K, D = {"c2": (9170, 76), "c4": (20480, 153), "c5": (10240, 307)}[cfg]
+    kpers = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
+    shapes = [(2 * D, 2 * D)] + [(D, D)] * 4
     shapes = shapes * 3
+    flops = sum(2 * M * (N + 1) * K for M, N in shapes)
     bufs = []
     arr = (_lib.WgradProblem * len(shapes))()
     for i, (M, N) in enumerate(shapes):
@@ -30,8 +34,14 @@ def main():
     n = len(shapes)
     ws = torch.empty(lib.aimx_wgrad_grouped_workspace_bytes(arr, n) // 4 + 1, device=dev)
     cnt = _lib.counters(dev)
-    res = {}
-    for path in ("current",):
+    res = {"config": cfg, "K": K, "D": D, "gflop": round(flops / 1e9, 2)}
+    for kper in kpers:
+        path = f"kper{kper}" if kper else "default"
+        if kper:
+            os.environ["AIMX_WGRAD_KPER"] = str(kper)
+        else:
+            os.environ.pop("AIMX_WGRAD_KPER", None)
+        ws = torch.empty(lib.aimx_wgrad_grouped_workspace_bytes(arr, n) // 4 + 1, device=dev)
         fn = lambda: lib.aimx_wgrad_grouped(arr, n, ws.data_ptr(), ws.numel() * 4, cnt.data_ptr(), _lib.N_COUNTERS,
                                             torch.cuda.current_stream().cuda_stream)
         s = torch.cuda.Stream()
@@ -51,7 +61,9 @@ def main():
             g.replay()
         t1.record()
         t1.synchronize()
-        res[path + "_us"] = round(t0.elapsed_time(t1) / 50 * 1e3, 1)
+        us = t0.elapsed_time(t1) / 50 * 1e3
+        res[path + "_us"] = round(us, 1)
+        res[path + "_tfs"] = round(flops / us / 1e6, 1)
     print(json.dumps(res), flush=True)
 
 
