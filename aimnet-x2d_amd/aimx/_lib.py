@@ -52,6 +52,7 @@ class GemmArgs(ctypes.Structure):
         ("splits", c_i32), ("workspace", c_ptr), ("workspace_bytes", c_size),
         ("counters", c_ptr), ("n_counters", c_i64),
         ("zc_rowptr", c_ptr), ("zc_rows", c_i64), ("zc_chunks", c_i32), ("zc_width", c_i64), ("zc_dim", c_i32),
+        ("precision", c_i32),
     ]
 
 
@@ -69,7 +70,7 @@ class ShellStack(ctypes.Structure):
         ("x_in", c_ptr), ("x_in_ld", c_i64),
         ("out", c_ptr), ("out_ld", c_i64),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
-        ("counters", c_ptr), ("n_counters", c_i64),
+        ("counters", c_ptr), ("n_counters", c_i64), ("precision", c_i32),
     ]
 
 

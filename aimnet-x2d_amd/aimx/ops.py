@@ -94,6 +94,7 @@ class _MPStack(torch.autograd.Function):
         s = ShellStack()
         s.N, s.D, s.num_hops, s.num_layers, s.num_mlp = n, d, h, nl, nm
         s.act, s.use_pc, s.training, s.mode_single = spec["act"], int(spec["use_pc"]), int(drop), int(spec["single"])
+        s.precision = spec["prec"]
         s.drop_p = float(spec["drop_p"]) if drop else 0.0
         s.drop_seed = ptr(drop_seed) if drop else None
         s.fwd_rowptr, s.fwd_col = ptr(plan.fwd.rowptr), ptr(plan.fwd.col)
@@ -148,6 +149,7 @@ class _MPStack(torch.autograd.Function):
         s = ShellStack()
         s.N, s.D, s.num_hops, s.num_layers, s.num_mlp = n, d, h, nl, nm
         s.act, s.use_pc, s.training, s.mode_single = spec["act"], int(spec["use_pc"]), int(st["drop"]), int(spec["single"])
+        s.precision = spec["prec"]
         s.drop_p = float(spec["drop_p"]) if st["drop"] else 0.0
         s.drop_seed = ptr(st["seed"]) if st["drop"] else None
         s.fwd_rowptr, s.fwd_col = ptr(plan.fwd.rowptr), ptr(plan.fwd.col)
@@ -280,7 +282,7 @@ def message_passing_stack(plan, x, params, *, num_hops, num_layers, num_mlp, act
     n, d = x.shape
     spec = dict(N=n, D=d, num_hops=num_hops, num_layers=num_layers, num_mlp=num_mlp, act=_lib.ACT_KIND[act]
                 if isinstance(act, str) else int(act), use_pc=bool(use_pc), training=bool(training),
-                drop_p=float(drop_p), single=bool(single))
+                drop_p=float(drop_p), single=bool(single), prec=amp_precision())
     if use_pc and (plan.graph is None or total_charges is None):
         raise _lib.AimxError("aimx: partial charges need batch indices and total charges")
     tc = total_charges.contiguous().float() if total_charges is not None else None
@@ -504,10 +506,23 @@ def partial_charges(plan, x, total_charges):
 # ---------------------------------------------------------------------------------------------
 # Dense layers on the fused fp32 MFMA GEMM (nn.Linear semantics, optional fused activation)
 # ---------------------------------------------------------------------------------------------
-def _gemm_args(M, N, K):
+PREC_FP32, PREC_BF16 = 0, 1  # AimxGemmArgs.precision (include/aimx.h)
+
+
+def amp_precision():
+    """The GEMM precision of the reference's --mixed_precision path (trainer.py:134): inside
+    torch.autocast('cuda') the node-update / dense GEMMs take bf16 operands (fp32 accumulation and
+    fp32 outputs; whatever the autocast dtype, bf16 is the MI355X choice: fp32 range, no loss
+    scaling needed); otherwise exact fp32, the parity path. Autograd Functions record it at
+    forward (ctx.prec) and their backward GEMMs use the same."""
+    return PREC_BF16 if torch.is_autocast_enabled("cuda") else PREC_FP32
+
+
+def _gemm_args(M, N, K, prec=PREC_FP32):
     a = _lib.GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.act, a.dact_kind = -1, -1
+    a.precision = prec
     return a
 
 
@@ -524,11 +539,11 @@ def _run_gemm(a, dev):
     return ws
 
 
-def gemm_linear_fwd(x, ldx, W, b, out, ldo, act=-1, pre=None):
+def gemm_linear_fwd(x, ldx, W, b, out, ldo, act=-1, pre=None, prec=PREC_FP32):
     """out[M, n_out] = act(x[M, n_in] W^T + b)  (pre-activation to `pre` when act >= 0)."""
     M, n_in = x.shape
     n_out = W.shape[0]
-    a = _gemm_args(M, n_out, n_in)
+    a = _gemm_args(M, n_out, n_in, prec)
     a.A, a.sam, a.sak = ptr(x), ldx, 1
     a.B, a.sbk, a.sbn = ptr(W), 1, n_in
     a.C, a.ldc = ptr(out), ldo
@@ -540,18 +555,18 @@ def gemm_linear_fwd(x, ldx, W, b, out, ldo, act=-1, pre=None):
     return _run_gemm(a, x.device)
 
 
-def gemm_linear_bwd(dy, ldy, x, ldx, W, dx, dW, db):
+def gemm_linear_bwd(dy, ldy, x, ldx, W, dx, dW, db, prec=PREC_FP32):
     """dx = dy W ; dW = dy^T x ; db = sum_rows dy (ones-column fusion, split-K)."""
     M, n_out = dy.shape
     n_in = W.shape[1]
     dev = dy.device
     if dx is not None:
-        a = _gemm_args(M, n_in, n_out)
+        a = _gemm_args(M, n_in, n_out, prec)
         a.A, a.sam, a.sak = ptr(dy), ldy, 1
         a.B, a.sbk, a.sbn = ptr(W), n_in, 1
         a.C, a.ldc = ptr(dx), n_in
         _run_gemm(a, dev)
-    a = _gemm_args(n_out, n_in + 1, M)
+    a = _gemm_args(n_out, n_in + 1, M, prec)
     a.A, a.sam, a.sak = ptr(dy), 1, ldy
     a.B, a.sbk, a.sbn = ptr(x), ldx, 1
     a.C, a.ldc = ptr(dW), n_in
@@ -576,7 +591,9 @@ class _Linear(torch.autograd.Function):
         M = x2.shape[0]
         out = torch.empty(M, W.shape[0], dtype=_F32, device=x.device)
         pre = torch.empty_like(out) if act >= 0 else None
-        gemm_linear_fwd(x2, ldx, W.contiguous(), b.contiguous() if b is not None else None, out, W.shape[0], act, pre)
+        ctx.prec = amp_precision()
+        gemm_linear_fwd(x2, ldx, W.contiguous(), b.contiguous() if b is not None else None, out, W.shape[0], act, pre,
+                        ctx.prec)
         ctx.act, ctx.ldx, ctx.shape, ctx.has_b = act, ldx, shape, b is not None
         ctx.save_for_backward(x2, W, pre)
         return out.view(*shape[:-1], W.shape[0])
@@ -591,7 +608,7 @@ class _Linear(torch.autograd.Function):
         dx = torch.empty(x2.shape[0], W.shape[1], dtype=_F32, device=dy.device) if ctx.needs_input_grad[0] else None
         dW = torch.empty_like(W)
         db = torch.empty(W.shape[0], dtype=_F32, device=dy.device)
-        gemm_linear_bwd(dy2, ldy, x2, ctx.ldx, W.contiguous(), dx, dW, db)
+        gemm_linear_bwd(dy2, ldy, x2, ctx.ldx, W.contiguous(), dx, dW, db, ctx.prec)
         dx = dx.view(*ctx.shape[:-1], W.shape[1]) if dx is not None else None
         return dx, dW, (db if ctx.has_b else None), None
 
@@ -637,7 +654,8 @@ class _EmbedProject(torch.autograd.Function):
         check(lib.aimx_embedding_gather(ctypes.byref(ts), n, ptr(E), width, stream_ptr(dev)), "embedding_gather")
         out = torch.empty(n, W.shape[0], dtype=_F32, device=dev)
         pre = torch.empty_like(out) if act >= 0 else None
-        gemm_linear_fwd(E, width, W.contiguous(), b.contiguous(), out, W.shape[0], act, pre)
+        ctx.prec = amp_precision()
+        gemm_linear_fwd(E, width, W.contiguous(), b.contiguous(), out, W.shape[0], act, pre, ctx.prec)
         ctx.act = act
         ctx.idx = idx
         ctx.save_for_backward(E, W, pre, *tables)
@@ -653,7 +671,7 @@ class _EmbedProject(torch.autograd.Function):
         dE = torch.empty_like(E)
         dW = torch.empty_like(W)
         db = torch.empty(W.shape[0], dtype=_F32, device=dev)
-        gemm_linear_bwd(dpre, dpre.shape[1], E, E.shape[1], W.contiguous(), dE, dW, db)
+        gemm_linear_bwd(dpre, dpre.shape[1], E, E.shape[1], W.contiguous(), dE, dW, db, ctx.prec)
         grads = [torch.empty_like(t) for t in tables]
         ts = _tables_struct(ctx.idx, tables, grads)
         wsb = lib.aimx_embedding_backward_workspace_bytes(ctypes.byref(ts), E.shape[0])
@@ -702,6 +720,7 @@ class _LinearBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W1, b1, W2, b2, act, drop_p, skip, seed):
+        ctx.prec = amp_precision()
         dev = x.device
         shape = x.shape
         x2, ldx = _rows(x.reshape(-1, shape[-1]))
@@ -712,7 +731,7 @@ class _LinearBlock(torch.autograd.Function):
         V = torch.empty(M, n_out, dtype=_F32, device=dev)
         drop = seed is not None and drop_p > 0
         mask = torch.empty(M, n_out, dtype=torch.uint8, device=dev) if drop else None
-        a = _gemm_args(M, n_out, n_in)
+        a = _gemm_args(M, n_out, n_in, ctx.prec)
         a.A, a.sam, a.sak = ptr(x2), ldx, 1
         a.B, a.sbk, a.sbn = ptr(W1), 1, n_in
         a.C, a.ldc = ptr(H), n_out
@@ -723,7 +742,7 @@ class _LinearBlock(torch.autograd.Function):
             a.mask_out, a.ldmask = ptr(mask), n_out
         _run_gemm(a, dev)
         Y = torch.empty(M, n_out, dtype=_F32, device=dev)
-        a = _gemm_args(M, n_out, n_out)
+        a = _gemm_args(M, n_out, n_out, ctx.prec)
         a.A, a.sam, a.sak = ptr(H), n_out, 1
         a.B, a.sbk, a.sbn = ptr(W2), 1, n_out
         a.C, a.ldc = ptr(Y), n_out
@@ -743,7 +762,7 @@ class _LinearBlock(torch.autograd.Function):
         n_out = W1.shape[0]
         dY, ldy = _rows(dy.reshape(-1, n_out))
         dV = torch.empty(M, n_out, dtype=_F32, device=dev)
-        a = _gemm_args(M, n_out, n_out)  # dV = (dY W2) * mask/(1-p) * act'(V)
+        a = _gemm_args(M, n_out, n_out, ctx.prec)  # dV = (dY W2) * mask/(1-p) * act'(V)
         a.A, a.sam, a.sak = ptr(dY), ldy, 1
         a.B, a.sbk, a.sbn = ptr(W2), n_out, 1
         a.C, a.ldc = ptr(dV), n_out
@@ -754,7 +773,7 @@ class _LinearBlock(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, n_in, dtype=_F32, device=dev)
-            a = _gemm_args(M, n_in, n_out)  # dx = dV W1 [+ dY]
+            a = _gemm_args(M, n_in, n_out, ctx.prec)  # dx = dV W1 [+ dY]
             a.A, a.sam, a.sak = ptr(dV), n_out, 1
             a.B, a.sbk, a.sbn = ptr(W1), n_in, 1
             a.C, a.ldc = ptr(dx), n_in

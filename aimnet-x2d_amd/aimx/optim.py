@@ -125,18 +125,23 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         hyper_g = self._shared_hyper()
-        # the tensor table is rebuilt only when the set of stepped parameters or a gradient's
-        # address changed (steady state: the caching allocator hands autograd the same blocks)
-        key = []
-        for group in self.param_groups:
-            for p in group["params"]:
-                g = p.grad
-                key.append(p.data_ptr())
-                key.append(0 if g is None else g.data_ptr())
-        key = tuple(key)
+        # the tensor table is rebuilt only when the set of stepped parameters changed (or a
+        # parameter moved); a gradient that merely lives at a new address (eager steps with
+        # zero_grad(set_to_none=True)) is patched into its row
+        key = tuple((p.data_ptr(), p.grad is not None) for group in self.param_groups for p in group["params"])
         if key != self._table_key:
             self._build_table()
             self._table_key = key
+        elif self._arr is not None:
+            arr = self._arr
+            for i, row in enumerate(self._rows):
+                g = row[0].grad
+                gp = g.data_ptr()
+                if gp != arr[i].grad:
+                    if g.dtype != torch.float32 or not g.is_contiguous() or not g.is_cuda:
+                        raise AimxError("FusedAdam: gradients must be contiguous fp32 device tensors")
+                    arr[i].grad = gp
+                    self._rows[i] = (row[0], g) + tuple(row[2:])
         if self._arr is None:
             return loss
         rows, arr, dev = self._rows, self._arr, self._dev

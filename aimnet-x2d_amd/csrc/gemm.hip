@@ -207,9 +207,18 @@ __device__ __forceinline__ void zero_tile(const AimxGemmArgs& a, int m0, int n0,
 // operand to be a multiple of 4 floats and 16-byte aligned rows (checked by the host), so a float4
 // is wholly valid or wholly outside: invalid ones are pointed past the descriptor's extent and
 // read as zeros (an address select — no value select for hipcc to turn into a branch).
-template <int BM, int BN, bool AK, bool BKC, bool V4>
+// BF (AimxGemmArgs.precision == AIMX_PREC_BF16, the AMP path): operands are rounded to bf16 (RNE)
+// as they are staged into LDS, always as a k-contiguous [m][k] / [n][k] image (row stride BK + 8
+// bf16 = 80 B: the 16-byte fragment reads of a 16-lane group hit disjoint banks), and each 32-deep
+// slice is ONE v_mfma_f32_16x16x32_bf16 per fragment pair (fp32 accumulation, fp32 epilogue).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, bool AK, bool BKC, bool V4, bool BF>
 __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
   constexpr int BK = kBK;
+  constexpr int SH = BK + 8;                       // BF: bf16 row stride of both LDS images
+  constexpr int LAH = BM * SH, LBH = BN * SH;      // BF: bf16 elements per stage and operand
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int SA = AK ? BK + 2 : BM + 16;
@@ -350,6 +359,52 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     }
   };
   auto store_slice = [&](const float (&ra)[NA], const float (&rb)[NB], int stage) {
+    if constexpr (BF) {
+      __bf16* Ah = reinterpret_cast<__bf16*>(smem) + stage * (LAH + LBH);
+      __bf16* Bh = Ah + LAH;
+      if constexpr (V4) {
+#pragma unroll
+        for (int i = 0; i < NA4; ++i) {
+          const int q = tid + i * 256;
+          const int mm = AK ? q / (BK / 4) : (q % (BM / 4)) * 4;
+          const int kk = AK ? (q % (BK / 4)) * 4 : q / (BM / 4);
+          if (AK) {
+            *reinterpret_cast<bf16x4*>(&Ah[mm * SH + kk]) =
+                bf16x4{(__bf16)ra[4 * i], (__bf16)ra[4 * i + 1], (__bf16)ra[4 * i + 2], (__bf16)ra[4 * i + 3]};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Ah[(mm + e) * SH + kk] = (__bf16)ra[4 * i + e];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NB4; ++i) {
+          const int q = tid + i * 256;
+          const int nn = BKC ? q / (BK / 4) : (q % (BN / 4)) * 4;
+          const int kk = BKC ? (q % (BK / 4)) * 4 : q / (BN / 4);
+          if (BKC) {
+            *reinterpret_cast<bf16x4*>(&Bh[nn * SH + kk]) =
+                bf16x4{(__bf16)rb[4 * i], (__bf16)rb[4 * i + 1], (__bf16)rb[4 * i + 2], (__bf16)rb[4 * i + 3]};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Bh[(nn + e) * SH + kk] = (__bf16)rb[4 * i + e];
+          }
+        }
+        return;
+      }
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int mm = AK ? a_m + i * A_STEP : a_m;
+        const int kk = AK ? a_k : a_k + i * A_STEP;
+        Ah[mm * SH + kk] = (__bf16)ra[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int nn = BKC ? b_n + i * B_STEP : b_n;
+        const int kk = BKC ? b_k : b_k + i * B_STEP;
+        Bh[nn * SH + kk] = (__bf16)rb[i];
+      }
+      return;
+    }
     float* As = smem + stage * (LA + LB);
     float* Bs = As + LA;
     if constexpr (V4) {
@@ -395,6 +450,22 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     }
   };
   auto compute_slice = [&](int stage) {
+    if constexpr (BF) {
+      const __bf16* Ah = reinterpret_cast<const __bf16*>(smem) + stage * (LAH + LBH);
+      const __bf16* Bh = Ah + LAH;
+      bf16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(&Ah[(wr * WM + i * 16 + (lane & 15)) * SH + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[j] = *reinterpret_cast<const bf16x8*>(&Bh[(wc * WN + j * 16 + (lane & 15)) * SH + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      return;
+    }
     const float* As = smem + stage * (LA + LB);
     const float* Bs = As + LA;
 #pragma unroll
@@ -997,6 +1068,8 @@ struct Plan {
 // Weight-gradient layout (A m-contiguous, B n-contiguous) with a long K: k_wgrad.
 inline bool is_wgrad(const AimxGemmArgs& a) {
   static const bool off = getenv("AIMX_GEMM_NO_WGRAD") != nullptr;  // A/B experiments only
+  // (also under AIMX_PREC_BF16: long-K weight gradients stay exact fp32 on k_wgrad — the tiled
+  // kernel at these shapes, ~150 workgroups, measured 3-5x slower: profiles/r02_c4_amp_seq.txt)
   return !off && a.sam == 1 && a.sbn == 1 && a.sak != 1 && a.K >= 512;
 }
 
@@ -1056,26 +1129,34 @@ bool v4_ok(const AimxGemmArgs& a) {
   return true;
 }
 
-template <int BM, int BN, bool V4>
+template <int BM, int BN, bool V4, bool BF>
 void launch_tile_v(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
   const bool ak = (a.sak == 1), bk = (a.sbk == 1);
   const int kc = (int)p.kchunk;
   if (ak && bk)
-    hipLaunchKernelGGL((k_gemm<BM, BN, true, true, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, true, true, V4, BF>), grid, dim3(256), 0, s, a, kc, ab, bb);
   else if (ak)
-    hipLaunchKernelGGL((k_gemm<BM, BN, true, false, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, true, false, V4, BF>), grid, dim3(256), 0, s, a, kc, ab, bb);
   else if (bk)
-    hipLaunchKernelGGL((k_gemm<BM, BN, false, true, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, false, true, V4, BF>), grid, dim3(256), 0, s, a, kc, ab, bb);
   else
-    hipLaunchKernelGGL((k_gemm<BM, BN, false, false, V4>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    hipLaunchKernelGGL((k_gemm<BM, BN, false, false, V4, BF>), grid, dim3(256), 0, s, a, kc, ab, bb);
 }
 
 template <int BM, int BN>
 void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
-  if (v4_ok(a))
-    launch_tile_v<BM, BN, true>(a, p, grid, s, ab, bb);
-  else
-    launch_tile_v<BM, BN, false>(a, p, grid, s, ab, bb);
+  const bool bf = a.precision == AIMX_PREC_BF16;
+  if (v4_ok(a)) {
+    if (bf)
+      launch_tile_v<BM, BN, true, true>(a, p, grid, s, ab, bb);
+    else
+      launch_tile_v<BM, BN, true, false>(a, p, grid, s, ab, bb);
+  } else {
+    if (bf)
+      launch_tile_v<BM, BN, false, true>(a, p, grid, s, ab, bb);
+    else
+      launch_tile_v<BM, BN, false, false>(a, p, grid, s, ab, bb);
+  }
 }
 
 }  // namespace
@@ -1182,6 +1263,7 @@ size_t gemm_workspace_floats(const AimxGemmArgs& a) {
 int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   AimxGemmArgs a = a_in;
   if (a.M < 0 || a.N < 0 || a.K < 0) return AIMX_EARG;
+  if (a.precision != AIMX_PREC_FP32 && a.precision != AIMX_PREC_BF16) return AIMX_EARG;
   if (a.M == 0 || a.N == 0) return AIMX_OK;
   if (a.ones_col && (!a.col_out || a.N < 1)) return AIMX_EARG;
   if ((a.mask_out || a.mask_in) && !(a.drop_p < 1.f)) return AIMX_EARG;

@@ -113,6 +113,7 @@ struct Ws {
   size_t bytes;
   int32_t* counters;
   int64_t n_counters;
+  int32_t precision;
 };
 
 int run(AimxGemmArgs a, const Ws& ws, hipStream_t s) {
@@ -120,6 +121,7 @@ int run(AimxGemmArgs a, const Ws& ws, hipStream_t s) {
   a.workspace_bytes = ws.bytes;
   a.counters = ws.counters;
   a.n_counters = ws.n_counters;
+  a.precision = ws.precision;
   return launch_gemm(a, s);
 }
 
@@ -182,7 +184,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
   if (N == 0) return AIMX_OK;
-  const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters};
+  const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters, s->precision};
   const bool drop = s->training && s->drop_p > 0.f;
   for (int64_t l = 0; l < L; ++l) {
     float* F = s->F[l];
@@ -380,7 +382,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   const bool aux = g->aux_stream && g->events && g->n_events >= L + 1 && s->counters && s->n_counters >= 2;
   hipStream_t ast = (hipStream_t)g->aux_stream;
   const int64_t main_counters = aux ? s->n_counters / 2 : s->n_counters;
-  const Ws ws{s->workspace, s->workspace_bytes, s->counters, main_counters};
+  const Ws ws{s->workspace, s->workspace_bytes, s->counters, main_counters, s->precision};
   int32_t* aux_cnt = aux ? s->counters + main_counters : nullptr;
   const int64_t aux_ncnt = aux ? s->n_counters - main_counters : 0;
   float* wg_ws = base + lay.wg;

@@ -498,6 +498,9 @@ def main():
     ap.add_argument("--stream-mols", type=int, default=200_000, help="molecules in the --feed stream file")
     ap.add_argument("--stream-path", default=None, help="--feed stream file (default: generated under $TMPDIR)")
     ap.add_argument("--feed-threads", type=int, default=4)
+    ap.add_argument("--amp", action="store_true",
+                    help="the reference's --mixed_precision path (trainer.py:134): the step runs under "
+                         "torch.autocast('cuda', bfloat16) -> bf16 MFMA operands, fp32 accumulation in the GEMMs")
     ap.add_argument("--no-eager", action="store_true", help="skip the eager (no-graph) side measurement")
     ap.add_argument("--eager-steps", type=int, default=20)
     ap.add_argument("--ddp-world1", action="store_true",
@@ -565,7 +568,8 @@ def main():
         # backward, the bucketed RCCL all-reduces overlapped with the backward (world > 1), clip and
         # Adam; each timed step copies a fresh resident batch into the static inputs and replays.
         from aimx.train import GraphedTrainStep
-        graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.amp):  # captured in the context
+            graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync)
 
         def step(i):
             graphed(next(feeder) if feeder is not None else batches[i % len(batches)])
@@ -573,8 +577,9 @@ def main():
         def step(i):
             b = next(feeder) if feeder is not None else batches[i % len(batches)]
             opt.zero_grad(set_to_none=True)
-            out, _, _ = model(*b.model_args())
-            loss = loss_fn(out[:B], b.targets[:B])
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.amp):
+                out, _, _ = model(*b.model_args())
+                loss = loss_fn(out[:B], b.targets[:B])
             loss.backward()
             if sync is not None:
                 sync.finish()
@@ -612,7 +617,7 @@ def main():
     value = mol / dt
 
     eager = None
-    if rank == 0 and world == 1 and args.graph and feeder is None and not args.no_eager:
+    if rank == 0 and world == 1 and args.graph and feeder is None and not args.no_eager and not args.amp:
         eager = eager_rate(cfg, device, batches_eager=4, steps=args.eager_steps)
     roof = extra = None
     if rank == 0 and not args.no_roofline:
@@ -642,7 +647,9 @@ def main():
             "metric": "molecules/sec fwd+bwd on QM9-shaped batches; achieved HBM GB/s on scatter-add hop",
             "value": round(value, 1), "unit": "molecules/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 GEMM operands, fp32 accumulation and tensors (AMP)" if args.amp else "fp32",
+            "data": "synthetic",
             "config": {"workload": f"{args.config}: " + ("QM9-shaped" if cfg["source"] == "qm9" else "40-atom synthetic")
                        + f", hidden {cfg['hidden']}, {cfg['hops']} hops, {cfg['tasks']} task(s), attention pool, "
                        "train step fwd+bwd+clip+Adam, dropout 0.05"

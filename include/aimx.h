@@ -151,7 +151,15 @@ typedef struct AimxGemmArgs {
    *             written as 0 without loads or MFMA work (plain-store epilogue only).
    * Results are identical to the untrimmed product (only exact zeros are skipped). */
   const int32_t* zc_rowptr; int64_t zc_rows; int32_t zc_chunks; int64_t zc_width; int32_t zc_dim;
+  /* AIMX_PREC_FP32 (0, the parity path): exact fp32 products (v_mfma_f32_16x16x4_f32).
+   * AIMX_PREC_BF16 (1, the mixed-precision path of the reference's --mixed_precision, trainer.py:
+   * 134/238): A and B rounded to bf16 (RNE) when staged, products accumulated in fp32
+   * (v_mfma_f32_16x16x32_bf16); C, the epilogue and every other tensor stay fp32. Long-K
+   * weight-gradient GEMMs (A m-contiguous, B n-contiguous, K >= 512) stay exact fp32. */
+  int32_t precision;
 } AimxGemmArgs;
+#define AIMX_PREC_FP32 0
+#define AIMX_PREC_BF16 1
 
 size_t aimx_gemm_workspace_bytes(const AimxGemmArgs* args);
 int aimx_gemm(const AimxGemmArgs* args, aimx_stream_t stream);
@@ -187,6 +195,7 @@ typedef struct AimxShellStack {
   float* out; int64_t out_ld;
   float* workspace; size_t workspace_bytes;
   int32_t* counters; int64_t n_counters; /* as in AimxGemmArgs */
+  int32_t precision; /* AIMX_PREC_*: of the stack's node-update GEMMs (weight gradients stay fp32) */
 } AimxShellStack;
 
 typedef struct AimxShellStackGrad {

@@ -1,0 +1,89 @@
+"""Mixed-precision (AMP) path: the reference's --mixed_precision (trainer.py:134 autocast, 238
+GradScaler) on MI355X = bf16 MFMA operands with fp32 accumulation in every node-update / dense GEMM
+(AimxGemmArgs.precision = AIMX_PREC_BF16), everything else fp32. fp32 stays the parity path.
+
+Tolerances (stated here):
+  * kernel level: against the fp64 product of the bf16-rounded operands, norm-relative 2e-5 (only
+    the fp32 accumulation differs), and provably NOT the exact-fp32 product (> 1e-4 away);
+  * model level (c2 golden case, forward + backward under torch.autocast): every output and
+    parameter gradient within 3e-2 norm-relative of the fp64 oracle — bf16 has an 8-bit mantissa
+    (2^-9 relative rounding per operand) — and the loss of a short AMP training run tracks the fp32
+    run's."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import norm_rel
+from golden_cases import case_stereo, load_case
+from test_gpu_parity import _build_model, _gemm, _oracle_run
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("M,N,K,layout", [
+    (9170, 152, 304, "NT"), (9170, 76, 76, "NT"), (1000, 304, 152, "NN"), (2049, 153, 153, "NT"),
+    (153, 613, 2000, "TN"), (256, 257, 9186, "TN"), (17, 5, 3, "NT"), (1027, 77, 301, "TT"), (512, 512, 512, "NT")])
+def test_gemm_bf16_operands_fp32_accumulate(M, N, K, layout):
+    C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True, prec=1)
+    err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-5, err
+    C32, _, _, ref32, _ = _gemm(M, N, K, layout, bias=True, res=True, prec=0)
+    if K >= 16:  # the bf16 path really ran: far from the exact fp32 product
+        assert (C.double() - ref32).abs().max().item() / ref32.abs().max().item() > 1e-4
+
+
+def test_model_under_autocast_bf16():
+    z, cfg, inputs = load_case("c2")
+    torch.set_num_threads(8)
+    ref64 = _oracle_run(z, cfg, inputs, torch.float64)
+    model = _build_model(cfg, int(z["seed"]))
+    af, edges, batch, tc = load_case("c2", DEV)[2]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out, attn, _ = model(af, edges, batch, tc, *case_stereo(z, DEV))
+        assert out.dtype == torch.float32
+    (out * torch.from_numpy(z["loss_w"]).to(DEV)).sum().backward()
+    ours = {"out": out.detach().cpu().numpy(), "attn": attn.detach().cpu().numpy()}
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            ours["grad." + k] = p.grad.cpu().numpy()
+    errs = {k: norm_rel(v, ref64[k]) for k, v in ours.items() if k in ref64}
+    for k in [k for k in errs if ".attention_weights." in k and k.endswith(".bias")]:
+        # exact value 0 (softmax shift invariance): judged against its weight gradient's scale,
+        # as tests/conftest.py parity_failures does
+        w = ref64[k[:-len("bias")] + "weight"]
+        errs[k] = float(np.abs(ours[k] - ref64[k]).max() / np.abs(w).max())
+    assert len(errs) >= 60
+    bad = {k: e for k, e in errs.items() if e > 3e-2}
+    assert not bad, bad
+    assert errs["out"] > 1e-5, "autocast did not switch the GEMMs to bf16 operands"
+    # outside autocast the same model is back on the exact fp32 path
+    model.zero_grad(set_to_none=True)
+    out32, _, _ = model(af, edges, batch, tc, *case_stereo(z, DEV))
+    assert norm_rel(out32.detach().cpu().numpy(), ref64["out"]) < 1e-5
+
+
+def test_amp_training_tracks_fp32():
+    """A few graph-replayed train steps under autocast (captured inside the autocast context) track
+    the fp32 steps' losses (same data, same init) within a few percent."""
+    import bench
+    from aimx.optim import FusedAdam
+    from aimx.train import GraphedTrainStep
+    from models import L1Loss
+    cfg = dict(bench.CONFIGS["c2"], batch=128)
+    bs = bench.make_batches(cfg, 4, 3, DEV, pad=True)
+    losses = {}
+    for amp in (False, True):
+        torch.manual_seed(0)
+        m = bench.build_model(cfg, DEV)
+        opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=128, warmup=1)
+        ls = []
+        for i in range(12):
+            before = g.loss_sum.item()
+            g(bs[i % 4])
+            ls.append((g.loss_sum.item() - before) / 128)
+        losses[amp] = np.array(ls)
+    assert np.all(np.isfinite(losses[True]))
+    np.testing.assert_allclose(losses[True], losses[False], rtol=5e-2, atol=1e-3)

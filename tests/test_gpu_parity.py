@@ -217,6 +217,7 @@ def _gemm(M, N, K, layout, **epi):
     if ones:
         a.ones_col, a.col_out = 1, col.data_ptr()
     a.splits = epi.get("splits", 0)
+    a.precision = epi.get("prec", 0)
     if epi.get("zc") is not None:
         rp, rows, chunks, width, dim = epi["zc"]
         a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width, a.zc_dim = rp.data_ptr(), rows, chunks, width, dim
@@ -229,7 +230,10 @@ def _gemm(M, N, K, layout, **epi):
     torch.cuda.synchronize()
     Am = A if layout[0] == "N" else A.t()
     Bm = B if layout[1] == "N" else B.t()
-    ref = Am.double() @ Bm.double()
+    if epi.get("prec", 0) == 1:  # bf16 operands (RNE), exact products accumulated in fp64 here
+        ref = Am.to(torch.bfloat16).double() @ Bm.to(torch.bfloat16).double()
+    else:
+        ref = Am.double() @ Bm.double()
     if bias is not None:
         ref = ref + bias.cpu().double()
     if res is not None:
