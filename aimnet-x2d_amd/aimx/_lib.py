@@ -28,6 +28,20 @@ class AimxError(RuntimeError):
     pass
 
 
+class Stereo(ctypes.Structure):
+    """AimxStereo (include/aimx.h): the stereochemistry feature op's arguments."""
+    _fields_ = [("x", ctypes.c_void_p), ("ldx", ctypes.c_int64), ("N", ctypes.c_int64), ("D", ctypes.c_int64),
+                ("tet", ctypes.c_void_p), ("tet_stride0", ctypes.c_int64), ("tet_stride1", ctypes.c_int64),
+                ("M", ctypes.c_int64),
+                ("cis", ctypes.c_void_p), ("cis_stride0", ctypes.c_int64), ("cis_stride1", ctypes.c_int64),
+                ("n_cis", ctypes.c_int64),
+                ("trans", ctypes.c_void_p), ("trans_stride0", ctypes.c_int64), ("trans_stride1", ctypes.c_int64),
+                ("n_trans", ctypes.c_int64),
+                ("t_rowptr", ctypes.c_void_p), ("t_col", ctypes.c_void_p),
+                ("scratch", ctypes.c_void_p), ("stats", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("ldo", ctypes.c_int64)]
+
+
 class LossAccum(ctypes.Structure):
     """AimxLossAccum (include/aimx.h): the train step's device-side loss / NaN / step bookkeeping."""
     _fields_ = [("loss_sum", ctypes.c_void_p), ("nan_count", ctypes.c_void_p), ("steps", ctypes.c_void_p),
@@ -183,6 +197,8 @@ _SIGS = {
     "aimx_head_backward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
     "aimx_head_backward": (c_i32, [ctypes.POINTER(Head), ctypes.POINTER(HeadGrad), c_ptr]),
     "aimx_dropout_seeds": (c_i32, [c_ptr, c_ptr, c_i32, c_ptr]),
+    "aimx_stereo_forward": (c_i32, [ctypes.c_void_p, c_ptr]),
+    "aimx_stereo_backward": (c_i32, [ctypes.c_void_p, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr]),
     "aimx_l1_loss_forward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr]),
     "aimx_l1_loss_forward_accum": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr,
                                            ctypes.c_void_p, c_ptr]),

@@ -255,6 +255,69 @@ def _pack_ig(params, nl, nm, d, k):
     return packed, w_ig, b_ig
 
 
+class _Stereo(torch.autograd.Function):
+    """[x | cis/trans | tetrahedral] features (gnn.py:310-326 before stereochemical_embedding_2),
+    aimx_stereo_forward / _backward (csrc/stereo.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, tet, cis, trans):
+        from .plan import build_csr, _zero_status
+        import ctypes
+        lib = _lib.load()
+        x, ldx = _rows(x)
+        n, d = x.shape
+        dev = x.device
+        tet = tet.to(torch.int64).contiguous() if tet.numel() else tet.new_empty(0, 4, dtype=torch.int64)
+        m = tet.shape[0] if tet.numel() else 0
+        a = _lib.Stereo()
+        a.x, a.ldx, a.N, a.D = ptr(x), ldx, n, d
+        keep = [x, tet]
+        if m:
+            status = torch.empty(1, dtype=torch.int32, device=dev)
+            csr = build_csr(tet.data_ptr(), 1, 0, None, 0, 0, 4 * m, n, dev, status)
+            scratch = torch.empty(4 * m, d, dtype=_F32, device=dev)
+            stats = torch.empty(m, 8, dtype=_F32, device=dev)
+            a.tet, a.tet_stride0, a.tet_stride1, a.M = ptr(tet), 4, 1, m
+            a.t_rowptr, a.t_col, a.scratch, a.stats = ptr(csr.rowptr), ptr(csr.col), ptr(scratch), ptr(stats)
+            keep += [csr.rowptr, csr.col, stats]
+        for name, t in (("cis", cis), ("trans", trans)):
+            if t.numel():
+                if t.dim() != 2 or t.shape[0] < 2 or t.dtype != torch.int64:
+                    raise _lib.AimxError(f"aimx.stereo: {name} must be int64 [rows >= 2, cols] (the reference "
+                                         f"reads rows 0 and 1)")
+                setattr(a, name, ptr(t))
+                setattr(a, name + "_stride0", t.stride(0))
+                setattr(a, name + "_stride1", t.stride(1))
+                setattr(a, "n_" + name, t.shape[0])
+                keep.append(t)
+        out = torch.empty(n, 3 * d, dtype=_F32, device=dev)
+        a.out, a.ldo = ptr(out), 3 * d
+        check(lib.aimx_stereo_forward(ctypes.byref(a), stream_ptr(dev)), "stereo_forward")
+        ctx.args, ctx.keep, ctx.m, ctx.shape = a, keep, m, (n, d)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        import ctypes
+        lib = _lib.load()
+        n, d = ctx.shape
+        g = g.contiguous()
+        dx = torch.empty(n, d, dtype=_F32, device=g.device)
+        gs = torch.empty(max(4 * ctx.m, 1), d, dtype=_F32, device=g.device)
+        check(lib.aimx_stereo_backward(ctypes.byref(ctx.args), ptr(g), 3 * d, ptr(dx), d, ptr(gs),
+                                       stream_ptr(g.device)), "stereo_backward")
+        return dx, None, None, None
+
+
+def stereo_features(x, tet, cis, trans):
+    """[x | cis_trans(x) | tetrahedral(x)] ([N, 3D]) of the reference's stereochemistry
+    (gnn.py:310-497) on the HIP kernels; differentiable in x."""
+    _lib.require_device(x)
+    if x.dtype != _F32:
+        raise _lib.AimxError("aimx.stereo: fp32 features")
+    return _Stereo.apply(x, tet, cis, trans)
+
+
 def dropout_seeds(owner, n, device):
     """n int64 dropout seeds for one forward, drawn on the device from a counter kept on `owner`
     (aimx_dropout_seeds; one launch, graph-safe). The counter starts from torch's generator."""

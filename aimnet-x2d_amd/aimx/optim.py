@@ -149,7 +149,8 @@ class FusedAdam(torch.optim.Optimizer):
         lib = _lib.load()
         wsb = self._wsb
         if self._ws is None or self._ws.numel() * 8 < wsb:
-            self._ws = torch.empty((wsb + 7) // 8, dtype=torch.float64, device=dev)
+            # zero-filled once: holds aimx_fused_adam's self-resetting arrival counter
+            self._ws = torch.zeros((wsb + 7) // 8, dtype=torch.float64, device=dev)
         h = AdamHyper()
         h.beta1, h.beta2 = hyper_g["betas"]
         h.one_minus_beta1, h.one_minus_beta2 = 1.0 - hyper_g["betas"][0], 1.0 - hyper_g["betas"][1]

@@ -6,7 +6,7 @@
 // these as ~2 elementwise launches per parameter tensor (plus foreach norm kernels): hundreds of
 // 3-5 us launches per step for this model. Here:
 //   1. k_adam_sumsq   : per-(tensor, slice) partial sums of g^2 (fp64)  -> workspace
-//   2. k_adam_scalars : one wave: total norm, clip coefficient
+//      (its last-arriving workgroup: total norm, clip coefficient — the former k_adam_scalars)
 // (each tensor's own step counter, torch.optim.Adam's per-parameter state['step'], is advanced by
 // the first workgroup of that tensor in launch 1 and read by launch 3 for its bias corrections:
 // a parameter without a gradient in a step keeps its count, as in torch)
@@ -47,8 +47,35 @@ __device__ __forceinline__ int find_tensor(const AdamTable& t, int b) {
   return i;
 }
 
+// The clip coefficient from every slice's partial sum of squares (read in the order k_adam_scalars
+// read them: lane j sums partials j, j + 64, ... then a butterfly), by ONE wave.
+template <bool SC1>
+__device__ __forceinline__ void adam_scalars_wave(const double* partial, int64_t n_partial, float max_norm,
+                                                  float* scal, float* norm_out) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  for (int64_t j = lane; j < n_partial; j += 64)
+    s += SC1 ? __hip_atomic_load(partial + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : partial[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) {
+    const float total = (float)sqrt(s);
+    float coef = 1.f;
+    if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
+    scal[0] = coef;
+    scal[3] = total;
+    if (norm_out) *norm_out = total;
+  }
+}
+
+// Launch 1. The partial of each slice is stored device-coherent (sc1) and the workgroup then
+// arrives on a self-resetting counter (MI355X_MICROARCH.md "Valid forms", row 1: drained sc1
+// stores -> barrier -> one relaxed agent-scope add); the last of all `total` workgroups (over
+// every chunk launch) computes the clip coefficient itself, so there is no separate scalars launch.
 __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, double* __restrict__ partial,
-                                                             float* __restrict__ steps) {
+                                                             float* __restrict__ steps, int64_t base, int64_t total,
+                                                             int32_t* __restrict__ arrive, float max_norm,
+                                                             float* __restrict__ scal, float* __restrict__ norm_out) {
   const int i = find_tensor(t, blockIdx.x);
   if (blockIdx.x == t.blk0[i] && threadIdx.x == 0) steps[t.gs[i] >> 8] += 1.f;
   const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
@@ -65,29 +92,21 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, 
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
+  __shared__ int last;
   if (threadIdx.x == 0) {
     double s = 0.0;
     for (int w = 0; w < kAdamThreads / kWave; ++w) s += red[w];
-    partial[blockIdx.x] = s;
+    __hip_atomic_store(partial + base + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (old == (int)(total - 1));
+    if (last) __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
   }
+  __syncthreads();
+  if (last && threadIdx.x < 64) adam_scalars_wave<true>(partial, total, max_norm, scal, norm_out);
 }
 
 // scal[0] = clip coefficient, scal[3] = total gradient norm (the value clip_grad_norm_ returns)
-__global__ void k_adam_scalars(const double* __restrict__ partial, int n_partial, float max_norm,
-                               float* __restrict__ scal, float* __restrict__ norm_out) {
-  double s = 0.0;
-  for (int j = threadIdx.x; j < n_partial; j += 64) s += partial[j];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (threadIdx.x == 0) {
-    const float total = (float)sqrt(s);
-    float coef = 1.f;
-    if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
-    scal[0] = coef;
-    scal[3] = total;
-    if (norm_out) *norm_out = total;
-  }
-}
 
 __global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t, const float* __restrict__ scal,
                                                               const float* __restrict__ steps,
@@ -146,10 +165,14 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
     for (int32_t k = 0; k < i; ++k)  // each counter advanced once per call
       if (tensors[k].step_slot == x.step_slot) return AIMX_EARG;
   }
-  double* partial = (double*)workspace;
+  // workspace: [arrival counter (8 B, zero before the first call, left zero)] [partials] [scalars];
+  // the counter's place is fixed whatever the table size, so a table that shrinks between calls
+  // never finds a stale partial where its counter should be
+  int32_t* arrive = (int32_t*)workspace;
+  double* partial = (double*)workspace + 1;
   int64_t total_blocks = 0;
   for (int32_t i = 0; i < n; ++i) total_blocks += blocks_of(tensors[i].numel);
-  float* scal = (float*)(partial + total_blocks + 1);
+  float* scal = (float*)(partial + total_blocks);
   // chunk tables (host, by value into the kernel arguments)
   auto for_chunks = [&](auto&& launch) -> int {
     int64_t blk = 0;
@@ -176,14 +199,12 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
     return AIMX_OK;
   };
   int rc = for_chunks([&](const AdamTable& t, int32_t nb, int64_t blk) -> int {
-    hipLaunchKernelGGL(k_adam_sumsq, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, partial + blk, step);
+    hipLaunchKernelGGL(k_adam_sumsq, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, partial, step, blk,
+                       total_blocks, arrive, h->max_grad_norm, scal, norm_out);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(k_adam_scalars, dim3(1), dim3(64), 0, s, (const double*)partial, (int)total_blocks,
-                     h->max_grad_norm, scal, norm_out);
-  AIMX_CHECK_LAUNCH();
   return for_chunks([&](const AdamTable& t, int32_t nb, int64_t) -> int {
     hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal,
                        (const float*)step, lr, h->beta1, h->one_minus_beta1, h->beta2, h->one_minus_beta2, h->eps,

@@ -11,9 +11,9 @@ What changes is where the hot path runs:
   * the message-passing stack (gnn.py:276-308: partial charges -> ShellConvolutionLayer -> +x,
     for every layer) is ONE fused HIP operator (aimx.ops.message_passing_stack);
   * pooling runs the one-molecule-per-workgroup HIP kernels (models/pooling.py).
-Embedding lookups, the embedding/concat projections (N x hidden, hipBLASLt) and the per-molecule
-FFN stay on PyTorch. Stereochemistry (off in every BASELINE config) is plain PyTorch around the
-per-layer HIP operators, as the reference computes it (gnn.py:310-509).
+Stereochemistry (off in every BASELINE config) runs per layer between the HIP layer operators, as
+the reference computes it (gnn.py:288-306): the [x | cis/trans | tetrahedral] features are one HIP
+operator (ops.stereo_features, csrc/stereo.hip) feeding stereochemical_embedding_2.
 """
 import os
 from typing import Dict, Optional, Tuple
@@ -245,9 +245,14 @@ class GNN(nn.Module):
 
     # -- stereochemistry (plain PyTorch; reference gnn.py:310-509) ----------------------------
     def _apply_stereochemistry(self, x_other, tetrahedral_indices, cis_indices, trans_indices):
-        ct = self._cis_trans_calculation(x_other, cis_indices, trans_indices)
-        tet = self._tetrahedral_feature_calculation_physics_inspired(x_other, tetrahedral_indices)
-        return self.stereochemical_embedding_2(torch.cat([x_other, ct, tet], dim=-1))
+        # [x | cis/trans | tetrahedral] in one HIP op (csrc/stereo.hip) forward and backward; the
+        # two methods below keep the reference's PyTorch formulation (AIMX_STEREO_TORCH=1 uses them)
+        if os.environ.get("AIMX_STEREO_TORCH", "0") == "1":
+            ct = self._cis_trans_calculation(x_other, cis_indices, trans_indices)
+            tet = self._tetrahedral_feature_calculation_physics_inspired(x_other, tetrahedral_indices)
+            return self.stereochemical_embedding_2(torch.cat([x_other, ct, tet], dim=-1))
+        return self.stereochemical_embedding_2(ops.stereo_features(x_other, tetrahedral_indices, cis_indices,
+                                                                   trans_indices))
 
     def _tetrahedral_feature_calculation_physics_inspired(self, atom_features, tetrahedral_indices):
         """Chirality term on unit-normalised neighbour features, rescaled by tanh(mean |x| / 3),

@@ -336,7 +336,10 @@ int aimx_wgrad_grouped(const AimxWgradProblem* problems, int32_t n, void* worksp
  * parameter left out of a step (no gradient) keeps its count, as in torch. `step` and `lr` (one
  * float per parameter group, group < 256) are device memory, so the call is graph-capturable and
  * schedulers update lr without re-capture. *norm_out (nullable, device) receives the total norm
- * clip_grad_norm_ returns.
+ * clip_grad_norm_ returns. The workspace (aimx_fused_adam_workspace_bytes) must be ZERO-filled
+ * before its first use and is then reused as is: one of its words is a self-resetting arrival
+ * counter (the launch that sums the squares also forms the clip coefficient, in its last
+ * workgroup), which every call leaves zero.
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
   float* param;
@@ -459,6 +462,33 @@ typedef struct {
   int64_t n;
 } AimxCopyItem;
 int aimx_multi_copy(const AimxCopyItem* items, int32_t n_items, aimx_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Stereochemistry features (reference GNN._apply_stereochemistry, gnn.py:310-326, with
+ * _cis_trans_calculation gnn.py:452-497 and _tetrahedral_feature_calculation_physics_inspired
+ * gnn.py:376-450): out [N, 3D] = [x | ct | tet], the input of stereochemical_embedding_2.
+ *   ct  = x + scatter of (-x[cis[0, i]] at cis[1, i]) then (+x[trans[0, i]] at trans[1, i]), i = 0, 1
+ *         (rows 0 and 1 of the collated [rows, 2] cis / trans tensors, as the reference indexes
+ *         them; rows 0 or >= 2 required, out-of-range atoms skipped)
+ *   tet = rows named by a centre: x + the chirality terms of every centre naming them, in item
+ *         order; other rows 0; M == 0: tet = x.
+ * Tetrahedral items are ordered by a stable CSR of tet.flat (t_rowptr [N+1], t_col [4M]: item ids,
+ * aimx_csr_build with key = tet, n_rows = N), so results are deterministic. scratch [4M, D] and
+ * stats [M, 8] (floats) are written by the forward and read by the backward; the backward's
+ * grad_scratch is another [4M, D]. D <= 1024. All pointers are device memory.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct AimxStereo {
+  const float* x; int64_t ldx, N, D;
+  const int64_t* tet; int64_t tet_stride0, tet_stride1, M;
+  const int64_t* cis; int64_t cis_stride0, cis_stride1, n_cis;
+  const int64_t* trans; int64_t trans_stride0, trans_stride1, n_trans;
+  const int32_t* t_rowptr; const int32_t* t_col;
+  float* scratch; float* stats;
+  float* out; int64_t ldo;
+} AimxStereo;
+int aimx_stereo_forward(const AimxStereo* p, aimx_stream_t stream);
+int aimx_stereo_backward(const AimxStereo* p, const float* d_out, int64_t ld_dout, float* dx, int64_t lddx,
+                         float* grad_scratch, aimx_stream_t stream);
 
 /* Dropout seeds of one forward: seeds[0..n) in [0, 2^62) from the device-resident counter state[0]
  * (a splitmix64 sequence), which advances. Replaces the per-forward torch.randint draw, whose

@@ -26,9 +26,13 @@ DEV = "cuda"
     (153, 613, 2000, "TN"), (256, 257, 9186, "TN"), (17, 5, 3, "NT"), (1027, 77, 301, "TT"), (512, 512, 512, "NT")])
 def test_gemm_bf16_operands_fp32_accumulate(M, N, K, layout):
     C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True, prec=1)
+    C32, _, _, ref32, _ = _gemm(M, N, K, layout, bias=True, res=True, prec=0)
+    if layout == "TN" and K >= 512:
+        # a long-K weight gradient (A m-contiguous, B n-contiguous): stays exact fp32 (include/aimx.h)
+        assert torch.equal(C, C32)
+        return
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-5, err
-    C32, _, _, ref32, _ = _gemm(M, N, K, layout, bias=True, res=True, prec=0)
     if K >= 16:  # the bf16 path really ran: far from the exact fp32 product
         assert (C.double() - ref32).abs().max().item() / ref32.abs().max().item() > 1e-4
 

@@ -868,3 +868,34 @@ def test_fused_mlp_opt_in_parity(name, monkeypatch):
     the model within the parity contract (outputs and every gradient vs the fp64 oracle)."""
     monkeypatch.setenv("AIMX_FUSED_MLP", "1")
     test_model_case(name)
+
+
+# ------------------------------------------------------------------------------- stereochemistry
+@pytest.mark.parametrize("D,M,with_ct", [(76, 40, True), (153, 7, True), (307, 0, True), (64, 25, False),
+                                         (1024, 3, True)])
+def test_stereo_features_match_oracle(D, M, with_ct):
+    """ops.stereo_features ([x | cis/trans | tetrahedral], csrc/stereo.hip) against the oracle's
+    restatement of gnn.py:376-497 run in fp64 with autograd: values and the input gradient,
+    with atoms shared by several centres, a zero row (the normalize eps branch), no centres (the
+    tetrahedral block is x itself) and no cis/trans items."""
+    from aimx import ops
+    _, om = _oracle()
+    g = torch.Generator().manual_seed(D + M)
+    n = 300
+    x = torch.randn(n, D, generator=g)
+    x[5] = 0.0
+    tet = torch.randint(0, n, (M, 4), generator=g)
+    if M:
+        tet[0, 2] = 5  # a zero neighbour row
+        tet[1] = tet[0]  # two centres naming the same atoms
+    cis = torch.randint(0, n, (3, 2), generator=g) if with_ct else torch.empty(0, 2, dtype=torch.long)
+    trans = torch.randint(0, n, (2, 2), generator=g) if with_ct else torch.empty(0, 2, dtype=torch.long)
+    w = torch.randn(n, 3 * D, generator=g)
+    xd = x.to(DEV).requires_grad_()
+    out = ops.stereo_features(xd, tet.to(DEV), cis.to(DEV), trans.to(DEV))
+    (out * w.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_()
+    ref = torch.cat([x64, om.cis_trans(x64, cis, trans), om.tetrahedral(x64, tet)], -1)
+    (ref * w.double()).sum().backward()
+    assert norm_rel(out.detach().cpu().numpy(), ref.detach().numpy()) < 1e-6
+    assert norm_rel(xd.grad.cpu().numpy(), x64.grad.numpy()) < 1e-5

@@ -71,3 +71,57 @@ def test_training_reduces_loss():
     losses = [train_epoch(m, bs, crit, opt, DEV, graphed=g)[0] for _ in range(4)]
     assert losses[-1] < 0.95 * losses[0] and max(losses[1:]) < losses[0], losses
     assert all(np.isfinite(losses))
+
+
+def test_full_train_step_matches_oracle():
+    """A18 end to end: two whole reference train steps (trainer.py:151-164: forward, L1 criterion,
+    backward, clip_grad_norm_(1.0), Adam) on the c2 golden batch — ours (fp32 HIP path, FusedAdam)
+    against the oracle run in fp64 with torch's own clip and Adam. Dropout is inactive (eval-mode
+    modules), so both sides compute the same function. Checks: the loss, the pre-clip total gradient
+    norm, and every parameter after each step. Adam's first step is ~ -lr * sign(g), so entries whose
+    gradient is at fp32 noise level may legitimately flip: those are counted, not required."""
+    from aimx.optim import FusedAdam
+    from golden_cases import load_case
+    from models import L1Loss
+    from test_gpu_parity import _build_model, _oracle
+    _, om = _oracle()
+    z, cfg, (af, edges, batch, tc) = load_case("c2")
+    lr = 1e-3
+    y = torch.from_numpy(np.random.default_rng(3).standard_normal((len(z["n_mol_atoms"]), cfg["output_dim"]))).float()
+    model = _build_model(cfg, int(z["seed"]))
+    opt = FusedAdam(model.parameters(), lr=lr, max_grad_norm=1.0)
+    p64 = {k: v.double().requires_grad_() for k, v in om.seeded_params(cfg, int(z["seed"])).items()}
+    ref_opt = torch.optim.Adam(list(p64.values()), lr=lr)
+    afd = {k: v.to(DEV) for k, v in af.items()}
+    e0 = torch.empty(0, 2, dtype=torch.long, device=DEV)
+    args = (afd, edges.to(DEV), batch.to(DEV), tc.to(DEV), torch.empty(0, 4, dtype=torch.long, device=DEV), e0, e0)
+    crit = L1Loss()
+    for step in range(2):
+        opt.zero_grad(set_to_none=True)
+        out, _, _ = model(*args)
+        loss = crit(out, y.to(DEV))
+        loss.backward()
+        opt.step()
+        ref_opt.zero_grad(set_to_none=True)
+        o64, _, _ = om.gnn_forward(p64, cfg, af, edges, batch, tc.double())
+        l64 = (o64 - y.double()).abs().mean()
+        l64.backward()
+        tn = torch.nn.utils.clip_grad_norm_([v for v in p64.values() if v.grad is not None], 1.0)
+        ref_opt.step()
+        assert abs(loss.item() - l64.item()) <= 1e-5 * abs(l64.item()), (step, loss.item(), l64.item())
+        assert abs(float(opt.last_grad_norm) - float(tn)) <= 1e-5 * float(tn), (step, float(opt.last_grad_norm), float(tn))
+        flips = total = 0
+        for k, p in model.named_parameters():
+            ref = p64[k].detach()
+            ours = p.detach().cpu().double()
+            tol = 1e-2 * lr
+            d = (ours - ref).abs()
+            total += d.numel()
+            flips += int((d > tol).sum())
+            g = p64[k].grad
+            if g is not None:  # entries with a clearly resolved gradient must agree tightly
+                # (step 2's m/sqrt(v) amplifies the fp32 gradient noise where g2 ~ -g1: 1e-2 lr)
+                big = g.abs() > 1e-3 * g.abs().max()
+                tol_big = (1e-3 if step == 0 else 1e-2) * lr
+                assert (d[big] <= tol_big + 1e-6 * ref[big].abs()).all(), (step, k, d[big].max().item())
+        assert flips <= 1e-3 * total, (step, flips, total)

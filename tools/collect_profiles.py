@@ -39,7 +39,7 @@ for name in ("bench_plain.log", "roof.log"):
 print(json.dumps(json.load(open(os.path.join(dst, "hop_traffic.json"))), indent=1))
 
 # extra configs (c3/c4/c5 bench lines), the c4 step breakdown and its MFMA utilisation
-for cfgname in ("c3", "c4", "c5"):
+for cfgname in ("c3", "c4", "c5", "c2_amp", "c4_amp", "c5_amp"):
     p = os.path.join(src, f"bench_{cfgname}.log")
     if os.path.exists(p):
         lines = [ln for ln in open(p) if ln.startswith("{")]
@@ -49,7 +49,9 @@ if os.path.isdir(os.path.join(src, "c4_trace")):
     with open(os.path.join(dst, f"{tag}_c4_step_breakdown.txt"), "w") as f:
         f.write(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "step_kernels.py"),
                                 os.path.join(src, "c4_trace")], capture_output=True, text=True, check=True).stdout)
-if os.path.isdir(os.path.join(src, "c4_mfma")):
-    with open(os.path.join(dst, f"{tag}_c4_mfma_util.json"), "w") as f:
-        f.write(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_summary.py"),
-                                os.path.join(src, "c4_mfma"), "15"], capture_output=True, text=True, check=True).stdout)
+for cfgname in ("c2", "c4", "c5"):
+    if os.path.isdir(os.path.join(src, f"{cfgname}_mfma")):
+        with open(os.path.join(dst, f"{tag}_{cfgname}_mfma_util.json"), "w") as f:
+            f.write(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_summary.py"),
+                                    os.path.join(src, f"{cfgname}_mfma"), "15"], capture_output=True, text=True,
+                                   check=True).stdout)
