@@ -95,6 +95,7 @@ class ShellStackGrad(ctypes.Structure):
         ("d_w_ig", c_ptr), ("d_b_ig", c_ptr), ("d_w1", c_ptr), ("d_b1", c_ptr), ("d_w2", c_ptr), ("d_b2", c_ptr),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
         ("aux_stream", c_ptr), ("events", c_ptr), ("n_events", c_i32),
+        ("aux_mode", c_i32), ("aux_counters", c_ptr), ("n_aux_counters", c_i64),
     ]
 
 
@@ -301,17 +302,45 @@ def aux_stream(device):
     return hit
 
 
+_SIDE = {}
+
+
+def side_stream(device):
+    """Per-device side stream + event handles on which the backward's weight gradients run beside
+    the activation-gradient chain (ops.side_fork). Opt-in (AIMX_SIDE_WGRAD=1), single process only:
+    measured on MI355X (profiles/r02_side_wgrad_ab.txt) the forked graph is SLOWER at every config
+    (c2 0.979 -> 1.053 ms, c4 3.53 -> 3.59, c5 5.28 -> 5.35): the activation-gradient chain's
+    kernels already occupy the CUs, so the weight gradients only time-share them and the fork/join
+    costs ~70 us per step."""
+    if os.environ.get("AIMX_SIDE_WGRAD", "0") != "1":
+        return None
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return None
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    hit = _SIDE.get(key)
+    if hit is None:
+        lib = load()
+        ev = (c_ptr * N_EVENTS)()
+        check(lib.aimx_events_create(N_EVENTS, ev), "events_create")
+        hit = (torch.cuda.Stream(device=torch.device("cuda", key)), ev)
+        _SIDE[key] = hit
+    return hit
+
+
 _COUNTERS = {}
 N_COUNTERS = 1 << 16
 
 
-def counters(device):
-    """Per-device split-K arrival counters: zeroed once, kept zero by the kernels themselves."""
+def counters(device, slot=0):
+    """Per-device split-K arrival counters: zeroed once, kept zero by the kernels themselves.
+    slot 1: a second array for kernels running concurrently on the side stream (ops.side_fork), so
+    two streams' split-K tickets never share a counter."""
     key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
-    buf = _COUNTERS.get(key)
+    buf = _COUNTERS.get((key, slot))
     if buf is None:
         buf = torch.zeros(N_COUNTERS, dtype=torch.int32, device=device)
-        _COUNTERS[key] = buf
+        _COUNTERS[(key, slot)] = buf
     return buf
 
 

@@ -379,7 +379,8 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   const int n_pr = stack_wgrad_problems(s, g, base, &lay, pr.data());
   // with an auxiliary stream, each layer's weight gradients fork off as soon as its activation
   // gradients exist; the two streams split the counter array so their split-K tickets never meet
-  const bool aux = g->aux_stream && g->events && g->n_events >= L + 1 && s->counters && s->n_counters >= 2;
+  const bool tail = g->aux_mode == 1 && g->aux_stream && g->events && g->n_events >= 1 && g->aux_counters;
+  const bool aux = !tail && g->aux_stream && g->events && g->n_events >= L + 1 && s->counters && s->n_counters >= 2;
   hipStream_t ast = (hipStream_t)g->aux_stream;
   const int64_t main_counters = aux ? s->n_counters / 2 : s->n_counters;
   const Ws ws{s->workspace, s->workspace_bytes, s->counters, main_counters, s->precision};
@@ -469,6 +470,13 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     AIMX_CHECK_HIP(hipEventRecord(ev, ast));
     AIMX_CHECK_HIP(hipStreamWaitEvent(st, ev, 0));
     return AIMX_OK;
+  }
+  if (tail) {  // fork the grouped weight gradients; the caller joins (AimxShellStackGrad.aux_mode)
+    hipEvent_t ev = (hipEvent_t)g->events[0];
+    AIMX_CHECK_HIP(hipEventRecord(ev, st));
+    AIMX_CHECK_HIP(hipStreamWaitEvent(ast, ev, 0));
+    return aimx_wgrad_grouped(pr.data(), n_pr, wg_ws, wg_bytes, g->aux_counters, g->n_aux_counters,
+                              (aimx_stream_t)ast);
   }
   // every weight and bias gradient of the stack in one grouped launch
   return aimx_wgrad_grouped(pr.data(), n_pr, wg_ws, wg_bytes, s->counters, s->n_counters, stream_);

@@ -223,8 +223,13 @@ class GradientSync:
             flat = torch.empty(sum(p.numel() for p in bucket), dtype=bucket[0].dtype, device=bucket[0].device)
             self._flat[i] = flat
         if self.comm is not None:
-            # pack every gradient (zeros for a missing one) into the flat buffer: one launch
+            # pack every gradient (zeros for a missing one) into the flat buffer: one launch. Weight
+            # gradients may still be in flight on the backward's side stream (aimx.ops.side_fork):
+            # the pack waits for them (an event, no host sync)
             from aimx import _lib
+            hit = _lib.side_stream(flat.device)
+            if hit is not None:
+                torch.cuda.current_stream(flat.device).wait_stream(hit[0])
             pairs, off = [], 0
             for p in bucket:
                 n = p.numel()
@@ -234,6 +239,11 @@ class GradientSync:
                 off += n
             _lib.multi_copy(pairs, flat.device)
         else:
+            if flat.is_cuda:
+                from aimx import _lib
+                hit = _lib.side_stream(flat.device)
+                if hit is not None:
+                    torch.cuda.current_stream(flat.device).wait_stream(hit[0])
             grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket]
             torch.cat(grads, out=flat)
         if self.comm is not None:

@@ -214,6 +214,13 @@ typedef struct AimxShellStackGrad {
    * execution see the same dependencies. aux_stream uses the upper half of the counter array.
    * events: hipEvent_t handles from aimx_events_create. */
   aimx_stream_t aux_stream; void* const* events; int32_t n_events;
+  /* aux_mode 1 ("tail fork"): instead of the per-layer forks above, the stack's single grouped
+   * weight-gradient launch runs on aux_stream after an event fork (events[0]) at the end of the
+   * activation-gradient chain, and the call returns WITHOUT joining: the caller joins aux_stream
+   * before it reads a weight gradient or releases the workspace / activations. The launch uses
+   * aux_counters (a counter array of its own, as in AimxGemmArgs), so the two streams' split-K
+   * tickets never meet. */
+  int32_t aux_mode; int32_t* aux_counters; int64_t n_aux_counters;
 } AimxShellStackGrad;
 
 size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s);
