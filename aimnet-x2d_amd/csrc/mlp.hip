@@ -329,6 +329,449 @@ __global__ __launch_bounds__(512) void k_mlp_bwd(const MlpBwd p) {
   }
 }
 
+// ---- Weight-resident variant (small D: every block's weights fit in LDS) --------------------------
+// The per-row-tile kernels above re-stream each weight fragment from L2 in every GEMM phase of every
+// workgroup, with the first loads of each phase exposed (measured 48 / 54 us per layer at c2 vs
+// ~42 / 43 us for the four separate GEMMs). Here a persistent workgroup (one per CU) stages ALL
+// 2*nm weight matrices of the layer in LDS once — as k-contiguous rows, transposed for the backward
+// — and then walks row chunks of 16*rt atoms: each GEMM phase is rt x CF (16 x 16) output tiles, one
+// per wave, over K padded to 16 with zeros, every operand read from LDS by 16-byte ds_reads with the
+// k order permuted identically for A and B (lane l supplies k = 16 g + 4 (l >> 4) + j to MFMA step
+// j of group g, so one ds_read_b128 per operand feeds 4 v_mfma_f32_16x16x4_f32). Epilogues are the
+// per-row-tile kernels' (same dropout hash, salts and rounding order).
+constexpr int kWMaxWaves = 16;
+constexpr int kMlpwDynLds = 160 * 1024 - 1024;  // + the static pointer table, within one CU's LDS
+
+#ifdef AIMX_MLPW_TRACE  // diagnostics build only: phase timestamps of workgroup 0 (forward)
+__device__ long long g_mlpw_trace[64];
+#define MLPW_STAMP(k)                                                                           \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && (k) < 64) g_mlpw_trace[(k)] = (long long)wall_clock64(); \
+  } while (0)
+#else
+#define MLPW_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
+__host__ __device__ inline int pad16(int d) { return (d + 15) / 16 * 16; }
+__host__ __device__ inline int wstride(int d) { return pad16(d) + 4; }  // 4 mod 64 or 20 mod 64 ... conflict-free b128
+
+// C tile (t, f) = A[16 t .., :Kp] . Bt[16 f .., :Kp]^T, both LDS images row stride S (k contiguous).
+__device__ __forceinline__ floatx4 tile_mma(const float* A, const float* Bt, int S, int Kp, int t, int f) {
+  const int lane = threadIdx.x & 63, lr = lane & 15, kq = 4 * (lane >> 4);
+  const float* a0 = A + (16 * t + lr) * S + kq;
+  const float* b0 = Bt + (16 * f + lr) * S + kq;
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < Kp; g += 16) {
+    const floatx4 a = *reinterpret_cast<const floatx4*>(a0 + g);
+    const floatx4 b = *reinterpret_cast<const floatx4*>(b0 + g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// Initial fill of a workgroup's LDS: nmat D x D weights as k-contiguous [Kp][S] images (rows n,
+// zero beyond D; TR: transposed, image row n = column n of W, for the backward's B(k, n) = W[k][n])
+// and the first row chunk (rows [r0, r0 + R) x cols [0, D) of src, zero beyond D and beyond N).
+// Global latency is the cost here (~2 us per dependent round trip on a loaded chip), so every
+// thread issues up to kFillU weight loads and kFillR row loads before the first LDS store: one
+// round trip for the whole fill at c2's sizes. Matrix pointers come from an LDS table (no private
+// arrays, which would live in scratch).
+constexpr int kFillW = 8, kFillM = 4, kFillR = 8;
+
+// Workgroup barrier for LDS hand-offs only: the LDS writes are drained (lgkmcnt), outstanding
+// global stores are NOT waited for (__syncthreads' fence would wait for every epilogue store).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Buffer descriptor over [p, p + bytes): loads past the extent return 0, so an out-of-range element
+// is a load from an address past the end (an ADDRESS select) — a value select after the load lets
+// hipcc branch around every load and wait for each one in turn (cdna_hip_programming.md §5 trap (c)).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* q = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ float mlp_bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+template <bool TR>
+__device__ __forceinline__ void fill_lds(float* Wl, const float* const* wtab, int nmat, int D, int Kp, int S,
+                                         float* Rl, const float* src, int64_t lds_, int64_t r0, int R, int64_t N) {
+  const int NT = blockDim.x, tid = threadIdx.x;
+  const int per = Kp * Kp, totr = R * Kp;
+  const uint32_t wbytes = 4u * (uint32_t)(D * D), OOB = 0xFFFFFFF0u;
+  const int64_t nrows = max<int64_t>(0, min<int64_t>(R, N - r0));
+  const __amdgpu_buffer_rsrc_t rr = mlp_rsrc(src + r0 * lds_, (uint32_t)(4 * max<int64_t>(1, nrows * lds_)));
+  for (int m0 = 0; m0 < nmat; m0 += kFillM) {
+    for (int e0 = 0; e0 < per; e0 += kFillW * NT) {
+      float v[kFillM][kFillW], q[kFillR];
+#pragma unroll
+      for (int mi = 0; mi < kFillM; ++mi) {
+        const int m = min(m0 + mi, nmat - 1);
+        const __amdgpu_buffer_rsrc_t rw = mlp_rsrc(wtab[m], wbytes);
+#pragma unroll
+        for (int u = 0; u < kFillW; ++u) {
+          const int e = e0 + u * NT + tid, n = e / Kp, k = e - n * Kp;
+          const bool ok = e < per && n < D && k < D;
+          v[mi][u] = mlp_bload(rw, ok ? 4u * (uint32_t)(TR ? k * D + n : n * D + k) : OOB);
+        }
+      }
+      const bool rows = m0 == 0 && e0 == 0;  // the row chunk rides along with the first batch
+#pragma unroll
+      for (int u = 0; u < kFillR; ++u) {
+        const int e = u * NT + tid, r = e / Kp, c = e - r * Kp;
+        const bool ok = rows && e < totr && c < D && r < nrows;
+        q[u] = mlp_bload(rr, ok ? 4u * (uint32_t)(r * lds_ + c) : OOB);
+      }
+#pragma unroll
+      for (int mi = 0; mi < kFillM; ++mi) {
+        if (m0 + mi >= nmat) break;
+#pragma unroll
+        for (int u = 0; u < kFillW; ++u) {
+          const int e = e0 + u * NT + tid;
+          if (e < per) {
+            const int n = e / Kp, k = e - n * Kp;
+            Wl[(m0 + mi) * Kp * S + n * S + k] = v[mi][u];
+          }
+        }
+      }
+      if (rows) {
+#pragma unroll
+        for (int u = 0; u < kFillR; ++u) {
+          const int e = u * NT + tid;
+          if (e < totr) {
+            const int r = e / Kp, c = e - r * Kp;
+            Rl[r * S + c] = q[u];
+          }
+        }
+      }
+    }
+  }
+  for (int e = kFillR * NT + tid; e < totr; e += NT) {  // rows beyond one batch (large R * Kp)
+    const int r = e / Kp, c = e - r * Kp;
+    Rl[r * S + c] = (c < D && r < nrows) ? src[(r0 + r) * lds_ + c] : 0.f;
+  }
+}
+
+// rows [r0, r0 + R) x cols [0, D) of src (row stride lds_) -> LDS rows of stride S, zero beyond D
+// (to Kp) and beyond N
+__device__ __forceinline__ void load_rows(float* dst, int S, const float* src, int64_t lds_, int64_t r0, int R, int D,
+                                          int Kp, int64_t N) {
+  const int total = R * Kp;
+  for (int e0 = 0; e0 < total; e0 += kFillR * (int)blockDim.x) {
+    float v[kFillR];
+#pragma unroll
+    for (int u = 0; u < kFillR; ++u) {
+      const int e = e0 + u * blockDim.x + threadIdx.x;
+      const int r = e / Kp, c = e - r * Kp;
+      const bool ok = e < total && c < D && r0 + r < N;
+      const float x = src[ok ? (r0 + r) * lds_ + c : 0];
+      v[u] = ok ? x : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kFillR; ++u) {
+      const int e = e0 + u * blockDim.x + threadIdx.x;
+      if (e < total) {
+        const int r = e / Kp, c = e - r * Kp;
+        dst[r * S + c] = v[u];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, int rt) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int D = (int)p.D, Kp = pad16(D), S = wstride(D), CF = Kp / 16, nm = p.nm;
+  const int R = 16 * rt;
+  float* W = lds;                        // W1_k at 2k, W2_k at 2k+1: [Kp][S] each
+  float* Xa = W + 2 * nm * Kp * S;       // block input a_k [R][S]
+  float* Hb = Xa + R * S;                // r_k             [R][S]
+  float* Bia = Hb + R * S;               // b1_k at 2k, b2_k at 2k+1: [Kp] each
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __shared__ const float* wtab[16];
+  __shared__ const float* btab[16];
+  if (threadIdx.x < 2 * nm) {
+    wtab[threadIdx.x] = (threadIdx.x & 1) ? p.w2[threadIdx.x >> 1] : p.w1[threadIdx.x >> 1];
+    btab[threadIdx.x] = (threadIdx.x & 1) ? p.b2[threadIdx.x >> 1] : p.b1[threadIdx.x >> 1];
+  }
+  for (int e = threadIdx.x; e < R * S; e += blockDim.x) Hb[e] = 0.f;  // k padding of the 2nd GEMM's A
+  __syncthreads();
+  MLPW_STAMP(0);
+  const int64_t N = p.N;
+  const int64_t nchunk = (N + R - 1) / R;
+  // biases (in flight beside the fill), weights and the first chunk's a0 = act(u) = UG[:, :D] rows
+  float bv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = threadIdx.x + u * (int)blockDim.x, m = min(e / Kp, 2 * nm - 1), c = min(e - (e / Kp) * Kp, D - 1);
+    bv[u] = btab[m][c];
+  }
+  fill_lds<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, 2 * p.D, (int64_t)blockIdx.x * R, R, N);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = threadIdx.x + u * (int)blockDim.x;
+    if (e < 2 * nm * Kp) Bia[e] = (e - (e / Kp) * Kp) < D ? bv[u] : 0.f;
+  }
+  for (int e = threadIdx.x + 2 * (int)blockDim.x; e < 2 * nm * Kp; e += blockDim.x) {  // large nm * Kp
+    const int m = e / Kp, c = e - m * Kp;
+    Bia[e] = c < D ? btab[m][c] : 0.f;
+  }
+  lds_sync();
+  MLPW_STAMP(1);
+  int st = 2;
+  (void)st;
+  const float scale = drop_scale(p.drop_p);
+  const uint64_t seed = p.drop ? (uint64_t)*p.seed : 0;
+  const int items = rt * CF;
+  const bool single = items <= nw;  // one (tile, fragment) item per wave: prefetch across phases
+  for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+    const int64_t r0 = ch * R;
+    if (ch != (int64_t)blockIdx.x) {
+      __syncthreads();  // the previous chunk's last epilogue reads of Xa are done
+      load_rows(Xa, S, p.ug, 2 * p.D, r0, R, D, Kp, N);
+      __syncthreads();
+    }
+    MLPW_STAMP(st++);
+    float resid[4] = {0.f, 0.f, 0.f, 0.f};  // the last block's g (+ x), prefetched during its GEMM 1
+    for (int k = 0; k < nm; ++k) {
+      const bool last = k == nm - 1;
+      const float* W1 = W + (2 * k) * Kp * S;
+      const float* W2 = W1 + Kp * S;
+      float* V = p.V[k];
+      float* Rk = p.R[k];
+      uint8_t* M = p.M[k];
+      const uint32_t salt = (uint32_t)(p.salt0 + k);
+      for (int it = wave; it < items; it += nw) {
+        const int t = it / CF, f = it - t * CF;
+        const int c = 16 * f + (lane & 15), cc = min(c, D - 1);
+        if (last && single) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int64_t gc = min(r0 + 16 * t + 4 * (lane >> 4) + i, N - 1);
+            resid[i] = p.ug[gc * 2 * p.D + p.D + cc];
+            if (p.x) resid[i] += p.x[gc * p.ldx + cc];
+          }
+        }
+        const float bias = Bia[(2 * k) * Kp + cc];
+        const floatx4 acc = tile_mma(Xa, W1, S, Kp, t, f);
+        if (c < D) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 16 * t + 4 * (lane >> 4) + i;
+            const int64_t g = r0 + r;
+            const float v = acc[i] + bias;
+            float a = act_fwd(p.act, v);
+            if (p.drop) {
+              const bool keep = hash_uniform(seed, salt, (uint64_t)g * (uint64_t)D + (uint64_t)c) >= p.drop_p;
+              a = keep ? a * scale : 0.f;
+              if (g < N) M[g * D + c] = keep ? 1 : 0;
+            }
+            Hb[r * S + c] = a;
+            if (g < N) {
+              V[g * D + c] = v;
+              Rk[g * D + c] = a;
+            }
+          }
+        }
+      }
+      lds_sync();
+      MLPW_STAMP(st++);
+      float* Ak = last ? nullptr : p.A[k];
+      for (int it = wave; it < items; it += nw) {
+        const int t = it / CF, f = it - t * CF;
+        const int c = 16 * f + (lane & 15), cc = min(c, D - 1);
+        float add[4];
+        const float b2 = Bia[(2 * k + 1) * Kp + cc];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          add[i] = b2;
+          if (last) {
+            if (single) {
+              add[i] += resid[i];
+            } else {
+              const int64_t gc = min(r0 + 16 * t + 4 * (lane >> 4) + i, N - 1);
+              float rr = p.ug[gc * 2 * p.D + p.D + cc];
+              if (p.x) rr += p.x[gc * p.ldx + cc];
+              add[i] += rr;
+            }
+          }
+        }
+        const floatx4 acc = tile_mma(Hb, W2, S, Kp, t, f);
+        if (c < D) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 16 * t + 4 * (lane >> 4) + i;
+            const int64_t g = r0 + r;
+            const float a = acc[i] + add[i] + Xa[r * S + c];
+            Xa[r * S + c] = a;
+            if (g < N) {
+              if (last)
+                p.out[g * p.ldo + c] = a;
+              else
+                Ak[g * D + c] = a;
+            }
+          }
+        }
+      }
+      lds_sync();
+      MLPW_STAMP(st++);
+    }
+  }
+  MLPW_STAMP(63);
+}
+
+__global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, int rt) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int D = (int)p.D, Kp = pad16(D), S = wstride(D), CF = Kp / 16, nm = p.nm;
+  const int R = 16 * rt;
+  float* W = lds;                        // W2_k^T at 2k, W1_k^T at 2k+1: [Kp][S] each
+  float* DA = W + 2 * nm * Kp * S;       // gradient w.r.t. the current block output [R][S]
+  float* DV = DA + R * S;                // dV_k                                     [R][S]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __shared__ const float* wtab[16];
+  if (threadIdx.x < 2 * nm) wtab[threadIdx.x] = (threadIdx.x & 1) ? p.w1[threadIdx.x >> 1] : p.w2[threadIdx.x >> 1];
+  for (int e = threadIdx.x; e < R * S; e += blockDim.x) DV[e] = 0.f;
+  __syncthreads();
+  const int64_t N = p.N;
+  const int64_t nchunk = (N + R - 1) / R;
+  const float scale = drop_scale(p.drop_p);
+  const int items = rt * CF;
+  const bool single = items <= nw;  // one (tile, fragment) item per wave: prefetch across phases
+  // the dV epilogue operands (act'(v) input and dropout mask) of block k for this wave's item
+  float ag[4], mf[4];
+  auto pre_dv = [&](int k, int64_t r0, int it) {
+    const int t = it / CF, f = it - t * CF, cc = min(16 * f + (lane & 15), D - 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t gc = min(r0 + 16 * t + 4 * (lane >> 4) + i, N - 1);
+      mf[i] = p.drop ? (p.M[k][gc * D + cc] ? scale : 0.f) : 1.f;
+      ag[i] = p.V[k][gc * D + cc];
+    }
+  };
+  if (single && (int64_t)blockIdx.x < nchunk) pre_dv(nm - 1, (int64_t)blockIdx.x * R, wave);
+  fill_lds<true>(W, wtab, 2 * nm, D, Kp, S, DA, p.dy, p.lddy, (int64_t)blockIdx.x * R, R, N);
+  for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+    const int64_t r0 = ch * R;
+    if (ch != (int64_t)blockIdx.x) {
+      __syncthreads();
+      load_rows(DA, S, p.dy, p.lddy, r0, R, D, Kp, N);
+      if (single) pre_dv(nm - 1, r0, wave);
+    }
+    lds_sync();
+    for (int e = threadIdx.x; e < R * D; e += blockDim.x) {  // dg = dY (from the LDS copy)
+      const int r = e / D, c = e - r * D;
+      if (r0 + r < N) p.dug[(r0 + r) * 2 * p.D + p.D + c] = DA[r * S + c];
+    }
+    float uu[4] = {0.f, 0.f, 0.f, 0.f};  // act'(u) input for block 0's dA phase
+    for (int k = nm - 1; k >= 0; --k) {
+      const float* W2t = W + (2 * k) * Kp * S;
+      const float* W1t = W2t + Kp * S;
+      float* dVk = p.dV[k];
+      for (int it = wave; it < items; it += nw) {  // dV = (dA W2) * mask/(1-p) * act'(v)
+        const int t = it / CF, f = it - t * CF;
+        const int c = 16 * f + (lane & 15), cc = min(c, D - 1);
+        if (!single) pre_dv(k, r0, it);
+        if (k == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) uu[i] = p.u[min(r0 + 16 * t + 4 * (lane >> 4) + i, N - 1) * D + cc];
+        }
+        const floatx4 acc = tile_mma(DA, W2t, S, Kp, t, f);
+        if (c < D) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 16 * t + 4 * (lane >> 4) + i;
+            const int64_t g = r0 + r;
+            const float dv = (g < N) ? acc[i] * mf[i] * act_grad(p.act, ag[i]) : 0.f;
+            DV[r * S + c] = dv;
+            if (g < N) dVk[g * D + c] = dv;
+          }
+        }
+      }
+      lds_sync();
+      float* dAk = k > 0 ? p.dA[k - 1] : nullptr;
+      for (int it = wave; it < items; it += nw) {  // dA_k = dA_{k+1} + dV W1 ; k == 0: du = dA_0 act'(u)
+        const int t = it / CF, f = it - t * CF;
+        const int c = 16 * f + (lane & 15), cc = min(c, D - 1);
+        if (single && k > 0) pre_dv(k - 1, r0, it);  // the next block's dV operands
+        if (!single && k == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) uu[i] = p.u[min(r0 + 16 * t + 4 * (lane >> 4) + i, N - 1) * D + cc];
+        }
+        const floatx4 acc = tile_mma(DV, W1t, S, Kp, t, f);
+        if (c < D) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 16 * t + 4 * (lane >> 4) + i;
+            const int64_t g = r0 + r;
+            const float da = DA[r * S + c] + acc[i];
+            DA[r * S + c] = da;
+            if (g < N) {
+              if (k > 0)
+                dAk[g * D + c] = da;
+              else
+                p.dug[g * 2 * p.D + c] = da * act_grad(p.act, uu[i]);
+            }
+          }
+        }
+      }
+      lds_sync();
+    }
+  }
+}
+
+#ifdef AIMX_MLPW_TRACE
+}  // namespace
+extern "C" int aimx_mlpw_trace_read(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mlpw_trace), sizeof(long long) * 64) == hipSuccess ? 0 : -1;
+}
+namespace {
+#endif
+
+size_t mlpw_lds_bytes(int64_t D, int64_t nm, int rt) {
+  const int Kp = pad16((int)D), S = wstride((int)D);
+  return sizeof(float) * (size_t)((2 * nm * Kp + 2 * 16 * rt) * S + 2 * nm * Kp);  // + the bias table
+}
+
+int g_num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+// rows per chunk: enough 16-row tiles that the chunks fit one round of one workgroup per CU, at
+// most 4 tiles and 16 waves' worth of (tile, fragment) items, within the LDS
+int mlpw_rt(int64_t N, int64_t D, int64_t nm) {
+  const int CF = pad16((int)D) / 16;
+  const int64_t tiles = (N + 15) / 16;
+  int rt = (int)std::min<int64_t>(4, std::max<int64_t>(1, (tiles + g_num_cus() - 1) / g_num_cus()));
+  while (rt > 1 && (rt * CF > 2 * kWMaxWaves || mlpw_lds_bytes(D, nm, rt) > (size_t)kMlpwDynLds)) --rt;
+  return rt;
+}
+
+bool mlpw_lds_ok(int64_t D, int64_t nm) {
+  static const bool set = [] {
+    // dynamic LDS cap: the CU's 160 KiB less the kernels' static table (wtab)
+    (void)hipFuncSetAttribute((const void*)k_mlpw_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpwDynLds);
+    (void)hipFuncSetAttribute((const void*)k_mlpw_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpwDynLds);
+    return true;
+  }();
+  (void)set;
+  return D >= 1 && D <= 128 && nm >= 1 && nm <= 8 && mlpw_lds_bytes(D, nm, 1) <= (size_t)kMlpwDynLds;
+}
+
 size_t mlp_lds_bytes(int64_t D) {
   const int nw = std::min<int>(kMaxWaves, (int)((D + 15) / 16));
   return sizeof(float) * (size_t)(nw * kWS + 2 * kRows * lds_stride((int)D));
@@ -352,7 +795,16 @@ bool mlp_lds_ok(int64_t D) {
 // slower than the per-GEMM path it replaces: train step 1148-1182 vs 1110 us (32- and 16-row
 // workgroups). Each workgroup walks 2 * nm dependent GEMM phases with only ~1-2 workgroups per CU
 // to overlap them, while the per-GEMM kernels spread each phase over ~440 workgroups.
+// The weight-resident kernels (default for D <= 128 whose weights fit LDS; AIMX_MLPW=0 turns them
+// off) or the per-row-tile ones (AIMX_FUSED_MLP=1).
+// (read per call, ~6 calls per train step: tests switch the paths inside one process)
+bool mlpw_on(int64_t D, int64_t nm) {
+  const char* e = getenv("AIMX_MLPW");
+  return (!e || atoi(e) != 0) && mlpw_lds_ok(D, nm);
+}
+
 bool mlp_fused_ok(int64_t D, int64_t nm) {
+  if (mlpw_on(D, nm)) return true;
   const char* e = getenv("AIMX_FUSED_MLP");
   return e && atoi(e) == 1 && D >= 4 && D % 4 == 0 && nm >= 1 && nm <= 8 && mlp_lds_ok(D);
 }
@@ -385,6 +837,16 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
   }
   p.out = out;
   p.ldo = ldo;
+  if (mlpw_on(s->D, nm)) {
+    const int rt = mlpw_rt(s->N, s->D, nm);
+    const int items = rt * (pad16((int)s->D) / 16);
+    const int64_t chunks = cdiv(s->N, 16 * rt);
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(chunks, g_num_cus()));
+    hipLaunchKernelGGL(k_mlpw_fwd, dim3(blocks), dim3(64 * std::min(items, kWMaxWaves)), mlpw_lds_bytes(s->D, nm, rt), st,
+                       p, rt);
+    AIMX_CHECK_LAUNCH();
+    return AIMX_OK;
+  }
   const unsigned blocks = (unsigned)cdiv(s->N, kRows);
   hipLaunchKernelGGL(k_mlp_fwd, dim3(blocks), dim3(mlp_threads(s->D)), mlp_lds_bytes(s->D), st, p);
   AIMX_CHECK_LAUNCH();
@@ -414,6 +876,16 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
     p.dA[k] = (k < nm - 1) ? dA[k] : nullptr;
   }
   p.dug = dug;
+  if (mlpw_on(s->D, nm)) {
+    const int rt = mlpw_rt(s->N, s->D, nm);
+    const int items = rt * (pad16((int)s->D) / 16);
+    const int64_t chunks = cdiv(s->N, 16 * rt);
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(chunks, g_num_cus()));
+    hipLaunchKernelGGL(k_mlpw_bwd, dim3(blocks), dim3(64 * std::min(items, kWMaxWaves)), mlpw_lds_bytes(s->D, nm, rt), st,
+                       p, rt);
+    AIMX_CHECK_LAUNCH();
+    return AIMX_OK;
+  }
   const unsigned blocks = (unsigned)cdiv(s->N, kRows);
   hipLaunchKernelGGL(k_mlp_bwd, dim3(blocks), dim3(mlp_threads(s->D)), mlp_lds_bytes(s->D), st, p);
   AIMX_CHECK_LAUNCH();

@@ -864,9 +864,18 @@ def test_fused_head_clusters_bit_identical(G, monkeypatch):
 
 @pytest.mark.parametrize("name", ["c2", "c3"])
 def test_fused_mlp_opt_in_parity(name, monkeypatch):
-    """AIMX_FUSED_MLP=1 (all MLP blocks of a shell layer in one launch each way, mlp.hip) keeps
-    the model within the parity contract (outputs and every gradient vs the fp64 oracle)."""
+    """AIMX_MLPW=0 AIMX_FUSED_MLP=1 (the per-row-tile fused MLP chain, mlp.hip) keeps the model
+    within the parity contract (outputs and every gradient vs the fp64 oracle)."""
+    monkeypatch.setenv("AIMX_MLPW", "0")
     monkeypatch.setenv("AIMX_FUSED_MLP", "1")
+    test_model_case(name)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "act_gelu", "stereo"])
+def test_per_gemm_mlp_path_parity(name, monkeypatch):
+    """AIMX_MLPW=0 (one GEMM per MLP linear, the path D > 128 always takes) keeps the small-D cases
+    within the parity contract too (the default there is the weight-resident fused chain)."""
+    monkeypatch.setenv("AIMX_MLPW", "0")
     test_model_case(name)
 
 
