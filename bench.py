@@ -166,6 +166,9 @@ def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launch
     from aimx.plan import GraphPlan
     n0 = batch.num_atoms
     d = int(0.3 * hidden)
+    # the hop kernel indexes its output with 32-bit thread ids (rows * D < 2^31, hop.hip): wide
+    # configs (c5: 6 hops x 307 columns) get a proportionally smaller probe graph
+    target_atoms = min(target_atoms, int(0.95 * (2 ** 31 - 1) / (hops * d)))
     reps = max(1, target_atoms // n0)
     e0 = batch.edges
     off = (torch.arange(reps, device=device, dtype=torch.int64) * n0).view(reps, 1, 1)
