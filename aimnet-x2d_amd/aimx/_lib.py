@@ -48,6 +48,18 @@ class LossAccum(ctypes.Structure):
                 ("scale", ctypes.c_float)]
 
 
+class PadBatch(ctypes.Structure):
+    """AimxPadBatch (include/aimx.h): static padded inputs of one autograph shape bucket."""
+    _fields_ = [("feat", ctypes.c_void_p * 4), ("feat_stride", ctypes.c_int64 * 4),
+                ("edges", ctypes.c_void_p), ("edge_s0", ctypes.c_int64), ("edge_s1", ctypes.c_int64),
+                ("batch", ctypes.c_void_p), ("batch_stride", ctypes.c_int64),
+                ("charges", ctypes.c_void_p), ("charge_stride", ctypes.c_int64),
+                ("N", ctypes.c_int64), ("E", ctypes.c_int64), ("G", ctypes.c_int64),
+                ("out_feat", ctypes.c_void_p), ("out_edges", ctypes.c_void_p), ("out_batch", ctypes.c_void_p),
+                ("out_charges", ctypes.c_void_p), ("Np", ctypes.c_int64), ("Ep", ctypes.c_int64),
+                ("pad_mols", ctypes.c_int64)]
+
+
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ("M", c_i64), ("N", c_i64), ("K", c_i64),
@@ -198,6 +210,7 @@ _SIGS = {
     "aimx_head_backward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
     "aimx_head_backward": (c_i32, [ctypes.POINTER(Head), ctypes.POINTER(HeadGrad), c_ptr]),
     "aimx_dropout_seeds": (c_i32, [c_ptr, c_ptr, c_i32, c_ptr]),
+    "aimx_pad_batch": (c_i32, [c_ptr, c_ptr]),
     "aimx_stereo_forward": (c_i32, [ctypes.c_void_p, c_ptr]),
     "aimx_stereo_backward": (c_i32, [ctypes.c_void_p, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr]),
     "aimx_l1_loss_forward": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr]),

@@ -1,0 +1,261 @@
+"""Drop-in autograph: the unchanged eager trainer's GNN forward and backward replayed as HIP graphs.
+
+The reference trainer (src/training/trainer.py:151-164) runs every step eagerly:
+    output, _, _ = model(*batch); loss = criterion(output, y); loss.backward(); optimizer.step()
+Eagerly, the c2 step is bound by the host (~60 operator calls through Python and ctypes per
+step, ~2 ms) rather than by the ~0.9 ms of device work. By default (AIMX_AUTOGRAPH=0 or
+`enable(model, False)` turns it off), `GNN.forward` in training mode instead:
+
+  * pads the batch into the static inputs of a shape bucket — the smallest live one with the same
+    molecule count and room for the batch's atoms (plus one slack atom) and edges; a new bucket
+    takes ~6 % headroom, atoms rounded up to a multiple of 512 and edges to 4096 — in ONE
+    launch (`aimx_pad_batch`: slack atoms form 8 padding molecules, slack edges are self-pairs
+    over them, the layout of aimx.data.pad_collated, so no real molecule's values change);
+  * replays the bucket's forward graph and returns the real molecules' rows of the output through
+    an autograd node whose backward copies the incoming gradient into the static gradient buffer
+    and replays the bucket's backward graph;
+  * hands the parameters their gradients as the bucket's static gradient tensors (assigned when
+    `.grad` is None — `zero_grad(set_to_none=True)`, PyTorch's default; accumulated otherwise).
+
+A bucket is captured on first use (warm-up on a side stream, then the forward graph and the
+backward graph, each in its own memory pool so that no replay overwrites the other's live
+tensors). The eager path
+is used instead when a graph cannot reproduce eager semantics: grad disabled or eval mode,
+stereochemistry inputs, a batch without edges, stream capture already active (GraphedTrainStep),
+gradient hooks on the parameters or an initialised multi-rank process group (DDP's reducer hooks
+the gradient accumulators, which a replay bypasses), or parameters replaced since the capture
+(re-captured). The attention weights and partial charges come back as detached copies.
+"""
+import ctypes
+import os
+
+import torch
+
+from . import _lib
+from ._lib import AimxError, check, ptr, stream_ptr
+
+ATOM_QUANTUM = 512
+EDGE_QUANTUM = 4096
+PAD_MOLS = 8
+MAX_BUCKETS = 4
+_FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
+
+
+def enable(model, on=True):
+    """Turn the autograph on (or off) for one GNN, whatever AIMX_AUTOGRAPH says."""
+    model._aimx_autograph_on = bool(on)
+    return model
+
+
+def wanted(model, args):
+    on = getattr(model, "_aimx_autograph_on", None)
+    if on is None:
+        on = os.environ.get("AIMX_AUTOGRAPH", "1") != "0"
+    if not on or getattr(model, "_aimx_autograph_off", False):
+        return False
+    if not (model.training and torch.is_grad_enabled()) or torch.cuda.is_current_stream_capturing():
+        return False
+    feats, edges, batch, charges, tet, cis, trans = args
+    if edges.numel() == 0 or edges.dim() != 2 or edges.shape[1] != 2 or edges.dtype != torch.int64:
+        return False
+    if model.use_stereochemistry and (tet.numel() or cis.numel() or trans.numel()):
+        return False
+    if charges.dtype != torch.float32 or batch.dtype != torch.int64 or charges.dim() != 1:
+        return False
+    if any(feats[k].dtype != torch.int64 or feats[k].dim() != 1 for k in _FEATURE_KEYS):
+        return False
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return False
+    except Exception:  # pragma: no cover
+        return False
+    st = _state(model)
+    return not st.hooked(model)
+
+
+class _State:
+    def __init__(self):
+        self.buckets = {}
+        self.order = []
+        self.anchor = None
+
+    def hooked(self, model):
+        """Gradient hooks on a parameter or forward hooks on a submodule (a replay fires neither)."""
+        return any(getattr(p, "_post_accumulate_grad_hooks", None) or getattr(p, "_backward_hooks", None)
+                   for p in model.parameters()) or \
+            any(m._forward_hooks or m._forward_pre_hooks for m in model.modules() if m is not model)
+
+
+def _state(model):
+    st = model.__dict__.get("_aimx_autograph_state")
+    if st is None:
+        st = _State()
+        model.__dict__["_aimx_autograph_state"] = st
+    return st
+
+
+def _round_up(x, q):
+    return (x + q - 1) // q * q
+
+
+class _Bucket:
+    """Static padded inputs, the captured forward / backward graphs and their static outputs."""
+
+    def __init__(self, model, Np, Ep, G, dev):
+        i64 = torch.int64
+        self.Np, self.Ep, self.G, self.dev = Np, Ep, G, dev
+        self.feat = torch.zeros(4, Np, dtype=i64, device=dev)
+        self.edges = torch.zeros(Ep, 2, dtype=i64, device=dev)
+        self.batch = torch.zeros(Np, dtype=i64, device=dev)
+        self.charges = torch.zeros(G + PAD_MOLS, dtype=torch.float32, device=dev)
+        self.empty4 = torch.empty(0, 4, dtype=i64, device=dev)
+        self.empty2 = torch.empty(0, 2, dtype=i64, device=dev)
+        a = _lib.PadBatch()
+        a.out_feat, a.out_edges, a.out_batch, a.out_charges = ptr(self.feat), ptr(self.edges), ptr(self.batch), \
+            ptr(self.charges)
+        a.Np, a.Ep, a.pad_mols = Np, Ep, PAD_MOLS
+        self.pad = a
+        self.params = [p for p in model.parameters()]
+        self.param_key = tuple(p.data_ptr() for p in self.params)
+        self.gen = 0        # forward replays so far
+        self.done = -1      # generation whose backward has run
+
+    def static_args(self):
+        return ({k: self.feat[i] for i, k in enumerate(_FEATURE_KEYS)}, self.edges, self.batch, self.charges,
+                self.empty4, self.empty2, self.empty2)
+
+    def fill(self, feats, edges, batch, charges):
+        a = self.pad
+        for i, k in enumerate(_FEATURE_KEYS):
+            t = feats[k]
+            a.feat[i] = t.data_ptr()
+            a.feat_stride[i] = t.stride(0)
+        a.edges, a.edge_s0, a.edge_s1 = edges.data_ptr(), edges.stride(0), edges.stride(1)
+        a.batch, a.batch_stride = batch.data_ptr(), batch.stride(0)
+        a.charges, a.charge_stride = charges.data_ptr(), charges.stride(0)
+        a.N, a.E, a.G = batch.shape[0], edges.shape[0], charges.shape[0]
+        check(_lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(self.dev)), "autograph pad_batch")
+
+    def capture(self, model, warmup=2):
+        params = self.params
+        saved = [p.grad for p in params]
+        for p in params:
+            p.grad = None
+        args = self.static_args()
+        cur = torch.cuda.current_stream(self.dev)
+        side = torch.cuda.Stream(device=self.dev)
+        side.wait_stream(cur)
+        try:
+            with torch.cuda.stream(side):  # warm-up: plans, workspaces, allocator pools, seed state
+                for _ in range(warmup):
+                    out = model._aimx_forward(*args)[0]
+                    out.backward(torch.zeros_like(out))
+                    for p in params:
+                        p.grad = None
+            cur.wait_stream(side)
+            torch.cuda.synchronize(self.dev)
+            self.g_fwd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_fwd):
+                self.outs = model._aimx_forward(*args)
+            self.gout = torch.zeros_like(self.outs[0])
+            # the backward graph gets its own memory pool: in a shared one, the gradient tensors it
+            # leaves behind could sit in blocks the forward graph used (and frees) for temporaries,
+            # and the next forward replay would overwrite the caller's .grad
+            self.g_bwd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_bwd):
+                torch.autograd.backward(self.outs[0], self.gout)
+            self.grads = [p.grad for p in params]
+            self.outs = tuple(o.detach() if o is not None else None for o in self.outs)
+        finally:
+            for p, g in zip(params, saved):
+                p.grad = g
+
+
+class _Replay(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, bucket, G):
+        ctx.bucket, ctx.G, ctx.gen = bucket, G, bucket.gen
+        return bucket.outs[0][:G].clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        b = ctx.bucket
+        if b.gen != ctx.gen or b.done == ctx.gen:
+            raise AimxError("aimx autograph: this output's saved state was overwritten by a later forward of the "
+                            "same shape bucket (or its backward already ran); run one backward per forward, or "
+                            "set AIMX_AUTOGRAPH=0")
+        b.gout[:ctx.G].copy_(gout)
+        # the replay overwrites the static gradient tensors: keep what a caller that did not
+        # set .grad to None expects to accumulate onto
+        keep = {}
+        for p, sg in zip(b.params, b.grads):
+            if sg is not None and p.grad is sg:
+                keep[id(p)] = sg.clone()
+        b.g_bwd.replay()
+        b.done = ctx.gen
+        for p, sg in zip(b.params, b.grads):
+            if sg is None:
+                continue
+            if p.grad is None:
+                p.grad = sg                      # zero_grad(set_to_none=True): the fast path
+            elif p.grad is sg:
+                sg.add_(keep[id(p)])
+            else:
+                p.grad.add_(sg)
+        return None, None, None
+
+
+def _pick(st, N, E, G, dev):
+    """The smallest live bucket that holds this batch (same molecule count, room for one slack atom
+    and every edge), else a new one sized with ~6 % headroom so the batches of an epoch settle on
+    one or two buckets."""
+    best = None
+    for key, b in st.buckets.items():
+        if key[2] == G and key[3] == dev.index and key[0] > N and key[1] >= E and \
+                (best is None or key[0] + key[1] < best[0] + best[1]):
+            best = key
+    if best is not None:
+        return best, False
+    return (_round_up(int(1.06 * (N + 1)) + 1, ATOM_QUANTUM), _round_up(int(1.06 * E) + 1, EDGE_QUANTUM), G,
+            dev.index), True
+
+
+def run(model, args):
+    """GNN.forward through the bucket's graphs (see the module docstring)."""
+    feats, edges, batch, charges = args[:4]
+    N, E, G = batch.shape[0], edges.shape[0], charges.shape[0]
+    dev = batch.device
+    st = _state(model)
+    key, fresh = _pick(st, N, E, G, dev)
+    b = st.buckets.get(key)
+    if b is not None and b.param_key != tuple(p.data_ptr() for p in b.params):
+        st.buckets.pop(key)
+        st.order.remove(key)
+        b, fresh = None, True
+    if fresh:
+        if len(st.order) >= MAX_BUCKETS:
+            st.buckets.pop(st.order.pop(0))
+        b = _Bucket(model, key[0], key[1], G, dev)
+    else:
+        st.order.remove(key)
+    st.order.append(key)  # least recently used first
+    b.fill(feats, edges, batch, charges)
+    if fresh:
+        b.capture(model)
+        st.buckets[key] = b
+    b.g_fwd.replay()
+    b.gen += 1
+    if st.anchor is None or st.anchor.device != dev:
+        st.anchor = torch.zeros((), device=dev, requires_grad=True)
+    out = _Replay.apply(st.anchor, b, G)
+    return out, _atoms(b.outs[1], b.Np, N), _atoms(b.outs[2], b.Np, N)
+
+
+def _atoms(t, Np, N):
+    """The real atoms' part of a per-atom static output (atoms on its first or last dim), copied."""
+    if t is None:
+        return None
+    if t.shape[-1] == Np:
+        return t[..., :N].clone()
+    return t[:N].clone()

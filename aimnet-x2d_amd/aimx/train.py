@@ -64,6 +64,7 @@ class GraphedTrainStep:
                  ddp_graph=None):
         import os
         self.model, self.criterion, self.optimizer, self.sync = model, criterion, optimizer, sync
+        model._aimx_autograph_off = True  # this step captures the model itself (aimx.autograph stays off)
         self.B = _real_rows(example_batch) if n_real is None else int(n_real)
         self.static = example_batch.clone()
         dev = self.static._blob.device

@@ -64,10 +64,61 @@ __global__ void k_dropout_seeds(int64_t* __restrict__ state, int64_t* __restrict
   state[0] = (int64_t)(s + 0x9E3779B97F4A7C15ull * (uint64_t)(n + 1));
 }
 
+// Static padded inputs of one autograph bucket (aimx_pad_batch): real rows copied, slack atoms
+// dealt to pad_mols padding molecules of near-equal size (molecule ids G, G+1, ...; the first
+// slack % pad_mols take one atom more), slack edges self-pairs spread over the slack atoms — the
+// layout of aimx.data.pad_collated, so every real molecule's values are untouched.
+__global__ __launch_bounds__(256) void k_pad_batch(const AimxPadBatch p) {
+  const int64_t slack = p.Np - p.N;
+  const int64_t q = slack / p.pad_mols, r = slack % p.pad_mols;
+  const int64_t total = max(max(p.Np, p.Ep), p.G + p.pad_mols);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < p.Np) {
+      const bool real = i < p.N;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p.out_feat[k * p.Np + i] = real ? p.feat[k][i * p.feat_stride[k]] : 0;
+      int64_t m;
+      if (real) {
+        m = p.batch[i * p.batch_stride];
+      } else {
+        const int64_t s = i - p.N;
+        m = p.G + (s < r * (q + 1) ? s / (q + 1) : r + (s - r * (q + 1)) / q);
+      }
+      p.out_batch[i] = m;
+    }
+    if (i < p.Ep) {
+      int64_t t, s;
+      if (i < p.E) {
+        t = p.edges[i * p.edge_s0];
+        s = p.edges[i * p.edge_s0 + p.edge_s1];
+      } else {
+        t = s = p.N + (i - p.E) % slack;
+      }
+      p.out_edges[2 * i] = t;
+      p.out_edges[2 * i + 1] = s;
+    }
+    if (i < p.G + p.pad_mols) p.out_charges[i] = i < p.G ? p.charges[i * p.charge_stride] : 0.f;
+  }
+}
+
 }  // namespace
 }  // namespace aimx
 
 using namespace aimx;
+
+extern "C" int aimx_pad_batch(const AimxPadBatch* p, aimx_stream_t stream) {
+  if (!p || p->N < 0 || p->E < 0 || p->G < 0 || p->pad_mols < 1 || p->Np <= p->N || p->Ep < p->E) return AIMX_EARG;
+  for (int k = 0; k < 4; ++k)
+    if ((p->N > 0 && !p->feat[k]) || p->feat_stride[k] < 1) return AIMX_EARG;
+  if ((p->N > 0 && !p->batch) || (p->E > 0 && !p->edges) || (p->G > 0 && !p->charges) || !p->out_feat ||
+      !p->out_batch || !p->out_edges || !p->out_charges || p->batch_stride < 1 || p->charge_stride < 1)
+    return AIMX_EARG;
+  const int64_t total = std::max({p->Np, p->Ep, p->G + p->pad_mols});
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(total, 256), 2048);
+  hipLaunchKernelGGL(k_pad_batch, dim3(grid), dim3(256), 0, (hipStream_t)stream, *p);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
 
 extern "C" int aimx_multi_copy(const AimxCopyItem* items, int32_t n_items, aimx_stream_t stream) {
   if (n_items < 0 || (n_items > 0 && !items)) return AIMX_EARG;

@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from aimx import _lib, ops
+from aimx import _lib, autograph, ops
 from aimx.plan import GraphPlan
 from utils.activation import activation_name, get_activation_function
 
@@ -121,7 +121,16 @@ class GNN(nn.Module):
                 batch_indices: torch.Tensor, total_charges: torch.Tensor, tetrahedral_indices: torch.Tensor,
                 cis_indices: torch.Tensor, trans_indices: torch.Tensor
                 ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
+        args = (atom_features, multi_hop_edge_indices, batch_indices, total_charges, tetrahedral_indices,
+                cis_indices, trans_indices)
         _lib.require_device(multi_hop_edge_indices, batch_indices, total_charges)
+        if autograph.wanted(self, args):  # per-shape-bucket graph replay (aimx/autograph.py; AIMX_AUTOGRAPH=0: off)
+            return autograph.run(self, args)
+        return self._aimx_forward(*args)
+
+    def _aimx_forward(self, atom_features, multi_hop_edge_indices, batch_indices, total_charges,
+                      tetrahedral_indices, cis_indices, trans_indices):
+        """gnn.py:197-260 eagerly: one HIP operator per reference stage."""
         # gnn.py:221-225: four lookups + cat + projection + activation, fused on the device
         atom_embeddings = ops.embed_project(
             [atom_features[k] for k in _FEATURE_KEYS],

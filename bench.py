@@ -448,13 +448,17 @@ def _cpu_rate(cfg, threads, seconds, max_steps):
                       f"{cfg['hops']} hops), oracle/model.py fp32 torch-CPU, {threads} threads"}
 
 
-def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5):
+def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False):
     """The drop-in (unchanged reference trainer) rate: a fresh model trained eagerly on unpadded
     resident batches — forward, L1 loss, backward, clip + Adam, one Python call per op as
-    trainer.py:151-164 runs it (no graph). A side measurement; never the metric `value`."""
+    trainer.py:151-164 runs it (no graph). autograph: the same loop with aimx.autograph on (the
+    model's forward and backward replayed per shape bucket, AIMX_AUTOGRAPH=1); the bucket's
+    capture happens in the warm-up. A side measurement; never the metric `value`."""
     from aimx.optim import FusedAdam
     from models import L1Loss
     model = build_model(cfg, device)
+    from aimx import autograph as ag
+    ag.enable(model, autograph)
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
     loss_fn = L1Loss()
     bs = make_batches(cfg, batches_eager, 777, device, pad=False)
@@ -476,7 +480,10 @@ def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5):
     del model, opt, bs
     torch.cuda.empty_cache()
     return {"value": round(cfg["batch"] * steps / dt, 1), "unit": "molecules/s", "ms_per_step": round(dt / steps * 1e3, 4),
-            "steps": steps, "warmup": warmup, "mode": "eager (no HIP graph), unpadded batches, same step"}
+            "steps": steps, "warmup": warmup,
+            "mode": ("eager loop as the unchanged trainer runs it; the model's forward/backward replayed per "
+                     "shape bucket by aimx.autograph (the default), unpadded batches, same step") if autograph else
+            "eager, every operator launched from Python (AIMX_AUTOGRAPH=0), unpadded batches, same step"}
 
 
 def main():
@@ -622,6 +629,7 @@ def main():
     eager = None
     if rank == 0 and world == 1 and args.graph and feeder is None and not args.no_eager and not args.amp:
         eager = eager_rate(cfg, device, batches_eager=4, steps=args.eager_steps)
+        eager["autograph"] = eager_rate(cfg, device, batches_eager=4, steps=args.eager_steps, autograph=True)
     roof = extra = None
     if rank == 0 and not args.no_roofline:
         del batches

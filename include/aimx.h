@@ -503,6 +503,32 @@ int aimx_stereo_backward(const AimxStereo* p, const float* d_out, int64_t ld_dou
  * state once from torch's generator, so torch.manual_seed still fixes the masks. */
 int aimx_dropout_seeds(int64_t* state, int64_t* seeds, int32_t n, aimx_stream_t stream);
 
+/* Static padded inputs of one shape bucket of the drop-in autograph (aimx/autograph.py): the
+ * reference's collated tensors (molecular.py:339-458: 4 int64 feature columns [N], edges [E, 2]
+ * int64 (target, source), batch [N] int64, total_charges [G] f32; any element strides) copied
+ * into static buffers of Np > N atoms and Ep >= E edges. The Np - N slack atoms form pad_mols
+ * padding molecules (ids G .. G + pad_mols - 1, near-equal sizes) and the slack edges are
+ * self-pairs over them, so no real molecule's values change (aimx.data.pad_collated's layout).
+ * out_feat holds the 4 columns back to back ([4][Np]); out_edges is [Ep, 2] contiguous; one
+ * launch. Replaces the per-shape re-collate the reference would need to replay a graph. */
+typedef struct AimxPadBatch {
+  const int64_t* feat[4];
+  int64_t feat_stride[4];
+  const int64_t* edges;
+  int64_t edge_s0, edge_s1;
+  const int64_t* batch;
+  int64_t batch_stride;
+  const float* charges;
+  int64_t charge_stride;
+  int64_t N, E, G;
+  int64_t* out_feat;
+  int64_t* out_edges;
+  int64_t* out_batch;
+  float* out_charges;
+  int64_t Np, Ep, pad_mols;
+} AimxPadBatch;
+int aimx_pad_batch(const AimxPadBatch* p, aimx_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Gradient all-reduce over RCCL (xGMI inside an MI355X node) — the DDP reducer's collective
  * (reference runner.py:703-707 wraps the model in DistributedDataParallel over "nccl" = RCCL).

@@ -1,0 +1,164 @@
+"""GPU: the drop-in autograph (aimx/autograph.py). An unchanged eager training loop
+(reference trainer.py:151-164) with AIMX_AUTOGRAPH on must give the eager path's outputs,
+gradients and parameter trajectory; the padding of its shape buckets must not leak into any real
+molecule."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CFG = dict(source="qm9", hidden=128, hops=3, batch=64, tasks=1, pc=False)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import aimx
+    aimx.load()
+
+
+def _model(seed=0, dropout=0.0, pc=False, ag=False):
+    """ag: the autograph on (the default for GNN) or off (every operator launched eagerly)."""
+    from aimx import autograph
+    from models import GNN
+    torch.manual_seed(seed)
+    fs = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+    m = GNN(fs, CFG["hidden"], 1, num_shells=3, dropout=dropout, shell_conv_dropout=dropout, ffn_dropout=dropout,
+            use_partial_charges=pc).to(DEV).train()
+    return autograph.enable(m, ag)
+
+
+def _batches(n, seed, batch=None):
+    import bench
+    cfg = dict(CFG, batch=batch or CFG["batch"])
+    return bench.make_batches(cfg, n, seed, DEV, pad=False)
+
+
+def _rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("pc", [False, True])
+def test_autograph_matches_eager_forward_and_gradients(pc):
+    from aimx import autograph
+    b = _batches(1, 11)[0]
+    m1 = _model(pc=pc)
+    m2 = _model(pc=pc)
+    m2.load_state_dict(m1.state_dict())
+    autograph.enable(m2)
+    for _ in range(2):  # first call captures the bucket, second replays it
+        for m in (m1, m2):
+            m.zero_grad(set_to_none=True)
+        o1, a1, q1 = m1(*b.model_args())
+        o2, a2, q2 = m2(*b.model_args())
+        (o1.square().sum() + o1.sum()).backward()
+        (o2.square().sum() + o2.sum()).backward()
+        assert o2.shape == o1.shape and _rel(o2, o1) < 1e-6
+        assert a2.shape == a1.shape and _rel(a2, a1) < 1e-6
+        if pc:
+            assert q2.shape == q1.shape and _rel(q2, q1) < 1e-6
+        for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+            if p1.grad is None:
+                assert p2.grad is None, k
+                continue
+            assert _rel(p2.grad, p1.grad) < 1e-5, k
+    st = m2.__dict__["_aimx_autograph_state"]
+    assert len(st.buckets) == 1
+
+
+def test_autograph_training_tracks_eager_over_buckets():
+    """Adam over batches of two sizes (two shape buckets, each replayed): same trajectory."""
+    from aimx import autograph
+    from aimx.optim import FusedAdam
+    from models import L1Loss
+    bs = _batches(3, 21) + _batches(2, 22, batch=40)
+    order = [0, 3, 1, 4, 2, 0, 3]
+    m1 = _model()
+    m2 = _model()
+    m2.load_state_dict(m1.state_dict())
+    autograph.enable(m2)
+    o1 = FusedAdam(m1.parameters(), lr=1e-3, max_grad_norm=1.0)
+    o2 = FusedAdam(m2.parameters(), lr=1e-3, max_grad_norm=1.0)
+    crit = L1Loss()
+    l1s, l2s = [], []
+    for i in order:
+        b = bs[i]
+        for m, o, ls in ((m1, o1, l1s), (m2, o2, l2s)):
+            o.zero_grad(set_to_none=True)
+            out, _, _ = m(*b.model_args())
+            loss = crit(out, b.targets)
+            loss.backward()
+            o.step()
+            ls.append(loss.item())
+    np.testing.assert_allclose(l2s, l1s, rtol=1e-4, atol=1e-6)
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert (p1 - p2).abs().max().item() <= 1e-4 * max(1.0, p1.abs().max().item()), k
+    assert len(m2.__dict__["_aimx_autograph_state"].buckets) == 2
+
+
+def test_autograph_accumulates_without_set_to_none():
+    from aimx import autograph
+    b = _batches(1, 31)[0]
+    m1 = _model()
+    m2 = _model()
+    m2.load_state_dict(m1.state_dict())
+    autograph.enable(m2)
+    for m in (m1, m2):
+        for _ in range(2):  # two backward passes into the same .grad (gradient accumulation)
+            out, _, _ = m(*b.model_args())
+            out.sum().backward()
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        if p1.grad is not None:
+            assert _rel(p2.grad, p1.grad) < 1e-5, k
+    for m in (m1, m2):
+        m.zero_grad(set_to_none=False)  # in-place zero: the next backward must not add stale values
+        out, _, _ = m(*b.model_args())
+        out.sum().backward()
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        if p1.grad is not None:
+            assert _rel(p2.grad, p1.grad) < 1e-5, k
+
+
+def test_autograph_is_the_default_and_reuses_buckets():
+    """GNN's training forward goes through the autograph unless AIMX_AUTOGRAPH=0; batches that fit a
+    live bucket (same molecule count) reuse it instead of capturing another."""
+    import os
+    from aimx import autograph
+    from models import GNN
+    assert os.environ.get("AIMX_AUTOGRAPH", "1") != "0"
+    torch.manual_seed(0)
+    fs = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+    m = GNN(fs, CFG["hidden"], 1, num_shells=3).to(DEV).train()
+    bs = sorted(_batches(4, 51), key=lambda b: -b.num_atoms)
+    for b in bs:
+        assert autograph.wanted(m, b.model_args())
+        out, _, _ = m(*b.model_args())
+        out.sum().backward()
+        m.zero_grad(set_to_none=True)
+    assert len(m.__dict__["_aimx_autograph_state"].buckets) == 1
+
+
+def test_autograph_falls_back_and_guards():
+    from aimx import autograph
+    from aimx._lib import AimxError
+    b = _batches(1, 41)[0]
+    m = _model()
+    autograph.enable(m)
+    with torch.no_grad():
+        m(*b.model_args())  # grad disabled: eager, no bucket
+    m.eval()
+    m(*b.model_args())      # eval mode: eager
+    m.train()
+    assert not m.__dict__.get("_aimx_autograph_state") or not m.__dict__["_aimx_autograph_state"].buckets
+    o1, _, _ = m(*b.model_args())
+    o2, _, _ = m(*b.model_args())  # second forward of the same bucket before the first backward
+    o2.sum().backward()
+    with pytest.raises(AimxError):
+        o1.sum().backward()
+    h = m.pooling.register_forward_hook(lambda *a: None)
+    try:
+        assert not autograph.wanted(m, b.model_args())  # module hooks would stop firing on replay
+    finally:
+        h.remove()

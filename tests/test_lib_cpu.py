@@ -38,7 +38,8 @@ def test_struct_layouts_match_header():
     for cname, py in (("AimxGemmArgs", _lib.GemmArgs), ("AimxShellStack", _lib.ShellStack),
                       ("AimxShellStackGrad", _lib.ShellStackGrad), ("AimxEmbeddingTables", _lib.EmbeddingTables),
                       ("AimxHead", _lib.Head), ("AimxHeadGrad", _lib.HeadGrad), ("AimxAdamTensor", _lib.AdamTensor),
-                      ("AimxAdamHyper", _lib.AdamHyper), ("AimxLossAccum", _lib.LossAccum)):
+                      ("AimxAdamHyper", _lib.AdamHyper), ("AimxLossAccum", _lib.LossAccum),
+                      ("AimxPadBatch", _lib.PadBatch)):
         body = re.search(r"typedef struct (?:%s )?\{([^{}]*)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = re.findall(r"\**\s*(\w+)\s*(?:\[[^\]]*\])?\s*[;,]", body)
