@@ -152,6 +152,7 @@ struct MlpFwd {
   uint8_t* M[8];
   float* out;
   int64_t ldo;
+  int32_t v4;  // fill with 16-byte loads (D, 2D and every weight / row pointer 4-float aligned)
 };
 
 __global__ __launch_bounds__(512) void k_mlp_fwd(const MlpFwd p) {
@@ -255,6 +256,7 @@ struct MlpBwd {
   float* dV[8];
   float* dA[8];     // dA_k for k = 1..nm-1 (the gradient w.r.t. block k's input), index k - 1
   float* dug;       // [N, 2D]: [du | dY]
+  int32_t v4;       // fill with 16-byte loads (D, lddy and every weight / dy pointer 4-float aligned)
 };
 
 __global__ __launch_bounds__(512) void k_mlp_bwd(const MlpBwd p) {
@@ -462,6 +464,82 @@ __device__ __forceinline__ void fill_lds(float* Wl, const float* const* wtab, in
   }
 }
 
+// fill_lds with 16-byte loads (MlpFwd/MlpBwd.v4: D, the row stride and every pointer 4-float
+// aligned). A dword load is address-rate bound at a quarter of a dwordx4's bytes, and the fill's
+// ~25 k weight floats per workgroup made it ~7 us of a ~23 us layer at c2. Weights come in as
+// float4 along their contiguous dim: [n][k..k+3] stored as one 16-byte LDS write; for TR the
+// column run W[k][n..n+3] lands in 4 image rows (4 dword LDS writes). Zero padding as in fill_lds
+// (a group is wholly inside D or wholly past it, since D % 4 == 0).
+constexpr int kFillW4 = 2, kFillR4 = 2;
+template <bool TR>
+__device__ __forceinline__ void fill_lds_v4(float* Wl, const float* const* wtab, int nmat, int D, int Kp, int S,
+                                            float* Rl, const float* src, int64_t lds_, int64_t r0, int R, int64_t N) {
+  const int NT = blockDim.x, tid = threadIdx.x;
+  const int kq = Kp / 4, per4 = Kp * kq, totr4 = R * kq;
+  const uint32_t wbytes = 4u * (uint32_t)(D * D), OOB = 0xFFFFFFF0u;
+  const int64_t nrows = max<int64_t>(0, min<int64_t>(R, N - r0));
+  const __amdgpu_buffer_rsrc_t rr = mlp_rsrc(src + r0 * lds_, (uint32_t)(4 * max<int64_t>(1, nrows * lds_)));
+  auto ld4 = [](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  };
+  for (int m0 = 0; m0 < nmat; m0 += kFillM) {
+    for (int e0 = 0; e0 < per4; e0 += kFillW4 * NT) {
+      floatx4 v[kFillM][kFillW4], q[kFillR4];
+#pragma unroll
+      for (int mi = 0; mi < kFillM; ++mi) {
+        const int m = min(m0 + mi, nmat - 1);
+        const __amdgpu_buffer_rsrc_t rw = mlp_rsrc(wtab[m], wbytes);
+#pragma unroll
+        for (int u = 0; u < kFillW4; ++u) {
+          const int g = e0 + u * NT + tid, a = g / kq, b4 = 4 * (g - a * kq);  // (row a, cols b4..b4+3) of W
+          const bool ok = g < per4 && a < D && b4 < D;
+          v[mi][u] = ld4(rw, ok ? 4u * (uint32_t)(a * D + b4) : OOB);
+        }
+      }
+      const bool rows = m0 == 0 && e0 == 0;
+#pragma unroll
+      for (int u = 0; u < kFillR4; ++u) {
+        const int g = u * NT + tid, r = g / kq, c = 4 * (g - r * kq);
+        const bool ok = rows && g < totr4 && c < D && r < nrows;
+        q[u] = ld4(rr, ok ? 4u * (uint32_t)(r * lds_ + c) : OOB);
+      }
+#pragma unroll
+      for (int mi = 0; mi < kFillM; ++mi) {
+        if (m0 + mi >= nmat) break;
+        float* img = Wl + (m0 + mi) * Kp * S;
+#pragma unroll
+        for (int u = 0; u < kFillW4; ++u) {
+          const int g = e0 + u * NT + tid;
+          if (g < per4) {
+            const int a = g / kq, b4 = 4 * (g - a * kq);
+            if (TR) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) img[(b4 + j) * S + a] = v[mi][u][j];
+            } else {
+              *reinterpret_cast<floatx4*>(img + a * S + b4) = v[mi][u];
+            }
+          }
+        }
+      }
+      if (rows) {
+#pragma unroll
+        for (int u = 0; u < kFillR4; ++u) {
+          const int g = u * NT + tid;
+          if (g < totr4) {
+            const int r = g / kq, c = 4 * (g - r * kq);
+            *reinterpret_cast<floatx4*>(Rl + r * S + c) = q[u];
+          }
+        }
+      }
+    }
+  }
+  for (int g = kFillR4 * NT + tid; g < totr4; g += NT) {  // rows beyond one batch (large R * Kp)
+    const int r = g / kq, c = 4 * (g - r * kq);
+    *reinterpret_cast<floatx4*>(Rl + r * S + c) =
+        ld4(rr, (c < D && r < nrows) ? 4u * (uint32_t)(r * lds_ + c) : OOB);
+  }
+}
+
 // rows [r0, r0 + R) x cols [0, D) of src (row stride lds_) -> LDS rows of stride S, zero beyond D
 // (to Kp) and beyond N
 __device__ __forceinline__ void load_rows(float* dst, int S, const float* src, int64_t lds_, int64_t r0, int R, int D,
@@ -515,7 +593,10 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, in
     const int e = threadIdx.x + u * (int)blockDim.x, m = min(e / Kp, 2 * nm - 1), c = min(e - (e / Kp) * Kp, D - 1);
     bv[u] = btab[m][c];
   }
-  fill_lds<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, 2 * p.D, (int64_t)blockIdx.x * R, R, N);
+  if (p.v4)
+    fill_lds_v4<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, 2 * p.D, (int64_t)blockIdx.x * R, R, N);
+  else
+    fill_lds<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, 2 * p.D, (int64_t)blockIdx.x * R, R, N);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int e = threadIdx.x + u * (int)blockDim.x;
@@ -658,7 +739,10 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
     }
   };
   if (single && (int64_t)blockIdx.x < nchunk) pre_dv(nm - 1, (int64_t)blockIdx.x * R, wave);
-  fill_lds<true>(W, wtab, 2 * nm, D, Kp, S, DA, p.dy, p.lddy, (int64_t)blockIdx.x * R, R, N);
+  if (p.v4)
+    fill_lds_v4<true>(W, wtab, 2 * nm, D, Kp, S, DA, p.dy, p.lddy, (int64_t)blockIdx.x * R, R, N);
+  else
+    fill_lds<true>(W, wtab, 2 * nm, D, Kp, S, DA, p.dy, p.lddy, (int64_t)blockIdx.x * R, R, N);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0 = ch * R;
     if (ch != (int64_t)blockIdx.x) {
@@ -837,6 +921,12 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
   }
   p.out = out;
   p.ldo = ldo;
+  {
+    auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    bool v4 = s->D % 4 == 0 && al(p.ug);
+    for (int64_t k = 0; k < nm; ++k) v4 = v4 && al(p.w1[k]) && al(p.w2[k]);
+    p.v4 = (v4 && !getenv("AIMX_MLPW_FILL1")) ? 1 : 0;  // AIMX_MLPW_FILL1: dword fill (A/B)
+  }
   if (mlpw_on(s->D, nm)) {
     const int rt = mlpw_rt(s->N, s->D, nm);
     const int items = rt * (pad16((int)s->D) / 16);
@@ -876,6 +966,12 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
     p.dA[k] = (k < nm - 1) ? dA[k] : nullptr;
   }
   p.dug = dug;
+  {
+    auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    bool v4 = s->D % 4 == 0 && lddy % 4 == 0 && al(dy);
+    for (int64_t k = 0; k < nm; ++k) v4 = v4 && al(p.w1[k]) && al(p.w2[k]);
+    p.v4 = (v4 && !getenv("AIMX_MLPW_FILL1")) ? 1 : 0;
+  }
   if (mlpw_on(s->D, nm)) {
     const int rt = mlpw_rt(s->N, s->D, nm);
     const int items = rt * (pad16((int)s->D) / 16);

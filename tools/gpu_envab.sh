@@ -9,7 +9,7 @@ for c in $cfgs; do
   for e in "$@"; do
     tag=$(echo "${c}_${e}" | tr -c 'A-Za-z0-9_=\n' '_')
     ev=""; [ "$e" != "default" ] && ev="${e//,/ }"
-    timeout -k 10 240 env $ev python3 bench.py --config $c --no-cpu-baseline --no-roofline --steps 40 --warmup 10 \
+    timeout -k 10 240 env $ev python3 bench.py --config $c --no-cpu-baseline --no-roofline --no-eager --steps 40 --warmup 10 \
       > gpurun_out/envab/$tag.log 2>&1
     rc=$?
     ms=$(grep -o '"ms_per_step": [0-9.]*' gpurun_out/envab/$tag.log | awk '{print $2}')
