@@ -25,6 +25,7 @@
 // hash-dropout with mask store, mask/act' multiplication for the backward, and an implicit ones
 // column that turns a weight-gradient GEMM's last column into the bias gradient.
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 
 #include "aimx_common.h"
@@ -589,18 +590,20 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       if (gridDim.z > 1) epi_load<NEPI>(a, em, en, epre);
       epi_apply<NEPI>(a, em, en, ev, epre);
     } else {
+      // chunks of 8 outputs, each chunk's epilogue operands in flight together (one round trip
+      // per chunk: 2 for a 64x64 tile, was 4 with chunks of 4; all 16 at once needs ~200 VGPRs)
 #pragma unroll
-      for (int q0 = 0; q0 < NEPI; q0 += 4) {
-        int qm[4], qn[4];
-        float ev[4];
+      for (int q0 = 0; q0 < NEPI; q0 += 8) {
+        int qm[8], qn[8];
+        float ev[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const int e = tid + (q0 + u) * 256;
           qm[u] = em[q0 + u];
           qn[u] = en[q0 + u];
           ev[u] = smem[(e / BN) * CS + e % BN];
         }
-        epilogue_n<4>(a, qm, qn, ev);
+        epilogue_n<8>(a, qm, qn, ev);
       }
     }
   }
@@ -1101,6 +1104,21 @@ Plan plan_gemm(const AimxGemmArgs& a) {
       best = w;
       p.bm = c[0];
       p.bn = c[1];
+    }
+  }
+  // Small products (M·N·K < 1.5e9: c1–c3's projections, M ≈ 9 k rows, N, K ≤ 304) take 32 x 32
+  // tiles: ~2300 workgroups instead of ~580 hide the latency of their fused epilogues (bias,
+  // activation, pre-activation / mask stores, residuals) — measured in the c2 step every such GEMM
+  // is 10-20 % faster and the step 0.848 -> 0.809 ms, c3 1.033 -> 0.992 ms, although the bare
+  // GEMMs (tools/gemm_micro.py, no epilogue operands) run faster on 64 x 64; c4/c5's larger
+  // products keep the rule above (32 x 32 there: c4 3.48 -> 3.53, c5 5.23 -> 5.42 ms;
+  // profiles/r02_gemm_tile_ab.txt).
+  if (a.M * a.N * a.K < (int64_t)1500000000) p.bm = p.bn = 32;
+  if (const char* f = getenv("AIMX_GEMM_TILE")) {  // A/B experiments only: "64x64", "64x32", "32x32"
+    const int fm = atoi(f), fn = atoi(strchr(f, 'x') ? strchr(f, 'x') + 1 : f);
+    if ((fm == 64 && (fn == 64 || fn == 32)) || (fm == 32 && fn == 32)) {
+      p.bm = fm;
+      p.bn = fn;
     }
   }
   const int64_t t = tiles(p.bm, p.bn);

@@ -79,7 +79,7 @@ __device__ __forceinline__ void put(const Cluster& cl, float* p, float v) {
 // as 0 by the buffer range check) into the LDS buffer dst (row stride ldl) with sc1 loads.
 template <int W>
 __device__ __forceinline__ void exchange(Cluster& cl, const float* src, int64_t ld, int nvalid, int ncols,
-                                         float* dst, int ldl) {
+                                         float* dst, int ldl, int fofs = 0) {
   if (cl.S == 1) {
     __syncthreads();
     return;
@@ -101,9 +101,17 @@ __device__ __forceinline__ void exchange(Cluster& cl, const float* src, int64_t 
   cl.phase++;
   __syncthreads();
   const __amdgpu_buffer_rsrc_t r = head_rsrc(src, (uint32_t)(4 * (int64_t)max(nvalid, 0) * ld));
-  const int c4 = ncols / 4;  // ncols % 4 == 0
-  for (int e = threadIdx.x; e < kR * c4; e += 64 * W) {
-    const int row = e / c4, c = 4 * (e - row * c4);
+  // Only the partners' 16-column fragments are loaded: this workgroup's own ones (fragment f + fofs
+  // of the producing GEMM belongs to member (f + fofs) % S) are already in dst, written by its
+  // epilogue. The j-th foreign fragment of a row is f = (j / (S-1)) * S + j % (S-1), skipping the
+  // own residue.
+  const int S = cl.S, nf = ncols / 16;  // ncols % 16 == 0
+  const int own = ((cl.rank - fofs) % S + S) % S;
+  const int nfor = nf - (nf / S + (own < nf % S ? 1 : 0));
+  for (int e = threadIdx.x; e < kR * nfor * 4; e += 64 * W) {
+    const int row = e / (nfor * 4), q = e - row * (nfor * 4), j = q >> 2;
+    const int jj = j % (S - 1), f = (j / (S - 1)) * S + jj + (jj >= own ? 1 : 0);
+    const int c = 16 * f + 4 * (q & 3);
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(4 * (row * ld + c)), 0, 16);  // sc1
     *reinterpret_cast<floatx4*>(dst + row * ldl + c) = __builtin_bit_cast(floatx4, v);
   }
@@ -489,7 +497,7 @@ __global__ __launch_bounds__(64 * W) void k_head_bwd(const AimxHead h, const Aim
       }
     });
     HEAD_STAMP(32 + st++);
-    exchange<W>(cl, d.ds + g0 * F, F, nvalid, F, DV, kS1);
+    exchange<W>(cl, d.ds + g0 * F, F, nvalid, F, DV, kS1, F / 16);  // ds = fragments F/16.. of [dz | ds]
     HEAD_STAMP(32 + st++);
     // dz += ds Ws (fragment f of this GEMM has the owner of fragment f of the one above: the
     // direct dz columns it adds are in this workgroup's LDS)
