@@ -24,6 +24,8 @@
 namespace aimx {
 namespace {
 
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
 constexpr int kAdamChunk = 80;        // tensors per launch (kernel-argument table, < 4 KiB: a
                                       // reference GNN's ~75 parameters take one launch each way)
 constexpr int kAdamThreads = 256;
@@ -82,8 +84,19 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, 
   const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
   const float* __restrict__ g = t.grad[i];
   double acc = 0.0;
+  int64_t j0 = s0;
+  if ((((uintptr_t)g) & 15) == 0) {  // 16-byte loads (same fp64 sums, per-thread order changes)
+    const int64_t q1 = s0 + ((s1 - s0) & ~(int64_t)3);
+#pragma unroll 2
+    for (int64_t j = s0 + 4 * threadIdx.x; j < q1; j += 4 * kAdamThreads) {
+      const floatx4 x = *reinterpret_cast<const floatx4*>(g + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += (double)x[e] * (double)x[e];
+    }
+    j0 = q1;
+  }
 #pragma unroll 8
-  for (int64_t j = s0 + threadIdx.x; j < s1; j += kAdamThreads) {
+  for (int64_t j = j0 + threadIdx.x; j < s1; j += kAdamThreads) {
     const double x = g[j];
     acc += x * x;
   }
@@ -122,18 +135,45 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t,
   float* __restrict__ g = t.grad[i];
   float* __restrict__ m = t.m[i];
   float* __restrict__ v = t.v[i];
-#pragma unroll 8
-  for (int64_t j = s0 + threadIdx.x; j < s1; j += kAdamThreads) {
-    float gj = g[j] * coef;
-    g[j] = gj;
-    const float pj = p[j];
+  auto upd = [&](float& gj_io, float& pj_io, float& mj_io, float& vj_io) {
+    float gj = gj_io * coef;
+    gj_io = gj;
+    const float pj = pj_io;
     if (wd != 0.f) gj += wd * pj;
-    const float mj = m[j] + omb1 * (gj - m[j]);       // exp_avg.lerp_(grad, 1 - beta1)
-    const float vj = beta2 * v[j] + omb2 * gj * gj;   // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-    m[j] = mj;
-    v[j] = vj;
-    p[j] = pj - step_size * (mj / (sqrtf(vj) / bc2s + eps));
+    const float mj = mj_io + omb1 * (gj - mj_io);     // exp_avg.lerp_(grad, 1 - beta1)
+    const float vj = beta2 * vj_io + omb2 * gj * gj;  // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+    mj_io = mj;
+    vj_io = vj;
+    pj_io = pj - step_size * (mj / (sqrtf(vj) / bc2s + eps));
+  };
+  // 16-byte accesses when all four tensors are 16-byte aligned (a dword access moves a quarter
+  // of the bytes per address cycle); the same per-element arithmetic, so results are unchanged
+  const bool vec = ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0;
+  int64_t j0 = s0;
+  if (vec) {
+    const int64_t q1 = s0 + ((s1 - s0) & ~(int64_t)3);
+#pragma unroll 2
+    for (int64_t j = s0 + 4 * threadIdx.x; j < q1; j += 4 * kAdamThreads) {
+      floatx4 gv = *reinterpret_cast<const floatx4*>(g + j), pv = *reinterpret_cast<const floatx4*>(p + j);
+      floatx4 mv = *reinterpret_cast<const floatx4*>(m + j), vv = *reinterpret_cast<const floatx4*>(v + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float ge = gv[e], pe = pv[e], me = mv[e], ve = vv[e];
+        upd(ge, pe, me, ve);
+        gv[e] = ge;
+        pv[e] = pe;
+        mv[e] = me;
+        vv[e] = ve;
+      }
+      *reinterpret_cast<floatx4*>(g + j) = gv;
+      *reinterpret_cast<floatx4*>(p + j) = pv;
+      *reinterpret_cast<floatx4*>(m + j) = mv;
+      *reinterpret_cast<floatx4*>(v + j) = vv;
+    }
+    j0 = q1;
   }
+#pragma unroll 8
+  for (int64_t j = j0 + threadIdx.x; j < s1; j += kAdamThreads) upd(g[j], p[j], m[j], v[j]);
 }
 
 int64_t blocks_of(int64_t numel) { return std::max<int64_t>(1, cdiv(numel, kSliceElems)); }

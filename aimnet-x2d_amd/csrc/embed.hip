@@ -35,6 +35,36 @@ __global__ void k_embed_gather(AimxEmbeddingTables t, int64_t N, float* __restri
   }
 }
 
+// 16-byte form of k_embed_gather (dim % 4 == 0, ldo % 4 == 0, 16-byte aligned out and tables,
+// N * width < 2^31): one float4 of one table row per thread, 32-bit index math (the int64
+// divisions of the generic form cost more than its loads).
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+__global__ void k_embed_gather4(AimxEmbeddingTables t, int32_t N, float* __restrict__ out, int32_t ldo) {
+  const int32_t q = t.dim >> 2, wq = t.n_tables * q, total = N * wq;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int32_t j = i / wq, k = i - j * wq, tb = k / q, c = 4 * (k - tb * q);
+    const int64_t r = t.index[tb][j];
+    const bool ok = r >= 0 && r < t.rows[tb];
+    const floatx4 v = *reinterpret_cast<const floatx4*>(t.table[tb] + (ok ? r : 0) * t.dim + c);
+    *reinterpret_cast<floatx4*>(out + (int64_t)j * ldo + tb * t.dim + c) = ok ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// 16-byte form of k_act_bwd (N, ldy, ldp, ldo % 4 == 0, aligned pointers, M * N < 2^31).
+__global__ void k_act_bwd4(int kind, const float* __restrict__ dy, int32_t ldy, const float* __restrict__ pre,
+                           int32_t ldp, int32_t M, int32_t N, float* __restrict__ out, int32_t ldo) {
+  const int32_t q = N >> 2, total = M * q;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int32_t m = i / q, n = 4 * (i - m * q);
+    const floatx4 d = *reinterpret_cast<const floatx4*>(dy + (int64_t)m * ldy + n);
+    const floatx4 p = *reinterpret_cast<const floatx4*>(pre + (int64_t)m * ldp + n);
+    floatx4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = d[e] * act_grad(kind, p[e]);
+    *reinterpret_cast<floatx4*>(out + (int64_t)m * ldo + n) = o;
+  }
+}
+
 // blockDim.x == n_tables * dim (<= 1024); dynamic LDS = total_rows * dim floats.
 __global__ void k_embed_bwd_partial(AimxEmbeddingTables t, int64_t N, int64_t chunk, const float* __restrict__ dE,
                                     int64_t ldd, float* __restrict__ partial, int64_t total_rows) {
@@ -146,8 +176,15 @@ extern "C" int aimx_embedding_gather(const AimxEmbeddingTables* t, int64_t N, fl
   if (!tables_ok(t) || N < 0 || !out) return AIMX_EARG;
   if (N == 0) return AIMX_OK;
   const int64_t total = N * t->n_tables * t->dim;
-  hipLaunchKernelGGL(k_embed_gather, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)), dim3(256), 0,
-                     (hipStream_t)s, *t, N, out, ldo);
+  bool v4 = t->dim % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 && total < (int64_t)INT32_MAX &&
+            N * ldo < (int64_t)INT32_MAX;
+  for (int i = 0; i < t->n_tables; ++i) v4 = v4 && ((uintptr_t)t->table[i] & 15) == 0;
+  if (v4)
+    hipLaunchKernelGGL(k_embed_gather4, dim3((unsigned)std::min<int64_t>(cdiv(total / 4, 256), 8192)), dim3(256), 0,
+                       (hipStream_t)s, *t, (int32_t)N, out, (int32_t)ldo);
+  else
+    hipLaunchKernelGGL(k_embed_gather, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)), dim3(256), 0,
+                       (hipStream_t)s, *t, N, out, ldo);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
@@ -191,8 +228,15 @@ extern "C" int aimx_act_backward(int32_t kind, const float* dy, int64_t ldy, con
                                  int64_t N, float* out, int64_t ldo, aimx_stream_t s) {
   if (M < 0 || N < 0) return AIMX_EARG;
   if (M == 0 || N == 0) return AIMX_OK;
-  hipLaunchKernelGGL(k_act_bwd, dim3((unsigned)std::min<int64_t>(cdiv(M * N, 256), 8192)), dim3(256), 0,
-                     (hipStream_t)s, (int)kind, dy, ldy, pre, ldp, M, N, out, ldo);
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (N % 4 == 0 && ldy % 4 == 0 && ldp % 4 == 0 && ldo % 4 == 0 && al(dy) && al(pre) && al(out) &&
+      M * std::max({ldy, ldp, ldo}) < (int64_t)INT32_MAX)
+    hipLaunchKernelGGL(k_act_bwd4, dim3((unsigned)std::min<int64_t>(cdiv(M * N / 4, 256), 8192)), dim3(256), 0,
+                       (hipStream_t)s, (int)kind, dy, (int32_t)ldy, pre, (int32_t)ldp, (int32_t)M, (int32_t)N, out,
+                       (int32_t)ldo);
+  else
+    hipLaunchKernelGGL(k_act_bwd, dim3((unsigned)std::min<int64_t>(cdiv(M * N, 256), 8192)), dim3(256), 0,
+                       (hipStream_t)s, (int)kind, dy, ldy, pre, ldp, M, N, out, ldo);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
