@@ -748,9 +748,17 @@ def _tables_struct(indices, tables, grads=None):
     return t
 
 
+def _act_backward_into(kind, dy, pre, out):
+    """out = dy * act'(pre) for 2-D views with unit column stride (any row strides)."""
+    lib = _lib.load()
+    dy, ldy = _rows(dy)
+    check(lib.aimx_act_backward(kind, ptr(dy), ldy, ptr(pre), pre.stride(0), pre.shape[0], pre.shape[1], ptr(out),
+                                out.stride(0), stream_ptr(pre.device)), "act_backward")
+
+
 class _EmbedProject(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, indices, act, W, b, *tables):
+    def forward(ctx, indices, act, split, W, b, *tables):
         import ctypes
         lib = _lib.load()
         dev = W.device
@@ -768,16 +776,32 @@ class _EmbedProject(torch.autograd.Function):
         gemm_linear_fwd(E, width, W.contiguous(), b.contiguous(), out, W.shape[0], act, pre, ctx.prec)
         ctx.act = act
         ctx.idx = idx
+        ctx.split = split
         ctx.save_for_backward(E, W, pre, *tables)
+        if split:  # [x_self | x_other] as two views (gnn.py:227-231): their gradients need no cat
+            return out[:, :split], out[:, split:]
         return out
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, *grads):
         import ctypes
         lib = _lib.load()
         E, W, pre, *tables = ctx.saved_tensors
-        dev = dy.device
-        dpre = act_backward(ctx.act, dy, pre) if ctx.act >= 0 else dy.contiguous()
+        dev = E.device
+        if ctx.split:
+            xs = ctx.split
+            n, width = E.shape[0], W.shape[0]
+            parts = [g if g is not None else torch.zeros(n, w, dtype=_F32, device=dev)
+                     for g, w in zip(grads, (xs, width - xs))]
+            if ctx.act >= 0:  # act' applied per part, straight into the two column ranges of dpre
+                dpre = torch.empty(n, width, dtype=_F32, device=dev)
+                _act_backward_into(ctx.act, parts[0], pre[:, :xs], dpre[:, :xs])
+                _act_backward_into(ctx.act, parts[1], pre[:, xs:], dpre[:, xs:])
+            else:
+                dpre = torch.cat(parts, dim=1)
+        else:
+            dy = grads[0]
+            dpre = act_backward(ctx.act, dy, pre) if ctx.act >= 0 else dy.contiguous()
         dE = torch.empty_like(E)
         dW = torch.empty_like(W)
         db = torch.empty(W.shape[0], dtype=_F32, device=dev)
@@ -788,14 +812,16 @@ class _EmbedProject(torch.autograd.Function):
         ws = torch.empty(wsb // 4 + 1, dtype=_F32, device=dev)
         check(lib.aimx_embedding_backward(ctypes.byref(ts), E.shape[0], ptr(dE), dE.shape[1], ptr(ws), wsb,
                                           stream_ptr(dev)), "embedding_backward")
-        return (None, None, dW, db, *grads)
+        return (None, None, None, dW, db, *grads)
 
 
-def embed_project(indices, tables, W, b, act=None):
-    """act(cat_t(table_t[indices_t]) W^T + b) — gather, GEMM and activation on the device."""
+def embed_project(indices, tables, W, b, act=None, split=None):
+    """act(cat_t(table_t[indices_t]) W^T + b) — gather, GEMM and activation on the device.
+    split=k: returns the column views (out[:, :k], out[:, k:]) (gnn.py:227-231's torch.split) whose
+    gradients the backward takes separately (no concatenation launch)."""
     _lib.require_device(W, *indices)
     kind = -1 if act is None else _lib.ACT_KIND[act]
-    return _EmbedProject.apply(list(indices), kind, W, b, *tables)
+    return _EmbedProject.apply(list(indices), kind, int(split) if split else 0, W, b, *tables)
 
 
 # ---------------------------------------------------------------------------------------------

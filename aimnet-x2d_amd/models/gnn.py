@@ -132,21 +132,23 @@ class GNN(nn.Module):
                       tetrahedral_indices, cis_indices, trans_indices):
         """gnn.py:197-260 eagerly: one HIP operator per reference stage."""
         # gnn.py:221-225: four lookups + cat + projection + activation, fused on the device
-        atom_embeddings = ops.embed_project(
+        # (the split of gnn.py:227-231 comes back as the two column views, so the backward needs no
+        # concatenation of their gradients)
+        x_self, x_other = ops.embed_project(
             [atom_features[k] for k in _FEATURE_KEYS],
             [self.atom_type_embedding.weight, self.hydrogen_count_embedding.weight, self.degree_embedding.weight,
              self.hybridization_embedding.weight],
-            self.embedding_projection.weight, self.embedding_projection.bias, act=activation_name(self.activation))
-        x_self, x_other = torch.split(atom_embeddings, [self.x_self_dim, self.x_other_dim], dim=-1)
+            self.embedding_projection.weight, self.embedding_projection.bias, act=activation_name(self.activation),
+            split=self.x_self_dim)
 
-        plan = GraphPlan(atom_embeddings.shape[0], self.num_shells, edges=multi_hop_edge_indices,
+        plan = GraphPlan(x_self.shape[0], self.num_shells, edges=multi_hop_edge_indices,
                          batch=batch_indices, num_graphs=total_charges.shape[0])
         # every dropout seed of this forward (message-passing stack + FFN blocks) from ONE draw
         blocks = list(self.ffn.layers)
         need = (self.message_passing_layers[0]._aimx_dropout()[0] if len(self.message_passing_layers) else False) or \
             any(b.dropout.training and b.dropout.p > 0 for b in blocks)
         if need:  # (MC-dropout may switch single Dropout modules on in eval mode: follow their flags)
-            seeds = ops.dropout_seeds(self, 1 + len(blocks), atom_embeddings.device)
+            seeds = ops.dropout_seeds(self, 1 + len(blocks), x_self.device)
             self._aimx_stack_seed = seeds[0:1]
             for i, blk in enumerate(blocks):
                 blk._aimx_seed = seeds[1 + i:2 + i]
