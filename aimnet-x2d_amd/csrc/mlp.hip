@@ -722,6 +722,9 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
   if (threadIdx.x < 2 * nm) wtab[threadIdx.x] = (threadIdx.x & 1) ? p.w1[threadIdx.x >> 1] : p.w2[threadIdx.x >> 1];
   for (int e = threadIdx.x; e < R * S; e += blockDim.x) DV[e] = 0.f;
   __syncthreads();
+  MLPW_STAMP(32);
+  int sb = 33;  // backward stamps: slots 32..62 (trace build only)
+  (void)sb;
   const int64_t N = p.N;
   const int64_t nchunk = (N + R - 1) / R;
   const float scale = drop_scale(p.drop_p);
@@ -751,6 +754,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
       if (single) pre_dv(nm - 1, r0, wave);
     }
     lds_sync();
+    MLPW_STAMP(sb++);
     for (int e = threadIdx.x; e < R * D; e += blockDim.x) {  // dg = dY (from the LDS copy)
       const int r = e / D, c = e - r * D;
       if (r0 + r < N) p.dug[(r0 + r) * 2 * p.D + p.D + c] = DA[r * S + c];
@@ -781,6 +785,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
         }
       }
       lds_sync();
+      MLPW_STAMP(sb++);
       float* dAk = k > 0 ? p.dA[k - 1] : nullptr;
       for (int it = wave; it < items; it += nw) {  // dA_k = dA_{k+1} + dV W1 ; k == 0: du = dA_0 act'(u)
         const int t = it / CF, f = it - t * CF;
@@ -808,6 +813,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
         }
       }
       lds_sync();
+      MLPW_STAMP(sb++);
     }
   }
 }
