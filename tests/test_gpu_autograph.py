@@ -162,3 +162,42 @@ def test_autograph_falls_back_and_guards():
         assert not autograph.wanted(m, b.model_args())  # module hooks would stop firing on replay
     finally:
         h.remove()
+
+
+@pytest.mark.parametrize("slack", [1, 7, 8, 9, 300])
+def test_pad_batch_matches_pad_collated(slack):
+    """aimx_pad_batch (one launch) builds exactly aimx.data.pad_collated's static layout: real rows
+    copied, slack atoms in 8 near-equal padding molecules, slack edges self-pairs over them."""
+    import ctypes
+    from aimx import _lib
+    from aimx.autograph import PAD_MOLS
+    from aimx.data import FEATURE_KEYS, pad_collated
+    from aimx._lib import check, ptr, stream_ptr
+    b = _batches(1, 61)[0]
+    N, E, G = b.num_atoms, b.edges.shape[0], b.num_graphs
+    Np, Ep = N + slack, E + 3 * slack + 5
+    col = {"feats": np.stack([b.atom_features[k].cpu().numpy() for k in FEATURE_KEYS], 1),
+           "edges": b.edges.cpu().numpy(), "batch": b.batch.cpu().numpy(), "n_atoms": np.zeros(G, np.int64)}
+    ref = pad_collated(col, Np, Ep, G, PAD_MOLS)
+    feat = torch.full((4, Np), -1, dtype=torch.int64, device=DEV)
+    edges = torch.full((Ep, 2), -1, dtype=torch.int64, device=DEV)
+    batch = torch.full((Np,), -1, dtype=torch.int64, device=DEV)
+    charges = torch.full((G + PAD_MOLS,), -1.0, device=DEV)
+    a = _lib.PadBatch()
+    for i, k in enumerate(FEATURE_KEYS):
+        a.feat[i], a.feat_stride[i] = b.atom_features[k].data_ptr(), b.atom_features[k].stride(0)
+    a.edges, a.edge_s0, a.edge_s1 = b.edges.data_ptr(), b.edges.stride(0), b.edges.stride(1)
+    a.batch, a.batch_stride = b.batch.data_ptr(), b.batch.stride(0)
+    a.charges, a.charge_stride = b.total_charges.data_ptr(), b.total_charges.stride(0)
+    a.N, a.E, a.G = N, E, G
+    a.out_feat, a.out_edges, a.out_batch, a.out_charges = ptr(feat), ptr(edges), ptr(batch), ptr(charges)
+    a.Np, a.Ep, a.pad_mols = Np, Ep, PAD_MOLS
+    check(_lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(DEV)), "pad_batch")
+    torch.cuda.synchronize()
+    assert np.array_equal(feat.cpu().numpy().T, ref["feats"])
+    assert np.array_equal(edges.cpu().numpy(), ref["edges"])
+    assert np.array_equal(batch.cpu().numpy(), ref["batch"])
+    q = charges.cpu().numpy()
+    assert np.array_equal(q[:G], b.total_charges.cpu().numpy()) and not q[G:].any()
+    a.Np = N  # no slack atom: rejected
+    assert _lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(DEV)) != 0
