@@ -491,7 +491,10 @@ __device__ __forceinline__ void fill_lds_v4(float* Wl, const float* const* wtab,
         const __amdgpu_buffer_rsrc_t rw = mlp_rsrc(wtab[m], wbytes);
 #pragma unroll
         for (int u = 0; u < kFillW4; ++u) {
-          const int g = e0 + u * NT + tid, a = g / kq, b4 = 4 * (g - a * kq);  // (row a, cols b4..b4+3) of W
+          // (row a, cols b4..b4+3) of W; TR walks a fastest, so a wave's 4 dword LDS writes per group
+          // land on consecutive image columns (conflict-free) instead of rows 4 apart (16-way)
+          const int g = e0 + u * NT + tid;
+          const int a = TR ? g % Kp : g / kq, b4 = TR ? 4 * (g / Kp) : 4 * (g - a * kq);
           const bool ok = g < per4 && a < D && b4 < D;
           v[mi][u] = ld4(rw, ok ? 4u * (uint32_t)(a * D + b4) : OOB);
         }
@@ -511,7 +514,7 @@ __device__ __forceinline__ void fill_lds_v4(float* Wl, const float* const* wtab,
         for (int u = 0; u < kFillW4; ++u) {
           const int g = e0 + u * NT + tid;
           if (g < per4) {
-            const int a = g / kq, b4 = 4 * (g - a * kq);
+            const int a = TR ? g % Kp : g / kq, b4 = TR ? 4 * (g / Kp) : 4 * (g - a * kq);
             if (TR) {
 #pragma unroll
               for (int j = 0; j < 4; ++j) img[(b4 + j) * S + a] = v[mi][u][j];
@@ -741,11 +744,13 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
       ag[i] = p.V[k][gc * D + cc];
     }
   };
-  if (single && (int64_t)blockIdx.x < nchunk) pre_dv(nm - 1, (int64_t)blockIdx.x * R, wave);
   if (p.v4)
     fill_lds_v4<true>(W, wtab, 2 * nm, D, Kp, S, DA, p.dy, p.lddy, (int64_t)blockIdx.x * R, R, N);
   else
     fill_lds<true>(W, wtab, 2 * nm, D, Kp, S, DA, p.dy, p.lddy, (int64_t)blockIdx.x * R, R, N);
+  // the first dV epilogue's operands, issued AFTER the fill: vmcnt retires in order, so loads issued
+  // before it would hold up the fill's LDS writes (these are only needed after the first GEMM)
+  if (single && (int64_t)blockIdx.x < nchunk) pre_dv(nm - 1, (int64_t)blockIdx.x * R, wave);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0 = ch * R;
     if (ch != (int64_t)blockIdx.x) {

@@ -192,7 +192,7 @@ def test_pad_batch_matches_pad_collated(slack):
     a.N, a.E, a.G = N, E, G
     a.out_feat, a.out_edges, a.out_batch, a.out_charges = ptr(feat), ptr(edges), ptr(batch), ptr(charges)
     a.Np, a.Ep, a.pad_mols = Np, Ep, PAD_MOLS
-    check(_lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(DEV)), "pad_batch")
+    check(_lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(b.edges.device)), "pad_batch")
     torch.cuda.synchronize()
     assert np.array_equal(feat.cpu().numpy().T, ref["feats"])
     assert np.array_equal(edges.cpu().numpy(), ref["edges"])
@@ -200,4 +200,4 @@ def test_pad_batch_matches_pad_collated(slack):
     q = charges.cpu().numpy()
     assert np.array_equal(q[:G], b.total_charges.cpu().numpy()) and not q[G:].any()
     a.Np = N  # no slack atom: rejected
-    assert _lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(DEV)) != 0
+    assert _lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(b.edges.device)) != 0
