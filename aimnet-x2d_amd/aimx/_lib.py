@@ -146,6 +146,7 @@ class EmbeddingTables(ctypes.Structure):
     _fields_ = [
         ("n_tables", c_i32), ("dim", c_i64),
         ("table", c_ptr * 8), ("index", c_ptr * 8), ("rows", c_i64 * 8), ("grad", c_ptr * 8),
+        ("seed_state", c_ptr), ("seeds", c_ptr), ("n_seeds", c_i32),
     ]
 
 

@@ -326,16 +326,27 @@ def stereo_features(x, tet, cis, trans):
     return _Stereo.apply(x, tet, cis, trans)
 
 
-def dropout_seeds(owner, n, device):
-    """n int64 dropout seeds for one forward, drawn on the device from a counter kept on `owner`
-    (aimx_dropout_seeds; one launch, graph-safe). The counter starts from torch's generator."""
+def _seed_state(owner, device):
     st = getattr(owner, "_aimx_seed_state", None)
     if st is None or st.device != device:
         st = torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
         owner._aimx_seed_state = st
+    return st
+
+
+def dropout_seeds(owner, n, device):
+    """n int64 dropout seeds for one forward, drawn on the device from a counter kept on `owner`
+    (aimx_dropout_seeds; one launch, graph-safe). The counter starts from torch's generator."""
+    st = _seed_state(owner, device)
     seeds = torch.empty(n, dtype=torch.int64, device=device)
     check(_lib.load().aimx_dropout_seeds(ptr(st), ptr(seeds), int(n), stream_ptr(device)), "dropout_seeds")
     return seeds
+
+
+def dropout_seed_slots(owner, n, device):
+    """(counter, seeds) for embed_project(..., seeds=...): the same draw as dropout_seeds, done by
+    the embedding gather's launch instead of a launch of its own."""
+    return _seed_state(owner, device), torch.empty(n, dtype=torch.int64, device=device)
 
 
 def _ct_addr(arr):
@@ -758,7 +769,7 @@ def _act_backward_into(kind, dy, pre, out):
 
 class _EmbedProject(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, indices, act, split, W, b, *tables):
+    def forward(ctx, indices, act, split, seeds, W, b, *tables):
         import ctypes
         lib = _lib.load()
         dev = W.device
@@ -769,6 +780,8 @@ class _EmbedProject(torch.autograd.Function):
         width = len(tables) * tables[0].shape[1]
         E = torch.empty(n, width, dtype=_F32, device=dev)
         ts = _tables_struct(idx, tables)
+        if seeds is not None:  # the forward's dropout seeds ride in the gather launch
+            ts.seed_state, ts.seeds, ts.n_seeds = ptr(seeds[0]), ptr(seeds[1]), seeds[1].numel()
         check(lib.aimx_embedding_gather(ctypes.byref(ts), n, ptr(E), width, stream_ptr(dev)), "embedding_gather")
         out = torch.empty(n, W.shape[0], dtype=_F32, device=dev)
         pre = torch.empty_like(out) if act >= 0 else None
@@ -812,16 +825,17 @@ class _EmbedProject(torch.autograd.Function):
         ws = torch.empty(wsb // 4 + 1, dtype=_F32, device=dev)
         check(lib.aimx_embedding_backward(ctypes.byref(ts), E.shape[0], ptr(dE), dE.shape[1], ptr(ws), wsb,
                                           stream_ptr(dev)), "embedding_backward")
-        return (None, None, None, dW, db, *grads)
+        return (None, None, None, None, dW, db, *grads)
 
 
-def embed_project(indices, tables, W, b, act=None, split=None):
+def embed_project(indices, tables, W, b, act=None, split=None, seeds=None):
     """act(cat_t(table_t[indices_t]) W^T + b) — gather, GEMM and activation on the device.
     split=k: returns the column views (out[:, :k], out[:, k:]) (gnn.py:227-231's torch.split) whose
-    gradients the backward takes separately (no concatenation launch)."""
+    gradients the backward takes separately (no concatenation launch). seeds=(counter, out) from
+    dropout_seed_slots: the gather launch also draws the forward's dropout seeds into out."""
     _lib.require_device(W, *indices)
     kind = -1 if act is None else _lib.ACT_KIND[act]
-    return _EmbedProject.apply(list(indices), kind, int(split) if split else 0, W, b, *tables)
+    return _EmbedProject.apply(list(indices), kind, int(split) if split else 0, seeds, W, b, *tables)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -62,6 +62,21 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, uint32_t salt, uint
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
 
+// The n dropout seeds of one forward from the device counter at state (one thread): splitmix64 of
+// the counter, in [0, 2^62) like torch.randint(0, 2**62); the counter advances by n + 1 golden
+// steps (aimx_dropout_seeds, and the embedding gather's optional seed draw).
+__device__ __forceinline__ void draw_dropout_seeds(int64_t* state, int64_t* seeds, int32_t n) {
+  const uint64_t s = (uint64_t)state[0];
+  for (int32_t i = 0; i < n; ++i) {
+    uint64_t z = s + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    seeds[i] = (int64_t)(z >> 2);
+  }
+  state[0] = (int64_t)(s + 0x9E3779B97F4A7C15ull * (uint64_t)(n + 1));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -53,15 +53,7 @@ int64_t slices(int64_t n) { return std::max<int64_t>(1, cdiv(n, kSlice)); }
 // Dropout seeds of one forward from a device-resident counter (aimx_dropout_seeds).
 __global__ void k_dropout_seeds(int64_t* __restrict__ state, int64_t* __restrict__ seeds, int32_t n) {
   if (threadIdx.x != 0) return;
-  const uint64_t s = (uint64_t)state[0];
-  for (int32_t i = 0; i < n; ++i) {
-    uint64_t z = s + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    seeds[i] = (int64_t)(z >> 2);  // [0, 2^62), the range torch.randint(0, 2**62) drew
-  }
-  state[0] = (int64_t)(s + 0x9E3779B97F4A7C15ull * (uint64_t)(n + 1));
+  draw_dropout_seeds(state, seeds, n);
 }
 
 // Static padded inputs of one autograph bucket (aimx_pad_batch): real rows copied, slack atoms

@@ -24,6 +24,7 @@ constexpr int kUnroll = 8;   // atoms whose index + gradient loads are in flight
 constexpr int kReduceCols = 64, kReduceWaves = 4;
 
 __global__ void k_embed_gather(AimxEmbeddingTables t, int64_t N, float* __restrict__ out, int64_t ldo) {
+  if (t.n_seeds > 0 && blockIdx.x == 0 && threadIdx.x == 0) draw_dropout_seeds(t.seed_state, t.seeds, t.n_seeds);
   const int64_t width = (int64_t)t.n_tables * t.dim;
   const int64_t total = N * width;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -40,6 +41,7 @@ __global__ void k_embed_gather(AimxEmbeddingTables t, int64_t N, float* __restri
 // divisions of the generic form cost more than its loads).
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 __global__ void k_embed_gather4(AimxEmbeddingTables t, int32_t N, float* __restrict__ out, int32_t ldo) {
+  if (t.n_seeds > 0 && blockIdx.x == 0 && threadIdx.x == 0) draw_dropout_seeds(t.seed_state, t.seeds, t.n_seeds);
   const int32_t q = t.dim >> 2, wq = t.n_tables * q, total = N * wq;
   for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int32_t j = i / wq, k = i - j * wq, tb = k / q, c = 4 * (k - tb * q);
@@ -173,17 +175,18 @@ using namespace aimx;
 
 extern "C" int aimx_embedding_gather(const AimxEmbeddingTables* t, int64_t N, float* out, int64_t ldo,
                                      aimx_stream_t s) {
-  if (!tables_ok(t) || N < 0 || !out) return AIMX_EARG;
-  if (N == 0) return AIMX_OK;
+  if (!tables_ok(t) || N < 0 || !out || (t->n_seeds > 0 && (!t->seed_state || !t->seeds)) || t->n_seeds < 0)
+    return AIMX_EARG;
+  if (N == 0 && t->n_seeds == 0) return AIMX_OK;
   const int64_t total = N * t->n_tables * t->dim;
   bool v4 = t->dim % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 && total < (int64_t)INT32_MAX &&
             N * ldo < (int64_t)INT32_MAX;
   for (int i = 0; i < t->n_tables; ++i) v4 = v4 && ((uintptr_t)t->table[i] & 15) == 0;
   if (v4)
-    hipLaunchKernelGGL(k_embed_gather4, dim3((unsigned)std::min<int64_t>(cdiv(total / 4, 256), 8192)), dim3(256), 0,
+    hipLaunchKernelGGL(k_embed_gather4, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(total / 4, 256), 8192))), dim3(256), 0,
                        (hipStream_t)s, *t, (int32_t)N, out, (int32_t)ldo);
   else
-    hipLaunchKernelGGL(k_embed_gather, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)), dim3(256), 0,
+    hipLaunchKernelGGL(k_embed_gather, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(total, 256), 8192))), dim3(256), 0,
                        (hipStream_t)s, *t, N, out, ldo);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;

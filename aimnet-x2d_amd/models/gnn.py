@@ -131,6 +131,12 @@ class GNN(nn.Module):
     def _aimx_forward(self, atom_features, multi_hop_edge_indices, batch_indices, total_charges,
                       tetrahedral_indices, cis_indices, trans_indices):
         """gnn.py:197-260 eagerly: one HIP operator per reference stage."""
+        # every dropout seed of this forward (message-passing stack + FFN blocks) from ONE draw, made
+        # by the embedding gather's launch
+        blocks = list(self.ffn.layers)
+        need = (self.message_passing_layers[0]._aimx_dropout()[0] if len(self.message_passing_layers) else False) or \
+            any(b.dropout.training and b.dropout.p > 0 for b in blocks)
+        slots = ops.dropout_seed_slots(self, 1 + len(blocks), multi_hop_edge_indices.device) if need else None
         # gnn.py:221-225: four lookups + cat + projection + activation, fused on the device
         # (the split of gnn.py:227-231 comes back as the two column views, so the backward needs no
         # concatenation of their gradients)
@@ -139,16 +145,12 @@ class GNN(nn.Module):
             [self.atom_type_embedding.weight, self.hydrogen_count_embedding.weight, self.degree_embedding.weight,
              self.hybridization_embedding.weight],
             self.embedding_projection.weight, self.embedding_projection.bias, act=activation_name(self.activation),
-            split=self.x_self_dim)
+            split=self.x_self_dim, seeds=slots)
 
         plan = GraphPlan(x_self.shape[0], self.num_shells, edges=multi_hop_edge_indices,
                          batch=batch_indices, num_graphs=total_charges.shape[0])
-        # every dropout seed of this forward (message-passing stack + FFN blocks) from ONE draw
-        blocks = list(self.ffn.layers)
-        need = (self.message_passing_layers[0]._aimx_dropout()[0] if len(self.message_passing_layers) else False) or \
-            any(b.dropout.training and b.dropout.p > 0 for b in blocks)
         if need:  # (MC-dropout may switch single Dropout modules on in eval mode: follow their flags)
-            seeds = ops.dropout_seeds(self, 1 + len(blocks), x_self.device)
+            seeds = slots[1]
             self._aimx_stack_seed = seeds[0:1]
             for i, blk in enumerate(blocks):
                 blk._aimx_seed = seeds[1 + i:2 + i]

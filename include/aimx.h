@@ -292,6 +292,12 @@ typedef struct AimxEmbeddingTables {
   const int64_t* index[AIMX_MAX_TABLES];
   int64_t rows[AIMX_MAX_TABLES];
   float* grad[AIMX_MAX_TABLES];
+  /* optional (n_seeds > 0, gather only): the gather launch also draws the forward's n_seeds
+   * dropout seeds from the counter at seed_state, exactly as aimx_dropout_seeds would (one launch
+   * fewer per step) */
+  int64_t* seed_state;
+  int64_t* seeds;
+  int32_t n_seeds;
 } AimxEmbeddingTables;
 
 int aimx_embedding_gather(const AimxEmbeddingTables* t, int64_t N, float* out, int64_t ldo,
