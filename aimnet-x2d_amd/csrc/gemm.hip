@@ -881,6 +881,7 @@ struct WbTable {
   uint32_t a_bytes[kWgMaxProb], b_bytes[kWgMaxProb];
   int64_t ws_off[kWgMaxProb], cnt_off[kWgMaxProb];
   AimxWgradProblem p[kWgMaxProb];
+  int32_t xcd;  // XCD-aware work order (AIMX_WGRAD_XCD=0: launch order, for A/B)
 };
 
 __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
@@ -890,7 +891,17 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
   int q = 0;
   while (q + 1 < t.n && t.blk0[q + 1] <= (int)blockIdx.x) ++q;
   const int nb = t.nblk[q];
-  const int local = blockIdx.x - t.blk0[q];
+  int local = blockIdx.x - t.blk0[q];
+  // XCD-aware work order: blocks b and b + 8 share an XCD (and its L2). The problem's work items
+  // (split-major, output blocks fastest) are dealt in 8 contiguous runs, one per XCD, so the nb
+  // blocks that read the same K slice of dY and X run on one XCD and share its L2 instead of
+  // fetching the slice once per XCD. Only the first floor(items/8)*8 items move. Speed only.
+  // Measured (profiles/r02_wgrad_xcd_ab.txt): c2 -12 us, c4 -30 us per step; with c5's 64 blocks
+  // per K slice it was 35 us slower, so problems with more than 32 blocks keep the launch order.
+  if (t.xcd && nb <= 32) {
+    const int items = nb * t.splits[q], i8 = items & ~7;
+    if (local < i8) local = (local & 7) * (i8 >> 3) + (local >> 3);
+  }
   const int z = local / nb, blk = local - z * nb;
   const AimxWgradProblem& pr = t.p[q];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1383,6 +1394,10 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   auto flush = [&](bool lds) {
     if (lds) {
       tb.blk0[tb.n] = blkb;
+      {
+        const char* e = getenv("AIMX_WGRAD_XCD");  // =0: launch order (A/B experiments only)
+        tb.xcd = (e && atoi(e) == 0) ? 0 : 1;
+      }
       if (blkb > 0)
         hipLaunchKernelGGL(k_wgrad_lds, dim3((unsigned)blkb), dim3(kWbT), 0, (hipStream_t)stream, tb, (float*)workspace,
                            counters);
