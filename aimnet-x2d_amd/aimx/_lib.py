@@ -45,7 +45,8 @@ class Stereo(ctypes.Structure):
 class LossAccum(ctypes.Structure):
     """AimxLossAccum (include/aimx.h): the train step's device-side loss / NaN / step bookkeeping."""
     _fields_ = [("loss_sum", ctypes.c_void_p), ("nan_count", ctypes.c_void_p), ("steps", ctypes.c_void_p),
-                ("scale", ctypes.c_float)]
+                ("scale", ctypes.c_float), ("d_loss", ctypes.c_void_p), ("d_pred", ctypes.c_void_p),
+                ("ldd", ctypes.c_int64), ("rows_total", ctypes.c_int64)]
 
 
 class PadBatch(ctypes.Structure):

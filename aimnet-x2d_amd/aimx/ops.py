@@ -959,7 +959,7 @@ def linear_block(x, W1, b1, W2, b2, act, drop_p=0.0, training=False, skip=False,
 # ---------------------------------------------------------------------------------------------
 class _L1Loss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, target, weights, per_sample, rows, accum):
+    def forward(ctx, pred, target, weights, per_sample, rows, accum, grad_of):
         import ctypes
         lib = _lib.load()
         p, ldp = _rows(pred.reshape(pred.shape[0], -1) if pred.dim() != 2 else pred)
@@ -969,9 +969,14 @@ class _L1Loss(torch.autograd.Function):
         w = weights.contiguous().float() if weights is not None else None
         loss = torch.empty((), dtype=_F32, device=pred.device)
         acc = None
+        ctx.pre = None
         if accum is not None:
             loss_sum, nan_count, steps, scale = accum
             acc = _lib.LossAccum(ptr(loss_sum), ptr(nan_count), ptr(steps), float(scale))
+            if grad_of is not None:  # the backward's d_pred for that upstream gradient, in this launch
+                dp = torch.empty(total, cols, dtype=_F32, device=pred.device)
+                acc.d_loss, acc.d_pred, acc.ldd, acc.rows_total = ptr(grad_of), ptr(dp), cols, total
+                ctx.pre = (dp, grad_of.data_ptr(), grad_of._version)
         check(lib.aimx_l1_loss_forward_accum(ptr(p), ldp, ptr(t), ldt, rows, cols, ptr(w), int(per_sample), ptr(loss),
                                              ctypes.byref(acc) if acc is not None else None,
                                              stream_ptr(pred.device)), "l1_loss_forward")
@@ -984,15 +989,19 @@ class _L1Loss(torch.autograd.Function):
         lib = _lib.load()
         p, t, w = ctx.saved_tensors
         ldp, ldt, per_sample, shape, rows = ctx.meta
+        if ctx.pre is not None:
+            dp, gptr, gver = ctx.pre
+            if g.data_ptr() == gptr and g._version == gver and g.numel() == 1:
+                return dp.view(shape), None, None, None, None, None, None  # written by the forward launch
         total, cols = p.shape
         g = g.contiguous()
         dp = torch.empty(total, cols, dtype=_F32, device=p.device)
         check(lib.aimx_l1_loss_backward_padded(ptr(p), ldp, ptr(t), ldt, rows, total, cols, ptr(w), per_sample, ptr(g),
                                                ptr(dp), cols, stream_ptr(p.device)), "l1_loss_backward")
-        return dp.view(shape), None, None, None, None, None
+        return dp.view(shape), None, None, None, None, None, None
 
 
-def l1_loss(pred, target, weights=None, per_sample=False, rows=None, accum=None):
+def l1_loss(pred, target, weights=None, per_sample=False, rows=None, accum=None, grad_of=None):
     """mean |pred - target| (per_sample=False, weights None: nn.L1Loss) or
     mean over samples of sum_t w_t |pred - target| (per_sample=True: WeightedL1Loss).
     rows=B: the loss of pred[:B] against target (B rows), with pred's remaining rows (the padding
@@ -1000,7 +1009,12 @@ def l1_loss(pred, target, weights=None, per_sample=False, rows=None, accum=None)
     l1_loss(pred[:B], target) without autograd's slice-backward zero fill and copy.
     accum=(loss_sum f32[], nan_count i32[], steps i64[], scale): the train step's device-side
     bookkeeping in the same launch (loss_sum += loss * scale, nan_count += any(isnan(pred[:rows])),
-    steps += 1; aimx_l1_loss_forward_accum)."""
+    steps += 1; aimx_l1_loss_forward_accum).
+    grad_of (with accum): the f32 scalar tensor the caller will pass to backward(); the forward
+    launch then also writes the backward's gradient, and a backward with that same, unmodified
+    tensor needs no launch (any other gradient runs the backward kernel as usual)."""
+    if grad_of is not None and (accum is None or grad_of.dtype != _F32 or grad_of.numel() != 1):
+        raise _lib.AimxError("aimx.l1_loss: grad_of is an f32 scalar tensor and needs accum")
     if accum is not None:
         ls, nc, st, _ = accum
         if ls.dtype != _F32 or nc.dtype != torch.int32 or st.dtype != torch.int64 or \
@@ -1014,7 +1028,7 @@ def l1_loss(pred, target, weights=None, per_sample=False, rows=None, accum=None)
             raise _lib.AimxError("aimx.l1_loss: pred and target must have one shape")
     elif not (0 <= rows <= pred.shape[0] and target.shape[0] == rows and target.shape[1:] == pred.shape[1:]):
         raise _lib.AimxError("aimx.l1_loss: rows must be <= pred rows and equal target rows")
-    return _L1Loss.apply(pred, target, weights, bool(per_sample), rows, accum)
+    return _L1Loss.apply(pred, target, weights, bool(per_sample), rows, accum, grad_of)
 
 
 # ---------------------------------------------------------------------------------------------

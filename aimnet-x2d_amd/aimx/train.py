@@ -81,7 +81,7 @@ class GraphedTrainStep:
                 # fused L1: the padding rows' zero gradient in the loss's backward launch, and the
                 # step's loss sum / NaN flag / step count in its forward launch
                 loss = padded(out, self.static.targets[:B], B,
-                              accum=(self.loss_sum, self.nan_count, self.steps, float(B)))
+                              accum=(self.loss_sum, self.nan_count, self.steps, float(B)), grad_of=one)
             else:
                 loss = criterion(out[:B], self.static.targets[:B])
             loss.backward(one)  # d loss = 1 from a resident tensor (no per-step fill launch)

@@ -47,6 +47,20 @@ __global__ __launch_bounds__(256) void k_l1_fwd(const float* __restrict__ p, int
       acc.steps[0] += 1;
     }
   }
+  if (acc.d_pred) {  // the backward's d_pred for the promised upstream gradient (k_l1_bwd's formula)
+    const float g = acc.d_loss[0] * inv_div;
+    const int64_t nt = acc.rows_total * cols;
+    for (int64_t e = threadIdx.x; e < nt; e += 256) {
+      const int64_t i = e / cols, t = e - i * cols;
+      float v = 0.f;
+      if (i < rows) {
+        const float d = p[i * ldp + t] - y[i * ldy + t];
+        const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        v = sg * (w ? w[t] : 1.f) * g;
+      }
+      acc.d_pred[i * acc.ldd + t] = v;
+    }
+  }
 }
 
 __global__ void k_l1_bwd(const float* __restrict__ p, int64_t ldp, const float* __restrict__ y, int64_t ldy,
@@ -79,6 +93,7 @@ extern "C" int aimx_l1_loss_forward_accum(const float* pred, int64_t ldp, const 
   AimxLossAccum acc{};
   if (accum) {
     if (!accum->loss_sum || !accum->nan_count || !accum->steps) return AIMX_EARG;
+    if (accum->d_pred && (!accum->d_loss || accum->ldd < cols || accum->rows_total < rows)) return AIMX_EARG;
     acc = *accum;
   }
   const double div = per_sample ? (double)rows : (double)rows * (double)cols;

@@ -18,10 +18,11 @@ class L1Loss(nn.Module):
     def forward(self, y_pred: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:
         return ops.l1_loss(y_pred, y_true)
 
-    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int, accum=None) -> torch.Tensor:
+    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int, accum=None, grad_of=None) -> torch.Tensor:
         """forward(y_pred[:rows], y_true) for a static padded batch, the padding rows' zero gradient
-        written by the same backward launch (no slice-backward fill + copy); accum: ops.l1_loss."""
-        return ops.l1_loss(y_pred, y_true, rows=rows, accum=accum)
+        written by the same backward launch (no slice-backward fill + copy); accum, grad_of:
+        ops.l1_loss."""
+        return ops.l1_loss(y_pred, y_true, rows=rows, accum=accum, grad_of=grad_of)
 
 
 class WeightedL1Loss(nn.Module):
@@ -34,5 +35,6 @@ class WeightedL1Loss(nn.Module):
     def forward(self, y_pred: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:
         return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True)
 
-    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int, accum=None) -> torch.Tensor:
-        return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True, rows=rows, accum=accum)
+    def padded(self, y_pred: torch.Tensor, y_true: torch.Tensor, rows: int, accum=None, grad_of=None) -> torch.Tensor:
+        return ops.l1_loss(y_pred, y_true, self.weights.to(y_pred.device), per_sample=True, rows=rows, accum=accum,
+                           grad_of=grad_of)

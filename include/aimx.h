@@ -442,12 +442,20 @@ int aimx_l1_loss_forward(const float* pred, int64_t ldp, const float* target, in
  * `torch.isnan(outputs).any()` and `loss.item() * batch_size`, kept on the device so the loop never
  * synchronises), in the loss's own launch:
  *   *loss_sum += loss * scale (fp32 multiply, then fp32 add), *nan_count += any(isnan(pred[:rows])),
- *   *steps += 1.  accum NULL: aimx_l1_loss_forward. */
+ *   *steps += 1.  accum NULL: aimx_l1_loss_forward.
+ * d_pred non-NULL: the same launch also writes the backward's d_pred (ld ldd, rows_total rows:
+ * rows >= `rows` get 0) for the upstream gradient *d_loss, exactly as
+ * aimx_l1_loss_backward_padded would — for a caller that will run the backward with that very
+ * d_loss tensor (the captured train step's resident 1), so the backward needs no launch. */
 typedef struct AimxLossAccum {
   float* loss_sum;
   int32_t* nan_count;
   int64_t* steps;
   float scale;
+  const float* d_loss;
+  float* d_pred;
+  int64_t ldd;
+  int64_t rows_total;
 } AimxLossAccum;
 int aimx_l1_loss_forward_accum(const float* pred, int64_t ldp, const float* target, int64_t ldt, int64_t rows,
                                int64_t cols, const float* weights, int32_t per_sample, float* loss,

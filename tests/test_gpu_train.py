@@ -125,3 +125,27 @@ def test_full_train_step_matches_oracle():
                 tol_big = (1e-3 if step == 0 else 1e-2) * lr
                 assert (d[big] <= tol_big + 1e-6 * ref[big].abs()).all(), (step, k, d[big].max().item())
         assert flips <= 1e-3 * total, (step, flips, total)
+
+
+def test_l1_loss_gradient_in_forward_launch():
+    """l1_loss(..., accum, grad_of=one): the forward launch writes the backward's gradient; a
+    backward with that same tensor returns it (no launch) and equals the backward kernel's result;
+    any other upstream gradient still runs the kernel."""
+    from aimx import ops
+    g = torch.Generator().manual_seed(5)
+    pred = torch.randn(40, 3, generator=g).to(DEV)
+    y = torch.randn(32, 3, generator=g).to(DEV)
+    w = torch.rand(3, generator=g).to(DEV)
+    for weights, per_sample in ((None, False), (w, True)):
+        acc = lambda: (torch.zeros((), device=DEV), torch.zeros((), dtype=torch.int32, device=DEV),  # noqa: E731
+                       torch.zeros((), dtype=torch.int64, device=DEV), 32.0)
+        one = torch.ones((), device=DEV)
+        p1 = pred.clone().requires_grad_()
+        ops.l1_loss(p1, y, weights, per_sample, rows=32, accum=acc()).backward(one)
+        p2 = pred.clone().requires_grad_()
+        ops.l1_loss(p2, y, weights, per_sample, rows=32, accum=acc(), grad_of=one).backward(one)
+        assert torch.equal(p1.grad, p2.grad) and not p2.grad[32:].any()
+        p3 = pred.clone().requires_grad_()
+        half = torch.full((), 0.5, device=DEV)
+        ops.l1_loss(p3, y, weights, per_sample, rows=32, accum=acc(), grad_of=one).backward(half)
+        assert torch.equal(p3.grad, 0.5 * p1.grad)
