@@ -852,6 +852,7 @@ int mlpw_rt(int64_t N, int64_t D, int64_t nm) {
   const int CF = pad16((int)D) / 16;
   const int64_t tiles = (N + 15) / 16;
   int rt = (int)std::min<int64_t>(4, std::max<int64_t>(1, (tiles + g_num_cus() - 1) / g_num_cus()));
+  if (const char* e = getenv("AIMX_MLPW_RT")) rt = std::max(1, std::min(4, atoi(e)));  // A/B experiments only
   while (rt > 1 && (rt * CF > 2 * kWMaxWaves || mlpw_lds_bytes(D, nm, rt) > (size_t)kMlpwDynLds)) --rt;
   return rt;
 }
