@@ -531,7 +531,10 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   const int threads = 256;
   // tile height: ~2 vector units per thread, then shorter tiles while the grid is under 4
   // workgroups per CU (small batches are latency-bound: more workgroups hide more latency)
-  const int64_t tile_units = env_i64("AIMX_HOP_TILE_UNITS", 2 * threads);
+  // (rows of 129..256 vector units, c4's D = 153: two units per thread left 3-row tiles; 4 per
+  // thread measured 20 us faster per c4 step, neutral at c2 and slower at c5's 307-wide rows —
+  // profiles/r02_hop_tile_ab.txt; results never depend on the tiling)
+  const int64_t tile_units = env_i64("AIMX_HOP_TILE_UNITS", (upr_i > 128 && upr_i <= 256) ? 4 * threads : 2 * threads);
   int64_t tr = std::min<int64_t>(kMaxTileRows, std::max<int64_t>(1, tile_units / upr_i));
   while (tr > 1 && cdiv(rows, tr) < 1024) tr = std::max<int64_t>(1, tr / 2);
   // output rows past the first chunk (hop chunks >= 1; out_rpc = rows per chunk) go in big tiles
