@@ -1117,14 +1117,18 @@ Plan plan_gemm(const AimxGemmArgs& a) {
       p.bn = c[1];
     }
   }
-  // Small products (M·N·K < 1.5e9: c1–c3's projections, M ≈ 9 k rows, N, K ≤ 304) take 32 x 32
+  // Small products (M·N·K < 7.5e8, K < 1024: c1–c3's projections, M ≈ 9 k rows, N, K ≤ 304; c4's
+  // node-update GEMMs and head) take 32 x 32
   // tiles: ~2300 workgroups instead of ~580 hide the latency of their fused epilogues (bias,
   // activation, pre-activation / mask stores, residuals) — measured in the c2 step every such GEMM
   // is 10-20 % faster and the step 0.848 -> 0.809 ms, c3 1.033 -> 0.992 ms, although the bare
   // GEMMs (tools/gemm_micro.py, no epilogue operands) run faster on 64 x 64; c4/c5's larger
   // products keep the rule above (32 x 32 there: c4 3.48 -> 3.53, c5 5.23 -> 5.42 ms;
   // profiles/r02_gemm_tile_ab.txt).
-  if (a.M * a.N * a.K < (int64_t)1500000000) p.bm = p.bn = 32;
+  // (bounded at 7.5e8 and K < 1024: c5's 10.4 k x 307 x 307 node-update GEMMs run faster on
+  // 64 x 64, and K >= 1024 products (c5's head GEMMs) on 64 x 64 with split K — per-GEMM step
+  // traces in profiles/r02_gemm_tile_ab.txt)
+  if (a.M * a.N * a.K < (int64_t)750000000 && a.K < 1024) p.bm = p.bn = 32;
   if (const char* f = getenv("AIMX_GEMM_TILE")) {  // A/B experiments only: "64x64", "64x32", "32x32"
     const int fm = atoi(f), fn = atoi(strchr(f, 'x') ? strchr(f, 'x') + 1 : f);
     if ((fm == 64 && (fn == 64 || fn == 32)) || (fm == 32 && fn == 32)) {
