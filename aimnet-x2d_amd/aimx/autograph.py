@@ -23,8 +23,9 @@ tensors). The eager path
 is used instead when a graph cannot reproduce eager semantics: grad disabled or eval mode,
 stereochemistry inputs, a batch without edges, stream capture already active (GraphedTrainStep),
 gradient hooks on the parameters or an initialised multi-rank process group (DDP's reducer hooks
-the gradient accumulators, which a replay bypasses), or parameters replaced since the capture
-(re-captured). The attention weights and partial charges come back as detached copies.
+the gradient accumulators, which a replay bypasses). Parameters replaced since the capture (new
+Parameter objects or moved storage) re-capture the bucket, and the autocast state is part of the
+bucket key (a capture bakes in the GEMMs' bf16 or fp32 operands). The attention weights and partial charges come back as detached copies.
 """
 import ctypes
 import os
@@ -99,6 +100,18 @@ def _round_up(x, q):
     return (x + q - 1) // q * q
 
 
+def _param_key(model):
+    """Identity and storage of the model's live parameters: a replaced Parameter object
+    (load_state_dict(assign=True), a swapped submodule) or moved storage re-captures the bucket."""
+    return tuple((id(p), p.data_ptr()) for p in model.parameters())
+
+
+def _amp_key():
+    """The autocast state a capture bakes in (the GEMMs pick bf16 or fp32 operands at capture)."""
+    on = torch.is_autocast_enabled("cuda")
+    return (on, torch.get_autocast_dtype("cuda") if on else None)
+
+
 class _Bucket:
     """Static padded inputs, the captured forward / backward graphs and their static outputs."""
 
@@ -117,7 +130,7 @@ class _Bucket:
         a.Np, a.Ep, a.pad_mols = Np, Ep, PAD_MOLS
         self.pad = a
         self.params = [p for p in model.parameters()]
-        self.param_key = tuple(p.data_ptr() for p in self.params)
+        self.param_key = _param_key(model)
         self.gen = 0        # forward replays so far
         self.done = -1      # generation whose backward has run
 
@@ -206,19 +219,19 @@ class _Replay(torch.autograd.Function):
         return None, None, None
 
 
-def _pick(st, N, E, G, dev):
-    """The smallest live bucket that holds this batch (same molecule count, room for one slack atom
-    and every edge), else a new one sized with ~6 % headroom so the batches of an epoch settle on
-    one or two buckets."""
+def _pick(st, N, E, G, dev, amp):
+    """The smallest live bucket that holds this batch (same molecule count and autocast state, room
+    for one slack atom and every edge), else a new one sized with ~6 % headroom so the batches of an
+    epoch settle on one or two buckets."""
     best = None
     for key, b in st.buckets.items():
-        if key[2] == G and key[3] == dev.index and key[0] > N and key[1] >= E and \
+        if key[2] == G and key[3] == dev.index and key[4] == amp and key[0] > N and key[1] >= E and \
                 (best is None or key[0] + key[1] < best[0] + best[1]):
             best = key
     if best is not None:
         return best, False
     return (_round_up(int(1.06 * (N + 1)) + 1, ATOM_QUANTUM), _round_up(int(1.06 * E) + 1, EDGE_QUANTUM), G,
-            dev.index), True
+            dev.index, amp), True
 
 
 def run(model, args):
@@ -227,9 +240,9 @@ def run(model, args):
     N, E, G = batch.shape[0], edges.shape[0], charges.shape[0]
     dev = batch.device
     st = _state(model)
-    key, fresh = _pick(st, N, E, G, dev)
+    key, fresh = _pick(st, N, E, G, dev, _amp_key())
     b = st.buckets.get(key)
-    if b is not None and b.param_key != tuple(p.data_ptr() for p in b.params):
+    if b is not None and b.param_key != _param_key(model):
         st.buckets.pop(key)
         st.order.remove(key)
         b, fresh = None, True

@@ -94,14 +94,32 @@ class FusedAdam(torch.optim.Optimizer):
                 raise AimxError("FusedAdam: parameter groups may differ in lr only")
         return g0
 
+    def add_param_group(self, param_group):
+        super().add_param_group(param_group)
+        self._table_key = None  # new slots: the device arrays grow and the table is rebuilt
+
     def _device_state(self, dev):
+        n = max(sum(len(g["params"]) for g in self.param_groups), 1)
         if self._step_t is None:
             # one step counter per parameter (torch.optim.Adam's state['step']), advanced on the
             # device only for parameters that have a gradient in that step
-            n = sum(len(g["params"]) for g in self.param_groups)
-            self._step_t = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+            self._step_t = torch.zeros(n, dtype=torch.float32, device=dev)
             self._norm = torch.zeros(1, dtype=torch.float32, device=dev)
             self._lr_t = torch.zeros(len(self.param_groups), dtype=torch.float32, device=dev)
+        elif self._step_t.numel() < n or self._lr_t.numel() != len(self.param_groups):
+            # add_param_group after the first step: slots are numbered over the groups in order, so
+            # the new parameters' slots come after the existing ones, whose counters are kept
+            step = torch.zeros(n, dtype=torch.float32, device=dev)
+            step[: self._step_t.numel()].copy_(self._step_t)
+            self._step_t = step
+            k = 0
+            for group in self.param_groups:  # re-point the 0-dim views (they index the old array)
+                for p in group["params"]:
+                    if p in self.state and "step" in self.state[p]:
+                        self.state[p]["step"] = step[k]
+                    k += 1
+            self._lr_t = torch.zeros(len(self.param_groups), dtype=torch.float32, device=dev)
+            self._lr_host = None
         lrs = [float(g["lr"]) for g in self.param_groups]
         if lrs != self._lr_host and not torch.cuda.is_current_stream_capturing():
             self._lr_t.copy_(torch.tensor(lrs, dtype=torch.float32))

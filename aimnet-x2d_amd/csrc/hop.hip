@@ -16,6 +16,7 @@
 #include <cstdlib>
 
 #include "aimx_common.h"
+#include "hop_common.h"
 
 namespace aimx {
 namespace {
@@ -54,26 +55,6 @@ template <>
 __device__ __forceinline__ float2 vzero<float2>() { return make_float2(0.f, 0.f); }
 template <>
 __device__ __forceinline__ float4 vzero<float4>() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-
-// Division by a run-time invariant (Granlund-Montgomery), valid for n < 2^31.
-struct FastDiv {
-  uint32_t d, m, l;
-};
-inline FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f{d, 0, 0};
-  if (d == 0) return f;
-  while ((1ull << f.l) < d) ++f.l;
-  f.m = (uint32_t)((((1ull << 32) * ((1ull << f.l) - d)) / d) + 1);
-  return f;
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(f.m, n) + n) >> f.l; }
-
-// Row r of a chunked matrix: base + (r % rpc)*ld + (r / rpc)*chunk_stride (rpc == 0: plain rows).
-__device__ __forceinline__ int64_t row_off(uint32_t r, int64_t ld, const FastDiv& rpc, int64_t cstride) {
-  if (rpc.d == 0) return (int64_t)r * ld;
-  const uint32_t q = fdiv(r, rpc);
-  return (int64_t)(r - q * rpc.d) * ld + (int64_t)q * cstride;
-}
 
 // Row tiles: a workgroup owns `tile_rows` consecutive output rows. It stages their rowptr slice and
 // (when it fits) their whole col slice in LDS with two coalesced loads, so the per-output-element
@@ -525,6 +506,13 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
     return true;
   };
   const int vec = ok(4) ? 4 : (ok(2) ? 2 : 1);
+  // rows that are not runs of 16-byte vectors (odd D, unaligned chunk offsets) go through LDS to
+  // aligned 16-byte accesses (hop_rows.hip); AIMX_HOP_ROWS=0 keeps them here (dword lanes),
+  // AIMX_HOP_ROWS=2 sends every width there (A/B)
+  static const int64_t rows_mode = env_i64("AIMX_HOP_ROWS", 1);
+  if ((vec < 4 && rows_mode == 1) || rows_mode == 2)
+    return launch_gather_rows(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
+                              add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream);
   const int64_t upr_i = D / vec;
   // 32-bit thread indexing (rows * D / vec < 2^31) and int32 chunked row ids.
   if (rows * upr_i >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;

@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -82,8 +84,12 @@ bool decode_record(const uint8_t* p, size_t n, int32_t n_hops, int32_t n_tasks, 
   for (int32_t h = 0; h < n_hops; ++h) {
     const Obj& e = *mh->items[h];
     if (e.k != Kind::Array || e.shape.size() != 2 || e.shape[0] != 2) return false;
-    m->hop_len[h] = e.shape[1];
-    tot += e.shape[1];
+    // a first-visit pair list holds at most na * (na - 1) pairs (features.py:97-150); the
+    // decoder already checked the payload holds exactly 2 * E elements
+    const int64_t E = e.shape[1];
+    if (E < 0 || E > na * std::max<int64_t>(na - 1, 0)) return false;
+    m->hop_len[h] = E;
+    tot += E;
   }
   m->pairs.resize(size_t(2 * tot));
   int32_t* dst = m->pairs.data();
@@ -138,12 +144,24 @@ void parallel_for(int64_t n, int threads, F&& f) {
     f(0, n);
     return;
   }
+  // an exception inside a worker (e.g. bad_alloc) must not reach std::terminate: the first one
+  // is rethrown on the calling thread after every worker joined
   std::vector<std::thread> th;
+  std::exception_ptr first;
+  std::mutex mu;
   for (int t = 0; t < threads; ++t) {
     const int64_t lo = n * t / threads, hi = n * (t + 1) / threads;
-    th.emplace_back([&f, lo, hi] { f(lo, hi); });
+    th.emplace_back([&f, &first, &mu, lo, hi] {
+      try {
+        f(lo, hi);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!first) first = std::current_exception();
+      }
+    });
   }
   for (auto& x : th) x.join();
+  if (first) std::rethrow_exception(first);
 }
 
 // scalar attribute helpers (missing attribute: false)

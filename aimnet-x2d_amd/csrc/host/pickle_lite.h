@@ -162,6 +162,8 @@ inline bool as_f64(const Obj* o, double* out) {
 
 class Decoder {
  public:
+  static constexpr int64_t kMaxElems = int64_t(1) << 40;  // per array; keeps numel * itemsize < 2^63
+
   // Decode one pickle; returns nullptr (and sets err) on malformed input or a disallowed opcode.
   Ref decode(const uint8_t* p, size_t n, std::string* err) {
     p_ = p;
@@ -287,6 +289,7 @@ class Decoder {
       a->dtype = args->items[0]->s;
       a->order = args->items[0]->order;
       a->raw = args->items[1];
+      if (!size_ok(*a)) return false;
       st_.push_back(a);
       return true;
     }
@@ -298,11 +301,9 @@ class Decoder {
       a->raw = args->items[0];
       a->dtype = args->items[1]->s;
       a->order = args->items[1]->order;
-      for (auto& d : args->items[2]->items) {
-        if (d->k != Kind::Int) return err("_frombuffer shape");
-        a->shape.push_back(d->i);
-      }
+      if (!set_shape(a.get(), args->items[2])) return false;
       a->fortran = args->items[3]->k == Kind::Str && args->items[3]->s == "F";
+      if (!size_ok(*a)) return false;
       st_.push_back(a);
       return true;
     }
@@ -319,23 +320,38 @@ class Decoder {
       if (state->k != Kind::Tuple || state->items.size() < 5) return err("ndarray state");
       const auto& it = state->items;
       if (it[1]->k != Kind::Tuple || it[2]->k != Kind::Dtype || it[4]->k != Kind::Bytes) return err("ndarray state types");
-      obj->shape.clear();
-      for (auto& d : it[1]->items) {
-        if (d->k != Kind::Int) return err("ndarray shape");
-        obj->shape.push_back(d->i);
-      }
+      if (!set_shape(obj.get(), it[1])) return false;
       obj->dtype = it[2]->s;
       obj->order = it[2]->order;
       obj->fortran = it[3]->k == Kind::Bool && it[3]->i;
       obj->raw = it[4];
-      if (obj->numel() * itemsize(obj->dtype) != obj->nbytes()) return err("ndarray size");
-      return true;
+      return size_ok(*obj);
     }
     return err("BUILD on an unsupported object");
   }
   bool err(const std::string& m) {
     msg_ = m;
     return false;
+  }
+  // shape dims from a tuple of Ints: each >= 0, the element count bounded (no overflow later in
+  // numel() * itemsize); false on anything else (malformed input never reaches an allocation)
+  bool set_shape(Obj* a, const Ref& tup) {
+    a->shape.clear();
+    int64_t n = 1;
+    for (auto& d : tup->items) {
+      if (d->k != Kind::Int || d->i < 0) return err("array shape");
+      if (d->i > 0 && n > kMaxElems / d->i) return err("array too large");
+      n *= d->i;
+      a->shape.push_back(d->i);
+    }
+    return true;
+  }
+  // the payload holds exactly numel * itemsize bytes of a known dtype
+  bool size_ok(const Obj& a) {
+    const int sz = itemsize(a.dtype);
+    if (sz <= 0 || sz > 16) return err("array dtype");
+    if (a.numel() * sz != a.nbytes()) return err("array size");
+    return true;
   }
 
   bool step(uint8_t op) {

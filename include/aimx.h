@@ -98,8 +98,10 @@ int aimx_csr_build_multi(const AimxCsrSpec* specs, int32_t n, void* workspace, s
  * row_seg (nullable, stride row_seg_stride): segment id per row of the first output chunk —
  * the molecule index (batch_indices) for the hop and its backward, whose rows are atoms. Rows
  * of one segment are consecutive and edges stay inside a segment, so row tiles cut at segment
- * starts (when one lies within 64 rows of the nominal cut) stage their source rows exactly once.
- * The result does not depend on row_seg (it only moves tile boundaries).
+ * starts (when one lies within 64 rows of the nominal cut) stage their source rows exactly once;
+ * for rows that are not 16-byte vectors (odd D such as 153 / 307, or unaligned chunk offsets) a
+ * tile is the set of whole segments that start in a window of rows. The result does not depend on
+ * row_seg (it only moves tile boundaries). Rows must be 4-byte aligned (fp32).
  * ------------------------------------------------------------------------------------------ */
 int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rows_per_chunk,
                             int64_t src_chunk_stride, int64_t D,

@@ -164,6 +164,38 @@ def test_autograph_falls_back_and_guards():
         h.remove()
 
 
+def test_autograph_amp_state_and_replaced_parameters():
+    """The autocast state is part of the bucket key (a capture bakes in bf16 or fp32 GEMM operands):
+    the same batch under autocast gets its own bucket and matches the eager AMP path; replacing the
+    Parameter objects (load_state_dict(assign=True)) re-captures instead of replaying stale weights."""
+    from aimx import autograph
+    b = _batches(1, 61)[0]
+    m1 = _model()
+    m2 = _model()
+    m2.load_state_dict(m1.state_dict())
+    autograph.enable(m2)
+    for amp in (False, True, False, True):
+        outs = []
+        for m in (m1, m2):
+            m.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                out, _, _ = m(*b.model_args())
+            out.sum().backward()
+            outs.append(out.detach())
+        assert _rel(outs[1], outs[0]) < 1e-5, amp
+    st = m2.__dict__["_aimx_autograph_state"]
+    assert len(st.buckets) == 2
+    with torch.no_grad():  # new Parameter objects with new values
+        sd = {k: v * 1.5 for k, v in m1.state_dict().items()}
+    m1.load_state_dict(sd)
+    m2.load_state_dict(sd, assign=True)
+    o1 = m1(*b.model_args())[0]
+    o2 = m2(*b.model_args())[0]
+    assert _rel(o2.detach(), o1.detach()) < 1e-5
+    o2.sum().backward()
+    assert all(p.grad is not None for n, p in m2.named_parameters() if "long_range" not in n)
+
+
 @pytest.mark.parametrize("slack", [1, 7, 8, 9, 300])
 def test_pad_batch_matches_pad_collated(slack):
     """aimx_pad_batch (one launch) builds exactly aimx.data.pad_collated's static layout: real rows

@@ -648,6 +648,37 @@ def test_fused_adam_missing_gradients_keep_per_parameter_steps():
         assert norm_rel(opt.state[a]["exp_avg_sq"].cpu().numpy(), topt.state[b]["exp_avg_sq"].cpu().numpy()) < 1e-6
 
 
+def test_fused_adam_add_param_group_after_steps():
+    """optimizer.add_param_group() after the first step (torch.optim.Adam supports it): the step
+    counters and learning rates grow with the groups; existing parameters keep their counts."""
+    from aimx.optim import FusedAdam
+    g = torch.Generator().manual_seed(13)
+    shapes1, shapes2 = [(40, 8), (8,)], [(300,), (7, 3)]
+    p1 = [torch.randn(s, generator=g) for s in shapes1]
+    p2 = [torch.randn(s, generator=g) for s in shapes2]
+    ours1, ref1 = [x.clone().to(DEV).requires_grad_() for x in p1], [x.clone().to(DEV).requires_grad_() for x in p1]
+    ours2, ref2 = [x.clone().to(DEV).requires_grad_() for x in p2], [x.clone().to(DEV).requires_grad_() for x in p2]
+    opt = FusedAdam(ours1, lr=1e-2, max_grad_norm=1.0)
+    topt = torch.optim.Adam(ref1, lr=1e-2)
+
+    def step(ours, ref):
+        for a, b in zip(ours, ref):
+            gr = torch.randn(a.shape, generator=g)
+            a.grad, b.grad = gr.to(DEV).clone(), gr.to(DEV).clone()
+        opt.step()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        topt.step()
+    for _ in range(3):
+        step(ours1, ref1)
+    opt.add_param_group({"params": ours2, "lr": 3e-3})
+    topt.add_param_group({"params": ref2, "lr": 3e-3})
+    for _ in range(2):
+        step(ours1 + ours2, ref1 + ref2)
+    for a, b in zip(ours1 + ours2, ref1 + ref2):
+        assert float(opt.state[a]["step"]) == float(topt.state[b]["step"])
+        assert norm_rel(a.detach().cpu().numpy(), b.detach().cpu().numpy()) < 1e-6
+
+
 def test_aux_stream_weight_gradients_identical(monkeypatch):
     """AIMX_AUX=1 (weight gradients forked onto an auxiliary stream, event fork/join) gives the
     same gradients bit for bit as the single grouped launch (eager execution)."""
