@@ -126,6 +126,24 @@ def test_pickle_decoder_executes_nothing():
     assert h5.decode_record(b"\x80\x04garbage", 3)[0] is False
 
 
+def test_malformed_array_shapes_are_rejected():
+    """Protocol-5 records whose hop array claims a negative or oversized shape (2, -5) / (2, 2e9):
+    the decoder rejects them (dims checked, numel * itemsize must equal the payload) instead of
+    writing outside the record's buffer or throwing bad_alloc inside a worker thread."""
+    import struct
+    mols = synth_molecules(1, seed=3)
+    rec = h5.make_record(*mols[0], 3, 1.0)
+    e1 = rec["precomputed"]["multi_hop_edges"][0].shape[1]
+    assert e1 < 256
+    blob = pickle.dumps(rec, protocol=5)
+    pat = b"K\x02K" + bytes([e1]) + b"\x86"  # the first hop array's shape tuple (2, E1)
+    assert pat in blob
+    assert h5.decode_record(blob, 3)[0] is True
+    for bad in (-5, 2_000_000_000, 0x7FFFFFFF):
+        evil = blob.replace(pat, b"K\x02J" + struct.pack("<i", bad) + b"\x86", 1)
+        assert h5.decode_record(evil, 3) == (False, 0, 0), bad
+
+
 def test_rank_shards_equal_and_covering():
     """Equal shard lengths (the reference's contiguous ceil split leaves the last ranks short or
     empty, molecular.py:228-237); every record appears; shuffle is seeded per rank."""
