@@ -61,8 +61,13 @@ class GraphedTrainStep:
     """
 
     def __init__(self, model, criterion, optimizer, example_batch, n_real=None, sync=None, warmup=3,
-                 ddp_graph=None):
+                 ddp_graph=None, inject_capture_failure=None):
         import os
+        # test hook (tests/test_gpu_ddp.py): make the "capture" attempt raise as a failing RCCL build
+        # would, to exercise the split fallback on any box
+        if inject_capture_failure is None:
+            inject_capture_failure = os.environ.get("AIMX_TEST_CAPTURE_FAIL", "0") == "1"
+        self.capture_error = None
         self.model, self.criterion, self.optimizer, self.sync = model, criterion, optimizer, sync
         model._aimx_autograph_off = True  # this step captures the model itself (aimx.autograph stays off)
         self.B = _real_rows(example_batch) if n_real is None else int(n_real)
@@ -127,14 +132,17 @@ class GraphedTrainStep:
                 with torch.cuda.graph(self.g1, capture_error_mode="thread_local"):
                     fwd_bwd()
                     sync.finish()
+                    if inject_capture_failure:
+                        raise RuntimeError("injected capture failure (test hook)")
                     optimizer.step()
-            except RuntimeError as e:  # pragma: no cover (depends on the RCCL build)
+            except RuntimeError as e:  # depends on the RCCL build (and the test hook)
                 ok, err = False, e
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if int(flag.item()) == 0:
                 import sys
                 print(f"aimx.train: RCCL all-reduce capture failed ({err}); using split graphs", file=sys.stderr)
+                self.capture_error = str(err) if err is not None else "failed on another rank"
                 sync._reset()
                 optimizer.zero_grad(set_to_none=True)
                 self.g1 = torch.cuda.CUDAGraph()

@@ -121,6 +121,25 @@ def barrier() -> None:
         dist.barrier()
 
 
+def replica_checksums(params, device=None):
+    """(plain, position-weighted) exact int64 sums of the parameters' fp32 bit patterns, all-reduced
+    MAX and MIN over the ranks: data-parallel replicas are bit-identical iff max == min for both (up to
+    hash collisions). Returns (identical, local sums, max, min)."""
+    ps = [p.detach().reshape(-1) for p in params]
+    dev = device or (ps[0].device if ps else "cpu")
+    h = torch.zeros(2, dtype=torch.int64, device=dev)
+    for i, p in enumerate(ps):
+        bits = p.contiguous().view(torch.int32).to(torch.int64)
+        h[0] += bits.sum()
+        w = (torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 1021) + 1 + i
+        h[1] += (bits * w).sum()
+    mx, mn = h.clone(), h.clone()
+    if _ready():
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+    return bool(torch.equal(mx, mn)), h.tolist(), mx.tolist(), mn.tolist()
+
+
 class GradientSync:
     """Bucketed, backward-overlapped gradient all-reduce over one flat fp32 buffer per bucket.
 
@@ -294,6 +313,39 @@ class GradientSync:
             elif dst:
                 torch._foreach_copy_(dst, src)
         self._reset()
+
+    def time_allreduce(self, iters: int = 20) -> float:
+        """Microseconds per step of this sync's collectives alone: every bucket's all-reduce on its
+        flat buffer, back to back, `iters` times (HIP events on the collectives' stream for RCCL,
+        wall clock for gloo). Call after training steps (the flat buffers exist; their contents
+        are scratch until the next pack)."""
+        import time
+        if not self.active or any(f is None for f in self._flat):
+            return 0.0
+        dev = self._flat[0].device
+        if self.comm is not None:
+            s = self._stream if self.side_stream else torch.cuda.current_stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for f in self._flat:  # warm
+                self.comm.all_reduce(f, average=True, stream=s)
+            t0.record(s)
+            for _ in range(iters):
+                for f in self._flat:
+                    self.comm.all_reduce(f, average=True, stream=s)
+            t1.record(s)
+            t1.synchronize()
+            torch.cuda.current_stream(dev).wait_stream(s)
+            return t0.elapsed_time(t1) * 1e3 / iters
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(iters):
+            for f in self._flat:
+                dist.all_reduce(f, group=self.group)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t) * 1e6 / iters
 
     def remove(self):
         for h in self._hooks:

@@ -613,6 +613,21 @@ def main():
         dt = float(t.item())
     if feeder is not None:
         feeder.close()
+    ddp_check = None
+    if sync is not None:
+        # self-verification of the data-parallel run (every rank takes part): replicas bit-identical
+        # after the timed steps, and the collectives' own cost per step
+        from utils.distributed import replica_checksums
+        identical, local, mx, mn = replica_checksums(list(model.parameters()), device)
+        ar_us = sync.time_allreduce(iters=20)
+        t = torch.tensor([ar_us], device=device, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ddp_check = {"replicas_identical": identical, "param_checksum_max": mx, "param_checksum_min": mn,
+                     "allreduce_us_per_step": round(float(t.item()), 2),
+                     "allreduce_note": "every bucket's all-reduce alone, back to back (HIP events on the "
+                                       "collectives' stream), max over ranks; inside the timed steps they "
+                                       "overlap the backward"}
     from aimx import _lib as alib
     # a clustered head wait gave up on ANY rank: the run is invalid (max over ranks)
     tmo = alib.head_sync_flag(device).reshape(1)
@@ -683,17 +698,33 @@ def main():
         if sync is not None:
             line["ddp"] = {"world_size_reported": dist.get_world_size(), "backend": dist.get_backend(),
                            "graph_mode": graphed.mode if graphed is not None else "eager",
+                           "capture_fallback": graphed is not None and graphed.capture_error is not None,
                            "buckets": len(sync.buckets),
-                           "bucket_mb": [round(sum(p.numel() for p in bk) * 4 / 2 ** 20, 3) for bk in sync.buckets]}
+                           "bucket_mb": [round(sum(p.numel() for p in bk) * 4 / 2 ** 20, 3) for bk in sync.buckets],
+                           **ddp_check}
             if args.gpus != world:
                 line["ddp"]["note"] = f"--gpus {args.gpus} but WORLD_SIZE {world}"
         if cpu is not None:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         if head_timeout:
             line["invalid"] = "clustered head wait timed out"
+        if ddp_check is not None and not ddp_check["replicas_identical"]:
+            line["invalid"] = "data-parallel replicas diverged"
         print(json.dumps(line), flush=True)
+    # a data-parallel run that diverged, or whose RCCL capture fell back to split graphs, is reported
+    # above and then fails the command (every rank knows both facts)
+    rc = 0
+    if ddp_check is not None and not ddp_check["replicas_identical"]:
+        print("bench: data-parallel replicas diverged (parameter checksums differ across ranks)", file=sys.stderr)
+        rc = 3
+    elif graphed is not None and graphed.capture_error is not None:
+        print(f"bench: the RCCL all-reduce capture fell back to split graphs ({graphed.capture_error})",
+              file=sys.stderr)
+        rc = 4
     if dist.is_initialized():
         dist.destroy_process_group()
+    if rc:
+        sys.exit(rc)
 
 
 if __name__ == "__main__":

@@ -124,3 +124,29 @@ def test_gradient_sync_bucket_layout():
         assert sum(p.numel() for p in b) * 4 <= 2 * 2 ** 20 or len(b) == 1
     assert not sync.active and not sync.capturable  # no process group: finish() is a no-op
     sync.finish()
+
+
+def _checksums(rank, world):
+    from utils.distributed import GradientSync, replica_checksums
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Linear(5, 3))
+    same = replica_checksums(list(net.parameters()))[0]
+    with torch.no_grad():
+        if rank == 1:  # one ulp on one replica
+            w = net[0].weight.view(-1)
+            w[3] = torch.nextafter(w[3], torch.tensor(float("inf")))
+    differ = replica_checksums(list(net.parameters()))[0]
+    sync = GradientSync(net.parameters(), bucket_mb=0.0001)
+    net(torch.randn(2, 7)).sum().backward()
+    sync.finish()
+    us = sync.time_allreduce(iters=3)
+    return {"same": same, "differ": differ, "us": us, "buckets": len(sync.buckets)}
+
+
+def test_replica_checksums_and_allreduce_timing():
+    """bench.py's self-check of a data-parallel run: identical replicas agree, one ulp of difference
+    on one rank is caught on every rank; the collectives' own time per step is measured."""
+    out = _run("_checksums")
+    for r in range(2):
+        assert out[r]["same"] and not out[r]["differ"], out[r]
+        assert out[r]["us"] > 0 and out[r]["buckets"] >= 2

@@ -172,6 +172,15 @@ def ddp_split_graph(rank, world):
     torch.cuda.synchronize()
     res["mode"] = g.mode
     res["graph"] = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    from utils.distributed import replica_checksums
+    res["identical"] = replica_checksums(list(m.parameters()))[0]
+    with torch.no_grad():  # one replica perturbed by one ulp: the check must see it
+        p0 = next(m.parameters())
+        if rank == 1:
+            p0.view(-1)[0] = torch.nextafter(p0.view(-1)[0], torch.tensor(float("inf"), device=p0.device))
+        res["perturbed_identical"] = replica_checksums(list(m.parameters()))[0]
+        if rank == 1:
+            p0.view(-1)[0] = torch.nextafter(p0.view(-1)[0], torch.tensor(float("-inf"), device=p0.device))
     sync.remove()
     m = _model()
     opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
@@ -187,6 +196,8 @@ def test_split_graph_ddp_replicas_agree_and_equal_eager():
     out = _run("ddp_split_graph")
     assert out[0]["mode"] == out[1]["mode"] == "split"  # gloo collectives cannot be captured
     np.testing.assert_array_equal(out[0]["graph"], out[1]["graph"])  # replicas stay identical
+    assert out[0]["identical"] and out[1]["identical"]  # ... and the bench's checksum agrees
+    assert not out[0]["perturbed_identical"] and not out[1]["perturbed_identical"]
     np.testing.assert_array_equal(out[0]["eager"], out[1]["eager"])
     scale = np.abs(out[0]["eager"]).max()
     assert np.abs(out[0]["graph"] - out[0]["eager"]).max() <= 1e-5 * scale
@@ -223,6 +234,79 @@ def test_rccl_allreduce_captured_in_step_graph():
     assert out["mode"] == "capture", out
     assert out["buckets"] > 2
     assert out["err"] <= 1e-5 * out["scale"], out
+
+
+def rccl_capture_fallback_world1(rank, world):
+    """The capture of the RCCL all-reduces fails (injected, as a failing RCCL build would): every
+    rank falls back to split graphs, and the split step still equals the eager step."""
+    from aimx.optim import FusedAdam
+    from aimx.train import GraphedTrainStep, train_step
+    from models import L1Loss
+    from utils.distributed import GradientSync, replica_checksums
+    bs = _padded_batches(0, 4)
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    sync = GradientSync(m.parameters(), unused=m.unused_parameters(), always=True, bucket_mb=0.25,
+                        first_bucket_mb=0.05)
+    g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1, inject_capture_failure=True)
+    for b in bs[1:]:
+        g(b)
+    torch.cuda.synchronize()
+    got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    ident = replica_checksums(list(m.parameters()))[0]
+    ar_us = sync.time_allreduce(iters=3)
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    for b in bs:
+        train_step(m, b, L1Loss(), opt, n_real=B_HALF)
+    torch.cuda.synchronize()
+    want = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    return {"mode": g.mode, "capture_error": g.capture_error, "err": float(np.abs(got - want).max()),
+            "scale": float(np.abs(want).max()), "identical": ident, "ar_us": ar_us}
+
+
+def test_rccl_capture_failure_falls_back_to_split():
+    out = _run("rccl_capture_fallback_world1", world=1, backend="nccl")[0]
+    assert out["mode"] == "split" and "injected" in out["capture_error"], out
+    assert out["err"] <= 1e-5 * out["scale"], out
+    assert out["identical"] and out["ar_us"] > 0, out
+
+
+def ddp_wrapped(rank, world):
+    """The reference's own data-parallel wrapping, unchanged (runner.py:703-707):
+    DistributedDataParallel(GNN, find_unused_parameters=True) over this GNN — the autograph steps
+    aside under a multi-rank group, DDP's reducer averages the gradients."""
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from aimx import autograph
+    from models import L1Loss
+    b = _qm9_batch(np.arange(rank * B_HALF, (rank + 1) * B_HALF))
+    m = _model()
+    assert not autograph.wanted(m, b.model_args())  # multi-rank group: eager path
+    ddp = DDP(m, device_ids=[0], find_unused_parameters=True)
+    out, _, _ = ddp(*b.model_args())
+    L1Loss()(out, b.targets).backward()
+    torch.cuda.synchronize()
+    return {"grads": _grads(m)}
+
+
+def test_ddp_wrapped_drop_in_equals_full_batch():
+    """INTEGRATION.md's claim: the reference trainer's DDP wrapping still works on this GNN, and two
+    ranks' averaged gradients equal one process's full-batch gradients (1e-5 norm-relative)."""
+    from models import L1Loss
+    out = _run("ddp_wrapped")
+    m = _model()
+    b = _qm9_batch(np.arange(2 * B_HALF))
+    o, _, _ = m(*b.model_args())
+    L1Loss()(o, b.targets).backward()
+    full = _grads(m)
+    for r in range(2):
+        got = out[r]["grads"]
+        assert set(got) == set(full), r
+        for k, want in full.items():
+            den = max(np.abs(want).max(), 1e-12)
+            if ".attention_weights." in k and k.endswith(".bias"):
+                den = max(np.abs(full[k[:-4] + "weight"]).max(), 1e-12)
+            assert np.abs(got[k] - want).max() / den <= 1e-5, (k, r)
 
 
 def test_multi_copy_exact():
