@@ -17,6 +17,9 @@ step, ~2 ms) rather than by the ~0.9 ms of device work. By default (AIMX_AUTOGRA
   * hands the parameters their gradients as the bucket's static gradient tensors (assigned when
     `.grad` is None — `zero_grad(set_to_none=True)`, PyTorch's default; accumulated otherwise).
 
+By default it applies to batches whose atoms x hidden width is at most MAX_WORK (device-bound
+larger steps run eagerly, measured faster); `enable(model, True)` forces it for any size.
+
 A bucket is captured on first use (warm-up on a side stream, then the forward graph and the
 backward graph, each in its own memory pool so that no replay overwrites the other's live
 tensors). The eager path
@@ -48,8 +51,17 @@ def enable(model, on=True):
     return model
 
 
+# The replay pays off while the eager step is bound by the host's launches (c2: 2.2 ms eager vs
+# 0.92 ms replayed); once the device work per step outgrows them, the bucket's padding and the per-step
+# CSR build cost more than the launches saved (c4: 4.00 vs 3.29 ms eager, c5: 5.64 vs 5.14 ms;
+# profiles/r02_bench_c4.json, r02_bench_c5.json). Gate: atoms x hidden width of the batch (c2 / c3
+# 2.4 M, c4 / c5 10.4 M); an explicit enable(model, True) replays whatever the size.
+MAX_WORK = int(float(os.environ.get("AIMX_AUTOGRAPH_MAX_WORK", "6e6")))
+
+
 def wanted(model, args):
     on = getattr(model, "_aimx_autograph_on", None)
+    explicit = on is not None
     if on is None:
         on = os.environ.get("AIMX_AUTOGRAPH", "1") != "0"
     if not on or getattr(model, "_aimx_autograph_off", False):
@@ -57,6 +69,8 @@ def wanted(model, args):
     if not (model.training and torch.is_grad_enabled()) or torch.cuda.is_current_stream_capturing():
         return False
     feats, edges, batch, charges, tet, cis, trans = args
+    if not explicit and batch.shape[0] * int(getattr(model, "hidden_dim", 0)) > MAX_WORK:
+        return False
     if edges.numel() == 0 or edges.dim() != 2 or edges.shape[1] != 2 or edges.dtype != torch.int64:
         return False
     if model.use_stereochemistry and (tet.numel() or cis.numel() or trans.numel()):

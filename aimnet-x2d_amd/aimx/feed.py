@@ -65,6 +65,8 @@ def load_host():
     lib.aimx_store_num_molecules.argtypes = [c_ptr]
     lib.aimx_store_num_atoms.restype = c_i64
     lib.aimx_store_num_atoms.argtypes = [c_ptr, c_i64]
+    lib.aimx_store_atom_counts.restype = c_i32
+    lib.aimx_store_atom_counts.argtypes = [c_ptr, c_ptr]
     lib.aimx_collator_create.restype = c_i32
     lib.aimx_collator_create.argtypes = [c_i32, c_i32, ctypes.POINTER(c_ptr)]
     lib.aimx_collator_destroy.argtypes = [c_ptr]
@@ -74,6 +76,8 @@ def load_host():
     lib.aimx_collate_write.argtypes = [c_ptr, ctypes.POINTER(CollateOut)]
     lib.aimx_csr_host_build.restype = c_i32
     lib.aimx_csr_host_build.argtypes = [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32] + [c_ptr] * 6
+    lib.aimx_collate_csr.restype = c_i32
+    lib.aimx_collate_csr.argtypes = [c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32] + [c_ptr] * 6
     _lib = lib
     return lib
 
@@ -156,7 +160,8 @@ class HostStore:
         s._lib, s._h = lib, handle
         s.n_feat, s.n_tasks = int(n_feat), int(n_tasks)
         s.n_mols = int(lib.aimx_store_num_molecules(handle))
-        s.n_atoms = np.array([lib.aimx_store_num_atoms(handle, m) for m in range(s.n_mols)], np.int64)
+        s.n_atoms = np.empty(s.n_mols, np.int64)
+        _check(lib.aimx_store_atom_counts(handle, s.n_atoms.ctypes.data), "store_atom_counts")
         return s
 
     @classmethod
@@ -221,6 +226,7 @@ class HostCollator:
         self.max_hops = int(max_hops)
         # collate_blob also builds the batch's CSR views for a model of max_hops hops (csr=False: not)
         self.csr_hops = self.max_hops if csr else 0
+        self._layouts = {}
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -260,16 +266,30 @@ class HostCollator:
         return {"edges": edges, "feats": feats.T.copy(), "batch": batch, "n_atoms": na, "total_charges": tc,
                 "targets": tg[:, :store.n_tasks]}
 
-    def collate_blob(self, store, idx, pinned=True, n_max=0, e_max=0, pad_mols=0, n_tasks=None):
-        """Plan + write one batch into a (pinned) host byte tensor in DeviceBatch layout.
-        Returns (blob uint8 tensor, layout, G_rows, N_rows, real (G, N, E))."""
+    def blob_layout(self, nr, er, gr, t):
+        """(layout, nbytes) of a blob of these row counts (cached: the same every padded batch)."""
+        key = (nr, er, gr, t)
+        hit = self._layouts.get(key)
+        if hit is None:
+            hit = self._layouts[key] = adata.blob_layout(adata.batch_fields(nr, er, gr, max(t, 1), self.csr_hops))
+        return hit
+
+    def collate_blob(self, store, idx, pinned=True, n_max=0, e_max=0, pad_mols=0, n_tasks=None, out=None):
+        """Plan + write one batch into a (pinned) host byte tensor in DeviceBatch layout (`out`: an
+        existing one of the right size, e.g. a feeder ring slot). Returns (blob uint8 tensor,
+        layout, G_rows, N_rows, real (G, N, E))."""
         n, e = self.plan(store, idx)
         g = self._idx.shape[0]
         pad = n_max > 0
         nr, er, gr = (n_max, e_max, g + pad_mols) if pad else (n, e, g)
         t = store.n_tasks if n_tasks is None else n_tasks
-        layout, nbytes = adata.blob_layout(adata.batch_fields(nr, er, gr, max(t, 1), self.csr_hops))
-        blob = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
+        layout, nbytes = self.blob_layout(nr, er, gr, t)
+        if out is not None:
+            if out.numel() != nbytes:
+                raise HostError(f"collate_blob: out has {out.numel()} bytes, the batch needs {nbytes}")
+            blob = out
+        else:
+            blob = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
         base = blob.data_ptr()
         ptr = [base + o for o, _, _ in layout]
         if t == 0:  # no targets in the store: zero the target field
@@ -278,9 +298,25 @@ class HostCollator:
         self.write(ptr[:4], ptr[4], ptr[5], ptr[6], ptr[7] if t else None, None, n_max if pad else 0,
                    e_max if pad else 0, pad_mols if pad else 0)
         if self.csr_hops > 0:  # the step's CSR views ride in the same blob (one H2D copy)
-            _check(self._lib.aimx_csr_host_build(ptr[4], er, ptr[5], nr, gr, self.csr_hops, *ptr[8:14]),
-                   "csr_host_build")
+            _check(self._lib.aimx_collate_csr(self._h, ptr[4], er, ptr[5], nr, gr, self.csr_hops, *ptr[8:14]),
+                   "collate_csr")
         return blob, layout, gr, nr, (g, n, e)
+
+
+class _Slot:
+    """One ring entry of a static-shape BatchFeeder: pinned host blob, device blob, the DeviceBatch
+    views over the device blob (built once), and the events that guard their reuse."""
+    __slots__ = ("host", "dev", "batch", "h2d", "released", "index", "refs", "out")
+
+    def __init__(self, nbytes, layout, gr, nr, hops, device):
+        self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        self.batch = adata.DeviceBatch.from_blob(self.dev, layout, gr, nr, hops)
+        self.h2d = torch.cuda.Event()       # the copy out of `host` is done (host reuse)
+        self.released = torch.cuda.Event()  # the consumer's work on the batch is enqueued before it
+        self.index = -1                     # item last held
+        self.refs = None                    # reference count of `batch` while only the ring holds it
+        self.out = False                    # handed to the consumer, `released` not yet recorded
 
 
 class BatchFeeder:
@@ -288,10 +324,17 @@ class BatchFeeder:
 
     batches: iterable of molecule-index arrays into `store`, or of (store, index array) pairs (a
     stream whose chunks are separate stores, aimx.h5.HDF5MolecularStream.batches; `store` may then
-    be None). Yields DeviceBatch objects whose copy has been
-    enqueued on the feeder's copy stream; the consumer's current stream waits on it (event), so
-    the step never reads a half-copied batch and never blocks the host on the copy. Padding to
-    static shapes (n_max/e_max/pad_mols) makes the batches replayable by one captured HIP graph.
+    be None). Yields DeviceBatch objects whose copy has been enqueued on the feeder's copy stream;
+    the consumer's current stream waits on it (event), so the step never reads a half-copied batch
+    and never blocks the host on the copy. Padding to static shapes (n_max/e_max/pad_mols) makes the
+    batches replayable by one captured HIP graph.
+
+    Static shapes also let the feeder keep a ring of pinned host / device blobs with their batch
+    views built once, so a batch costs one native collate (the pool's threads, GIL released), one
+    async copy and two events, and no allocation. A ring slot is written again only when nothing
+    outside the ring still references its batch (a consumer that keeps batches, e.g. list(feeder),
+    makes the ring grow instead) and, on the device, after the consumer's work on it: its stream
+    records `released` when it asks for the next batch.
     """
 
     def __init__(self, store, index_batches, max_hops, device, depth=3, threads=4, n_max=0, e_max=0, pad_mols=0):
@@ -303,41 +346,129 @@ class BatchFeeder:
         self._it = iter(index_batches)
         self._stop = False
         self._err = None
+        self._ring = []           # static shapes: _Slot list (grows while the consumer keeps batches)
+        self._next_slot = 0
+        self._last = None         # the slot handed out last (released at the next request)
+        # seconds spent per stage (feeder thread: next index batch / native collate / H2D enqueue /
+        # batch views / waiting for queue room; consumer: waiting for a batch), and counts
+        self.reset_stats()
         self._th = threading.Thread(target=self._run, daemon=True)
         self._th.start()
 
+    def reset_stats(self):
+        """Zero the stage times in place (the feeder thread keeps updating the same dict)."""
+        if not hasattr(self, "times"):
+            self.times = {}
+        for k in ("source", "collate", "h2d", "views", "put_wait", "get_wait"):
+            self.times[k] = 0.0
+        self.times["batches"] = 0
+
+    def _slot(self, nbytes, layout, gr, nr):
+        """A ring slot free for the next batch: the oldest one nothing else references, else a new one."""
+        import sys
+        n = len(self._ring)
+        for k in range(n):
+            sl = self._ring[(self._next_slot + k) % n]
+            if not sl.out and sys.getrefcount(sl.batch) <= sl.refs and sl.dev.numel() == nbytes:
+                self._next_slot = (self._next_slot + k + 1) % n
+                return sl
+        sl = _Slot(nbytes, layout, gr, nr, self.collator.csr_hops, self.device)
+        self._ring.insert(self._next_slot, sl)
+        self._next_slot = (self._next_slot + 1) % len(self._ring)
+        sl.refs = sys.getrefcount(sl.batch)
+        return sl
+
     def _run(self):
+        import time
+        T = self.times
+        static = self.pad[0] > 0
         try:
-            for item in self._it:
+            it = iter(self._it)
+            while True:
+                t0 = time.perf_counter()
+                try:
+                    item = next(it)
+                except StopIteration:
+                    break
                 if self._stop:
                     break
+                t1 = time.perf_counter()
                 store, idx = item if isinstance(item, tuple) else (self.store, item)
-                blob, layout, gr, nr, real = self.collator.collate_blob(store, idx, True, *self.pad)
-                with torch.cuda.stream(self.stream):
-                    dev = blob.to(self.device, non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(self.stream)
-                b = adata.DeviceBatch.from_blob(dev, layout, gr, nr, self.collator.csr_hops)
+                if static:
+                    n, e = self.collator.plan(store, idx)
+                    nr, er, gr = self.pad[0], self.pad[1], len(idx) + self.pad[2]
+                    t = store.n_tasks
+                    layout, nbytes = self.collator.blob_layout(nr, er, gr, t)
+                    sl = self._slot(nbytes, layout, gr, nr)
+                    if sl.index >= 0:
+                        sl.h2d.synchronize()  # the pinned blob's previous copy has left it
+                    blob, layout, gr, nr, real = self.collator.collate_blob(store, idx, True, *self.pad, out=sl.host)
+                    t2 = time.perf_counter()
+                    with torch.cuda.stream(self.stream):
+                        if sl.index >= 0:
+                            self.stream.wait_event(sl.released)
+                        sl.dev.copy_(sl.host, non_blocking=True)
+                        sl.h2d.record(self.stream)
+                    sl.index += 1
+                    t3 = time.perf_counter()
+                    b = sl.batch
+                    ev, keep = sl.h2d, sl
+                else:
+                    blob, layout, gr, nr, real = self.collator.collate_blob(store, idx, True, *self.pad)
+                    t2 = time.perf_counter()
+                    with torch.cuda.stream(self.stream):
+                        dev = blob.to(self.device, non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(self.stream)
+                    t3 = time.perf_counter()
+                    b = adata.DeviceBatch.from_blob(dev, layout, gr, nr, self.collator.csr_hops)
+                    keep = blob
                 b.real_graphs, b.real_atoms, b.real_edges = real
-                self._q.put((b, ev, blob))
+                t4 = time.perf_counter()
+                self._q.put((b, ev, keep))
+                t5 = time.perf_counter()
+                T["source"] += t1 - t0
+                T["collate"] += t2 - t1
+                T["h2d"] += t3 - t2
+                T["views"] += t4 - t3
+                T["put_wait"] += t5 - t4
+                T["batches"] += 1
         except Exception as exc:  # surfaced to the consumer
             self._err = exc
         self._q.put(None)
+
+    def stats(self):
+        """Milliseconds per batch of each stage (see reset_stats), and the ring size."""
+        n = max(self.times["batches"], 1)
+        return {k: round(v * 1e3 / n, 4) for k, v in self.times.items() if k != "batches"} | \
+            {"batches": self.times["batches"], "ring": len(self._ring)}
 
     def __iter__(self):
         return self
 
     def __next__(self):
+        import time
+        cur = torch.cuda.current_stream(self.device)
+        if self._last is not None:  # the consumer's work on the previous batch is enqueued
+            self._last.released.record(cur)
+            self._last.out = False
+            self._last = None
+        t0 = time.perf_counter()
         item = self._q.get()
+        self.times["get_wait"] += time.perf_counter() - t0
         if item is None:
             if self._err is not None:
                 raise self._err
             raise StopIteration
-        b, ev, blob = item
-        torch.cuda.current_stream(self.device).wait_event(ev)
-        b._host_blob = blob  # keep the pinned source alive until the copy has been consumed
-        # the consumer's stream must not reuse the device blob before its own work is done
-        b._blob.record_stream(torch.cuda.current_stream(self.device))
+        b, ev, keep = item
+        cur.wait_event(ev)
+        if isinstance(keep, _Slot):
+            keep.out = True
+            self._last = keep
+        else:
+            b._host_blob = keep  # keep the pinned source alive until the copy has been consumed
+            # the consumer's stream must not reuse the device blob before its own work is done
+            b._blob.record_stream(cur)
         return b
 
     def close(self):

@@ -41,7 +41,7 @@ _ERR = {-1: "invalid argument", -3: "out of host memory", -10: "HDF5 I/O error",
 
 class H5Info(ctypes.Structure):
     _fields_ = [("n_records", c_i64), ("num_samples", c_i64), ("max_hops", c_i64),
-                ("preprocessing_applied", c_i32), ("task_type", ctypes.c_char * 32)]
+                ("preprocessing_applied", c_i32), ("task_type", ctypes.c_char * 32), ("direct_read", c_i32)]
 
 
 _lib = None
@@ -160,6 +160,7 @@ class H5File:
         self.max_hops = int(info.max_hops)
         self.preprocessing_applied = bool(info.preprocessing_applied)
         self.task_type = info.task_type.decode()
+        self.direct_read = bool(info.direct_read)
         self._mtx = threading.Lock()  # one read at a time per handle
 
     def read_store(self, positions, n_hops, n_tasks=1, threads=4):

@@ -6,15 +6,20 @@
 // these as ~2 elementwise launches per parameter tensor (plus foreach norm kernels): hundreds of
 // 3-5 us launches per step for this model. Here:
 //   1. k_adam_sumsq   : per-(tensor, slice) partial sums of g^2 (fp64)  -> workspace
-//      (its last-arriving workgroup: total norm, clip coefficient — the former k_adam_scalars)
 // (each tensor's own step counter, torch.optim.Adam's per-parameter state['step'], is advanced by
 // the first workgroup of that tensor in launch 1 and read by launch 3 for its bias corrections:
 // a parameter without a gradient in a step keeps its count, as in torch)
+//   2. k_adam_fold    : one workgroup folds the partials in a fixed order: total norm, clip
+//                       coefficient (no arrival atomics: deterministic, no serialised tail)
 //   3. k_adam_update  : g *= coef (in place, as clip_grad_norm_ leaves it), [g += wd * p],
 //                       m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
 //                       p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // The tensor table travels in the kernel arguments (chunks of kAdamChunk tensors), so nothing is
 // copied host->device and the three launches capture into a HIP graph as plain kernel nodes. The
+// sum-of-squares slice (one workgroup) is 2048 elements or more, sized so a call makes about
+// kTargetSlices partials (c5's ~15M parameters: 16384-element slices, ~1,000 partials instead of
+// 7,284, each of which used to end in an atomic arrival on one counter: a serialised ~80 us tail);
+// the update keeps 2048-element slices (many workgroups: it moves 8 bytes per byte the sum reads). The
 // step counter and the per-group learning rates live in device memory (capturable).
 #include <algorithm>
 #include <cmath>
@@ -29,7 +34,8 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int kAdamChunk = 80;        // tensors per launch (kernel-argument table, < 4 KiB: a
                                       // reference GNN's ~75 parameters take one launch each way)
 constexpr int kAdamThreads = 256;
-constexpr int64_t kSliceElems = 2048; // elements per workgroup slice (8 per thread, loads unrolled)
+constexpr int64_t kSliceElems = 2048; // smallest workgroup slice (8 elements per thread)
+constexpr int64_t kTargetSlices = 1536;  // about this many slices per call (>> 256 CUs)
 
 struct AdamTable {
   int32_t n;
@@ -49,19 +55,34 @@ __device__ __forceinline__ int find_tensor(const AdamTable& t, int b) {
   return i;
 }
 
-// The clip coefficient from every slice's partial sum of squares (read in the order k_adam_scalars
-// read them: lane j sums partials j, j + 64, ... then a butterfly), by ONE wave.
-template <bool SC1>
-__device__ __forceinline__ void adam_scalars_wave(const double* partial, int64_t n_partial, float max_norm,
-                                                  float* scal, float* norm_out) {
-  const int lane = threadIdx.x & 63;
+// Launch 2: the clip coefficient from every slice's partial sum of squares, by one workgroup:
+// thread t sums partials t, t + 256, ... in that order with 8 loads in flight, then the threads'
+// sums are combined in a fixed order. Deterministic: the same bits every call.
+// scal[0] = clip coefficient, scal[3] = total gradient norm (the value clip_grad_norm_ returns)
+__global__ __launch_bounds__(kAdamThreads) void k_adam_fold(const double* __restrict__ partial, int64_t n_partial,
+                                                            float max_norm, float* __restrict__ scal,
+                                                            float* __restrict__ norm_out) {
+  constexpr int kInFlight = 8;
+  __shared__ double red[kAdamThreads / kWave];
   double s = 0.0;
-  for (int64_t j = lane; j < n_partial; j += 64)
-    s += SC1 ? __hip_atomic_load(partial + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : partial[j];
+  for (int64_t j0 = threadIdx.x; j0 < n_partial; j0 += (int64_t)kInFlight * kAdamThreads) {
+    double v[kInFlight];
+#pragma unroll
+    for (int q = 0; q < kInFlight; ++q) {
+      const int64_t j = j0 + (int64_t)q * kAdamThreads;
+      v[q] = j < n_partial ? partial[j] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kInFlight; ++q) s += v[q];
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (lane == 0) {
-    const float total = (float)sqrt(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kAdamThreads / kWave; ++w) t += red[w];
+    const float total = (float)sqrt(t);
     float coef = 1.f;
     if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
     scal[0] = coef;
@@ -70,24 +91,21 @@ __device__ __forceinline__ void adam_scalars_wave(const double* partial, int64_t
   }
 }
 
-// Launch 1. The partial of each slice is stored device-coherent (sc1) and the workgroup then
-// arrives on a self-resetting counter (MI355X_MICROARCH.md "Valid forms", row 1: drained sc1
-// stores -> barrier -> one relaxed agent-scope add); the last of all `total` workgroups (over
-// every chunk launch) computes the clip coefficient itself, so there is no separate scalars launch.
+// Launch 1: the partial sum of squares of each slice (fp64; the first workgroup of each tensor
+// advances that tensor's step counter).
 __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, double* __restrict__ partial,
-                                                             float* __restrict__ steps, int64_t base, int64_t total,
-                                                             int32_t* __restrict__ arrive, float max_norm,
-                                                             float* __restrict__ scal, float* __restrict__ norm_out) {
+                                                             float* __restrict__ steps, int64_t base,
+                                                             int64_t slice) {
   const int i = find_tensor(t, blockIdx.x);
   if (blockIdx.x == t.blk0[i] && threadIdx.x == 0) steps[t.gs[i] >> 8] += 1.f;
-  const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
-  const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
+  const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * slice;
+  const int64_t s1 = min(t.numel[i], s0 + slice);
   const float* __restrict__ g = t.grad[i];
   double acc = 0.0;
   int64_t j0 = s0;
   if ((((uintptr_t)g) & 15) == 0) {  // 16-byte loads (same fp64 sums, per-thread order changes)
     const int64_t q1 = s0 + ((s1 - s0) & ~(int64_t)3);
-#pragma unroll 2
+#pragma unroll 4
     for (int64_t j = s0 + 4 * threadIdx.x; j < q1; j += 4 * kAdamThreads) {
       const floatx4 x = *reinterpret_cast<const floatx4*>(g + j);
 #pragma unroll
@@ -105,31 +123,24 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, 
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  __shared__ int last;
   if (threadIdx.x == 0) {
     double s = 0.0;
     for (int w = 0; w < kAdamThreads / kWave; ++w) s += red[w];
-    __hip_atomic_store(partial + base + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (old == (int)(total - 1));
-    if (last) __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+    partial[base + blockIdx.x] = s;
   }
-  __syncthreads();
-  if (last && threadIdx.x < 64) adam_scalars_wave<true>(partial, total, max_norm, scal, norm_out);
 }
 
-// scal[0] = clip coefficient, scal[3] = total gradient norm (the value clip_grad_norm_ returns)
-
+// Launch 3.
 __global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t, const float* __restrict__ scal,
-                                                              const float* __restrict__ steps,
+                                                              int64_t slice, const float* __restrict__ steps,
                                                               const float* __restrict__ lr, float beta1, float omb1,
                                                               float beta2, float omb2, float eps, float wd) {
+  const float coef = scal[0];
   const int i = find_tensor(t, blockIdx.x);
-  const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * kSliceElems;
-  const int64_t s1 = min(t.numel[i], s0 + kSliceElems);
+  const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * slice;
+  const int64_t s1 = min(t.numel[i], s0 + slice);
   const float st = steps[t.gs[i] >> 8];
-  const float coef = scal[0], inv_bc1 = 1.f / (1.f - powf(beta1, st)), bc2s = sqrtf(1.f - powf(beta2, st));
+  const float inv_bc1 = 1.f / (1.f - powf(beta1, st)), bc2s = sqrtf(1.f - powf(beta2, st));
   const float step_size = lr[t.gs[i] & 255] * inv_bc1;
   float* __restrict__ p = t.param[i];
   float* __restrict__ g = t.grad[i];
@@ -176,7 +187,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t,
   for (int64_t j = j0 + threadIdx.x; j < s1; j += kAdamThreads) upd(g[j], p[j], m[j], v[j]);
 }
 
-int64_t blocks_of(int64_t numel) { return std::max<int64_t>(1, cdiv(numel, kSliceElems)); }
+int64_t blocks_of(int64_t numel, int64_t slice = kSliceElems) { return std::max<int64_t>(1, cdiv(numel, slice)); }
 
 }  // namespace
 }  // namespace aimx
@@ -205,16 +216,21 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
     for (int32_t k = 0; k < i; ++k)  // each counter advanced once per call
       if (tensors[k].step_slot == x.step_slot) return AIMX_EARG;
   }
-  // workspace: [arrival counter (8 B, zero before the first call, left zero)] [partials] [scalars];
-  // the counter's place is fixed whatever the table size, so a table that shrinks between calls
-  // never finds a stale partial where its counter should be
-  int32_t* arrive = (int32_t*)workspace;
+  // workspace: [8 B, unused (the former arrival counter; keeps the partials' place)] [partials]
+  // [scalars]; the partials fit: a slice is never smaller than kSliceElems
   double* partial = (double*)workspace + 1;
-  int64_t total_blocks = 0;
-  for (int32_t i = 0; i < n; ++i) total_blocks += blocks_of(tensors[i].numel);
-  float* scal = (float*)(partial + total_blocks);
-  // chunk tables (host, by value into the kernel arguments)
-  auto for_chunks = [&](auto&& launch) -> int {
+  int64_t elems = 0;
+  for (int32_t i = 0; i < n; ++i) elems += tensors[i].numel;
+  int64_t slice = kSliceElems;
+  while (slice < (int64_t(1) << 24) && elems > slice * kTargetSlices) slice *= 2;
+  int64_t total_blocks = 0, max_blocks = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    total_blocks += blocks_of(tensors[i].numel, slice);
+    max_blocks += blocks_of(tensors[i].numel);
+  }
+  float* scal = (float*)(partial + max_blocks);
+  // chunk tables (host, by value into the kernel arguments), workgroups of `sl` elements
+  auto for_chunks = [&](int64_t sl, auto&& launch) -> int {
     int64_t blk = 0;
     for (int32_t c0 = 0; c0 < n; c0 += kAdamChunk) {
       AdamTable t{};
@@ -229,7 +245,7 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
         t.grad[k] = x.grad;
         t.m[k] = x.exp_avg;
         t.v[k] = x.exp_avg_sq;
-        b += (int32_t)blocks_of(x.numel);
+        b += (int32_t)blocks_of(x.numel, sl);
       }
       t.blk0[t.n] = b;
       const int rc = launch(t, b, blk);
@@ -238,17 +254,19 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
     }
     return AIMX_OK;
   };
-  int rc = for_chunks([&](const AdamTable& t, int32_t nb, int64_t blk) -> int {
-    hipLaunchKernelGGL(k_adam_sumsq, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, partial, step, blk,
-                       total_blocks, arrive, h->max_grad_norm, scal, norm_out);
+  int rc = for_chunks(slice, [&](const AdamTable& t, int32_t nb, int64_t blk) -> int {
+    hipLaunchKernelGGL(k_adam_sumsq, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, partial, step, blk, slice);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   });
   if (rc) return rc;
-  return for_chunks([&](const AdamTable& t, int32_t nb, int64_t) -> int {
+  hipLaunchKernelGGL(k_adam_fold, dim3(1), dim3(kAdamThreads), 0, s, (const double*)partial, total_blocks,
+                     h->max_grad_norm, scal, norm_out);
+  AIMX_CHECK_LAUNCH();
+  return for_chunks(kSliceElems, [&](const AdamTable& t, int32_t nb, int64_t) -> int {
     hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal,
-                       (const float*)step, lr, h->beta1, h->one_minus_beta1, h->beta2, h->one_minus_beta2, h->eps,
-                       h->weight_decay);
+                       kSliceElems, (const float*)step, lr, h->beta1, h->one_minus_beta1, h->beta2,
+                       h->one_minus_beta2, h->eps, h->weight_decay);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   });

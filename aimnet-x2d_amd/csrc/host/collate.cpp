@@ -211,6 +211,7 @@ struct aimx_collator {
   std::vector<int32_t> mol_worker;
   int64_t G = 0, N = 0, E = 0;
   bool planned = false;
+  std::vector<int32_t> csr_next_f, csr_next_b;  // aimx_collate_csr row cursors
   aimx_collator(int32_t h, int32_t t) : max_hops(h), pool(t), scratch(pool.size()), wpairs(pool.size()) {}
 };
 
@@ -363,6 +364,12 @@ int64_t aimx_store_num_molecules(const aimx_mol_store* s) { return s ? s->n_mols
 int64_t aimx_store_num_atoms(const aimx_mol_store* s, int64_t m) {
   if (!s || m < 0 || m >= s->n_mols) return AIMX_HOST_EARG;
   return s->atom_ptr[m + 1] - s->atom_ptr[m];
+}
+
+int aimx_store_atom_counts(const aimx_mol_store* s, int64_t* out) {
+  if (!s || (s->n_mols > 0 && !out)) return AIMX_HOST_EARG;
+  for (int64_t m = 0; m < s->n_mols; ++m) out[m] = s->atom_ptr[m + 1] - s->atom_ptr[m];
+  return AIMX_HOST_OK;
 }
 
 int aimx_collator_create(int32_t max_hops, int32_t n_threads, aimx_collator** out) {
@@ -556,11 +563,108 @@ extern "C" int aimx_csr_host_build(const int64_t* edges, int64_t E, const int64_
   for (int64_t i = 0; i < N; ++i)
     if (batch[i] < 0 || batch[i] >= G) return AIMX_HOST_EARG;
   try {
-    auto src = [&](int64_t i) { return int32_t(((edges[2 * i + 1] % N) + N) % N); };
+    auto src = [&](int64_t i) {
+      const int64_t x = edges[2 * i + 1];
+      return int32_t(x >= 0 && x < N ? x : ((x % N) + N) % N);
+    };
     counting_csr(E, HN, [&](int64_t i) { return edges[2 * i]; }, src, fwd_rowptr, fwd_col);
     counting_csr(E, N, src, [&](int64_t i) { return int32_t(edges[2 * i]); }, bwd_rowptr, bwd_col);
     counting_csr(N, G, [&](int64_t i) { return batch[i]; }, [](int64_t i) { return int32_t(i); }, graph_rowptr,
                  graph_col);
+  } catch (const std::bad_alloc&) {
+    return AIMX_HOST_ENOMEM;
+  }
+  return AIMX_HOST_OK;
+}
+
+// The same three CSRs for the batch this collator has just written (aimx_collate_write), built by
+// its worker pool: a molecule's edges (edge_off[g] .. edge_off[g+1]) join only its own atoms, so
+// the rows each worker counts and fills are its molecules' own and the order inside a row (edge
+// order) is kept without a global sort. The slack edges past the planned ones (padding self
+// loops) are counted and placed on the calling thread, after the molecules' (their order). Input
+// that does not have this shape goes to the serial aimx_csr_host_build: identical results.
+extern "C" int aimx_collate_csr(aimx_collator* c, const int64_t* edges, int64_t E, const int64_t* batch, int64_t N,
+                                int64_t G, int32_t hops, int32_t* fwd_rowptr, int32_t* fwd_col, int32_t* bwd_rowptr,
+                                int32_t* bwd_col, int32_t* graph_rowptr, int32_t* graph_col) {
+  auto serial = [&] {
+    return aimx_csr_host_build(edges, E, batch, N, G, hops, fwd_rowptr, fwd_col, bwd_rowptr, bwd_col, graph_rowptr,
+                               graph_col);
+  };
+  const int64_t lim = int64_t(1) << 31;
+  if (!c || !c->planned || E < c->E || N < c->N || G < c->G || E <= 0 || N <= 0 || hops < 1 || E >= lim ||
+      G >= lim || int64_t(hops) * N >= lim || !edges || !batch || !fwd_rowptr || !fwd_col || !bwd_rowptr ||
+      !bwd_col || !graph_rowptr || !graph_col)
+    return serial();
+  const int P = c->pool.size();
+  const int64_t HN = int64_t(hops) * N, G0 = c->G, N0 = c->N, E0 = c->E;
+  try {
+    std::atomic<bool> shaped{true};
+    // zero the count arrays, check the molecules' locality and batch order, count their rows
+    c->pool.run([&](int w) {
+      int64_t lo, hi;
+      split_range(HN + 1, P, w, &lo, &hi);
+      std::fill(fwd_rowptr + lo, fwd_rowptr + hi, 0);
+      split_range(N + 1, P, w, &lo, &hi);
+      std::fill(bwd_rowptr + lo, bwd_rowptr + hi, 0);
+    });
+    c->pool.run([&](int w) {
+      int64_t lo, hi;
+      split_range(N, P, w, &lo, &hi);
+      for (int64_t i = lo; i < hi; ++i)
+        if (batch[i] < 0 || batch[i] >= G || (i > 0 && batch[i] < batch[i - 1])) {
+          shaped = false;
+          return;
+        }
+      split_range(G0, P, w, &lo, &hi);
+      for (int64_t g = lo; g < hi; ++g) {
+        const int64_t a0 = c->atom_off[g], a1 = c->atom_off[g + 1];
+        for (int64_t i = c->edge_off[g]; i < c->edge_off[g + 1]; ++i) {
+          const int64_t t = edges[2 * i], u = edges[2 * i + 1];
+          if (t < a0 || t >= a1 || u < a0 || u >= a1) {
+            shaped = false;
+            return;
+          }
+          ++fwd_rowptr[t + 1];
+          ++bwd_rowptr[u + 1];
+        }
+      }
+    });
+    if (shaped)
+      for (int64_t i = E0; i < E; ++i) {
+        const int64_t t = edges[2 * i], u = edges[2 * i + 1];
+        if (t < N0 || t >= N || u < N0 || u >= N) {
+          shaped = false;
+          break;
+        }
+        ++fwd_rowptr[t + 1];
+        ++bwd_rowptr[u + 1];
+      }
+    if (!shaped) return serial();
+    for (int64_t r = 0; r < HN; ++r) fwd_rowptr[r + 1] += fwd_rowptr[r];
+    for (int64_t r = 0; r < N; ++r) bwd_rowptr[r + 1] += bwd_rowptr[r];
+    c->csr_next_f.assign(fwd_rowptr, fwd_rowptr + N);  // rows >= N (hop offsets) hold no item here
+    c->csr_next_b.assign(bwd_rowptr, bwd_rowptr + N);
+    int32_t* nf = c->csr_next_f.data();
+    int32_t* nb = c->csr_next_b.data();
+    c->pool.run([&](int w) {
+      int64_t lo, hi;
+      split_range(G0, P, w, &lo, &hi);
+      for (int64_t i = lo < hi ? c->edge_off[lo] : 0; i < (lo < hi ? c->edge_off[hi] : 0); ++i) {
+        const int64_t t = edges[2 * i], u = edges[2 * i + 1];
+        fwd_col[nf[t]++] = int32_t(u);
+        bwd_col[nb[u]++] = int32_t(t);
+      }
+    });
+    for (int64_t i = E0; i < E; ++i) {
+      const int64_t t = edges[2 * i], u = edges[2 * i + 1];
+      fwd_col[nf[t]++] = int32_t(u);
+      bwd_col[nb[u]++] = int32_t(t);
+    }
+    // graph CSR: batch is non-decreasing, so the stable order is the identity
+    std::fill(graph_rowptr, graph_rowptr + G + 1, 0);
+    for (int64_t i = 0; i < N; ++i) ++graph_rowptr[batch[i] + 1];
+    for (int64_t g = 0; g < G; ++g) graph_rowptr[g + 1] += graph_rowptr[g];
+    for (int64_t i = 0; i < N; ++i) graph_col[i] = int32_t(i);
   } catch (const std::bad_alloc&) {
     return AIMX_HOST_ENOMEM;
   }

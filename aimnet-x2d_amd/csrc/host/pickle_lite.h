@@ -16,6 +16,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <vector>
 
 namespace aimx_pickle {
@@ -23,27 +24,38 @@ namespace aimx_pickle {
 enum class Kind { None, Bool, Int, Float, Str, Bytes, List, Tuple, Dict, Global, Dtype, Array, Mark };
 
 struct Obj;
-using Ref = std::shared_ptr<Obj>;
+// Objects live in the Decoder's arena (reused record after record: no allocation once warm) and
+// stay valid until its next decode(); strings and payloads are views into the pickle's bytes.
+using Ref = Obj*;
 
 struct Obj {
   Kind k = Kind::None;
   int64_t i = 0;
   double f = 0.0;
-  std::string s;           // Str / Bytes / Global ("module\nname") / Dtype descr ("i8", "f4", ...)
+  // Str / Bytes / Global ("module\nname") / Dtype descr ("i8", "f4", ...): sp[0..sn), a view into
+  // the pickle or into `own` (strings the decoder built: globals, latin-1 bytes)
+  const char* sp = nullptr;
+  size_t sn = 0;
+  std::string own;
   char order = '<';        // Dtype byte order
   std::vector<Ref> items;  // List / Tuple; Dict: key, value, key, value, ...
   // Array
   std::string dtype;
   std::vector<int64_t> shape;
   bool fortran = false;
-  Ref raw;  // the Bytes object holding the array payload (shared, not copied)
-  const char* bytes() const { return raw ? raw->s.data() : nullptr; }
-  int64_t nbytes() const { return raw ? (int64_t)raw->s.size() : 0; }
+  Ref raw = nullptr;  // the Bytes object holding the array payload (not copied)
+  std::string_view s() const { return std::string_view(sp ? sp : "", sn); }
+  void set_own() {
+    sp = own.data();
+    sn = own.size();
+  }
+  const char* bytes() const { return raw ? raw->sp : nullptr; }
+  int64_t nbytes() const { return raw ? (int64_t)raw->sn : 0; }
 
   const Obj* get(const char* key) const {  // Dict lookup by str key
     if (k != Kind::Dict) return nullptr;
     for (size_t j = 0; j + 1 < items.size(); j += 2)
-      if (items[j]->k == Kind::Str && items[j]->s == key) return items[j + 1].get();
+      if (items[j]->k == Kind::Str && items[j]->s() == key) return items[j + 1];
     return nullptr;
   }
   int64_t numel() const {
@@ -168,6 +180,7 @@ class Decoder {
   Ref decode(const uint8_t* p, size_t n, std::string* err) {
     p_ = p;
     end_ = p + n;
+    used_ = 0;
     st_.clear();
     marks_.clear();
     memo_.clear();
@@ -189,6 +202,8 @@ class Decoder {
   std::vector<size_t> marks_;
   std::vector<Ref> memo_;
   std::string msg_;
+  std::vector<std::unique_ptr<Obj>> arena_;
+  size_t used_ = 0;
 
   Ref fail(std::string* err, const std::string& m) {
     if (err) *err = m;
@@ -202,15 +217,28 @@ class Decoder {
     p_ += sizeof(T);
     return true;
   }
-  static Ref mk(Kind k) {
-    auto o = std::make_shared<Obj>();
+  Ref mk(Kind k) {
+    if (used_ == arena_.size()) arena_.push_back(std::make_unique<Obj>());
+    Obj* o = arena_[used_++].get();
     o->k = k;
+    o->i = 0;
+    o->f = 0.0;
+    o->sp = nullptr;
+    o->sn = 0;
+    o->own.clear();
+    o->order = '<';
+    o->items.clear();
+    o->dtype.clear();
+    o->shape.clear();
+    o->fortran = false;
+    o->raw = nullptr;
     return o;
   }
   bool push_str(Kind k, size_t len) {
     if (!need(len)) return false;
     auto o = mk(k);
-    o->s.assign((const char*)p_, len);
+    o->sp = (const char*)p_;
+    o->sn = len;
     p_ += len;
     st_.push_back(o);
     return true;
@@ -238,7 +266,7 @@ class Decoder {
     return true;
   }
   static bool is_global(const Ref& fn, const char* np_sub, const char* name) {  // numpy[._core|.core].<sub>\n<name>
-    const std::string& g = fn->s;
+    const std::string_view g = fn->s();
     for (const char* pre : {"numpy._core.", "numpy.core."}) {
       const size_t lp = std::strlen(pre), ls = std::strlen(np_sub), ln = std::strlen(name);
       if (g.size() == lp + ls + 1 + ln && g.compare(0, lp, pre) == 0 && g.compare(lp, ls, np_sub) == 0 &&
@@ -253,32 +281,34 @@ class Decoder {
       st_.push_back(mk(Kind::Array));
       return true;
     }
-    const std::string& g = fn->s;
+    const std::string_view g = fn->s();
     if (g == "_codecs\nencode") {  // protocol <= 2 bytes: _codecs.encode(str, 'latin1')
       if (args->items.size() != 2 || args->items[0]->k != Kind::Str || args->items[1]->k != Kind::Str ||
-          (args->items[1]->s != "latin1" && args->items[1]->s != "latin-1"))
+          (args->items[1]->s() != "latin1" && args->items[1]->s() != "latin-1"))
         return err("_codecs.encode args");
       auto b = mk(Kind::Bytes);
-      const std::string& u = args->items[0]->s;  // UTF-8 of code points < 256
+      const std::string_view u = args->items[0]->s();  // UTF-8 of code points < 256
       for (size_t j = 0; j < u.size(); ++j) {
         const unsigned char c = (unsigned char)u[j];
         if (c < 0x80) {
-          b->s.push_back((char)c);
+          b->own.push_back((char)c);
         } else if ((c & 0xE0) == 0xC0 && j + 1 < u.size() && c <= 0xC3) {
-          b->s.push_back((char)(((c & 0x1F) << 6) | ((unsigned char)u[j + 1] & 0x3F)));
+          b->own.push_back((char)(((c & 0x1F) << 6) | ((unsigned char)u[j + 1] & 0x3F)));
           ++j;
         } else {
           return err("_codecs.encode: not latin-1");
         }
       }
+      b->set_own();
       st_.push_back(b);
       return true;
     }
     if (g == "numpy\ndtype") {
       if (args->items.empty() || args->items[0]->k != Kind::Str) return err("numpy.dtype args");
       auto d = mk(Kind::Dtype);
-      d->s = args->items[0]->s;
-      d->order = d->s == "i1" || d->s == "u1" || d->s == "b1" ? '|' : '<';
+      d->sp = args->items[0]->sp;
+      d->sn = args->items[0]->sn;
+      d->order = d->s() == "i1" || d->s() == "u1" || d->s() == "b1" ? '|' : '<';
       st_.push_back(d);
       return true;
     }
@@ -286,7 +316,7 @@ class Decoder {
       if (args->items.size() < 2 || args->items[0]->k != Kind::Dtype || args->items[1]->k != Kind::Bytes)
         return err("numpy scalar args");
       auto a = mk(Kind::Array);
-      a->dtype = args->items[0]->s;
+      a->dtype = std::string(args->items[0]->s());
       a->order = args->items[0]->order;
       a->raw = args->items[1];
       if (!size_ok(*a)) return false;
@@ -299,29 +329,29 @@ class Decoder {
         return err("_frombuffer args");
       auto a = mk(Kind::Array);
       a->raw = args->items[0];
-      a->dtype = args->items[1]->s;
+      a->dtype = std::string(args->items[1]->s());
       a->order = args->items[1]->order;
-      if (!set_shape(a.get(), args->items[2])) return false;
-      a->fortran = args->items[3]->k == Kind::Str && args->items[3]->s == "F";
+      if (!set_shape(a, args->items[2])) return false;
+      a->fortran = args->items[3]->k == Kind::Str && args->items[3]->s() == "F";
       if (!size_ok(*a)) return false;
       st_.push_back(a);
       return true;
     }
-    return err("global not allowed: " + g);
+    return err("global not allowed: " + std::string(g));
   }
   bool build(const Ref& obj, const Ref& state) {
     if (obj->k == Kind::Dtype) {  // (version, byteorder, ...)
       if (state->k == Kind::Tuple && state->items.size() >= 2 && state->items[1]->k == Kind::Str &&
-          !state->items[1]->s.empty())
-        obj->order = state->items[1]->s[0];
+          state->items[1]->sn > 0)
+        obj->order = state->items[1]->sp[0];
       return true;
     }
     if (obj->k == Kind::Array) {  // (version, shape, dtype, is_fortran, raw bytes)
       if (state->k != Kind::Tuple || state->items.size() < 5) return err("ndarray state");
       const auto& it = state->items;
       if (it[1]->k != Kind::Tuple || it[2]->k != Kind::Dtype || it[4]->k != Kind::Bytes) return err("ndarray state types");
-      if (!set_shape(obj.get(), it[1])) return false;
-      obj->dtype = it[2]->s;
+      if (!set_shape(obj, it[1])) return false;
+      obj->dtype = std::string(it[2]->s());
       obj->order = it[2]->order;
       obj->fortran = it[3]->k == Kind::Bool && it[3]->i;
       obj->raw = it[4];
@@ -512,7 +542,10 @@ class Decoder {
       case 0x93:  // STACK_GLOBAL
         if (!pop(&b) || !pop(&a) || a->k != Kind::Str || b->k != Kind::Str) return false;
         c = mk(Kind::Global);
-        c->s = a->s + "\n" + b->s;
+        c->own.assign(a->sp ? a->sp : "", a->sn);
+        c->own.push_back('\n');
+        c->own.append(b->sp ? b->sp : "", b->sn);
+        c->set_own();
         st_.push_back(c);
         return true;
       case 'c': {  // GLOBAL "module\nname\n"
@@ -521,7 +554,8 @@ class Decoder {
         while (q < end_ && nl < 2) nl += (*q++ == '\n');
         if (nl < 2) return false;
         c = mk(Kind::Global);
-        c->s.assign((const char*)p_, q - p_ - 1);
+        c->sp = (const char*)p_;
+        c->sn = size_t(q - p_ - 1);
         p_ = q;
         st_.push_back(c);
         return true;

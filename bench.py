@@ -115,6 +115,9 @@ def native_feeder(cfg, seed, device, threads, pad):
                                  n_max=n_max, e_max=e_max, pad_mols=PAD_MOLS if pad else 0))
 
 
+STREAM_INFO = {}
+
+
 def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None):
     """Endless BatchFeeder over an HDF5 molecule stream in the reference's dataset format
     (features.py:381-431 / molecular.py:102-329): a synthetic file of n_mols molecules (made once
@@ -124,17 +127,27 @@ def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None):
     from aimx import feed, h5
     path = path or os.path.join(os.environ.get("TMPDIR", "/tmp"),
                                 f"aimx_stream_{cfg['source']}_{cfg['hops']}h_{cfg['tasks']}t_{n_mols}.h5")
+    info = {"path": path, "molecules": n_mols}
     if rank == 0 and not os.path.exists(path):
         t0 = time.perf_counter()
         tmp = path + f".part{os.getpid()}"
         h5.make_synthetic_stream(tmp, n_mols, cfg["source"], cfg["hops"], cfg["tasks"], seed=0,
                                  workers=min(16, os.cpu_count() or 4))
         os.replace(tmp, path)
-        print(f"bench: wrote {n_mols}-molecule stream {path} in {time.perf_counter() - t0:.1f} s", file=sys.stderr)
+        info["write_s"] = round(time.perf_counter() - t0, 1)
+        print(f"bench: wrote {n_mols}-molecule stream {path} in {info['write_s']} s", file=sys.stderr)
     if world > 1:
         dist.barrier()
     stream = h5.HDF5MolecularStream(path, shuffle=True, ddp_enabled=world > 1, rank=rank, world_size=world,
                                     n_hops=cfg["hops"], n_tasks=cfg["tasks"], threads=threads)
+    # the reader's own rate (shuffled positions, the feed's threads): read + decode + pack into stores
+    pos = stream.positions(0)[:65536]
+    t0 = time.perf_counter()
+    for s0 in range(0, len(pos), 16384):
+        stream.file.read_store(pos[s0:s0 + 16384], cfg["hops"], cfg["tasks"], threads)
+    info.update(bytes=os.path.getsize(path), direct_read=stream.file.direct_read,
+                read_mol_per_s=round(len(pos) / (time.perf_counter() - t0)), read_threads=threads)
+    STREAM_INFO.update(info)
     B = cfg["batch"]
     n_max = e_max = 0
     if pad:  # static capacity from the first chunk's batches + margin (an overflow raises HostError)
@@ -396,15 +409,20 @@ def cpu_info():
     return model, os.cpu_count(), affinity
 
 
-def cpu_baseline(cfg, seconds=10.0, max_steps=40, one_thread_seconds=6.0):
+def cpu_baseline(cfg, seconds=10.0, max_steps=40, one_thread_seconds=6.0, all_cores_seconds=6.0):
     """Oracle CPU restatement of the reference train step (fwd+bwd+clip+Adam, dropout on): on the
-    box's CPU share (min(16, cpu_count) threads) and on 1 thread (BASELINE.md CPU-baseline plan);
-    the port/reference ratio comes from profiles/port_vs_reference.json (the reference itself only
-    runs in the development container)."""
+    box's CPU share (min(16, cpu_count) threads, `value`), on torch.set_num_threads(os.cpu_count())
+    and on 1 thread (BASELINE.md CPU-baseline plan item 3); the port/reference ratio comes from
+    profiles/port_vs_reference.json (the reference itself only runs in the development container)."""
     threads = min(16, os.cpu_count() or 1)
     res = _cpu_rate(cfg, threads, seconds, max_steps)
     res1 = _cpu_rate(cfg, 1, one_thread_seconds, 8)
     model, count, affinity = cpu_info()
+    if (count or 1) != threads:
+        resa = _cpu_rate(cfg, count or 1, all_cores_seconds, 10)
+        res.update({"value_all_cores": resa["value"], "sample_all_cores": resa["sample"],
+                    "note_all_cores": f"torch.set_num_threads(os.cpu_count() = {count}) on a box process whose "
+                                      f"CPU affinity holds {affinity} CPUs"})
     res.update({"value_1thread": res1["value"], "sample_1thread": res1["sample"], "cpu_model": model,
                 "cpu_count": count, "cpu_affinity": affinity})
     pvr = os.path.join(ROOT, "profiles", "port_vs_reference.json")
@@ -458,7 +476,8 @@ def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False
     from models import L1Loss
     model = build_model(cfg, device)
     from aimx import autograph as ag
-    ag.enable(model, autograph)
+    if not autograph:
+        ag.enable(model, False)  # autograph=True: the default drop-in behaviour (size-gated replay)
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
     loss_fn = L1Loss()
     bs = make_batches(cfg, batches_eager, 777, device, pad=False)
@@ -477,12 +496,15 @@ def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False
         step(i)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    replayed = bool(autograph and ag.wanted(model.train(), bs[0].model_args()))
     del model, opt, bs
     torch.cuda.empty_cache()
     return {"value": round(cfg["batch"] * steps / dt, 1), "unit": "molecules/s", "ms_per_step": round(dt / steps * 1e3, 4),
             "steps": steps, "warmup": warmup,
-            "mode": ("eager loop as the unchanged trainer runs it; the model's forward/backward replayed per "
-                     "shape bucket by aimx.autograph (the default), unpadded batches, same step") if autograph else
+            "mode": ("eager loop as the unchanged trainer runs it, the default drop-in behaviour: the model's "
+                     "forward/backward replayed per shape bucket by aimx.autograph when atoms x hidden <= "
+                     f"{ag.MAX_WORK} (here: {'replayed' if replayed else 'eager launches'}), unpadded batches, "
+                     "same step") if autograph else
             "eager, every operator launched from Python (AIMX_AUTOGRAPH=0), unpadded batches, same step"}
 
 
@@ -507,7 +529,7 @@ def main():
                          "prefetch thread (this rank's equal shard)")
     ap.add_argument("--stream-mols", type=int, default=200_000, help="molecules in the --feed stream file")
     ap.add_argument("--stream-path", default=None, help="--feed stream file (default: generated under $TMPDIR)")
-    ap.add_argument("--feed-threads", type=int, default=4)
+    ap.add_argument("--feed-threads", type=int, default=8)
     ap.add_argument("--amp", action="store_true",
                     help="the reference's --mixed_precision path (trainer.py:134): the step runs under "
                          "torch.autocast('cuda', bfloat16) -> bf16 MFMA operands, fp32 accumulation in the GEMMs")
@@ -600,6 +622,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if feeder is not None:
+        feeder.reset_stats()  # the feed's per-stage times over the timed steps only
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
@@ -611,7 +635,9 @@ def main():
         t = torch.tensor([dt], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    feed_stats = None
     if feeder is not None:
+        feed_stats = feeder.stats()
         feeder.close()
     ddp_check = None
     if sync is not None:
@@ -695,6 +721,10 @@ def main():
             line.update(extra)
         if eager is not None:
             line["eager"] = eager
+        if feed_stats is not None:
+            line["feed_ms_per_batch"] = feed_stats
+        if STREAM_INFO:
+            line["stream_file"] = dict(STREAM_INFO)
         if sync is not None:
             line["ddp"] = {"world_size_reported": dist.get_world_size(), "backend": dist.get_backend(),
                            "graph_mode": graphed.mode if graphed is not None else "eager",

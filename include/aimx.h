@@ -337,7 +337,8 @@ int aimx_wgrad_grouped(const AimxWgradProblem* problems, int32_t n, void* worksp
                        int32_t* counters, int64_t n_counters, aimx_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
- * Fused global-norm gradient clip + Adam step over a list of fp32 tensors (three launches).
+ * Fused global-norm gradient clip + Adam step over a list of fp32 tensors (sum of squares and
+ * update: one launch each per chunk of 80 tensors; one fold launch between them).
  * Replaces the trainer's  torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0);
  * optimizer.step()  with optimizer = torch.optim.Adam(...) (reference
  * src/training/trainer.py:163-164 and 221-223):
@@ -351,10 +352,9 @@ int aimx_wgrad_grouped(const AimxWgradProblem* problems, int32_t n, void* worksp
  * parameter left out of a step (no gradient) keeps its count, as in torch. `step` and `lr` (one
  * float per parameter group, group < 256) are device memory, so the call is graph-capturable and
  * schedulers update lr without re-capture. *norm_out (nullable, device) receives the total norm
- * clip_grad_norm_ returns. The workspace (aimx_fused_adam_workspace_bytes) must be ZERO-filled
- * before its first use and is then reused as is: one of its words is a self-resetting arrival
- * counter (the launch that sums the squares also forms the clip coefficient, in its last
- * workgroup), which every call leaves zero.
+ * clip_grad_norm_ returns. The workspace (aimx_fused_adam_workspace_bytes) holds the per-slice
+ * partial sums of squares, folded by one workgroup in a fixed order into the clip coefficient
+ * (deterministic, no arrival counter; zero-filling it is harmless, not needed).
  * ------------------------------------------------------------------------------------------ */
 typedef struct {
   float* param;

@@ -30,6 +30,8 @@ typedef struct AimxH5Info {
   int64_t max_hops;              /* metadata attr (-1 when absent) */
   int32_t preprocessing_applied; /* metadata attr, else metadata/sae attr 'applied' (molecular.py:159-174) */
   char task_type[32];            /* metadata attr ("" when absent) */
+  int32_t direct_read;           /* reader: 1 = records come straight from the memory-mapped file
+                                    (contiguous /data, checked against H5Dread at open), 0 = H5Dread */
 } AimxH5Info;
 
 typedef struct aimx_h5_reader aimx_h5_reader;

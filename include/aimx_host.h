@@ -74,6 +74,8 @@ int aimx_store_create_hops(int64_t n_mols, const int64_t* atom_ptr, const int32_
 void aimx_store_destroy(aimx_mol_store* store);
 int64_t aimx_store_num_molecules(const aimx_mol_store* store);
 int64_t aimx_store_num_atoms(const aimx_mol_store* store, int64_t mol);
+/* Atom counts of every molecule at once: out[n_mols] (one call instead of n_mols). */
+int aimx_store_atom_counts(const aimx_mol_store* store, int64_t* out);
 
 /* ------------------------------------------------------------------------------------------
  * Collator: plan (BFS or cache lookup for the G molecules of a batch, sizes) then write into
@@ -120,6 +122,14 @@ int aimx_collate_write(aimx_collator* c, const AimxCollateOut* out);
 int aimx_csr_host_build(const int64_t* edges, int64_t E, const int64_t* batch, int64_t N, int64_t G, int32_t hops,
                         int32_t* fwd_rowptr, int32_t* fwd_col, int32_t* bwd_rowptr, int32_t* bwd_col,
                         int32_t* graph_rowptr, int32_t* graph_col);
+
+/* aimx_csr_host_build's contract and bit-identical output, built by the collator's worker pool
+ * for the batch it has just written (aimx_collate_write into these edges / batch buffers, padded
+ * or not): each molecule's edges join only its own atoms, so each worker fills its molecules' rows.
+ * Any other input is handed to aimx_csr_host_build. */
+int aimx_collate_csr(aimx_collator* c, const int64_t* edges, int64_t E, const int64_t* batch, int64_t N, int64_t G,
+                     int32_t hops, int32_t* fwd_rowptr, int32_t* fwd_col, int32_t* bwd_rowptr, int32_t* bwd_col,
+                     int32_t* graph_rowptr, int32_t* graph_col);
 
 #ifdef __cplusplus
 }

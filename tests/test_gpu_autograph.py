@@ -164,6 +164,21 @@ def test_autograph_falls_back_and_guards():
         h.remove()
 
 
+def test_autograph_size_gate(monkeypatch):
+    """By default the replay applies only while atoms x hidden <= MAX_WORK (device-bound larger steps
+    run eagerly: measured faster at c4 / c5); enable(model, True) forces it."""
+    from aimx import autograph
+    from models import GNN
+    b = _batches(1, 71)[0]
+    fs = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+    m = GNN(fs, CFG["hidden"], 1, num_shells=3).to(DEV).train()
+    assert autograph.wanted(m, b.model_args())
+    monkeypatch.setattr(autograph, "MAX_WORK", b.num_atoms * CFG["hidden"] - 1)
+    assert not autograph.wanted(m, b.model_args())
+    autograph.enable(m, True)
+    assert autograph.wanted(m, b.model_args())
+
+
 def test_autograph_amp_state_and_replaced_parameters():
     """The autocast state is part of the bucket key (a capture bakes in bf16 or fp32 GEMM operands):
     the same batch under autocast gets its own bucket and matches the eager AMP path; replacing the

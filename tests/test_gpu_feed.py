@@ -81,3 +81,40 @@ def test_feeder_surfaces_collate_errors():
     f = feed.BatchFeeder(store, iter([np.array([0, len(asset)])]), 3, DEV, depth=1)
     with pytest.raises(feed.HostError):
         next(f)
+
+
+def test_feeder_ring_reuse_is_race_free():
+    """Static shapes: the ring reuses a slot only after the consumer has moved past its batch. A
+    busy consumer stream (long GEMMs queued before each batch is read) lets the copy stream run
+    ahead; every batch read must still equal the host-collated blob byte for byte. Consumed one at
+    a time the ring stays a few slots; kept (list) it grows instead of overwriting."""
+    asset = QM9Asset()
+    store = feed.HostStore.from_qm9_asset(asset, precompute_hops=3, threads=3)
+    rng = np.random.default_rng(5)
+    idxs = [rng.integers(0, len(asset), 64) for _ in range(24)]
+    c = feed.HostCollator(3, 2)
+    sizes = np.array([c.plan(store, i) for i in idxs])
+    pad = (int(sizes[:, 0].max()) + 7, int(sizes[:, 1].max()) + 11, 4)
+    want = [c.collate_blob(store, i, False, *pad)[0].clone() for i in idxs]
+    layout = c.collate_blob(store, idxs[0], False, *pad)[1]
+
+    def same(a, b):  # every field's bytes (the 256-byte alignment gaps are never written)
+        return all(torch.equal(a[o:o + int(np.prod(sh)) * np.dtype(dt).itemsize],
+                               b[o:o + int(np.prod(sh)) * np.dtype(dt).itemsize]) for o, dt, sh in layout)
+    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=pad[0], e_max=pad[1], pad_mols=pad[2])
+    x = torch.randn(2048, 2048, device=DEV)
+    got = []
+    for b in f:
+        for _ in range(4):
+            x = torch.tanh(x @ x)
+        got.append(b._blob.clone())
+    torch.cuda.synchronize()
+    assert len(got) == len(idxs)
+    for g, w in zip(got, want):
+        assert same(g.cpu(), w)
+    assert f.stats()["ring"] <= 6
+    kept = list(feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=pad[0], e_max=pad[1],
+                                 pad_mols=pad[2]))
+    torch.cuda.synchronize()
+    for b, w in zip(kept, want):
+        assert same(b._blob.cpu(), w)

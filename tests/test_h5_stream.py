@@ -169,3 +169,70 @@ def test_stream_batches_span_chunks():
         col = feed.HostCollator(3).collate(store, idx)
         got.append(col["n_atoms"])
     assert np.array_equal(np.concatenate(got), z["n_atoms"])
+
+
+def _read_all(path, pos, hops, direct, threads=3):
+    old = os.environ.get("AIMX_H5_DIRECT")
+    os.environ["AIMX_H5_DIRECT"] = "1" if direct else "0"
+    try:
+        f = h5.H5File(path)
+    finally:
+        if old is None:
+            del os.environ["AIMX_H5_DIRECT"]
+        else:
+            os.environ["AIMX_H5_DIRECT"] = old
+    assert f.direct_read == direct
+    store, kept = f.read_store(pos, hops, 1, threads)
+    return _collate_h(store, hops), kept
+
+
+def test_direct_read_equals_hdf5_read(tmp_path):
+    """The mapped-file path (records found in the global heap directly, no H5Dread) returns exactly
+    what the HDF5 library returns: the fixture, and a file large enough that the open-time check
+    samples only some records; unsorted positions with repeats (the H5Dread path sorts them)."""
+    z = np.load(EXP)
+    for path, n, hops in [(FIX, 63, 3), (None, 300, 3)]:
+        if path is None:
+            mols = synth_molecules(n, seed=9)
+            recs = [h5.make_record(a, b, f, hops, 0.25 * i) for i, (a, b, f) in enumerate(mols)]
+            recs[17] = None
+            path = str(tmp_path / "big.h5")
+            h5.write_hdf5(path, recs, hops, chunk_size=64)
+        rng = np.random.default_rng(3)
+        pos = np.concatenate([rng.permutation(n), rng.integers(0, n, 40)]).astype(np.int64)
+        a, ka = _read_all(path, pos, hops, True)
+        b, kb = _read_all(path, pos, hops, False)
+        assert np.array_equal(ka, kb)
+        for k in ("edges", "feats", "batch", "n_atoms", "total_charges", "targets"):
+            assert np.array_equal(a[k], b[k]), k
+        if path == FIX:
+            full, kf = _read_all(FIX, np.arange(63), 3, True)
+            assert np.array_equal(kf, z["positions"])
+            assert np.array_equal(full["edges"], z["edges"])
+
+
+def test_direct_read_never_returns_wrong_bytes(tmp_path):
+    """A damaged global heap collection: the direct path is refused at open (sampled records
+    differ from H5Dread's) or the read of a damaged record fails; it never yields other bytes."""
+    mols = synth_molecules(200, seed=4)
+    recs = [h5.make_record(a, b, f, 3, float(i)) for i, (a, b, f) in enumerate(mols)]
+    good = str(tmp_path / "good.h5")
+    h5.write_hdf5(good, recs, 3)
+    raw = bytearray(open(good, "rb").read())
+    hits = [i for i in range(len(raw) - 4) if raw[i:i + 4] == b"GCOL"]
+    assert len(hits) >= 2
+    ref, kref = _read_all(good, np.arange(200), 3, True)
+    for victim in (hits[0], hits[len(hits) // 2]):
+        bad = bytearray(raw)
+        bad[victim + 3] = ord("X")
+        p = str(tmp_path / f"bad{victim}.h5")
+        open(p, "wb").write(bytes(bad))
+        f = h5.H5File(p)
+        if not f.direct_read:
+            continue
+        try:
+            store, kept = f.read_store(np.arange(200), 3, 1, 3)
+        except Exception:
+            continue
+        col = _collate_h(store, 3)
+        assert np.array_equal(kept, kref) and np.array_equal(col["edges"], ref["edges"])

@@ -226,3 +226,40 @@ def test_feeder_blob_carries_host_csr(asset):
     a, r = b.edges._aimx_csr, ref.edges._aimx_csr
     for k in ("fwd_rowptr", "fwd_col", "bwd_rowptr", "bwd_col", "graph_rowptr", "graph_col"):
         assert torch.equal(getattr(a, k), getattr(r, k)), k
+
+
+def _csr_views(nr, er, gr, h):
+    return [np.empty(h * nr + 1, np.int32), np.empty(er, np.int32), np.empty(nr + 1, np.int32),
+            np.empty(er, np.int32), np.empty(gr + 1, np.int32), np.empty(nr, np.int32)]
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_collator_parallel_csr_equals_serial(asset, threads):
+    """aimx_collate_csr (the collator's pool, rows per molecule) == aimx_csr_host_build (one
+    global stable sort), padded and unpadded batches, repeats, 3 and 6 hops; a batch whose edges
+    cross molecules (not the collator's shape) takes the serial build and still agrees."""
+    lib = feed.load_host()
+    rng = np.random.default_rng(threads)
+    stores = [(feed.HostStore.from_qm9_asset(asset, precompute_hops=3), 3),
+              (feed.HostStore.from_molecules(synth_molecules(300, seed=2), precompute_hops=6), 6)]
+    for store, h in stores:
+        c = feed.HostCollator(h, threads)
+        for trial in range(4):
+            idx = rng.integers(0, len(store), int(rng.integers(1, 90)))
+            n, e = c.plan(store, idx)
+            pad = trial % 2 == 1
+            nr, er, gr = (n + 37, e + 101, len(idx) + 3) if pad else (n, e, len(idx))
+            feats = [np.empty(nr, np.int64) for _ in range(4)]
+            edges = np.empty((er, 2), np.int64)
+            batch = np.empty(nr, np.int64)
+            c.write([f.ctypes.data for f in feats], edges.ctypes.data, batch.ctypes.data, n_max=nr if pad else 0,
+                    e_max=er if pad else 0, pad_mols=3 if pad else 0)
+            for mutate in (False, True):
+                if mutate and er > 1:  # one edge joins molecules 0 and the last: not the collator's shape
+                    edges[0, 1] = nr - 1
+                got, ref = _csr_views(nr, er, gr, h), _csr_views(nr, er, gr, h)
+                feed._check(lib.aimx_collate_csr(c._h, edges.ctypes.data, er, batch.ctypes.data, nr, gr, h,
+                                                 *[v.ctypes.data for v in got]), "collate_csr")
+                adata.host_csr_into(ref, edges, batch, gr, h)
+                for a, b in zip(got, ref):
+                    assert np.array_equal(a, b)
