@@ -851,28 +851,34 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const WgradTable t, float
               tile, nt, ws + t.ws_off[q], counters ? counters + t.cnt_off[q] : nullptr, red);
 }
 
-// ---- Long-K weight gradients through LDS: 80 x 80 output blocks ----------------------------------
+// ---- Long-K weight gradients through LDS: 80 x 80 or 160 x 160 output blocks ------------------
 // k_wgrad_grouped's waves load their MFMA fragments straight from global memory: one dword load
 // per MFMA, re-read by every 32 x 32 tile of the output, which leaves that kernel address-rate
-// bound (~30 % MFMA issue). Here a workgroup owns an 80 x 80 block (a whole 76 x 76 + bias MLP
-// weight of c2, or a quarter of its input projection) and a K slice: 32 k rows of dY and X are
-// staged in LDS by 16-byte loads (each element read once per block), prefetched into registers
-// while the previous rows compute; wave w (of 5) owns fragment row w and runs its 5 MFMAs per k
-// step from LDS (A read once, reused across the row). The LDS row stride of 80 floats puts the 4
-// k rows of a fragment read on bank offsets 0/16/32/48: conflict-free. Split-K slices are summed
-// as in k_wgrad_grouped (sc1 slabs, last arriver adds them in slice order): deterministic.
-constexpr int kWbB = 80;                             // block edge
-constexpr int kWbF = kWbB / 16;                      // fragments per edge = waves per workgroup
+// bound (~30 % MFMA issue). Here a workgroup owns a BB x BB block (80: a whole 76 x 76 + bias MLP
+// weight of c2, or a quarter of its input projection; 160: c4's 153 x 154 weight whole, c5's
+// 307 x 308 in four) and a K slice: 32 k rows of dY and X are staged in LDS by 16-byte loads (each
+// element read once per block), prefetched into registers while the previous rows compute; wave w
+// (of BB / 16) owns fragment row w and runs its BB / 16 MFMAs per k step from LDS (A read once,
+// reused across the row). The 160-wide block halves the operand bytes per MFMA (global loads and
+// LDS writes per flop) and gives each wave 10 MFMAs per k step against 11 LDS reads. LDS row
+// strides 80 / 176 floats put the 4 k rows of a fragment read on bank offsets 0/16/32/48:
+// conflict-free. Split-K slices are summed as in k_wgrad_grouped (sc1 slabs, last arriver adds
+// them in slice order): deterministic.
 constexpr int kWbK = 32;                             // k rows per LDS fill
 #ifndef AIMX_WBD
 #define AIMX_WBD 2
 #endif
 constexpr int kWbD = AIMX_WBD;                       // LDS fills in flight (register ring)
-constexpr int kWbT = 64 * kWbF;                      // threads per workgroup
-constexpr int kWbSlab = kWbB * kWbB;                 // floats per split-K slab
-constexpr int kWbQ = kWbK * kWbB / 4;                // float4 per operand per fill
-constexpr int kWbV = 2 * kWbQ / kWbT;                // float4 per thread per fill
-static_assert(kWbQ % kWbT == 0, "each thread's float4s belong to one operand");
+template <int BB>
+struct WbGeom {
+  static constexpr int F = BB / 16;                  // fragments per edge = waves per workgroup
+  static constexpr int T = 64 * F;                   // threads per workgroup
+  static constexpr int S = BB == 80 ? 80 : BB + 16;  // LDS row stride (floats)
+  static constexpr int Slab = BB * BB;               // floats per split-K slab
+  static constexpr int Q = kWbK * BB / 4;            // float4 per operand per fill
+  static constexpr int V = 2 * Q / T;                // float4 per thread per fill
+  static_assert(Q % T == 0, "each thread's float4s belong to one operand");
+};
 
 struct WbTable {
   int32_t n;
@@ -884,9 +890,12 @@ struct WbTable {
   int32_t xcd;  // XCD-aware work order (AIMX_WGRAD_XCD=0: launch order, for A/B)
 };
 
-__global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
-  __shared__ __attribute__((aligned(16))) float sA[kWbK * kWbB];
-  __shared__ __attribute__((aligned(16))) float sB[kWbK * kWbB];
+template <int BB>
+__global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
+  using G = WbGeom<BB>;
+  constexpr int kWbF = G::F, kWbT = G::T, kWbV = G::V, kLd = G::S;
+  __shared__ __attribute__((aligned(16))) float sA[kWbK * kLd];
+  __shared__ __attribute__((aligned(16))) float sB[kWbK * kLd];
   __shared__ int flag;
   int q = 0;
   while (q + 1 < t.n && t.blk0[q + 1] <= (int)blockIdx.x) ++q;
@@ -908,7 +917,7 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
   const int lm = lane & 15, lk = lane >> 4;
   const int M = (int)pr.M, Nreal = (int)pr.N, ones = pr.col_out != nullptr;
   const int N = Nreal + ones;
-  const int m0 = (blk / t.bn[q]) * kWbB, n0 = (blk % t.bn[q]) * kWbB;
+  const int m0 = (blk / t.bn[q]) * BB, n0 = (blk % t.bn[q]) * BB;
   const int S = t.splits[q];
   AimxGemmArgs a = {};
   a.M = M;
@@ -921,10 +930,10 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
   a.ones_col = ones;
   a.col_out = pr.col_out;
   if (pr.zc_rowptr && n0 >= zc_extent(pr.zc_rowptr, pr.zc_rows, pr.zc_chunks, pr.zc_width) &&
-      !(ones && n0 + kWbB > Nreal)) {  // a block wholly inside the empty hop chunks: zero, no work
+      !(ones && n0 + BB > Nreal)) {  // a block wholly inside the empty hop chunks: zero, no work
     if (z == 0)
-      for (int e = tid; e < kWbSlab; e += kWbT) {
-        const int m = m0 + e / kWbB, n = n0 + e % kWbB;
+      for (int e = tid; e < G::Slab; e += kWbT) {
+        const int m = m0 + e / BB, n = n0 + e % BB;
         if (m < M && n < Nreal) pr.dW[(int64_t)m * pr.ld_dw + n] = 0.f;
       }
     return;
@@ -946,7 +955,7 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
     for (int u = 0; u < kWbV; ++u) {
       const bool isb = u >= kWbV / 2;
       const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
-      const int row = f / (kWbB / 4), c = 4 * (f % (kWbB / 4));
+      const int row = f / (BB / 4), c = 4 * (f % (BB / 4));
       const int k = k0 + row;
       const int col = (isb ? n0 : m0) + c, lim = isb ? Nreal : M;
       const uint32_t ld = isb ? ldb : lda, bytes = isb ? bb : ab;
@@ -991,13 +1000,13 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
       for (int u = 0; u < kWbV; ++u) {
         const bool isb = u >= kWbV / 2;
         const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
-        *reinterpret_cast<floatx4*>((isb ? sB : sA) + 4 * f) = ring[d][u];
+        *reinterpret_cast<floatx4*>((isb ? sB : sA) + (f / (BB / 4)) * kLd + 4 * (f % (BB / 4))) = ring[d][u];
       }
       __syncthreads();
       if (s + kWbD < nsub) fetch(kb + (s + kWbD) * kWbK, ring[d]);
 #pragma unroll
       for (int k4 = 0; k4 < kWbK / 4; ++k4) {
-        const int r = (k4 * 4 + lk) * kWbB + lm;
+        const int r = (k4 * 4 + lk) * kLd + lm;
         const float av = sA[r + w * 16];
         float bv[kWbF];
 #pragma unroll
@@ -1009,11 +1018,11 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
   }
 
   if (S > 1) {
-    const __amdgpu_buffer_rsrc_t rws = make_rsrc(ws + t.ws_off[q], (uint32_t)(4 * (int64_t)S * nb * kWbSlab));
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(ws + t.ws_off[q], (uint32_t)(4 * (int64_t)S * nb * G::Slab));
     const uint32_t own = 16u * (uint32_t)((w * kWbF) * 64 + lane);
 #pragma unroll
     for (int j = 0; j < kWbF; ++j)
-      store_sc1(rws, 4u * (uint32_t)((z * nb + blk) * kWbSlab) + own + 16u * 64u * (uint32_t)j, acc[j]);
+      store_sc1(rws, 4u * (uint32_t)((z * nb + blk) * G::Slab) + own + 16u * 64u * (uint32_t)j, acc[j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -1031,7 +1040,7 @@ __global__ __launch_bounds__(kWbT) void k_wgrad_lds(const WbTable t, float* ws, 
       floatx4 v[kWbF];
 #pragma unroll
       for (int j = 0; j < kWbF; ++j)
-        v[j] = load_sc1(rws, 4u * (uint32_t)((zz * nb + blk) * kWbSlab) + own + 16u * 64u * (uint32_t)j);
+        v[j] = load_sc1(rws, 4u * (uint32_t)((zz * nb + blk) * G::Slab) + own + 16u * 64u * (uint32_t)j);
 #pragma unroll
       for (int j = 0; j < kWbF; ++j) acc[j] += v[j];
     }
@@ -1201,7 +1210,8 @@ constexpr int64_t kLoneWgs = 1024;  // workgroups a lone long-K GEMM's LDS launc
 namespace {
 struct WgPlan {
   int tiles_x, tiles_y, splits, kchunk;
-  bool lds;    // k_wgrad_lds (80 x 80 blocks) instead of k_wgrad_grouped (32 x 32 tiles)
+  bool lds;    // k_wgrad_lds (bb x bb blocks) instead of k_wgrad_grouped (32 x 32 tiles)
+  int bb;      // k_wgrad_lds block edge: 80 or 160
   int64_t slab;  // floats per split-K slab
 };
 // min_wgs > 0 (a lone long-K GEMM routed here): split K further until the launch has about that
@@ -1212,11 +1222,16 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
   WgPlan w;
   const int64_t N = p.col_out ? p.N + 1 : p.N;
   if (!no_lds && p.K >= 2048) {
-    // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks
+    // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks.
+    // 160-wide blocks once both edges reach 144 (at most ~10 % of a block past the edge); the
+    // AIMX_WGRAD_BB=80/160 override is for A/B runs
     w.lds = true;
-    w.slab = kWbSlab;
-    w.tiles_x = (int)cdiv(p.M, kWbB);
-    w.tiles_y = (int)cdiv(N, kWbB);
+    const char* be = getenv("AIMX_WGRAD_BB");
+    const int force = be ? atoi(be) : 0;
+    w.bb = force == 80 || force == 160 ? force : (std::min<int64_t>(p.M, N) >= 144 ? 160 : 80);
+    w.slab = (int64_t)w.bb * w.bb;
+    w.tiles_x = (int)cdiv(p.M, w.bb);
+    w.tiles_y = (int)cdiv(N, w.bb);
     const char* kp = getenv("AIMX_WGRAD_KPER");  // atoms per workgroup (tuning experiments)
     const int64_t kper = kp ? std::max(64, atoi(kp)) : 512;
     int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
@@ -1227,6 +1242,7 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
     return w;
   }
   w.lds = false;
+  w.bb = 0;
   w.slab = 1024;
   w.tiles_x = (int)cdiv(p.M, 32);
   w.tiles_y = (int)cdiv(N, 32);
@@ -1393,18 +1409,25 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   // problems per launch each); workspace slabs and counters are laid out in problem order
   int64_t ws_off = 0, cnt_off = 0;
   WgradTable t{};
-  WbTable tb{};
-  int32_t blk = 0, blkb = 0;
-  auto flush = [&](bool lds) {
+  WbTable tbs[2] = {};  // 80- and 160-wide problems: one launch family each
+  int32_t blk = 0, blkbs[2] = {0, 0};
+  auto flush = [&](bool lds, int wide = 0) {
     if (lds) {
+      WbTable& tb = tbs[wide];
+      int32_t& blkb = blkbs[wide];
       tb.blk0[tb.n] = blkb;
       {
         const char* e = getenv("AIMX_WGRAD_XCD");  // =0: launch order (A/B experiments only)
         tb.xcd = (e && atoi(e) == 0) ? 0 : 1;
       }
-      if (blkb > 0)
-        hipLaunchKernelGGL(k_wgrad_lds, dim3((unsigned)blkb), dim3(kWbT), 0, (hipStream_t)stream, tb, (float*)workspace,
-                           counters);
+      if (blkb > 0) {
+        if (wide)
+          hipLaunchKernelGGL(k_wgrad_lds<160>, dim3((unsigned)blkb), dim3(WbGeom<160>::T), 0, (hipStream_t)stream, tb,
+                             (float*)workspace, counters);
+        else
+          hipLaunchKernelGGL(k_wgrad_lds<80>, dim3((unsigned)blkb), dim3(WbGeom<80>::T), 0, (hipStream_t)stream, tb,
+                             (float*)workspace, counters);
+      }
       tb = WbTable{};
       blkb = 0;
     } else {
@@ -1421,6 +1444,9 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
     const WgPlan w = wg_plan(pr, min_wgs);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {
+      const int wide = w.bb == 160;
+      WbTable& tb = tbs[wide];
+      int32_t& blkb = blkbs[wide];
       const int k = tb.n++;
       const int64_t Kr = std::max<int64_t>(pr.K, 1) - 1;
       const bool v4 = pr.ld_dy % 4 == 0 && pr.ld_x % 4 == 0 && (uintptr_t)pr.dY % 16 == 0 && (uintptr_t)pr.X % 16 == 0;
@@ -1440,7 +1466,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
       tb.ws_off[k] = ws_off;
       tb.cnt_off[k] = cnt_off;
       blkb += w.splits * nt;
-      if (tb.n == kWgMaxProb) flush(true);
+      if (tb.n == kWgMaxProb) flush(true, wide);
     } else {
       const int k = t.n++;
       t.p[k] = pr;
@@ -1460,7 +1486,8 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
     cnt_off += nt;
   }
   if (t.n) flush(false);
-  if (tb.n) flush(true);
+  if (tbs[0].n) flush(true, 0);
+  if (tbs[1].n) flush(true, 1);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
