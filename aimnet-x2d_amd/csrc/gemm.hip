@@ -1223,12 +1223,13 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
   const int64_t N = p.col_out ? p.N + 1 : p.N;
   if (!no_lds && p.K >= 2048) {
     // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks.
-    // 160-wide blocks once both edges reach 144 (at most ~10 % of a block past the edge); the
-    // AIMX_WGRAD_BB=80/160 override is for A/B runs
+    // 160-wide blocks (AIMX_WGRAD_BB=160, opt-in) measured slower: wgrad launch c4 472 -> 490 us,
+    // c5 853 -> 880 us; steps c2 0.78 -> 0.90, c4 3.30 -> 3.37, c5 4.98 -> 5.11 ms (a quarter of
+    // the workgroups, 109 VGPRs: 4 waves per SIMD; profiles/r03_gemm_ab.txt)
     w.lds = true;
     const char* be = getenv("AIMX_WGRAD_BB");
     const int force = be ? atoi(be) : 0;
-    w.bb = force == 80 || force == 160 ? force : (std::min<int64_t>(p.M, N) >= 144 ? 160 : 80);
+    w.bb = force == 160 ? 160 : 80;
     w.slab = (int64_t)w.bb * w.bb;
     w.tiles_x = (int)cdiv(p.M, w.bb);
     w.tiles_y = (int)cdiv(N, w.bb);
