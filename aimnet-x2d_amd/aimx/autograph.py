@@ -8,9 +8,10 @@ step, ~2 ms) rather than by the ~0.9 ms of device work. By default (AIMX_AUTOGRA
 
   * pads the batch into the static inputs of a shape bucket — the smallest live one with the same
     molecule count and room for the batch's atoms (plus one slack atom) and edges; a new bucket
-    takes ~6 % headroom, atoms rounded up to a multiple of 512 and edges to 4096 — in ONE
-    launch (`aimx_pad_batch`: slack atoms form 8 padding molecules, slack edges are self-pairs
-    over them, the layout of aimx.data.pad_collated, so no real molecule's values change);
+    takes ~6 % headroom, atoms rounded up to a multiple of 512 and edges to 4096; a bucket serves
+    batches of at least 80 % of its atoms — in ONE launch (`aimx_pad_batch`: slack atoms form
+    padding molecules of at most ~64 atoms (at least 8 of them), slack edges are self-pairs over
+    them, the layout of aimx.data.pad_collated, so no real molecule's values change);
   * replays the bucket's forward graph and returns the real molecules' rows of the output through
     an autograd node whose backward copies the incoming gradient into the static gradient buffer
     and replays the bucket's backward graph;
@@ -40,7 +41,9 @@ from ._lib import AimxError, check, ptr, stream_ptr
 
 ATOM_QUANTUM = 512
 EDGE_QUANTUM = 4096
-PAD_MOLS = 8
+PAD_MOLS = 8          # fewest padding molecules of a bucket
+PAD_ATOMS = 64        # ... and their size: a bucket serves batches of >= (1 - MAX_SLACK) * Np atoms,
+MAX_SLACK = 0.2       # whose slack is split over enough padding molecules to keep each <= PAD_ATOMS
 MAX_BUCKETS = 4
 _FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
 
@@ -114,6 +117,13 @@ def _round_up(x, q):
     return (x + q - 1) // q * q
 
 
+def pad_mols_for(Np):
+    """Padding molecules of a bucket of Np atoms (aimx.data.pad_mols_for for batches down to
+    (1 - MAX_SLACK) * Np atoms)."""
+    from .data import pad_mols_for as pm
+    return pm(Np, int((1 - MAX_SLACK) * Np), PAD_ATOMS, PAD_MOLS)
+
+
 def _param_key(model):
     """Identity and storage of the model's live parameters: a replaced Parameter object
     (load_state_dict(assign=True), a swapped submodule) or moved storage re-captures the bucket."""
@@ -135,13 +145,14 @@ class _Bucket:
         self.feat = torch.zeros(4, Np, dtype=i64, device=dev)
         self.edges = torch.zeros(Ep, 2, dtype=i64, device=dev)
         self.batch = torch.zeros(Np, dtype=i64, device=dev)
-        self.charges = torch.zeros(G + PAD_MOLS, dtype=torch.float32, device=dev)
+        self.pad_mols = pad_mols_for(Np)
+        self.charges = torch.zeros(G + self.pad_mols, dtype=torch.float32, device=dev)
         self.empty4 = torch.empty(0, 4, dtype=i64, device=dev)
         self.empty2 = torch.empty(0, 2, dtype=i64, device=dev)
         a = _lib.PadBatch()
         a.out_feat, a.out_edges, a.out_batch, a.out_charges = ptr(self.feat), ptr(self.edges), ptr(self.batch), \
             ptr(self.charges)
-        a.Np, a.Ep, a.pad_mols = Np, Ep, PAD_MOLS
+        a.Np, a.Ep, a.pad_mols = Np, Ep, self.pad_mols
         self.pad = a
         self.params = [p for p in model.parameters()]
         self.param_key = _param_key(model)
@@ -235,12 +246,12 @@ class _Replay(torch.autograd.Function):
 
 def _pick(st, N, E, G, dev, amp):
     """The smallest live bucket that holds this batch (same molecule count and autocast state, room
-    for one slack atom and every edge), else a new one sized with ~6 % headroom so the batches of an
-    epoch settle on one or two buckets."""
+    for one slack atom and every edge, at most MAX_SLACK of its atoms slack), else a new one sized
+    with ~6 % headroom so the batches of an epoch settle on one or two buckets."""
     best = None
     for key, b in st.buckets.items():
         if key[2] == G and key[3] == dev.index and key[4] == amp and key[0] > N and key[1] >= E and \
-                (best is None or key[0] + key[1] < best[0] + best[1]):
+                N >= (1 - MAX_SLACK) * key[0] and (best is None or key[0] + key[1] < best[0] + best[1]):
             best = key
     if best is not None:
         return best, False

@@ -200,6 +200,14 @@ class DeviceBatch:
                 self.trans)
 
 
+def pad_mols_for(n_max, n_min, atoms_per_pad=64, least=8):
+    """Padding molecules for a static batch of n_max atoms whose real atom count may drop to n_min:
+    the slack is split over enough molecules that none exceeds atoms_per_pad atoms (at least
+    `least` of them). A padding molecule above 128 atoms leaves the attention pool's row-resident
+    path (pool.hip): 8 molecules over c4's ~1.3 k slack atoms made k_attn_fwd / bwd ~6x slower."""
+    return max(least, -(-(int(n_max) - int(n_min)) // atoms_per_pad))
+
+
 def pad_collated(col, n_max, e_max, g_real, n_pad_mols=8):
     """Pad a collated batch to static shapes for graph replay (SURVEY.md §8d "padded batches").
 

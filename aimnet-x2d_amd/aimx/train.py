@@ -231,6 +231,7 @@ def main(argv=None):
     from models import GNN, L1Loss
     from utils.distributed import GradientSync
 
+    from . import data as adata
     from . import feed
     from .optim import FusedAdam
     from .synth import QM9Asset
@@ -274,17 +275,18 @@ def main(argv=None):
     shard = tr_idx[rank::world]  # disjoint per rank (DistributedSampler semantics)
     steps = len(shard) // B
     pad = not a.eager
-    n_max = e_max = 0
+    n_max = e_max = pm = 0
     if pad:
         probe = feed.HostCollator(a.hops, 2)
         sz = np.array([probe.plan(store, shard[rng.permutation(len(shard))[:B]]) for _ in range(64)])
         n_max, e_max = int(sz[:, 0].max() * 1.05) + 64, int(sz[:, 1].max() * 1.05) + 256
+        pm = adata.pad_mols_for(n_max, int(sz[:, 0].min() * 0.95))
 
     def epoch_batches(ep):
         p = np.random.default_rng(a.seed * 1000 + ep).permutation(len(shard))
         idx = [shard[p[i * B:(i + 1) * B]] for i in range(steps)]
         return feed.BatchFeeder(store, iter(idx), a.hops, dev, depth=3, threads=4, n_max=n_max, e_max=e_max,
-                                pad_mols=8 if pad else 0)
+                                pad_mols=pm)
 
     graphed = None
     for ep in range(a.epochs):

@@ -69,18 +69,20 @@ PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from t
 
 
 def make_batches(cfg, n_batches, seed, device, pad=False):
-    """Device-resident batches. pad=True: static shapes for graph replay (PAD_MOLS padding molecules)."""
+    """Device-resident batches. pad=True: static shapes for graph replay (padding molecules of at
+    most 64 atoms each, pad_mols_for)."""
     cols = make_collated(cfg, n_batches, seed)
     if not pad:
         return [adata.DeviceBatch(c, device, targets=t, total_charges=q, csr_hops=cfg["hops"]) for c, t, q in cols]
     n_max = max(c["batch"].shape[0] for c, _, _ in cols) + 64
     e_max = max(c["edges"].shape[0] for c, _, _ in cols) + 256
+    pm = pad_mols_for(n_max, min(c["batch"].shape[0] for c, _, _ in cols))
     out = []
     for c, t, q in cols:
         real_atoms, real_edges = c["batch"].shape[0], c["edges"].shape[0]
-        pc = adata.pad_collated(c, n_max, e_max, cfg["batch"], PAD_MOLS)
-        tg = np.concatenate([t, np.zeros((PAD_MOLS, t.shape[1]), np.float32)])
-        qq = np.concatenate([q, np.zeros(PAD_MOLS, np.float32)])
+        pc = adata.pad_collated(c, n_max, e_max, cfg["batch"], pm)
+        tg = np.concatenate([t, np.zeros((pm, t.shape[1]), np.float32)])
+        qq = np.concatenate([q, np.zeros(pm, np.float32)])
         b = adata.DeviceBatch(pc, device, targets=tg, total_charges=qq, csr_hops=cfg["hops"])
         b.real_atoms, b.real_edges, b.real_graphs = real_atoms, real_edges, cfg["batch"]
         out.append(b)
@@ -102,17 +104,23 @@ def native_feeder(cfg, seed, device, threads, pad):
         store = feed.HostStore.from_molecules(mols, rng.standard_normal((len(mols), cfg["tasks"])),
                                               precompute_hops=cfg["hops"], threads=threads)
     B = cfg["batch"]
-    n_max = e_max = 0
+    n_max = e_max = pm = 0
     if pad:  # static capacity: the largest of 256 sampled batches + margin (overflow raises HostError)
         probe = feed.HostCollator(cfg["hops"], threads)
         sizes = np.array([probe.plan(store, rng.integers(0, len(store), B)) for _ in range(256)])
         n_max, e_max = int(sizes[:, 0].max() * 1.03) + 64, int(sizes[:, 1].max() * 1.03) + 256
+        pm = pad_mols_for(n_max, int(sizes[:, 0].min()))
 
     def index_stream():
         while True:
             yield rng.integers(0, len(store), B)
     return iter(feed.BatchFeeder(store, index_stream(), cfg["hops"], device, depth=4, threads=threads,
-                                 n_max=n_max, e_max=e_max, pad_mols=PAD_MOLS if pad else 0))
+                                 n_max=n_max, e_max=e_max, pad_mols=pm))
+
+
+def pad_mols_for(n_max, n_min):
+    """Padding molecules of at most 64 atoms each (aimx.data.pad_mols_for; at least PAD_MOLS)."""
+    return adata.pad_mols_for(n_max, n_min, 64, PAD_MOLS)
 
 
 STREAM_INFO = {}
@@ -149,13 +157,14 @@ def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None):
                 read_mol_per_s=round(len(pos) / (time.perf_counter() - t0)), read_threads=threads)
     STREAM_INFO.update(info)
     B = cfg["batch"]
-    n_max = e_max = 0
+    n_max = e_max = pm = 0
     if pad:  # static capacity from the first chunk's batches + margin (an overflow raises HostError)
         store, _ = stream.file.read_store(stream.positions(0)[:16384], cfg["hops"], cfg["tasks"], threads)
         probe = feed.HostCollator(cfg["hops"], threads)
         rng = np.random.default_rng(rank)
         sizes = np.array([probe.plan(store, rng.integers(0, len(store), B)) for _ in range(256)])
         n_max, e_max = int(sizes[:, 0].max() * 1.08) + 64, int(sizes[:, 1].max() * 1.08) + 256
+        pm = pad_mols_for(n_max, int(sizes[:, 0].min() * 0.97))
 
     def batches():
         epoch = 0
@@ -163,7 +172,7 @@ def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None):
             yield from stream.batches(B, chunk_size=16384, epoch_seed=epoch)
             epoch += 1
     return iter(feed.BatchFeeder(None, batches(), cfg["hops"], device, depth=4, threads=threads,
-                                 n_max=n_max, e_max=e_max, pad_mols=PAD_MOLS if pad else 0))
+                                 n_max=n_max, e_max=e_max, pad_mols=pm))
 
 
 def build_model(cfg, device):
