@@ -8,10 +8,11 @@ step, ~2 ms) rather than by the ~0.9 ms of device work. By default (AIMX_AUTOGRA
 
   * pads the batch into the static inputs of a shape bucket — the smallest live one with the same
     molecule count and room for the batch's atoms (plus one slack atom) and edges; a new bucket
-    takes ~6 % headroom, atoms rounded up to a multiple of 512 and edges to 4096; a bucket serves
-    batches of at least 80 % of its atoms — in ONE launch (`aimx_pad_batch`: slack atoms form
-    padding molecules of at most ~64 atoms (at least 8 of them), slack edges are self-pairs over
-    them, the layout of aimx.data.pad_collated, so no real molecule's values change);
+    takes ~6 % headroom, atoms rounded up to a multiple of 512 and edges to 4096; a bucket serves a
+    batch only while its padding molecules stay within 96 atoms — in ONE launch (`aimx_pad_batch`:
+    slack atoms form padding molecules (at least 8, ~64 atoms each down to 80 % occupancy), slack
+    edges are self-pairs over them, the layout of aimx.data.pad_collated, so no real molecule's
+    values change);
   * replays the bucket's forward graph and returns the real molecules' rows of the output through
     an autograd node whose backward copies the incoming gradient into the static gradient buffer
     and replays the bucket's backward graph;
@@ -42,8 +43,9 @@ from ._lib import AimxError, check, ptr, stream_ptr
 ATOM_QUANTUM = 512
 EDGE_QUANTUM = 4096
 PAD_MOLS = 8          # fewest padding molecules of a bucket
-PAD_ATOMS = 64        # ... and their size: a bucket serves batches of >= (1 - MAX_SLACK) * Np atoms,
-MAX_SLACK = 0.2       # whose slack is split over enough padding molecules to keep each <= PAD_ATOMS
+PAD_ATOMS = 64        # ... sized for batches of >= (1 - MAX_SLACK) * Np atoms to keep each <= PAD_ATOMS
+MAX_SLACK = 0.2
+PAD_ATOMS_MAX = 96    # a bucket serves a batch only if its padding molecules stay within this (< 128)
 MAX_BUCKETS = 4
 _FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
 
@@ -246,12 +248,13 @@ class _Replay(torch.autograd.Function):
 
 def _pick(st, N, E, G, dev, amp):
     """The smallest live bucket that holds this batch (same molecule count and autocast state, room
-    for one slack atom and every edge, at most MAX_SLACK of its atoms slack), else a new one sized
+    for one slack atom and every edge, padding molecules within PAD_ATOMS_MAX), else a new one sized
     with ~6 % headroom so the batches of an epoch settle on one or two buckets."""
     best = None
     for key, b in st.buckets.items():
         if key[2] == G and key[3] == dev.index and key[4] == amp and key[0] > N and key[1] >= E and \
-                N >= (1 - MAX_SLACK) * key[0] and (best is None or key[0] + key[1] < best[0] + best[1]):
+                key[0] - N <= pad_mols_for(key[0]) * PAD_ATOMS_MAX and \
+                (best is None or key[0] + key[1] < best[0] + best[1]):
             best = key
     if best is not None:
         return best, False
