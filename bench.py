@@ -216,25 +216,29 @@ def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launch
     ms = t0.elapsed_time(t1) / launches
     alg_bytes = 4 * (n * d + e + (hops * n + 1) + hops * n * d)
     gbs = alg_bytes / (ms * 1e-3) / 1e9
-    traffic = None
-    tp = os.path.join(ROOT, "profiles", "hop_traffic.json")
+    traffic = bwd_traffic = None
+    tname = "hop_traffic.json" if d % 4 == 0 else f"hop_traffic_d{d}.json"
+    tp = os.path.join(ROOT, "profiles", tname)
     if os.path.exists(tp):
         try:
             rec = json.load(open(tp))
             if rec.get("atoms") == n and rec.get("edges") == e:
                 traffic = rec.get("hbm_bytes_per_launch")
+                bwd_traffic = (rec.get("bwd") or {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
     bwd = hop_bwd_roofline(plan, n, d, hops, device)
+    bwd["traffic"] = bwd_traffic
     del plan, x
     torch.cuda.empty_cache()
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_source": ("profiles/hop_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same "
+            "traffic_source": (f"profiles/{tname}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same "
                                "command (bench.py --roofline-only), per launch, gfx950 corrections applied; not "
                                "measured inside this run") if traffic is not None else None,
             "bwd": bwd,
-            "kernel": "k_gather_sum (hop fwd)", "atoms": n, "edges": e, "D": d, "hops": hops,
+            "kernel": ("k_gather_sum" if d % 4 == 0 else "k_gather_rows") + " (hop fwd)", "atoms": n, "edges": e,
+            "D": d, "hops": hops,
             "algorithmic_bytes_per_launch": alg_bytes, "ms_per_launch": round(ms, 4)}
 
 
@@ -327,7 +331,8 @@ def hop_bwd_roofline(plan, n, d, hops, device, launches=20):
     t1.record(stream)
     t1.synchronize()
     us = t0.elapsed_time(t1) / launches * 1e3
-    return _bw("k_gather_sum (hop bwd)", 4 * (n * d + plan.E + (n + 1) + n * d), us)
+    return _bw(("k_gather_sum" if d % 4 == 0 else "k_gather_rows") + " (hop bwd)",
+               4 * (n * d + plan.E + (n + 1) + n * d), us)
 
 
 def attn_in_step(batch, hidden, device, heads=4):
