@@ -215,8 +215,17 @@ __device__ __forceinline__ void zero_tile(const AimxGemmArgs& a, int m0, int n0,
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, bool AK, bool BKC, bool V4, bool BF>
+// VU (fp32, !V4): the k-contiguous operands whose rows are not 16-byte aligned (c4/c5's D = 153 /
+// 307 activations and weights) are staged with 16-byte loads anyway: each row's 32-k slice is the
+// 9 aligned float4s covering it (descriptor based at the operand's 16-byte-aligned floor), and
+// each float4's components go to their shifted LDS columns, so per slice a thread issues ~2-3
+// 16-byte loads instead of 8 dword loads (the dword path is address-rate bound). Components
+// outside the slice or past K read as zero. The aligned 16-byte granules around valid elements
+// are always mapped, and the descriptor's extent is the granule-rounded end of the operand.
+template <int BM, int BN, bool AK, bool BKC, bool V4, bool BF, bool VU = false>
 __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
+  static_assert(!VU || (!V4 && !BF), "VU is the fp32 dword-path replacement");
+  constexpr bool VUA = VU && AK, VUB = VU && BKC;
   constexpr int BK = kBK;
   constexpr int SH = BK + 8;                       // BF: bf16 row stride of both LDS images
   constexpr int LAH = BM * SH, LBH = BN * SH;      // BF: bf16 elements per stage and operand
@@ -246,8 +255,13 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       return;
     }
   }
-  const __amdgpu_buffer_rsrc_t ra_ = make_rsrc(a.A, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb_ = make_rsrc(a.B, b_bytes);
+  // VU: descriptors from the 16-byte-aligned floor of each operand (mis_* floats below it)
+  const uint32_t mis_a = VUA ? (uint32_t)(((uintptr_t)a.A >> 2) & 3) : 0u;
+  const uint32_t mis_b = VUB ? (uint32_t)(((uintptr_t)a.B >> 2) & 3) : 0u;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      VUA ? make_rsrc(a.A - mis_a, (a_bytes + 4u * mis_a + 15u) & ~15u) : make_rsrc(a.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb_ =
+      VUB ? make_rsrc(a.B - mis_b, (b_bytes + 4u * mis_b + 15u) & ~15u) : make_rsrc(a.B, b_bytes);
   const uint32_t sam = (uint32_t)a.sam, sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
 
   // Per-thread fixed coordinates of the staging pattern.
@@ -287,7 +301,38 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   }
 
   constexpr int NA4 = V4 ? BM * BK / 1024 : 1, NB4 = V4 ? BN * BK / 1024 : 1;
-  auto load_slice = [&](int k0, bool tail, float (&ra)[NA], float (&rb)[NB]) {
+  // VU: float4 q (< rows * 9) of an operand's slice is (row q / 9, aligned float4 q % 9)
+  constexpr int VQ = BK / 4 + 1;
+  constexpr int NVA = VUA ? (BM * VQ + 255) / 256 : 1, NVB = VUB ? (BN * VQ + 255) / 256 : 1;
+  struct Regs {
+    float a[VUA ? 1 : NA];
+    float b[VUB ? 1 : NB];
+    floatx4 va[NVA];
+    floatx4 vb[NVB];
+    int k0;  // the slice's first k (VU: sets each row's shift at the LDS store)
+  };
+  auto load_slice = [&](int k0, bool tail, Regs& R) {
+    float(&ra)[VUA ? 1 : NA] = R.a;
+    float(&rb)[VUB ? 1 : NB] = R.b;
+    R.k0 = k0;
+    if constexpr (VUA) {
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) {
+        const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
+        const uint32_t p0 = mis_a + (uint32_t)(m0 + row) * sam + (uint32_t)k0;
+        const bool ok = q < BM * VQ;
+        R.va[i] = bload4(ra_, ok ? 4u * ((p0 & ~3u) + 4u * (uint32_t)j) : 0xFFFFFFF0u, 0);
+      }
+    }
+    if constexpr (VUB) {
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) {
+        const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
+        const uint32_t p0 = mis_b + (uint32_t)(n0 + row) * sbn + (uint32_t)k0;
+        const bool ok = q < BN * VQ;
+        R.vb[i] = bload4(rb_, ok ? 4u * ((p0 & ~3u) + 4u * (uint32_t)j) : 0xFFFFFFF0u, 0);
+      }
+    }
     if constexpr (V4) {
 #pragma unroll
       for (int i = 0; i < NA4; ++i) {
@@ -321,7 +366,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     }
     (void)tail;
     // A
-    if (AK) {
+    if constexpr (VUA) {
+    } else if (AK) {
       const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) * sam + (uint32_t)(k0 + a_k));
       const bool kok = !tail || (k0 + a_k < kend);
 #pragma unroll
@@ -339,7 +385,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       }
     }
     // B
-    if (BKC) {
+    if constexpr (VUB) {
+    } else if (BKC) {
       const uint32_t voff = 4u * ((uint32_t)(n0 + b_n) * sbn + (uint32_t)(k0 + b_k));
       const bool kok = !tail || (k0 + b_k < kend);
 #pragma unroll
@@ -359,7 +406,59 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       }
     }
   };
-  auto store_slice = [&](const float (&ra)[NA], const float (&rb)[NB], int stage) {
+  auto store_slice = [&](const Regs& R, int stage) {
+    const float(&ra)[VUA ? 1 : NA] = R.a;
+    const float(&rb)[VUB ? 1 : NB] = R.b;
+    if constexpr (VU) {
+      float* As = smem + stage * (LA + LB);
+      float* Bs = As + LA;
+      const int kend_rel = kend;  // components at k >= kend are zero
+      const int cur_k0 = R.k0;
+      if constexpr (VUA) {
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) {
+          const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
+          if (q < BM * VQ) {
+            const int m = (int)((mis_a + (uint32_t)(m0 + row) * sam + (uint32_t)cur_k0) & 3u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int kc = 4 * j + e - m;
+              if (kc >= 0 && kc < BK) As[row * SA + kc] = (cur_k0 + kc < kend_rel) ? R.va[i][e] : 0.f;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int mm = AK ? a_m + i * A_STEP : a_m;
+          const int kk = AK ? a_k : a_k + i * A_STEP;
+          As[AK ? (mm * SA + kk) : (kk * SA + mm)] = ra[i];
+        }
+      }
+      if constexpr (VUB) {
+#pragma unroll
+        for (int i = 0; i < NVB; ++i) {
+          const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
+          if (q < BN * VQ) {
+            const int m = (int)((mis_b + (uint32_t)(n0 + row) * sbn + (uint32_t)cur_k0) & 3u);
+            const bool one = a.ones_col && (n0 + row == N - 1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int kc = 4 * j + e - m;
+              if (kc >= 0 && kc < BK) Bs[row * SB + kc] = (cur_k0 + kc < kend_rel) ? (one ? 1.f : R.vb[i][e]) : 0.f;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int nn = BKC ? b_n + i * B_STEP : b_n;
+          const int kk = BKC ? b_k : b_k + i * B_STEP;
+          Bs[BKC ? (nn * SB + kk) : (kk * SB + nn)] = rb[i];
+        }
+      }
+      return;
+    }
     if constexpr (BF) {
       __bf16* Ah = reinterpret_cast<__bf16*>(smem) + stage * (LAH + LBH);
       __bf16* Bh = Ah + LAH;
@@ -494,26 +593,26 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   // LDS, slice s+1 waits in registers (its loads were issued one slice earlier) and slice s+2's
   // loads are in flight, so each global load has two slices of MFMA work to land behind.
   const int nsl = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  float ra0[NA], rb0[NB], ra1[NA], rb1[NB];
-  if (nsl > 0) load_slice(kbeg, kbeg + BK > kend, ra0, rb0);
-  if (nsl > 1) load_slice(kbeg + BK, kbeg + 2 * BK > kend, ra1, rb1);
-  if (nsl > 0) store_slice(ra0, rb0, 0);
+  Regs r0, r1;
+  if (nsl > 0) load_slice(kbeg, kbeg + BK > kend, r0);
+  if (nsl > 1) load_slice(kbeg + BK, kbeg + 2 * BK > kend, r1);
+  if (nsl > 0) store_slice(r0, 0);
   __syncthreads();
   for (int sl = 0; sl < nsl; sl += 2) {
     if (sl + 2 < nsl) {
       const int k2 = kbeg + (sl + 2) * BK;
-      load_slice(k2, k2 + BK > kend, ra0, rb0);
+      load_slice(k2, k2 + BK > kend, r0);
     }
     compute_slice(0);
-    if (sl + 1 < nsl) store_slice(ra1, rb1, 1);
+    if (sl + 1 < nsl) store_slice(r1, 1);
     __syncthreads();
     if (sl + 1 >= nsl) break;
     if (sl + 3 < nsl) {
       const int k3 = kbeg + (sl + 3) * BK;
-      load_slice(k3, k3 + BK > kend, ra1, rb1);
+      load_slice(k3, k3 + BK > kend, r1);
     }
     compute_slice(1);
-    if (sl + 2 < nsl) store_slice(ra0, rb0, 0);
+    if (sl + 2 < nsl) store_slice(r0, 0);
     __syncthreads();
   }
 
@@ -1185,9 +1284,29 @@ void launch_tile_v(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t 
     hipLaunchKernelGGL((k_gemm<BM, BN, false, false, V4, BF>), grid, dim3(256), 0, s, a, kc, ab, bb);
 }
 
+// The VU staging (k_gemm) for fp32 operands that fail v4_ok with at least one k-contiguous operand:
+// opt-in (AIMX_GEMM_VU=1). Bit-identical to the dword path but measured slower: c4 step 3.34 ->
+// 3.56 ms, c5 4.99 -> 5.86 ms, c3 unchanged (profiles/r03_gemm_vu_ab.txt) — the dword loads were
+// not what bounds these tiles; the shifted dword LDS writes and ~20 more VGPRs cost more.
+bool vu_on() {
+  const char* e = getenv("AIMX_GEMM_VU");  // read per call: tests switch it in one process
+  return e && atoi(e) == 1;
+}
+
 template <int BM, int BN>
 void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
   const bool bf = a.precision == AIMX_PREC_BF16;
+  if (!bf && !v4_ok(a) && (a.sak == 1 || a.sbk == 1) && vu_on()) {
+    const bool ak = (a.sak == 1), bk = (a.sbk == 1);
+    const int kc = (int)p.kchunk;
+    if (ak && bk)
+      hipLaunchKernelGGL((k_gemm<BM, BN, true, true, false, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    else if (ak)
+      hipLaunchKernelGGL((k_gemm<BM, BN, true, false, false, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    else
+      hipLaunchKernelGGL((k_gemm<BM, BN, false, true, false, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
+    return;
+  }
   if (v4_ok(a)) {
     if (bf)
       launch_tile_v<BM, BN, true, true>(a, p, grid, s, ab, bb);

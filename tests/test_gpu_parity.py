@@ -252,6 +252,65 @@ def test_gemm_layouts(M, N, K, layout):
     assert err < 2e-6, err
 
 
+def _gemm_raw(M, N, K, layout, off, pa, pb, ones=False):
+    """aimx_gemm on operands that start `off` floats into their buffers with row strides padded by
+    pa / pb floats; returns (C, bias-gradient column, fp64 reference)."""
+    import ctypes
+    from aimx import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K + off)
+    rA, cA = (M, K) if layout[0] == "N" else (K, M)
+    rB, cB = (K, N) if layout[1] == "N" else (N, K)
+    la, lb = cA + pa, cB + pb
+    bufA = torch.randn(off + rA * la, generator=g)
+    bufB = torch.randn(off + rB * lb, generator=g)
+    A = bufA[off:].view(rA, la)[:, :cA]
+    B = bufB[off:].view(rB, lb)[:, :cB]
+    dA, dB = bufA.to(DEV), bufB.to(DEV)
+    C = torch.zeros(M, N, device=DEV)
+    col = torch.zeros(M, device=DEV)
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = M, N + (1 if ones else 0), K
+    a.A = dA.data_ptr() + 4 * off
+    a.sam, a.sak = (la, 1) if layout[0] == "N" else (1, la)
+    a.B = dB.data_ptr() + 4 * off
+    a.sbk, a.sbn = (lb, 1) if layout[1] == "N" else (1, lb)
+    a.C, a.ldc = C.data_ptr(), N
+    a.act, a.dact_kind = -1, -1
+    if ones:
+        a.ones_col, a.col_out = 1, col.data_ptr()
+    a.counters, a.n_counters = _lib.counters(DEV).data_ptr(), _lib.N_COUNTERS
+    wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
+    ws = torch.empty(max(wsb // 4, 1) + 64 * 1024, device=DEV)
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    assert lib.aimx_gemm(ctypes.byref(a), torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    Am = A if layout[0] == "N" else A.t()
+    Bm = B if layout[1] == "N" else B.t()
+    return C.cpu(), col.cpu(), Am.double() @ Bm.double(), Am
+
+
+@pytest.mark.parametrize("M,N,K,layout,off,pa,pb,ones", [
+    (2049, 153, 153, "NT", 1, 0, 0, False), (2049, 153, 153, "NN", 2, 3, 0, False), (1003, 307, 307, "NT", 3, 0, 1, False),
+    (1003, 307, 306, "NN", 0, 1, 2, False), (517, 77, 153, "NT", 1, 0, 0, True), (33, 5, 3, "NT", 2, 0, 0, False),
+    (700, 153, 31, "NT", 3, 2, 0, False), (64, 160, 614, "NT", 1, 1, 3, False), (300, 45, 153, "TT", 2, 1, 0, False)])
+def test_gemm_unaligned_vector_staging_equals_dword_path(M, N, K, layout, off, pa, pb, ones, monkeypatch):
+    """The 16-byte staging of unaligned k-contiguous operands (k_gemm VU: c4/c5's D = 153 / 307
+    rows; opt-in AIMX_GEMM_VU=1) fills the same LDS tiles as the dword path, so the two results are
+    bit-identical: odd widths and row strides, every base misalignment, K tails shorter than a
+    slice, the ones column; and within 2e-6 of fp64."""
+    monkeypatch.setenv("AIMX_GEMM_VU", "1")
+    C1, col1, ref, Am = _gemm_raw(M, N, K, layout, off, pa, pb, ones)
+    monkeypatch.setenv("AIMX_GEMM_VU", "0")
+    C0, col0, _, _ = _gemm_raw(M, N, K, layout, off, pa, pb, ones)
+    assert torch.equal(C1, C0) and torch.equal(col1, col0)
+    err = (C1.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    if ones:
+        rs = Am.double().sum(1)
+        assert (col1.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
+
+
 @pytest.mark.parametrize("M,N,K,layout,off", [(2049, 153, 153, "NT", 1), (2049, 307, 153, "NN", 3),
                                                (153, 307, 4099, "TN", 2), (1027, 77, 301, "TT", 1),
                                                (5, 3, 7, "NT", 3)])
