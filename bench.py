@@ -434,9 +434,18 @@ def cpu_baseline(cfg, seconds=10.0, max_steps=40, one_thread_seconds=6.0, all_co
     model, count, affinity = cpu_info()
     if (count or 1) != threads:
         resa = _cpu_rate(cfg, count or 1, all_cores_seconds, 10)
+        quota = None
+        try:  # cgroup v2 CPU quota: "max period" or "<quota> <period>" (CPUs' worth of time)
+            q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
         res.update({"value_all_cores": resa["value"], "sample_all_cores": resa["sample"],
+                    "cgroup_cpu_quota": quota,
                     "note_all_cores": f"torch.set_num_threads(os.cpu_count() = {count}) on a box process whose "
-                                      f"CPU affinity holds {affinity} CPUs"})
+                                      f"CPU affinity holds {affinity} CPUs"
+                                      + (f" but whose cgroup quota is {quota} CPUs' worth of time: the threads "
+                                         "oversubscribe it" if quota is not None and quota < (count or 1) else "")})
     res.update({"value_1thread": res1["value"], "sample_1thread": res1["sample"], "cpu_model": model,
                 "cpu_count": count, "cpu_affinity": affinity})
     pvr = os.path.join(ROOT, "profiles", "port_vs_reference.json")
@@ -609,6 +618,7 @@ def main():
         sync = GradientSync(model.parameters(), unused=model.unused_parameters(), always=True)
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)  # clip(1.0) + Adam, trainer.py:163-164
     graphed = None
+    pad_mols_used = batches[0].num_graphs - B if args.graph else 0
     if args.graph:
         # Whole-step HIP-graph capture on static padded inputs (aimx.train.GraphedTrainStep): forward,
         # backward, the bucketed RCCL all-reduces overlapped with the backward (world > 1), clip and
@@ -719,8 +729,8 @@ def main():
             "config": {"workload": f"{args.config}: " + ("QM9-shaped" if cfg["source"] == "qm9" else "40-atom synthetic")
                        + f", hidden {cfg['hidden']}, {cfg['hops']} hops, {cfg['tasks']} task(s), attention pool, "
                        "train step fwd+bwd+clip+Adam, dropout 0.05"
-                       + (", HIP-graph replay of padded static batches (+8 padding molecules, excluded"
-                          " from the loss)" if args.graph else ", eager"),
+                       + (f", HIP-graph replay of padded static batches (+{pad_mols_used} padding molecules of"
+                          " <= 64 atoms, excluded from the loss)" if args.graph else ", eager"),
                        "feed": ("resident pool of %d batches in HBM" % args.pool if feeder is None else
                                 "native C++ collate + pinned H2D per step (PCIe-inclusive; not the metric value)"
                                 if args.feed == "native" else
