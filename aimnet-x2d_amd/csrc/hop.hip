@@ -483,6 +483,30 @@ int64_t env_i64(const char* name, int64_t dflt) {
   return e ? std::max<int64_t>(0, atoll(e)) : dflt;
 }
 
+// The launcher's A/B knobs, read from the environment once per process (an eager step calls the
+// launcher ~6 times; -1: unset, the launcher's own default applies)
+struct HopEnv {
+  int64_t rows_mode, tile_units, big_mul, col_cap, stage_bytes, flat, nt, interleave, spec;
+  bool no_seg;
+};
+const HopEnv& hop_env() {
+  static const HopEnv e = [] {
+    HopEnv v;
+    v.rows_mode = env_i64("AIMX_HOP_ROWS", 1);
+    v.tile_units = env_i64("AIMX_HOP_TILE_UNITS", -1);
+    v.big_mul = env_i64("AIMX_HOP_BIG_MUL", -1);
+    v.col_cap = env_i64("AIMX_HOP_COL_CAP", -1);
+    v.stage_bytes = env_i64("AIMX_HOP_STAGE_BYTES", -1);
+    v.flat = env_i64("AIMX_HOP_FLAT", 1);
+    v.nt = env_i64("AIMX_HOP_NT", 0);
+    v.interleave = env_i64("AIMX_HOP_INTERLEAVE", 1);
+    v.spec = env_i64("AIMX_HOP_SPEC", 1);
+    v.no_seg = getenv("AIMX_HOP_NO_SEG") != nullptr;
+    return v;
+  }();
+  return e;
+}
+
 }  // namespace
 }  // namespace aimx
 
@@ -509,7 +533,8 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   // rows that are not runs of 16-byte vectors (odd D, unaligned chunk offsets) go through LDS to
   // aligned 16-byte accesses (hop_rows.hip); AIMX_HOP_ROWS=0 keeps them here (dword lanes),
   // AIMX_HOP_ROWS=2 sends every width there (A/B)
-  static const int64_t rows_mode = env_i64("AIMX_HOP_ROWS", 1);
+  const HopEnv& E = hop_env();
+  const int64_t rows_mode = E.rows_mode;
   if ((vec < 4 && rows_mode == 1) || rows_mode == 2)
     return launch_gather_rows(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
                               add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream);
@@ -522,21 +547,21 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   // (rows of 129..256 vector units, c4's D = 153: two units per thread left 3-row tiles; 4 per
   // thread measured 20 us faster per c4 step, neutral at c2 and slower at c5's 307-wide rows —
   // profiles/r02_hop_tile_ab.txt; results never depend on the tiling)
-  const int64_t tile_units = env_i64("AIMX_HOP_TILE_UNITS", (upr_i > 128 && upr_i <= 256) ? 4 * threads : 2 * threads);
+  const int64_t tile_units = E.tile_units >= 0 ? E.tile_units : ((upr_i > 128 && upr_i <= 256) ? 4 * threads : 2 * threads);
   int64_t tr = std::min<int64_t>(kMaxTileRows, std::max<int64_t>(1, tile_units / upr_i));
   while (tr > 1 && cdiv(rows, tr) < 1024) tr = std::max<int64_t>(1, tr / 2);
   // output rows past the first chunk (hop chunks >= 1; out_rpc = rows per chunk) go in big tiles
   // once those rows hold >= 2048 tiles (8 per CU) to spare
   const int64_t split = (out_rpc > 0 && out_rpc < rows) ? out_rpc : rows;
-  const int64_t big_max = std::max<int64_t>(1, env_i64("AIMX_HOP_BIG_MUL", kBigMul));
+  const int64_t big_max = std::max<int64_t>(1, (E.big_mul >= 0 ? E.big_mul : kBigMul));
   const int64_t big_mul = std::max<int64_t>(1, std::min<int64_t>(big_max, cdiv(rows - split, tr) / 2048));
   const int64_t big = tr * big_mul;
   const int64_t nsmall = cdiv(split, tr);
   const int64_t blocks = nsmall + cdiv(rows - split, big);
   // LDS budget for the staged source span (AIMX_HOP_STAGE_BYTES overrides; 0 disables staging)
   // (the defaults keep 8 workgroups = 32 waves per CU resident: <= 20 KiB of LDS each)
-  const int64_t col_cap = (std::max<int64_t>(64, env_i64("AIMX_HOP_COL_CAP", kColCap)) + 3) / 4 * 4;
-  const int64_t stage_bytes = env_i64("AIMX_HOP_STAGE_BYTES", kStageBytes);
+  const int64_t col_cap = (std::max<int64_t>(64, (E.col_cap >= 0 ? E.col_cap : kColCap)) + 3) / 4 * 4;
+  const int64_t stage_bytes = (E.stage_bytes >= 0 ? E.stage_bytes : kStageBytes);
   int64_t xcap = stage_bytes / (4 * D);
   if (xcap < 2) xcap = 0;
   xcap = std::min<int64_t>(xcap, 4096);
@@ -568,14 +593,14 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   // source span is in use (the alignment is what makes the span equal the tile)
   // (tiles of >= 16 rows only: moving a cut of a 3-row tile up to a 40-atom molecule start turns
   // most tiles empty and the rest too tall to stage — c4/c5 measured 6-20 % slower)
-  a.seg = (row_seg && xcap > 0 && tr >= 16 && getenv("AIMX_HOP_NO_SEG") == nullptr) ? row_seg : nullptr;
+  a.seg = (row_seg && xcap > 0 && tr >= 16 && !E.no_seg) ? row_seg : nullptr;
   a.seg_stride = row_seg_stride;
   // chunks >= 1 contiguous after chunk 0 (a plain [h*N, D] output, as the hop op writes it)
   const bool contiguous = out_ld == D && (out_rpc <= 0 || out_cs == out_rpc * out_ld);
-  a.flat_zero = (contiguous && !add0 && !add1 && env_i64("AIMX_HOP_FLAT", 1) != 0) ? 1 : 0;
-  a.nt_store = env_i64("AIMX_HOP_NT", 0) != 0 ? 1 : 0;
-  a.interleave = env_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
-  a.spec_stage = env_i64("AIMX_HOP_SPEC", 1) != 0 ? 1 : 0;
+  a.flat_zero = (contiguous && !add0 && !add1 && E.flat != 0) ? 1 : 0;
+  a.nt_store = E.nt != 0 ? 1 : 0;
+  a.interleave = E.interleave != 0 ? 1 : 0;
+  a.spec_stage = E.spec != 0 ? 1 : 0;
   using KFn = void (*)(const HopArgs);
   const bool chunked = src_rpc > 0;
   KFn fn = vec == 4 ? (chunked ? k_gather_sum<4, true> : k_gather_sum<4, false>)

@@ -3,8 +3,8 @@ zero-store phase (chunks 1..h-1) and prints copy / fill reference rates on the s
 
 usage: python tools/hop_micro.py [--atoms 4000000] [--launches 20] [--env "A=1 B=2" ...] [--rounds 2]
 Each line: {"case", "ms", "alg_GBs"} (algorithmic bytes of that case / time). With --env, the hop
-cases run once per environment setting (AIMX_HOP_* knobs are read at every launch), interleaved
-over --rounds rounds so that box-to-box and drift effects cancel in the comparison.
+cases run once per environment setting, each in a child process (the launcher reads its AIMX_HOP_*
+knobs once per process), interleaved over --rounds rounds so that drift cancels in the comparison.
 """
 import argparse
 import json
@@ -40,7 +40,19 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--env", action="append", default=[])
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--label", default="")
     a = ap.parse_args()
+    if a.env:
+        import subprocess
+        for rnd in range(a.rounds):
+            for ev in a.env:
+                env = dict(os.environ)
+                for kv in ev.replace(",", " ").split():
+                    k, v = kv.split("=")
+                    env[k] = v
+                subprocess.run([sys.executable, os.path.abspath(__file__), "--atoms", str(a.atoms), "--launches",
+                                str(a.launches), "--label", f"[{ev}] r{rnd}"], env=env, check=True)
+        return
     dev = torch.device("cuda:0")
     cfg = bench.CONFIGS["c2"]
     batch = bench.make_batches(cfg, 1, 99, dev)[0]
@@ -54,20 +66,13 @@ def main():
     g0 = batch.num_graphs
     mol = (batch.batch.unsqueeze(0) + torch.arange(reps, device=dev, dtype=torch.int64).view(reps, 1) * g0).reshape(-1)
     plans = {h: GraphPlan(n, h, edges=edges, batch=mol, num_graphs=g0 * reps) for h in (3, 1)}
-    envs = a.env or [""]
     for rnd in range(a.rounds):
-        for ev in envs:
-            for kv in ev.replace(",", " ").split():
-                k, v = kv.split("=")
-                os.environ[k] = v
-            for h in (3, 1):
-                plan = plans[h]
-                ms = timeit(lambda: ops.hop(plan, x), a.launches)
-                b = 4 * (n * d + e + (h * n + 1) + h * n * d)
-                out.append({"case": f"hop h={h} [{ev}] r{rnd}", "ms": ms, "alg_GBs": b / ms / 1e6})
-                print(json.dumps(out[-1]), flush=True)
-            for kv in ev.replace(",", " ").split():
-                os.environ.pop(kv.split("=")[0], None)
+        for h in (3, 1):
+            plan = plans[h]
+            ms = timeit(lambda: ops.hop(plan, x), a.launches)
+            b = 4 * (n * d + e + (h * n + 1) + h * n * d)
+            out.append({"case": f"hop h={h} {a.label} r{rnd}", "ms": ms, "alg_GBs": b / ms / 1e6})
+            print(json.dumps(out[-1]), flush=True)
     del plans
     plan = GraphPlan(n, 2, edges=edges[:0])
     ms = timeit(lambda: ops.hop(plan, x), a.launches)
