@@ -390,8 +390,8 @@ def head_sync_timed_out(device):
     return buf is not None and int(buf[0].item()) != 0
 
 
-def head_cluster():
-    """Workgroups per 16-molecule tile of the fused head.
+def head_cluster(F=256):
+    """Workgroups per 16-molecule tile of the fused head (F: the ffn width).
 
     The clustered head (2 workgroups per tile, about 3 % of the c2 step) relies on both workgroups
     of a cluster running at once. Nothing guarantees that while other kernels share the CUs: RCCL
@@ -399,16 +399,23 @@ def head_cluster():
     is 2 only for a lone process (torch.distributed not initialised with world > 1, AIMX_AUX off);
     otherwise 1, which has no inter-workgroup wait at all. AIMX_HEAD_CLUSTER overrides both. A wait
     that still gives up poisons that launch's outputs with NaN (head.hip cluster_poisoned), so the
-    per-step NaN count of the train loop sees it on the step it happens."""
+    per-step NaN count of the train loop sees it on the step it happens. At F = 512 (c4) the
+    chain is 4x the work per tile and 4 workgroups per tile measured best (c4 step 3.278 ms vs
+    3.337 / 3.558 / 3.416 ms with 2 / 1 / 8; profiles/r03_head_f512_ab.txt)."""
     env = os.environ.get("AIMX_HEAD_CLUSTER")
     if env is not None:
         return int(env)
+    if not head_cluster_allowed():
+        return 1
+    return 4 if F > 256 else 2
+
+
+def head_cluster_allowed():
+    """False when other kernels may share the CUs with the clustered head (see head_cluster)."""
     if os.environ.get("AIMX_AUX", "0") == "1":
-        return 1
+        return False
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        return 1
-    return 2
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
 
 def ptr(t):

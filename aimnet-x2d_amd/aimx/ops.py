@@ -11,6 +11,8 @@ Each operator corresponds to a reference interface:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -1034,7 +1036,8 @@ def l1_loss(pred, target, weights=None, per_sample=False, rows=None, accum=None,
 # ---------------------------------------------------------------------------------------------
 # Fused post-pool head (gnn.py:252-258; MultiLayerPerceptron / LinearBlock layers.py:170-267)
 # ---------------------------------------------------------------------------------------------
-HEAD_MAX_F = 256
+# widest ffn the fused head takes (head.hip kMaxF = 512); AIMX_HEAD_MAX_F lowers it (A/B)
+HEAD_MAX_F = min(512, int(os.environ.get("AIMX_HEAD_MAX_F", "512")))
 
 
 class _Head(torch.autograd.Function):
@@ -1157,7 +1160,7 @@ def head(x_pooled, wp, bp, blocks, ws, bs, wo, bo, *, act, drop_p=0.0, training=
     if drop and seed is None:
         seed = torch.randint(0, 2 ** 62, (1,), device=x_pooled.device, dtype=torch.int64)
     spec = dict(nb=nb, act=kind, training=bool(training), drop_p=float(drop_p),
-                skip=tuple(bool(s) for s in (skips or [False] * nb)), cluster=_lib.head_cluster())
+                skip=tuple(bool(s) for s in (skips or [False] * nb)), cluster=_lib.head_cluster(int(wp.shape[0])))
     flat = []
     for b in blocks:
         flat += list(b)

@@ -29,7 +29,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int kR = 16;          // molecules per workgroup (the MFMA's 16 rows)
 constexpr int kBK = 32;         // k slice of one weight-ring slot
 constexpr int kP = 8;           // weight slices in flight from global memory (ring slots)
-constexpr int kMaxF = 256;      // widest ffn supported (activations [16][2F] stay in LDS)
+constexpr int kMaxF = 512;      // widest ffn supported (activations [16][2F] stay in LDS: 129 KiB at 512)
 constexpr int kS1 = kMaxF + 4;      // LDS row stride of the [16][F] activation buffers (= 4 mod 64:
 constexpr int kS2 = 2 * kMaxF + 4;  //  conflict-free ds_read_b128 of A) ... of the [16][2F] ones
 constexpr int kMaxBlocks = AIMX_HEAD_MAX_BLOCKS;
@@ -274,8 +274,8 @@ __device__ long long g_head_trace[2][64];
 #endif
 
 // LDS: three activation buffers [16][F], [16][F], [16][2F].
-// The array is one static size for every variant: 84 KiB, above half of the CU's 160 KiB, so a
-// clustered launch gets one workgroup per CU (the hand-off's measured form; see Cluster).
+// The array is one static size for every variant: 129 KiB (F up to 512), above half of the CU's
+// 160 KiB, so a clustered launch gets one workgroup per CU (the hand-off's measured form; see Cluster).
 constexpr int kActFloats = 2 * kR * kS1 + kR * kS2;
 constexpr int kHeadLdsFloats = std::max(kActFloats, 84 * 1024 / 4);
 

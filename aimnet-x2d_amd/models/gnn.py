@@ -193,13 +193,18 @@ class GNN(nn.Module):
 
     def _aimx_head_ok(self) -> bool:
         """The fused head covers the reference's post-pool chain when every LinearBlock is F -> F
-        with one activation and one dropout setting, F <= 256, F and the input width multiples of 32
-        (AIMX_NO_FUSED_HEAD=1 disables)."""
+        with one activation and one dropout setting, F <= 512 (above 256 only where clustered
+        launches are allowed), F and the input width multiples of 32 (AIMX_NO_FUSED_HEAD=1 disables)."""
         if os.environ.get("AIMX_NO_FUSED_HEAD", "0") == "1":
             return False
         pp, blocks = self.post_pooling_projection, list(self.ffn.layers)
         F = pp.out_features
         if not (32 <= F <= ops.HEAD_MAX_F and F % 32 == 0 and pp.in_features % 32 == 0 and 1 <= len(blocks) <= 8):
+            return False
+        # above F = 256 the fused chain pays off only clustered (c4: 3.28 ms with 4 workgroups per
+        # tile, 3.56 with 1 vs 3.32 on the module path): where clusters are not allowed (multi-rank,
+        # auxiliary stream) the module path runs instead
+        if F > 256 and _lib.head_cluster(F) == 1:
             return False
         if self.skip_transform.in_features != F or self.skip_transform.out_features != F or \
                 self.output_layer.in_features != 2 * F:
