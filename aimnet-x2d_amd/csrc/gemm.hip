@@ -36,6 +36,10 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 32;
+#ifndef AIMX_LDS_PIPE
+#define AIMX_LDS_PIPE 0  // 1: software-pipelined LDS fragment reads (k_wgrad_lds, k_gemm) — measured
+                         // neutral to slower (profiles/r03_lds_pipe_ab.txt), kept for A/B builds
+#endif
 
 // Epilogue over the NE outputs a thread owns, in two phases. epi_load issues every global load
 // the epilogue needs (C for beta, bias, residuals, act' pre-activation, dropout mask) and folds
@@ -568,10 +572,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     }
     const float* As = smem + stage * (LA + LB);
     const float* Bs = As + LA;
-#pragma unroll
-    for (int s = 0; s < BK / 4; ++s) {
+    auto rd = [&](int s, float (&af)[TM], float (&bf)[TN]) {
       const int kr = 4 * s + (lane >> 4);
-      float af[TM], bf[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int mm = wr * WM + i * 16 + (lane & 15);
@@ -582,11 +584,34 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
         const int nn = wc * WN + j * 16 + (lane & 15);
         bf[j] = Bs[BKC ? (nn * SB + kr) : (kr * SB + nn)];
       }
+    };
+#if AIMX_LDS_PIPE
+    // fragments of k step s + 1 read before the MFMAs of step s (see k_wgrad_lds)
+    float af[2][TM], bf[2][TN];
+    rd(0, af[0], bf[0]);
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+      const int c = s & 1;
+      if (s + 1 < BK / 4) rd(s + 1, af[c ^ 1], bf[c ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[c][i], bf[c][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+      float af[TM], bf[TN];
+      rd(s, af, bf);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+#endif
   };
 
   // Software pipeline: two register sets and two LDS stages. While slice s is multiplied from
@@ -1103,6 +1128,28 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
       }
       __syncthreads();
       if (s + kWbD < nsub) fetch(kb + (s + kWbD) * kWbK, ring[d]);
+#if AIMX_LDS_PIPE
+      // the fragments of k step k4 + 1 are read from LDS before the MFMAs of step k4 issue (two
+      // register sets; sched_barriers keep that order), so each step's MFMAs wait only for reads
+      // issued one step earlier instead of a full LDS round trip per step
+      float av[2], bv[2][kWbF];
+      auto rd = [&](int k4, int sl) {
+        const int r = (k4 * 4 + lk) * kLd + lm;
+        av[sl] = sA[r + w * 16];
+#pragma unroll
+        for (int j = 0; j < kWbF; ++j) bv[sl][j] = sB[r + j * 16];
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int k4 = 0; k4 < kWbK / 4; ++k4) {
+        const int c = k4 & 1;
+        if (k4 + 1 < kWbK / 4) rd(k4 + 1, c ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], bv[c][j], acc[j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#else
 #pragma unroll
       for (int k4 = 0; k4 < kWbK / 4; ++k4) {
         const int r = (k4 * 4 + lk) * kLd + lm;
@@ -1113,6 +1160,7 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
 #pragma unroll
         for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
       }
+#endif
     }
   }
 
