@@ -45,9 +45,12 @@ def train_step(model, batch, criterion, optimizer, sync=None, n_real=None):
 class GraphedTrainStep:
     """The train step captured as HIP graphs on a static padded batch (see module docstring).
 
-    Every replayed batch must have the static batch's layout (same padded atom / edge / molecule
-    counts and task count) and the same number of real molecules B (rows >= B of the per-molecule
-    outputs are padding and excluded from the loss). optimizer must be capturable (FusedAdam).
+    Every replayed batch must have the same number of real molecules B (rows >= B of the
+    per-molecule outputs are padding and excluded from the loss); a batch with the static batch's
+    layout (same padded atom / edge / molecule counts and task count) is replayed, any other (a
+    feeder's rare over-capacity batch, handed out unpadded) runs the same step eagerly on the same
+    parameters, gradients, optimizer state and loss accumulators. optimizer must be capturable
+    (FusedAdam).
 
     Data-parallel modes (`sync`: a utils.distributed.GradientSync; `ddp_graph` or the
     AIMX_DDP_GRAPH environment variable picks one):
@@ -79,16 +82,18 @@ class GraphedTrainStep:
         one = torch.ones((), dtype=torch.float32, device=dev)
         padded = getattr(criterion, "padded", None)
         B = self.B
+        self.eager_steps = 0
 
-        def fwd_bwd():
-            out, _, _ = model(*self.static.model_args())
+        def fwd_bwd(batch=None):
+            batch = self.static if batch is None else batch
+            out, _, _ = model(*batch.model_args())
             if padded is not None:
                 # fused L1: the padding rows' zero gradient in the loss's backward launch, and the
                 # step's loss sum / NaN flag / step count in its forward launch
-                loss = padded(out, self.static.targets[:B], B,
+                loss = padded(out, batch.targets[:B], B,
                               accum=(self.loss_sum, self.nan_count, self.steps, float(B)), grad_of=one)
             else:
-                loss = criterion(out[:B], self.static.targets[:B])
+                loss = criterion(out[:B], batch.targets[:B])
             loss.backward(one)  # d loss = 1 from a resident tensor (no per-step fill launch)
             if padded is None:
                 self.loss_sum.add_(loss.detach() * B)
@@ -172,11 +177,25 @@ class GraphedTrainStep:
             if n_real != self.B:  # e.g. a trailing partial batch: padding rows would enter the loss
                 raise ValueError(f"GraphedTrainStep: batch has {n_real} real molecules, the captured step "
                                  f"takes exactly {self.B} (run partial batches through train_step)")
+            if batch._layout != self.static._layout:
+                self._eager(batch)
+                return
             self.static.copy_(batch)
         self.g1.replay()
         if self.g2 is not None:
             self.sync.finish()
             self.g2.replay()
+
+    def _eager(self, batch):
+        """The captured step, run eagerly on a batch of another layout. The gradients are zeroed in
+        place (not set to None): the parameters keep the .grad tensors the graphs write and the
+        optimizer reads; with a GradientSync the same bucketed all-reduces run (hooks, finish)."""
+        self.eager_steps += 1
+        self.optimizer.zero_grad(set_to_none=False)
+        self._fwd_bwd(batch)
+        if self.sync is not None:
+            self.sync.finish()
+        self.optimizer.step()
 
 
 def train_epoch(model, batches: Iterable, criterion, optimizer, device, sync=None, graphed: Optional[
@@ -277,10 +296,8 @@ def main(argv=None):
     pad = not a.eager
     n_max = e_max = pm = 0
     if pad:
-        probe = feed.HostCollator(a.hops, 2)
-        sz = np.array([probe.plan(store, shard[rng.permutation(len(shard))[:B]]) for _ in range(64)])
-        n_max, e_max = int(sz[:, 0].max() * 1.05) + 64, int(sz[:, 1].max() * 1.05) + 256
-        pm = adata.pad_mols_for(n_max, int(sz[:, 0].min() * 0.95))
+        n_max, e_max, pm = feed.static_capacity(feed.HostCollator(a.hops, 2), store,
+                                                [shard[rng.permutation(len(shard))[:B]] for _ in range(256)])
 
     def epoch_batches(ep):
         p = np.random.default_rng(a.seed * 1000 + ep).permutation(len(shard))

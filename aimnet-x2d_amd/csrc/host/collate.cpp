@@ -13,6 +13,7 @@
 // the caller's (pinned) buffers by the same workers — no intermediate Python objects and one
 // contiguous write stream per worker.
 #include "../../../include/aimx_host.h"
+#include "store.h"
 
 #include <algorithm>
 #include <atomic>
@@ -21,6 +22,7 @@
 #include <functional>
 #include <mutex>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -32,8 +34,17 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 class Pool {
  public:
+  // A host that refuses more threads (EAGAIN under a pid / task limit) gets a smaller pool, not
+  // std::terminate from a half-built thread vector.
   explicit Pool(int n) : n_(std::max(1, n)) {
-    for (int i = 1; i < n_; ++i) th_.emplace_back([this, i] { loop(i); });
+    for (int i = 1; i < n_; ++i) {
+      try {
+        th_.emplace_back([this, i] { loop(i); });
+      } catch (const std::system_error&) {
+        n_ = i;
+        break;
+      }
+    }
   }
   ~Pool() {
     {
@@ -186,19 +197,6 @@ bool bfs_molecule(int32_t n, const int32_t* bonds, int64_t nb, int32_t max_hops,
 // ---------------------------------------------------------------------------------------------
 // Store
 // ---------------------------------------------------------------------------------------------
-struct aimx_mol_store {
-  int64_t n_mols = 0;
-  int32_t n_feat = 0, n_tasks = 0, cached_hops = 0;
-  std::vector<int64_t> atom_ptr, bond_ptr;
-  std::vector<int32_t> bonds, feats;
-  std::vector<float> targets, charge;
-  // cached hop pairs: pair_ptr[m] .. pair_ptr[m+1] (uint16 (u, w) interleaved, hop-major);
-  // hop sizes per molecule in hop_len[m * cached_hops + h]
-  std::vector<int64_t> pair_ptr;
-  std::vector<uint16_t> pairs;
-  std::vector<int32_t> hop_len;
-};
-
 struct aimx_collator {
   int32_t max_hops;
   Pool pool;

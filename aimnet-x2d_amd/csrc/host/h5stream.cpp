@@ -12,8 +12,8 @@
 //                  subgroup sae (attrs applied (bool), note (str)); optional target_columns (str[])
 // h5py is not part of this toolchain; the library is the HDF5 C library itself (1.10, as h5py
 // links), so the files are the ones h5py reads and writes. Records are decoded by
-// pickle_lite.h (data only; nothing executes) in parallel worker threads and packed into a
-// store (aimx_store_create_hops) in one pass, with no Python objects per molecule.
+// pickle_lite.h (data only; nothing executes) in parallel worker threads, in file order, and
+// written into a new store (store.h) in request order, with no Python objects per molecule.
 #include <fcntl.h>
 #include <hdf5.h>
 #include <sys/mman.h>
@@ -26,15 +26,18 @@
 #include <cstdio>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 #include "../../../include/aimx_h5.h"
 #include "../../../include/aimx_host.h"
 #include "pickle_lite.h"
+#include "store.h"
 
 using aimx_pickle::Kind;
 using aimx_pickle::Obj;
@@ -43,16 +46,16 @@ namespace {
 
 const char* kFeatureKeys[4] = {"atom_type", "hydrogen_count", "degree", "hybridization"};
 
-// Decoded molecules in flat form, appended record after record (one Part per worker: no
-// allocation per molecule once the buffers have grown).
+// Decoded molecules in flat form, appended record after record (one Part per worker, kept by the
+// reader between reads: no allocation per molecule or per read once the buffers have grown).
 struct Part {
   std::vector<int32_t> n_atoms;  // per molecule
   std::vector<int32_t> feats;    // [atoms, 4]
   std::vector<int64_t> hop_len;  // [molecules, n_hops]
-  std::vector<int32_t> pairs;    // (u, w) rows, hop-major per molecule
+  std::vector<uint16_t> pairs;   // (u, w) rows, hop-major per molecule (local indices < 65536)
   std::vector<float> target;     // [molecules, n_tasks]
   std::vector<float> charge;     // per molecule
-  std::vector<int64_t> pos;      // requested position of each molecule
+  std::vector<int64_t> req;      // request index of each molecule
   void clear() {
     n_atoms.clear();
     feats.clear();
@@ -60,7 +63,7 @@ struct Part {
     pairs.clear();
     target.clear();
     charge.clear();
-    pos.clear();
+    req.clear();
   }
 };
 
@@ -137,7 +140,7 @@ bool decode_record(const uint8_t* p, size_t n, int32_t n_hops, int32_t n_tasks, 
     });
   }
   if (good) m->pairs.resize(p0 + size_t(2 * tot));
-  int32_t* dst = m->pairs.data() + p0;
+  uint16_t* dst = m->pairs.data() + p0;
   for (int32_t h = 0; h < n_hops && good; ++h) {
     const Obj& e = *mh->items[h];
     const int64_t E = e.shape[1];
@@ -147,8 +150,8 @@ bool decode_record(const uint8_t* p, size_t n, int32_t n_hops, int32_t n_tasks, 
       for (int64_t q = 0; q < E; ++q) {
         const int64_t u = get(e.fortran ? 2 * q : q), w = get(e.fortran ? 2 * q + 1 : E + q);
         in_range &= u >= 0 && u < na && w >= 0 && w < na;
-        dst[2 * q] = (int32_t)u;
-        dst[2 * q + 1] = (int32_t)w;
+        dst[2 * q] = (uint16_t)u;
+        dst[2 * q + 1] = (uint16_t)w;
       }
     }) && in_range;
     dst += 2 * E;
@@ -178,16 +181,23 @@ void parallel_for(int64_t n, int threads, F&& f) {
   std::vector<std::thread> th;
   std::exception_ptr first;
   std::mutex mu;
+  auto work = [&f, &first, &mu](int t, int64_t lo, int64_t hi) {
+    try {
+      f(t, lo, hi);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(mu);
+      if (!first) first = std::current_exception();
+    }
+  };
   for (int t = 0; t < threads; ++t) {
     const int64_t lo = n * t / threads, hi = n * (t + 1) / threads;
-    th.emplace_back([&f, &first, &mu, t, lo, hi] {
-      try {
-        f(t, lo, hi);
-      } catch (...) {
-        std::lock_guard<std::mutex> g(mu);
-        if (!first) first = std::current_exception();
-      }
-    });
+    bool spawned = false;
+    try {
+      th.emplace_back(work, t, lo, hi);
+      spawned = true;
+    } catch (const std::system_error&) {  // no more threads on this host: run the range here
+    }
+    if (!spawned) work(t, lo, hi);
   }
   for (auto& x : th) x.join();
   if (first) std::rethrow_exception(first);
@@ -364,6 +374,7 @@ struct aimx_h5_reader {
   const uint8_t* map = nullptr;
   size_t map_size = 0;
   uint64_t desc = 0, addr_base = 0;
+  std::vector<Part> parts;  // decode buffers, reused read after read (one read at a time per handle)
   ~aimx_h5_reader() {
     if (map) munmap(const_cast<uint8_t*>(map), map_size);
     if (memtype >= 0) H5Tclose(memtype);
@@ -406,7 +417,9 @@ static void try_direct(aimx_h5_reader* r, const char* path) {
   if (fd < 0) return;
   struct stat st;
   void* m = MAP_FAILED;
-  if (fstat(fd, &st) == 0 && st.st_size > 0) m = mmap(nullptr, size_t(st.st_size), PROT_READ, MAP_SHARED, fd, 0);
+  const char* pe = std::getenv("AIMX_H5_POPULATE");
+  const int flags = MAP_SHARED | (pe && pe[0] == '1' ? MAP_POPULATE : 0);
+  if (fstat(fd, &st) == 0 && st.st_size > 0) m = mmap(nullptr, size_t(st.st_size), PROT_READ, flags, fd, 0);
   ::close(fd);
   if (m == MAP_FAILED) return;
   const uint8_t* map = static_cast<const uint8_t*>(m);
@@ -549,53 +562,49 @@ int aimx_h5_read_store(aimx_h5_reader* r, const int64_t* pos, int64_t n, int32_t
     if (pos[k] < 0 || pos[k] >= r->n_records) return AIMX_HOST_EARG;
   const int P = (int)std::max<int64_t>(1, std::min<int64_t>(std::max(n_threads, 1), n));
   try {
-    std::vector<Part> parts(static_cast<size_t>(P));
-    // decode records [lo, hi) of the request into part t (request order within and across parts)
+    if ((int)r->parts.size() < P) r->parts.resize(size_t(P));
+    // visit records in file order (the request sorted by record index, stable): the mapped file
+    // and HDF5's point reads are walked forward; the store is still written in request order
+    std::vector<int64_t> vis(static_cast<size_t>(n));
+    for (int64_t k = 0; k < n; ++k) vis[k] = k;
+    std::stable_sort(vis.begin(), vis.end(),
+                     [&](int64_t a, int64_t b) { return r->index_map[pos[a]] < r->index_map[pos[b]]; });
+    // decode visits [lo, hi) into part t
     auto decode_range = [&](int t, int64_t lo, int64_t hi, auto&& bytes_of) {
-      Part& m = parts[size_t(t)];
+      Part& m = r->parts[size_t(t)];
       m.clear();
-      for (int64_t k = lo; k < hi; ++k) {
+      for (int64_t j = lo; j < hi; ++j) {
         const uint8_t* p = nullptr;
         size_t len = 0;
-        if (bytes_of(k, &p, &len) && decode_record(p, len, n_hops, n_tasks, &m)) m.pos.push_back(pos[k]);
+        if (bytes_of(j, &p, &len) && decode_record(p, len, n_hops, n_tasks, &m)) m.req.push_back(vis[j]);
       }
     };
     if (n > 0 && r->map) {
       // direct path: every worker finds and decodes its records in the mapped file
       std::atomic<bool> corrupt{false};
       parallel_for(n, P, [&](int t, int64_t lo, int64_t hi) {
-        decode_range(t, lo, hi, [&](int64_t k, const uint8_t** p, size_t* len) {
-          const int rc = direct_record(r->map, r->map_size, r->desc, r->addr_base, r->index_map[pos[k]], p, len);
+        decode_range(t, lo, hi, [&](int64_t j, const uint8_t** p, size_t* len) {
+          const int rc = direct_record(r->map, r->map_size, r->desc, r->addr_base, r->index_map[pos[vis[j]]], p, len);
           if (rc < 0) corrupt = true;
           return rc == 1;
         });
       });
       if (corrupt) return AIMX_H5_EFORMAT;
     } else if (n > 0) {
-      // records index_map[pos[k]]: one hyperslab when contiguous, else a point list in file order
-      // (HDF5 reads a sorted point list several times faster), mapped back to request order
+      // one hyperslab when the visits are a contiguous run, else a point list (already in file
+      // order: HDF5 reads a sorted point list several times faster); raw[j] is visit j's record
       std::vector<hsize_t> coord(static_cast<size_t>(n));
       bool run = true;
-      for (int64_t k = 0; k < n; ++k) {
-        coord[k] = (hsize_t)r->index_map[pos[k]];
-        if (k && coord[k] != coord[k - 1] + 1) run = false;
+      for (int64_t j = 0; j < n; ++j) {
+        coord[j] = (hsize_t)r->index_map[pos[vis[j]]];
+        if (j && coord[j] != coord[j - 1] + 1) run = false;
       }
-      std::vector<int64_t> slot(static_cast<size_t>(n));  // raw index of request k
       herr_t sel;
       if (run) {
-        for (int64_t k = 0; k < n; ++k) slot[k] = k;
         hsize_t start[1] = {coord[0]}, count[1] = {(hsize_t)n};
         sel = H5Sselect_hyperslab(r->space, H5S_SELECT_SET, start, nullptr, count, nullptr);
       } else {
-        std::vector<int64_t> order(static_cast<size_t>(n));
-        for (int64_t k = 0; k < n; ++k) order[k] = k;
-        std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return coord[a] < coord[b]; });
-        std::vector<hsize_t> sorted(static_cast<size_t>(n));
-        for (int64_t j = 0; j < n; ++j) {
-          sorted[j] = coord[order[j]];
-          slot[order[j]] = j;
-        }
-        sel = H5Sselect_elements(r->space, H5S_SELECT_SET, (size_t)n, sorted.data());
+        sel = H5Sselect_elements(r->space, H5S_SELECT_SET, (size_t)n, coord.data());
       }
       std::vector<hvl_t> raw(static_cast<size_t>(n));
       hsize_t md[1] = {(hsize_t)n};
@@ -606,8 +615,8 @@ int aimx_h5_read_store(aimx_h5_reader* r, const int64_t* pos, int64_t n, int32_t
       }
       try {
         parallel_for(n, P, [&](int t, int64_t lo, int64_t hi) {
-          decode_range(t, lo, hi, [&](int64_t k, const uint8_t** p, size_t* len) {
-            const hvl_t& v = raw[size_t(slot[k])];
+          decode_range(t, lo, hi, [&](int64_t j, const uint8_t** p, size_t* len) {
+            const hvl_t& v = raw[size_t(j)];
             *p = (const uint8_t*)v.p;
             *len = v.len;
             return v.len > 0;
@@ -621,41 +630,71 @@ int aimx_h5_read_store(aimx_h5_reader* r, const int64_t* pos, int64_t n, int32_t
       H5Dvlen_reclaim(r->memtype, ms, H5P_DEFAULT, raw.data());
       H5Sclose(ms);
     }
-    // pack the parts (request order) into the store's flat arrays, each part by its own worker
-    std::vector<int64_t> mo(size_t(P) + 1, 0), ao(size_t(P) + 1, 0), po(size_t(P) + 1, 0);
-    for (int t = 0; t < P; ++t) {
-      const Part& m = parts[size_t(t)];
-      mo[t + 1] = mo[t] + (int64_t)m.n_atoms.size();
-      ao[t + 1] = ao[t] + (int64_t)m.feats.size() / 4;
-      po[t + 1] = po[t] + (int64_t)m.pairs.size() / 2;
-    }
-    const int64_t nv = mo[P];
-    std::vector<int64_t> atom_ptr(size_t(nv) + 1, 0), hop_ptr(size_t(nv) * n_hops + 1, 0);
-    std::vector<int32_t> feats(static_cast<size_t>(ao[P] * 4)), pairs(static_cast<size_t>(po[P] * 2));
-    std::vector<float> targets(size_t(nv) * n_tasks), charge(static_cast<size_t>(nv));
+    // request-order placement: molecule, atom and pair offsets of every valid request
+    std::vector<int32_t> na_k(static_cast<size_t>(n), -1);
+    std::vector<int64_t> np_k(static_cast<size_t>(n), 0);
     parallel_for(P, P, [&](int, int64_t lo, int64_t hi) {
       for (int64_t t = lo; t < hi; ++t) {
-        const Part& m = parts[size_t(t)];
-        const int64_t nm = mo[t + 1] - mo[t];
-        std::copy(m.feats.begin(), m.feats.end(), feats.begin() + ao[t] * 4);
-        std::copy(m.pairs.begin(), m.pairs.end(), pairs.begin() + po[t] * 2);
-        std::copy(m.target.begin(), m.target.end(), targets.begin() + mo[t] * n_tasks);
-        std::copy(m.charge.begin(), m.charge.end(), charge.begin() + mo[t]);
-        if (valid_pos) std::copy(m.pos.begin(), m.pos.end(), valid_pos + mo[t]);
-        int64_t a = ao[t], q = po[t];
-        for (int64_t j = 0; j < nm; ++j) {
-          a += m.n_atoms[j];
-          atom_ptr[mo[t] + j + 1] = a;
-          for (int32_t h = 0; h < n_hops; ++h) {
-            q += m.hop_len[j * n_hops + h];
-            hop_ptr[(mo[t] + j) * n_hops + h + 1] = q;
-          }
+        const Part& m = r->parts[size_t(t)];
+        for (size_t i = 0; i < m.req.size(); ++i) {
+          int64_t q = 0;
+          for (int32_t h = 0; h < n_hops; ++h) q += m.hop_len[i * n_hops + h];
+          na_k[m.req[i]] = m.n_atoms[i];
+          np_k[m.req[i]] = q;
+        }
+      }
+    });
+    std::vector<int64_t> mol_k(static_cast<size_t>(n)), atom_k(static_cast<size_t>(n)), pair_k(static_cast<size_t>(n));
+    int64_t nv = 0, NA = 0, NP = 0;
+    for (int64_t k = 0; k < n; ++k) {
+      mol_k[k] = nv;
+      atom_k[k] = NA;
+      pair_k[k] = NP;
+      if (na_k[k] >= 0) {
+        ++nv;
+        NA += na_k[k];
+        NP += np_k[k];
+      }
+    }
+    // the store, filled in place by the workers, each copying its own part's molecules
+    auto* s = new aimx_mol_store();
+    std::unique_ptr<aimx_mol_store> own(s);
+    s->n_mols = nv;
+    s->n_feat = 4;
+    s->n_tasks = n_tasks;
+    s->cached_hops = n_hops;
+    s->atom_ptr.resize(size_t(nv) + 1);
+    s->bond_ptr.assign(size_t(nv) + 1, 0);
+    s->feats.resize(size_t(NA) * 4);
+    s->targets.resize(size_t(nv) * n_tasks);
+    s->charge.resize(size_t(nv));
+    s->hop_len.resize(size_t(nv) * n_hops);
+    s->pair_ptr.resize(size_t(nv) + 1);
+    s->pairs.resize(size_t(NP) * 2);
+    s->atom_ptr[0] = 0;
+    s->pair_ptr[0] = 0;
+    parallel_for(P, P, [&](int, int64_t lo, int64_t hi) {
+      for (int64_t t = lo; t < hi; ++t) {
+        const Part& m = r->parts[size_t(t)];
+        int64_t fa = 0, fq = 0;  // this molecule's atom / pair offset in the part
+        for (size_t i = 0; i < m.req.size(); ++i) {
+          const int64_t k = m.req[i], mol = mol_k[k], na = na_k[k], nq = np_k[k];
+          std::memcpy(&s->feats[size_t(atom_k[k]) * 4], &m.feats[size_t(fa) * 4], sizeof(int32_t) * 4 * na);
+          std::memcpy(&s->pairs[size_t(pair_k[k]) * 2], &m.pairs[size_t(fq) * 2], sizeof(uint16_t) * 2 * nq);
+          for (int32_t h = 0; h < n_hops; ++h) s->hop_len[mol * n_hops + h] = int32_t(m.hop_len[i * n_hops + h]);
+          std::memcpy(&s->targets[size_t(mol) * n_tasks], &m.target[i * n_tasks], sizeof(float) * n_tasks);
+          s->charge[mol] = m.charge[i];
+          s->atom_ptr[mol + 1] = atom_k[k] + na;
+          s->pair_ptr[mol + 1] = pair_k[k] + nq;
+          if (valid_pos) valid_pos[mol] = pos[k];
+          fa += na;
+          fq += nq;
         }
       }
     });
     if (n_valid) *n_valid = nv;
-    return aimx_store_create_hops(nv, atom_ptr.data(), feats.data(), 4, n_hops, hop_ptr.data(), pairs.data(),
-                                  targets.data(), n_tasks, charge.data(), out);
+    *out = own.release();
+    return AIMX_HOST_OK;
   } catch (const std::bad_alloc&) {
     return AIMX_HOST_ENOMEM;
   }

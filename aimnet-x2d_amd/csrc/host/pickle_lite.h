@@ -249,12 +249,11 @@ class Decoder {
     st_.pop_back();
     return true;
   }
-  bool pop_mark(std::vector<Ref>* out) {
+  // the stack above the innermost MARK: [*from, st_.end()) (false without a mark)
+  bool mark_from(size_t* from) {
     if (marks_.empty() || marks_.back() > st_.size()) return false;
-    const size_t m = marks_.back();
+    *from = marks_.back();
     marks_.pop_back();
-    out->assign(st_.begin() + m, st_.end());
-    st_.resize(m);
     return true;
   }
   bool tuple_n(size_t n) {
@@ -509,10 +508,11 @@ class Decoder {
       case 0x86: return tuple_n(2);
       case 0x87: return tuple_n(3);
       case 't': {
-        std::vector<Ref> v;
-        if (!pop_mark(&v)) return false;
+        size_t m;
+        if (!mark_from(&m)) return false;
         auto t = mk(Kind::Tuple);
-        t->items = std::move(v);
+        t->items.assign(st_.begin() + m, st_.end());
+        st_.resize(m);
         st_.push_back(t);
         return true;
       }
@@ -521,10 +521,11 @@ class Decoder {
         st_.back()->items.push_back(a);
         return true;
       case 'e': {  // APPENDS
-        std::vector<Ref> v;
-        if (!pop_mark(&v) || st_.empty() || st_.back()->k != Kind::List) return false;
-        auto& L = st_.back()->items;
-        L.insert(L.end(), v.begin(), v.end());
+        size_t m;
+        if (!mark_from(&m) || m == 0 || st_[m - 1]->k != Kind::List) return false;
+        auto& L = st_[m - 1]->items;
+        L.insert(L.end(), st_.begin() + m, st_.end());
+        st_.resize(m);
         return true;
       }
       case 's':  // SETITEM
@@ -533,10 +534,11 @@ class Decoder {
         st_.back()->items.push_back(b);
         return true;
       case 'u': {  // SETITEMS
-        std::vector<Ref> v;
-        if (!pop_mark(&v) || (v.size() & 1) || st_.empty() || st_.back()->k != Kind::Dict) return false;
-        auto& D = st_.back()->items;
-        D.insert(D.end(), v.begin(), v.end());
+        size_t m;
+        if (!mark_from(&m) || ((st_.size() - m) & 1) || m == 0 || st_[m - 1]->k != Kind::Dict) return false;
+        auto& D = st_[m - 1]->items;
+        D.insert(D.end(), st_.begin() + m, st_.end());
+        st_.resize(m);
         return true;
       }
       case 0x93:  // STACK_GLOBAL

@@ -105,11 +105,10 @@ def native_feeder(cfg, seed, device, threads, pad):
                                               precompute_hops=cfg["hops"], threads=threads)
     B = cfg["batch"]
     n_max = e_max = pm = 0
-    if pad:  # static capacity: the largest of 256 sampled batches + margin (overflow raises HostError)
-        probe = feed.HostCollator(cfg["hops"], threads)
-        sizes = np.array([probe.plan(store, rng.integers(0, len(store), B)) for _ in range(256)])
-        n_max, e_max = int(sizes[:, 0].max() * 1.03) + 64, int(sizes[:, 1].max() * 1.03) + 256
-        pm = pad_mols_for(n_max, int(sizes[:, 0].min()))
+    if pad:  # static capacity from 256 sampled batches (a batch over it is stepped eagerly)
+        n_max, e_max, pm = feed.static_capacity(feed.HostCollator(cfg["hops"], threads), store,
+                                                [rng.integers(0, len(store), B) for _ in range(256)],
+                                                least_pad_mols=PAD_MOLS)
 
     def index_stream():
         while True:
@@ -126,7 +125,7 @@ def pad_mols_for(n_max, n_min):
 STREAM_INFO = {}
 
 
-def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None):
+def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None, read_threads=None):
     """Endless BatchFeeder over an HDF5 molecule stream in the reference's dataset format
     (features.py:381-431 / molecular.py:102-329): a synthetic file of n_mols molecules (made once
     on this host by rank 0), this rank's equal shard read in chunks by the C++ reader (HDF5 C
@@ -146,25 +145,25 @@ def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None):
         print(f"bench: wrote {n_mols}-molecule stream {path} in {info['write_s']} s", file=sys.stderr)
     if world > 1:
         dist.barrier()
+    read_threads = read_threads or threads
     stream = h5.HDF5MolecularStream(path, shuffle=True, ddp_enabled=world > 1, rank=rank, world_size=world,
-                                    n_hops=cfg["hops"], n_tasks=cfg["tasks"], threads=threads)
+                                    n_hops=cfg["hops"], n_tasks=cfg["tasks"], threads=read_threads)
     # the reader's own rate (shuffled positions, the feed's threads): read + decode + pack into stores
     pos = stream.positions(0)[:65536]
     t0 = time.perf_counter()
     for s0 in range(0, len(pos), 16384):
-        stream.file.read_store(pos[s0:s0 + 16384], cfg["hops"], cfg["tasks"], threads)
+        stream.file.read_store(pos[s0:s0 + 16384], cfg["hops"], cfg["tasks"], read_threads)
     info.update(bytes=os.path.getsize(path), direct_read=stream.file.direct_read,
-                read_mol_per_s=round(len(pos) / (time.perf_counter() - t0)), read_threads=threads)
+                read_mol_per_s=round(len(pos) / (time.perf_counter() - t0)), read_threads=read_threads)
     STREAM_INFO.update(info)
     B = cfg["batch"]
     n_max = e_max = pm = 0
-    if pad:  # static capacity from the first chunk's batches + margin (an overflow raises HostError)
+    if pad:  # static capacity from 256 batches of the first chunk (a batch over it is stepped eagerly)
         store, _ = stream.file.read_store(stream.positions(0)[:16384], cfg["hops"], cfg["tasks"], threads)
-        probe = feed.HostCollator(cfg["hops"], threads)
         rng = np.random.default_rng(rank)
-        sizes = np.array([probe.plan(store, rng.integers(0, len(store), B)) for _ in range(256)])
-        n_max, e_max = int(sizes[:, 0].max() * 1.08) + 64, int(sizes[:, 1].max() * 1.08) + 256
-        pm = pad_mols_for(n_max, int(sizes[:, 0].min() * 0.97))
+        n_max, e_max, pm = feed.static_capacity(feed.HostCollator(cfg["hops"], threads), store,
+                                                [rng.integers(0, len(store), B) for _ in range(256)],
+                                                least_pad_mols=PAD_MOLS)
 
     def batches():
         epoch = 0
@@ -553,6 +552,7 @@ def main():
     ap.add_argument("--stream-mols", type=int, default=200_000, help="molecules in the --feed stream file")
     ap.add_argument("--stream-path", default=None, help="--feed stream file (default: generated under $TMPDIR)")
     ap.add_argument("--feed-threads", type=int, default=8)
+    ap.add_argument("--read-threads", type=int, default=None, help="HDF5 reader threads (default: --feed-threads)")
     ap.add_argument("--amp", action="store_true",
                     help="the reference's --mixed_precision path (trainer.py:134): the step runs under "
                          "torch.autocast('cuda', bfloat16) -> bf16 MFMA operands, fp32 accumulation in the GEMMs")
@@ -587,7 +587,7 @@ def main():
         batches = [next(feeder)]
     elif args.feed == "stream":
         feeder = stream_feeder(cfg, rank, world, device, args.feed_threads, args.graph, args.stream_mols,
-                               args.stream_path)
+                               args.stream_path, read_threads=args.read_threads)
         batches = [next(feeder)]
     else:
         batches = make_batches(cfg, args.pool, 1234 + rank, device, pad=args.graph)
@@ -747,6 +747,8 @@ def main():
             line["eager"] = eager
         if feed_stats is not None:
             line["feed_ms_per_batch"] = feed_stats
+            if graphed is not None:  # steps (warmup included) whose batch was over the static capacity
+                line["graph_eager_steps"] = graphed.eager_steps
         if STREAM_INFO:
             line["stream_file"] = dict(STREAM_INFO)
         if sync is not None:

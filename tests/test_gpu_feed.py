@@ -118,3 +118,34 @@ def test_feeder_ring_reuse_is_race_free():
     torch.cuda.synchronize()
     for b, w in zip(kept, want):
         assert same(b._blob.cpu(), w)
+
+
+def test_overflow_batch_goes_out_unpadded():
+    """Static shapes from a few sample batches: a later batch above that capacity is handed out
+    unpadded (its own layout, bit-exact to the dynamic collate) and counted, the others padded."""
+    asset = QM9Asset()
+    store = feed.HostStore.from_qm9_asset(asset, precompute_hops=3, threads=2)
+    rng = np.random.default_rng(2)
+    idxs = [rng.integers(0, len(asset), 64) for _ in range(10)]
+    c = feed.HostCollator(3, 2)
+    sizes = np.array([c.plan(store, i) for i in idxs])
+    big = int(np.argmax(sizes[:, 1]))
+    rest = [k for k in range(len(idxs)) if k != big]
+    n_max, e_max = int(sizes[rest, 0].max()) + 3, int(sizes[rest, 1].max())
+    assert sizes[big, 1] > e_max
+    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=n_max, e_max=e_max, pad_mols=6)
+    got = [b for b in f]
+    torch.cuda.synchronize()
+    assert f.stats()["overflow"] == 1
+    for k, (b, idx) in enumerate(zip(got, idxs)):
+        col = adata.collate(asset.molecules(idx), 3)
+        tg, tc = asset.targets[idx], asset.total_charge[idx]
+        if k != big:
+            col = adata.pad_collated(col, n_max, e_max, len(idx), 6)
+            tg = np.concatenate([tg, np.zeros((6, tg.shape[1]), np.float32)])
+            tc = np.concatenate([tc, np.zeros(6, np.float32)])
+        ref = adata.DeviceBatch(col, DEV, targets=tg, total_charges=tc, csr_hops=3)
+        assert b._layout == ref._layout, k
+        for x, y in zip(_fields(b), _fields(ref)):
+            assert torch.equal(x, y)
+        assert b.real_graphs == len(idx)

@@ -63,6 +63,33 @@ def test_graphed_step_matches_eager_step():
         assert (p1 - p2).abs().max().item() <= 1e-5 * max(1.0, p1.abs().max().item()), k
 
 
+def test_graphed_step_runs_off_layout_batch_eagerly():
+    """A batch over the static capacity arrives unpadded (BatchFeeder overflow): the graphed step
+    runs it eagerly on the same parameters, gradients, optimizer state and loss accumulators, and
+    the replays after it continue from there: the whole sequence equals the eager steps."""
+    from aimx import feed
+    from aimx.train import GraphedTrainStep, train_step
+    store, m1, crit, opt1 = _setup()
+    bs = _batches(store, 6)
+    rng = np.random.default_rng(7)
+    odd = next(iter(feed.BatchFeeder(store, iter([rng.integers(0, len(store), 128)]), 3, DEV, depth=1)))
+    seq = bs[1:3] + [odd] + bs[3:]
+    _, m2, _, opt2 = _setup()
+    m2.load_state_dict(m1.state_dict())
+    train_step(m1, bs[0], crit, opt1, n_real=128)
+    eager = [train_step(m1, b, crit, opt1, n_real=128)[0].item() for b in seq]
+    g = GraphedTrainStep(m2, crit, opt2, bs[0], n_real=128, warmup=1)
+    graphed = []
+    for b in seq:
+        before = g.loss_sum.item()
+        g(b)
+        graphed.append((g.loss_sum.item() - before) / 128)
+    assert g.eager_steps == 1
+    np.testing.assert_allclose(graphed, eager, rtol=2e-5, atol=1e-6)
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert (p1 - p2).abs().max().item() <= 1e-5 * max(1.0, p1.abs().max().item()), k
+
+
 def test_training_reduces_loss():
     from aimx.train import GraphedTrainStep, train_epoch
     store, m, crit, opt = _setup(dropout=0.05)
