@@ -417,9 +417,7 @@ static void try_direct(aimx_h5_reader* r, const char* path) {
   if (fd < 0) return;
   struct stat st;
   void* m = MAP_FAILED;
-  const char* pe = std::getenv("AIMX_H5_POPULATE");
-  const int flags = MAP_SHARED | (pe && pe[0] == '1' ? MAP_POPULATE : 0);
-  if (fstat(fd, &st) == 0 && st.st_size > 0) m = mmap(nullptr, size_t(st.st_size), PROT_READ, flags, fd, 0);
+  if (fstat(fd, &st) == 0 && st.st_size > 0) m = mmap(nullptr, size_t(st.st_size), PROT_READ, MAP_SHARED, fd, 0);
   ::close(fd);
   if (m == MAP_FAILED) return;
   const uint8_t* map = static_cast<const uint8_t*>(m);
