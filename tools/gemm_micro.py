@@ -78,6 +78,14 @@ if len(sys.argv) > 1 and sys.argv[1] == "dw":
             run(M, N, K, "TN", f"{lab} splits={sp}", splits=sp, torch_ref=False)
     sys.exit(0)
 
+if len(sys.argv) > 1 and sys.argv[1] == "node":
+    # the c4 / c5 node-update GEMMs (D = 153 / 307) against the same GEMMs at widths padded to 4 / 16
+    for M, D in ((20800, 153), (10240, 307)):
+        for w in (D, (D + 3) // 4 * 4, (D + 15) // 16 * 16):
+            run(M, w, w, "NT", f"node fwd D={D} w={w}")
+            run(M, w, w, "NN", f"node bwd D={D} w={w}")
+    sys.exit(0)
+
 if len(sys.argv) > 1 and sys.argv[1] == "splits":
     for M, N, K, lab in [(76, 77, 9170, "c2 dW mlp"), (152, 305, 9170, "c2 dW_ig"), (256, 257, 9170, "c2 concat dW")]:
         for sp in (0, 4, 8, 12, 16, 24, 32, 48, 64):
