@@ -140,6 +140,18 @@ def replica_checksums(params, device=None):
     return bool(torch.equal(mx, mn)), h.tolist(), mx.tolist(), mn.tolist()
 
 
+def broadcast_parameters(tensors, src_rank: int = 0, process_group=None) -> None:
+    """Every rank's copies of `tensors` (parameters, buffers) become rank src_rank's, in place:
+    the start state data-parallel replicas need, which DistributedDataParallel's constructor sets
+    the same way (module states broadcast from rank 0; reference runner.py:703-707). A no-op
+    without an initialised process group of more than one rank."""
+    if not _ready() or dist.get_world_size(process_group) < 2:
+        return
+    with torch.no_grad():
+        for t in tensors:
+            dist.broadcast(t.data, src=src_rank, group=process_group)
+
+
 class GradientSync:
     """Bucketed, backward-overlapped gradient all-reduce over one flat fp32 buffer per bucket.
 
@@ -154,6 +166,10 @@ class GradientSync:
     gnn.py:146): they take no part in the sync and keep grad None, as DDP(find_unused_parameters)
     leaves them; without this their bucket could only start at finish(). Every rank must pass the
     same set.
+
+    Start state: like DDP's constructor, the constructor broadcasts every parameter it is given
+    (the unused ones too) from rank 0, so replicas initialised from different seeds start equal
+    (`broadcast_params=False` skips it for callers that have synchronised them already).
 
     Transport: over the "nccl" backend (RCCL) the buckets go through an RCCL communicator of the
     library's own (aimx._lib.Comm, include/aimx.h aimx_comm_*): one ncclAllReduce(ncclAvg) per
@@ -171,7 +187,12 @@ class GradientSync:
     """
 
     def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True,
-                 first_bucket_mb: float = 1.0, unused=(), always: bool = False):
+                 first_bucket_mb: float = 1.0, unused=(), always: bool = False, broadcast_params: bool = True):
+        params = list(params)
+        unused = list(unused)
+        if broadcast_params:
+            seen = {id(p) for p in params}
+            broadcast_parameters(params + [p for p in unused if id(p) not in seen], 0, process_group)
         skip = {id(p) for p in unused}
         self.params = [p for p in params if p.requires_grad and id(p) not in skip]
         self.group = process_group

@@ -150,3 +150,30 @@ def test_replica_checksums_and_allreduce_timing():
     for r in range(2):
         assert out[r]["same"] and not out[r]["differ"], out[r]
         assert out[r]["us"] > 0 and out[r]["buckets"] >= 2
+
+
+def _start_state(rank, world):
+    """Replicas built from different seeds (bench.py seeds per rank): GradientSync's constructor
+    broadcasts rank 0's parameters (DDP's constructor does the same), the unused ones included, so
+    after identical averaged steps every replica is bit-identical (replica_checksums)."""
+    from utils.distributed import GradientSync, replica_checksums
+    torch.manual_seed(100 + rank)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.SiLU(), torch.nn.Linear(5, 3), torch.nn.Linear(3, 3))
+    before = replica_checksums(net.parameters())[0]
+    sync = GradientSync(net.parameters(), bucket_mb=0.0001, unused=list(net[3].parameters()))
+    after = replica_checksums(net.parameters())[0]
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(rank)
+    for _ in range(3):
+        opt.zero_grad()
+        net[:3](torch.randn(4, 7, generator=g)).pow(2).sum().backward()
+        sync.finish()
+        opt.step()
+    return before, after, replica_checksums(net.parameters())[0]
+
+
+def test_gradient_sync_broadcasts_start_state():
+    out = _run("_start_state")
+    for r in (0, 1):
+        before, after, trained = out[r]
+        assert not before and after and trained
