@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 R=gpurun_out/seq
 mkdir -p $R
 for c in c2 c4 c5; do
-  tools/gpu_steps.sh "300 seq/$c.log rocprofv3 --kernel-trace --output-format csv -d $R/$c -- python3 bench.py --config $c --no-cpu-baseline --no-roofline --steps 10 --warmup 3" || exit $?
+  tools/gpu_steps.sh "300 seq/$c.log rocprofv3 --kernel-trace --output-format csv -d $R/$c -- python3 bench.py --config $c --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3" || exit $?
   python3 tools/step_seq.py $R/$c > $R/${c}_seq.txt 2>&1
   rm -rf $R/$c
 done
