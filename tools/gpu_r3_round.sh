@@ -13,4 +13,9 @@ tools/gpu_steps.sh \
   "300 r3_round/bench_c3.log python bench.py --config c3 --no-cpu-baseline --no-roofline --no-eager" \
   "400 r3_round/bench_c4.log python bench.py --config c4 --no-cpu-baseline --no-eager" \
   "400 r3_round/bench_c5.log python bench.py --config c5 --no-cpu-baseline --no-eager" \
+  "400 r3_round/bench_c2_stream.log python bench.py --config c2 --feed stream --steps 300 --warmup 20 --no-cpu-baseline --no-roofline --no-eager" \
+  "600 r3_round/bench_c4_stream1m.log python bench.py --config c4 --feed stream --stream-mols 1000000 --steps 400 --warmup 20 --no-cpu-baseline --no-roofline --no-eager" \
   "400 r3_round/roof_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/roof_trace -- python3 bench.py --roofline-only"
+rc=$?
+rm -f /tmp/aimx_stream_*.h5
+exit $rc
