@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 3: hop_rows occupancy variants (3 result units per thread: 69 VGPRs, 7 waves per SIMD;
+# smaller LDS footprints) at c4 / c5, roofline + in-step; bit-exact tests under the chosen knobs.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export PYTHONDONTWRITEBYTECODE=1
+mkdir -p gpurun_out
+out=gpurun_out/r3_maxu.jsonl; : > $out
+for ev in "AIMX_X=0" "AIMX_HOPR_MAXU=3" "AIMX_HOPR_MAXU=3 AIMX_HOPR_COL_CAP=1024" \
+          "AIMX_HOPR_MAXU=3 AIMX_HOPR_COL_CAP=1024 AIMX_HOPR_SCAP=48" \
+          "AIMX_HOPR_MAXU=3 AIMX_HOPR_WC=56 AIMX_HOPR_COL_CAP=1024" \
+          "AIMX_HOPR_COL_CAP=1024 AIMX_HOPR_SCAP=48 AIMX_HOPR_CAP=48" ${EXTRA_ENVS}; do
+  env $ev timeout -k 10 300 python -u tools/hop_cfg_micro.py --configs ${CFGS:-c4,c5} >> $out || exit 1
+done
+python - <<'PY'
+import json
+for l in open("gpurun_out/r3_maxu.jsonl"):
+    r = json.loads(l); s = r["in_step"]; f = r.get("roofline", {})
+    print(r["config"], f"[{r['env']}]", "step fwd", s["fwd"]["us_per_launch"], "bwd", s["bwd"]["us_per_launch"],
+          "| roof fwd", f.get("fwd_frac"), "bwd", f.get("bwd_frac"))
+PY
