@@ -393,12 +393,11 @@ def head_sync_timed_out(device):
 def head_cluster(F=256):
     """Workgroups per 16-molecule tile of the fused head (F: the ffn width).
 
-    The clustered head (2 workgroups per tile, about 3 % of the c2 step) relies on both workgroups
-    of a cluster running at once. Nothing guarantees that while other kernels share the CUs: RCCL
-    collectives under DDP, another process on the same GPU, or the auxiliary stream. So the default
-    is 2 only for a lone process (torch.distributed not initialised with world > 1, AIMX_AUX off);
-    otherwise 1, which has no inter-workgroup wait at all. AIMX_HEAD_CLUSTER overrides both. A wait
-    that still gives up poisons that launch's outputs with NaN (head.hip cluster_poisoned), so the
+    The clustered head (2 workgroups per tile, about 5 % of the c2 step) relies on both workgroups
+    of a cluster running at once, which holds while no other process's kernels share the GPU and
+    no kernel of this process runs beside the head (see head_cluster_allowed). Otherwise the default
+    is 1, which has no inter-workgroup wait at all. AIMX_HEAD_CLUSTER overrides both. A wait that
+    still gives up poisons that launch's outputs with NaN (head.hip cluster_poisoned), so the
     per-step NaN count of the train loop sees it on the step it happens. At F = 512 (c4) the
     chain is 4x the work per tile and 4 workgroups per tile measured best (c4 step 3.278 ms vs
     3.337 / 3.558 / 3.416 ms with 2 / 1 / 8; profiles/r03_head_f512_ab.txt)."""
@@ -411,11 +410,31 @@ def head_cluster(F=256):
 
 
 def head_cluster_allowed():
-    """False when other kernels may share the CUs with the clustered head (see head_cluster)."""
+    """False when other kernels may share the CUs with the clustered head.
+
+    * AIMX_AUX=1: the stack's weight gradients run on an auxiliary stream beside the backward.
+    * Several ranks on one GPU (the gloo rehearsal, spawned test ranks): two processes' clustered
+      launches can each hold part of the CUs while their partners wait for the rest.
+    Data parallelism with one GPU per rank (torchrun: LOCAL_WORLD_SIZE <= the visible GPUs, this
+    rank on cuda:LOCAL_RANK) keeps the clusters: the gradient all-reduces cannot run beside the
+    head. The head is the last stage of the forward, so every parameter gradient (and with it every
+    bucket's collective) follows the head's backward, and the step joins every collective before the
+    optimizer, ahead of the next forward's head (stream order in eager steps, graph edges in
+    captured ones). Other ranks' kernels run on other GPUs. A cluster that still times out poisons
+    its outputs (see head_cluster)."""
     if os.environ.get("AIMX_AUX", "0") == "1":
         return False
     import torch.distributed as dist
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return True
+    try:
+        lws = int(os.environ["LOCAL_WORLD_SIZE"])
+        lr = int(os.environ["LOCAL_RANK"])
+    except (KeyError, ValueError):
+        return False
+    import torch
+    n = torch.cuda.device_count()
+    return 0 < lws <= n and torch.cuda.current_device() == lr
 
 
 def ptr(t):

@@ -202,8 +202,8 @@ class GNN(nn.Module):
         if not (32 <= F <= ops.HEAD_MAX_F and F % 32 == 0 and pp.in_features % 32 == 0 and 1 <= len(blocks) <= 8):
             return False
         # above F = 256 the fused chain pays off only clustered (c4: 3.28 ms with 4 workgroups per
-        # tile, 3.56 with 1 vs 3.32 on the module path): where clusters are not allowed (multi-rank,
-        # auxiliary stream) the module path runs instead
+        # tile, 3.56 with 1 vs 3.32 on the module path): where clusters are not allowed (ranks sharing
+        # a GPU, auxiliary stream) the module path runs instead
         if F > 256 and _lib.head_cluster(F) == 1:
             return False
         if self.skip_transform.in_features != F or self.skip_transform.out_features != F or \

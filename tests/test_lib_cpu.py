@@ -114,3 +114,33 @@ def test_fused_adam_has_no_cpu_path():
     p.grad = torch.ones(4)
     with pytest.raises(AimxError):
         FusedAdam([p], lr=1e-3, max_grad_norm=1.0).step()
+
+
+def test_head_cluster_rule(monkeypatch):
+    """Clustered head launches: a lone process and data parallelism with one GPU per rank keep them;
+    ranks sharing a GPU, an unknown launcher layout and the auxiliary stream drop to 1 workgroup
+    per tile (aimx/_lib.py head_cluster_allowed)."""
+    import torch.distributed as dist
+
+    from aimx import _lib
+    for k in ("AIMX_HEAD_CLUSTER", "AIMX_AUX", "LOCAL_WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert _lib.head_cluster(256) == 2 and _lib.head_cluster(512) == 4  # lone process
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda group=None: 8)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    assert _lib.head_cluster(256) == 1  # no LOCAL_WORLD_SIZE: layout unknown
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert _lib.head_cluster(256) == 2 and _lib.head_cluster(512) == 4  # torchrun, one GPU per rank
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    assert _lib.head_cluster(256) == 1  # this rank is not on its own device
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert _lib.head_cluster(256) == 1  # 8 ranks share one GPU (rehearsal)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("AIMX_AUX", "1")
+    assert _lib.head_cluster(256) == 1
+    monkeypatch.setenv("AIMX_HEAD_CLUSTER", "4")
+    assert _lib.head_cluster(256) == 4  # explicit override
