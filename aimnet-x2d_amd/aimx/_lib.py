@@ -208,6 +208,8 @@ _SIGS = {
     "aimx_embedding_backward_workspace_bytes": (c_size, [ctypes.POINTER(EmbeddingTables), c_i64]),
     "aimx_embedding_backward": (c_i32, [ctypes.POINTER(EmbeddingTables), c_i64, c_ptr, c_i64, c_ptr, c_size, c_ptr]),
     "aimx_act_backward": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_act_backward2": (c_i32, [c_i32, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64,
+                                   c_ptr]),
     "aimx_head_forward": (c_i32, [ctypes.POINTER(Head), c_ptr]),
     "aimx_head_backward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
     "aimx_head_backward": (c_i32, [ctypes.POINTER(Head), ctypes.POINTER(HeadGrad), c_ptr]),

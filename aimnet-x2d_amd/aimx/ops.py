@@ -808,10 +808,16 @@ class _EmbedProject(torch.autograd.Function):
             n, width = E.shape[0], W.shape[0]
             parts = [g if g is not None else torch.zeros(n, w, dtype=_F32, device=dev)
                      for g, w in zip(grads, (xs, width - xs))]
-            if ctx.act >= 0:  # act' applied per part, straight into the two column ranges of dpre
+            if ctx.act >= 0 and width % 4:  # act' per part, into the two column ranges of dpre
                 dpre = torch.empty(n, width, dtype=_F32, device=dev)
                 _act_backward_into(ctx.act, parts[0], pre[:, :xs], dpre[:, :xs])
                 _act_backward_into(ctx.act, parts[1], pre[:, xs:], dpre[:, xs:])
+            elif ctx.act >= 0:  # act' over both parts into dpre in one launch (the two column sources)
+                dpre = torch.empty(n, width, dtype=_F32, device=dev)
+                d0, ld0 = _rows(parts[0])
+                d1, ld1 = _rows(parts[1])
+                check(lib.aimx_act_backward2(ctx.act, ptr(d0), ld0, xs, ptr(d1), ld1, ptr(pre), pre.stride(0), n,
+                                             width, ptr(dpre), dpre.stride(0), stream_ptr(dev)), "act_backward2")
             else:
                 dpre = torch.cat(parts, dim=1)
         else:

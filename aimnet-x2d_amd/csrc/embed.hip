@@ -67,6 +67,36 @@ __global__ void k_act_bwd4(int kind, const float* __restrict__ dy, int32_t ldy, 
   }
 }
 
+// Two-source form: columns [0, n0) of dy come from dy0 (ld ldy0), columns [n0, N) from dy1 (ld
+// ldy1, column n -> dy1[n - n0]); pre / out rows hold N % 4 == 0 floats at 16-byte-aligned starts.
+// One float4 of pre / out per thread; dy is read as a float4 where the source's 4 columns are
+// 16-byte aligned and inside one part, else element by element (the split of gnn.py:227-231 at
+// hidden 512 / 1024 puts both parts at odd column counts).
+__global__ void k_act_bwd2(int kind, const float* __restrict__ dy0, int32_t ldy0, int32_t n0,
+                           const float* __restrict__ dy1, int32_t ldy1, const float* __restrict__ pre, int32_t ldp,
+                           int32_t M, int32_t N, float* __restrict__ out, int32_t ldo) {
+  const int32_t q = N >> 2, total = M * q;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int32_t m = i / q, n = 4 * (i - m * q);
+    const floatx4 p = *reinterpret_cast<const floatx4*>(pre + (int64_t)m * ldp + n);
+    floatx4 d;
+    const float* s0 = dy0 + (int64_t)m * ldy0 + n;
+    const float* s1 = dy1 + (int64_t)m * ldy1 + (n - n0);
+    if (n + 4 <= n0 && ((uintptr_t)s0 & 15) == 0) {
+      d = *reinterpret_cast<const floatx4*>(s0);
+    } else if (n >= n0 && ((uintptr_t)s1 & 15) == 0) {
+      d = *reinterpret_cast<const floatx4*>(s1);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = (n + e < n0) ? s0[e] : s1[e];
+    }
+    floatx4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = d[e] * act_grad(kind, p[e]);
+    *reinterpret_cast<floatx4*>(out + (int64_t)m * ldo + n) = o;
+  }
+}
+
 // blockDim.x == n_tables * dim (<= 1024); dynamic LDS = total_rows * dim floats.
 __global__ void k_embed_bwd_partial(AimxEmbeddingTables t, int64_t N, int64_t chunk, const float* __restrict__ dE,
                                     int64_t ldd, float* __restrict__ partial, int64_t total_rows) {
@@ -240,6 +270,23 @@ extern "C" int aimx_act_backward(int32_t kind, const float* dy, int64_t ldy, con
   else
     hipLaunchKernelGGL(k_act_bwd, dim3((unsigned)std::min<int64_t>(cdiv(M * N, 256), 8192)), dim3(256), 0,
                        (hipStream_t)s, (int)kind, dy, ldy, pre, ldp, M, N, out, ldo);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
+extern "C" int aimx_act_backward2(int32_t kind, const float* dy0, int64_t ldy0, int64_t n0, const float* dy1,
+                                  int64_t ldy1, const float* pre, int64_t ldp, int64_t M, int64_t N, float* out,
+                                  int64_t ldo, aimx_stream_t s) {
+  if (M < 0 || N < 0 || n0 < 0 || n0 > N) return AIMX_EARG;
+  if (M == 0 || N == 0) return AIMX_OK;
+  if ((n0 > 0 && !dy0) || (n0 < N && !dy1) || !pre || !out) return AIMX_EARG;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (N % 4 || ldp % 4 || ldo % 4 || !al(pre) || !al(out) || M * std::max({ldy0, ldy1, ldp, ldo}) >= (int64_t)INT32_MAX ||
+      ((uintptr_t)dy0 & 3) || ((uintptr_t)dy1 & 3))
+    return AIMX_EARG;
+  hipLaunchKernelGGL(k_act_bwd2, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(M * N / 4, 256), 8192))),
+                     dim3(256), 0, (hipStream_t)s, (int)kind, dy0, (int32_t)ldy0, (int32_t)n0, dy1, (int32_t)ldy1, pre,
+                     (int32_t)ldp, (int32_t)M, (int32_t)N, out, (int32_t)ldo);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }

@@ -18,6 +18,7 @@
 // Molecules never span workgroups, so there are no atomics; weight gradients are per-molecule
 // partial slabs reduced in molecule order by a second kernel (deterministic).
 #include <algorithm>
+#include <cstdlib>
 
 #include "aimx_common.h"
 
@@ -688,8 +689,12 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_bwd(
     const float* __restrict__ tau_p, int H, const int32_t* __restrict__ gptr, const int32_t* __restrict__ gperm,
     const float* __restrict__ attn, const float* __restrict__ scores, const float* __restrict__ dpool,
     const float* __restrict__ dattn, float* __restrict__ dx, int64_t lddx, float* __restrict__ dW_part,
-    double* __restrict__ db_part, double* __restrict__ dtau_part, double* __restrict__ ds_glob) {
+    double* __restrict__ db_part, double* __restrict__ dtau_part, double* __restrict__ ds_glob,
+    int32_t* __restrict__ red_cnt, int n_red_cnt) {
   constexpr int NT = S * P * 64;
+  // the arrival counters of the fused partial reduction (k_attn_reduce) that follows this launch
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < n_red_cnt; i += NT) red_cnt[i] = 0;
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<S, P, HM>()];
   __shared__ double red[NT / 64];
   const int g = blockIdx.x;
@@ -763,6 +768,68 @@ __global__ __launch_bounds__(256) void k_attn_reduce2(int64_t n_slices, int H, i
     db[t - nw] = (float)s;
   else
     *dtau = (float)s;
+}
+
+// Both levels in one launch: the k_attn_reduce1 tile, its slice slab stored device-coherent, and
+// the last-arriving workgroup of each 64-column block sums the block's slices in slice order (the
+// same order and fp64 sums as k_attn_reduce2: bit-identical results). Hand-off as the split-K GEMM
+// slabs (MI355X_MICROARCH.md "Valid forms" row 1): agent-scope slab stores, every storing wave
+// drained before the workgroup barrier, one agent-scope arrival add, agent-scope slab loads. The
+// counters are zeroed by the k_attn_bwd launch that precedes this one on the stream.
+__global__ __launch_bounds__(256) void k_attn_reduce(int64_t G, int H, int64_t C, const float* __restrict__ dW_part,
+                                                     const double* __restrict__ db_part,
+                                                     const double* __restrict__ dtau_part, double* __restrict__ slab,
+                                                     int32_t* __restrict__ cnt, float* __restrict__ dW,
+                                                     float* __restrict__ db, float* __restrict__ dtau) {
+  __shared__ double red[4][64];
+  __shared__ int last;
+  const int64_t nw = (int64_t)H * C, tot = nw + H + 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t g0 = (int64_t)blockIdx.y * kRedSlice + w * (kRedSlice / 4);
+  double s = 0.0;
+  if (t < tot) {
+    double v[kRedSlice / 4];
+#pragma unroll
+    for (int k = 0; k < kRedSlice / 4; ++k)
+      v[k] = g0 + k < G ? partial_at(t, g0 + k, nw, H, dW_part, db_part, dtau_part) : 0.0;
+#pragma unroll
+    for (int k = 0; k < kRedSlice / 4; ++k) s += v[k];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && t < tot) {
+    const double r = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(slab + (int64_t)blockIdx.y * tot + t),
+                       __builtin_bit_cast(unsigned long long, r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.y - 1;
+  __syncthreads();
+  if (!last || w != 0 || t >= tot) return;
+  const int64_t ns = gridDim.y;
+  double acc = 0.0;
+  for (int64_t k0 = 0; k0 < ns; k0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      v[k] = k0 + k < ns ? __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(
+                                                                           slab + (k0 + k) * tot + t),
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                         : 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k0 + k < ns) acc += v[k];
+  }
+  if (t < nw)
+    dW[t] = (float)acc;
+  else if (t < nw + H)
+    db[t - nw] = (float)acc;
+  else
+    *dtau = (float)acc;
 }
 
 // kind: 0 mean, 1 max, 2 sum
@@ -844,14 +911,15 @@ template <int S, int P, int R>
 void launch_attn_bwd(int H, unsigned G, hipStream_t st, const float* x, int64_t ldx, int64_t N, int64_t C,
                      const float* W, const float* tau, const int32_t* gptr, const int32_t* gperm, const float* attn,
                      const float* scores, const float* dpool, const float* dattn, float* dx, int64_t lddx,
-                     float* dW_part, double* db_part, double* dtau_part, double* ds_glob) {
+                     float* dW_part, double* db_part, double* dtau_part, double* ds_glob, int32_t* red_cnt,
+                     int n_red_cnt) {
   const dim3 block(S * P * 64);
   if (H <= 4)
     hipLaunchKernelGGL((k_attn_bwd<S, P, R, 4>), dim3(G), block, 0, st, x, ldx, N, C, W, tau, H, gptr, gperm, attn,
-                       scores, dpool, dattn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+                       scores, dpool, dattn, dx, lddx, dW_part, db_part, dtau_part, ds_glob, red_cnt, n_red_cnt);
   else
     hipLaunchKernelGGL((k_attn_bwd<S, P, R, 8>), dim3(G), block, 0, st, x, ldx, N, C, W, tau, H, gptr, gperm, attn,
-                       scores, dpool, dattn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+                       scores, dpool, dattn, dx, lddx, dW_part, db_part, dtau_part, ds_glob, red_cnt, n_red_cnt);
 }
 
 }  // namespace
@@ -861,7 +929,8 @@ using namespace aimx;
 
 extern "C" size_t aimx_attn_pool_workspace_bytes(int64_t N, int64_t C, int64_t H, int64_t G) {
   return sizeof(float) * (size_t)(G * H * C + 32) +
-         sizeof(double) * (size_t)(G * H + G + 2 * H * N + cdiv(G, kRedSlice) * (H * C + H + 1) + 40);
+         sizeof(double) * (size_t)(G * H + G + 2 * H * N + cdiv(G, kRedSlice) * (H * C + H + 1) + 40) +
+         sizeof(int32_t) * (size_t)(cdiv(H * C + H + 1, 64) + 16);
 }
 
 extern "C" int aimx_attn_pool_forward(const float* x, int64_t ldx, int64_t N, int64_t C, const float* W, const float* b,
@@ -894,23 +963,32 @@ extern "C" int aimx_attn_pool_backward(const float* x, int64_t ldx, int64_t N, i
   double* dtau_part = db_part + G * H;
   double* ds_glob = (double*)(((uintptr_t)(dtau_part + G) + 63) & ~(uintptr_t)63);
   double* slab = (double*)(((uintptr_t)(ds_glob + 2 * H * N) + 63) & ~(uintptr_t)63);
+  const int64_t tot = H * C + H + 1, n_slices = std::max<int64_t>(1, cdiv(G, kRedSlice));
+  int32_t* red_cnt = (int32_t*)(((uintptr_t)(slab + n_slices * tot) + 63) & ~(uintptr_t)63);
+  const int n_red_cnt = (int)cdiv(tot, 64);
   if (G > 0) {
     switch (pool_slices(C)) {
       case 1:
         launch_attn_bwd<1, 4, 8>((int)H, (unsigned)G, s, x, ldx, N, C, W, tau, gptr, gperm, attn, scores, d_pooled, d_attn,
-                              dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+                              dx, lddx, dW_part, db_part, dtau_part, ds_glob, red_cnt, n_red_cnt);
         break;
       case 2:
         launch_attn_bwd<2, 4, 12>((int)H, (unsigned)G, s, x, ldx, N, C, W, tau, gptr, gperm, attn, scores, d_pooled,
-                               d_attn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+                               d_attn, dx, lddx, dW_part, db_part, dtau_part, ds_glob, red_cnt, n_red_cnt);
         break;
       default:
         launch_attn_bwd<4, 2, 24>((int)H, (unsigned)G, s, x, ldx, N, C, W, tau, gptr, gperm, attn, scores, d_pooled,
-                               d_attn, dx, lddx, dW_part, db_part, dtau_part, ds_glob);
+                               d_attn, dx, lddx, dW_part, db_part, dtau_part, ds_glob, red_cnt, n_red_cnt);
     }
     AIMX_CHECK_LAUNCH();
   }
-  const int64_t tot = H * C + H + 1, n_slices = std::max<int64_t>(1, cdiv(G, kRedSlice));
+  static const bool two_launch = getenv("AIMX_ATTN_RED2") != nullptr;  // A/B: the two-launch reduction
+  if (G > 0 && !two_launch) {
+    hipLaunchKernelGGL(k_attn_reduce, dim3((unsigned)n_red_cnt, (unsigned)n_slices), dim3(256), 0, s, G, (int)H, C,
+                       dW_part, db_part, dtau_part, slab, red_cnt, dW, db, dtau);
+    AIMX_CHECK_LAUNCH();
+    return AIMX_OK;
+  }
   hipLaunchKernelGGL(k_attn_reduce1, dim3((unsigned)cdiv(tot, 64), (unsigned)n_slices), dim3(256), 0, s, G, (int)H, C,
                      dW_part, db_part, dtau_part, slab);
   AIMX_CHECK_LAUNCH();

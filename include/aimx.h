@@ -310,6 +310,12 @@ int aimx_embedding_backward(const AimxEmbeddingTables* t, int64_t N, const float
 /* out[m,n] = dy[m,n] * act'(pre[m,n]) */
 int aimx_act_backward(int32_t kind, const float* dy, int64_t ldy, const float* pre, int64_t ldp,
                       int64_t M, int64_t N, float* out, int64_t ldo, aimx_stream_t stream);
+/* The same over two column sources: dy[:, :n0] = dy0 (ld ldy0), dy[:, n0:] = dy1 (ld ldy1) — the
+ * gradients of the x_self / x_other views of the embedding projection (gnn.py:227-231) in one
+ * launch. Requires N, ldp, ldo % 4 == 0, 16-byte-aligned pre / out, 4-byte-aligned dy0 / dy1. */
+int aimx_act_backward2(int32_t kind, const float* dy0, int64_t ldy0, int64_t n0, const float* dy1, int64_t ldy1,
+                       const float* pre, int64_t ldp, int64_t M, int64_t N, float* out, int64_t ldo,
+                       aimx_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------
  * Grouped weight gradients: for each problem, dW[M, N] = dY^T X over K rows (atoms) and, when

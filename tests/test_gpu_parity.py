@@ -457,6 +457,28 @@ def test_gemm_activation_epilogue(act, fn):
 
 
 # --------------------------------------------------------------------------------------- layers
+@pytest.mark.parametrize("n,width,xs,off", [(37, 256, 180, 0), (1031, 512, 359, 0), (19, 1024, 717, 1), (5, 8, 0, 0),
+                                         (5, 8, 8, 3)])
+def test_act_backward_two_sources(n, width, xs, off):
+    """aimx_act_backward2 (the embedding projection's act' over the x_self / x_other gradients, one
+    launch) equals dy * act'(pre) per element; dy0 a strided view (ld = width + off), dy1 contiguous."""
+    from aimx import _lib
+    lib = _lib.load()
+    P = _lib.ptr
+    g = torch.Generator(device="cpu").manual_seed(n + width)
+    pre = torch.randn(n, width, generator=g).to(DEV)
+    big = torch.randn(n, width + off + 3, generator=g).to(DEV)
+    dy0 = big[:, off:off + xs]
+    dy1 = torch.randn(n, width - xs, generator=g).to(DEV)
+    out = torch.full((n, width), float("nan"), device=DEV)
+    assert lib.aimx_act_backward2(_lib.ACT_KIND["silu"], P(dy0), big.stride(0), xs, P(dy1), max(1, width - xs), P(pre),
+                                  width, n, width, P(out), width, _lib.stream_ptr(pre.device)) == 0
+    p64 = pre.double()
+    sg = torch.sigmoid(p64)
+    ref = torch.cat([dy0.double(), dy1.double()], 1) * (sg * (1 + p64 * (1 - sg)))
+    assert torch.allclose(out.double(), ref, rtol=1e-6, atol=1e-6)
+
+
 def test_shell_layer_standalone():
     from models.layers import ShellConvolutionLayer
     z = load_golden("mp_general")
