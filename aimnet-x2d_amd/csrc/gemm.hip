@@ -1014,13 +1014,19 @@ struct WbTable {
   int32_t xcd;  // XCD-aware work order (AIMX_WGRAD_XCD=0: launch order, for A/B)
 };
 
-template <int BB>
+// DB: two LDS buffers per operand (80-wide blocks only: 40 KiB, four workgroups fill a CU's
+// 160 KiB). Fill s + 1 is written to the idle buffer while fill s computes from the other, so each
+// fill costs one workgroup barrier instead of two and the LDS writes overlap other waves' MFMAs.
+template <int BB, bool DB>
 __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
   using G = WbGeom<BB>;
   constexpr int kWbF = G::F, kWbT = G::T, kWbV = G::V, kLd = G::S;
-  __shared__ __attribute__((aligned(16))) float sA[kWbK * kLd];
-  __shared__ __attribute__((aligned(16))) float sB[kWbK * kLd];
-  __shared__ int flag;
+  constexpr int kBuf = kWbK * kLd;  // floats per operand buffer
+  static_assert(!DB || BB == 80, "double-buffered LDS only for 80-wide blocks");
+  __shared__ __attribute__((aligned(16))) float sA[(DB ? 2 : 1) * kBuf];
+  __shared__ __attribute__((aligned(16))) float sB[(DB ? 2 : 1) * kBuf];
+  // the split-K arrival flag lives in sA: written only after the barrier that ends every LDS read
+  int& flag = *reinterpret_cast<int*>(sA);
   int q = 0;
   while (q + 1 < t.n && t.blk0[q + 1] <= (int)blockIdx.x) ++q;
   const int nb = t.nblk[q];
@@ -1108,59 +1114,91 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
   floatx4 acc[kWbF];
 #pragma unroll
   for (int j = 0; j < kWbF; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // kWbD fills in flight: fill s lands in register slot s % kWbD, is copied to LDS kWbD - 1
-  // compute periods after its loads were issued, and the slot is refilled with fill s + kWbD
   floatx4 ring[kWbD][kWbV];
+  // fill in registers -> LDS buffer (sa, sb)
+  auto put = [&](const floatx4(&stage)[kWbV], float* sa, float* sb) {
+#pragma unroll
+    for (int u = 0; u < kWbV; ++u) {
+      const bool isb = u >= kWbV / 2;
+      const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
+      *reinterpret_cast<floatx4*>((isb ? sb : sa) + (f / (BB / 4)) * kLd + 4 * (f % (BB / 4))) = stage[u];
+    }
+  };
+  // the kWbK k rows staged in (sa, sb) into this wave's accumulators
+  auto compute = [&](const float* sa, const float* sb) {
+#if AIMX_LDS_PIPE
+    // the fragments of k step k4 + 1 are read from LDS before the MFMAs of step k4 issue (two
+    // register sets; sched_barriers keep that order), so each step's MFMAs wait only for reads
+    // issued one step earlier instead of a full LDS round trip per step
+    float av[2], bv[2][kWbF];
+    auto rd = [&](int k4, int sl) {
+      const int r = (k4 * 4 + lk) * kLd + lm;
+      av[sl] = sa[r + w * 16];
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j) bv[sl][j] = sb[r + j * 16];
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int k4 = 0; k4 < kWbK / 4; ++k4) {
+      const int c = k4 & 1;
+      if (k4 + 1 < kWbK / 4) rd(k4 + 1, c ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], bv[c][j], acc[j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
+#pragma unroll
+    for (int k4 = 0; k4 < kWbK / 4; ++k4) {
+      const int r = (k4 * 4 + lk) * kLd + lm;
+      const float av = sa[r + w * 16];
+      float bv[kWbF];
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j) bv[j] = sb[r + j * 16];
+#pragma unroll
+      for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
+    }
+#endif
+  };
 #pragma unroll
   for (int d = 0; d < kWbD; ++d)
     if (d < nsub) fetch(kb + d * kWbK, ring[d]);
-  for (int s0 = 0; s0 < nsub; s0 += kWbD) {
+  if constexpr (DB) {
+    static_assert(kWbD == 2, "the double-buffered schedule keeps two fills in registers");
+    // fill s computes from buffer s & 1; fill s + 1 (loaded two compute periods earlier) goes to
+    // the other buffer first, and its register slot is refilled with fill s + 3
+    if (nsub > 0) {
+      put(ring[0], sA, sB);
+      if (2 < nsub) fetch(kb + 2 * kWbK, ring[0]);
+    }
+    __syncthreads();
+    for (int s0 = 0; s0 < nsub; s0 += 2) {
 #pragma unroll
-    for (int d = 0; d < kWbD; ++d) {
-      const int s = s0 + d;
-      if (s >= nsub) break;
-      __syncthreads();  // the previous rows' MFMA reads are done
-#pragma unroll
-      for (int u = 0; u < kWbV; ++u) {
-        const bool isb = u >= kWbV / 2;
-        const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
-        *reinterpret_cast<floatx4*>((isb ? sB : sA) + (f / (BB / 4)) * kLd + 4 * (f % (BB / 4))) = ring[d][u];
+      for (int d = 0; d < 2; ++d) {
+        const int s = s0 + d;
+        if (s >= nsub) break;
+        if (s + 1 < nsub) {
+          put(ring[d ^ 1], sA + (d ^ 1) * kBuf, sB + (d ^ 1) * kBuf);
+          if (s + 3 < nsub) fetch(kb + (s + 3) * kWbK, ring[d ^ 1]);
+        }
+        compute(sA + d * kBuf, sB + d * kBuf);
+        __syncthreads();  // fill s + 1 visible; every read of buffer d done before it is refilled
       }
-      __syncthreads();
-      if (s + kWbD < nsub) fetch(kb + (s + kWbD) * kWbK, ring[d]);
-#if AIMX_LDS_PIPE
-      // the fragments of k step k4 + 1 are read from LDS before the MFMAs of step k4 issue (two
-      // register sets; sched_barriers keep that order), so each step's MFMAs wait only for reads
-      // issued one step earlier instead of a full LDS round trip per step
-      float av[2], bv[2][kWbF];
-      auto rd = [&](int k4, int sl) {
-        const int r = (k4 * 4 + lk) * kLd + lm;
-        av[sl] = sA[r + w * 16];
+    }
+  } else {
+    // kWbD fills in flight: fill s lands in register slot s % kWbD, is copied to LDS kWbD - 1
+    // compute periods after its loads were issued, and the slot is refilled with fill s + kWbD
+    for (int s0 = 0; s0 < nsub; s0 += kWbD) {
 #pragma unroll
-        for (int j = 0; j < kWbF; ++j) bv[sl][j] = sB[r + j * 16];
-      };
-      rd(0, 0);
-#pragma unroll
-      for (int k4 = 0; k4 < kWbK / 4; ++k4) {
-        const int c = k4 & 1;
-        if (k4 + 1 < kWbK / 4) rd(k4 + 1, c ^ 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], bv[c][j], acc[j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+      for (int d = 0; d < kWbD; ++d) {
+        const int s = s0 + d;
+        if (s >= nsub) break;
+        __syncthreads();  // the previous rows' MFMA reads are done
+        put(ring[d], sA, sB);
+        __syncthreads();
+        if (s + kWbD < nsub) fetch(kb + (s + kWbD) * kWbK, ring[d]);
+        compute(sA, sB);
       }
-#else
-#pragma unroll
-      for (int k4 = 0; k4 < kWbK / 4; ++k4) {
-        const int r = (k4 * 4 + lk) * kLd + lm;
-        const float av = sA[r + w * 16];
-        float bv[kWbF];
-#pragma unroll
-        for (int j = 0; j < kWbF; ++j) bv[j] = sB[r + j * 16];
-#pragma unroll
-        for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
-      }
-#endif
     }
   }
 
@@ -1383,7 +1421,8 @@ struct WgPlan {
 };
 // min_wgs > 0 (a lone long-K GEMM routed here): split K further until the launch has about that
 // many workgroups, so the LDS fills of a few blocks are spread over the whole chip
-WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
+// kper0: atoms of K per workgroup unless AIMX_WGRAD_KPER overrides it (group_kper picks it)
+WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0, int64_t kper0 = 512) {
   const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
   const bool no_lds = e && atoi(e) == 0;
   WgPlan w;
@@ -1401,7 +1440,7 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
     w.tiles_x = (int)cdiv(p.M, w.bb);
     w.tiles_y = (int)cdiv(N, w.bb);
     const char* kp = getenv("AIMX_WGRAD_KPER");  // atoms per workgroup (tuning experiments)
-    const int64_t kper = kp ? std::max(64, atoi(kp)) : 512;
+    const int64_t kper = kp ? std::max(64, atoi(kp)) : kper0;
     int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
     if (min_wgs > 0)
       sp = std::max(sp, std::min<int64_t>({64, p.K / 128, cdiv(min_wgs, (int64_t)w.tiles_x * w.tiles_y)}));
@@ -1419,6 +1458,20 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
   w.kchunk = (int)(cdiv(cdiv(std::max<int64_t>(p.K, 1), sp), 16) * 16);
   w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
   return w;
+}
+// K per workgroup for a grouped launch: 512 atoms, or 256 when the LDS problems would leave fewer
+// than ~4 workgroups per CU (c2's 36 blocks x 17 slices: 612 workgroups). Measured
+// (tools/wgrad_micro.py, profiles/r03_wgrad_dbuf_ab.txt): c2 70 -> 60 us; c4 / c5 (3840 / 7680
+// workgroups at 512) are slower at 256 and keep 512. Lone GEMMs (min_wgs > 0) keep 512.
+constexpr int64_t kWgKperSmall = 256;
+int64_t group_kper(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
+  if (min_wgs > 0) return 512;
+  int64_t total = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const WgPlan w = wg_plan(p[i], 0, 512);
+    if (w.lds) total += (int64_t)w.splits * w.tiles_x * w.tiles_y;
+  }
+  return total > 0 && total < 1024 ? kWgKperSmall : 512;
 }
 bool wg_valid(const AimxWgradProblem& p) {
   if (p.M < 1 || p.N < 1 || p.K < 0 || !p.dY || !p.X || !p.dW) return false;
@@ -1553,9 +1606,11 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
 namespace aimx {
 size_t wgrad_ws_bytes(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
   if (!p || n < 0) return 0;
+  // sized for the smaller K per workgroup whatever group_kper picks, so a workspace sized for a
+  // problem list also serves any subset of it (the stack's per-layer launches)
   size_t f = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i], min_wgs);
+    const WgPlan w = wg_plan(p[i], min_wgs, min_wgs > 0 ? 512 : kWgKperSmall);
     if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab;
   }
   return sizeof(float) * f;
@@ -1567,9 +1622,10 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   for (int32_t i = 0; i < n; ++i)
     if (!wg_valid(p[i])) return AIMX_EARG;
   if (workspace_bytes < wgrad_ws_bytes(p, n, min_wgs) || (workspace_bytes && !workspace)) return AIMX_EARG;
+  const int64_t kper = group_kper(p, n, min_wgs);
   int64_t ctiles = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i], min_wgs);
+    const WgPlan w = wg_plan(p[i], min_wgs, kper);
     ctiles += (int64_t)w.tiles_x * w.tiles_y;
   }
   if (!counters || ctiles > n_counters) return AIMX_EARG;
@@ -1589,12 +1645,22 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
         tb.xcd = (e && atoi(e) == 0) ? 0 : 1;
       }
       if (blkb > 0) {
+        // double-buffered LDS for the long slices only: at 8 fills per workgroup (the small-group
+        // K) it measured slower (c2 micro 59.6 -> 65.7 us), at 16 it is 0.5-1.5 % faster (c4 / c5).
+        // AIMX_WGRAD_DBUF=0: the single-buffered schedule everywhere (A/B experiments; read once)
+        static const bool dbuf = [] {
+          const char* e = getenv("AIMX_WGRAD_DBUF");
+          return !(e && atoi(e) == 0);
+        }();
         if (wide)
-          hipLaunchKernelGGL(k_wgrad_lds<160>, dim3((unsigned)blkb), dim3(WbGeom<160>::T), 0, (hipStream_t)stream, tb,
-                             (float*)workspace, counters);
+          hipLaunchKernelGGL((k_wgrad_lds<160, false>), dim3((unsigned)blkb), dim3(WbGeom<160>::T), 0,
+                             (hipStream_t)stream, tb, (float*)workspace, counters);
+        else if (dbuf && kper != kWgKperSmall)
+          hipLaunchKernelGGL((k_wgrad_lds<80, true>), dim3((unsigned)blkb), dim3(WbGeom<80>::T), 0,
+                             (hipStream_t)stream, tb, (float*)workspace, counters);
         else
-          hipLaunchKernelGGL(k_wgrad_lds<80>, dim3((unsigned)blkb), dim3(WbGeom<80>::T), 0, (hipStream_t)stream, tb,
-                             (float*)workspace, counters);
+          hipLaunchKernelGGL((k_wgrad_lds<80, false>), dim3((unsigned)blkb), dim3(WbGeom<80>::T), 0,
+                             (hipStream_t)stream, tb, (float*)workspace, counters);
       }
       tb = WbTable{};
       blkb = 0;
@@ -1609,7 +1675,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
-    const WgPlan w = wg_plan(pr, min_wgs);
+    const WgPlan w = wg_plan(pr, min_wgs, kper);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {
       const int wide = w.bb == 160;
