@@ -1421,8 +1421,7 @@ struct WgPlan {
 };
 // min_wgs > 0 (a lone long-K GEMM routed here): split K further until the launch has about that
 // many workgroups, so the LDS fills of a few blocks are spread over the whole chip
-// kper0: atoms of K per workgroup unless AIMX_WGRAD_KPER overrides it (group_kper picks it)
-WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0, int64_t kper0 = 512) {
+WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
   const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
   const bool no_lds = e && atoi(e) == 0;
   WgPlan w;
@@ -1440,7 +1439,7 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0, int64_t kper0 = 5
     w.tiles_x = (int)cdiv(p.M, w.bb);
     w.tiles_y = (int)cdiv(N, w.bb);
     const char* kp = getenv("AIMX_WGRAD_KPER");  // atoms per workgroup (tuning experiments)
-    const int64_t kper = kp ? std::max(64, atoi(kp)) : kper0;
+    const int64_t kper = kp ? std::max(64, atoi(kp)) : 512;
     int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
     if (min_wgs > 0)
       sp = std::max(sp, std::min<int64_t>({64, p.K / 128, cdiv(min_wgs, (int64_t)w.tiles_x * w.tiles_y)}));
@@ -1458,20 +1457,6 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0, int64_t kper0 = 5
   w.kchunk = (int)(cdiv(cdiv(std::max<int64_t>(p.K, 1), sp), 16) * 16);
   w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
   return w;
-}
-// K per workgroup for a grouped launch: 512 atoms, or 256 when the LDS problems would leave fewer
-// than ~4 workgroups per CU (c2's 36 blocks x 17 slices: 612 workgroups). Measured
-// (tools/wgrad_micro.py, profiles/r03_wgrad_dbuf_ab.txt): c2 70 -> 60 us; c4 / c5 (3840 / 7680
-// workgroups at 512) are slower at 256 and keep 512. Lone GEMMs (min_wgs > 0) keep 512.
-constexpr int64_t kWgKperSmall = 256;
-int64_t group_kper(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
-  if (min_wgs > 0) return 512;
-  int64_t total = 0;
-  for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i], 0, 512);
-    if (w.lds) total += (int64_t)w.splits * w.tiles_x * w.tiles_y;
-  }
-  return total > 0 && total < 1024 ? kWgKperSmall : 512;
 }
 bool wg_valid(const AimxWgradProblem& p) {
   if (p.M < 1 || p.N < 1 || p.K < 0 || !p.dY || !p.X || !p.dW) return false;
@@ -1606,11 +1591,9 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
 namespace aimx {
 size_t wgrad_ws_bytes(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
   if (!p || n < 0) return 0;
-  // sized for the smaller K per workgroup whatever group_kper picks, so a workspace sized for a
-  // problem list also serves any subset of it (the stack's per-layer launches)
   size_t f = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i], min_wgs, min_wgs > 0 ? 512 : kWgKperSmall);
+    const WgPlan w = wg_plan(p[i], min_wgs);
     if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab;
   }
   return sizeof(float) * f;
@@ -1622,10 +1605,9 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   for (int32_t i = 0; i < n; ++i)
     if (!wg_valid(p[i])) return AIMX_EARG;
   if (workspace_bytes < wgrad_ws_bytes(p, n, min_wgs) || (workspace_bytes && !workspace)) return AIMX_EARG;
-  const int64_t kper = group_kper(p, n, min_wgs);
   int64_t ctiles = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i], min_wgs, kper);
+    const WgPlan w = wg_plan(p[i], min_wgs);
     ctiles += (int64_t)w.tiles_x * w.tiles_y;
   }
   if (!counters || ctiles > n_counters) return AIMX_EARG;
@@ -1645,9 +1627,8 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
         tb.xcd = (e && atoi(e) == 0) ? 0 : 1;
       }
       if (blkb > 0) {
-        // double-buffered LDS for the long slices only: at 8 fills per workgroup (the small-group
-        // K) it measured slower (c2 micro 59.6 -> 65.7 us), at 16 it is 0.5-1.5 % faster (c4 / c5).
-        // AIMX_WGRAD_DBUF=0: the single-buffered schedule everywhere (A/B experiments; read once)
+        // double-buffered LDS: 0.5-1.5 % faster at c4 / c5, neutral at c2 (16 fills per workgroup;
+        // profiles/r03_wgrad_dbuf_ab.txt). AIMX_WGRAD_DBUF=0: single-buffered (A/B only; read once)
         static const bool dbuf = [] {
           const char* e = getenv("AIMX_WGRAD_DBUF");
           return !(e && atoi(e) == 0);
@@ -1655,7 +1636,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
         if (wide)
           hipLaunchKernelGGL((k_wgrad_lds<160, false>), dim3((unsigned)blkb), dim3(WbGeom<160>::T), 0,
                              (hipStream_t)stream, tb, (float*)workspace, counters);
-        else if (dbuf && kper != kWgKperSmall)
+        else if (dbuf)
           hipLaunchKernelGGL((k_wgrad_lds<80, true>), dim3((unsigned)blkb), dim3(WbGeom<80>::T), 0,
                              (hipStream_t)stream, tb, (float*)workspace, counters);
         else
@@ -1675,7 +1656,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
-    const WgPlan w = wg_plan(pr, min_wgs, kper);
+    const WgPlan w = wg_plan(pr, min_wgs);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {
       const int wide = w.bb == 160;
