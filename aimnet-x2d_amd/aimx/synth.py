@@ -65,7 +65,7 @@ def synth_molecules(count, seed=0):
 
 
 class QM9Asset:
-    """Committed QM9-val graphs (13,389 molecules, 17.9 atoms incl. H on average)."""
+    """Committed QM9-val graphs (13,373 molecules, 17.9 atoms incl. H on average; the 16 SMILES RDKit would reject are dropped)."""
 
     def __init__(self, path=_ASSET):
         z = np.load(path, allow_pickle=False)

@@ -237,7 +237,7 @@ def train_epoch(model, batches: Iterable, criterion, optimizer, device, sync=Non
 
 
 def main(argv=None):
-    """QM9 training on the committed QM9-val graph asset (13,389 molecules): 90/10 split, one target
+    """QM9 training on the committed QM9-val graph asset (13,373 molecules): 90/10 split, one target
     (z-scored), the reference defaults (hidden 256, 3 hops, attention pool, L1, Adam 2.5e-4,
     clip 1.0), native feed, graphed steps. One process per GPU under torchrun (disjoint index
     shards per rank, gradients all-reduced by GradientSync over RCCL)."""

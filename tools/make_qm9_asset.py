@@ -13,7 +13,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "aimnet-x2d_amd"))
-from aimx.smiles import featurize  # noqa: E402
+from aimx.smiles import SmilesError, featurize  # noqa: E402
 
 SRC = "/root/reference/sample-data/qm9/sample-splits/val.csv"
 
@@ -22,8 +22,13 @@ def main():
     rows = list(csv.reader(open(SRC)))
     header, rows = rows[0], rows[1:]
     n_atoms, feats, bonds_i, bonds_j, nbonds, targets, charges, smiles = [], [], [], [], [], [], [], []
+    dropped = 0
     for r in rows:
-        f = featurize(r[0])
+        try:
+            f = featurize(r[0])
+        except SmilesError:  # compute_all returns None -> precompute_all_and_filter drops it
+            dropped += 1
+            continue
         adj = f["adj"]
         iu, ju = np.nonzero(np.triu(adj, 1))
         n_atoms.append(adj.shape[0])
@@ -49,7 +54,7 @@ def main():
     )
     na = np.array(n_atoms)
     print(out, os.path.getsize(out), "mols", len(na), "mean atoms", na.mean(), "max", na.max(),
-          "mean bonds", np.mean(nbonds))
+          "mean bonds", np.mean(nbonds), "dropped", dropped)
 
 
 if __name__ == "__main__":
