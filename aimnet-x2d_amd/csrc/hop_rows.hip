@@ -69,6 +69,7 @@ struct RowsArgs {
   const int64_t* seg;  // molecule id per row of [0, split) (optional)
   int64_t seg_stride;
   int32_t dbg;  // AIMX_HOPR_DBG phase knock-outs (timing experiments only; results are wrong when != 0)
+  int32_t lean;  // fewer barriers per piece (AIMX_HOPR_LEAN=0: the round-3 schedule, for A/B)
 };
 
 __device__ __forceinline__ uint32_t misal(const void* p) { return (uint32_t)((uintptr_t)p >> 2) & 3u; }
@@ -213,18 +214,28 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
   uint32_t first = r0, span = nr;
   if (mode == 1) {
     const Pass ps = pass_of(a, p0);
-    if (threadIdx.x == 0) {
-      s_misc[0] = INT_MAX;
-      s_misc[1] = INT_MIN;
+    const int32_t rb = (int32_t)a.wc * 4;
+    // lean: the lo / hi words were reset by scan_window or by the previous piece (after a barrier
+    // that follows every read of them), and a molecule piece stores its col slice already as byte
+    // offsets into its own staged rows, so the common case needs no barrier after the min / max
+    const bool conv = a.lean && spec;
+    if (!a.lean) {
+      if (threadIdx.x == 0) {
+        s_misc[0] = INT_MAX;
+        s_misc[1] = INT_MIN;
+      }
+      __syncthreads();
     }
-    __syncthreads();
     int32_t lo = INT_MAX, hi = INT_MIN;
     for (int32_t i = threadIdx.x; i < ncols; i += kRT) {
       const int32_t c = a.col[base + i];
-      s_col[i] = c;
+      // (wrapping arithmetic: an entry far outside the piece only matters if the piece is not its own
+      // source span, and then the slice is re-read from global below)
+      s_col[i] = conv ? (int32_t)((uint32_t)(c - (int32_t)r0) * (uint32_t)rb) : c;
       lo = min(lo, c);
       hi = max(hi, c);
     }
+    if (conv && threadIdx.x == 0) s_col[ncols] = (int32_t)nr * rb;
     // a molecule tile's sources are its own rows: stage them while the col slice is in flight
     if (spec) stage_rows<SRC_CHUNKED>(a, s_x, r0, nr, ps);
 #pragma unroll
@@ -239,8 +250,10 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
     __syncthreads();
     lo = s_misc[0];
     hi = s_misc[1];
-    if (spec && lo >= (int32_t)r0 && hi < (int32_t)(r0 + nr)) {
-      // staged: own rows
+    bool sync = true;
+    const bool own = spec && lo >= (int32_t)r0 && hi < (int32_t)(r0 + nr);
+    if (own) {
+      sync = !conv;  // staged: own rows (converted already under conv)
     } else if ((uint32_t)(hi - lo) < a.cap) {
       first = (uint32_t)lo;
       span = (uint32_t)(hi - lo + 1);
@@ -248,12 +261,15 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
     } else {
       mode = 2;  // s_col keeps the raw col slice
     }
-    if (mode == 1) {
-      const int32_t rb = (int32_t)a.wc * 4;
+    // each thread rewrites only the entries it stored itself; the sentinel is thread 0's
+    if (mode == 1 && !conv) {
       for (int32_t i = threadIdx.x; i < ncols; i += kRT) s_col[i] = (s_col[i] - (int32_t)first) * rb;
       if (threadIdx.x == 0) s_col[ncols] = (int32_t)span * rb;
-    }
-    __syncthreads();
+    } else if (mode == 1 && !own) {  // conv, restaged at [first, first + span): raw cols from global
+      for (int32_t i = threadIdx.x; i < ncols; i += kRT) s_col[i] = (a.col[base + i] - (int32_t)first) * rb;
+      if (threadIdx.x == 0) s_col[ncols] = (int32_t)span * rb;
+    }  // mode 2 after conv reads the raw cols from global (col_raw below)
+    if (sync) __syncthreads();
   }
   const char* xb = reinterpret_cast<const char*>(s_x);
   const char* cb = reinterpret_cast<const char*>(s_col);
@@ -300,7 +316,7 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
           // fallback (tile sources wider than the staging capacity, or an over-long col slice):
           // dword gathers from global, same order
           const int32_t b = P[rl] - base, e = P[rl + 1] - base;
-          const int32_t* cols = (uint32_t)ncols < a.col_cap ? s_col : a.col + base;
+          const int32_t* cols = ((uint32_t)ncols < a.col_cap && !(a.lean && spec)) ? s_col : a.col + base;
           const int32_t lim = (int32_t)ps.w - (int32_t)(4 * v);
           float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
           for (int32_t k = b; k < e; ++k) {
@@ -318,6 +334,10 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
       res[j] = acc;
     }
     __syncthreads();  // every staged row read: s_x becomes the output tile
+    if (a.lean && p == p0 && threadIdx.x == 0) {  // every lo / hi read is behind this barrier
+      s_misc[0] = INT_MAX;
+      s_misc[1] = INT_MIN;
+    }
 #pragma unroll
     for (int j = 0; j < kRMaxU; ++j) {
       const uint32_t t = threadIdx.x + (uint32_t)j * kRT;
@@ -352,6 +372,10 @@ __device__ __forceinline__ uint32_t scan_window(const RowsArgs& a, int32_t* s_pt
                                                 uint32_t limit, bool with_seg) {
   const uint32_t pn = min((uint32_t)kRScan, limit - pb);
   for (uint32_t t = threadIdx.x; t <= pn; t += kRT) s_ptr[t] = a.rowptr[pb + t];
+  if (a.lean && threadIdx.x == 0) {  // the next piece's col-slice min / max
+    s_misc[0] = INT_MAX;
+    s_misc[1] = INT_MIN;
+  }
   if (with_seg && threadIdx.x < 128) {
     const uint32_t q = pb + threadIdx.x;
     bool st = false;
@@ -499,6 +523,7 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   static const int32_t dbg = (int32_t)env_i64("AIMX_HOPR_DBG", 0);
   static const bool no_seg = env_i64("AIMX_HOP_NO_SEG", 0) != 0;
   static const int64_t lds_pad = env_i64("AIMX_HOPR_LDS_PAD", 0);  // experiments: fewer workgroups per CU
+  static const int32_t lean = env_i64("AIMX_HOPR_LEAN", 1) != 0 ? 1 : 0;
   // column passes: the fewest equal passes of at most wc_max floats
   const int64_t passes = cdiv(D, wc_max);
   const int64_t wc = (cdiv(D, passes) + 3) / 4 * 4;
@@ -558,6 +583,7 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   a.flat_zero = (contiguous && !add0 && !add1) ? 1 : 0;
   a.interleave = interleave;
   a.dbg = dbg;
+  a.lean = lean;
   const int64_t blocks = nsmall + nbig;
   if (blocks <= 0) return AIMX_OK;
   if (blocks >= (int64_t)INT32_MAX) return AIMX_EARG;
