@@ -136,6 +136,56 @@ __device__ __forceinline__ void stage_rows(const RowsArgs& a, float* s_x, uint32
   for (uint32_t t = threadIdx.x; t < a.wc / 4; t += kRT) z[t] = f4zero();
 }
 
+// stage_rows in two halves: the aligned float4 loads into registers (at most kRMaxU per thread;
+// the caller checks span * uo <= kRMaxU * kRT), and later their LDS stores plus the zero row. The
+// loads of the next column pass are issued before this pass's output stores, so their round trip
+// overlaps the stores instead of following the barrier after them.
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ void stage_load(const RowsArgs& a, float4 (&v)[kRMaxU], uint32_t first, uint32_t span,
+                                           const Pass& ps) {
+  const uint32_t units = span * ps.uo.d;
+#pragma unroll
+  for (int j = 0; j < kRMaxU; ++j) {
+    const uint32_t t = threadIdx.x + (uint32_t)j * kRT;
+    v[j] = f4zero();  // written on every path: the registers carry nothing across passes
+    if (t < units) {
+      const uint32_t rl = fdiv(t, ps.uo);
+      const uint32_t k = t - rl * ps.uo.d;
+      const float* g = src_row<SRC_CHUNKED>(a, first + rl) + ps.c0;
+      const uint32_t m = misal(g);
+      if ((int32_t)(4 * k) - (int32_t)m < (int32_t)ps.w) v[j] = *reinterpret_cast<const float4*>(g - m + 4 * k);
+    }
+  }
+}
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ void stage_put(const RowsArgs& a, float* s_x, const float4 (&v)[kRMaxU], uint32_t first,
+                                          uint32_t span, const Pass& ps) {
+  const uint32_t units = span * ps.uo.d;
+  const int32_t wi = (int32_t)ps.w;
+#pragma unroll
+  for (int j = 0; j < kRMaxU; ++j) {
+    const uint32_t t = threadIdx.x + (uint32_t)j * kRT;
+    if (t < units) {
+      const uint32_t rl = fdiv(t, ps.uo);
+      const uint32_t k = t - rl * ps.uo.d;
+      const uint32_t m = misal(src_row<SRC_CHUNKED>(a, first + rl) + ps.c0);
+      const int32_t c = (int32_t)(4 * k) - (int32_t)m;
+      if (c >= wi) continue;
+      float* d = s_x + rl * a.wc;
+      if (m == 0 && c + 3 < wi) {
+        *reinterpret_cast<float4*>(d + c) = v[j];
+      } else {
+        if (c >= 0) d[c] = v[j].x;
+        if (c + 1 >= 0 && c + 1 < wi) d[c + 1] = v[j].y;
+        if (c + 2 >= 0 && c + 2 < wi) d[c + 2] = v[j].z;
+        if (c + 3 < wi) d[c + 3] = v[j].w;
+      }
+    }
+  }
+  float4* z = reinterpret_cast<float4*>(s_x + span * a.wc);
+  for (uint32_t t = threadIdx.x; t < a.wc / 4; t += kRT) z[t] = f4zero();
+}
+
 // v (columns c .. c+3 of a row, c = 4u - m) += the same columns of row `arow` (pass-relative base).
 // first: v = add + v (the order hop.hip uses for add0), else v = v + add.
 __device__ __forceinline__ void add_cols(float4& v, const float* arow, uint32_t m, uint32_t u, int32_t c, int32_t w,
@@ -204,7 +254,7 @@ __device__ __forceinline__ void tile_put(float* s_t, uint32_t ot, uint32_t rl, u
 // [p0, p1). Called by the whole workgroup after a barrier; leaves every LDS region except the row
 // pointers reusable. spec: the piece is (part of) a molecule, so its own rows are staged while
 // the col slice loads.
-template <bool SRC_CHUNKED>
+template <bool SRC_CHUNKED, bool PRE>
 __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32_t* s_misc, int32_t* s_col,
                                       float* s_x, uint32_t r0, uint32_t nr, bool spec, uint32_t p0, uint32_t p1) {
   const int32_t base = P[0];
@@ -274,6 +324,8 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
   const char* xb = reinterpret_cast<const char*>(s_x);
   const char* cb = reinterpret_cast<const char*>(s_col);
   const uint32_t ot = a.wc + 4;
+  float4 pre[kRMaxU];  // the next pass's staged rows (stage_load), when they fit
+  bool pre_ok = false;
   for (uint32_t p = p0; p < p1; ++p) {
     const Pass ps = pass_of(a, p);
     const FastDiv& wu = ps.wu;
@@ -283,7 +335,10 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
       continue;
     }
     if (p > p0 && mode == 1) {
-      stage_rows<SRC_CHUNKED>(a, s_x, first, span, ps);
+      if (pre_ok)
+        stage_put<SRC_CHUNKED>(a, s_x, pre, first, span, ps);
+      else
+        stage_rows<SRC_CHUNKED>(a, s_x, first, span, ps);
       __syncthreads();
     }
     // sum phase: normalized units (row rl, columns 4v..4v+3 of this pass), in registers
@@ -348,6 +403,12 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
       }
     }
     __syncthreads();
+    pre_ok = false;
+    if (PRE && mode == 1 && p + 1 < p1) {
+      const Pass pn = pass_of(a, p + 1);
+      pre_ok = span * pn.uo.d <= (uint32_t)(kRMaxU * kRT);
+      if (pre_ok) stage_load<SRC_CHUNKED>(a, pre, first, span, pn);
+    }
     const uint32_t ounits = (a.dbg & 4) ? 0 : nr * uo.d;
     for (uint32_t t = threadIdx.x; t < ounits; t += kRT) {
       const uint32_t rl = fdiv(t, uo);
@@ -404,7 +465,9 @@ __device__ __forceinline__ int64_t next_start(const int32_t* s_misc, uint32_t pb
   return -1;
 }
 
-template <bool SRC_CHUNKED>
+// PRE: the next column pass's staging loads are issued before this pass's stores (stage_load):
+// 112 VGPRs (4 waves per SIMD) instead of 88 (5)
+template <bool SRC_CHUNKED, bool PRE>
 __global__ __launch_bounds__(kRT) void k_gather_rows(const RowsArgs a) {
   // [row pointers | misc | pad] [col_cap col entries] [staged rows / output tile]
   extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
@@ -490,7 +553,7 @@ __global__ __launch_bounds__(kRT) void k_gather_rows(const RowsArgs a) {
     }
     uint32_t pe = min(end, m + a.cap);
     while (pe > m + 1 && (uint32_t)(s_ptr[pe - pb] - s_ptr[m - pb]) >= a.col_cap) pe = m + (pe - m) / 2;
-    piece<SRC_CHUNKED>(a, s_ptr + (m - pb), s_misc, s_col, s_x, m, pe - m, seg, p0, p1);
+    piece<SRC_CHUNKED, PRE>(a, s_ptr + (m - pb), s_misc, s_col, s_x, m, pe - m, seg, p0, p1);
     m = pe;
   }
 }
@@ -524,6 +587,7 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   static const bool no_seg = env_i64("AIMX_HOP_NO_SEG", 0) != 0;
   static const int64_t lds_pad = env_i64("AIMX_HOPR_LDS_PAD", 0);  // experiments: fewer workgroups per CU
   static const int32_t lean = env_i64("AIMX_HOPR_LEAN", 1) != 0 ? 1 : 0;
+  static const int32_t prefetch = env_i64("AIMX_HOPR_PREFETCH", 0) != 0 ? 1 : 0;
   // column passes: the fewest equal passes of at most wc_max floats
   const int64_t passes = cdiv(D, wc_max);
   const int64_t wc = (cdiv(D, passes) + 3) / 4 * 4;
@@ -588,7 +652,8 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   if (blocks <= 0) return AIMX_OK;
   if (blocks >= (int64_t)INT32_MAX) return AIMX_EARG;
   using KFn = void (*)(const RowsArgs);
-  KFn fn = src_rpc > 0 ? k_gather_rows<true> : k_gather_rows<false>;
+  KFn fn = prefetch ? (src_rpc > 0 ? k_gather_rows<true, true> : k_gather_rows<false, true>)
+                    : (src_rpc > 0 ? k_gather_rows<true, false> : k_gather_rows<false, false>);
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kRT), dyn, stream, a);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
