@@ -27,8 +27,11 @@ backward graph, each in its own memory pool so that no replay overwrites the oth
 tensors). The eager path
 is used instead when a graph cannot reproduce eager semantics: grad disabled or eval mode,
 stereochemistry inputs, a batch without edges, stream capture already active (GraphedTrainStep),
-gradient hooks on the parameters or an initialised multi-rank process group (DDP's reducer hooks
-the gradient accumulators, which a replay bypasses). Parameters replaced since the capture (new
+or forward hooks on a submodule (a replay fires none). Under an initialised process group
+(DistributedDataParallel's reducer hooks every gradient accumulator, reference runner.py:703-707)
+or with gradient hooks on the parameters, the replayed gradients are handed out through autograd
+(_ReplayGrads) so the accumulators, their hooks and DDP's bucketed all-reduce see every one of
+them. Parameters replaced since the capture (new
 Parameter objects or moved storage) re-capture the bucket, and the autocast state is part of the
 bucket key (a capture bakes in the GEMMs' bf16 or fp32 operands). The attention weights and partial charges come back as detached copies.
 """
@@ -84,14 +87,22 @@ def wanted(model, args):
         return False
     if any(feats[k].dtype != torch.int64 or feats[k].dim() != 1 for k in _FEATURE_KEYS):
         return False
+    st = _state(model)
+    return not st.forward_hooked(model)
+
+
+def _through_autograd(model):
+    """Hand the gradients out through autograd (the parameters' AccumulateGrad nodes) instead of
+    assigning .grad: whenever something may be watching them — a process group is initialised
+    (DistributedDataParallel's reducer hooks every gradient accumulator, reference runner.py:703-707,
+    and averages the buckets as they become ready), or a parameter carries gradient hooks."""
     try:
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            return False
+        if dist.is_available() and dist.is_initialized():
+            return True
     except Exception:  # pragma: no cover
-        return False
-    st = _state(model)
-    return not st.hooked(model)
+        return True
+    return _state(model).grad_hooked(model)
 
 
 class _State:
@@ -100,11 +111,14 @@ class _State:
         self.order = []
         self.anchor = None
 
-    def hooked(self, model):
-        """Gradient hooks on a parameter or forward hooks on a submodule (a replay fires neither)."""
+    def forward_hooked(self, model):
+        """Forward hooks on a submodule: a replay cannot fire them (the eager path runs instead)."""
+        return any(m._forward_hooks or m._forward_pre_hooks for m in model.modules() if m is not model)
+
+    def grad_hooked(self, model):
+        """Gradient hooks on a parameter: the replay then hands its gradients out through autograd."""
         return any(getattr(p, "_post_accumulate_grad_hooks", None) or getattr(p, "_backward_hooks", None)
-                   for p in model.parameters()) or \
-            any(m._forward_hooks or m._forward_pre_hooks for m in model.modules() if m is not model)
+                   for p in model.parameters())
 
 
 def _state(model):
@@ -246,6 +260,30 @@ class _Replay(torch.autograd.Function):
         return None, None, None
 
 
+class _ReplayGrads(torch.autograd.Function):
+    """_Replay for watched gradients (_through_autograd): the parameters with a gradient are inputs,
+    and the backward replay's static gradients come back as their gradients, so autograd's
+    AccumulateGrad nodes — and every hook on them, DDP's reducer included — see each one. (The
+    engine clones a gradient the bucket still references, so each step's values stay the caller's.)"""
+
+    @staticmethod
+    def forward(ctx, anchor, bucket, G, *params):
+        ctx.bucket, ctx.G, ctx.gen = bucket, G, bucket.gen
+        return bucket.outs[0][:G].clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        b = ctx.bucket
+        if b.gen != ctx.gen or b.done == ctx.gen:
+            raise AimxError("aimx autograph: this output's saved state was overwritten by a later forward of the "
+                            "same shape bucket (or its backward already ran); run one backward per forward, or "
+                            "set AIMX_AUTOGRAPH=0")
+        b.gout[:ctx.G].copy_(gout)
+        b.g_bwd.replay()
+        b.done = ctx.gen
+        return (None, None, None, *[sg for sg in b.grads if sg is not None])
+
+
 def _pick(st, N, E, G, dev, amp):
     """The smallest live bucket that holds this batch (same molecule count and autocast state, room
     for one slack atom and every edge, padding molecules within PAD_ATOMS_MAX), else a new one sized
@@ -289,7 +327,10 @@ def run(model, args):
     b.gen += 1
     if st.anchor is None or st.anchor.device != dev:
         st.anchor = torch.zeros((), device=dev, requires_grad=True)
-    out = _Replay.apply(st.anchor, b, G)
+    if _through_autograd(model):
+        out = _ReplayGrads.apply(st.anchor, b, G, *[p for p, sg in zip(b.params, b.grads) if sg is not None])
+    else:
+        out = _Replay.apply(st.anchor, b, G)
     return out, _atoms(b.outs[1], b.Np, N), _atoms(b.outs[2], b.Np, N)
 
 

@@ -362,15 +362,21 @@ class BatchFeeder:
     and never blocks the host on the copy. Padding to static shapes (n_max/e_max/pad_mols) makes the
     batches replayable by one captured HIP graph.
 
-    Static shapes also let the feeder keep a ring of pinned host / device blobs with their batch
-    views built once, so a batch costs one native collate (the pool's threads, GIL released), one
-    async copy and two events, and no allocation. A ring slot is written again only when nothing
-    outside the ring still references its batch (a consumer that keeps batches, e.g. list(feeder),
-    makes the ring grow instead) and, on the device, after the consumer's work on it: its stream
-    records `released` when it asks for the next batch.
+    ring=True (static shapes only) keeps a ring of pinned host / device blobs with their batch views
+    built once, so a batch costs one native collate (the pool's threads, GIL released), one async
+    copy and two events, and no allocation. It is for consumers that COPY each batch before asking
+    for the next one (GraphedTrainStep copies it into its static inputs): a slot is written again
+    once its DeviceBatch object is referenced by nothing outside the ring (a consumer that keeps
+    batch objects, e.g. list(feeder), makes the ring grow instead) and, on the device, after the
+    consumer's work on it (its stream records `released` when it asks for the next batch) — but a
+    kept tensor VIEW of a batch (batch.targets appended for an epoch metric) is not seen, and its
+    contents change when the slot is refilled. By default (ring=False) every batch has a blob of
+    its own, so anything kept stays valid.
     """
 
-    def __init__(self, store, index_batches, max_hops, device, depth=3, threads=4, n_max=0, e_max=0, pad_mols=0):
+    def __init__(self, store, index_batches, max_hops, device, depth=3, threads=4, n_max=0, e_max=0, pad_mols=0,
+                 ring=False):
+        self.ring = bool(ring)
         self.store, self.device = store, torch.device(device)
         self.collator = HostCollator(max_hops, threads)
         self.pad = (n_max, e_max, pad_mols)
@@ -418,6 +424,7 @@ class BatchFeeder:
         import time
         T = self.times
         static = self.pad[0] > 0
+        use_ring = static and self.ring
         try:
             it = iter(self._it)
             while True:
@@ -431,7 +438,8 @@ class BatchFeeder:
                 t1 = time.perf_counter()
                 store, idx = item if isinstance(item, tuple) else (self.store, item)
                 tc = t1
-                if static:
+                sl = None
+                if use_ring:
                     nr, er, gr = self.pad[0], self.pad[1], len(idx) + self.pad[2]
                     t = store.n_tasks
                     layout, nbytes = self.collator.blob_layout(nr, er, gr, t)
@@ -448,7 +456,7 @@ class BatchFeeder:
                             raise
                         sl = None  # larger than the static capacity: this batch goes out unpadded
                     t2 = time.perf_counter()
-                if static and sl is not None:
+                if sl is not None:
                     with torch.cuda.stream(self.stream):
                         if sl.index >= 0:
                             self.stream.wait_event(sl.released)
@@ -459,9 +467,17 @@ class BatchFeeder:
                     b = sl.batch
                     ev, keep = sl.h2d, sl
                 else:
-                    if static:
-                        T["overflow"] += 1
-                    blob, layout, gr, nr, real = self.collator.collate_blob(store, idx, True)
+                    blob = None
+                    if static and not use_ring:  # padded into a blob of its own
+                        try:
+                            blob, layout, gr, nr, real = self.collator.collate_blob(store, idx, True, *self.pad)
+                        except HostError as e:
+                            if e.code != -2:
+                                raise
+                    if blob is None:  # unpadded, or over the static capacity
+                        if static:
+                            T["overflow"] += 1
+                        blob, layout, gr, nr, real = self.collator.collate_blob(store, idx, True)
                     t2 = time.perf_counter()
                     with torch.cuda.stream(self.stream):
                         dev = blob.to(self.device, non_blocking=True)

@@ -302,8 +302,9 @@ def main(argv=None):
     def epoch_batches(ep):
         p = np.random.default_rng(a.seed * 1000 + ep).permutation(len(shard))
         idx = [shard[p[i * B:(i + 1) * B]] for i in range(steps)]
+        # ring: the graphed step copies each batch into its static inputs (feed.BatchFeeder)
         return feed.BatchFeeder(store, iter(idx), a.hops, dev, depth=3, threads=4, n_max=n_max, e_max=e_max,
-                                pad_mols=pm)
+                                pad_mols=pm, ring=pad)
 
     graphed = None
     for ep in range(a.epochs):

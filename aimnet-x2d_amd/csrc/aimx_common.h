@@ -99,10 +99,15 @@ int launch_charge_bwd(const float* x, int64_t ldx, int64_t N, int64_t D, const i
                       hipStream_t s);
 
 // Fused node-update MLP of one shell layer (mlp.hip): all MLP blocks in one launch each way.
-bool mlp_fused_ok(int64_t D, int64_t nm);
+// D > 128 takes the weight-streamed kernels, which read their weights from MFMA-fragment images:
+// mlp_pack_floats(s) floats (0: not needed) written by launch_mlp_pack once per call and direction,
+// passed as `pack` (nullptr: the weight-resident kernels).
+bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision);
+size_t mlp_pack_floats(const AimxShellStack* s);
+int launch_mlp_pack(const AimxShellStack* s, bool bwd, float* dst, hipStream_t st);
 int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64_t ldx, float* out, int64_t ldo,
-                   hipStream_t st);
+                   const float* pack, hipStream_t st);
 int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t lddy, float* const* dV,
-                   float* const* dA, float* dug, hipStream_t st);
+                   float* const* dA, float* dug, const float* pack, hipStream_t st);
 
 }  // namespace aimx

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     if (a.zc_dim == 0) {
       kend = min(kend, zE);
     } else if (n0 >= zE && !(a.ones_col && n0 + BN > Nreal)) {  // never the tile of the ones column
-      if (blockIdx.z == 0) zero_tile<BM, BN>(a, m0, n0, M, Nreal);
+      if (blockIdx.z == 0 && a.zc_dim == 1) zero_tile<BM, BN>(a, m0, n0, M, Nreal);  // zc_dim 2: no store
       return;
     }
   }
@@ -1523,10 +1523,10 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   if (a.ones_col && (!a.col_out || a.N < 1)) return AIMX_EARG;
   if ((a.mask_out || a.mask_in) && !(a.drop_p < 1.f)) return AIMX_EARG;
   if (a.mask_out && !a.drop_seed) return AIMX_EARG;
-  if (a.zc_rowptr) {  // trimming: sane chunk geometry; zc_dim 1 only with a plain-store epilogue
-    if (a.zc_chunks < 0 || a.zc_rows < 0 || a.zc_width < 0 || (a.zc_dim != 0 && a.zc_dim != 1)) return AIMX_EARG;
+  if (a.zc_rowptr) {  // trimming: sane chunk geometry; zc_dim 1 / 2 only with a plain-store epilogue
+    if (a.zc_chunks < 0 || a.zc_rows < 0 || a.zc_width < 0 || a.zc_dim < 0 || a.zc_dim > 2) return AIMX_EARG;
     if (a.zc_width * (a.zc_chunks + 1) >= (1ll << 31)) return AIMX_EARG;
-    if (a.zc_dim == 1 && (a.beta != 0.f || a.bias || a.res[0] || a.res[1] || a.res[2] || a.act_ncols > 0 ||
+    if (a.zc_dim != 0 && (a.beta != 0.f || a.bias || a.res[0] || a.res[1] || a.res[2] || a.act_ncols > 0 ||
                           a.pre || a.dact_pre || a.mask_in || a.mask_out))
       return AIMX_EARG;
   }

@@ -68,7 +68,6 @@ struct RowsArgs {
   int64_t add1_ld;
   const int64_t* seg;  // molecule id per row of [0, split) (optional)
   int64_t seg_stride;
-  int32_t dbg;  // AIMX_HOPR_DBG phase knock-outs (timing experiments only; results are wrong when != 0)
   int32_t lean;  // fewer barriers per piece (AIMX_HOPR_LEAN=0: the round-3 schedule, for A/B)
 };
 
@@ -112,7 +111,7 @@ template <bool SRC_CHUNKED>
 __device__ __forceinline__ void stage_rows(const RowsArgs& a, float* s_x, uint32_t first, uint32_t span,
                                            const Pass& ps) {
   const FastDiv& su = ps.uo;
-  const uint32_t units = (a.dbg & 2) ? 0 : span * su.d;
+  const uint32_t units = span * su.d;
   const int32_t wi = (int32_t)ps.w;
   for (uint32_t t = threadIdx.x; t < units; t += kRT) {
     const uint32_t rl = fdiv(t, su);
@@ -348,7 +347,7 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
     for (int j = 0; j < kRMaxU; ++j) {
       const uint32_t t = threadIdx.x + (uint32_t)j * kRT;
       float4 acc = f4zero();
-      if (t < units && !(a.dbg & 1)) {
+      if (t < units) {
         const uint32_t rl = fdiv(t, wu);
         const uint32_t v = t - rl * wu.d;
         if (mode == 1) {
@@ -409,7 +408,7 @@ __device__ __forceinline__ void piece(const RowsArgs& a, const int32_t* P, int32
       pre_ok = span * pn.uo.d <= (uint32_t)(kRMaxU * kRT);
       if (pre_ok) stage_load<SRC_CHUNKED>(a, pre, first, span, pn);
     }
-    const uint32_t ounits = (a.dbg & 4) ? 0 : nr * uo.d;
+    const uint32_t ounits = nr * uo.d;
     for (uint32_t t = threadIdx.x; t < ounits; t += kRT) {
       const uint32_t rl = fdiv(t, uo);
       const uint32_t u = t - rl * uo.d;
@@ -499,7 +498,6 @@ __global__ __launch_bounds__(kRT) void k_gather_rows(const RowsArgs a) {
     R0 = w * a.win;
     R1 = min(R0 + a.win, a.split);
   } else {
-    if (a.dbg & 8) return;
     R0 = a.split + bbig * a.big_rows;
     R1 = min(R0 + a.big_rows, a.rows);
     if (threadIdx.x == 0) {
@@ -583,7 +581,6 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   static const int64_t split_env = env_i64("AIMX_HOPR_SPLIT", 2);
   static const int64_t split_below = env_i64("AIMX_HOPR_SPLIT_BELOW", 8192);
   static const int32_t interleave = env_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
-  static const int32_t dbg = (int32_t)env_i64("AIMX_HOPR_DBG", 0);
   static const bool no_seg = env_i64("AIMX_HOP_NO_SEG", 0) != 0;
   static const int64_t lds_pad = env_i64("AIMX_HOPR_LDS_PAD", 0);  // experiments: fewer workgroups per CU
   static const int32_t lean = env_i64("AIMX_HOPR_LEAN", 1) != 0 ? 1 : 0;
@@ -646,7 +643,6 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   const bool contiguous = out_ld == D && (out_rpc <= 0 || out_cs == out_rpc * out_ld);
   a.flat_zero = (contiguous && !add0 && !add1) ? 1 : 0;
   a.interleave = interleave;
-  a.dbg = dbg;
   a.lean = lean;
   const int64_t blocks = nsmall + nbig;
   if (blocks <= 0) return AIMX_OK;

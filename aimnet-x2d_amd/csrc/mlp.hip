@@ -8,14 +8,18 @@
 // backward, given dY = d out:
 //   dA_nm = dY ; dV_k = (dA_{k+1} W2_k) * mask / (1-p) * act'(v_k) ; dA_k = dA_{k+1} + dV_k W1_k
 //   du = dA_0 * act'(u) ;  dUG = [du | dY]
-// Launched per GEMM these are 2 * nm latency-bound kernels per layer and direction (N = atoms
-// rows, D x D weights: ~8-12 us each at c2). Here a workgroup owns 32 atoms: its activations stay
-// in LDS for the whole chain, each wave owns 16 output columns (both 16-row tiles, two independent
-// MFMA accumulators) and streams its own weight rows through a private LDS slice, so the only
-// workgroup barriers are the one per GEMM. Dropout uses the same hash, salt and index as the
-// per-GEMM path (hash(seed, layer * nm + k, row * D + col)), so the masks are identical.
+// Launched per GEMM these are 2 * nm kernels per layer and direction, each re-reading its row
+// operand from HBM and paying a launch. Two variants keep a row chunk's activations on chip for
+// the whole chain:
+//   * weight-resident (k_mlpw_*, D <= 128): every block's weights staged in LDS once per CU;
+//   * weight-streamed (k_mlps_*, D > 128, where 2 * nm D x D weights exceed the LDS): the weights
+//     are pre-packed once per call in MFMA fragment order and each wave streams its own column
+//     fragments straight from L2 into a register ring, 4 k-groups ahead, across GEMM boundaries.
+// Dropout uses the same hash, salt and index as the per-GEMM path (hash(seed, layer * nm + k,
+// row * D + col)), so the masks are identical.
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "aimx_common.h"
 
@@ -23,114 +27,10 @@ namespace aimx {
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-constexpr int kRT = 1;                 // 16-row tiles per workgroup
-constexpr int kRows = 16 * kRT;        // atoms per workgroup
-constexpr int kBK = 32;                // k slice
-constexpr int kBSt = kBK + 4;          // LDS row stride of a staged weight slice
-constexpr int kWS = 16 * kBSt;         // floats of one wave's staging slice
-constexpr int kP = 4;                  // weight slices in flight per wave
-constexpr int kInitUnroll = 12;        // tile loads in flight per thread at kernel start
-constexpr int kMaxWaves = 8;  // <= 512 threads: up to 256 VGPRs per lane (no spills)
-
-__host__ __device__ inline int pad32(int d) { return (d + 31) / 32 * 32; }
-__host__ __device__ inline int lds_stride(int d) { return pad32(d) + 4; }  // = 4 mod 32: conflict-free b128
-
-// C[32][N] = A[32][K] . B over a workgroup; A in LDS (row stride lda, zero in columns [K, Kp)).
-// B(k, n) = W[n * ldw + k] when KC (k-contiguous: nn.Linear forward) else W[k * ldw + n].
-// Wave w owns column fragments cf = w, w + nwaves, ... (16 columns each) for both row tiles.
-template <bool KC, class Pre, class Epi>
-__device__ __forceinline__ void rows_gemm(const float* A, int lda, int K, const float* W, int64_t ldw, int N,
-                                          float* Bs, Pre pre, Epi epi) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int nsl = pad32(K) / kBK;
-  const int lr = lane & 15, lq = 4 * (lane >> 4);
-  float* Bw = Bs + wave * kWS;
-  const int CF = (N + 15) / 16;
-  for (int cf = wave; cf < CF; cf += nw) {
-    const int n0 = cf * 16;
-    // staging sources (clamped: rows/cols past N and k past K read valid finite weights whose
-    // products meet zero A columns or land in dropped outputs)
-    const float* src[2];
-    int dst[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (KC) {
-        const int row = 8 * i + (lane >> 3), kq = (lane & 7) * 4;
-        src[i] = W + (int64_t)min(n0 + row, N - 1) * ldw + kq;
-        dst[i] = row * kBSt + kq;
-      } else {
-        const int kr = (lane >> 2) + 16 * i, nq = min(n0 + (lane & 3) * 4, N - 4) - n0;
-        src[i] = W + (int64_t)kr * ldw + n0 + nq;
-        dst[i] = nq * kBSt + kr;  // transposed on the store
-      }
-    }
-    const int col = n0 + lr;
-    float2 pv[kRT][4];
-#pragma unroll
-    for (int t = 0; t < kRT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pv[t][r] = pre(t * 16 + (lane >> 4) * 4 + r, min(col, N - 1));
-    floatx4 acc[kRT];
-#pragma unroll
-    for (int t = 0; t < kRT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    floatx4 rg[kP][2];
-    auto load = [&](int sl, floatx4 (&r)[2]) {
-      const int s = min(sl, nsl - 1);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (KC) {
-          // k quad past K: clamp to the last full quad (K % 4 == 0 is required on the host)
-          const int k = min(s * kBK + (lane & 7) * 4, K - 4) - (lane & 7) * 4;
-          r[i] = *reinterpret_cast<const floatx4*>(src[i] + k);
-        } else {
-          const int k = min(s * kBK + (lane >> 2) + 16 * i, K - 1) - ((lane >> 2) + 16 * i);
-          r[i] = *reinterpret_cast<const floatx4*>(src[i] + (int64_t)k * ldw);
-        }
-      }
-    };
-#pragma unroll
-    for (int q = 0; q < kP; ++q) load(q, rg[q]);
-    __builtin_amdgcn_sched_barrier(0);
-    const float* b0 = Bw + lr * kBSt + lq;
-    for (int s0 = 0; s0 < nsl; s0 += kP) {
-#pragma unroll
-      for (int q = 0; q < kP; ++q) {
-        const int sl = s0 + q;
-        if (sl < nsl) {  // uniform
-          if (KC) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) *reinterpret_cast<floatx4*>(Bw + dst[i]) = rg[q][i];
-          } else {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) Bw[dst[i] + e * kBSt] = rg[q][i][e];
-          }
-          load(sl + kP, rg[q]);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const floatx4 b = *reinterpret_cast<const floatx4*>(b0 + 16 * h);
-#pragma unroll
-            for (int t = 0; t < kRT; ++t) {
-              const floatx4 a = *reinterpret_cast<const floatx4*>(A + (t * 16 + lr) * lda + sl * kBK + lq + 16 * h);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc[t], 0, 0, 0);
-            }
-          }
-        }
-      }
-    }
-    if (col < N) {
-#pragma unroll
-      for (int t = 0; t < kRT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) epi(t * 16 + (lane >> 4) * 4 + r, col, acc[t][r], pv[t][r]);
-    }
-  }
-  __syncthreads();
-}
+// global-address-space views of pointers read from LDS tables (a generic pointer makes every access a
+// flat op, which the waitcnt pass must treat as both LDS and VMEM: vmcnt(0) lgkmcnt(0) everywhere)
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) uint8_t gu8;
 
 __device__ __forceinline__ float drop_scale(float p) { return p < 1.f ? 1.f / (1.f - p) : 0.f; }
 
@@ -155,93 +55,6 @@ struct MlpFwd {
   int32_t v4;  // fill with 16-byte loads (D, 2D and every weight / row pointer 4-float aligned)
 };
 
-__global__ __launch_bounds__(512) void k_mlp_fwd(const MlpFwd p) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int D = (int)p.D, lda = lds_stride(D), Dp = pad32(D);
-  const int nw = blockDim.x >> 6;
-  float* Bs = lds;
-  float* Xa = lds + nw * kWS;    // current block input a_k   [32][lda]
-  float* Hb = Xa + kRows * lda;  // r_k                        [32][lda]
-  const int64_t r0 = (int64_t)blockIdx.x * kRows;
-  const int64_t N = p.N;
-  // all of the tile's loads in flight at once (a plain strided loop issues them one round trip
-  // at a time); zero k padding for both A operands
-  for (int e0 = 0; e0 < kRows * Dp; e0 += kInitUnroll * (int)blockDim.x) {
-    float v[kInitUnroll];
-#pragma unroll
-    for (int u = 0; u < kInitUnroll; ++u) {
-      const int e = e0 + u * blockDim.x + threadIdx.x;
-      const int r = e / Dp, c = e - r * Dp;
-      const int64_t g = r0 + r;
-      const bool ok = e < kRows * Dp && c < D && g < N;
-      v[u] = p.ug[(ok ? g * 2 * D + c : 0)];
-      v[u] = ok ? v[u] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < kInitUnroll; ++u) {
-      const int e = e0 + u * blockDim.x + threadIdx.x;
-      if (e < kRows * Dp) {
-        const int r = e / Dp, c = e - r * Dp;
-        Xa[r * lda + c] = v[u];
-        Hb[r * lda + c] = 0.f;
-      }
-    }
-  }
-  __syncthreads();
-  const float scale = drop_scale(p.drop_p);
-  const uint64_t seed = p.drop ? (uint64_t)*p.seed : 0;
-  for (int k = 0; k < p.nm; ++k) {
-    const bool last = k == p.nm - 1;
-    float* V = p.V[k];
-    float* R = p.R[k];
-    uint8_t* M = p.M[k];
-    const float* b1 = p.b1[k];
-    const uint32_t salt = (uint32_t)(p.salt0 + k);
-    rows_gemm<true>(Xa, lda, D, p.w1[k], D, D, Bs, [&](int, int c) { return make_float2(b1[c], 0.f); },
-                    [&](int r, int c, float acc, float2 pv) {
-                      const int64_t g = r0 + r;
-                      const float v = acc + pv.x;
-                      float a = act_fwd(p.act, v);
-                      if (p.drop) {
-                        const bool keep = hash_uniform(seed, salt, (uint64_t)g * (uint64_t)D + (uint64_t)c) >= p.drop_p;
-                        a = keep ? a * scale : 0.f;
-                        if (g < N) M[g * D + c] = keep ? 1 : 0;
-                      }
-                      Hb[r * lda + c] = a;
-                      if (g < N) {
-                        V[g * D + c] = v;
-                        R[g * D + c] = a;
-                      }
-                    });
-    const float* b2 = p.b2[k];
-    float* Ak = last ? nullptr : p.A[k];
-    // epilogue operands: b2, and for the last block the global skip g (+ outer residual x)
-    rows_gemm<true>(Hb, lda, D, p.w2[k], D, D, Bs,
-                    [&](int r, int c) {
-                      float add = b2[c];
-                      if (last) {
-                        const int64_t g = min(r0 + r, N - 1);
-                        add += p.ug[g * 2 * D + D + c];
-                        if (p.x) add += p.x[g * p.ldx + c];
-                      }
-                      return make_float2(add, 0.f);
-                    },
-                    [&](int r, int c, float acc, float2 pv) {
-                      const int64_t g = r0 + r;
-                      // a_{k+1} = r W2^T + b2 + a_k (+ g + x): the GEMM path's epilogue order
-                      // (bias, then residuals in argument order) up to fp32 rounding
-                      const float a = acc + pv.x + Xa[r * lda + c];
-                      Xa[r * lda + c] = a;
-                      if (g < N) {
-                        if (last)
-                          p.out[g * p.ldo + c] = a;
-                        else
-                          Ak[g * D + c] = a;
-                      }
-                    });
-  }
-}
-
 struct MlpBwd {
   int64_t N, D;
   int32_t nm, act, drop;
@@ -259,82 +72,10 @@ struct MlpBwd {
   int32_t v4;       // fill with 16-byte loads (D, lddy and every weight / dy pointer 4-float aligned)
 };
 
-__global__ __launch_bounds__(512) void k_mlp_bwd(const MlpBwd p) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int D = (int)p.D, lda = lds_stride(D), Dp = pad32(D);
-  const int nw = blockDim.x >> 6;
-  float* Bs = lds;
-  float* DA = lds + nw * kWS;    // gradient w.r.t. the current block output   [32][lda]
-  float* DV = DA + kRows * lda;  // dV_k                                        [32][lda]
-  const int64_t r0 = (int64_t)blockIdx.x * kRows;
-  const int64_t N = p.N;
-  for (int e0 = 0; e0 < kRows * Dp; e0 += kInitUnroll * (int)blockDim.x) {
-    float v[kInitUnroll];
-#pragma unroll
-    for (int u = 0; u < kInitUnroll; ++u) {
-      const int e = e0 + u * blockDim.x + threadIdx.x;
-      const int r = e / Dp, c = e - r * Dp;
-      const int64_t g = r0 + r;
-      const bool ok = e < kRows * Dp && c < D && g < N;
-      v[u] = p.dy[(ok ? g * p.lddy + c : 0)];
-      v[u] = ok ? v[u] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < kInitUnroll; ++u) {
-      const int e = e0 + u * blockDim.x + threadIdx.x;
-      if (e < kRows * Dp) {
-        const int r = e / Dp, c = e - r * Dp;
-        const int64_t g = r0 + r;
-        DA[r * lda + c] = v[u];
-        DV[r * lda + c] = 0.f;
-        if (c < D && g < N) p.dug[g * 2 * D + D + c] = v[u];  // dg = dY
-      }
-    }
-  }
-  __syncthreads();
-  const float scale = drop_scale(p.drop_p);
-  for (int k = p.nm - 1; k >= 0; --k) {
-    const float* V = p.V[k];
-    const uint8_t* M = p.M[k];
-    float* dVk = p.dV[k];
-    // dV = (dA W2) * mask/(1-p) * act'(v)
-    rows_gemm<false>(DA, lda, D, p.w2[k], D, D, Bs,
-                     [&](int r, int c) {
-                       const int64_t g = min(r0 + r, N - 1);
-                       const float m = p.drop ? (M[g * D + c] ? scale : 0.f) : 1.f;
-                       return make_float2(act_grad(p.act, V[g * D + c]), m);
-                     },
-                     [&](int r, int c, float acc, float2 pv) {
-                       const int64_t g = r0 + r;
-                       const float dv = (g < N) ? acc * pv.y * pv.x : 0.f;
-                       DV[r * lda + c] = dv;
-                       if (g < N) dVk[g * D + c] = dv;
-                     });
-    // dA_k = dA_{k+1} + dV W1 ; for k == 0: du = dA_0 * act'(u)
-    float* dAk = k > 0 ? p.dA[k - 1] : nullptr;
-    rows_gemm<false>(DV, lda, D, p.w1[k], D, D, Bs,
-                     [&](int r, int c) {
-                       const int64_t g = min(r0 + r, N - 1);
-                       return make_float2(k == 0 ? act_grad(p.act, p.u[g * D + c]) : 1.f, 0.f);
-                     },
-                     [&](int r, int c, float acc, float2 pv) {
-                       const int64_t g = r0 + r;
-                       const float da = DA[r * lda + c] + acc;
-                       DA[r * lda + c] = da;
-                       if (g < N) {
-                         if (k > 0)
-                           dAk[g * D + c] = da;
-                         else
-                           p.dug[g * 2 * D + c] = da * pv.x;
-                       }
-                     });
-  }
-}
-
 // ---- Weight-resident variant (small D: every block's weights fit in LDS) --------------------------
-// The per-row-tile kernels above re-stream each weight fragment from L2 in every GEMM phase of every
-// workgroup, with the first loads of each phase exposed (measured 48 / 54 us per layer at c2 vs
-// ~42 / 43 us for the four separate GEMMs). Here a persistent workgroup (one per CU) stages ALL
+// A first per-row-tile chain (16 rows per workgroup, each weight fragment re-streamed from L2 through
+// LDS in every GEMM phase, first loads of each phase exposed) measured 48 / 54 us per layer at c2 vs
+// ~42 / 43 us for the four separate GEMMs (round 2; removed). Here a persistent workgroup (one per CU) stages ALL
 // 2*nm weight matrices of the layer in LDS once — as k-contiguous rows, transposed for the backward
 // — and then walks row chunks of 16*rt atoms: each GEMM phase is rt x CF (16 x 16) output tiles, one
 // per wave, over K padded to 16 with zeros, every operand read from LDS by 16-byte ds_reads with the
@@ -404,6 +145,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* p, uint32
 __device__ __forceinline__ float mlp_bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off) { return mlp_bload(r, off); }
 
 template <bool TR>
 __device__ __forceinline__ void fill_lds(float* Wl, const float* const* wtab, int nmat, int D, int Kp, int S,
@@ -831,6 +573,402 @@ extern "C" int aimx_mlpw_trace_read(long long* out) {
 namespace {
 #endif
 
+// ---- Weight-streamed variant (D > 128) ------------------------------------------------------------
+// At c4 / c5 (D = 153 / 307) one block's two D x D weights already exceed the LDS, and per GEMM the
+// node update ran as 2 * nm separate MFMA GEMMs of 29-47 us each (16-33 % of the fp32 MFMA peak).
+// Here a workgroup owns a chunk of R = 16 rt rows (rt picked so the chunks fill the CUs in one round:
+// c4 96 rows, c5 48) and keeps the chain's two activation tiles in LDS (forward: the block input a_k
+// and r_k; backward: dA and dV). Wave w owns 16-column fragments w, w + nw, ... (NF of them) of
+// every GEMM and all rt row tiles of the chunk, so one B fragment feeds rt MFMAs. The B operand never
+// touches LDS: k_mlps_pack lays every weight out once per call in MFMA fragment order (the image of
+// matrix m is [fragment f][k group g][lane] float4s: lane l holds B(16 g + 4 (l >> 4) + j, 16 f + (l & 15)),
+// j = 0..3, zero outside D x D), so a wave's B for one 16-wide k group is ONE coalesced 1 KiB
+// load, streamed from L2 into a register ring P = 4 or 5 groups ahead. The ring runs over the whole chain:
+// the next GEMM's first groups are in flight during the current GEMM's last ones and its epilogue.
+// The A operand is the k-permuted 16-byte LDS read of the weight-resident kernels (one ds_read_b128
+// per row tile feeds 4 MFMAs). Epilogues, dropout hash, salts and outputs (V, R, M, A, out / dV, dA,
+// dUG) are the per-GEMM path's.
+constexpr int kSMaxThreads = 768;                // <= 12 waves: up to 170 VGPRs per lane
+constexpr int kMlpsDynLds = 160 * 1024 - 1024;   // + the static pointer tables
+
+struct SGeom {
+  int32_t CF;  // 16-wide output fragments of D: pad16(D) / 16
+  int32_t G;   // 16-wide k groups streamed per GEMM: CF rounded up to a multiple of the ring depth P
+  int32_t S;   // LDS row stride of an activation tile (floats): 16 G + 4 (conflict-free b128 reads)
+  int32_t nw;  // waves
+};
+
+struct MlpPack {
+  const float* w[32];
+  int32_t nmat, D, CF, G, tr;  // tr: image of W^T (backward: B(k, n) = W[k][n])
+  floatx4* dst;                 // one layer's block: CF * nmat * G * 64 float4s
+};
+
+__global__ void k_mlps_pack(const MlpPack p) {
+  // images of one layer: [f][phase][g][lane] (BStream); p.nmat = 2 nm phases of one layer
+  const int64_t total = (int64_t)p.CF * p.nmat * p.G * 64;
+  __shared__ const float* tab[32];
+  if (threadIdx.x < 32) tab[threadIdx.x] = p.w[threadIdx.x];
+  __syncthreads();
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < total; u += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(u & 63);
+    const int64_t q = u >> 6;
+    const int g = (int)(q % p.G);
+    const int m = (int)((q / p.G) % p.nmat);
+    const int f = (int)(q / ((int64_t)p.G * p.nmat));
+    const int n = 16 * f + (lane & 15), k0 = 16 * g + 4 * (lane >> 4);
+    const float* W = tab[m];
+    floatx4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + j;
+      v[j] = (n < p.D && k < p.D) ? (p.tr ? W[k * p.D + n] : W[n * p.D + k]) : 0.f;
+    }
+    p.dst[u] = v;
+  }
+}
+
+// One k group of the chain's GEMM stream: acc[t][i] += A(rows of tile t, k group g) . B(k group, fragment i).
+// Row tiles go in pairs (two independent accumulators per B value), each pair's A operands read just
+// before its MFMAs: all RT tiles' A reads in flight at once would hold 4 RT VGPRs.
+template <int RT, int NF>
+__device__ __forceinline__ void mlps_group(floatx4 (&acc)[RT][NF], const float* As, int S, int g, const floatx4 (&b)[NF]) {
+  const int lane = threadIdx.x & 63, lr = lane & 15, lq = 4 * (lane >> 4);
+  const float* a0 = As + lr * S + 16 * g + lq;
+#pragma unroll
+  for (int t0 = 0; t0 < RT; t0 += 2) {
+    constexpr int kW = 2;
+    floatx4 a[kW];
+#pragma unroll
+    for (int u = 0; u < kW; ++u)
+      if (t0 + u < RT) a[u] = *reinterpret_cast<const floatx4*>(a0 + 16 * (t0 + u) * S);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < kW; ++u)
+#pragma unroll
+        for (int i = 0; i < NF; ++i)
+          if (t0 + u < RT) acc[t0 + u][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], b[i][j], acc[t0 + u][i], 0, 0, 0);
+    if (t0 + 2 < RT) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The B stream of one wave: items s = (phase, k group) in chain order. An image block holds, per
+// fragment f, all 2 nm phases' G k groups back to back ([f][phase][g][lane] float4s; G >= CF,
+// G % P == 0, groups past CF zero), so item s of fragment f is ONE pointer step from item s - 1, and
+// item s always sits in ring slot s % P (every GEMM starts at slot 0).
+template <int NF>
+struct BStream {
+  const floatx4* ptr[NF];  // this lane's float4 of the next item, per fragment
+  const floatx4* last[NF];  // the last item (loads past the end re-read it: never used)
+  __device__ __forceinline__ void next(floatx4 (&r)[NF]) {
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      r[i] = *ptr[i];
+      ptr[i] = ptr[i] + 64 < last[i] ? ptr[i] + 64 : last[i];
+    }
+  }
+  __device__ __forceinline__ void init(const floatx4* img, const int (&fr)[NF], int total) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      ptr[i] = img + (int64_t)fr[i] * total * 64 + lane;
+      last[i] = ptr[i] + (int64_t)(total - 1) * 64;
+    }
+  }
+};
+
+// The k group loop of one GEMM of the chain (G groups from ring slot 0), keeping the ring P ahead.
+template <int RT, int NF, int P>
+__device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring)[P][NF], BStream<NF>& bs, const float* As,
+                                          int S, int G) {
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int i = 0; i < NF; ++i) acc[t][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int g0 = 0; g0 < G; g0 += P) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      mlps_group<RT, NF>(acc, As, S, g0 + q, ring[q]);
+      // refill the slot only after its MFMAs have read it: the load then targets the same registers
+      // (a refill issued before the last read needs fresh registers and a copy at the loop's back
+      // edge, and copying a register with a load in flight waits for that load: vmcnt(0))
+      bs.next(ring[q]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// p.X[k] for a uniform runtime k without indexing the kernel-argument array (dynamic indexing copies
+// the whole argument struct to scratch): scalar loads at fixed offsets and selects
+template <class T>
+__device__ __forceinline__ T pick8(T const (&a)[8], int k) {
+  T r = a[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) r = (k == i) ? a[i] : r;
+  return r;
+}
+
+template <int RT, int NF, int P>
+__global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int R = 16 * RT;
+  // epilogue operands prefetched into registers during the GEMM where they fit (else loaded in the
+  // epilogue): 8 RT NF VGPRs
+  constexpr bool kPre = NF == 1 || RT <= 2;
+  const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
+  float* Xa = lds;              // block input a_k [R][S]
+  float* Hb = lds + R * S;      // r_k             [R][S]
+  float* Bia = lds + 2 * R * S;  // b1_k at 2k, b2_k at 2k+1: [16 CF] each
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = 4 * (lane >> 4);
+  for (int e = threadIdx.x; e < 2 * nm * 16 * CF; e += blockDim.x) {
+    const int m = e / (16 * CF), c = e - m * (16 * CF);
+    const float* bb = pick8((m & 1) ? p.b2 : p.b1, m >> 1);
+    Bia[e] = c < D ? bb[c] : 0.f;
+  }
+  const int64_t N = p.N, nchunk = cdiv(N, R);
+  const int nph = 2 * nm;
+  int fr[NF];
+  bool fok[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    fok[i] = wave + i * nw < CF && 16 * (wave + i * nw) + lr < D;
+    fr[i] = min(wave + i * nw, CF - 1);
+  }
+  const float scale = drop_scale(p.drop_p);
+  const uint64_t seed = p.drop ? (uint64_t)*p.seed : 0;
+  // the last block's residual operands as buffer loads (an absent x reads 0: no branch per load)
+  const __amdgpu_buffer_rsrc_t rug = mlp_rsrc(p.ug, (uint32_t)(4 * N * 2 * D));
+  const __amdgpu_buffer_rsrc_t rx_ = mlp_rsrc(p.x, p.x ? (uint32_t)(4 * ((N - 1) * p.ldx + D)) : 0u);
+  for (int e = threadIdx.x; e < R * S; e += blockDim.x) Hb[e] = 0.f;  // k padding of the W2 GEMMs' A
+  for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+    const int64_t r0c = ch * R;
+    __syncthreads();  // the previous chunk's last reads of Xa are done
+    load_rows(Xa, S, p.ug, 2 * p.D, r0c, R, D, 16 * G, N);  // a0 = act(u) = UG[:, :D]; zero beyond D and N
+    __syncthreads();
+    BStream<NF> bs;
+    bs.init(img, fr, nph * G);
+    floatx4 ring[P][NF];
+#pragma unroll
+    for (int q = 0; q < P; ++q) bs.next(ring[q]);
+    floatx4 acc[RT][NF];
+    for (int ph = 0; ph < nph; ++ph) {
+      // an opaque per-GEMM copy of the chunk origin: every epilogue address derives from it, so the
+      // compiler recomputes them per GEMM instead of hoisting RT x NF x 4 of them out of the loop
+      int64_t r0 = r0c;
+      asm volatile("" : "+s"(r0));
+      const int k = ph >> 1;
+      const bool w1 = (ph & 1) == 0, last = ph == nph - 1;
+      // epilogue operands, in flight during the GEMM (consumed only in the epilogue: an add here
+      // would wait for the loads at once): bias; after the last block g and x
+      float bia[NF], rg[RT][NF][4], rx[RT][NF][4];
+#pragma unroll
+      for (int i = 0; i < NF; ++i) bia[i] = Bia[ph * 16 * CF + 16 * fr[i] + lr];
+      if (kPre && last) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int i = 0; i < NF; ++i) {
+            const int c = min(16 * fr[i] + lr, D - 1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t gr = (uint32_t)min(r0 + 16 * t + lq + r, N - 1);
+              rg[t][i][r] = bload(rug, 4u * (gr * (uint32_t)(2 * D) + (uint32_t)(D + c)));
+              rx[t][i][r] = bload(rx_, 4u * (gr * (uint32_t)p.ldx + (uint32_t)c));  // 0 without x
+            }
+          }
+      }
+      mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G);
+      // everything the epilogue addresses derives from these opaque copies, so none of it is
+      // computed ahead of the GEMM and held across it
+      int lo = lane;
+      asm volatile("" : "+s"(r0), "+v"(lo));
+      const int lr = lo & 15, lq = 4 * (lo >> 4);
+      if (w1) {  // v = a W1^T + b1 ; r = dropout(act(v))
+        gfloat* V = (gfloat*)pick8(p.V, k);
+        gfloat* Rk = (gfloat*)pick8(p.R, k);
+        gu8* M = (gu8*)pick8(p.M, k);
+        const uint32_t salt = (uint32_t)(p.salt0 + k);
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int i = 0; i < NF; ++i) {
+            if (!fok[i]) continue;
+            const int c = 16 * fr[i] + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * t + lq + r;
+              const int64_t gr = r0 + row;
+              const uint32_t o = (uint32_t)gr * (uint32_t)D + (uint32_t)c;
+              const float v = acc[t][i][r] + bia[i];
+              float a = act_fwd(p.act, v);
+              if (p.drop) {
+                const bool keep = hash_uniform(seed, salt, (uint64_t)o) >= p.drop_p;
+                a = keep ? a * scale : 0.f;
+                if (gr < N) M[o] = keep ? 1 : 0;
+              }
+              Hb[row * S + c] = a;
+              if (gr < N) {
+                V[o] = v;
+                Rk[o] = a;
+              }
+            }
+          }
+      } else {  // a_{k+1} = r W2^T + b2 + a_k (+ g + x after the last block)
+        gfloat* Ak = (gfloat*)pick8(p.A, k);
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int i = 0; i < NF; ++i) {
+            if (!fok[i]) continue;
+            const int c = 16 * fr[i] + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * t + lq + r;
+              const int64_t gr = r0 + row;
+              float a = (acc[t][i][r] + bia[i]) + Xa[row * S + c];
+              if (last) {
+                if (kPre) {
+                  a = (a + rg[t][i][r]) + rx[t][i][r];
+                } else {
+                  const uint32_t gq = (uint32_t)min(gr, N - 1);
+                  a = (a + bload(rug, 4u * (gq * (uint32_t)(2 * D) + (uint32_t)(D + c)))) +
+                      bload(rx_, 4u * (gq * (uint32_t)p.ldx + (uint32_t)c));
+                }
+              }
+              Xa[row * S + c] = a;
+              if (gr < N) {
+                if (last)
+                  p.out[(uint32_t)gr * (uint32_t)p.ldo + (uint32_t)c] = a;
+                else
+                  Ak[(uint32_t)gr * (uint32_t)D + (uint32_t)c] = a;
+              }
+            }
+          }
+      }
+      lds_sync();  // hand the tile to the next GEMM
+    }
+  }
+}
+
+template <int RT, int NF, int P>
+__global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int R = 16 * RT;
+  constexpr bool kPre = NF == 1 || RT <= 2;  // as in k_mlps_fwd
+  const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
+  float* DA = lds;          // gradient w.r.t. the current block output [R][S]
+  float* DV = lds + R * S;  // dV_k                                     [R][S]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = 4 * (lane >> 4);
+  const int64_t N = p.N, nchunk = cdiv(N, R);
+  const int nph = 2 * nm;
+  int fr[NF];
+  bool fok[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    fok[i] = wave + i * nw < CF && 16 * (wave + i * nw) + lr < D;
+    fr[i] = min(wave + i * nw, CF - 1);
+  }
+  const float scale = drop_scale(p.drop_p);
+  for (int e = threadIdx.x; e < R * S; e += blockDim.x) DV[e] = 0.f;
+  for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+    const int64_t r0c = ch * R;
+    __syncthreads();
+    load_rows(DA, S, p.dy, p.lddy, r0c, R, D, 16 * G, N);
+    __syncthreads();
+    for (int e = threadIdx.x; e < R * D; e += blockDim.x) {  // dg = dY (from the LDS copy)
+      const int r = e / D, c = e - r * D;
+      if (r0c + r < N) p.dug[(r0c + r) * 2 * p.D + p.D + c] = DA[r * S + c];
+    }
+    BStream<NF> bs;
+    bs.init(img, fr, nph * G);
+    floatx4 ring[P][NF];
+#pragma unroll
+    for (int q = 0; q < P; ++q) bs.next(ring[q]);
+    floatx4 acc[RT][NF];
+    for (int ph = 0; ph < nph; ++ph) {
+      int64_t r0 = r0c;  // opaque per GEMM (see k_mlps_fwd)
+      asm volatile("" : "+s"(r0));
+      const int k = nm - 1 - (ph >> 1);
+      const bool dv = (ph & 1) == 0;
+      // epilogue operands, in flight during the GEMM (raw: any arithmetic here would wait for the
+      // loads at once): dV: v and the dropout mask; dA of block 0: u
+      float ev[RT][NF][4];
+      uint32_t em[RT][NF][4];
+      if (kPre && (dv || k == 0)) {
+        const gfloat* V = (const gfloat*)(dv ? pick8(p.V, k) : p.u);
+        const gu8* M = (const gu8*)pick8(p.M, k);
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int i = 0; i < NF; ++i) {
+            const uint32_t c = (uint32_t)min(16 * fr[i] + lr, D - 1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t o = (uint32_t)min(r0 + 16 * t + lq + r, N - 1) * (uint32_t)D + c;
+              ev[t][i][r] = V[o];
+              em[t][i][r] = (dv && p.drop) ? (uint32_t)M[o] : 1u;
+            }
+          }
+      }
+      mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G);
+      int lo = lane;  // opaque copies: see k_mlps_fwd
+      asm volatile("" : "+s"(r0), "+v"(lo));
+      const int lr = lo & 15, lq = 4 * (lo >> 4);
+      if (dv) {  // dV = (dA W2) * mask/(1-p) * act'(v)
+        gfloat* dVk = (gfloat*)pick8(p.dV, k);
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int i = 0; i < NF; ++i) {
+            if (!fok[i]) continue;
+            const int c = 16 * fr[i] + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * t + lq + r;
+              const int64_t gr = r0 + row;
+              float v = ev[t][i][r];
+              uint32_t mk = em[t][i][r];
+              if (!kPre) {
+                const uint32_t o = (uint32_t)min(gr, N - 1) * (uint32_t)D + (uint32_t)c;
+                v = ((const gfloat*)pick8(p.V, k))[o];
+                mk = p.drop ? (uint32_t)((const gu8*)pick8(p.M, k))[o] : 1u;
+              }
+              const float m = p.drop ? (mk ? scale : 0.f) : 1.f;
+              const float d = (gr < N) ? acc[t][i][r] * m * act_grad(p.act, v) : 0.f;
+              DV[row * S + c] = d;
+              if (gr < N) dVk[(uint32_t)gr * (uint32_t)D + (uint32_t)c] = d;
+            }
+          }
+      } else {  // dA_k = dA_{k+1} + dV W1 ; k == 0: du = dA_0 act'(u) -> dUG[:, :D]
+        gfloat* dAk = (gfloat*)pick8(p.dA, max(k - 1, 0));
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int i = 0; i < NF; ++i) {
+            if (!fok[i]) continue;
+            const int c = 16 * fr[i] + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * t + lq + r;
+              const int64_t gr = r0 + row;
+              const float da = DA[row * S + c] + acc[t][i][r];
+              DA[row * S + c] = da;
+              if (gr < N) {
+                if (k > 0)
+                  dAk[(uint32_t)gr * (uint32_t)D + (uint32_t)c] = da;
+                else
+                  p.dug[(uint32_t)gr * (uint32_t)(2 * D) + (uint32_t)c] =
+                      da * act_grad(p.act, kPre ? ev[t][i][r] : p.u[(uint32_t)gr * (uint32_t)D + (uint32_t)c]);
+              }
+            }
+          }
+      }
+      lds_sync();
+    }
+  }
+}
+
 size_t mlpw_lds_bytes(int64_t D, int64_t nm, int rt) {
   const int Kp = pad16((int)D), S = wstride((int)D);
   return sizeof(float) * (size_t)((2 * nm * Kp + 2 * 16 * rt) * S + 2 * nm * Kp);  // + the bias table
@@ -868,45 +1006,136 @@ bool mlpw_lds_ok(int64_t D, int64_t nm) {
   return D >= 1 && D <= 128 && nm >= 1 && nm <= 8 && mlpw_lds_bytes(D, nm, 1) <= (size_t)kMlpwDynLds;
 }
 
-size_t mlp_lds_bytes(int64_t D) {
-  const int nw = std::min<int>(kMaxWaves, (int)((D + 15) / 16));
-  return sizeof(float) * (size_t)(nw * kWS + 2 * kRows * lds_stride((int)D));
+// ---- weight-streamed geometry and launches ----
+struct MlpsPlan {
+  bool ok;
+  int RT, NF, P;
+  SGeom geo;
+  unsigned blocks;
+  size_t lds;
+};
+
+MlpsPlan mlps_plan(int64_t N, int64_t D) {
+  MlpsPlan pl{};
+  const int CF = (int)cdiv(D, 16);
+  if (D < 1 || CF > 24) return pl;  // beyond 2 fragments per wave: the per-GEMM path
+  pl.NF = CF <= 12 ? 1 : 2;
+  pl.geo.CF = CF;
+  // ring depth P in {5, 4}: the k groups per GEMM rounded up to a multiple of it (fewer zero groups
+  // first, then the deeper ring)
+  const int g5 = (int)cdiv(CF, 5) * 5, g4 = (int)cdiv(CF, 4) * 4;
+  pl.P = g5 <= g4 ? 5 : 4;
+  pl.geo.G = std::min(g5, g4);
+  pl.geo.S = 16 * pl.geo.G + 4;
+  pl.geo.nw = (int)cdiv(CF, pl.NF);
+  const int rt_max = pl.NF == 1 ? 7 : 3;
+  // enough rows per chunk that the chunks fit one round of one workgroup per CU
+  int rt = (int)std::min<int64_t>(rt_max, std::max<int64_t>(1, cdiv(cdiv(std::max<int64_t>(N, 1), g_num_cus()), 16)));
+  if (const char* e = getenv("AIMX_MLPS_RT")) rt = std::max(1, std::min(rt_max, atoi(e)));  // A/B experiments only
+  // two activation tiles + the forward's bias table (2 nm x 16 CF floats, nm <= 8)
+  auto lds = [&](int r) { return sizeof(float) * (size_t)(2 * 16 * r * pl.geo.S + 2 * 8 * 16 * CF); };
+  while (rt > 1 && lds(rt) > (size_t)kMlpsDynLds) --rt;
+  if (lds(rt) > (size_t)kMlpsDynLds) return pl;
+  pl.RT = rt;
+  pl.lds = lds(rt);
+  pl.blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(N, 16 * rt), g_num_cus()));
+  pl.ok = true;
+  return pl;
 }
 
-int mlp_threads(int64_t D) { return 64 * std::min<int>(kMaxWaves, (int)((D + 15) / 16)); }
-
-bool mlp_lds_ok(int64_t D) {
+template <int RT, int NF, int P>
+int mlps_launch(const MlpsPlan& pl, const MlpFwd* pf, const MlpBwd* pb, const float* img, hipStream_t st) {
   static const bool set = [] {
-    (void)hipFuncSetAttribute((const void*)k_mlp_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_mlp_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_mlps_fwd<RT, NF, P>, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpsDynLds);
+    (void)hipFuncSetAttribute((const void*)k_mlps_bwd<RT, NF, P>, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpsDynLds);
     return true;
   }();
   (void)set;
-  return mlp_lds_bytes(D) <= 160 * 1024;
+  const dim3 grid(pl.blocks), block(64 * pl.geo.nw);
+  if (pf)
+    hipLaunchKernelGGL((k_mlps_fwd<RT, NF, P>), grid, block, pl.lds, st, *pf, reinterpret_cast<const floatx4*>(img),
+                       pl.geo);
+  else
+    hipLaunchKernelGGL((k_mlps_bwd<RT, NF, P>), grid, block, pl.lds, st, *pb, reinterpret_cast<const floatx4*>(img),
+                       pl.geo);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
+int mlps_dispatch(const MlpsPlan& pl, const MlpFwd* pf, const MlpBwd* pb, const float* img, hipStream_t st) {
+#define AIMX_MLPS_CASE(rt, nf)                                                          \
+  if (pl.RT == rt && pl.NF == nf)                                                       \
+    return pl.P == 5 ? mlps_launch<rt, nf, 5>(pl, pf, pb, img, st) : mlps_launch<rt, nf, 4>(pl, pf, pb, img, st);
+  AIMX_MLPS_CASE(1, 1) AIMX_MLPS_CASE(2, 1) AIMX_MLPS_CASE(3, 1) AIMX_MLPS_CASE(4, 1) AIMX_MLPS_CASE(5, 1)
+  AIMX_MLPS_CASE(6, 1) AIMX_MLPS_CASE(7, 1) AIMX_MLPS_CASE(1, 2) AIMX_MLPS_CASE(2, 2) AIMX_MLPS_CASE(3, 2)
+#undef AIMX_MLPS_CASE
+  return AIMX_EARG;
+}
+
+// floats of one packed weight image: CF fragments x G k groups x 256
+int64_t mlps_image_floats(int64_t D) {
+  const MlpsPlan pl = mlps_plan(1, D);
+  return (int64_t)pl.geo.CF * pl.geo.G * 256;
 }
 
 }  // namespace
 
-// Opt-in (AIMX_FUSED_MLP=1). Measured at c2 (N = 9.2k atoms, D = 76, MI355X) the fused chain is
-// slower than the per-GEMM path it replaces: train step 1148-1182 vs 1110 us (32- and 16-row
-// workgroups). Each workgroup walks 2 * nm dependent GEMM phases with only ~1-2 workgroups per CU
-// to overlap them, while the per-GEMM kernels spread each phase over ~440 workgroups.
-// The weight-resident kernels (default for D <= 128 whose weights fit LDS; AIMX_MLPW=0 turns them
-// off) or the per-row-tile ones (AIMX_FUSED_MLP=1).
-// (read per call, ~6 calls per train step: tests switch the paths inside one process)
+// The weight-resident kernels: default for D <= 128 whose weights fit the LDS (AIMX_MLPW=0 turns
+// them off). Read per call (~6 calls per train step): tests switch the paths inside one process.
 bool mlpw_on(int64_t D, int64_t nm) {
   const char* e = getenv("AIMX_MLPW");
   return (!e || atoi(e) != 0) && mlpw_lds_ok(D, nm);
 }
 
-bool mlp_fused_ok(int64_t D, int64_t nm) {
-  if (mlpw_on(D, nm)) return true;
-  const char* e = getenv("AIMX_FUSED_MLP");
-  return e && atoi(e) == 1 && D >= 4 && D % 4 == 0 && nm >= 1 && nm <= 8 && mlp_lds_ok(D);
+// The weight-streamed kernels: everything the weight-resident ones do not take, in fp32 (AMP keeps
+// the per-GEMM path's bf16 operands), up to D = 384 and 8 blocks. AIMX_MLPS=0 turns them off (the
+// per-GEMM path), AIMX_MLPS=1 makes them take small D too (tests).
+bool mlps_on(int64_t N, int64_t D, int64_t nm, int32_t precision) {
+  const char* e = getenv("AIMX_MLPS");
+  const int mode = e ? atoi(e) : -1;
+  if (mode == 0 || precision == AIMX_PREC_BF16 || nm < 1 || nm > 8) return false;
+  if (mode != 1 && mlpw_on(D, nm)) return false;
+  return mlps_plan(N, D).ok;
+}
+
+bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision) {
+  if (getenv("AIMX_MLPS") && atoi(getenv("AIMX_MLPS")) == 1) return mlps_on(N, D, nm, precision);
+  return mlpw_on(D, nm) || mlps_on(N, D, nm, precision);
+}
+
+size_t mlp_pack_floats(const AimxShellStack* s) {
+  if (!mlps_on(s->N, s->D, s->num_mlp, s->precision)) return 0;
+  return (size_t)(s->num_layers * 2 * s->num_mlp * mlps_image_floats(s->D));
+}
+
+// Every layer's MLP weights as MFMA-fragment images (k_mlps_pack), in the order the chain reads
+// them: forward W1_0, W2_0, W1_1, ... per layer; backward (transposed) W2_{nm-1}, W1_{nm-1}, ..., W1_0.
+int launch_mlp_pack(const AimxShellStack* s, bool bwd, float* dst, hipStream_t st) {
+  const int64_t nm = s->num_mlp, L = s->num_layers, D = s->D;
+  const MlpsPlan pl = mlps_plan(1, D);
+  const int64_t per = 2 * nm * mlps_image_floats(D) / 4;  // float4s per layer block
+  for (int64_t l = 0; l < L; ++l) {
+    MlpPack p{};
+    p.nmat = (int32_t)(2 * nm);
+    for (int64_t j = 0; j < 2 * nm; ++j) {
+      const int64_t k = bwd ? nm - 1 - (j >> 1) : (j >> 1);
+      const bool w2 = bwd ? (j & 1) == 0 : (j & 1) == 1;
+      p.w[j] = w2 ? s->w2[l * nm + k] : s->w1[l * nm + k];
+    }
+    p.D = (int32_t)D;
+    p.CF = pl.geo.CF;
+    p.G = pl.geo.G;
+    p.tr = bwd ? 1 : 0;
+    p.dst = reinterpret_cast<floatx4*>(dst) + l * per;
+    const int64_t blocks = std::min<int64_t>(cdiv(per, 256), 2048);
+    hipLaunchKernelGGL(k_mlps_pack, dim3((unsigned)blocks), dim3(256), 0, st, p);
+    AIMX_CHECK_LAUNCH();
+  }
+  return AIMX_OK;
 }
 
 int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64_t ldx, float* out, int64_t ldo,
-                   hipStream_t st) {
+                   const float* pack, hipStream_t st) {
   MlpFwd p{};
   const int64_t nm = s->num_mlp;
   p.N = s->N;
@@ -939,7 +1168,7 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
     for (int64_t k = 0; k < nm; ++k) v4 = v4 && al(p.w1[k]) && al(p.w2[k]);
     p.v4 = (v4 && !getenv("AIMX_MLPW_FILL1")) ? 1 : 0;  // AIMX_MLPW_FILL1: dword fill (A/B)
   }
-  if (mlpw_on(s->D, nm)) {
+  if (!pack && mlpw_on(s->D, nm)) {
     const int rt = mlpw_rt(s->N, s->D, nm);
     const int items = rt * (pad16((int)s->D) / 16);
     const int64_t chunks = cdiv(s->N, 16 * rt);
@@ -949,14 +1178,12 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   }
-  const unsigned blocks = (unsigned)cdiv(s->N, kRows);
-  hipLaunchKernelGGL(k_mlp_fwd, dim3(blocks), dim3(mlp_threads(s->D)), mlp_lds_bytes(s->D), st, p);
-  AIMX_CHECK_LAUNCH();
-  return AIMX_OK;
+  if (!pack) return AIMX_EARG;
+  return mlps_dispatch(mlps_plan(s->N, s->D), &p, nullptr, pack + l * 2 * nm * mlps_image_floats(s->D), st);
 }
 
 int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t lddy, float* const* dV,
-                   float* const* dA, float* dug, hipStream_t st) {
+                   float* const* dA, float* dug, const float* pack, hipStream_t st) {
   MlpBwd p{};
   const int64_t nm = s->num_mlp;
   p.N = s->N;
@@ -984,7 +1211,7 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
     for (int64_t k = 0; k < nm; ++k) v4 = v4 && al(p.w1[k]) && al(p.w2[k]);
     p.v4 = (v4 && !getenv("AIMX_MLPW_FILL1")) ? 1 : 0;
   }
-  if (mlpw_on(s->D, nm)) {
+  if (!pack && mlpw_on(s->D, nm)) {
     const int rt = mlpw_rt(s->N, s->D, nm);
     const int items = rt * (pad16((int)s->D) / 16);
     const int64_t chunks = cdiv(s->N, 16 * rt);
@@ -994,10 +1221,8 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   }
-  const unsigned blocks = (unsigned)cdiv(s->N, kRows);
-  hipLaunchKernelGGL(k_mlp_bwd, dim3(blocks), dim3(mlp_threads(s->D)), mlp_lds_bytes(s->D), st, p);
-  AIMX_CHECK_LAUNCH();
-  return AIMX_OK;
+  if (!pack) return AIMX_EARG;
+  return mlps_dispatch(mlps_plan(s->N, s->D), nullptr, &p, pack + l * 2 * nm * mlps_image_floats(s->D), st);
 }
 
 }  // namespace aimx

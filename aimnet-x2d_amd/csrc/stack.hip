@@ -162,8 +162,10 @@ bool valid(const AimxShellStack* s) {
 
 using namespace aimx;
 
-extern "C" size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s) {
-  if (!valid(s)) return 0;
+namespace aimx {
+namespace {
+// floats of the forward workspace's split-K region; the MLP weight images (mlp.hip) follow it
+size_t fwd_split_floats(const AimxShellStack* s) {
   const int64_t N = s->N, D = s->D, K = D * (s->num_hops + 1);
   size_t need = 0;
   // The largest split-K products: weight gradients with K = N rows.
@@ -175,7 +177,14 @@ extern "C" size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s) {
   need = std::max(need, gemm_workspace_floats(a));
   a = linear_dx(N, K, 2 * D, nullptr, 2 * D, nullptr, nullptr, K);
   need = std::max(need, gemm_workspace_floats(a));
-  return sizeof(float) * need + 256;
+  return (need + 63) / 64 * 64;
+}
+}  // namespace
+}  // namespace aimx
+
+extern "C" size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s) {
+  if (!valid(s)) return 0;
+  return sizeof(float) * (fwd_split_floats(s) + mlp_pack_floats(s)) + 256;
 }
 
 extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t stream_) {
@@ -184,7 +193,15 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
   if (N == 0) return AIMX_OK;
-  const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters, s->precision};
+  const size_t split = fwd_split_floats(s), npack = mlp_pack_floats(s);
+  float* pack = nullptr;
+  if (npack) {  // the MLP weights as MFMA-fragment images, once for all layers (weight-streamed MLP)
+    if (!s->workspace || s->workspace_bytes < sizeof(float) * (split + npack)) return AIMX_EARG;
+    pack = s->workspace + split;
+    RUN(launch_mlp_pack(s, false, pack, st));
+  }
+  const Ws ws{s->workspace, npack ? sizeof(float) * split : s->workspace_bytes, s->counters, s->n_counters,
+              s->precision};
   const bool drop = s->training && s->drop_p > 0.f;
   for (int64_t l = 0; l < L; ++l) {
     float* F = s->F[l];
@@ -210,7 +227,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
       RUN(run(a, ws, st));
     }
     // 4) MLP blocks: one fused launch for all of them (mlp.hip), or one GEMM per linear
-    if (mlp_fused_ok(D, nm)) {
+    if (mlp_fused_ok(N, D, nm, s->precision)) {
       float* dst;
       int64_t ldd;
       if (l == L - 1) {
@@ -223,7 +240,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
         dst = s->F[l + 1];
         ldd = K;
       }
-      RUN(launch_mlp_fwd(s, l, s->mode_single ? nullptr : F, K, dst, ldd, st));
+      RUN(launch_mlp_fwd(s, l, s->mode_single ? nullptr : F, K, dst, ldd, pack, st));
       continue;
     }
     for (int64_t k = 0; k < nm; ++k) {
@@ -288,7 +305,8 @@ namespace {
 // Backward scratch layout (floats, 64-aligned regions); every gradient a weight gradient needs
 // stays live until the grouped launch at the end.
 struct BwdLayout {
-  int64_t dF, dUG, dV, dA, dY, T0, wg, total;  // offsets (floats); wg: grouped-wgrad workspace
+  int64_t dF, dUG, dV, dA, dY, T0, pk, wg, total;  // offsets (floats); pk: MLP weight images (0 floats
+                                                    // unless weight-streamed); wg: grouped-wgrad workspace
   int64_t nA, nY;
 };
 
@@ -345,6 +363,7 @@ BwdLayout bwd_layout(const AimxShellStack* s) {
   b.dA = o, o += al64(std::max<int64_t>(b.nA, 1) * N * D);
   b.dY = o, o += al64(std::max<int64_t>(b.nY, 1) * N * D);
   b.T0 = o, o += al64(N * D);
+  b.pk = o, o += al64((int64_t)mlp_pack_floats(s));
   b.wg = o;
   // problem shapes only (null pointers, non-null col_out flags) for the grouped workspace size
   std::vector<AimxWgradProblem> pr(L * (2 * nm + 1));
@@ -389,6 +408,11 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   float* wg_ws = base + lay.wg;
   const size_t wg_bytes = sizeof(float) * (size_t)(lay.total - lay.wg);
   const bool drop = s->training && s->drop_p > 0.f;
+  float* pack = nullptr;
+  if (mlp_pack_floats(s)) {  // transposed MLP weight images for the weight-streamed chain
+    pack = base + lay.pk;
+    RUN(launch_mlp_pack(s, true, pack, st));
+  }
   for (int64_t l = L - 1; l >= 0; --l) {
     // dUG = [du | dg] with dg = dY: below the top layer the hop backward of layer l + 1 already
     // wrote dY into dUG's upper half (ld 2D), so only the top layer copies its upstream gradient
@@ -396,7 +420,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     const float* dY = (l == L - 1) ? g->d_out : dUG + D;
     const int64_t ldy = (l == L - 1) ? g->d_out_ld : D2;
     // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
-    const bool fused = mlp_fused_ok(D, nm);
+    const bool fused = mlp_fused_ok(N, D, nm, s->precision);
     if (fused) {  // the whole chain + dUG = [du | dY] in one launch (mlp.hip)
       float* dVs[8];
       float* dAs[8];
@@ -404,7 +428,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
         dVs[k] = base + lay.dV + (l * nm + k) * N * D;
         dAs[k] = (k < nm - 1) ? base + lay.dA + (l * (nm - 1) + k) * N * D : nullptr;
       }
-      RUN(launch_mlp_bwd(s, l, dY, ldy, dVs, dAs, dUG, st));
+      RUN(launch_mlp_bwd(s, l, dY, ldy, dVs, dAs, dUG, pack, st));
     }
     for (int64_t k = nm - 1; k >= 0 && !fused; --k) {
       const int64_t idx = l * nm + k;
@@ -446,9 +470,10 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       RUN(aimx_wgrad_grouped(pr.data() + (L - 1 - l) * per_layer, per_layer, wg_ws, wg_bytes, aux_cnt, aux_ncnt,
                              (aimx_stream_t)ast));
     }
-    {  // dF = dUG [Wi ; Wg]; the columns of empty chunks are zero (never read by the hop backward)
+    {  // dF = dUG [Wi ; Wg]; tiles wholly in the trailing empty chunks are not computed nor stored:
+       // the hop backward gathers only from chunks that hold targets (zc_dim 2)
       AimxGemmArgs a = linear_dx(N, K, D2, dUG, D2, s->w_ig[l], dF, K);
-      set_zc(a, s, 1);
+      set_zc(a, s, 2);
       RUN(run(a, ws, st));
     }
     // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]

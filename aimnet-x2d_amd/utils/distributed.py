@@ -141,15 +141,17 @@ def replica_checksums(params, device=None):
 
 
 def broadcast_parameters(tensors, src_rank: int = 0, process_group=None) -> None:
-    """Every rank's copies of `tensors` (parameters, buffers) become rank src_rank's, in place:
-    the start state data-parallel replicas need, which DistributedDataParallel's constructor sets
-    the same way (module states broadcast from rank 0; reference runner.py:703-707). A no-op
-    without an initialised process group of more than one rank."""
+    """Every rank's copies of `tensors` (parameters, buffers) become those of rank src_rank OF
+    `process_group` (its group rank; for the default group the global rank), in place: the start
+    state data-parallel replicas need, which DistributedDataParallel's constructor sets the same way
+    (module states broadcast from the group's rank 0; reference runner.py:703-707). A no-op without
+    an initialised process group of more than one rank."""
     if not _ready() or dist.get_world_size(process_group) < 2:
         return
+    src = dist.get_global_rank(process_group, src_rank) if process_group is not None else src_rank
     with torch.no_grad():
         for t in tensors:
-            dist.broadcast(t.data, src=src_rank, group=process_group)
+            dist.broadcast(t.data, src=src, group=process_group)
 
 
 class GradientSync:

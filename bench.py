@@ -4,7 +4,9 @@ metric: molecules/sec of a full training step (forward + backward + grad-norm cl
 dropout on, L1 loss) on QM9-shaped batches, plus the achieved HBM GB/s of the scatter-add hop.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
-  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+  N > 1: `python bench.py --gpus N` starts its own N rank processes (launch_ranks, one GPU each);
+         under torchrun (`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`)
+         it uses the launcher's ranks. --gpus must equal WORLD_SIZE, or the command fails.
 
 Workload (default c2 = BASELINE configs[1]): QM9, hidden 256, 3 hops, 512 molecules per GPU per
 step, single task, attention pooling. Data: synthetic QM9-shaped batches resampled from the
@@ -113,8 +115,9 @@ def native_feeder(cfg, seed, device, threads, pad):
     def index_stream():
         while True:
             yield rng.integers(0, len(store), B)
+    # ring: GraphedTrainStep copies every batch into its static inputs before asking for the next
     return iter(feed.BatchFeeder(store, index_stream(), cfg["hops"], device, depth=4, threads=threads,
-                                 n_max=n_max, e_max=e_max, pad_mols=pm))
+                                 n_max=n_max, e_max=e_max, pad_mols=pm, ring=pad))
 
 
 def pad_mols_for(n_max, n_min):
@@ -171,7 +174,7 @@ def stream_feeder(cfg, rank, world, device, threads, pad, n_mols, path=None, rea
             yield from stream.batches(B, chunk_size=16384, epoch_seed=epoch)
             epoch += 1
     return iter(feed.BatchFeeder(None, batches(), cfg["hops"], device, depth=4, threads=threads,
-                                 n_max=n_max, e_max=e_max, pad_mols=pm))
+                                 n_max=n_max, e_max=e_max, pad_mols=pm, ring=pad))
 
 
 def build_model(cfg, device):
@@ -274,37 +277,71 @@ def _bw(name, bytes_, us, **kw):
             "achieved": round(gbs, 1), "unit": "GB/s", "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), **kw}
 
 
+def cold_time_us(fn, device, launches=20, flush_mb=512):
+    """Device time per launch of fn() with a cold MALL / L2: each launch is bracketed by HIP
+    events on the current stream right behind a `flush_mb` zero fill (larger than the 256 MiB
+    Infinity Cache), which also keeps the GPU busy while the host enqueues the bracketed launch,
+    so the events see no launch gap. The mean over `launches`."""
+    flush = torch.empty(flush_mb * 2 ** 20 // 4, device=device)
+    stream = torch.cuda.current_stream(device)
+    for _ in range(3):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    for e0, e1 in ev:
+        flush.zero_()
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    us = sum(e0.elapsed_time(e1) for e0, e1 in ev) / launches * 1e3
+    del flush
+    return us
+
+
 def hop_in_step(batch, hops, hidden, device):
-    """The hop forward and backward at the config's own batch size (what one train step runs per
-    layer), timed by graph_time_us through the C ABI. Backward bytes: the gathered gradient rows
-    (every target row is < N for reference inputs, layers.py:154, so chunk 0 only), the src-keyed
-    CSR and the written dx — the minimal traffic, not SURVEY §8d's all-chunks upper bound."""
+    """The hop forward and backward exactly as one train step's stack runs them per layer
+    (stack.hip), at the config's own batch, through the C ABI, cold MALL (cold_time_us):
+      forward : src F[:, :D] (row stride K = D (h+1)), output written into F's columns
+                [D, K) (hop chunk j at column offset D + j D);
+      backward: the gathered rows dF[:, D:] at the targets (every target is < N for reference
+                inputs, layers.py:154, so chunk 0 only), plus the chunk-0 gradient dF[:, :D] and
+                the outer residual dY (row stride 2 D) added, written into the next-lower layer's
+                dUG slot (row stride 2 D).
+    Algorithmic bytes: fwd 4 [N D + E + (h N + 1) + h N D] (every chunk written);
+    bwd 4 [N D (gathered rows) + E + (N + 1) + 2 N D (the residual reads) + N D (written)]."""
     from aimx import _lib
     from aimx.plan import GraphPlan
     lib = _lib.load()
     P = _lib.ptr
     n, d = batch.num_atoms, int(0.3 * hidden)
+    K = d * (hops + 1)
     plan = GraphPlan(n, hops, edges=batch.edges, batch=batch.batch, num_graphs=batch.num_graphs)
     e = plan.E
-    x = torch.randn(n, d, device=device)
-    out = torch.empty(hops * n, d, device=device)
-    g = torch.randn(hops * n, d, device=device)
-    dx = torch.empty(n, d, device=device)
+    F = torch.randn(n, K, device=device)
+    dF = torch.randn(n, K, device=device)
+    dUG = torch.randn(n, 2 * d, device=device)   # dY in the upper half (row stride 2 D)
+    nxt = torch.empty(n, 2 * d, device=device)  # the next-lower layer's dUG slot
     seg, seg_st = plan.row_seg()
-    torch.cuda.synchronize()
+    s = _lib.stream_ptr(device)
+    fl = 4  # bytes per float: column offsets as pointer arithmetic
+    kern = "k_gather_sum" if d % 4 == 0 else "k_gather_rows"
 
     def fwd():
-        assert lib.aimx_segment_gather_sum(P(x), d, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n, P(out), d,
-                                           n, n * d, None, 0, None, 0, seg, seg_st, _lib.stream_ptr(device)) == 0
+        assert lib.aimx_segment_gather_sum(P(F), K, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n,
+                                           P(F) + fl * d, K, n, d, None, 0, None, 0, seg, seg_st, s) == 0
 
     def bwd():
-        assert lib.aimx_segment_gather_sum(P(g), d, 0, 0, d, P(plan.bwd.rowptr), P(plan.bwd.col), n, P(dx), d, 0, 0,
-                                           None, 0, None, 0, seg, seg_st, _lib.stream_ptr(device)) == 0
-    tf, tb = graph_time_us(fwd), graph_time_us(bwd)
+        assert lib.aimx_segment_gather_sum(P(dF) + fl * d, K, n, d, d, P(plan.bwd.rowptr), P(plan.bwd.col), n,
+                                           P(nxt) + fl * d, 2 * d, 0, 0, P(dF), K, P(dUG) + fl * d, 2 * d,
+                                           seg, seg_st, s) == 0
+    torch.cuda.synchronize()
+    tf, tb = cold_time_us(fwd, device), cold_time_us(bwd, device)
     bf = 4 * (n * d + e + (hops * n + 1) + hops * n * d)
-    bb = 4 * (n * d + e + (n + 1) + n * d)
+    bb = 4 * (n * d + e + (n + 1) + 2 * n * d + n * d)
+    note = "the stack's own layout (F column offset D, residual adds), cold MALL (512 MiB flush per launch)"
     return {"atoms": n, "edges": e, "D": d, "hops": hops,
-            "fwd": _bw("k_gather_sum (hop fwd)", bf, tf), "bwd": _bw("k_gather_sum (hop bwd)", bb, tb)}
+            "fwd": _bw(kern + " (hop fwd, in-step layout)", bf, tf, timing=note),
+            "bwd": _bw(kern + " (hop bwd + residual adds, in-step layout)", bb, tb, timing=note)}
 
 
 def hop_bwd_roofline(plan, n, d, hops, device, launches=20):
@@ -330,6 +367,7 @@ def hop_bwd_roofline(plan, n, d, hops, device, launches=20):
     t1.record(stream)
     t1.synchronize()
     us = t0.elapsed_time(t1) / launches * 1e3
+    # bytes: the gathered rows (chunk 0 only for reference inputs) + col + rowptr + dx written
     return _bw(("k_gather_sum" if d % 4 == 0 else "k_gather_rows") + " (hop bwd)",
                4 * (n * d + plan.E + (n + 1) + n * d), us)
 
@@ -530,6 +568,72 @@ def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False
             "eager, every operator launched from Python (AIMX_AUTOGRAPH=0), unpadded batches, same step"}
 
 
+def rank_env(base, rank, world, port, addr="127.0.0.1"):
+    """The environment of rank `rank` of a `world`-rank single-node job: what torchrun exports and
+    the reference reads (main/utils.py:41-52: LOCAL_RANK and WORLD_SIZE select DDP and the device),
+    plus RANK / LOCAL_WORLD_SIZE / MASTER_* for the process-group rendezvous (env://). One GPU per
+    rank: rank r runs on cuda:r."""
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "ROLE_RANK": str(rank),
+                "ROLE_WORLD_SIZE": str(world), "MASTER_ADDR": addr, "MASTER_PORT": str(port),
+                "TORCHELASTIC_RUN_ID": "aimx-bench"})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    return env
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv, poll_s=0.2, script=None):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this same script
+    (children, never an exec of this process) and wait for them. This process never touches the
+    GPU. Rank 0's stdout is this command's stdout (the one JSON line); the others' stdout goes to
+    stderr. The first rank to fail stops the rest, and its exit code is returned (a rank that dies
+    would otherwise leave its peers waiting in a collective)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv),
+                                      env=rank_env(os.environ, r, n, port),
+                                      stdout=None if r == 0 else sys.stderr.fileno(), start_new_session=True))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    except KeyboardInterrupt:
+        rc = 130
+    if rc:
+        print(f"bench: a rank exited with {rc}; stopping the other ranks", file=sys.stderr)
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        deadline = time.time() + 30
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return 128 - rc if rc < 0 else rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -565,11 +669,25 @@ def main():
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        print(f"bench: --gpus {args.gpus} must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N`: start the N ranks here, before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a {world}-rank run as "
+              f"{args.gpus} GPUs", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     if ndev and local >= ndev:  # rehearsal only (more ranks than GPUs): ranks share the box's GPUs
+        if args.dist_backend == "nccl":
+            print(f"bench: rank {rank} has LOCAL_RANK {local} but {ndev} visible GPU(s); RCCL needs one GPU "
+                  "per rank (--dist-backend gloo rehearses several ranks on one GPU)", file=sys.stderr)
+            sys.exit(2)
         local = local % ndev
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
@@ -758,8 +876,6 @@ def main():
                            "buckets": len(sync.buckets),
                            "bucket_mb": [round(sum(p.numel() for p in bk) * 4 / 2 ** 20, 3) for bk in sync.buckets],
                            **ddp_check}
-            if args.gpus != world:
-                line["ddp"]["note"] = f"--gpus {args.gpus} but WORLD_SIZE {world}"
         if cpu is not None:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         if head_timeout:

@@ -150,7 +150,10 @@ typedef struct AimxGemmArgs {
    * edge (zc_rowptr[(j+1)*zc_rows] > zc_rowptr[j*zc_rows]; c = 0 if none):
    *   zc_dim 0: operand entries with k >= E are zero, so the k loop stops at E;
    *   zc_dim 1: output columns >= E (ones column excluded) are zero: whole tiles there are
-   *             written as 0 without loads or MFMA work (plain-store epilogue only).
+   *             written as 0 without loads or MFMA work (plain-store epilogue only);
+   *   zc_dim 2: as 1, but whole tiles past E are not written at all (the caller never reads
+   *             those columns: the stack's hop-chunk input gradient, whose empty chunks the hop
+   *             backward never gathers).
    * Results are identical to the untrimmed product (only exact zeros are skipped). */
   const int32_t* zc_rowptr; int64_t zc_rows; int32_t zc_chunks; int64_t zc_width; int32_t zc_dim;
   /* AIMX_PREC_FP32 (0, the parity path): exact fp32 products (v_mfma_f32_16x16x4_f32).

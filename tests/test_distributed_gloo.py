@@ -177,3 +177,21 @@ def test_gradient_sync_broadcasts_start_state():
     for r in (0, 1):
         before, after, trained = out[r]
         assert not before and after and trained
+
+
+def _subgroup_broadcast(rank, world):
+    """broadcast_parameters over a subgroup that does not hold global rank 0: the source is the
+    GROUP's rank 0 (global rank 1), as DDP's constructor does."""
+    from utils.distributed import broadcast_parameters
+    grp = dist.new_group([1, 2])
+    t = torch.full((4,), float(rank))
+    if rank in (1, 2):
+        broadcast_parameters([t], 0, grp)
+    dist.barrier()
+    return t.tolist()
+
+
+def test_broadcast_parameters_subgroup_source():
+    out = _run("_subgroup_broadcast", world=3)
+    assert out[0] == [0.0] * 4
+    assert out[1] == [1.0] * 4 and out[2] == [1.0] * 4

@@ -248,3 +248,39 @@ def test_pad_batch_matches_pad_collated(slack):
     assert np.array_equal(q[:G], b.total_charges.cpu().numpy()) and not q[G:].any()
     a.Np = N  # no slack atom: rejected
     assert _lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(b.edges.device)) != 0
+
+
+def test_autograph_grad_hooks_fire_through_autograd():
+    """Gradient hooks on the parameters (what DDP's reducer relies on): the replay hands its
+    gradients out through autograd (_ReplayGrads), so every used parameter's post-accumulate hook
+    fires once per backward with the replayed gradient, equal to the eager gradients; the unused
+    long_range_projection gets none, as eagerly."""
+    from aimx import autograph
+    b = _batches(1, 13)[0]
+    m1 = _model()
+    m2 = _model()
+    m2.load_state_dict(m1.state_dict())
+    autograph.enable(m2)
+    seen = {}
+    hs = [p.register_post_accumulate_grad_hook(lambda p, n=n: seen.__setitem__(n, seen.get(n, 0) + 1))
+          for n, p in m2.named_parameters()]
+    try:
+        for it in range(2):
+            for m in (m1, m2):
+                m.zero_grad(set_to_none=True)
+            o1, _, _ = m1(*b.model_args())
+            o2, _, _ = m2(*b.model_args())
+            (o1.square().sum() + o1.sum()).backward()
+            (o2.square().sum() + o2.sum()).backward()
+            torch.cuda.synchronize()
+            assert autograph._state(m2).buckets, "the replay did not run"
+            used = {n for n, p in m1.named_parameters() if p.grad is not None}
+            assert set(seen) == used and all(v == it + 1 for v in seen.values()), seen
+            for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+                if p1.grad is None:
+                    assert p2.grad is None, n
+                else:
+                    assert _rel(p2.grad, p1.grad) < 1e-5, n
+    finally:
+        for h in hs:
+            h.remove()

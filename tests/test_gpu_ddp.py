@@ -272,34 +272,53 @@ def test_rccl_capture_failure_falls_back_to_split():
     assert out["identical"] and out["ar_us"] > 0, out
 
 
-def ddp_wrapped(rank, world):
+def _ddp_wrapped(rank, replay):
     """The reference's own data-parallel wrapping, unchanged (runner.py:703-707):
-    DistributedDataParallel(GNN, find_unused_parameters=True) over this GNN — the autograph steps
-    aside under a multi-rank group, DDP's reducer averages the gradients."""
+    DistributedDataParallel(GNN, find_unused_parameters=True) over this GNN, two iterations of the
+    unchanged loop (zero_grad(set_to_none) -> forward -> L1 -> backward). replay: the default
+    drop-in — the autograph replays the bucket's graphs and hands the gradients out through
+    autograd, so DDP's reducer averages them; else every operator eagerly."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     from aimx import autograph
     from models import L1Loss
     b = _qm9_batch(np.arange(rank * B_HALF, (rank + 1) * B_HALF))
     m = _model()
-    assert not autograph.wanted(m, b.model_args())  # multi-rank group: eager path
+    autograph.enable(m, replay)
+    assert autograph.wanted(m, b.model_args()) == replay
     ddp = DDP(m, device_ids=[0], find_unused_parameters=True)
-    out, _, _ = ddp(*b.model_args())
-    L1Loss()(out, b.targets).backward()
+    for _ in range(2):  # the second iteration: DDP found its reduction finished, buckets replayed again
+        for p in m.parameters():
+            p.grad = None
+        out, _, _ = ddp(*b.model_args())
+        L1Loss()(out, b.targets).backward()
     torch.cuda.synchronize()
-    return {"grads": _grads(m)}
+    return {"grads": _grads(m), "buckets": len(autograph._state(m).buckets),
+            "unused_grad_none": m.long_range_projection.weight.grad is None}
 
 
-def test_ddp_wrapped_drop_in_equals_full_batch():
-    """INTEGRATION.md's claim: the reference trainer's DDP wrapping still works on this GNN, and two
-    ranks' averaged gradients equal one process's full-batch gradients (1e-5 norm-relative)."""
+def ddp_wrapped(rank, world):
+    return _ddp_wrapped(rank, True)
+
+
+def ddp_wrapped_eager(rank, world):
+    return _ddp_wrapped(rank, False)
+
+
+@pytest.mark.parametrize("fn", ["ddp_wrapped", "ddp_wrapped_eager"])
+def test_ddp_wrapped_drop_in_equals_full_batch(fn):
+    """INTEGRATION.md's claim: the reference trainer's DDP wrapping still works on this GNN —
+    with the autograph's graph replay (default) and eagerly — and two ranks' averaged gradients
+    equal one process's full-batch gradients (1e-5 norm-relative)."""
     from models import L1Loss
-    out = _run("ddp_wrapped")
+    out = _run(fn)
     m = _model()
     b = _qm9_batch(np.arange(2 * B_HALF))
     o, _, _ = m(*b.model_args())
     L1Loss()(o, b.targets).backward()
     full = _grads(m)
     for r in range(2):
+        assert out[r]["buckets"] == (1 if fn == "ddp_wrapped" else 0), out[r]["buckets"]
+        assert out[r]["unused_grad_none"]
         got = out[r]["grads"]
         assert set(got) == set(full), r
         for k, want in full.items():

@@ -27,8 +27,8 @@ def _fields(b):
         [c.fwd_rowptr, c.fwd_col, c.bwd_rowptr, c.bwd_col, c.graph_rowptr, c.graph_col]
 
 
-@pytest.mark.parametrize("pad", [False, True])
-def test_feeder_batches_bit_exact_and_ordered(pad):
+@pytest.mark.parametrize("pad,ring", [(False, False), (True, False), (True, True)])
+def test_feeder_batches_bit_exact_and_ordered(pad, ring):
     asset = QM9Asset()
     store = feed.HostStore.from_qm9_asset(asset, precompute_hops=3, threads=3)
     rng = np.random.default_rng(11)
@@ -38,7 +38,8 @@ def test_feeder_batches_bit_exact_and_ordered(pad):
         c = feed.HostCollator(3, 1)
         sizes = np.array([c.plan(store, i) for i in idxs])
         n_max, e_max, pm = int(sizes[:, 0].max()) + 5, int(sizes[:, 1].max()) + 9, 8
-    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=3, n_max=n_max, e_max=e_max, pad_mols=pm)
+    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=3, n_max=n_max, e_max=e_max, pad_mols=pm,
+                         ring=ring)
     got = list(f)
     assert len(got) == len(idxs)
     for b, idx in zip(got, idxs):
@@ -101,7 +102,8 @@ def test_feeder_ring_reuse_is_race_free():
     def same(a, b):  # every field's bytes (the 256-byte alignment gaps are never written)
         return all(torch.equal(a[o:o + int(np.prod(sh)) * np.dtype(dt).itemsize],
                                b[o:o + int(np.prod(sh)) * np.dtype(dt).itemsize]) for o, dt, sh in layout)
-    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=pad[0], e_max=pad[1], pad_mols=pad[2])
+    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=pad[0], e_max=pad[1], pad_mols=pad[2],
+                         ring=True)
     x = torch.randn(2048, 2048, device=DEV)
     got = []
     for b in f:
@@ -114,13 +116,14 @@ def test_feeder_ring_reuse_is_race_free():
         assert same(g.cpu(), w)
     assert f.stats()["ring"] <= 6
     kept = list(feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=pad[0], e_max=pad[1],
-                                 pad_mols=pad[2]))
+                                 pad_mols=pad[2], ring=True))
     torch.cuda.synchronize()
     for b, w in zip(kept, want):
         assert same(b._blob.cpu(), w)
 
 
-def test_overflow_batch_goes_out_unpadded():
+@pytest.mark.parametrize("ring", [False, True])
+def test_overflow_batch_goes_out_unpadded(ring):
     """Static shapes from a few sample batches: a later batch above that capacity is handed out
     unpadded (its own layout, bit-exact to the dynamic collate) and counted, the others padded."""
     asset = QM9Asset()
@@ -133,7 +136,8 @@ def test_overflow_batch_goes_out_unpadded():
     rest = [k for k in range(len(idxs)) if k != big]
     n_max, e_max = int(sizes[rest, 0].max()) + 3, int(sizes[rest, 1].max())
     assert sizes[big, 1] > e_max
-    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=n_max, e_max=e_max, pad_mols=6)
+    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=n_max, e_max=e_max, pad_mols=6,
+                         ring=ring)
     got = [b for b in f]
     torch.cuda.synchronize()
     assert f.stats()["overflow"] == 1
@@ -149,3 +153,29 @@ def test_overflow_batch_goes_out_unpadded():
         for x, y in zip(_fields(b), _fields(ref)):
             assert torch.equal(x, y)
         assert b.real_graphs == len(idx)
+
+
+def test_kept_views_stay_valid_without_ring():
+    """The default feeder (ring=False) gives every static-shape batch a blob of its own: a consumer
+    that keeps only tensor views (batch.targets for an epoch metric, batch.batch), never the batch
+    object, still reads each batch's own values after the feeder has moved on, with a busy stream."""
+    asset = QM9Asset()
+    store = feed.HostStore.from_qm9_asset(asset, precompute_hops=3, threads=2)
+    rng = np.random.default_rng(9)
+    idxs = [rng.integers(0, len(asset), 64) for _ in range(16)]
+    c = feed.HostCollator(3, 2)
+    sizes = np.array([c.plan(store, i) for i in idxs])
+    pad = (int(sizes[:, 0].max()) + 7, int(sizes[:, 1].max()) + 11, 4)
+    f = feed.BatchFeeder(store, iter(idxs), 3, DEV, depth=2, threads=2, n_max=pad[0], e_max=pad[1], pad_mols=pad[2])
+    x = torch.randn(1024, 1024, device=DEV)
+    targets, mols = [], []
+    for b in f:
+        x = torch.tanh(x @ x)
+        targets.append(b.targets[:b.real_graphs])
+        mols.append(b.batch)
+        del b
+    torch.cuda.synchronize()
+    for t, m, idx in zip(targets, mols, idxs):
+        assert torch.equal(t.cpu(), torch.from_numpy(asset.targets[idx]))
+        assert torch.equal(m[:len(m) - (m >= len(idx)).sum()].cpu(),
+                           torch.from_numpy(adata.collate(asset.molecules(idx), 3)["batch"]))

@@ -4,6 +4,8 @@ Integer work (CSR / edge order) bit-exact; the hop forward bit-exact (same summa
 reference's CPU scatter_add_); floating point per tensor within the north-star tolerance
 (conftest.parity_failures: <= max(1e-5, 3x the reference's own fp32 error vs fp64)).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -600,6 +602,71 @@ def _oracle_run(z, cfg, inputs, dtype):
     return add_sketches(res, z)
 
 
+# config-sized batches (BASELINE configs[3] / [4] per GPU): the c4s / c5s architectures and seeds on
+# 512 / 256 synthetic 40-atom molecules (the bench's synth40 source), every output and gradient
+# compared element-wise with the fp64 oracle (no sketches)
+FULL_SIZE = {"c4": ("c4s", 512), "c5": ("c5s", 256)}
+
+
+def full_size_case(name):
+    """(fixture of the architecture, cfg, CPU inputs, loss weights) of a config-sized case."""
+    from aimx import data as adata
+    from aimx.synth import synth_molecules
+    base, mols = FULL_SIZE[name]
+    z = load_golden(base)
+    cfg = dict(load_case(base)[1])
+    col = adata.collate(synth_molecules(mols, seed=1000 + mols), cfg["num_shells"])
+    from golden_cases import FEATURE_KEYS
+    feats = torch.from_numpy(col["feats"].astype(np.int64))
+    af = {k: feats[:, i].contiguous() for i, k in enumerate(FEATURE_KEYS)}
+    inputs = (af, torch.from_numpy(col["edges"].astype(np.int64)).reshape(-1, 2),
+              torch.from_numpy(col["batch"].astype(np.int64)), torch.zeros(mols))
+    loss_w = np.random.default_rng(mols).standard_normal((mols, cfg["output_dim"])).astype(np.float32)
+    return z, cfg, inputs, loss_w
+
+
+def _run_full(cfg, seed, inputs, loss_w, device, dtype=torch.float32):
+    """(outputs and parameter gradients) of loss = sum(out * loss_w): the GPU model (device 'cuda')
+    or the oracle (device 'cpu', dtype fp32 / fp64)."""
+    af, edges, batch, tc = inputs
+    e0 = torch.empty(0, 2, dtype=torch.long)
+    if device == "cpu":
+        _, om = _oracle()
+        p = {k: v.to(dtype).requires_grad_() for k, v in om.seeded_params(cfg, seed).items()}
+        out, attn, _ = om.gnn_forward(p, cfg, af, edges, batch, tc.to(dtype))
+        (out * torch.from_numpy(loss_w).to(dtype)).sum().backward()
+        res = {"grad." + k: v.grad.numpy() for k, v in p.items() if v.grad is not None}
+    else:
+        model = _build_model(cfg, seed)
+        d = lambda t: t.to(DEV)  # noqa: E731
+        out, attn, _ = model({k: d(v) for k, v in af.items()}, d(edges), d(batch), d(tc),
+                             torch.empty(0, 4, dtype=torch.long, device=DEV), d(e0), d(e0))
+        (out * torch.from_numpy(loss_w).to(DEV)).sum().backward()
+        res = {"grad." + k: p.grad.cpu().numpy() for k, p in model.named_parameters() if p.grad is not None}
+    res["out"] = out.detach().cpu().numpy()
+    res["attn"] = attn.detach().cpu().numpy()
+    return res
+
+
+@pytest.mark.parametrize("name", sorted(FULL_SIZE))
+def test_model_full_size(name):
+    """c4 / c5 at their configured per-GPU batch (512 x 40-atom molecules h512 3 hops; 256 x
+    40-atom h1024 6 hops): outputs, attention and every parameter gradient, element for element,
+    within the parity contract against the fp64 oracle (the floor: the oracle's own fp32 run, the
+    reference's ATen ops pinned by tests/test_oracle_golden.py). Exercises what the 64 / 32-molecule
+    fixtures cannot: the weight-streamed MLP at its 96 / 48-row chunks, full-K (~20 k atom) split-K
+    weight gradients, multi-window hop tiling."""
+    z, cfg, inputs, loss_w = full_size_case(name)
+    torch.set_num_threads(min(16, os.cpu_count() or 8))
+    seed = int(z["seed"])
+    ref64 = _run_full(cfg, seed, inputs, loss_w, "cpu", torch.float64)
+    ref32 = _run_full(cfg, seed, inputs, loss_w, "cpu", torch.float32)
+    ours = _run_full(cfg, seed, inputs, loss_w, "cuda")
+    assert set(ours) == set(ref64), set(ours) ^ set(ref64)
+    bad = parity_failures(ours, ref32, ref64)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_model_case(name):
     z, cfg, inputs = load_case(name)
@@ -978,13 +1045,69 @@ def test_fused_head_clusters_bit_identical(G, monkeypatch):
             assert torch.equal(a, b), (S, i, (a - b).abs().max().item())
 
 
-@pytest.mark.parametrize("name", ["c2", "c3"])
-def test_fused_mlp_opt_in_parity(name, monkeypatch):
-    """AIMX_MLPW=0 AIMX_FUSED_MLP=1 (the per-row-tile fused MLP chain, mlp.hip) keeps the model
-    within the parity contract (outputs and every gradient vs the fp64 oracle)."""
-    monkeypatch.setenv("AIMX_MLPW", "0")
-    monkeypatch.setenv("AIMX_FUSED_MLP", "1")
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "act_gelu", "stereo"])
+def test_streamed_mlp_forced_parity(name, monkeypatch):
+    """AIMX_MLPS=1 (the weight-streamed node-update chain, mlp.hip k_mlps_*, the default for D > 128)
+    forced onto the small-D cases keeps the model within the parity contract."""
+    monkeypatch.setenv("AIMX_MLPS", "1")
     test_model_case(name)
+
+
+@pytest.mark.parametrize("name", ["c4s", "c5s"])
+def test_per_gemm_mlp_path_parity_wide(name, monkeypatch):
+    """AIMX_MLPS=0 (one GEMM per MLP linear) at D = 153 / 307 stays within the parity contract."""
+    monkeypatch.setenv("AIMX_MLPS", "0")
+    test_model_case(name)
+
+
+def _stack_case(hidden, hops, mols, seed=0):
+    from aimx import data as adata
+    from aimx.plan import GraphPlan
+    from aimx.synth import synth_molecules
+    from models.layers import ShellConvolutionLayer
+    torch.manual_seed(seed)
+    col = adata.collate(synth_molecules(mols, seed=seed), hops)
+    edges = torch.from_numpy(col["edges"]).to(DEV)
+    batch = torch.from_numpy(col["batch"]).to(DEV)
+    n, d = batch.shape[0], int(0.3 * hidden)
+    plan = GraphPlan(n, hops, edges=edges, batch=batch, num_graphs=mols)
+    layers = [ShellConvolutionLayer(d, d, num_hops=hops).to(DEV) for _ in range(3)]
+    params = [p for l in layers for p in l._aimx_params()]
+    return plan, params, n, d
+
+
+@pytest.mark.parametrize("hidden,hops,mols,rt", [(512, 3, 512, None), (512, 3, 512, "1"), (1024, 6, 256, None),
+                                                 (1024, 6, 256, "2"), (256, 3, 700, None), (640, 3, 64, None)])
+def test_streamed_mlp_matches_per_gemm(hidden, hops, mols, rt, monkeypatch):
+    """The weight-streamed chain against the per-GEMM path on the same stack, training mode with
+    dropout: outputs and every gradient within 1e-5 norm-relative (both fp32, different summation
+    order) — identical dropout masks are implied (one flipped mask element moves a tensor by far
+    more). Config-sized batches (c4: 512 x 40-atom molecules, D = 153, 96-row chunks; c5: 256
+    molecules, D = 307, two fragments per wave), forced small chunks (rt = 1 / 2: chunks > CUs, so
+    workgroups loop over several), D = 76 forced onto the streamed kernel, and D = 192."""
+    from aimx import ops
+    plan, params, n, d = _stack_case(hidden, hops, mols)
+    x = torch.randn(n, d, device=DEV)
+    seed = torch.tensor([4321], device=DEV)
+    kw = dict(num_hops=hops, num_layers=3, num_mlp=2, act="silu", training=True, drop_p=0.05, drop_seed=seed)
+    w = torch.randn(n, d, device=DEV)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("AIMX_MLPS", mode)
+        if rt is not None and mode == "1":
+            monkeypatch.setenv("AIMX_MLPS_RT", rt)
+        xs = x.clone().requires_grad_()
+        ps = [p.detach().clone().requires_grad_() for p in params]
+        y = ops.message_passing_stack(plan, xs, ps, **kw)
+        (y * w).sum().backward()
+        torch.cuda.synchronize()
+        res[mode] = [y.detach()] + [xs.grad] + [p.grad for p in ps]
+        monkeypatch.delenv("AIMX_MLPS_RT", raising=False)
+    for i, (a, b) in enumerate(zip(res["1"], res["0"])):
+        assert a is not None and b is not None, i
+        assert torch.isfinite(a).all(), i
+        err = norm_rel(a.cpu().numpy(), b.cpu().numpy())
+        assert err < 1e-5, (i, err)
 
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "act_gelu", "stereo"])
