@@ -172,6 +172,9 @@ class H5File:
             _check(self._lib.aimx_h5_read_store(self._h, pos.ctypes.data if pos.size else None, pos.size, n_hops,
                                                 n_tasks, threads, ctypes.byref(out), ctypes.byref(nv),
                                                 kept.ctypes.data), "read_store")
+            info = H5Info()
+            if self._lib.aimx_h5_info(self._h, ctypes.byref(info)) == 0:
+                self.direct_read = bool(info.direct_read)  # off once the file changed since open
         store = afeed.HostStore.from_handle(out, n_feat=len(afeed.adata.FEATURE_KEYS), n_tasks=n_tasks)
         return store, kept[:nv.value].copy()
 

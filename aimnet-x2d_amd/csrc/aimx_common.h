@@ -90,6 +90,13 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Internal launchers shared across translation units.
+// aimx_segment_gather_sum (hop.hip) with skip_tail: chunks in the trailing run of edge-less hop chunks
+// are not written (only for consumers that trim them: the stack's GEMMs via AimxGemmArgs.zc_*)
+int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
+                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
+                       int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
+                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
+                       int32_t skip_tail);
 int launch_gemm(const AimxGemmArgs& a, hipStream_t s);
 size_t gemm_workspace_floats(const AimxGemmArgs& a);
 int launch_charge_fwd(const float* x, int64_t ldx, int64_t N, int64_t D, const int32_t* gptr, const int32_t* gperm,

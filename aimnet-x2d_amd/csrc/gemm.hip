@@ -768,13 +768,17 @@ __device__ __forceinline__ void wgrad_block(const AimxGemmArgs& a, int kchunk, u
   const __amdgpu_buffer_rsrc_t rb_ = make_rsrc(a.B, b_bytes);
   const uint32_t sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk;
   const int lm = lane & 15, lk = lane >> 4;
+  // X columns in the trailing empty hop chunks (zc) read as zero: the stack's hop does not write
+  // them (segment_gather_sum skip_tail), and their exact gradient is zero
+  const int zlim = a.zc_rowptr ? zc_extent(a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width) : N;
   uint32_t va[2], vb[2];
-  bool one[2];
+  bool one[2], zcol[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     va[i] = 4u * ((uint32_t)(m0 + i * 16 + lm) + (uint32_t)lk * sak);
     vb[i] = 4u * ((uint32_t)(n0 + i * 16 + lm) + (uint32_t)lk * sbk);
     one[i] = a.ones_col && (n0 + i * 16 + lm == N - 1);
+    zcol[i] = !one[i] && n0 + i * 16 + lm >= zlim;
   }
   floatx4 acc[2][2];
 #pragma unroll
@@ -795,7 +799,7 @@ __device__ __forceinline__ void wgrad_block(const AimxGemmArgs& a, int kchunk, u
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         fa[u][i] = bload(ra_, kok ? va[i] : a_bytes, sa);
-        const float y = bload(rb_, kok ? vb[i] : b_bytes, sb);
+        const float y = bload(rb_, kok && !zcol[i] ? vb[i] : b_bytes, sb);
         fb[u][i] = one[i] ? 1.f : y;
       }
     }
@@ -1059,8 +1063,9 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
   a.dact_kind = -1;
   a.ones_col = ones;
   a.col_out = pr.col_out;
-  if (pr.zc_rowptr && n0 >= zc_extent(pr.zc_rowptr, pr.zc_rows, pr.zc_chunks, pr.zc_width) &&
-      !(ones && n0 + BB > Nreal)) {  // a block wholly inside the empty hop chunks: zero, no work
+  // X columns in the trailing empty hop chunks read as zero (see wgrad_block)
+  const int zlim = pr.zc_rowptr ? min(Nreal, zc_extent(pr.zc_rowptr, pr.zc_rows, pr.zc_chunks, pr.zc_width)) : Nreal;
+  if (pr.zc_rowptr && n0 >= zlim && !(ones && n0 + BB > Nreal)) {  // a block wholly inside the empty hop chunks: zero, no work
     if (z == 0)
       for (int e = tid; e < G::Slab; e += kWbT) {
         const int m = m0 + e / BB, n = n0 + e % BB;
@@ -1087,7 +1092,7 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
       const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
       const int row = f / (BB / 4), c = 4 * (f % (BB / 4));
       const int k = k0 + row;
-      const int col = (isb ? n0 : m0) + c, lim = isb ? Nreal : M;
+      const int col = (isb ? n0 : m0) + c, lim = isb ? zlim : M;
       const uint32_t ld = isb ? ldb : lda, bytes = isb ? bb : ab;
       const __amdgpu_buffer_rsrc_t r = isb ? rb : ra;
       const bool kok = k < kend;

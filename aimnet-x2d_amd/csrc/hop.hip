@@ -192,6 +192,7 @@ struct HopArgs {
   int64_t seg_stride;
   int32_t flat_zero;    // rows past split are one contiguous [rows - split, D] region, no adds
   int32_t nt_store;     // nontemporal stores for that fill
+  int32_t skip_tail;    // big tiles in the trailing EMPTY hop chunks are not written (segment_gather_sum)
   int32_t interleave;   // spread the big tiles among the small ones (block order)
   int32_t spec_stage;   // segment-aligned tiles in two round trips (process_tile_seg)
 };
@@ -200,7 +201,7 @@ struct HopArgs {
 // dynamic region shifts its base off 16-B alignment and every ds_read_b128 replays at ~64 cycles).
 struct HopLds {
   int32_t* ptr;   // [kMaxRows + 1]
-  int32_t* lohi;  // [2] (also the two aligned cuts of a segment-aligned tile)
+  int32_t* lohi;  // [3] (also the two aligned cuts of a segment-aligned tile; [2] a big tile's skip flag)
 };
 constexpr int kLdsHead = 136;  // ints ahead of the col slice: ptr (129) + lohi (2), padded to 16 B
 
@@ -450,8 +451,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   if (threadIdx.x == 0) {
     L.lohi[0] = a.rowptr[R0];
     L.lohi[1] = a.rowptr[R0 + NR];
+    // skip_tail: no edge from the start of R0's chunk to the end (every consumer trims those chunks)
+    L.lohi[2] = a.skip_tail && a.out_rpc.d > 0 && a.rowptr[fdiv(R0, a.out_rpc) * a.out_rpc.d] == a.rowptr[a.rows];
   }
   __syncthreads();
+  if (L.lohi[2]) return;
   if (L.lohi[0] == L.lohi[1]) {
     if (a.flat_zero) {
       // the big tile's rows are one contiguous [NR, D] region and there is nothing to add: a flat
@@ -512,12 +516,16 @@ const HopEnv& hop_env() {
 
 using namespace aimx;
 
-extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
-                                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out,
-                                       int64_t out_ld, int64_t out_rpc, int64_t out_cs, const float* add0,
-                                       int64_t add0_ld, const float* add1, int64_t add1_ld, const int64_t* row_seg,
-                                       int64_t row_seg_stride, aimx_stream_t stream_) {
-  hipStream_t stream = (hipStream_t)stream_;
+namespace aimx {
+// aimx_segment_gather_sum with skip_tail: the big tiles of output chunks that lie wholly in the
+// trailing run of edge-less chunks are not written (the message-passing stack: its GEMMs trim those
+// columns of F exactly, AimxGemmArgs.zc_*, so the zeros the reference's hop leaves there are never
+// read)
+int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
+                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
+                       int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
+                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
+                       int32_t skip_tail) {
   if (rows < 0 || D < 0) return AIMX_EARG;
   if (rows == 0 || D == 0) return AIMX_OK;
   if (!src || !rowptr || !out) return AIMX_EARG;
@@ -537,7 +545,7 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   const int64_t rows_mode = E.rows_mode;
   if ((vec < 4 && rows_mode == 1) || rows_mode == 2)
     return launch_gather_rows(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
-                              add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream);
+                              add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream, skip_tail);
   const int64_t upr_i = D / vec;
   // 32-bit thread indexing (rows * D / vec < 2^31) and int32 chunked row ids.
   if (rows * upr_i >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;
@@ -601,6 +609,7 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   a.nt_store = E.nt != 0 ? 1 : 0;
   a.interleave = E.interleave != 0 ? 1 : 0;
   a.spec_stage = E.spec != 0 ? 1 : 0;
+  a.skip_tail = skip_tail;
   using KFn = void (*)(const HopArgs);
   const bool chunked = src_rpc > 0;
   KFn fn = vec == 4 ? (chunked ? k_gather_sum<4, true> : k_gather_sum<4, false>)
@@ -609,4 +618,14 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(threads), dyn, stream, a);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
+}
+}  // namespace aimx
+
+extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
+                                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out,
+                                       int64_t out_ld, int64_t out_rpc, int64_t out_cs, const float* add0,
+                                       int64_t add0_ld, const float* add1, int64_t add1_ld, const int64_t* row_seg,
+                                       int64_t row_seg_stride, aimx_stream_t stream) {
+  return aimx::segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs,
+                                  add0, add0_ld, add1, add1_ld, row_seg, row_seg_stride, (hipStream_t)stream, 0);
 }

@@ -33,6 +33,6 @@ __device__ __forceinline__ int64_t row_off(uint32_t r, int64_t ld, const FastDiv
 int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
                        int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
-                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream);
+                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream, int32_t skip_tail = 0);
 
 }  // namespace aimx

@@ -69,6 +69,7 @@ struct RowsArgs {
   const int64_t* seg;  // molecule id per row of [0, split) (optional)
   int64_t seg_stride;
   int32_t lean;  // fewer barriers per piece (AIMX_HOPR_LEAN=0: the round-3 schedule, for A/B)
+  int32_t skip_tail;  // big tiles in the trailing EMPTY hop chunks are not written (segment_gather_sum)
 };
 
 __device__ __forceinline__ uint32_t misal(const void* p) { return (uint32_t)((uintptr_t)p >> 2) & 3u; }
@@ -503,8 +504,12 @@ __global__ __launch_bounds__(kRT) void k_gather_rows(const RowsArgs a) {
     if (threadIdx.x == 0) {
       s_misc[0] = a.rowptr[R0];
       s_misc[1] = a.rowptr[R1];
+      // skip_tail: no edge from the start of R0's chunk to the end (every consumer trims those chunks)
+      s_misc[2] = a.skip_tail && a.out_rpc.d > 0 &&
+                  a.rowptr[fdiv(R0, a.out_rpc) * a.out_rpc.d] == a.rowptr[a.rows];
     }
     __syncthreads();
+    if (s_misc[2]) return;
     const bool empty = s_misc[0] == s_misc[1];
     if (empty && a.flat_zero) {
       // the big tile's rows are one contiguous [NR, D] region: head dwords, aligned float4 body, tail
@@ -566,7 +571,8 @@ int64_t env_i64(const char* name, int64_t dflt) {
 int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
                        int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
-                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream) {
+                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
+                       int32_t skip_tail) {
   // 4-byte-aligned fp32 rows (the 16-byte fix-up works on float offsets)
   auto al4 = [](const void* p) { return ((uintptr_t)p & 3) == 0; };
   if (!al4(src) || !al4(out) || (add0 && !al4(add0)) || (add1 && !al4(add1))) return AIMX_EARG;
@@ -644,6 +650,7 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   a.flat_zero = (contiguous && !add0 && !add1) ? 1 : 0;
   a.interleave = interleave;
   a.lean = lean;
+  a.skip_tail = skip_tail;
   const int64_t blocks = nsmall + nbig;
   if (blocks <= 0) return AIMX_OK;
   if (blocks >= (int64_t)INT32_MAX) return AIMX_EARG;

@@ -374,9 +374,14 @@ struct aimx_h5_reader {
   const uint8_t* map = nullptr;
   size_t map_size = 0;
   uint64_t desc = 0, addr_base = 0;
+  // the mapped file's identity at open (re-checked before every direct read: a file replaced,
+  // truncated or rewritten since then is read through H5Dread instead of a stale or short mapping)
+  int map_fd = -1;
+  struct stat map_st {};
   std::vector<Part> parts;  // decode buffers, reused read after read (one read at a time per handle)
   ~aimx_h5_reader() {
     if (map) munmap(const_cast<uint8_t*>(map), map_size);
+    if (map_fd >= 0) ::close(map_fd);
     if (memtype >= 0) H5Tclose(memtype);
     if (space >= 0) H5Sclose(space);
     if (data >= 0) H5Dclose(data);
@@ -417,9 +422,11 @@ static void try_direct(aimx_h5_reader* r, const char* path) {
   if (fd < 0) return;
   struct stat st;
   void* m = MAP_FAILED;
-  if (fstat(fd, &st) == 0 && st.st_size > 0) m = mmap(nullptr, size_t(st.st_size), PROT_READ, MAP_SHARED, fd, 0);
-  ::close(fd);
-  if (m == MAP_FAILED) return;
+  if (fstat(fd, &st) == 0 && st.st_size > 0) m = mmap(nullptr, size_t(st.st_size), PROT_READ, MAP_PRIVATE, fd, 0);
+  if (m == MAP_FAILED) {
+    ::close(fd);
+    return;
+  }
   const uint8_t* map = static_cast<const uint8_t*>(m);
   const size_t size = size_t(st.st_size);
   std::vector<hsize_t> sample;
@@ -451,8 +458,11 @@ static void try_direct(aimx_h5_reader* r, const char* path) {
   H5Sclose(ms);
   if (base_found == ~uint64_t(0)) {
     munmap(m, size);
+    ::close(fd);
     return;
   }
+  r->map_fd = fd;
+  r->map_st = st;
   r->map = map;
   r->map_size = size;
   r->desc = uint64_t(off) + base_found;
@@ -577,8 +587,19 @@ int aimx_h5_read_store(aimx_h5_reader* r, const int64_t* pos, int64_t n, int32_t
         if (bytes_of(j, &p, &len) && decode_record(p, len, n_hops, n_tasks, &m)) m.req.push_back(vis[j]);
       }
     };
+    if (r->map) {  // the file must still be the one mapped at open (path, size, modification time)
+      struct stat now;
+      if (fstat(r->map_fd, &now) != 0 || now.st_size != r->map_st.st_size || now.st_nlink == 0 ||
+          now.st_mtim.tv_sec != r->map_st.st_mtim.tv_sec || now.st_mtim.tv_nsec != r->map_st.st_mtim.tv_nsec) {
+        munmap(const_cast<uint8_t*>(r->map), r->map_size);
+        r->map = nullptr;
+        r->info.direct_read = 0;
+      }
+    }
     if (n > 0 && r->map) {
-      // direct path: every worker finds and decodes its records in the mapped file
+      // direct path: every worker finds and decodes its records in the mapped file (the file must
+      // stay unmodified while a read is in progress: a change between the check above and the read
+      // is not caught)
       std::atomic<bool> corrupt{false};
       parallel_for(n, P, [&](int t, int64_t lo, int64_t hi) {
         decode_range(t, lo, hi, [&](int64_t j, const uint8_t** p, size_t* len) {

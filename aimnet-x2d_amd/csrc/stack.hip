@@ -127,9 +127,10 @@ int run(AimxGemmArgs a, const Ws& ws, hipStream_t s) {
 
 int gather(const AimxShellStack* st, const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
            const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld, int64_t out_rpc,
-           int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld, hipStream_t s) {
-  return aimx_segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
-                                 add0_ld, add1, add1_ld, st->row_seg, st->row_seg_stride, (aimx_stream_t)s);
+           int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld, hipStream_t s,
+           int32_t skip_tail = 0) {
+  return segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
+                            add0_ld, add1, add1_ld, st->row_seg, st->row_seg_stride, s, skip_tail);
 }
 
 // Empty hop chunks (AimxGemmArgs.zc_*): every GEMM over F's columns trims the all-zero chunks the
@@ -213,8 +214,12 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
     } else if (l == 0) {
       RUN(copy2d(s->x_in, s->x_in_ld, F, K, N, D, st));
     }
-    // 2) hop: chunks 1..h of F = scatter_add(x[src % N], target) in edge order
-    RUN(gather(s, F, K, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, K, N, D, nullptr, 0, nullptr, 0, st));
+    // 2) hop: chunks 1..h of F = scatter_add(x[src % N], target) in edge order. The trailing
+    //    edge-less chunks (all but the first for reference inputs, layers.py:154) are not written:
+    //    every GEMM over F trims them exactly (zc_*: the input projection's k loop stops before
+    //    them, the weight gradient reads them as zero), so their zeros would be dead stores
+    RUN(gather(s, F, K, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, K, N, D, nullptr, 0, nullptr, 0, st,
+               zc_on() ? 1 : 0));
     // 3) [u | g] = F [Wi ; Wg]^T + [bi ; bg], a0 = act(u)
     {
       AimxGemmArgs a = linear_fwd(N, K, D2, F, K, s->w_ig[l], s->UG[l], D2);

@@ -203,6 +203,59 @@ def test_split_graph_ddp_replicas_agree_and_equal_eager():
     assert np.abs(out[0]["graph"] - out[0]["eager"]).max() <= 1e-5 * scale
 
 
+def ddp_split_graph_offlayout(rank, world):
+    """Split-graph data-parallel steps where ONE rank gets a batch of another layout at step 2 (an
+    unpadded batch: the static capacity overflowed) and runs it through GraphedTrainStep._eager
+    while its peer replays: the collectives still pair up (same buckets, same order), the replicas
+    stay bit-identical, and the parameters equal the all-eager data-parallel run's."""
+    from aimx import feed
+    from aimx.optim import FusedAdam
+    from aimx.train import GraphedTrainStep, train_step
+    from models import L1Loss
+    from utils.distributed import GradientSync, replica_checksums
+    bs = _padded_batches(rank, 4)
+    if rank == 1:  # the same molecules, unpadded: another layout
+        from aimx.synth import QM9Asset
+        asset = QM9Asset()
+        y = asset.targets[:, :1]
+        store = feed.HostStore.from_arrays(asset.atom_off, asset.bond_off, np.stack([asset.bi, asset.bj], 1),
+                                           asset.feats, ((y - y.mean()) / y.std()).astype(np.float32),
+                                           asset.total_charge, precompute_hops=HOPS)
+        rng = np.random.default_rng(7)
+        idx = [rng.integers(0, len(store), 2 * B_HALF)[rank * B_HALF:(rank + 1) * B_HALF] for _ in range(4)]
+        bs[2] = next(iter(feed.BatchFeeder(store, iter([idx[2]]), HOPS, "cuda", depth=1)))
+        assert bs[2]._layout != bs[1]._layout
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    sync = GradientSync(m.parameters(), unused=m.unused_parameters())
+    g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1)
+    for b in bs[1:]:
+        g(b)
+    torch.cuda.synchronize()
+    res = {"mode": g.mode, "eager_steps": g.eager_steps,
+           "graph": torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy(),
+           "identical": replica_checksums(list(m.parameters()))[0]}
+    sync.remove()
+    m = _model()
+    opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
+    sync = GradientSync(m.parameters(), unused=m.unused_parameters())
+    for b in bs:
+        train_step(m, b, L1Loss(), opt, sync=sync, n_real=B_HALF)
+    torch.cuda.synchronize()
+    res["eager"] = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    return res
+
+
+def test_split_graph_ddp_one_rank_off_layout():
+    out = _run("ddp_split_graph_offlayout")
+    assert out[0]["mode"] == out[1]["mode"] == "split"
+    assert out[0]["eager_steps"] == 0 and out[1]["eager_steps"] == 1
+    assert out[0]["identical"] and out[1]["identical"]
+    np.testing.assert_array_equal(out[0]["graph"], out[1]["graph"])
+    scale = np.abs(out[0]["eager"]).max()
+    assert np.abs(out[0]["graph"] - out[0]["eager"]).max() <= 1e-5 * scale
+
+
 def rccl_capture_world1(rank, world):
     """One RCCL rank: the bucket all-reduces are recorded inside the step's single graph."""
     from aimx.optim import FusedAdam

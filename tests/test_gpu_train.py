@@ -91,15 +91,62 @@ def test_graphed_step_runs_off_layout_batch_eagerly():
 
 
 def test_training_reduces_loss():
+    """Under dropout 0.05 (the reference default): 4 epochs over 12 QM9 batches, the last epoch >= 5 %
+    below the first and the last two on average below it. Epoch losses are not monotone at this
+    scale in the reference either: the fp64 oracle without dropout, same data, gives e.g. 0.7752,
+    0.7236, 0.7135, 0.7166 for one seed; the no-dropout trajectory is pinned to the oracle's below."""
     from aimx.train import GraphedTrainStep, train_epoch
     store, m, crit, opt = _setup(dropout=0.05)
     bs = _batches(store, 12, B=128, seed=3)
     g = GraphedTrainStep(m, crit, opt, bs[0], n_real=128)
     losses = [train_epoch(m, bs, crit, opt, DEV, graphed=g)[0] for _ in range(4)]
-    # the last epoch >= 5 % below the first and the last two on average below it; a single early
-    # epoch may sit above the first under dropout (rebuilt QM9 asset: 0.748, 0.767, 0.730, 0.678)
     assert losses[-1] < 0.95 * losses[0] and np.mean(losses[2:]) < losses[0], losses
     assert all(np.isfinite(losses))
+
+
+def test_training_epochs_match_oracle():
+    """Dropout off: the same 4 graph-replayed epochs (48 steps of forward, L1, backward, clip(1.0),
+    Adam) against the fp64 oracle from the same initial weights on the same molecules — every
+    epoch's mean loss within 1e-3 relative — and the loss falls >= 5 % from the first epoch to the
+    last on both."""
+    from aimx.synth import QM9Asset
+    from aimx.train import GraphedTrainStep, train_epoch
+    from aimx import data as adata
+    from oracle import model as om
+    store, m, crit, opt = _setup(dropout=0.0)
+    init = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
+    bs = _batches(store, 12, B=128, seed=3)
+    g = GraphedTrainStep(m, crit, opt, bs[0], n_real=128)
+    ours = [train_epoch(m, bs, crit, opt, DEV, graphed=g)[0] for _ in range(4)]
+    asset = QM9Asset()
+    y = asset.targets[:, :1]
+    yn = (y - y.mean()) / y.std()
+    rng = np.random.default_rng(3)  # _batches' molecule draw
+    idx = [rng.integers(0, len(store), 128) for _ in range(12)]
+    cols = [adata.collate(asset.molecules(i), 3) for i in idx]
+    cfg = om.default_config(hidden_dim=128, num_shells=3, output_dim=1)
+    p = {k: v.clone().requires_grad_() for k, v in init.items()}
+    aopt = torch.optim.Adam(p.values(), lr=1e-3)
+    torch.set_num_threads(8)
+    ref = []
+    for _ in range(4):
+        ls = []
+        for c, i in zip(cols, idx):
+            feats = torch.from_numpy(c["feats"].astype(np.int64))
+            af = {k: feats[:, j].contiguous() for j, k in enumerate(("atom_type", "hydrogen_count", "degree",
+                                                                      "hybridization"))}
+            aopt.zero_grad(set_to_none=True)
+            out, _, _ = om.gnn_forward(p, cfg, af, torch.from_numpy(c["edges"].astype(np.int64)).reshape(-1, 2),
+                                       torch.from_numpy(c["batch"].astype(np.int64)),
+                                       torch.from_numpy(asset.total_charge[i].astype(np.float64)))
+            loss = torch.nn.functional.l1_loss(out, torch.from_numpy(yn[i].astype(np.float64)))
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_([v for v in p.values() if v.grad is not None], 1.0)
+            aopt.step()
+            ls.append(loss.item())
+        ref.append(float(np.mean(ls)))
+    np.testing.assert_allclose(ours, ref, rtol=1e-3, atol=0)
+    assert ours[-1] < 0.95 * ours[0] and ref[-1] < 0.95 * ref[0], (ours, ref)
 
 
 def test_full_train_step_matches_oracle():

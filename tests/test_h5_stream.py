@@ -261,3 +261,22 @@ def test_direct_read_never_returns_wrong_bytes(tmp_path):
             continue
         col = _collate_h(store, 3)
         assert np.array_equal(kept, kref) and np.array_equal(col["edges"], ref["edges"])
+
+
+def test_file_changed_after_open_falls_back_from_the_mapping(tmp_path):
+    """The direct path maps the file at open; a file modified afterwards (here: a copy of the
+    fixture, its tail truncated away — a stream regenerated by another process) is no longer read
+    through that mapping (which would fault past the new end): the reader re-checks the file's
+    size and time before each read and drops to H5Dread, which fails with an error instead."""
+    p = tmp_path / "s.h5"
+    shutil.copy(FIX, p)
+    f = h5.H5File(str(p))
+    assert f.direct_read
+    ok, _ = f.read_store(np.arange(f.n_records), 3, 1)
+    assert len(ok) > 0
+    os.truncate(p, os.path.getsize(p) // 2)
+    try:
+        f.read_store(np.arange(f.n_records), 3, 1)
+    except Exception:  # H5Dread of the truncated file: an error, never a crash
+        pass
+    assert not f.direct_read

@@ -2,6 +2,7 @@
 # round-4 working call (overwritten per call)
 export PYTHONDONTWRITEBYTECODE=1
 tools/gpu_steps.sh \
+ "60 r4a/mfma4x4.log tools/micro/mfma4x4" \
  "300 r4a/mlps_tests.log python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -k streamed_mlp_matches_per_gemm" \
  "?400 r4a/mlps_model.log python3 -u -m pytest tests/test_gpu_parity.py -v --timeout 120 --timeout-method thread -k 'full_size or c4s or c5s or streamed_mlp_forced'" \
  "300 r4a/bench_c4.log python3 bench.py --config c4 --steps 30 --warmup 5 --no-cpu-baseline --no-roofline --no-eager" \

@@ -11,7 +11,11 @@ attention, partial charges, every parameter gradient, gradient sketches), record
 All errors are norm-relative (max |a - b| / max |b|; attention-bias gradients, exactly 0 in exact
 arithmetic, against their weight's scale).
 
-Usage (GPU box): python tools/parity_report.py [--out profiles/r02_parity.json] [case ...]
+Config-sized cases (c4, c5: test_gpu_parity.FULL_SIZE) carry the oracle's own fp32 run as
+`vs_ref32` / `ref_floor` (no reference fixture at that size).
+
+Usage (GPU box): python tools/parity_report.py [--out profiles/r04_parity.json] [case ...]
+(default: every golden case, then c4 and c5 at their configured batch)
 """
 import argparse
 import json
@@ -34,7 +38,22 @@ def err(a, b, sc):
     return float(np.abs(a - b).max() / den) if den > 0 and b.size else 0.0
 
 
+def run_full(name):
+    """A config-sized case (test_gpu_parity.FULL_SIZE: c4 512 x 40-atom molecules, c5 256): the
+    reference fp32 floor is the oracle's own fp32 run (the fixture-pinned restatement of the
+    reference's ATen ops), every gradient compared whole."""
+    z, cfg, inputs, loss_w = T.full_size_case(name)
+    torch.set_num_threads(min(16, os.cpu_count() or 8))
+    seed = int(z["seed"])
+    ref64 = T._run_full(cfg, seed, inputs, loss_w, "cpu", torch.float64)
+    ref32 = T._run_full(cfg, seed, inputs, loss_w, "cpu", torch.float32)
+    ours = T._run_full(cfg, seed, inputs, loss_w, "cuda")
+    return _rows(ours, ref32, ref64)
+
+
 def run_case(name):
+    if name in T.FULL_SIZE:
+        return run_full(name)
     z, cfg, inputs = load_case(name)
     torch.set_num_threads(8)
     ref64 = T._oracle_run(z, cfg, inputs, torch.float64)
@@ -52,6 +71,10 @@ def run_case(name):
         if p.grad is not None:
             ours["grad." + k] = p.grad.cpu().numpy()
     add_sketches(ours, z)
+    return _rows(ours, ref32, ref64)
+
+
+def _rows(ours, ref32, ref64):
     rows = {}
     for k in sorted(ref64):
         if k not in ours:
@@ -73,7 +96,7 @@ def main():
     a = ap.parse_args()
     report = {"metric": "norm-relative error per tensor (see tools/parity_report.py)", "contract": 1e-5,
               "cases": {}}
-    for name in a.cases or CASES:
+    for name in a.cases or (CASES + sorted(T.FULL_SIZE)):
         rows = run_case(name)
         stored = [r for r in rows.values() if r["vs_ref32"] is not None]
         report["cases"][name] = {
