@@ -131,6 +131,7 @@ class Head(ctypes.Structure):
         ("mask", c_ptr * HEAD_MAX_BLOCKS), ("z", c_ptr * HEAD_MAX_BLOCKS), ("cat", c_ptr),
         ("out", c_ptr), ("ldo", c_i64),
         ("sync", c_ptr), ("cluster", c_i32),
+        ("fwd_ws", c_ptr), ("fwd_ws_bytes", c_size),
     ]
 
 
@@ -212,6 +213,7 @@ _SIGS = {
                                    c_ptr]),
     "aimx_head_forward": (c_i32, [ctypes.POINTER(Head), c_ptr]),
     "aimx_head_backward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
+    "aimx_head_forward_workspace_bytes": (c_size, [ctypes.POINTER(Head)]),
     "aimx_head_backward": (c_i32, [ctypes.POINTER(Head), ctypes.POINTER(HeadGrad), c_ptr]),
     "aimx_dropout_seeds": (c_i32, [c_ptr, c_ptr, c_i32, c_ptr]),
     "aimx_pad_batch": (c_i32, [c_ptr, c_ptr]),

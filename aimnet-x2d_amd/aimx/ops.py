@@ -1087,7 +1087,12 @@ class _Head(torch.autograd.Function):
         h.y0, h.cat = ptr(views[iy0]), ptr(views[icat])
         h.out, h.ldo = ptr(out), T
         h.sync, h.cluster = ptr(_lib.head_sync(dev)), spec["cluster"]
+        # the 8-molecule kernels' transposed chain weights (0 bytes: the 16-molecule kernels)
+        fwsb = lib.aimx_head_forward_workspace_bytes(h)
+        fws = torch.empty(max(fwsb // 4, 4), dtype=_F32, device=dev) if fwsb else None
+        h.fwd_ws, h.fwd_ws_bytes = (ptr(fws), fwsb) if fws is not None else (None, 0)
         check(lib.aimx_head_forward(h, stream_ptr(dev)), "head_forward")
+        del fws
         ctx.spec, ctx.drop = spec, drop
         ctx.save_for_backward(x0, seed if drop else None, *wts)
         ctx.state = dict(buf=buf, views=views, iy0=iy0, iv=iv, ih=ih, iz=iz, icat=icat, masks=masks)

@@ -90,6 +90,11 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Internal launchers shared across translation units.
+// The 8-molecule fused head (head8.hip); head.hip's entry points dispatch to it where it applies.
+bool head8_ok(const AimxHead* h);
+size_t head8_forward_workspace_floats(const AimxHead* h);
+int head8_forward(const AimxHead* h, float* wt, hipStream_t st);
+int head8_backward(const AimxHead* h, const AimxHeadGrad* d, hipStream_t st);
 // aimx_segment_gather_sum (hop.hip) with skip_tail: chunks in the trailing run of edge-less hop chunks
 // are not written (only for consumers that trim them: the stack's GEMMs via AimxGemmArgs.zc_*)
 int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,

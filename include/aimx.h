@@ -424,6 +424,9 @@ typedef struct AimxHead {
    * words, zeroed once by the caller and kept zero by the kernels (word 0 becomes non-zero if a
    * cluster wait ever timed out: results of that call are invalid). */
   int32_t* sync; int32_t cluster;
+  /* Forward workspace (aimx_head_forward_workspace_bytes(h), 16-B aligned; NULL: the 16-molecule
+   * kernels): the 8-molecule kernels read the transposed chain weights from it. */
+  float* fwd_ws; size_t fwd_ws_bytes;
 } AimxHead;
 
 typedef struct AimxHeadGrad {
@@ -433,6 +436,7 @@ typedef struct AimxHeadGrad {
   void* workspace; size_t workspace_bytes;  /* aimx_head_backward_workspace_bytes(h), 16-B aligned */
 } AimxHeadGrad;
 
+size_t aimx_head_forward_workspace_bytes(const AimxHead* h);
 int aimx_head_forward(const AimxHead* h, aimx_stream_t stream);
 size_t aimx_head_backward_workspace_bytes(const AimxHead* h);
 int aimx_head_backward(const AimxHead* h, const AimxHeadGrad* d, aimx_stream_t stream);
