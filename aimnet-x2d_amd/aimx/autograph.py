@@ -192,38 +192,37 @@ class _Bucket:
         check(_lib.load().aimx_pad_batch(ctypes.byref(a), stream_ptr(self.dev)), "autograph pad_batch")
 
     def capture(self, model, warmup=2):
+        # The warm-up and captured backward passes compute the gradients with autograd.grad, not
+        # .backward(): no AccumulateGrad node runs, so no hook on the parameters fires for them
+        # (DDP's reducer would take each for a real backward) and no .grad is touched
         params = self.params
-        saved = [p.grad for p in params]
-        for p in params:
-            p.grad = None
+        live = [p for p in params if p.requires_grad]
         args = self.static_args()
         cur = torch.cuda.current_stream(self.dev)
         side = torch.cuda.Stream(device=self.dev)
         side.wait_stream(cur)
-        try:
-            with torch.cuda.stream(side):  # warm-up: plans, workspaces, allocator pools, seed state
-                for _ in range(warmup):
-                    out = model._aimx_forward(*args)[0]
-                    out.backward(torch.zeros_like(out))
-                    for p in params:
-                        p.grad = None
-            cur.wait_stream(side)
-            torch.cuda.synchronize(self.dev)
-            self.g_fwd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_fwd):
-                self.outs = model._aimx_forward(*args)
-            self.gout = torch.zeros_like(self.outs[0])
-            # the backward graph gets its own memory pool: in a shared one, the gradient tensors it
-            # leaves behind could sit in blocks the forward graph used (and frees) for temporaries,
-            # and the next forward replay would overwrite the caller's .grad
-            self.g_bwd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_bwd):
-                torch.autograd.backward(self.outs[0], self.gout)
-            self.grads = [p.grad for p in params]
-            self.outs = tuple(o.detach() if o is not None else None for o in self.outs)
-        finally:
-            for p, g in zip(params, saved):
-                p.grad = g
+        with torch.cuda.stream(side):  # warm-up: plans, workspaces, allocator pools, seed state
+            for _ in range(warmup):
+                out = model._aimx_forward(*args)[0]
+                torch.autograd.grad(out, live, torch.zeros_like(out), allow_unused=True)
+                # drop the warm-up graph before the capture: alive, its nodes would stay bound to
+                # this side stream while the captured backward runs on the capture stream
+                del out
+        cur.wait_stream(side)
+        torch.cuda.synchronize(self.dev)
+        self.g_fwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fwd):
+            self.outs = model._aimx_forward(*args)
+        self.gout = torch.zeros_like(self.outs[0])
+        # the backward graph gets its own memory pool: in a shared one, the gradient tensors it
+        # leaves behind could sit in blocks the forward graph used (and frees) for temporaries,
+        # and the next forward replay would overwrite the caller's .grad
+        self.g_bwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_bwd):
+            gs = torch.autograd.grad(self.outs[0], live, self.gout, allow_unused=True)
+        by_id = {id(p): g for p, g in zip(live, gs)}
+        self.grads = [by_id.get(id(p)) for p in params]
+        self.outs = tuple(o.detach() if o is not None else None for o in self.outs)
 
 
 class _Replay(torch.autograd.Function):

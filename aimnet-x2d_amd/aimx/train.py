@@ -42,6 +42,47 @@ def train_step(model, batch, criterion, optimizer, sync=None, n_real=None):
     return loss.detach(), nan
 
 
+def _snapshot(model, optimizer, dev):
+    """Parameters, optimizer state and the dropout seed counters before GraphedTrainStep's warm-up."""
+    from . import ops
+    ops._seed_state(model, dev)  # the model's dropout counter exists before the warm-up draws from it
+    params = [(p, p.detach().clone()) for p in model.parameters()]
+    seeds = [(m._aimx_seed_state, m._aimx_seed_state.clone()) for m in model.modules()
+             if torch.is_tensor(getattr(m, "_aimx_seed_state", None))]
+    state = {p: {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+             for p, st in optimizer.state.items()}
+    step_t = getattr(optimizer, "_step_t", None)
+    return params, seeds, state, step_t.clone() if torch.is_tensor(step_t) else None
+
+
+@torch.no_grad()
+def _restore(saved, optimizer):
+    """Put back what _snapshot saw, in place (the graphs hold these tensors' addresses). State the
+    warm-up created (Adam's moments and step counts) goes back to its initial zeros."""
+    params, seeds, state, step_t = saved
+    for p, v in params:
+        p.copy_(v)
+    for t, v in seeds:
+        t.copy_(v)
+    for p, st in optimizer.state.items():
+        old = state.get(p, {})
+        for k, v in list(st.items()):
+            if torch.is_tensor(v):
+                if torch.is_tensor(old.get(k)):
+                    v.copy_(old[k])
+                else:
+                    v.zero_()
+            else:
+                st[k] = old.get(k, type(v)(0) if isinstance(v, (int, float)) else v)
+    cur = getattr(optimizer, "_step_t", None)
+    if torch.is_tensor(cur):
+        if step_t is not None and step_t.numel() <= cur.numel():
+            cur.zero_()
+            cur[: step_t.numel()].copy_(step_t)
+        else:
+            cur.zero_()
+
+
 class GraphedTrainStep:
     """The train step captured as HIP graphs on a static padded batch (see module docstring).
 
@@ -50,7 +91,9 @@ class GraphedTrainStep:
     layout (same padded atom / edge / molecule counts and task count) is replayed, any other (a
     feeder's rare over-capacity batch, handed out unpadded) runs the same step eagerly on the same
     parameters, gradients, optimizer state and loss accumulators. optimizer must be capturable
-    (FusedAdam).
+    (FusedAdam). Construction runs `warmup` real steps on example_batch (allocator pools, plans,
+    optimizer state, communicators) and then rewinds the parameters, the optimizer state and the
+    dropout counter, so the first call is the reference loop's first step.
 
     Data-parallel modes (`sync`: a utils.distributed.GradientSync; `ddp_graph` or the
     AIMX_DDP_GRAPH environment variable picks one):
@@ -108,6 +151,9 @@ class GraphedTrainStep:
             mode = "single"
         elif mode == "capture" and not sync.capturable:
             mode = "split"
+        # the warm-up steps below really train (optimizer state, dropout counter): their starting
+        # state is put back after the capture, so the first call is the loop's first step
+        saved = _snapshot(model, optimizer, dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up: allocator pools, plans, optimizer state, RCCL comms
@@ -163,6 +209,7 @@ class GraphedTrainStep:
             with torch.cuda.graph(self.g2):
                 optimizer.step()
         self.mode = mode
+        _restore(saved, optimizer)
         self.reset_stats()
 
     def reset_stats(self):

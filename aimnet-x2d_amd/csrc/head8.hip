@@ -374,14 +374,16 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
 
 }  // namespace
 
-// The 8-row kernels apply when every chain GEMM is F x F with F a multiple of 128 up to 512
+// The 8-row kernels apply when every chain GEMM is F x F with F = 128, 256 or 512
 // (H_in == F: the reference's defaults, ffn_hidden_dim = hidden_dim) and the LDS holds the tiles.
 bool head8_ok(const AimxHead* h) {
   if (const char* e = getenv("AIMX_HEAD8")) {
     if (atoi(e) == 0) return false;
   }
   const int64_t F = h->F;
-  if (F < 128 || F > kMaxF8 || F % 128 || h->H_in != F || h->nb < 1 || h->nb > AIMX_HEAD_MAX_BLOCKS) return false;
+  // the 16 waves split into F / 64 column groups x 16 / (F / 64) k ranges exactly: F = 128, 256, 512
+  if (F < 128 || F > kMaxF8 || kWaves % (F / 64) || F % 64 || h->H_in != F || h->nb < 1 || h->nb > AIMX_HEAD_MAX_BLOCKS)
+    return false;
   return lds8_floats(geo8((int)F)) * sizeof(float) <= 156 * 1024;
 }
 

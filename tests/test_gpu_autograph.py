@@ -68,6 +68,32 @@ def test_autograph_matches_eager_forward_and_gradients(pc):
     assert len(st.buckets) == 1
 
 
+def test_capture_leaves_no_stale_accumulate_grad_nodes():
+    """The capture's warm-up graph must be gone before the capture: alive, it would hand the
+    captured backward the warm-up stream's AccumulateGrad nodes (torch's stream-mismatch warning,
+    extra synchronisation)."""
+    import warnings
+    from aimx import autograph
+    from aimx.train import GraphedTrainStep
+    from aimx.optim import FusedAdam
+    from models import L1Loss
+    b = _batches(1, 12)[0]
+    m = autograph.enable(_model(), True)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        for _ in range(3):
+            m.zero_grad(set_to_none=True)
+            out, _, _ = m(*b.model_args())
+            out.sum().backward()
+        m2 = _model()
+        step = GraphedTrainStep(m2, L1Loss(), FusedAdam(m2.parameters(), lr=1e-3), b)
+        for _ in range(2):
+            step(b)
+        torch.cuda.synchronize()
+    bad = [str(x.message) for x in w if "AccumulateGrad" in str(x.message)]
+    assert not bad, bad[0]
+
+
 def test_autograph_training_tracks_eager_over_buckets():
     """Adam over batches of two sizes (two shape buckets, each replayed): same trajectory."""
     from aimx import autograph

@@ -167,7 +167,7 @@ def ddp_split_graph(rank, world):
     opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
     sync = GradientSync(m.parameters(), unused=m.unused_parameters())
     g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1)
-    for b in bs[1:]:
+    for b in bs:  # the warm-up step on bs[0] is rewound: bs[0] is the first real step
         g(b)
     torch.cuda.synchronize()
     res["mode"] = g.mode
@@ -185,7 +185,7 @@ def ddp_split_graph(rank, world):
     m = _model()
     opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
     sync = GradientSync(m.parameters(), unused=m.unused_parameters())
-    for b in bs:  # eager: the graph's warm-up step on bs[0] included
+    for b in bs:  # eager: the same steps
         train_step(m, b, L1Loss(), opt, sync=sync, n_real=B_HALF)
     torch.cuda.synchronize()
     res["eager"] = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
@@ -229,7 +229,7 @@ def ddp_split_graph_offlayout(rank, world):
     opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
     sync = GradientSync(m.parameters(), unused=m.unused_parameters())
     g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1)
-    for b in bs[1:]:
+    for b in bs:  # the warm-up step on bs[0] is rewound: bs[0] is the first real step
         g(b)
     torch.cuda.synchronize()
     res = {"mode": g.mode, "eager_steps": g.eager_steps,
@@ -268,7 +268,7 @@ def rccl_capture_world1(rank, world):
     sync = GradientSync(m.parameters(), unused=m.unused_parameters(), always=True, bucket_mb=0.25,
                         first_bucket_mb=0.05)
     g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1)
-    for b in bs[1:]:
+    for b in bs:  # the warm-up step on bs[0] is rewound: bs[0] is the first real step
         g(b)
     torch.cuda.synchronize()
     got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
@@ -302,7 +302,7 @@ def rccl_capture_fallback_world1(rank, world):
     sync = GradientSync(m.parameters(), unused=m.unused_parameters(), always=True, bucket_mb=0.25,
                         first_bucket_mb=0.05)
     g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=B_HALF, sync=sync, warmup=1, inject_capture_failure=True)
-    for b in bs[1:]:
+    for b in bs:  # the warm-up step on bs[0] is rewound: bs[0] is the first real step
         g(b)
     torch.cuda.synchronize()
     got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()

@@ -50,11 +50,11 @@ def test_graphed_step_matches_eager_step():
     bs = _batches(store, 6)
     _, m2, _, opt2 = _setup()
     m2.load_state_dict(m1.state_dict())
-    eager = [train_step(m1, b, crit, opt1, n_real=128)[0].item() for b in bs][1:]
-    # one warm-up step on bs[0] (optimizer state, lr upload) mirrors eager's first step
+    eager = [train_step(m1, b, crit, opt1, n_real=128)[0].item() for b in bs]
+    # the warm-up step's training is rewound after the capture: the first call is the first step
     g = GraphedTrainStep(m2, crit, opt2, bs[0], n_real=128, warmup=1)
     graphed = []
-    for b in bs[1:]:
+    for b in bs:
         before = g.loss_sum.item()
         g(b)
         graphed.append((g.loss_sum.item() - before) / 128)
@@ -73,10 +73,9 @@ def test_graphed_step_runs_off_layout_batch_eagerly():
     bs = _batches(store, 6)
     rng = np.random.default_rng(7)
     odd = next(iter(feed.BatchFeeder(store, iter([rng.integers(0, len(store), 128)]), 3, DEV, depth=1)))
-    seq = bs[1:3] + [odd] + bs[3:]
+    seq = bs[0:3] + [odd] + bs[3:]
     _, m2, _, opt2 = _setup()
     m2.load_state_dict(m1.state_dict())
-    train_step(m1, bs[0], crit, opt1, n_real=128)
     eager = [train_step(m1, b, crit, opt1, n_real=128)[0].item() for b in seq]
     g = GraphedTrainStep(m2, crit, opt2, bs[0], n_real=128, warmup=1)
     graphed = []
@@ -172,6 +171,7 @@ def test_full_train_step_matches_oracle():
     e0 = torch.empty(0, 2, dtype=torch.long, device=DEV)
     args = (afd, edges.to(DEV), batch.to(DEV), tc.to(DEV), torch.empty(0, 4, dtype=torch.long, device=DEV), e0, e0)
     crit = L1Loss()
+    g_prev = {}
     for step in range(2):
         opt.zero_grad(set_to_none=True)
         out, _, _ = model(*args)
@@ -194,12 +194,18 @@ def test_full_train_step_matches_oracle():
             d = (ours - ref).abs()
             total += d.numel()
             flips += int((d > tol).sum())
-            g = p64[k].grad
-            if g is not None:  # entries with a clearly resolved gradient must agree tightly
-                # (step 2's m/sqrt(v) amplifies the fp32 gradient noise where g2 ~ -g1: 1e-2 lr)
+            g = p64[k].grad  # the clipped gradient (clip_grad_norm_ scales .grad in place)
+            if g is not None:  # entries with a clearly resolved, well-conditioned update must agree tightly
                 big = g.abs() > 1e-3 * g.abs().max()
+                if step == 1 and k in g_prev:
+                    # step 2's first moment is 0.09 g1 + 0.1 g2: where the two cancel, m / sqrt(v)
+                    # amplifies the fp32 gradient noise without bound — keep the entries whose
+                    # cancellation costs at most a factor 10
+                    mag = 0.09 * g_prev[k].abs() + 0.1 * g.abs()
+                    big &= mag <= 10 * (0.09 * g_prev[k] + 0.1 * g).abs()
                 tol_big = (1e-3 if step == 0 else 1e-2) * lr
                 assert (d[big] <= tol_big + 1e-6 * ref[big].abs()).all(), (step, k, d[big].max().item())
+                g_prev[k] = g.detach().clone()
         assert flips <= 1e-3 * total, (step, flips, total)
 
 
