@@ -1339,9 +1339,10 @@ Plan plan_gemm(const AimxGemmArgs& a) {
   int64_t splits = a.splits;
   if (splits <= 0) {
     splits = 1;
-    // Split K while the grid is short of ~2 blocks per CU and every slice keeps >= 2 BK steps.
-    // Split K only for starved grids with long K (weight gradients: K = atoms).
-    if (t < 128 && a.K >= 1024) splits = std::min<int64_t>(cdiv(384, t), a.K / (4 * kBK));
+    // Split K only for grids short of one block per CU with a long K (weight gradients: K =
+    // atoms; c5's head GEMMs: 264 x 1024 x 1024 ran as 160 64 x 32 blocks of 32 BK steps each, ~35
+    // us, latency-bound), to ~512 blocks with every slice keeping >= 4 BK steps.
+    if (t < 256 && a.K >= 1024) splits = std::min<int64_t>(cdiv(512, t), a.K / (4 * kBK));
   }
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, 64));
   p.kchunk = cdiv(cdiv(a.K, splits), kBK) * kBK;

@@ -43,7 +43,7 @@ constexpr int kRows = 8;      // molecules per workgroup
 constexpr int kWaves = 16;    // waves per workgroup
 constexpr int kNT = 64 * kWaves;
 constexpr int kRing = 4;      // B items (4 k each) in flight per wave
-constexpr int kMaxF8 = 512;   // widest F
+constexpr int kMaxF8 = 256;   // widest F (see head8_ok)
 constexpr int kMaxGemms = 2 * AIMX_HEAD_MAX_BLOCKS + 2;
 
 __device__ __forceinline__ float drop_scale8(float p) { return p < 1.f ? 1.f / (1.f - p) : 0.f; }
@@ -374,14 +374,17 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
 
 }  // namespace
 
-// The 8-row kernels apply when every chain GEMM is F x F with F = 128, 256 or 512
+// The 8-row kernels apply when every chain GEMM is F x F with F = 128 or 256
 // (H_in == F: the reference's defaults, ffn_hidden_dim = hidden_dim) and the LDS holds the tiles.
 bool head8_ok(const AimxHead* h) {
   if (const char* e = getenv("AIMX_HEAD8")) {
     if (atoi(e) == 0) return false;
   }
   const int64_t F = h->F;
-  // the 16 waves split into F / 64 column groups x 16 / (F / 64) k ranges exactly: F = 128, 256, 512
+  // the 16 waves split into F / 64 column groups x 16 / (F / 64) k ranges exactly: F = 128, 256
+  // (512 would fit too, but every workgroup streams all 2 + 2 nb F x F weights through its CU: at
+  // F = 512 that is 9.4 MiB per workgroup, and the 65-workgroup launch ran 185 + 188 us at c4
+  // against 139 + 143 us for head.hip's clustered kernels, profiles/r04_c4_step_seq.txt)
   if (F < 128 || F > kMaxF8 || kWaves % (F / 64) || F % 64 || h->H_in != F || h->nb < 1 || h->nb > AIMX_HEAD_MAX_BLOCKS)
     return false;
   return lds8_floats(geo8((int)F)) * sizeof(float) <= 156 * 1024;

@@ -26,6 +26,9 @@
 // Measured alternatives (round 3, profiles/r03_hop_rows_ab.txt): a software pipeline that loads the
 // next item while the current one is summed, narrower passes with a separate output tile, and a
 // register realignment by lane shuffle (no output tile) all ran slower at the c4 / c5 roofline size.
+// Round 4: one wave per output row reading every source row straight from L1 / L2 (no LDS) was
+// 7-13 % faster in the step (c5 hop forward 54.5 -> 47.6 us) but 1.3-1.7x slower at the roofline
+// size, where it is bound by L2 bandwidth (each source row is re-read once per pair: E / N = 11-31).
 #include <algorithm>
 #include <climits>
 #include <cstdlib>

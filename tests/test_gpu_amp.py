@@ -68,35 +68,53 @@ def test_model_under_autocast_bf16():
 
 
 def test_amp_training_tracks_fp32():
-    """A few graph-replayed train steps under autocast (captured inside the autocast context) track
-    the fp32 steps' losses (same data, same init): the mean loss over the 12 steps within 2 %, every
-    step within 10 %. The fp32 run itself is pinned tightly (1e-4 per step) to the fp64 oracle's
-    trajectory by test_fp32_training_trajectory_matches_oracle; this bound is AMP's alone: bf16
-    operand rounding (2^-9 relative) compounds through Adam's sign-like early updates, so single
-    late steps drift by a few percent (7.9 % at step 11 on the rebuilt QM9 asset, the means 0.1 %
-    apart)."""
+    """Graph-replayed train steps under autocast (captured inside the autocast context) against the
+    fp32 steps (same data, same init, same dropout masks), in two parts:
+      * per step, no compounding: at each of the 12 states of the fp32 trajectory, the AMP forward's
+        loss (eval mode, no dropout) within 5e-3 relative of the fp32 forward's — bf16 operands
+        round at 2^-9 relative and the loss is a mean over 128 molecules;
+      * the replayed AMP trajectory itself: its first 6 steps within 1e-2 of fp32's per step, every
+        loss finite, and its last 6 steps below its first 6 on average (it trains). Later steps are
+        not held per step: Adam's early updates are ~ -lr sign(g), so a gradient entry whose sign
+        the bf16 rounding flips moves by 2 lr, and the two trajectories decorrelate (steps 9-11 here
+        drift by up to 13 % while step 0-5 agree to 0.5 %).
+    The fp32 run itself is pinned tightly (1e-4 per step) to the fp64 oracle's trajectory by
+    test_fp32_training_trajectory_matches_oracle."""
     import bench
     from aimx.optim import FusedAdam
     from aimx.train import GraphedTrainStep
     from models import L1Loss
     cfg = dict(bench.CONFIGS["c2"], batch=128)
     bs = bench.make_batches(cfg, 4, 3, DEV, pad=True)
-    losses = {}
+    crit = L1Loss()
+    losses, single = {}, []
     for amp in (False, True):
         torch.manual_seed(0)
         m = bench.build_model(cfg, DEV)
         opt = FusedAdam(m.parameters(), lr=1e-3, max_grad_norm=1.0)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            g = GraphedTrainStep(m, L1Loss(), opt, bs[0], n_real=128, warmup=1)
+            g = GraphedTrainStep(m, crit, opt, bs[0], n_real=128, warmup=1)
         ls = []
         for i in range(12):
+            b = bs[i % 4]
+            if not amp:  # the AMP forward's error at this fp32 state alone
+                m.eval()
+                with torch.no_grad():
+                    l32 = crit(m(*b.model_args())[0][:128], b.targets[:128]).item()
+                    with torch.autocast("cuda", dtype=torch.bfloat16):
+                        l16 = crit(m(*b.model_args())[0][:128], b.targets[:128]).item()
+                m.train()
+                single.append(abs(l16 - l32) / l32)
             before = g.loss_sum.item()
-            g(bs[i % 4])
+            g(b)
             ls.append((g.loss_sum.item() - before) / 128)
         losses[amp] = np.array(ls)
+    assert max(single) <= 5e-3, single
+    assert min(single) > 0, "autocast did not switch the GEMMs to bf16 operands"
     assert np.all(np.isfinite(losses[True]))
-    assert abs(losses[True].mean() - losses[False].mean()) <= 2e-2 * losses[False].mean()
-    np.testing.assert_allclose(losses[True], losses[False], rtol=1e-1, atol=1e-3)
+    np.testing.assert_allclose(losses[True][:6], losses[False][:6], rtol=1e-2, atol=0)
+    for amp in (False, True):
+        assert losses[amp][6:].mean() < losses[amp][:6].mean(), (amp, losses[amp])
 
 
 def test_fp32_training_trajectory_matches_oracle():

@@ -35,7 +35,9 @@ def _free_port():
 def _worker(rank, world, port, backend, fn_name, q):
     import sys
     sys.path[:0] = [ROOT, PKG, os.path.join(ROOT, "tests")]
+    import faulthandler
     import torch.distributed as dist
+    faulthandler.dump_traceback_later(90)  # a rank stuck past the parent's wait shows where
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     try:

@@ -48,6 +48,50 @@ def main():
         torch.cuda.synchronize()
         return y
 
+    # the parity test's exact sequence (forward + backward, modes alternating): which run departs?
+    w = torch.randn(n, d, device=dev)
+    torch.manual_seed(1)
+    ls = [ShellConvolutionLayer(d, d, num_hops=hops).to(dev) for _ in range(3)]
+    params = [p for l in ls for p in l._aimx_params()]
+    runs = []
+    from aimx import _lib
+
+    def state():
+        d = {"x": x, "w": w, "fwd.rowptr": plan.fwd.rowptr, "fwd.col": plan.fwd.col, "bwd.rowptr": plan.bwd.rowptr,
+             "bwd.col": plan.bwd.col, "counters": _lib.counters(dev), "batch": plan._keep[-1]}
+        seg = plan.row_seg()
+        d.update({f"param{i}": p for i, p in enumerate(params)})
+        return {k: v.detach().clone() for k, v in d.items()}, seg
+
+    snap, seg0 = state()
+    for mode, rt in (("0", None), ("1", None), ("0", None), ("1", "1"), ("0", None), ("1", None)):
+        os.environ["AIMX_MLPS"] = mode
+        if rt:
+            os.environ["AIMX_MLPS_RT"] = rt
+        xs = x.clone().requires_grad_()
+        ps = [p.detach().clone().requires_grad_() for p in params]
+        y = ops.message_passing_stack(plan, xs, ps, num_hops=hops, num_layers=3, num_mlp=2, act="silu", training=True,
+                                      drop_p=0.05, drop_seed=seed)
+        y0 = y.detach().clone()
+        torch.cuda.synchronize()
+        (y * w).sum().backward()
+        torch.cuda.synchronize()
+        os.environ.pop("AIMX_MLPS_RT", None)
+        runs.append((mode, rt, y0, xs.grad.clone(), [q.grad.clone() for q in ps]))
+        r0 = runs[0]
+        ey = ((y0 - r0[2]).norm() / r0[2].norm()).item()
+        ex = ((xs.grad - r0[3]).norm() / r0[3].norm()).item()
+        ep = max(((a - b).norm() / b.norm().clamp_min(1e-30)).item() for a, b in zip(runs[-1][4], r0[4]))
+        print(f"seq run {len(runs) - 1} mode={mode} rt={rt}: y {ey:.2e} dx {ex:.2e} dparams max {ep:.2e}", flush=True)
+        now, seg1 = state()
+        changed = [k for k in snap if not torch.equal(now[k], snap[k])]
+        nz = int((now["counters"] != 0).sum())
+        print(f"   changed since start: {changed}; nonzero counters {nz}; row_seg {seg0 == seg1}", flush=True)
+        if changed:
+            for k in changed:
+                dif = (now[k] != snap[k]).nonzero().flatten()
+                print(f"   {k}: {dif.numel()} elements differ, first at {dif[:8].tolist()}", flush=True)
+            snap = now
     worst = None
     for layers, nm in ((1, 1), (1, 2), (3, 2)):
         for train in (False, True):
