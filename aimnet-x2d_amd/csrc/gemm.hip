@@ -347,8 +347,11 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
         const uint32_t off = AK ? 4u * ((uint32_t)(m0 + mm) * sam + (uint32_t)(k0 + kk))
                                 : 4u * ((uint32_t)(m0 + mm) + (uint32_t)(k0 + kk) * sak);
         const floatx4 v = bload4(ra_, ok ? off : a_bytes, 0);
+        // k-contiguous float4s: a k end that is not a multiple of 4 (the zc trim at the empty hop
+        // chunks, zE = 2 D: 306 at c4) cuts one mid-vector, and the components past it are the
+        // next chunk's columns, which the stack's hop leaves unwritten (skip_tail)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ra[4 * i + e] = v[e];
+        for (int e = 0; e < 4; ++e) ra[4 * i + e] = (AK && k0 + kk + e >= kend) ? 0.f : v[e];
       }
 #pragma unroll
       for (int i = 0; i < NB4; ++i) {
@@ -363,7 +366,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const bool one = a.ones_col && kok && ((BKC ? n0 + nn : n0 + nn + e) == N - 1);
-          rb[4 * i + e] = one ? 1.f : v[e];
+          const bool kin = !BKC || k0 + kk + e < kend;  // as for A
+          rb[4 * i + e] = !kin ? 0.f : (one ? 1.f : v[e]);
         }
       }
       return;

@@ -39,7 +39,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) float gfloat;
 typedef __attribute__((address_space(1))) uint8_t gu8;
 
-constexpr int kRows = 8;      // molecules per workgroup
+constexpr int kRows = 8;      // molecules per workgroup (the most: head8_rows)
 constexpr int kWaves = 16;    // waves per workgroup
 constexpr int kNT = 64 * kWaves;
 constexpr int kRing = 4;      // B items (4 k each) in flight per wave
@@ -95,6 +95,7 @@ struct BStream8 {
 
 // This wave's share of one GEMM: rows 0-7 of A (LDS, row stride lda) times its B column group over
 // its k range, into acc0 (rows 0-3) / acc1 (rows 4-7) — lane l holds column 64 cg + l.
+template <int RW>
 __device__ __forceinline__ void gemm8(const float* A, int lda, int k0, int items, float (&ring)[kRing][4],
                                       BStream8& bs, floatx4& acc0, floatx4& acc1) {
   const int lane = threadIdx.x & 63;
@@ -107,11 +108,12 @@ __device__ __forceinline__ void gemm8(const float* A, int lda, int k0, int items
     for (int q = 0; q < kRing; ++q) {
       const int k = 4 * (i0 + q);
       const floatx4 x0 = *reinterpret_cast<const floatx4*>(a0 + k);
-      const floatx4 x1 = *reinterpret_cast<const floatx4*>(a1 + k);
+      floatx4 x1;
+      if (RW == 8) x1 = *reinterpret_cast<const floatx4*>(a1 + k);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         acc0 = __builtin_amdgcn_mfma_f32_4x4x1f32(x0[t], ring[q][t], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_4x4x1f32(x1[t], ring[q][t], acc1, 0, 0, 0);
+        if (RW == 8) acc1 = __builtin_amdgcn_mfma_f32_4x4x1f32(x1[t], ring[q][t], acc1, 0, 0, 0);
       }
       bs.next(ring[q]);  // refilled after its last read: the load reuses the registers
       __builtin_amdgcn_sched_barrier(0);
@@ -120,20 +122,22 @@ __device__ __forceinline__ void gemm8(const float* A, int lda, int k0, int items
 }
 
 // The wave's partial sums -> red[kq][row][col]
+template <int RW>
 __device__ __forceinline__ void put_partials(float* red, const Geo8& g, int kq, int col, const floatx4& acc0,
                                              const floatx4& acc1) {
-  float* p = red + (int64_t)kq * kRows * g.F + col;
+  float* p = red + (int64_t)kq * RW * g.F + col;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     p[r * g.F] = acc0[r];
-    p[(r + 4) * g.F] = acc1[r];
+    if (RW == 8) p[(r + 4) * g.F] = acc1[r];
   }
 }
 
 // sum over the k ranges in order
+template <int RW>
 __device__ __forceinline__ float sum_partials(const float* red, const Geo8& g, int r, int c) {
   float v = red[r * g.F + c];
-  for (int q = 1; q < g.ks; ++q) v += red[(int64_t)q * kRows * g.F + r * g.F + c];
+  for (int q = 1; q < g.ks; ++q) v += red[(int64_t)q * RW * g.F + r * g.F + c];
   return v;
 }
 
@@ -147,38 +151,40 @@ struct Lds8 {
 
 // + the operand pointer table (kMaxGemms pointers) at the end: every array lives in the dynamic
 // region (a static __shared__ ahead of it can shift its base off 16-byte alignment)
-__host__ __device__ inline size_t lds8_floats(const Geo8& g) {
-  return (size_t)2 * kRows * g.S + (size_t)kRows * g.S2 + (size_t)g.ks * kRows * g.F + 2 * kMaxGemms;
+__host__ __device__ inline size_t lds8_floats(const Geo8& g, int rw) {
+  return (size_t)2 * rw * g.S + (size_t)rw * g.S2 + (size_t)g.ks * rw * g.F + 2 * kMaxGemms;
 }
 
+template <int RW>
 __device__ __forceinline__ Lds8 carve8(float* lds, const Geo8& g) {
   Lds8 L;
   L.X = lds;
-  L.Hb = L.X + kRows * g.S;
-  L.Cb = L.Hb + kRows * g.S;
-  L.red = L.Cb + kRows * g.S2;
-  L.tab = reinterpret_cast<const gfloat**>(L.red + g.ks * kRows * g.F);
+  L.Hb = L.X + RW * g.S;
+  L.Cb = L.Hb + RW * g.S;
+  L.red = L.Cb + RW * g.S2;
+  L.tab = reinterpret_cast<const gfloat**>(L.red + g.ks * RW * g.F);
   return L;
 }
 
 // Forward operand table: GEMM order pp, (W1_i, W2_i) for each block, skip; each the row-major
 // [F][F] transpose of the nn.Linear weight (B(k, n) = W[n][k]) in the caller's workspace.
+template <int RW>
 __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float* __restrict__ wt) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = (int)h.F, T = (int)h.T, nb = h.nb;
   const Geo8 g = geo8(F);
-  const Lds8 L = carve8(lds, g);
+  const Lds8 L = carve8<RW>(lds, g);
   const gfloat** tab = L.tab;
   const int ng = 2 + 2 * nb;
   if (threadIdx.x < ng) tab[threadIdx.x] = (const gfloat*)(wt + (int64_t)threadIdx.x * F * F);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cg = wave % g.cgs, kq = wave / g.cgs;
-  const int64_t G = h.G, g0 = (int64_t)blockIdx.x * kRows;
+  const int64_t G = h.G, g0 = (int64_t)blockIdx.x * RW;
   const float scale = drop_scale8(h.drop_p);
   const bool drop = h.training && h.drop_p > 0.f && h.seed;
   const uint64_t seed = drop ? (uint64_t)*h.seed : 0;
   // x_pooled rows -> Cb[:, :F] (zero past G)
-  for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+  for (int e = threadIdx.x; e < RW * F; e += kNT) {
     const int r = e / F, c = e - r * F;
     L.Cb[r * g.S2 + c] = (g0 + r < G) ? ((const gfloat*)h.x0)[(g0 + r) * h.ldx0 + c] : 0.f;
   }
@@ -190,15 +196,15 @@ __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float
   floatx4 acc0, acc1;
   const int k0 = kq * 4 * g.items;
   auto gemm = [&](const float* A, int lda) __attribute__((always_inline)) {
-    gemm8(A, lda, k0, g.items, ring, bs, acc0, acc1);
-    put_partials(L.red, g, kq, 64 * cg + lane, acc0, acc1);
+    gemm8<RW>(A, lda, k0, g.items, ring, bs, acc0, acc1);
+    put_partials<RW>(L.red, g, kq, 64 * cg + lane, acc0, acc1);
     lds_sync8();
   };
   // y0 = x0 Wp^T + bp
   gemm(L.Cb, g.S2);
-  for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+  for (int e = threadIdx.x; e < RW * F; e += kNT) {
     const int r = e / F, c = e - r * F;
-    const float y = sum_partials(L.red, g, r, c) + ((const gfloat*)h.bp)[c];
+    const float y = sum_partials<RW>(L.red, g, r, c) + ((const gfloat*)h.bp)[c];
     L.X[r * g.S + c] = y;
     if (g0 + r < G) ((gfloat*)h.y0)[(g0 + r) * F + c] = y;
   }
@@ -211,10 +217,10 @@ __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float
       gfloat* Hs = (gfloat*)h.hid[i];
       gu8* M = (gu8*)h.mask[i];
       const gfloat* b1 = (const gfloat*)h.b1[i];
-      for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+      for (int e = threadIdx.x; e < RW * F; e += kNT) {
         const int r = e / F, c = e - r * F;
         const int64_t gr = g0 + r;
-        const float v = sum_partials(L.red, g, r, c) + b1[c];
+        const float v = sum_partials<RW>(L.red, g, r, c) + b1[c];
         float a = act_fwd(h.act, v);
         if (drop) {
           const bool keep = hash_uniform(seed, 0x4EADu + (uint32_t)i, (uint64_t)gr * (uint64_t)F + (uint64_t)c) >= h.drop_p;
@@ -235,9 +241,9 @@ __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float
       gfloat* Z = (gfloat*)h.z[i];
       const gfloat* b2 = (const gfloat*)h.b2[i];
       const bool skip = h.skip[i] != 0, last = i == nb - 1;
-      for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+      for (int e = threadIdx.x; e < RW * F; e += kNT) {
         const int r = e / F, c = e - r * F;
-        float z = sum_partials(L.red, g, r, c) + b2[c];
+        float z = sum_partials<RW>(L.red, g, r, c) + b2[c];
         if (skip) z += L.X[r * g.S + c];
         L.X[r * g.S + c] = z;
         if (last) L.Cb[r * g.S2 + c] = z;  // the z half of [z | s]
@@ -251,15 +257,15 @@ __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float
   }
   // s = z Ws^T + bs -> the s half of [z | s]
   gemm(L.X, g.S);
-  for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+  for (int e = threadIdx.x; e < RW * F; e += kNT) {
     const int r = e / F, c = e - r * F;
-    const float s = sum_partials(L.red, g, r, c) + ((const gfloat*)h.bs)[c];
+    const float s = sum_partials<RW>(L.red, g, r, c) + ((const gfloat*)h.bs)[c];
     L.Cb[r * g.S2 + F + c] = s;
     if (g0 + r < G) ((gfloat*)h.cat)[(g0 + r) * 2 * F + F + c] = s;
   }
   lds_sync8();
   // out = [z | s] Wo^T + bo: one wave per (row, task) dot product of length 2F
-  for (int p = wave; p < kRows * T; p += kWaves) {
+  for (int p = wave; p < RW * T; p += kWaves) {
     const int r = p / T, t = p - r * T;
     float acc = 0.f;
     const gfloat* wo = (const gfloat*)h.wo + (int64_t)t * 2 * F;
@@ -271,11 +277,12 @@ __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float
 
 // Input-gradient chain. Operands B(k, n) = W[k][n]: the weights themselves (row-major [F][F]),
 // GEMM order skip^T, (W2_i^T, W1_i^T) for blocks nb-1 .. 0, pp^T.
+template <int RW>
 __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxHeadGrad d) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = (int)h.F, T = (int)h.T, nb = h.nb;
   const Geo8 g = geo8(F);
-  const Lds8 L = carve8(lds, g);
+  const Lds8 L = carve8<RW>(lds, g);
   const gfloat** tab = L.tab;
   const int ng = 2 + 2 * nb;
   if (threadIdx.x == 0) {
@@ -288,13 +295,13 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cg = wave % g.cgs, kq = wave / g.cgs;
-  const int64_t G = h.G, g0 = (int64_t)blockIdx.x * kRows;
+  const int64_t G = h.G, g0 = (int64_t)blockIdx.x * RW;
   const float scale = drop_scale8(h.drop_p);
   const bool drop = h.training && h.drop_p > 0.f && h.seed;
   float* DZ = L.X;   // gradient w.r.t. the current block output
   float* DV = L.Hb;  // ds, then dv of each block
   // d[z | s] = d_out Wo (K = T): dz -> DZ, ds -> DV and HBM
-  for (int e = threadIdx.x; e < kRows * 2 * F; e += kNT) {
+  for (int e = threadIdx.x; e < RW * 2 * F; e += kNT) {
     const int r = e / (2 * F), n = e - r * 2 * F;
     float v = 0.f;
     if (g0 + r < G)
@@ -315,16 +322,16 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
   floatx4 acc0, acc1;
   const int k0 = kq * 4 * g.items;
   auto gemm = [&](const float* A) __attribute__((always_inline)) {
-    gemm8(A, g.S, k0, g.items, ring, bs, acc0, acc1);
-    put_partials(L.red, g, kq, 64 * cg + lane, acc0, acc1);
+    gemm8<RW>(A, g.S, k0, g.items, ring, bs, acc0, acc1);
+    put_partials<RW>(L.red, g, kq, 64 * cg + lane, acc0, acc1);
     lds_sync8();
   };
   const int last = nb - 1;
   // dz += ds Ws
   gemm(DV);
-  for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+  for (int e = threadIdx.x; e < RW * F; e += kNT) {
     const int r = e / F, c = e - r * F;
-    const float z = DZ[r * g.S + c] + sum_partials(L.red, g, r, c);
+    const float z = DZ[r * g.S + c] + sum_partials<RW>(L.red, g, r, c);
     DZ[r * g.S + c] = z;
     if (g0 + r < G) ((gfloat*)d.dz[last])[(g0 + r) * F + c] = z;
   }
@@ -336,13 +343,13 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
       const gfloat* V = (const gfloat*)h.v[i];
       const gu8* M = (const gu8*)h.mask[i];
       gfloat* DVg = (gfloat*)d.dv[i];
-      for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+      for (int e = threadIdx.x; e < RW * F; e += kNT) {
         const int r = e / F, c = e - r * F;
         const int64_t gr = g0 + r;
         float dv = 0.f;
         if (gr < G) {
           const float m = drop ? (M[gr * F + c] ? scale : 0.f) : 1.f;
-          dv = sum_partials(L.red, g, r, c) * m * act_grad(h.act, V[gr * F + c]);
+          dv = sum_partials<RW>(L.red, g, r, c) * m * act_grad(h.act, V[gr * F + c]);
           DVg[gr * F + c] = dv;
         }
         DV[r * g.S + c] = dv;
@@ -354,9 +361,9 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
     {
       const bool skip = h.skip[i] != 0;
       gfloat* dst = (gfloat*)(i > 0 ? d.dz[i - 1] : d.dy0);
-      for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+      for (int e = threadIdx.x; e < RW * F; e += kNT) {
         const int r = e / F, c = e - r * F;
-        float y = sum_partials(L.red, g, r, c);
+        float y = sum_partials<RW>(L.red, g, r, c);
         if (skip) y += DZ[r * g.S + c];
         DZ[r * g.S + c] = y;
         if (g0 + r < G) dst[(g0 + r) * F + c] = y;
@@ -366,9 +373,9 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
   }
   // d x_pooled = dy0 Wp
   gemm(DZ);
-  for (int e = threadIdx.x; e < kRows * F; e += kNT) {
+  for (int e = threadIdx.x; e < RW * F; e += kNT) {
     const int r = e / F, c = e - r * F;
-    if (g0 + r < G) ((gfloat*)d.d_x0)[(g0 + r) * d.ld_dx0 + c] = sum_partials(L.red, g, r, c);
+    if (g0 + r < G) ((gfloat*)d.d_x0)[(g0 + r) * d.ld_dx0 + c] = sum_partials<RW>(L.red, g, r, c);
   }
 }
 
@@ -387,35 +394,48 @@ bool head8_ok(const AimxHead* h) {
   // against 139 + 143 us for head.hip's clustered kernels, profiles/r04_c4_step_seq.txt)
   if (F < 128 || F > kMaxF8 || kWaves % (F / 64) || F % 64 || h->H_in != F || h->nb < 1 || h->nb > AIMX_HEAD_MAX_BLOCKS)
     return false;
-  return lds8_floats(geo8((int)F)) * sizeof(float) <= 156 * 1024;
+  return lds8_floats(geo8((int)F), kRows) * sizeof(float) <= 156 * 1024;
 }
 
 size_t head8_forward_workspace_floats(const AimxHead* h) { return (size_t)(2 + 2 * h->nb) * h->F * h->F; }
 
-// forward: W^T of every chain weight into the workspace (k_head_transpose, head.hip), then the chain
-int head8_forward(const AimxHead* h, float* wt, hipStream_t st) {
-  const int F = (int)h->F;
-  const Geo8 g = geo8(F);
-  const size_t lds = lds8_floats(g) * sizeof(float);
+namespace {
+// molecules per workgroup: 8 (two 4-row accumulators per wave), or 4 (AIMX_HEAD8_ROWS=4: one
+// accumulator, twice the workgroups; A/B)
+int head8_rows() {
+  static const int r = [] {
+    const char* e = getenv("AIMX_HEAD8_ROWS");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return r;
+}
+
+template <int RW>
+int head8_launch(const AimxHead* h, const float* wt, const AimxHeadGrad* d, hipStream_t st) {
   static const bool set = [] {
-    (void)hipFuncSetAttribute((const void*)k_head8_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_head8_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_head8_fwd<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_head8_bwd<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
     return true;
   }();
   (void)set;
-  const unsigned grid = (unsigned)cdiv(h->G, kRows);
-  hipLaunchKernelGGL(k_head8_fwd, dim3(grid), dim3(kNT), lds, st, *h, wt);
+  const size_t lds = lds8_floats(geo8((int)h->F), RW) * sizeof(float);
+  const unsigned grid = (unsigned)cdiv(h->G, RW);
+  if (d)
+    hipLaunchKernelGGL(k_head8_bwd<RW>, dim3(grid), dim3(kNT), lds, st, *h, *d);
+  else
+    hipLaunchKernelGGL(k_head8_fwd<RW>, dim3(grid), dim3(kNT), lds, st, *h, wt);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
+}  // namespace
+
+// forward: W^T of every chain weight into the workspace (k_head_transpose, head.hip), then the chain
+int head8_forward(const AimxHead* h, float* wt, hipStream_t st) {
+  return head8_rows() == 4 ? head8_launch<4>(h, wt, nullptr, st) : head8_launch<8>(h, wt, nullptr, st);
+}
 
 int head8_backward(const AimxHead* h, const AimxHeadGrad* d, hipStream_t st) {
-  const Geo8 g = geo8((int)h->F);
-  const size_t lds = lds8_floats(g) * sizeof(float);
-  const unsigned grid = (unsigned)cdiv(h->G, kRows);
-  hipLaunchKernelGGL(k_head8_bwd, dim3(grid), dim3(kNT), lds, st, *h, *d);
-  AIMX_CHECK_LAUNCH();
-  return AIMX_OK;
+  return head8_rows() == 4 ? head8_launch<4>(h, nullptr, d, st) : head8_launch<8>(h, nullptr, d, st);
 }
 
 }  // namespace aimx

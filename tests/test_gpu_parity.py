@@ -353,14 +353,17 @@ def test_gemm_unaligned_rows_and_bases(M, N, K, layout, off):
     assert err < 2e-6, err
 
 
+@pytest.mark.parametrize("d", [76, 153])
 @pytest.mark.parametrize("nonempty", [(True, False, False), (False, False, False), (True, True, False),
                                       (False, True, False), (True, False, True)])
-def test_gemm_empty_hop_chunk_trimming(nonempty):
+def test_gemm_empty_hop_chunk_trimming(nonempty, d):
     """zc_* trimming (the reference's all-zero hop chunks, layers.py:154): F = [x | c0 | c1 | c2]
     with the empty chunks zero. Forward (k loop stops at E) and weight gradient (zero tiles) equal
     the untrimmed products; the input gradient matches on every column < E and stores whole tiles
-    at n >= E as 0."""
-    n, d, h = 1500, 76, 3
+    at n >= E as 0. The trimmed GEMMs get F with NaN in the empty chunks (the stack's hop leaves
+    them unwritten): they must never read them — d = 153 puts E = 306 inside a 16-byte vector of
+    the 16-byte-staged path."""
+    n, h = 1500, 3
     K = d * (h + 1)
     counts = torch.zeros(h * n, dtype=torch.int32)
     for j, ne in enumerate(nonempty):
@@ -372,10 +375,12 @@ def test_gemm_empty_hop_chunk_trimming(nonempty):
     g = torch.Generator().manual_seed(5)
     F = torch.randn(n, K, generator=g)
     F[:, E:] = 0
+    Fnan = F.clone()
+    Fnan[:, E:] = float("nan")
     zc = lambda dim: (rowptr, n, h, d, dim)  # noqa: E731
     W = torch.randn(2 * d, K, generator=g)
     full, _, _, ref, _ = _gemm(n, 2 * d, K, "NT", A=F, B=W)
-    trim, _, _, _, _ = _gemm(n, 2 * d, K, "NT", A=F, B=W, zc=zc(0))
+    trim, _, _, _, _ = _gemm(n, 2 * d, K, "NT", A=Fnan, B=W, zc=zc(0))
     assert torch.equal(full, trim)
     assert (trim.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
     dUG = torch.randn(n, 2 * d, generator=g)  # dF = dUG W
@@ -386,7 +391,7 @@ def test_gemm_empty_hop_chunk_trimming(nonempty):
     assert not trim[:, past:].any()
     dY = torch.randn(n, 2 * d, generator=g)  # dW = dY^T F (+ bias column)
     full, fcol, _, ref, _ = _gemm(2 * d, K, n, "TN", A=dY, B=F, ones=True)
-    trim, tcol, _, _, _ = _gemm(2 * d, K, n, "TN", A=dY, B=F, ones=True, zc=zc(1))
+    trim, tcol, _, _, _ = _gemm(2 * d, K, n, "TN", A=dY, B=Fnan, ones=True, zc=zc(1))
     assert torch.equal(full, trim) and torch.equal(fcol, tcol)
     assert not trim[:, E:].any()
 

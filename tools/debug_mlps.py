@@ -58,13 +58,14 @@ def main():
 
     def state():
         d = {"x": x, "w": w, "fwd.rowptr": plan.fwd.rowptr, "fwd.col": plan.fwd.col, "bwd.rowptr": plan.bwd.rowptr,
-             "bwd.col": plan.bwd.col, "counters": _lib.counters(dev), "batch": plan._keep[-1]}
+             "bwd.col": plan.bwd.col, "counters": _lib.counters(dev), "batch": plan._keep[-1], "seed": seed}
         seg = plan.row_seg()
         d.update({f"param{i}": p for i, p in enumerate(params)})
         return {k: v.detach().clone() for k, v in d.items()}, seg
 
     snap, seg0 = state()
-    for mode, rt in (("0", None), ("1", None), ("0", None), ("1", "1"), ("0", None), ("1", None)):
+    for mode, rt in (("0", None), ("0", None), ("0", None), ("1", None), ("0", None), ("1", "1"), ("0", None),
+                     ("1", None)):
         os.environ["AIMX_MLPS"] = mode
         if rt:
             os.environ["AIMX_MLPS_RT"] = rt
