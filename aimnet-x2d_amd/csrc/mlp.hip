@@ -678,7 +678,13 @@ struct BStream {
   }
 };
 
-// The k group loop of one GEMM of the chain (G groups from ring slot 0), keeping the ring P ahead.
+// The k group loop of one GEMM of the chain (G groups from ring slot 0), keeping the ring P ahead
+// inside the GEMM. The last P groups load nothing: the next GEMM's first P items are loaded by the
+// caller after this GEMM's epilogue (mlps_refill), so that at every wait for a ring slot the only
+// newer vector-memory operations are ring loads. (With the refills crossing into the next GEMM,
+// the epilogue's ~3 x 4 RT NF global stores came after them; vmcnt counts stores too, the
+// counter's range was exceeded, and hipcc waited for vmcnt(0) at every loop head: at c4 / c5 the
+// whole ring drained every P groups.)
 template <int RT, int NF, int P>
 __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring)[P][NF], BStream<NF>& bs, const float* As,
                                           int S, int G) {
@@ -686,16 +692,35 @@ __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int i = 0; i < NF; ++i) acc[t][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int g0 = 0; g0 < G; g0 += P) {
+  for (int g0 = 0; g0 < G - P; g0 += P) {
 #pragma unroll
     for (int q = 0; q < P; ++q) {
       mlps_group<RT, NF>(acc, As, S, g0 + q, ring[q]);
       // refill the slot only after its MFMAs have read it: the load then targets the same registers
       // (a refill issued before the last read needs fresh registers and a copy at the loop's back
-      // edge, and copying a register with a load in flight waits for that load: vmcnt(0))
+      // edge, and copying a register with a load in flight waits for that load)
       bs.next(ring[q]);
       __builtin_amdgcn_sched_barrier(0);
     }
+  }
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    mlps_group<RT, NF>(acc, As, S, G - P + q, ring[q]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The next GEMM's first P items (clamped re-reads of the last item after the chain's end), issued
+// after an epilogue's global stores (see mlps_gemm).
+// The loads are pinned in slot order: hipcc would otherwise schedule them freely, and where a
+// GEMM is entered from two paths whose slots were filled in different orders (the preload and a
+// refill) it can only wait for all of them (vmcnt(0)) before the first MFMA.
+template <int NF, int P>
+__device__ __forceinline__ void mlps_refill(floatx4 (&ring)[P][NF], BStream<NF>& bs) {
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    bs.next(ring[q]);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -749,8 +774,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
     BStream<NF> bs;
     bs.init(img, fr, nph * G);
     floatx4 ring[P][NF];
-#pragma unroll
-    for (int q = 0; q < P; ++q) bs.next(ring[q]);
+    mlps_refill<NF, P>(ring, bs);
     floatx4 acc[RT][NF];
     for (int ph = 0; ph < nph; ++ph) {
       // an opaque per-GEMM copy of the chunk origin: every epilogue address derives from it, so the
@@ -846,6 +870,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
             }
           }
       }
+      mlps_refill<NF, P>(ring, bs);
       lds_sync();  // hand the tile to the next GEMM
     }
   }
@@ -883,8 +908,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
     BStream<NF> bs;
     bs.init(img, fr, nph * G);
     floatx4 ring[P][NF];
-#pragma unroll
-    for (int q = 0; q < P; ++q) bs.next(ring[q]);
+    mlps_refill<NF, P>(ring, bs);
     floatx4 acc[RT][NF];
     for (int ph = 0; ph < nph; ++ph) {
       int64_t r0 = r0c;  // opaque per GEMM (see k_mlps_fwd)
@@ -964,6 +988,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
             }
           }
       }
+      mlps_refill<NF, P>(ring, bs);
       lds_sync();
     }
   }
