@@ -1025,7 +1025,10 @@ struct WbTable {
 // DB: two LDS buffers per operand (80-wide blocks only: 40 KiB, four workgroups fill a CU's
 // 160 KiB). Fill s + 1 is written to the idle buffer while fill s computes from the other, so each
 // fill costs one workgroup barrier instead of two and the LDS writes overlap other waves' MFMAs.
-template <int BB, bool DB>
+// VM: the operands' staging, 1 = 16-byte loads for every problem of the launch, 0 = dword loads for
+// every problem, 2 = per problem (WbTable.v4). With a per-problem branch inside each fetch the
+// paths into the fill loop's head carry different load counts and hipcc waits for all loads there.
+template <int BB, bool DB, int VM>
 __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
   using G = WbGeom<BB>;
   constexpr int kWbF = G::F, kWbT = G::T, kWbV = G::V, kLd = G::S;
@@ -1084,11 +1087,14 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(pr.dY, ab);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(pr.X, bb);
   const uint32_t lda = (uint32_t)pr.ld_dy, ldb = (uint32_t)pr.ld_x;
-  const bool v4 = t.v4[q] != 0;
+  const bool v4 = VM == 2 ? t.v4[q] != 0 : VM == 1;
 
-  // rows k0.. of both operands -> registers. Invalid rows/columns read 0 (address moved past the
-  // descriptor's extent, or a component select for a float4 straddling the edge); X's implicit
-  // ones column (the bias gradient) reads 1 on valid rows.
+  // rows k0.. of both operands -> registers: loads only, every validity test an ADDRESS select
+  // (rows past kend and float4s wholly past the column limit point past the descriptor's extent
+  // and read 0). A value select here — zeroing the components of a float4 that straddles the limit,
+  // or writing X's implicit ones column — made hipcc wait for each load right after issuing it
+  // (a branch per load: cdna_hip_programming.md §5 trap (c)), so no fill was ever in flight during
+  // the compute; those selects run in put, where the data is needed anyway.
   auto fetch = [&](int k0, floatx4 (&stage)[kWbV]) {
 #pragma unroll
     for (int u = 0; u < kWbV; ++u) {
@@ -1103,18 +1109,10 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
       floatx4 v;
       if (v4) {
         v = bload4(r, kok && col < lim ? 4u * ((uint32_t)k * ld + (uint32_t)col) : bytes, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (col + i >= lim) v[i] = 0.f;
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           v[i] = bload(r, kok && col + i < lim ? 4u * ((uint32_t)k * ld + (uint32_t)(col + i)) : bytes, 0);
-      }
-      if (isb && ones) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (kok && col + i == Nreal) v[i] = 1.f;
       }
       stage[u] = v;
     }
@@ -1124,13 +1122,23 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
 #pragma unroll
   for (int j = 0; j < kWbF; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   floatx4 ring[kWbD][kWbV];
-  // fill in registers -> LDS buffer (sa, sb)
-  auto put = [&](const floatx4(&stage)[kWbV], float* sa, float* sb) {
+  // fill (rows k0..) in registers -> LDS buffer (sa, sb): components of a float4 straddling the
+  // column limit are zeroed, X's implicit ones column (the bias gradient) reads 1 on valid rows
+  auto put = [&](const floatx4(&stage)[kWbV], int k0, float* sa, float* sb) {
 #pragma unroll
     for (int u = 0; u < kWbV; ++u) {
       const bool isb = u >= kWbV / 2;
       const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
-      *reinterpret_cast<floatx4*>((isb ? sb : sa) + (f / (BB / 4)) * kLd + 4 * (f % (BB / 4))) = stage[u];
+      const int row = f / (BB / 4), c = 4 * (f % (BB / 4));
+      const int col = (isb ? n0 : m0) + c, lim = isb ? zlim : M;
+      const bool kok = k0 + row < kend;
+      floatx4 v = stage[u];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (v4 && col + i >= lim) v[i] = 0.f;
+        if (isb && ones && kok && col + i == Nreal) v[i] = 1.f;
+      }
+      *reinterpret_cast<floatx4*>((isb ? sb : sa) + row * kLd + c) = v;
     }
   };
   // the kWbK k rows staged in (sa, sb) into this wave's accumulators
@@ -1171,28 +1179,30 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
   };
 #pragma unroll
   for (int d = 0; d < kWbD; ++d)
-    if (d < nsub) fetch(kb + d * kWbK, ring[d]);
+    fetch(kb + d * kWbK, ring[d]);
   if constexpr (DB) {
     static_assert(kWbD == 2, "the double-buffered schedule keeps two fills in registers");
     // fill s computes from buffer s & 1; fill s + 1 (loaded two compute periods earlier) goes to
     // the other buffer first, and its register slot is refilled with fill s + 3
-    if (nsub > 0) {
-      put(ring[0], sA, sB);
-      if (2 < nsub) fetch(kb + 2 * kWbK, ring[0]);
-    }
+    put(ring[0], kb, sA, sB);
+    fetch(kb + 2 * kWbK, ring[0]);
     __syncthreads();
+    // put and fetch run unconditionally (fills past the slice are zeros, put into the idle
+    // buffer): with them under a condition, the paths into the loop head differ in their pending
+    // loads and hipcc waits for all of them there (vmcnt(0)), ending every fill's prefetch
+    // (sched_barrier: the fills' loads issue before the compute; hipcc would sink them below it)
     for (int s0 = 0; s0 < nsub; s0 += 2) {
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const int s = s0 + d;
-        if (s >= nsub) break;
-        if (s + 1 < nsub) {
-          put(ring[d ^ 1], sA + (d ^ 1) * kBuf, sB + (d ^ 1) * kBuf);
-          if (s + 3 < nsub) fetch(kb + (s + 3) * kWbK, ring[d ^ 1]);
-        }
-        compute(sA + d * kBuf, sB + d * kBuf);
-        __syncthreads();  // fill s + 1 visible; every read of buffer d done before it is refilled
-      }
+      put(ring[1], kb + (s0 + 1) * kWbK, sA + kBuf, sB + kBuf);
+      fetch(kb + (s0 + 3) * kWbK, ring[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(sA, sB);
+      __syncthreads();  // fill s0 + 1 visible; every read of buffer 0 done before it is refilled
+      if (s0 + 1 >= nsub) break;
+      put(ring[0], kb + (s0 + 2) * kWbK, sA, sB);
+      fetch(kb + (s0 + 4) * kWbK, ring[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(sA + kBuf, sB + kBuf);
+      __syncthreads();
     }
   } else {
     // kWbD fills in flight: fill s lands in register slot s % kWbD, is copied to LDS kWbD - 1
@@ -1203,7 +1213,7 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
         const int s = s0 + d;
         if (s >= nsub) break;
         __syncthreads();  // the previous rows' MFMA reads are done
-        put(ring[d], sA, sB);
+        put(ring[d], kb + s * kWbK, sA, sB);
         __syncthreads();
         if (s + kWbD < nsub) fetch(kb + (s + kWbD) * kWbK, ring[d]);
         compute(sA, sB);
@@ -1643,15 +1653,19 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
           const char* e = getenv("AIMX_WGRAD_DBUF");
           return !(e && atoi(e) == 0);
         }();
+        int nv4 = 0;
+        for (int k = 0; k < tb.n; ++k) nv4 += tb.v4[k] != 0;
+        const int vm = nv4 == tb.n ? 1 : (nv4 == 0 ? 0 : 2);
+        using WbFn = void (*)(const WbTable, float*, int32_t*);
+        WbFn fn;
         if (wide)
-          hipLaunchKernelGGL((k_wgrad_lds<160, false>), dim3((unsigned)blkb), dim3(WbGeom<160>::T), 0,
-                             (hipStream_t)stream, tb, (float*)workspace, counters);
+          fn = vm == 1 ? k_wgrad_lds<160, false, 1> : (vm == 0 ? k_wgrad_lds<160, false, 0> : k_wgrad_lds<160, false, 2>);
         else if (dbuf)
-          hipLaunchKernelGGL((k_wgrad_lds<80, true>), dim3((unsigned)blkb), dim3(WbGeom<80>::T), 0,
-                             (hipStream_t)stream, tb, (float*)workspace, counters);
+          fn = vm == 1 ? k_wgrad_lds<80, true, 1> : (vm == 0 ? k_wgrad_lds<80, true, 0> : k_wgrad_lds<80, true, 2>);
         else
-          hipLaunchKernelGGL((k_wgrad_lds<80, false>), dim3((unsigned)blkb), dim3(WbGeom<80>::T), 0,
-                             (hipStream_t)stream, tb, (float*)workspace, counters);
+          fn = vm == 1 ? k_wgrad_lds<80, false, 1> : (vm == 0 ? k_wgrad_lds<80, false, 0> : k_wgrad_lds<80, false, 2>);
+        hipLaunchKernelGGL(fn, dim3((unsigned)blkb), dim3(wide ? WbGeom<160>::T : WbGeom<80>::T), 0, (hipStream_t)stream,
+                           tb, (float*)workspace, counters);
       }
       tb = WbTable{};
       blkb = 0;
