@@ -347,11 +347,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
         const uint32_t off = AK ? 4u * ((uint32_t)(m0 + mm) * sam + (uint32_t)(k0 + kk))
                                 : 4u * ((uint32_t)(m0 + mm) + (uint32_t)(k0 + kk) * sak);
         const floatx4 v = bload4(ra_, ok ? off : a_bytes, 0);
-        // k-contiguous float4s: a k end that is not a multiple of 4 (the zc trim at the empty hop
-        // chunks, zE = 2 D: 306 at c4) cuts one mid-vector, and the components past it are the
-        // next chunk's columns, which the stack's hop leaves unwritten (skip_tail)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ra[4 * i + e] = (AK && k0 + kk + e >= kend) ? 0.f : v[e];
+        for (int e = 0; e < 4; ++e) ra[4 * i + e] = v[e];
       }
 #pragma unroll
       for (int i = 0; i < NB4; ++i) {
@@ -364,11 +361,7 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
                                  : 4u * ((uint32_t)(n0 + nn) + (uint32_t)(k0 + kk) * sbk);
         const floatx4 v = bload4(rb_, ok ? off : b_bytes, 0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bool one = a.ones_col && kok && ((BKC ? n0 + nn : n0 + nn + e) == N - 1);
-          const bool kin = !BKC || k0 + kk + e < kend;  // as for A
-          rb[4 * i + e] = !kin ? 0.f : (one ? 1.f : v[e]);
-        }
+        for (int e = 0; e < 4; ++e) rb[4 * i + e] = v[e];
       }
       return;
     }
@@ -377,46 +370,86 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     if constexpr (VUA) {
     } else if (AK) {
       const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) * sam + (uint32_t)(k0 + a_k));
-      const bool kok = !tail || (k0 + a_k < kend);
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const float v = bload(ra_, voff, 4u * (uint32_t)(i * A_STEP) * sam);
-        ra[i] = kok ? v : 0.f;
+        ra[i] = bload(ra_, voff, 4u * (uint32_t)(i * A_STEP) * sam);
       }
     } else {
       const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) + (uint32_t)(k0 + a_k) * sak);
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const float v = bload(ra_, voff, 4u * (uint32_t)(i * A_STEP) * sak);
-        const bool ok = a_m_ok && (!tail || (k0 + a_k + i * A_STEP < kend));
-        ra[i] = ok ? v : 0.f;
+        ra[i] = bload(ra_, voff, 4u * (uint32_t)(i * A_STEP) * sak);
       }
     }
     // B
     if constexpr (VUB) {
     } else if (BKC) {
       const uint32_t voff = 4u * ((uint32_t)(n0 + b_n) * sbn + (uint32_t)(k0 + b_k));
-      const bool kok = !tail || (k0 + b_k < kend);
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const float v = bload(rb_, voff, 4u * (uint32_t)(i * B_STEP) * sbn);
-        const int n = n0 + b_n + i * B_STEP;
-        const bool one = a.ones_col && (n == N - 1);
-        rb[i] = kok ? (one ? 1.f : v) : 0.f;
+        rb[i] = bload(rb_, voff, 4u * (uint32_t)(i * B_STEP) * sbn);
       }
     } else {
       const uint32_t voff = 4u * ((uint32_t)(n0 + b_n) + (uint32_t)(k0 + b_k) * sbk);
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const float v = bload(rb_, voff, 4u * (uint32_t)(i * B_STEP) * sbk);
-        const bool kok = !tail || (k0 + b_k + i * B_STEP < kend);
-        rb[i] = kok ? (b_n_one ? 1.f : (b_n_ok ? v : 0.f)) : 0.f;
+        rb[i] = bload(rb_, voff, 4u * (uint32_t)(i * B_STEP) * sbk);
       }
     }
   };
+  // The validity selects on loaded values (rows / k past the slice's end, the ones column, k past
+  // a trimmed kend inside a k-contiguous float4 — zc: 2 D = 306 at c4, where the unwritten next
+  // hop chunk begins) are made here, where the data is needed anyway: in load_slice hipcc placed
+  // them right after the loads and waited for each load at issue.
   auto store_slice = [&](const Regs& R, int stage) {
-    const float(&ra)[VUA ? 1 : NA] = R.a;
-    const float(&rb)[VUB ? 1 : NB] = R.b;
+    float ra[VUA ? 1 : NA], rb[VUB ? 1 : NB];
+    {
+      const int k0 = R.k0;
+      const bool tail = k0 + BK > kend;
+      if constexpr (V4) {
+#pragma unroll
+        for (int i = 0; i < NA4; ++i) {
+          const int q = tid + i * 256;
+          const int kk = AK ? (q % (BK / 4)) * 4 : q / (BM / 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ra[4 * i + e] = (AK && k0 + kk + e >= kend) ? 0.f : R.a[4 * i + e];
+        }
+#pragma unroll
+        for (int i = 0; i < NB4; ++i) {
+          const int q = tid + i * 256;
+          const int nn = BKC ? q / (BK / 4) : (q % (BN / 4)) * 4;
+          const int kk = BKC ? (q % (BK / 4)) * 4 : q / (BN / 4);
+          const bool kok = k0 + kk < kend;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool one = a.ones_col && kok && ((BKC ? n0 + nn : n0 + nn + e) == N - 1);
+            const bool kin = !BKC || k0 + kk + e < kend;
+            rb[4 * i + e] = !kin ? 0.f : (one ? 1.f : R.b[4 * i + e]);
+          }
+        }
+      } else {
+        if constexpr (!VUA) {
+#pragma unroll
+          for (int i = 0; i < NA; ++i) {
+            const bool ok = AK ? (!tail || k0 + a_k < kend) : (a_m_ok && (!tail || k0 + a_k + i * A_STEP < kend));
+            ra[i] = ok ? R.a[i] : 0.f;
+          }
+        }
+        if constexpr (!VUB) {
+#pragma unroll
+          for (int i = 0; i < NB; ++i) {
+            if (BKC) {
+              const bool kok = !tail || k0 + b_k < kend;
+              const bool one = a.ones_col && (n0 + b_n + i * B_STEP == N - 1);
+              rb[i] = kok ? (one ? 1.f : R.b[i]) : 0.f;
+            } else {
+              const bool kok = !tail || k0 + b_k + i * B_STEP < kend;
+              rb[i] = kok ? (b_n_one ? 1.f : (b_n_ok ? R.b[i] : 0.f)) : 0.f;
+            }
+          }
+        }
+      }
+    }
     if constexpr (VU) {
       float* As = smem + stage * (LA + LB);
       float* Bs = As + LA;
@@ -627,8 +660,11 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   if (nsl > 1) load_slice(kbeg + BK, kbeg + 2 * BK > kend, r1);
   if (nsl > 0) store_slice(r0, 0);
   __syncthreads();
+  // The loads run unconditionally (a slice past the end is never stored): under a condition, the
+  // two paths into the next wait carry different pending loads and hipcc waits for all of them
+  // (vmcnt(0)) before each store_slice, including the slice issued just before the compute.
   for (int sl = 0; sl < nsl; sl += 2) {
-    if (sl + 2 < nsl) {
+    {
       const int k2 = kbeg + (sl + 2) * BK;
       load_slice(k2, k2 + BK > kend, r0);
     }
@@ -636,7 +672,7 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     if (sl + 1 < nsl) store_slice(r1, 1);
     __syncthreads();
     if (sl + 1 >= nsl) break;
-    if (sl + 3 < nsl) {
+    {
       const int k3 = kbeg + (sl + 3) * BK;
       load_slice(k3, k3 + BK > kend, r1);
     }
