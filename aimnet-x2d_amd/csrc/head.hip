@@ -621,40 +621,12 @@ extern "C" size_t aimx_head_forward_workspace_bytes(const AimxHead* h) {
   return sizeof(float) * head8_forward_workspace_floats(h);
 }
 
-// The chain weights' transposes into the forward workspace (the 8-molecule kernels' B operands):
-// [F][F] each, in chain order pp, (W1_i, W2_i), skip.
-static int head8_transpose(const AimxHead* h, float* wt, hipStream_t st) {
-  TrTable t{};
-  const int F = (int)h->F;
-  auto add = [&](const float* src) {
-    const int q = t.n++;
-    t.src[q] = src;
-    t.dst[q] = wt + (int64_t)q * F * F;
-    t.rows[q] = F;
-    t.cols[q] = F;
-    t.ldd[q] = F;
-    t.blk0[q + 1] = t.blk0[q] + (int)(cdiv(F, 32) * cdiv(F, 32));
-  };
-  add(h->wp);
-  for (int i = 0; i < h->nb; ++i) {
-    add(h->w1[i]);
-    add(h->w2[i]);
-  }
-  add(h->ws);
-  hipLaunchKernelGGL(k_head_transpose, dim3((unsigned)t.blk0[t.n]), dim3(256), 0, st, t);
-  AIMX_CHECK_LAUNCH();
-  return AIMX_OK;
-}
-
 extern "C" int aimx_head_forward(const AimxHead* h, aimx_stream_t stream) {
   if (!head_valid(h)) return AIMX_EARG;
   if (h->G == 0) return AIMX_OK;
   if (head8_ok(h) && h->fwd_ws && h->fwd_ws_bytes >= aimx_head_forward_workspace_bytes(h) &&
-      ((uintptr_t)h->fwd_ws & 15) == 0) {
-    const int r = head8_transpose(h, h->fwd_ws, (hipStream_t)stream);
-    if (r != AIMX_OK) return r;
+      ((uintptr_t)h->fwd_ws & 15) == 0)
     return head8_forward(h, h->fwd_ws, (hipStream_t)stream);
-  }
   const HeadLaunch L = head_launch(h);
   switch (L.waves) {
     case 4: hipLaunchKernelGGL(k_head_fwd<4>, dim3(L.grid), dim3(256), 0, (hipStream_t)stream, *h); break;
@@ -673,7 +645,9 @@ extern "C" int aimx_head_trace_read(long long* out) {
 
 extern "C" size_t aimx_head_backward_workspace_bytes(const AimxHead* h) {
   if (!head_valid(h)) return 0;
-  return sizeof(float) * (size_t)head_ws(h->F, h->H_in, h->T, h->nb).total;
+  // the 16-molecule kernels' transposes, or the 8-molecule kernels' packed images (head8.hip)
+  const size_t t = (size_t)head_ws(h->F, h->H_in, h->T, h->nb).total;
+  return sizeof(float) * (head8_ok(h) ? std::max(t, head8_forward_workspace_floats(h)) : t);
 }
 
 extern "C" int aimx_head_backward(const AimxHead* h, const AimxHeadGrad* d, aimx_stream_t stream) {
@@ -684,7 +658,7 @@ extern "C" int aimx_head_backward(const AimxHead* h, const AimxHeadGrad* d, aimx
   for (int i = 0; i < h->nb; ++i)
     if (!d->dz[i] || !d->dv[i]) return AIMX_EARG;
   if (h->G == 0) return AIMX_OK;
-  if (head8_ok(h)) return head8_backward(h, d, (hipStream_t)stream);  // reads the weights as they are
+  if (head8_ok(h)) return head8_backward(h, d, (hipStream_t)stream);  // packs W into the workspace
   // transposed weight copies (one launch for all of them)
   const HeadWs L = head_ws(h->F, h->H_in, h->T, h->nb);
   float* wt = (float*)d->workspace;

@@ -18,10 +18,11 @@
 //
 // 16 waves: wave w takes column group w % (F/64) and k range w / (F/64) of every GEMM (F / 64
 // groups x 16 / (F / 64) k ranges), so each wave's operand stream is small and 16 streams keep
-// enough loads in flight. B(k, n) for 4 consecutive k comes as 4 coalesced dword loads (rows k..k+3
-// of a row-major [K][N] operand: the forward's W^T, transposed once per call into the caller's
-// workspace by k_head_transpose; the backward's W itself), held P items ahead in a register ring
-// that runs across GEMM boundaries (the weights do not depend on the activations). The k-range
+// enough loads in flight. B(k, n) for 4 consecutive k comes as ONE 16-byte load per lane from a
+// k4-interleaved image (k_head8_pack, once per call per direction: the forward's W^T into the
+// forward workspace, the backward's W into the backward workspace), held up to 8 items ahead in
+// a register ring that runs across GEMM boundaries (the weights do not depend on the
+// activations; 4 dword loads per item and a 4-item ring left the stream latency-bound). The k-range
 // partial sums meet in LDS and every thread finishes two or four outputs: the fixed-order sum, the
 // epilogue (bias, activation with the saved pre-activation, the dropout hash and mask, the block
 // skip, the [z | s] concat) and the stores the weight gradients need. The barriers wait on LDS
@@ -42,7 +43,7 @@ typedef __attribute__((address_space(1))) uint8_t gu8;
 constexpr int kRows = 8;      // molecules per workgroup (the most: head8_rows)
 constexpr int kWaves = 16;    // waves per workgroup
 constexpr int kNT = 64 * kWaves;
-constexpr int kRing = 4;      // B items (4 k each) in flight per wave
+constexpr int kRingMax = 8;   // B items (4 k each) in flight per wave (fewer when a GEMM has fewer)
 constexpr int kMaxF8 = 256;   // widest F (see head8_ok)
 constexpr int kMaxGemms = 2 * AIMX_HEAD_MAX_BLOCKS + 2;
 
@@ -73,19 +74,19 @@ __host__ __device__ inline Geo8 geo8(int F) {
   return g;
 }
 
-// One wave's operand stream over the chain: GEMM j's B is row-major [F][F] at B[j]; the wave reads
-// rows 4 i .. 4 i + 3 (its k range) of columns 64 cg + lane. Item s of the stream is item s % items
-// of GEMM s / items; past the end it re-reads the last item (never used).
+// One wave's operand stream over the chain. GEMM j's B is a k4-interleaved image at tab[j]
+// (head8_pack: B(k, n) at ((k / 4) * F + n) * 4 + k % 4), so the wave's 4 k rows of column
+// 64 cg + lane are ONE 16-byte load per lane, 1 KiB per wave contiguous. Item s of the stream is
+// item s % items of GEMM s / items; past the end it re-reads the last item (never used).
 struct BStream8 {
-  const gfloat* const* tab;  // per GEMM operand base (LDS table of global pointers)
+  const gfloat* const* tab;  // per GEMM image base (LDS table of global pointers)
   int n, items, F, k0;       // GEMMs, items per GEMM, row length, first k of the wave's range
   int col;                   // 64 cg + lane
   int j, i;                  // cursor: GEMM, item
-  __device__ __forceinline__ void next(float (&r)[4]) {
+  __device__ __forceinline__ void next(floatx4& r) {
     const bool in = j < n;
-    const gfloat* b = tab[in ? j : n - 1] + (int64_t)(k0 + 4 * (in ? i : items - 1)) * F + col;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) r[t] = b[(int64_t)t * F];
+    const gfloat* b = tab[in ? j : n - 1] + ((int64_t)(k0 / 4 + (in ? i : items - 1)) * F + col) * 4;
+    r = *reinterpret_cast<const __attribute__((address_space(1))) floatx4*>(b);
     if (++i == items) {
       i = 0;
       ++j;
@@ -95,17 +96,17 @@ struct BStream8 {
 
 // This wave's share of one GEMM: rows 0-7 of A (LDS, row stride lda) times its B column group over
 // its k range, into acc0 (rows 0-3) / acc1 (rows 4-7) — lane l holds column 64 cg + l.
-template <int RW>
-__device__ __forceinline__ void gemm8(const float* A, int lda, int k0, int items, float (&ring)[kRing][4],
+template <int RW, int RG>
+__device__ __forceinline__ void gemm8(const float* A, int lda, int k0, int items, floatx4 (&ring)[RG],
                                       BStream8& bs, floatx4& acc0, floatx4& acc1) {
   const int lane = threadIdx.x & 63;
   const float* a0 = A + (lane & 3) * lda + k0;
   const float* a1 = a0 + 4 * lda;
   acc0 = floatx4{0.f, 0.f, 0.f, 0.f};
   acc1 = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int i0 = 0; i0 < items; i0 += kRing) {
+  for (int i0 = 0; i0 < items; i0 += RG) {
 #pragma unroll
-    for (int q = 0; q < kRing; ++q) {
+    for (int q = 0; q < RG; ++q) {
       const int k = 4 * (i0 + q);
       const floatx4 x0 = *reinterpret_cast<const floatx4*>(a0 + k);
       floatx4 x1;
@@ -168,7 +169,7 @@ __device__ __forceinline__ Lds8 carve8(float* lds, const Geo8& g) {
 
 // Forward operand table: GEMM order pp, (W1_i, W2_i) for each block, skip; each the row-major
 // [F][F] transpose of the nn.Linear weight (B(k, n) = W[n][k]) in the caller's workspace.
-template <int RW>
+template <int RW, int RG>
 __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float* __restrict__ wt) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = (int)h.F, T = (int)h.T, nb = h.nb;
@@ -190,13 +191,16 @@ __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float
   }
   __syncthreads();
   BStream8 bs{tab, ng, g.items, F, kq * 4 * g.items, 64 * cg + lane, 0, 0};
-  float ring[kRing][4];
+  floatx4 ring[RG];
 #pragma unroll
-  for (int q = 0; q < kRing; ++q) bs.next(ring[q]);
+  for (int q = 0; q < RG; ++q) {
+    bs.next(ring[q]);
+    __builtin_amdgcn_sched_barrier(0);  // in slot order (see mlp.hip mlps_refill)
+  }
   floatx4 acc0, acc1;
   const int k0 = kq * 4 * g.items;
   auto gemm = [&](const float* A, int lda) __attribute__((always_inline)) {
-    gemm8<RW>(A, lda, k0, g.items, ring, bs, acc0, acc1);
+    gemm8<RW, RG>(A, lda, k0, g.items, ring, bs, acc0, acc1);
     put_partials<RW>(L.red, g, kq, 64 * cg + lane, acc0, acc1);
     lds_sync8();
   };
@@ -277,22 +281,15 @@ __global__ __launch_bounds__(kNT) void k_head8_fwd(const AimxHead h, const float
 
 // Input-gradient chain. Operands B(k, n) = W[k][n]: the weights themselves (row-major [F][F]),
 // GEMM order skip^T, (W2_i^T, W1_i^T) for blocks nb-1 .. 0, pp^T.
-template <int RW>
-__global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxHeadGrad d) {
+template <int RW, int RG>
+__global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxHeadGrad d, const float* __restrict__ wt) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int F = (int)h.F, T = (int)h.T, nb = h.nb;
   const Geo8 g = geo8(F);
   const Lds8 L = carve8<RW>(lds, g);
   const gfloat** tab = L.tab;
   const int ng = 2 + 2 * nb;
-  if (threadIdx.x == 0) {
-    tab[0] = (const gfloat*)h.ws;
-    for (int i = nb - 1, j = 1; i >= 0; --i, j += 2) {
-      tab[j] = (const gfloat*)h.w2[i];
-      tab[j + 1] = (const gfloat*)h.w1[i];
-    }
-    tab[ng - 1] = (const gfloat*)h.wp;
-  }
+  if (threadIdx.x < ng) tab[threadIdx.x] = (const gfloat*)(wt + (int64_t)threadIdx.x * F * F);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cg = wave % g.cgs, kq = wave / g.cgs;
   const int64_t G = h.G, g0 = (int64_t)blockIdx.x * RW;
@@ -316,13 +313,16 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
   }
   __syncthreads();
   BStream8 bs{tab, ng, g.items, F, kq * 4 * g.items, 64 * cg + lane, 0, 0};
-  float ring[kRing][4];
+  floatx4 ring[RG];
 #pragma unroll
-  for (int q = 0; q < kRing; ++q) bs.next(ring[q]);
+  for (int q = 0; q < RG; ++q) {
+    bs.next(ring[q]);
+    __builtin_amdgcn_sched_barrier(0);  // in slot order (see mlp.hip mlps_refill)
+  }
   floatx4 acc0, acc1;
   const int k0 = kq * 4 * g.items;
   auto gemm = [&](const float* A) __attribute__((always_inline)) {
-    gemm8<RW>(A, g.S, k0, g.items, ring, bs, acc0, acc1);
+    gemm8<RW, RG>(A, g.S, k0, g.items, ring, bs, acc0, acc1);
     put_partials<RW>(L.red, g, kq, 64 * cg + lane, acc0, acc1);
     lds_sync8();
   };
@@ -410,32 +410,105 @@ int head8_rows() {
   return r;
 }
 
-template <int RW>
+// The chain's B operands as k4-interleaved images (BStream8): forward B(k, n) = W[n][k] (tr), the
+// input-gradient chain B(k, n) = W[k][n], in the order each chain reads them. One thread per
+// float4 of the image: 4 consecutive k of one column n.
+struct Pack8 {
+  const float* w[kMaxGemms];
+  int32_t n, F, tr;
+  floatx4* dst;
+};
+
+__global__ __launch_bounds__(256) void k_head8_pack(const Pack8 p) {
+  __shared__ const float* tab[kMaxGemms];
+  if (threadIdx.x < kMaxGemms) tab[threadIdx.x] = p.w[threadIdx.x];
+  __syncthreads();
+  const int F = p.F;
+  const int64_t per = (int64_t)F * F / 4, total = per * p.n;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < total; u += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(u / per);
+    const int64_t r = u - m * per;
+    const int kq = (int)(r / F), nn = (int)(r - (int64_t)kq * F);
+    const float* W = tab[m];
+    floatx4 v;
+    if (p.tr) {
+      v = *reinterpret_cast<const floatx4*>(W + (int64_t)nn * F + 4 * kq);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = W[(int64_t)(4 * kq + t) * F + nn];
+    }
+    p.dst[u] = v;
+  }
+}
+
+int head8_pack(const AimxHead* h, bool fwd, float* dst, hipStream_t st) {
+  Pack8 p{};
+  const int nb = h->nb;
+  int j = 0;
+  if (fwd) {
+    p.w[j++] = h->wp;
+    for (int i = 0; i < nb; ++i) {
+      p.w[j++] = h->w1[i];
+      p.w[j++] = h->w2[i];
+    }
+    p.w[j++] = h->ws;
+  } else {
+    p.w[j++] = h->ws;
+    for (int i = nb - 1; i >= 0; --i) {
+      p.w[j++] = h->w2[i];
+      p.w[j++] = h->w1[i];
+    }
+    p.w[j++] = h->wp;
+  }
+  p.n = j;
+  p.F = (int)h->F;
+  p.tr = fwd ? 1 : 0;
+  p.dst = reinterpret_cast<floatx4*>(dst);
+  const int64_t total = (int64_t)p.n * h->F * h->F / 4;
+  hipLaunchKernelGGL(k_head8_pack, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 1024)), dim3(256), 0, st, p);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
+template <int RW, int RG>
 int head8_launch(const AimxHead* h, const float* wt, const AimxHeadGrad* d, hipStream_t st) {
   static const bool set = [] {
-    (void)hipFuncSetAttribute((const void*)k_head8_fwd<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_head8_bwd<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_head8_fwd<RW, RG>, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_head8_bwd<RW, RG>, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
     return true;
   }();
   (void)set;
   const size_t lds = lds8_floats(geo8((int)h->F), RW) * sizeof(float);
   const unsigned grid = (unsigned)cdiv(h->G, RW);
   if (d)
-    hipLaunchKernelGGL(k_head8_bwd<RW>, dim3(grid), dim3(kNT), lds, st, *h, *d);
+    hipLaunchKernelGGL((k_head8_bwd<RW, RG>), dim3(grid), dim3(kNT), lds, st, *h, *d, wt);
   else
-    hipLaunchKernelGGL(k_head8_fwd<RW>, dim3(grid), dim3(kNT), lds, st, *h, wt);
+    hipLaunchKernelGGL((k_head8_fwd<RW, RG>), dim3(grid), dim3(kNT), lds, st, *h, wt);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
+
+// ring depth: kRingMax items, or a GEMM's whole share when it has fewer (F = 128: 4)
+template <int RW>
+int head8_launch_rg(const AimxHead* h, const float* wt, const AimxHeadGrad* d, hipStream_t st) {
+  return geo8((int)h->F).items % kRingMax == 0 ? head8_launch<RW, kRingMax>(h, wt, d, st)
+                                                : head8_launch<RW, 4>(h, wt, d, st);
+}
 }  // namespace
 
-// forward: W^T of every chain weight into the workspace (k_head_transpose, head.hip), then the chain
+// forward: the chain weights' k4-interleaved images into the workspace, then the chain
 int head8_forward(const AimxHead* h, float* wt, hipStream_t st) {
-  return head8_rows() == 4 ? head8_launch<4>(h, wt, nullptr, st) : head8_launch<8>(h, wt, nullptr, st);
+  const int r = head8_pack(h, true, wt, st);
+  if (r != AIMX_OK) return r;
+  return head8_rows() == 4 ? head8_launch_rg<4>(h, wt, nullptr, st) : head8_launch_rg<8>(h, wt, nullptr, st);
 }
 
+// backward: the images of W itself into the caller's backward workspace (>= head8_forward_workspace_floats)
 int head8_backward(const AimxHead* h, const AimxHeadGrad* d, hipStream_t st) {
-  return head8_rows() == 4 ? head8_launch<4>(h, nullptr, d, st) : head8_launch<8>(h, nullptr, d, st);
+  float* wt = (float*)d->workspace;
+  const int r = head8_pack(h, false, wt, st);
+  if (r != AIMX_OK) return r;
+  return head8_rows() == 4 ? head8_launch_rg<4>(h, wt, d, st) : head8_launch_rg<8>(h, wt, d, st);
 }
 
 }  // namespace aimx
