@@ -839,8 +839,9 @@ __device__ __forceinline__ void wgrad_block(const AimxGemmArgs& a, int kchunk, u
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         fa[u][i] = bload(ra_, kok ? va[i] : a_bytes, sa);
-        const float y = bload(rb_, kok && !zcol[i] ? vb[i] : b_bytes, sb);
-        fb[u][i] = one[i] ? 1.f : y;
+        // raw: the ones column is substituted where the value is consumed (mma_group) — a select
+        // here made hipcc wait for this group's loads before the previous group's MFMAs
+        fb[u][i] = bload(rb_, kok && !zcol[i] ? vb[i] : b_bytes, sb);
       }
     }
   };
@@ -850,17 +851,22 @@ __device__ __forceinline__ void wgrad_block(const AimxGemmArgs& a, int kchunk, u
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[u][i], fb[u][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          const float b = one[j] ? 1.f : fb[u][j];  // (fa is 0 on rows past the wave's k range)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[u][i], b, acc[i][j], 0, 0, 0);
+        }
   };
   constexpr int KG = 4 * kWgU;
   const int ng = k1 > k0 ? (k1 - k0 + KG - 1) / KG : 0;
   float fa0[kWgU][2], fb0[kWgU][2], fa1[kWgU][2], fb1[kWgU][2];
   if (ng > 0) load_group(k0, fa0, fb0);
+  // loads unconditional (a group past the range reads 0): conditional ones leave hipcc waiting
+  // for every load at the loop head
   for (int g = 0; g < ng; g += 2) {
-    if (g + 1 < ng) load_group(k0 + (g + 1) * KG, fa1, fb1);
+    load_group(k0 + (g + 1) * KG, fa1, fb1);
     mma_group(fa0, fb0);
     if (g + 1 >= ng) break;
-    if (g + 2 < ng) load_group(k0 + (g + 2) * KG, fa0, fb0);
+    load_group(k0 + (g + 2) * KG, fa0, fb0);
     mma_group(fa1, fb1);
   }
   // intra-workgroup K reduction, wave order 0,1,2,3 (deterministic)

@@ -348,31 +348,15 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-// this wave's rows j = base + p + r*P of the molecule, lane channels c..c+3 (one burst): the R
-// row indices in one round of loads, then the R rows in a second, invalid ones as an ADDRESS
-// select past the buffer's extent (reads 0). A value select per row (`valid ? load : 0`) became a
-// branch and a wait per row: R dependent round trips instead of two.
-typedef float pfloatx4 __attribute__((ext_vector_type(4)));
+// this wave's rows j = base + p + r*P of the molecule, lane channels c..c+3 (one burst)
 template <int P, int R>
-__device__ __forceinline__ void load_rows(float4 (&xr)[R], const float* __restrict__ x, int64_t ldx, int64_t N,
-                                          int64_t C, const int32_t* __restrict__ gperm, int32_t b, int n, int base,
-                                          int p, int c, bool cv) {
-  const uint32_t bytes = (uint32_t)(4 * max<int64_t>((N - 1) * ldx + C, 1));  // < 2^32: the callers' row rule
-  const uint64_t a = (uint64_t)x;
-  void* q0 = (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-                     __builtin_amdgcn_readfirstlane((uint32_t)a));
-  const __amdgpu_buffer_rsrc_t rx =
-      __builtin_amdgcn_make_buffer_rsrc(q0, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-  int32_t q[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r)  // clamped into [0, N): an empty molecule reads a valid index it never uses
-    q[r] = N > 0 ? gperm[min((int64_t)b + max(min(base + p + r * P, n - 1), 0), N - 1)] : 0;
+__device__ __forceinline__ void load_rows(float4 (&xr)[R], const float* __restrict__ x, int64_t ldx,
+                                          const int32_t* __restrict__ gperm, int32_t b, int n, int base, int p,
+                                          int c, bool cv) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int j = base + p + r * P;
-    const uint32_t off = (cv && j < n) ? 4u * (uint32_t)((int64_t)q[r] * ldx + c) : bytes;
-    const pfloatx4 v = __builtin_bit_cast(pfloatx4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
-    xr[r] = make_float4(v[0], v[1], v[2], v[3]);
+    xr[r] = (cv && j < n) ? ld4(x + (int64_t)gperm[b + j] * ldx + c) : zero4();
   }
 }
 
@@ -416,7 +400,7 @@ __device__ __forceinline__ void attn_fwd_rows(const float* __restrict__ x, int64
   // 1) partial dots of this slice, reduced across the wave
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    load_rows<P, R>(xr, x, ldx, N, C, gperm, b, n, base, p, c, cv);
+    load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int q = 0; q < NCH; ++q) {
       float v[NVC];
@@ -473,7 +457,7 @@ __device__ __forceinline__ void attn_fwd_rows(const float* __restrict__ x, int64
   float4 acc = zero4();
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, N, C, gperm, b, n, base, p, c, cv);
+    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int j = base + p + r * P;
@@ -542,7 +526,7 @@ __device__ __forceinline__ void attn_bwd_rows(const float* __restrict__ x, int64
   // 1) centred dots with q and with each W_h for this slice, reduced across the wave
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    load_rows<P, R>(xr, x, ldx, N, C, gperm, b, n, base, p, c, cv);
+    load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int qq = 0; qq < NCH; ++qq) {
       float v[NVC];
@@ -618,7 +602,7 @@ __device__ __forceinline__ void attn_bwd_rows(const float* __restrict__ x, int64
   for (int h = 0; h < HM; ++h) dw[h] = zero4();
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, N, C, gperm, b, n, base, p, c, cv);
+    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int j = base + p + r * P;
@@ -687,9 +671,8 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_fwd(
   const int32_t b = gptr[g], e = gptr[g + 1];
   const int n = e - b;
   const float tau = *tau_p;
-  // (and x addressable by 32-bit buffer offsets: load_rows)
   const bool rows = n <= kMaxAtomsRows && H <= HM && C <= S * 256 && (C % 4) == 0 &&
-                    (ldx % 4) == 0 && al16(x) && al16(W) && al16(pooled) && (N - 1) * ldx + C < (int64_t)1 << 30;
+                    (ldx % 4) == 0 && al16(x) && al16(W) && al16(pooled);
   if (rows)
     attn_fwd_rows<S, P, R, HM>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, smem);
   else if (n <= kCap)
@@ -720,7 +703,7 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_bwd(
   const float tau = *tau_p;
   const bool rows = n <= kMaxAtomsRows && H <= HM && C <= S * 256 && (C % 4) == 0 &&
                     (ldx % 4) == 0 && (lddx % 4) == 0 && al16(x) && al16(W) && al16(dx) && al16(dpool) &&
-                    al16(dW_part) && (N - 1) * ldx + C < (int64_t)1 << 30;
+                    al16(dW_part);
   if (rows)
     attn_bwd_rows<S, P, R, HM>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, dpool, dattn, dx, lddx, dW_part, db_part,
                             dtau_part, smem);
