@@ -193,8 +193,11 @@ class _Bucket:
 
     def capture(self, model, warmup=2):
         # The warm-up and captured backward passes compute the gradients with autograd.grad, not
-        # .backward(): no AccumulateGrad node runs, so no hook on the parameters fires for them
-        # (DDP's reducer would take each for a real backward) and no .grad is touched
+        # .backward(), and with respect to stand-ins of the parameters (_aliased): no AccumulateGrad
+        # node runs or receives a gradient, so no hook on the parameters fires for them (DDP's
+        # reducer would take each for a real backward), no .grad is touched, and the engine never
+        # synchronises with the stream an accumulator was made on (DDP makes them at construction,
+        # on the default stream, which a capture must not wait on)
         params = self.params
         live = [p for p in params if p.requires_grad]
         args = self.static_args()
@@ -203,26 +206,56 @@ class _Bucket:
         side.wait_stream(cur)
         with torch.cuda.stream(side):  # warm-up: plans, workspaces, allocator pools, seed state
             for _ in range(warmup):
-                out = model._aimx_forward(*args)[0]
-                torch.autograd.grad(out, live, torch.zeros_like(out), allow_unused=True)
+                with _aliased(model, live) as al:
+                    out = model._aimx_forward(*args)[0]
+                    torch.autograd.grad(out, [al[id(p)] for p in live], torch.zeros_like(out), allow_unused=True)
                 # drop the warm-up graph before the capture: alive, its nodes would stay bound to
                 # this side stream while the captured backward runs on the capture stream
-                del out
+                del out, al
         cur.wait_stream(side)
         torch.cuda.synchronize(self.dev)
         self.g_fwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fwd):
-            self.outs = model._aimx_forward(*args)
+            with _aliased(model, live) as al:
+                self.outs = model._aimx_forward(*args)
+        stand_ins = [al[id(p)] for p in live]
+        del al
         self.gout = torch.zeros_like(self.outs[0])
         # the backward graph gets its own memory pool: in a shared one, the gradient tensors it
         # leaves behind could sit in blocks the forward graph used (and frees) for temporaries,
         # and the next forward replay would overwrite the caller's .grad
         self.g_bwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_bwd):
-            gs = torch.autograd.grad(self.outs[0], live, self.gout, allow_unused=True)
+            gs = torch.autograd.grad(self.outs[0], stand_ins, self.gout, allow_unused=True)
+        del stand_ins
         by_id = {id(p): g for p, g in zip(live, gs)}
         self.grads = [by_id.get(id(p)) for p in params]
         self.outs = tuple(o.detach() if o is not None else None for o in self.outs)
+
+
+class _aliased:
+    """Every live parameter swapped, in its modules' _parameters, for a non-leaf alias
+    (p.view_as(p): same storage, made on the current stream) while a warm-up or captured pass
+    builds its graph; the parameters are put back on exit. Gradients taken with respect to the
+    aliases stop at their view nodes, short of the parameters' AccumulateGrad nodes."""
+
+    def __init__(self, model, live):
+        self.model, self.live = model, live
+
+    def __enter__(self):
+        ids = {id(p) for p in self.live}
+        self.saved = [(m, n, p) for m in self.model.modules() for n, p in m._parameters.items()
+                      if p is not None and id(p) in ids]
+        al = {id(p): p.view_as(p) for p in self.live}
+        for m, n, p in self.saved:
+            m._parameters[n] = al[id(p)]
+        return al
+
+    def __exit__(self, *exc):
+        for m, n, p in self.saved:
+            m._parameters[n] = p
+        self.saved = None
+        return False
 
 
 class _Replay(torch.autograd.Function):

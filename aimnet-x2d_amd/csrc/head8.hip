@@ -400,14 +400,16 @@ bool head8_ok(const AimxHead* h) {
 size_t head8_forward_workspace_floats(const AimxHead* h) { return (size_t)(2 + 2 * h->nb) * h->F * h->F; }
 
 namespace {
-// molecules per workgroup: 8 (two 4-row accumulators per wave), or 4 (AIMX_HEAD8_ROWS=4: one
-// accumulator, twice the workgroups; A/B)
-int head8_rows() {
+// molecules per workgroup: 4 (one 4-row accumulator per wave) while G / 4 workgroups leave CUs
+// idle, 8 (two accumulators, half the weight stream per molecule) once G / 8 alone fills the chip;
+// AIMX_HEAD8_ROWS=4|8 forces one (c2, G = 520: 0.7275 ms with 4 vs 0.7678 ms with 8, r4e)
+int head8_rows(int64_t G) {
   static const int r = [] {
     const char* e = getenv("AIMX_HEAD8_ROWS");
-    return (e && atoi(e) == 4) ? 4 : 8;
+    return e ? atoi(e) : 0;
   }();
-  return r;
+  if (r == 4 || r == 8) return r;
+  return G >= 8 * 256 ? 8 : 4;
 }
 
 // The chain's B operands as k4-interleaved images (BStream8): forward B(k, n) = W[n][k] (tr), the
@@ -500,7 +502,7 @@ int head8_launch_rg(const AimxHead* h, const float* wt, const AimxHeadGrad* d, h
 int head8_forward(const AimxHead* h, float* wt, hipStream_t st) {
   const int r = head8_pack(h, true, wt, st);
   if (r != AIMX_OK) return r;
-  return head8_rows() == 4 ? head8_launch_rg<4>(h, wt, nullptr, st) : head8_launch_rg<8>(h, wt, nullptr, st);
+  return head8_rows(h->G) == 4 ? head8_launch_rg<4>(h, wt, nullptr, st) : head8_launch_rg<8>(h, wt, nullptr, st);
 }
 
 // backward: the images of W itself into the caller's backward workspace (>= head8_forward_workspace_floats)
@@ -508,7 +510,7 @@ int head8_backward(const AimxHead* h, const AimxHeadGrad* d, hipStream_t st) {
   float* wt = (float*)d->workspace;
   const int r = head8_pack(h, false, wt, st);
   if (r != AIMX_OK) return r;
-  return head8_rows() == 4 ? head8_launch_rg<4>(h, wt, d, st) : head8_launch_rg<8>(h, wt, d, st);
+  return head8_rows(h->G) == 4 ? head8_launch_rg<4>(h, wt, d, st) : head8_launch_rg<8>(h, wt, d, st);
 }
 
 }  // namespace aimx

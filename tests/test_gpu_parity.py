@@ -1014,6 +1014,40 @@ def test_fused_head_dropout():
     assert all(torch.isfinite(t.grad).all() for t in [x, wp, bp, ws, bs, wo, bo] + [p for b in blocks for p in b])
 
 
+def test_head8_row_tiles_agree():
+    """The 8-molecule head (H_in == F) at G = 2100 runs 8-row tiles (G >= 2048), at G = 300 4-row
+    tiles: the same 2100 molecules through both (the big batch whole, then in 300-molecule
+    slices) give the same outputs and input gradients row for row, and the same weight gradients
+    summed over the slices (1e-5 norm-relative)."""
+    from aimx import ops
+    g = torch.Generator().manual_seed(8)
+    F, G = 256, 2100
+    base = [torch.randn(G, F, generator=g) * 0.1, torch.randn(F, F, generator=g) * 0.06,
+            torch.randn(F, generator=g) * 0.1]
+    for _ in range(2):
+        base += [torch.randn(F, F, generator=g) * 0.06, torch.randn(F, generator=g) * 0.1,
+                 torch.randn(F, F, generator=g) * 0.06, torch.randn(F, generator=g) * 0.1]
+    base += [torch.randn(F, F, generator=g) * 0.06, torch.randn(F, generator=g) * 0.1,
+             torch.randn(2, 2 * F, generator=g) * 0.05, torch.randn(2, generator=g) * 0.1]
+    wy = torch.linspace(-1, 1, 2 * G).view(G, 2).to(DEV)
+    res = []
+    for step in (G, 300):
+        t = [b.to(DEV).requires_grad_() for b in base]
+        ys = []
+        for r0 in range(0, G, step):
+            x = t[0][r0:r0 + step]
+            y = ops.head(x, t[1], t[2], [tuple(t[3 + 4 * i:7 + 4 * i]) for i in range(2)], *t[11:15], act="silu",
+                         skips=[False, True])
+            (y * wy[r0:r0 + step]).sum().backward()
+            ys.append(y.detach())
+        torch.cuda.synchronize()
+        res.append((torch.cat(ys), [q.grad.detach().clone() for q in t]))
+    (y8, g8), (y4, g4) = res
+    assert norm_rel(y8.cpu().numpy(), y4.cpu().numpy()) < 1e-6
+    for i, (a, b) in enumerate(zip(g8, g4)):
+        assert norm_rel(a.cpu().numpy(), b.cpu().numpy()) < 1e-5, i
+
+
 @pytest.mark.parametrize("G", [5, 300, 2100])
 def test_fused_head_clusters_bit_identical(G, monkeypatch):
     """Clustered head launches (2, 4 or 8 workgroups per 16-molecule tile exchanging activations
