@@ -87,10 +87,13 @@ class GraphedTrainStep:
     """The train step captured as HIP graphs on a static padded batch (see module docstring).
 
     Every replayed batch must have the same number of real molecules B (rows >= B of the
-    per-molecule outputs are padding and excluded from the loss); a batch with the static batch's
-    layout (same padded atom / edge / molecule counts and task count) is replayed, any other (a
-    feeder's rare over-capacity batch, handed out unpadded) runs the same step eagerly on the same
-    parameters, gradients, optimizer state and loss accumulators. optimizer must be capturable
+    per-molecule outputs are padding and excluded from the loss); a batch with a captured layout
+    (same padded atom / edge / molecule counts and task count) is replayed. Without a data-parallel
+    sync up to `max_layouts` layouts are captured, each on first sight (or ahead of time by
+    prepare()): batches padded to a few atom-count buckets (bench.py pads to 256-atom buckets) then
+    carry little padding each. Any other batch (a feeder's rare over-capacity batch, handed out
+    unpadded) runs the same step eagerly on the same parameters, gradients, optimizer state and
+    loss accumulators. optimizer must be capturable
     (FusedAdam). Construction runs `warmup` real steps on example_batch (allocator pools, plans,
     optimizer state, communicators) and then rewinds the parameters, the optimizer state and the
     dropout counter, so the first call is the reference loop's first step.
@@ -107,7 +110,7 @@ class GraphedTrainStep:
     """
 
     def __init__(self, model, criterion, optimizer, example_batch, n_real=None, sync=None, warmup=3,
-                 ddp_graph=None, inject_capture_failure=None):
+                 ddp_graph=None, inject_capture_failure=None, max_layouts=1):
         import os
         # test hook (tests/test_gpu_ddp.py): make the "capture" attempt raise as a failing RCCL build
         # would, to exercise the split fallback on any box
@@ -115,10 +118,11 @@ class GraphedTrainStep:
             inject_capture_failure = os.environ.get("AIMX_TEST_CAPTURE_FAIL", "0") == "1"
         self.capture_error = None
         self.model, self.criterion, self.optimizer, self.sync = model, criterion, optimizer, sync
+        self.warmup = warmup
         model._aimx_autograph_off = True  # this step captures the model itself (aimx.autograph stays off)
         self.B = _real_rows(example_batch) if n_real is None else int(n_real)
-        self.static = example_batch.clone()
-        dev = self.static._blob.device
+        dev = example_batch._blob.device
+        self.dev = dev
         self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
         self.nan_count = torch.zeros((), dtype=torch.int32, device=dev)
         self.steps = torch.zeros((), dtype=torch.int64, device=dev)
@@ -127,8 +131,7 @@ class GraphedTrainStep:
         B = self.B
         self.eager_steps = 0
 
-        def fwd_bwd(batch=None):
-            batch = self.static if batch is None else batch
+        def fwd_bwd(batch):
             out, _, _ = model(*batch.model_args())
             if padded is not None:
                 # fused L1: the padding rows' zero gradient in the loss's backward launch, and the
@@ -151,26 +154,43 @@ class GraphedTrainStep:
             mode = "single"
         elif mode == "capture" and not sync.capturable:
             mode = "split"
+        # more than one captured layout only without a data-parallel sync: a rank meeting a new layout
+        # would capture (warm-up all-reduces) while its peers replay, and split mode's clip + Adam
+        # graph reads the one set of gradient tensors the first capture made
+        self.max_layouts = max(1, int(max_layouts)) if mode == "single" else 1
+        self._graphs = {}
+        self.mode = mode
+        self._capture(example_batch, inject_capture_failure)
+        self.reset_stats()
+
+    def _capture(self, example_batch, inject_capture_failure=False):
+        """Warm up on `example_batch` (real steps), capture the step on a static copy of it and rewind.
+        The captured graphs join self._graphs under the batch's layout and become the current ones."""
+        model, optimizer, sync, dev, mode = self.model, self.optimizer, self.sync, self.dev, self.mode
+        static = example_batch.clone()
+        fwd_bwd = self._fwd_bwd
         # the warm-up steps below really train (optimizer state, dropout counter): their starting
-        # state is put back after the capture, so the first call is the loop's first step
+        # state is put back after the capture, so the next step is the loop's next step
         saved = _snapshot(model, optimizer, dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up: allocator pools, plans, optimizer state, RCCL comms
-            for _ in range(warmup):
+            for _ in range(self.warmup):
                 optimizer.zero_grad(set_to_none=True)
-                fwd_bwd()
+                fwd_bwd(static)
                 if sync is not None:
                     sync.finish()
                 optimizer.step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        # single mode: each layout's graph holds its own gradient tensors (allocated in its capture,
+        # in its private pool) and the Adam step that reads them
         optimizer.zero_grad(set_to_none=True)
-        self.g1 = torch.cuda.CUDAGraph()
-        self.g2 = None
+        g1 = torch.cuda.CUDAGraph()
+        g2 = None
         if mode == "single":
-            with torch.cuda.graph(self.g1):
-                fwd_bwd()
+            with torch.cuda.graph(g1):
+                fwd_bwd(static)
                 optimizer.step()
         elif mode == "capture":
             ok = True
@@ -180,8 +200,8 @@ class GraphedTrainStep:
                 torch.cuda.synchronize(dev)
             try:
                 # thread_local: RCCL's watchdog thread may query events while this thread captures
-                with torch.cuda.graph(self.g1, capture_error_mode="thread_local"):
-                    fwd_bwd()
+                with torch.cuda.graph(g1, capture_error_mode="thread_local"):
+                    fwd_bwd(static)
                     sync.finish()
                     if inject_capture_failure:
                         raise RuntimeError("injected capture failure (test hook)")
@@ -196,21 +216,36 @@ class GraphedTrainStep:
                 self.capture_error = str(err) if err is not None else "failed on another rank"
                 sync._reset()
                 optimizer.zero_grad(set_to_none=True)
-                self.g1 = torch.cuda.CUDAGraph()
+                g1 = torch.cuda.CUDAGraph()
                 mode = "split"
         if mode == "split":
-            self.g2 = torch.cuda.CUDAGraph()
+            g2 = torch.cuda.CUDAGraph()
             hooks, sync._hooks = sync._hooks, []  # the eager all-reduce runs between the graphs
             for h in hooks:
                 h.remove()
             sync.overlap = False
-            with torch.cuda.graph(self.g1):
-                fwd_bwd()
-            with torch.cuda.graph(self.g2):
+            with torch.cuda.graph(g1):
+                fwd_bwd(static)
+            with torch.cuda.graph(g2):
                 optimizer.step()
         self.mode = mode
         _restore(saved, optimizer)
-        self.reset_stats()
+        self._graphs[tuple(static._layout)] = (static, g1, g2)
+        self.static, self.g1, self.g2 = static, g1, g2
+
+    def prepare(self, batches):
+        """Capture every new layout among `batches` now (up to max_layouts), so that no capture
+        falls inside a timed loop; returns the number of layouts held."""
+        for b in batches:
+            key = tuple(b._layout)
+            if key not in self._graphs and len(self._graphs) < self.max_layouts:
+                self._capture(b)
+        return len(self._graphs)
+
+    @property
+    def layouts(self):
+        """Captured layouts (static batch shapes) so far."""
+        return len(self._graphs)
 
     def reset_stats(self):
         self.loss_sum.zero_()
@@ -218,15 +253,22 @@ class GraphedTrainStep:
         self.steps.zero_()
 
     def __call__(self, batch=None):
-        """Copy `batch` (a DeviceBatch of the static layout) into the static inputs and replay."""
+        """Copy `batch` (a DeviceBatch of a captured layout) into its static inputs and replay. A batch
+        of a new layout is captured first while fewer than max_layouts are held, else run eagerly."""
         if batch is not None:
             n_real = _real_rows(batch)
             if n_real != self.B:  # e.g. a trailing partial batch: padding rows would enter the loss
                 raise ValueError(f"GraphedTrainStep: batch has {n_real} real molecules, the captured step "
                                  f"takes exactly {self.B} (run partial batches through train_step)")
             if batch._layout != self.static._layout:
-                self._eager(batch)
-                return
+                got = self._graphs.get(tuple(batch._layout))
+                if got is None and len(self._graphs) < self.max_layouts:
+                    self._capture(batch)
+                    got = self._graphs[tuple(batch._layout)]
+                if got is None:
+                    self._eager(batch)
+                    return
+                self.static, self.g1, self.g2 = got
             self.static.copy_(batch)
         self.g1.replay()
         if self.g2 is not None:

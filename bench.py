@@ -68,19 +68,32 @@ def make_collated(cfg, n_batches, seed):
 
 
 PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from the loss)
+LAYOUT_QUANTUM = 256  # atoms: one-GPU static batches are padded to the next multiple (one graph each)
 
 
-def make_batches(cfg, n_batches, seed, device, pad=False):
+def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):
     """Device-resident batches. pad=True: static shapes for graph replay (padding molecules of at
-    most 64 atoms each, pad_mols_for)."""
+    most 64 atoms each, pad_mols_for) — one shape for all (max atoms + 64, max edges + 256), or with
+    `buckets` one per atom-count bucket (real atoms + PAD_MOLS + 1 rounded up to LAYOUT_QUANTUM; edges
+    the bucket's max + 256), each captured as its own graph by GraphedTrainStep."""
     cols = make_collated(cfg, n_batches, seed)
     if not pad:
         return [adata.DeviceBatch(c, device, targets=t, total_charges=q, csr_hops=cfg["hops"]) for c, t, q in cols]
-    n_max = max(c["batch"].shape[0] for c, _, _ in cols) + 64
-    e_max = max(c["edges"].shape[0] for c, _, _ in cols) + 256
-    pm = pad_mols_for(n_max, min(c["batch"].shape[0] for c, _, _ in cols))
+
+    def bucket(c):
+        n = c["batch"].shape[0]
+        return -(-(n + PAD_MOLS + 1) // LAYOUT_QUANTUM) * LAYOUT_QUANTUM if buckets else 0
+    groups = {}
+    for c, _, _ in cols:
+        groups.setdefault(bucket(c), []).append(c)
+    shape = {}
+    for k, cs in groups.items():
+        n_max = k or max(c["batch"].shape[0] for c in cs) + 64
+        n_min = min(c["batch"].shape[0] for c in cs)
+        shape[k] = (n_max, max(c["edges"].shape[0] for c in cs) + 256, pad_mols_for(n_max, n_min))
     out = []
     for c, t, q in cols:
+        n_max, e_max, pm = shape[bucket(c)]
         real_atoms, real_edges = c["batch"].shape[0], c["edges"].shape[0]
         pc = adata.pad_collated(c, n_max, e_max, cfg["batch"], pm)
         tg = np.concatenate([t, np.zeros((pm, t.shape[1]), np.float32)])
@@ -526,7 +539,7 @@ def _cpu_rate(cfg, threads, seconds, max_steps):
                       f"{cfg['hops']} hops), oracle/model.py fp32 torch-CPU, {threads} threads"}
 
 
-def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False):
+def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False, seed=777):
     """The drop-in (unchanged reference trainer) rate: a fresh model trained eagerly on unpadded
     resident batches — forward, L1 loss, backward, clip + Adam, one Python call per op as
     trainer.py:151-164 runs it (no graph). autograph: the same loop with aimx.autograph on (the
@@ -540,7 +553,7 @@ def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False
         ag.enable(model, False)  # autograph=True: the default drop-in behaviour (size-gated replay)
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
     loss_fn = L1Loss()
-    bs = make_batches(cfg, batches_eager, 777, device, pad=False)
+    bs = make_batches(cfg, batches_eager, seed, device, pad=False)
 
     def step(i):
         b = bs[i % len(bs)]
@@ -708,7 +721,9 @@ def main():
                                args.stream_path, read_threads=args.read_threads)
         batches = [next(feeder)]
     else:
-        batches = make_batches(cfg, args.pool, 1234 + rank, device, pad=args.graph)
+        # one GPU: one captured graph per 256-atom bucket of the pool; data parallel: one shape for all
+        # (every rank must capture and replay the same graphs' collectives in step)
+        batches = make_batches(cfg, args.pool, 1234 + rank, device, pad=args.graph, buckets=world == 1)
     if args.roofline_only:
         print(json.dumps(hop_roofline(make_batches(cfg, 1, 99, device)[0], cfg["hops"], device, cfg["hidden"])))
         return
@@ -736,14 +751,16 @@ def main():
         sync = GradientSync(model.parameters(), unused=model.unused_parameters(), always=True)
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)  # clip(1.0) + Adam, trainer.py:163-164
     graphed = None
-    pad_mols_used = batches[0].num_graphs - B if args.graph else 0
+    pad_mols_used = "/".join(str(v) for v in sorted({b.num_graphs - B for b in batches})) if args.graph else "0"
     if args.graph:
         # Whole-step HIP-graph capture on static padded inputs (aimx.train.GraphedTrainStep): forward,
         # backward, the bucketed RCCL all-reduces overlapped with the backward (world > 1), clip and
         # Adam; each timed step copies a fresh resident batch into the static inputs and replays.
         from aimx.train import GraphedTrainStep
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.amp):  # captured in the context
-            graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync)
+            graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync,
+                                       max_layouts=8 if world == 1 else 1)
+            graphed.prepare(batches)
 
         def step(i):
             graphed(next(feeder) if feeder is not None else batches[i % len(batches)])
@@ -811,8 +828,10 @@ def main():
 
     eager = None
     if rank == 0 and world == 1 and args.graph and feeder is None and not args.no_eager and not args.amp:
-        eager = eager_rate(cfg, device, batches_eager=4, steps=args.eager_steps)
-        eager["autograph"] = eager_rate(cfg, device, batches_eager=4, steps=args.eager_steps, autograph=True)
+        # the same resident batches as the graphed loop, unpadded
+        eager = eager_rate(cfg, device, batches_eager=args.pool, steps=args.eager_steps, seed=1234)
+        eager["autograph"] = eager_rate(cfg, device, batches_eager=args.pool, steps=args.eager_steps, seed=1234,
+                                        autograph=True)
     roof = extra = None
     if rank == 0 and not args.no_roofline:
         del batches
@@ -848,7 +867,9 @@ def main():
                        + f", hidden {cfg['hidden']}, {cfg['hops']} hops, {cfg['tasks']} task(s), attention pool, "
                        "train step fwd+bwd+clip+Adam, dropout 0.05"
                        + (f", HIP-graph replay of padded static batches (+{pad_mols_used} padding molecules of"
-                          " <= 64 atoms, excluded from the loss)" if args.graph else ", eager"),
+                          " <= 64 atoms, excluded from the loss; "
+                          + (f"{graphed.layouts} captured layouts: {LAYOUT_QUANTUM}-atom buckets)" if world == 1
+                             else "one layout)") if args.graph else ", eager"),
                        "feed": ("resident pool of %d batches in HBM" % args.pool if feeder is None else
                                 "native C++ collate + pinned H2D per step (PCIe-inclusive; not the metric value)"
                                 if args.feed == "native" else
