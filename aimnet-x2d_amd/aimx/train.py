@@ -172,6 +172,7 @@ class GraphedTrainStep:
         # the warm-up steps below really train (optimizer state, dropout counter): their starting
         # state is put back after the capture, so the next step is the loop's next step
         saved = _snapshot(model, optimizer, dev)
+        stats = [t.clone() for t in (self.loss_sum, self.nan_count, self.steps)]
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up: allocator pools, plans, optimizer state, RCCL comms
@@ -230,6 +231,9 @@ class GraphedTrainStep:
                 optimizer.step()
         self.mode = mode
         _restore(saved, optimizer)
+        with torch.no_grad():  # ... and the warm-up steps' loss sum, NaN count and step count
+            for t, v in zip((self.loss_sum, self.nan_count, self.steps), stats):
+                t.copy_(v)
         self._graphs[tuple(static._layout)] = (static, g1, g2)
         self.static, self.g1, self.g2 = static, g1, g2
 

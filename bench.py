@@ -68,21 +68,22 @@ def make_collated(cfg, n_batches, seed):
 
 
 PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from the loss)
-LAYOUT_QUANTUM = 256  # atoms: one-GPU static batches are padded to the next multiple (one graph each)
+LAYOUT_QUANTUM = 128  # atoms: one-GPU static batches are padded to the next multiple (one graph each)
 
 
 def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):
     """Device-resident batches. pad=True: static shapes for graph replay (padding molecules of at
-    most 64 atoms each, pad_mols_for) — one shape for all (max atoms + 64, max edges + 256), or with
-    `buckets` one per atom-count bucket (real atoms + PAD_MOLS + 1 rounded up to LAYOUT_QUANTUM; edges
-    the bucket's max + 256), each captured as its own graph by GraphedTrainStep."""
+    most 64 atoms each, pad_mols_for) — one shape for all (max atoms + 64, max edges + 256, at least
+    PAD_MOLS padding molecules), or with `buckets` one per atom-count bucket (real atoms + 2 rounded up
+    to LAYOUT_QUANTUM, the bucket's max edges + 64, as few padding molecules as keep each within 64
+    atoms), each captured as its own graph by GraphedTrainStep."""
     cols = make_collated(cfg, n_batches, seed)
     if not pad:
         return [adata.DeviceBatch(c, device, targets=t, total_charges=q, csr_hops=cfg["hops"]) for c, t, q in cols]
 
     def bucket(c):
         n = c["batch"].shape[0]
-        return -(-(n + PAD_MOLS + 1) // LAYOUT_QUANTUM) * LAYOUT_QUANTUM if buckets else 0
+        return -(-(n + 2) // LAYOUT_QUANTUM) * LAYOUT_QUANTUM if buckets else 0
     groups = {}
     for c, _, _ in cols:
         groups.setdefault(bucket(c), []).append(c)
@@ -90,7 +91,8 @@ def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):
     for k, cs in groups.items():
         n_max = k or max(c["batch"].shape[0] for c in cs) + 64
         n_min = min(c["batch"].shape[0] for c in cs)
-        shape[k] = (n_max, max(c["edges"].shape[0] for c in cs) + 256, pad_mols_for(n_max, n_min))
+        e_max = max(c["edges"].shape[0] for c in cs) + (64 if k else 256)
+        shape[k] = (n_max, e_max, adata.pad_mols_for(n_max, n_min, 64, 1) if k else pad_mols_for(n_max, n_min))
     out = []
     for c, t, q in cols:
         n_max, e_max, pm = shape[bucket(c)]
