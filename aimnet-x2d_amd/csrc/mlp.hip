@@ -591,6 +591,23 @@ namespace {
 constexpr int kSMaxThreads = 768;                // <= 12 waves: up to 170 VGPRs per lane
 constexpr int kMlpsDynLds = 160 * 1024 - 1024;   // + the static pointer tables
 
+#ifdef AIMX_MLPS_TRACE  // diagnostics build only: per-wave phase timestamps of two workgroups
+// [direction][traced workgroup][wave][stamp], written by lane 0 of each wave with a vector store
+__device__ long long g_mlps_trace[2][2][12][24];
+__device__ __forceinline__ void mlps_stamp(int dir, int k) {
+  const int slot = blockIdx.x == 0 ? 0 : blockIdx.x == 77 ? 1 : -1;
+  if (slot >= 0 && (threadIdx.x & 63) == 0 && k < 24) {
+    const long long t = (long long)wall_clock64();
+    __builtin_nontemporal_store(t, &g_mlps_trace[dir][slot][threadIdx.x >> 6][k]);
+  }
+}
+#define MLPS_STAMP(dir, k) mlps_stamp(dir, k)
+#else
+#define MLPS_STAMP(dir, k) \
+  do {                     \
+  } while (0)
+#endif
+
 struct SGeom {
   int32_t CF;  // 16-wide output fragments of D: pad16(D) / 16
   int32_t G;   // 16-wide k groups streamed per GEMM: CF rounded up to a multiple of the ring depth P
@@ -737,6 +754,7 @@ __device__ __forceinline__ T pick8(T const (&a)[8], int k) {
 template <int RT, int NF, int P>
 __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  MLPS_STAMP(0, 0);
   constexpr int R = 16 * RT;
   // epilogue operands prefetched into registers during the GEMM where they fit (else loaded in the
   // epilogue): 8 RT NF VGPRs
@@ -766,11 +784,13 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
   const __amdgpu_buffer_rsrc_t rug = mlp_rsrc(p.ug, (uint32_t)(4 * N * 2 * D));
   const __amdgpu_buffer_rsrc_t rx_ = mlp_rsrc(p.x, p.x ? (uint32_t)(4 * ((N - 1) * p.ldx + D)) : 0u);
   for (int e = threadIdx.x; e < R * S; e += blockDim.x) Hb[e] = 0.f;  // k padding of the W2 GEMMs' A
+  MLPS_STAMP(0, 1);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
     __syncthreads();  // the previous chunk's last reads of Xa are done
     load_rows(Xa, S, p.ug, 2 * p.D, r0c, R, D, 16 * G, N);  // a0 = act(u) = UG[:, :D]; zero beyond D and N
     __syncthreads();
+    MLPS_STAMP(0, 2);
     BStream<NF> bs;
     bs.init(img, fr, nph * G);
     floatx4 ring[P][NF];
@@ -803,6 +823,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
           }
       }
       mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G);
+      MLPS_STAMP(0, 3 + 3 * ph);
       // everything the epilogue addresses derives from these opaque copies, so none of it is
       // computed ahead of the GEMM and held across it
       int lo = lane;
@@ -870,8 +891,10 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
             }
           }
       }
+      MLPS_STAMP(0, 4 + 3 * ph);
       mlps_refill<NF, P>(ring, bs);
       lds_sync();  // hand the tile to the next GEMM
+      MLPS_STAMP(0, 5 + 3 * ph);
     }
   }
 }
@@ -879,6 +902,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
 template <int RT, int NF, int P>
 __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  MLPS_STAMP(1, 0);
   constexpr int R = 16 * RT;
   constexpr bool kPre = NF == 1 || RT <= 2;  // as in k_mlps_fwd
   const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
@@ -896,6 +920,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
   }
   const float scale = drop_scale(p.drop_p);
   for (int e = threadIdx.x; e < R * S; e += blockDim.x) DV[e] = 0.f;
+  MLPS_STAMP(1, 1);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
     __syncthreads();
@@ -905,6 +930,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
       const int r = e / D, c = e - r * D;
       if (r0c + r < N) p.dug[(r0c + r) * 2 * p.D + p.D + c] = DA[r * S + c];
     }
+    MLPS_STAMP(1, 2);
     BStream<NF> bs;
     bs.init(img, fr, nph * G);
     floatx4 ring[P][NF];
@@ -936,6 +962,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
           }
       }
       mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G);
+      MLPS_STAMP(1, 3 + 3 * ph);
       int lo = lane;  // opaque copies: see k_mlps_fwd
       asm volatile("" : "+s"(r0), "+v"(lo));
       const int lr = lo & 15, lq = 4 * (lo >> 4);
@@ -988,8 +1015,10 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
             }
           }
       }
+      MLPS_STAMP(1, 4 + 3 * ph);
       mlps_refill<NF, P>(ring, bs);
       lds_sync();
+      MLPS_STAMP(1, 5 + 3 * ph);
     }
   }
 }
@@ -1251,3 +1280,11 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
 }
 
 }  // namespace aimx
+
+#ifdef AIMX_MLPS_TRACE
+extern "C" int aimx_mlps_trace_read(long long* out) {  // 2 x 2 x 12 x 24 stamps (wall clock, 100 MHz)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(aimx::g_mlps_trace), sizeof(long long) * 2 * 2 * 12 * 24) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif

@@ -1017,8 +1017,8 @@ def test_fused_head_dropout():
 def test_head8_row_tiles_agree():
     """The 8-molecule head (H_in == F) at G = 2100 runs 8-row tiles (G >= 2048), at G = 300 4-row
     tiles: the same 2100 molecules through both (the big batch whole, then in 300-molecule
-    slices) give the same outputs and input gradients row for row, and the same weight gradients
-    summed over the slices (5e-5 norm-relative; bias sums 5e-4)."""
+    slices) give the same outputs and input gradients row for row (1e-6), and the same weight
+    gradients summed over the slices (5e-5 norm-relative; bias sums 2e-3)."""
     from aimx import ops
     g = torch.Generator().manual_seed(8)
     F, G = 256, 2100
@@ -1047,8 +1047,10 @@ def test_head8_row_tiles_agree():
     for i, (a, b) in enumerate(zip(g8, g4)):
         # weight and bias gradients are 2100-row sums (one launch vs seven slices added by autograd)
         # that the linspace weights largely cancel: fp32 summation order alone moves them ~1e-5
-        # (weights, measured 1.25e-5) and ~1e-4 (biases, 8.9e-5) relative; an indexing fault, O(1)
-        tol = 5e-5 if a.dim() == 2 else 5e-4
+        # (weights, measured 1.25e-5) and ~1e-4 (biases, 0.9-5.9e-4) relative. They come from the
+        # grouped weight-gradient launch over the head's saved activations; the 8-row tiles reach
+        # them only through those, which the row-local checks above hold to 1e-6
+        tol = 1e-6 if i == 0 else 5e-5 if a.dim() == 2 else 2e-3  # [0]: the input gradient, row-local
         assert norm_rel(a.cpu().numpy(), b.cpu().numpy()) < tol, (i, norm_rel(a.cpu().numpy(), b.cpu().numpy()))
 
 

@@ -108,7 +108,7 @@ def test_graphed_step_captures_each_layout():
     _, m3, _, opt3 = _setup()
     m3.load_state_dict(m1.state_dict())
     eager = [train_step(m1, x, crit, opt1, n_real=128)[0].item() for x in seq]
-    for m, opt, layouts, n_eager in ((m2, opt2, 2, 1), (m3, opt3, 1, 3)):
+    for m, opt, layouts, n_eager in ((m2, opt2, 2, 1), (m3, opt3, 1, 4)):
         g = GraphedTrainStep(m, crit, opt, a[0], n_real=128, warmup=1, max_layouts=layouts)
         graphed = []
         for x in seq:
