@@ -541,12 +541,14 @@ def _cpu_rate(cfg, threads, seconds, max_steps):
                       f"{cfg['hops']} hops), oracle/model.py fp32 torch-CPU, {threads} threads"}
 
 
-def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False, seed=777):
+def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False, seed=777, ddp=False):
     """The drop-in (unchanged reference trainer) rate: a fresh model trained eagerly on unpadded
     resident batches — forward, L1 loss, backward, clip + Adam, one Python call per op as
     trainer.py:151-164 runs it (no graph). autograph: the same loop with aimx.autograph on (the
     model's forward and backward replayed per shape bucket, AIMX_AUTOGRAPH=1); the bucket's
-    capture happens in the warm-up. A side measurement; never the metric `value`."""
+    capture happens in the warm-up. ddp: the same loop on the model wrapped as the reference
+    runner wraps it (DistributedDataParallel(find_unused_parameters=True), runner.py:703-707) over
+    the initialised process group. A side measurement; never the metric `value`."""
     from aimx.optim import FusedAdam
     from models import L1Loss
     model = build_model(cfg, device)
@@ -556,11 +558,15 @@ def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False
     opt = FusedAdam(model.parameters(), lr=2.5e-4, max_grad_norm=1.0)
     loss_fn = L1Loss()
     bs = make_batches(cfg, batches_eager, seed, device, pad=False)
+    net = model
+    if ddp:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        net = DDP(model, device_ids=[torch.device(device).index or 0], find_unused_parameters=True)
 
     def step(i):
         b = bs[i % len(bs)]
         opt.zero_grad(set_to_none=True)
-        out, _, _ = model(*b.model_args())
+        out, _, _ = net(*b.model_args())
         loss_fn(out, b.targets).backward()
         opt.step()
     for i in range(warmup):
@@ -572,11 +578,13 @@ def eager_rate(cfg, device, batches_eager=4, steps=20, warmup=5, autograph=False
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     replayed = bool(autograph and ag.wanted(model.train(), bs[0].model_args()))
-    del model, opt, bs
+    del model, opt, bs, net
     torch.cuda.empty_cache()
     return {"value": round(cfg["batch"] * steps / dt, 1), "unit": "molecules/s", "ms_per_step": round(dt / steps * 1e3, 4),
             "steps": steps, "warmup": warmup,
-            "mode": ("eager loop as the unchanged trainer runs it, the default drop-in behaviour: the model's "
+            "mode": ("DistributedDataParallel(find_unused_parameters=True)-wrapped model over a world-size-"
+                     f"{dist.get_world_size() if dist.is_initialized() else 1} process group, " if ddp else "")
+            + ("eager loop as the unchanged trainer runs it, the default drop-in behaviour: the model's "
                      "forward/backward replayed per shape bucket by aimx.autograph when atoms x hidden <= "
                      f"{ag.MAX_WORK} (here: {'replayed' if replayed else 'eager launches'}), unpadded batches, "
                      "same step") if autograph else
@@ -725,7 +733,8 @@ def main():
     else:
         # one GPU: one captured graph per 256-atom bucket of the pool; data parallel: one shape for all
         # (every rank must capture and replay the same graphs' collectives in step)
-        batches = make_batches(cfg, args.pool, 1234 + rank, device, pad=args.graph, buckets=world == 1)
+        batches = make_batches(cfg, args.pool, 1234 + rank, device, pad=args.graph,
+                               buckets=world == 1 and not args.ddp_world1)
     if args.roofline_only:
         print(json.dumps(hop_roofline(make_batches(cfg, 1, 99, device)[0], cfg["hops"], device, cfg["hidden"])))
         return
@@ -761,7 +770,7 @@ def main():
         from aimx.train import GraphedTrainStep
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.amp):  # captured in the context
             graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync,
-                                       max_layouts=8 if world == 1 else 1)
+                                       max_layouts=8 if sync is None else 1)
             graphed.prepare(batches)
 
         def step(i):
@@ -834,6 +843,9 @@ def main():
         eager = eager_rate(cfg, device, batches_eager=args.pool, steps=args.eager_steps, seed=1234)
         eager["autograph"] = eager_rate(cfg, device, batches_eager=args.pool, steps=args.eager_steps, seed=1234,
                                         autograph=True)
+        if dist.is_initialized():  # --ddp-world1: the reference's DDP wrapping over the autograph
+            eager["ddp_wrapped"] = eager_rate(cfg, device, batches_eager=args.pool, steps=args.eager_steps,
+                                              seed=1234, autograph=True, ddp=True)
     roof = extra = None
     if rank == 0 and not args.no_roofline:
         del batches
@@ -870,7 +882,7 @@ def main():
                        "train step fwd+bwd+clip+Adam, dropout 0.05"
                        + (f", HIP-graph replay of padded static batches (+{pad_mols_used} padding molecules of"
                           " <= 64 atoms, excluded from the loss; "
-                          + (f"{graphed.layouts} captured layouts: {LAYOUT_QUANTUM}-atom buckets)" if world == 1
+                          + (f"{graphed.layouts} captured layouts: {LAYOUT_QUANTUM}-atom buckets)" if sync is None
                              else "one layout)") if args.graph else ", eager"),
                        "feed": ("resident pool of %d batches in HBM" % args.pool if feeder is None else
                                 "native C++ collate + pinned H2D per step (PCIe-inclusive; not the metric value)"
