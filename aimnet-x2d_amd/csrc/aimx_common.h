@@ -23,13 +23,20 @@ __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 
 // Activation kinds (reference: src/utils/activation.py:9-34).
 enum Act : int { ACT_NONE = -1, ACT_RELU = 0, ACT_LEAKYRELU = 1, ACT_ELU = 2, ACT_GELU = 3, ACT_SILU = 4 };
 
+// 1 / (1 + e^-v) from the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each, a few
+// ulp in all) instead of expf and a correctly rounded division (~20 VALU ops, a VALU-bound share
+// of the fused epilogues)
+__device__ __forceinline__ float silu_sigmoid(float v) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * v));
+}
+
 __device__ __forceinline__ float act_fwd(int kind, float v) {
   switch (kind) {
     case ACT_RELU: return v > 0.f ? v : 0.f;
     case ACT_LEAKYRELU: return v > 0.f ? v : 0.01f * v;
     case ACT_ELU: return v > 0.f ? v : expm1f(v);
     case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-    case ACT_SILU: return v / (1.f + expf(-v));
+    case ACT_SILU: return v * silu_sigmoid(v);
     default: return v;
   }
 }
@@ -46,20 +53,36 @@ __device__ __forceinline__ float act_grad(int kind, float v) {
       return cdf + v * pdf;
     }
     case ACT_SILU: {
-      const float s = 1.f / (1.f + expf(-v));
+      const float s = silu_sigmoid(v);
       return s * (1.f + v * (1.f - s));
     }
     default: return 1.f;
   }
 }
 
-// Counter-based hash for dropout masks: uniform in [0,1) from (seed, salt, index).
+// Counter-based hash for dropout masks: uniform in [0,1) from (seed, salt, index). The 64-bit seed
+// and the salt fold into two 32-bit keys (splitmix64; uniform per call site, so hoisted out of the
+// element loops), and each element costs two rounds of a 32-bit integer finaliser over its index
+// (lowbias32: 2 multiplies each). The earlier splitmix64 of the index took three 64-bit multiplies
+// (12 quarter-rate VALU ops) per element, which made the dropout epilogues VALU-bound (k_mlps c4:
+// 8-10 us of an 80 us launch). Rate, lag correlations and per-column rates checked on 2e7 draws.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
 __device__ __forceinline__ float hash_uniform(uint64_t seed, uint32_t salt, uint64_t idx) {
-  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(salt + 1)) ^ (idx * 0xD1B54A32D192ED03ull);
+  uint64_t z = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(salt + 1));
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
+  uint32_t h = mix32((uint32_t)idx ^ (uint32_t)z);
+  h = mix32(h ^ (uint32_t)(idx >> 32) ^ (uint32_t)(z >> 32));
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
 // The n dropout seeds of one forward from the device counter at state (one thread): splitmix64 of

@@ -311,6 +311,40 @@ __device__ __forceinline__ void load_rows(float* dst, int S, const float* src, i
   }
 }
 
+// The weight-streamed kernels' chunk load: rows [r0, r0 + R) x cols [0, D) of src (row stride ld)
+// into LDS rows of stride S with every load of a thread in flight at once (one round trip). Thread
+// t owns column t mod D of rows t / D, t / D + RG, ... (RG = blockDim.x / D rows per pass: >= 4 for
+// one fragment per wave, >= 2 for two, so MAXU = 4 RT NF passes cover R), so its addresses step by a
+// uniform stride; rows >= N read 0 through the buffer extent (an address select, not a value select,
+// which would wait for each load). The tile's columns D.. are zeroed once per kernel. gdst
+// (optional) also receives the values of the rows < N at gdst[(r0 + r) ldg + c].
+template <int MAXU>
+__device__ __forceinline__ void load_chunk(float* dst, int S, const float* src, int64_t ld, int64_t r0, int R, int D,
+                                           int64_t N, float* gdst = nullptr, int64_t ldg = 0) {
+  const int RG = (int)blockDim.x / D;
+  int rb = (int)threadIdx.x / D, c = (int)threadIdx.x - rb * D;
+  // opaque per call: hoisted out of the chunk loop, the MAXU row offsets and conditions would live
+  // (spilled) through every GEMM
+  asm volatile("" : "+v"(rb), "+v"(c));
+  const bool mine = rb < RG;
+  const int nrows = (int)max<int64_t>(0, min<int64_t>(R, N - r0));
+  const __amdgpu_buffer_rsrc_t rs = mlp_rsrc(src + r0 * ld, (uint32_t)(4 * max<int64_t>(1, (int64_t)nrows * ld)));
+  float v[MAXU];
+#pragma unroll
+  for (int u = 0; u < MAXU; ++u) {
+    const int r = rb + u * RG;
+    v[u] = mlp_bload(rs, (mine && r < nrows) ? 4u * (uint32_t)(r * ld + c) : 0xFFFFFFF0u);
+  }
+#pragma unroll
+  for (int u = 0; u < MAXU; ++u) {
+    const int r = rb + u * RG;
+    if (mine && r < R) {
+      dst[r * S + c] = v[u];
+      if (gdst && r < nrows) gdst[(r0 + r) * ldg + c] = v[u];
+    }
+  }
+}
+
 __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, int rt) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int D = (int)p.D, Kp = pad16(D), S = wstride(D), CF = Kp / 16, nm = p.nm;
@@ -589,6 +623,9 @@ namespace {
 // per row tile feeds 4 MFMAs). Epilogues, dropout hash, salts and outputs (V, R, M, A, out / dV, dA,
 // dUG) are the per-GEMM path's.
 constexpr int kSMaxThreads = 768;                // <= 12 waves: up to 170 VGPRs per lane
+// two workgroups per CU (OCC = 2): <= 10 waves each, 5 per SIMD, <= 102 VGPRs per lane, half the LDS
+// each, so one workgroup's chunk load, epilogues and barriers overlap the other's MFMA phases
+constexpr int kSOcc2Threads = 640;
 constexpr int kMlpsDynLds = 160 * 1024 - 1024;   // + the static pointer tables
 
 #ifdef AIMX_MLPS_TRACE  // diagnostics build only: per-wave phase timestamps of two workgroups
@@ -751,14 +788,15 @@ __device__ __forceinline__ T pick8(T const (&a)[8], int k) {
   return r;
 }
 
-template <int RT, int NF, int P>
-__global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo) {
+template <int RT, int NF, int P, int OCC>
+__global__ __launch_bounds__(OCC == 1 ? kSMaxThreads : kSOcc2Threads) __attribute__((amdgpu_waves_per_eu(OCC == 1 ? 1 : 5)))
+void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   MLPS_STAMP(0, 0);
   constexpr int R = 16 * RT;
   // epilogue operands prefetched into registers during the GEMM where they fit (else loaded in the
   // epilogue): 8 RT NF VGPRs
-  constexpr bool kPre = NF == 1 || RT <= 2;
+  constexpr bool kPre = OCC == 1 && (NF == 1 || RT <= 2);  // two per CU: the other workgroup hides the loads
   const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
   float* Xa = lds;              // block input a_k [R][S]
   float* Hb = lds + R * S;      // r_k             [R][S]
@@ -783,12 +821,13 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
   // the last block's residual operands as buffer loads (an absent x reads 0: no branch per load)
   const __amdgpu_buffer_rsrc_t rug = mlp_rsrc(p.ug, (uint32_t)(4 * N * 2 * D));
   const __amdgpu_buffer_rsrc_t rx_ = mlp_rsrc(p.x, p.x ? (uint32_t)(4 * ((N - 1) * p.ldx + D)) : 0u);
-  for (int e = threadIdx.x; e < R * S; e += blockDim.x) Hb[e] = 0.f;  // k padding of the W2 GEMMs' A
+  // k padding of both tiles (the chunk loads and the epilogues write columns < D only)
+  for (int e = threadIdx.x; e < 2 * R * S; e += blockDim.x) Xa[e] = 0.f;
   MLPS_STAMP(0, 1);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
     __syncthreads();  // the previous chunk's last reads of Xa are done
-    load_rows(Xa, S, p.ug, 2 * p.D, r0c, R, D, 16 * G, N);  // a0 = act(u) = UG[:, :D]; zero beyond D and N
+    load_chunk<4 * RT * NF>(Xa, S, p.ug, 2 * p.D, r0c, R, D, N);  // a0 = act(u) = UG[:, :D]; zero beyond N
     __syncthreads();
     MLPS_STAMP(0, 2);
     BStream<NF> bs;
@@ -899,12 +938,13 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
   }
 }
 
-template <int RT, int NF, int P>
-__global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo) {
+template <int RT, int NF, int P, int OCC>
+__global__ __launch_bounds__(OCC == 1 ? kSMaxThreads : kSOcc2Threads) __attribute__((amdgpu_waves_per_eu(OCC == 1 ? 1 : 5)))
+void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   MLPS_STAMP(1, 0);
   constexpr int R = 16 * RT;
-  constexpr bool kPre = NF == 1 || RT <= 2;  // as in k_mlps_fwd
+  constexpr bool kPre = OCC == 1 && (NF == 1 || RT <= 2);  // as in k_mlps_fwd
   const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
   float* DA = lds;          // gradient w.r.t. the current block output [R][S]
   float* DV = lds + R * S;  // dV_k                                     [R][S]
@@ -919,17 +959,13 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
     fr[i] = min(wave + i * nw, CF - 1);
   }
   const float scale = drop_scale(p.drop_p);
-  for (int e = threadIdx.x; e < R * S; e += blockDim.x) DV[e] = 0.f;
+  for (int e = threadIdx.x; e < 2 * R * S; e += blockDim.x) DA[e] = 0.f;  // k padding of DA and DV
   MLPS_STAMP(1, 1);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
     __syncthreads();
-    load_rows(DA, S, p.dy, p.lddy, r0c, R, D, 16 * G, N);
+    load_chunk<4 * RT * NF>(DA, S, p.dy, p.lddy, r0c, R, D, N, p.dug + p.D, 2 * p.D);  // and dg = dY
     __syncthreads();
-    for (int e = threadIdx.x; e < R * D; e += blockDim.x) {  // dg = dY (from the LDS copy)
-      const int r = e / D, c = e - r * D;
-      if (r0c + r < N) p.dug[(r0c + r) * 2 * p.D + p.D + c] = DA[r * S + c];
-    }
     MLPS_STAMP(1, 2);
     BStream<NF> bs;
     bs.init(img, fr, nph * G);
@@ -1063,7 +1099,7 @@ bool mlpw_lds_ok(int64_t D, int64_t nm) {
 // ---- weight-streamed geometry and launches ----
 struct MlpsPlan {
   bool ok;
-  int RT, NF, P;
+  int RT, NF, P, OCC;
   SGeom geo;
   unsigned blocks;
   size_t lds;
@@ -1082,46 +1118,58 @@ MlpsPlan mlps_plan(int64_t N, int64_t D) {
   pl.geo.G = std::min(g5, g4);
   pl.geo.S = 16 * pl.geo.G + 4;
   pl.geo.nw = (int)cdiv(CF, pl.NF);
-  const int rt_max = pl.NF == 1 ? 7 : 3;
-  // enough rows per chunk that the chunks fit one round of one workgroup per CU
-  int rt = (int)std::min<int64_t>(rt_max, std::max<int64_t>(1, cdiv(cdiv(std::max<int64_t>(N, 1), g_num_cus()), 16)));
+  // workgroups per CU: 2 where a workgroup has <= 10 waves of one fragment each (two fragments
+  // per wave need more than the 96 VGPRs of 5 waves per SIMD); A/B: AIMX_MLPS_OCC=1|2
+  const bool occ2_ok = pl.NF == 1 && 64 * pl.geo.nw <= kSOcc2Threads;
+  int occ = occ2_ok ? 2 : 1;
+  if (const char* e = getenv("AIMX_MLPS_OCC")) occ = (atoi(e) == 2 && occ2_ok) ? 2 : 1;
+  const int rt_max = occ == 2 ? 4 : (pl.NF == 1 ? 7 : 3);
+  // enough rows per chunk that the chunks fit one round of occ workgroups per CU
+  const int64_t slots = (int64_t)occ * g_num_cus();
+  int rt = (int)std::min<int64_t>(rt_max, std::max<int64_t>(1, cdiv(cdiv(std::max<int64_t>(N, 1), slots), 16)));
   if (const char* e = getenv("AIMX_MLPS_RT")) rt = std::max(1, std::min(rt_max, atoi(e)));  // A/B experiments only
-  // two activation tiles + the forward's bias table (2 nm x 16 CF floats, nm <= 8)
+  // two activation tiles + the forward's bias table (2 nm x 16 CF floats, nm <= 8), per workgroup
   auto lds = [&](int r) { return sizeof(float) * (size_t)(2 * 16 * r * pl.geo.S + 2 * 8 * 16 * CF); };
-  while (rt > 1 && lds(rt) > (size_t)kMlpsDynLds) --rt;
-  if (lds(rt) > (size_t)kMlpsDynLds) return pl;
+  const size_t cap = occ == 2 ? (size_t)(kMlpsDynLds / 2 - 1024) : (size_t)kMlpsDynLds;
+  while (rt > 1 && lds(rt) > cap) --rt;
+  if (lds(rt) > cap) return pl;
+  pl.OCC = occ;
   pl.RT = rt;
   pl.lds = lds(rt);
-  pl.blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(N, 16 * rt), g_num_cus()));
+  pl.blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(N, 16 * rt), slots));
   pl.ok = true;
   return pl;
 }
 
-template <int RT, int NF, int P>
+template <int RT, int NF, int P, int OCC>
 int mlps_launch(const MlpsPlan& pl, const MlpFwd* pf, const MlpBwd* pb, const float* img, hipStream_t st) {
   static const bool set = [] {
-    (void)hipFuncSetAttribute((const void*)k_mlps_fwd<RT, NF, P>, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpsDynLds);
-    (void)hipFuncSetAttribute((const void*)k_mlps_bwd<RT, NF, P>, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpsDynLds);
+    (void)hipFuncSetAttribute((const void*)k_mlps_fwd<RT, NF, P, OCC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kMlpsDynLds / OCC);
+    (void)hipFuncSetAttribute((const void*)k_mlps_bwd<RT, NF, P, OCC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kMlpsDynLds / OCC);
     return true;
   }();
   (void)set;
   const dim3 grid(pl.blocks), block(64 * pl.geo.nw);
   if (pf)
-    hipLaunchKernelGGL((k_mlps_fwd<RT, NF, P>), grid, block, pl.lds, st, *pf, reinterpret_cast<const floatx4*>(img),
-                       pl.geo);
+    hipLaunchKernelGGL((k_mlps_fwd<RT, NF, P, OCC>), grid, block, pl.lds, st, *pf,
+                       reinterpret_cast<const floatx4*>(img), pl.geo);
   else
-    hipLaunchKernelGGL((k_mlps_bwd<RT, NF, P>), grid, block, pl.lds, st, *pb, reinterpret_cast<const floatx4*>(img),
-                       pl.geo);
+    hipLaunchKernelGGL((k_mlps_bwd<RT, NF, P, OCC>), grid, block, pl.lds, st, *pb,
+                       reinterpret_cast<const floatx4*>(img), pl.geo);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
 
 int mlps_dispatch(const MlpsPlan& pl, const MlpFwd* pf, const MlpBwd* pb, const float* img, hipStream_t st) {
-#define AIMX_MLPS_CASE(rt, nf)                                                          \
-  if (pl.RT == rt && pl.NF == nf)                                                       \
-    return pl.P == 5 ? mlps_launch<rt, nf, 5>(pl, pf, pb, img, st) : mlps_launch<rt, nf, 4>(pl, pf, pb, img, st);
-  AIMX_MLPS_CASE(1, 1) AIMX_MLPS_CASE(2, 1) AIMX_MLPS_CASE(3, 1) AIMX_MLPS_CASE(4, 1) AIMX_MLPS_CASE(5, 1)
-  AIMX_MLPS_CASE(6, 1) AIMX_MLPS_CASE(7, 1) AIMX_MLPS_CASE(1, 2) AIMX_MLPS_CASE(2, 2) AIMX_MLPS_CASE(3, 2)
+#define AIMX_MLPS_CASE(rt, nf, occ)                                                                 \
+  if (pl.RT == rt && pl.NF == nf && pl.OCC == occ)                                                  \
+    return pl.P == 5 ? mlps_launch<rt, nf, 5, occ>(pl, pf, pb, img, st) : mlps_launch<rt, nf, 4, occ>(pl, pf, pb, img, st);
+  AIMX_MLPS_CASE(1, 1, 1) AIMX_MLPS_CASE(2, 1, 1) AIMX_MLPS_CASE(3, 1, 1) AIMX_MLPS_CASE(4, 1, 1)
+  AIMX_MLPS_CASE(5, 1, 1) AIMX_MLPS_CASE(6, 1, 1) AIMX_MLPS_CASE(7, 1, 1) AIMX_MLPS_CASE(1, 2, 1)
+  AIMX_MLPS_CASE(2, 2, 1) AIMX_MLPS_CASE(3, 2, 1)
+  AIMX_MLPS_CASE(1, 1, 2) AIMX_MLPS_CASE(2, 1, 2) AIMX_MLPS_CASE(3, 1, 2) AIMX_MLPS_CASE(4, 1, 2)
 #undef AIMX_MLPS_CASE
   return AIMX_EARG;
 }

@@ -1,8 +1,14 @@
 #!/bin/bash
 # round-4 working call (overwritten per call)
 export PYTHONDONTWRITEBYTECODE=1
-R=gpurun_out/r4i
+R=gpurun_out/r4j
 tools/gpu_steps.sh \
- "120 r4i/mlps_trace_c4.log python3 -u tools/mlps_trace.py c4" \
- "120 r4i/mlps_trace_c5.log python3 -u tools/mlps_trace.py c5" \
- "?900 r4i/tests.log python3 -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread"
+ "300 r4j/parity.log python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hop_rows.py -q -x --timeout 200 --timeout-method thread" \
+ "120 r4j/trace_c4.log python3 -u tools/mlps_trace.py c4" \
+ "120 r4j/trace_c4_occ1.log env AIMX_MLPS_OCC=1 python3 -u tools/mlps_trace.py c4" \
+ "120 r4j/trace_c5.log python3 -u tools/mlps_trace.py c5" \
+ "150 r4j/bench_c2.log python3 bench.py --config c2 --steps 100 --warmup 10 --no-cpu-baseline --no-roofline --no-eager" \
+ "200 r4j/bench_c4.log python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline" \
+ "200 r4j/bench_c4_occ1.log env AIMX_MLPS_OCC=1 python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager" \
+ "200 r4j/bench_c5.log python3 bench.py --config c5 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline" \
+ "?900 r4j/tests.log python3 -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread"
