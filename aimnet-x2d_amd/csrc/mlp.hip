@@ -311,6 +311,15 @@ __device__ __forceinline__ void load_rows(float* dst, int S, const float* src, i
   }
 }
 
+// columns [D, Kp) of `rows` LDS rows of stride S set to 0
+__device__ __forceinline__ void mlps_zero_pad(float* t, int rows, int S, int D, int Kp) {
+  const int w = Kp - D;
+  for (int e = threadIdx.x; e < rows * w; e += blockDim.x) {
+    const int r = e / w;
+    t[r * S + D + (e - r * w)] = 0.f;
+  }
+}
+
 // The weight-streamed kernels' chunk load: rows [r0, r0 + R) x cols [0, D) of src (row stride ld)
 // into LDS rows of stride S with every load of a thread in flight at once (one round trip). Thread
 // t owns column t mod D of rows t / D, t / D + RG, ... (RG = blockDim.x / D rows per pass: >= 4 for
@@ -685,7 +694,7 @@ __global__ void k_mlps_pack(const MlpPack p) {
 // One k group of the chain's GEMM stream: acc[t][i] += A(rows of tile t, k group g) . B(k group, fragment i).
 // Row tiles go in pairs (two independent accumulators per B value), each pair's A operands read just
 // before its MFMAs: all RT tiles' A reads in flight at once would hold 4 RT VGPRs.
-template <int RT, int NF>
+template <int RT, int NF, int NA = NF>  // NA: the wave's active fragments (0 .. NA-1 of NF)
 __device__ __forceinline__ void mlps_group(floatx4 (&acc)[RT][NF], const float* As, int S, int g, const floatx4 (&b)[NF]) {
   const int lane = threadIdx.x & 63, lr = lane & 15, lq = 4 * (lane >> 4);
   const float* a0 = As + lr * S + 16 * g + lq;
@@ -701,7 +710,7 @@ __device__ __forceinline__ void mlps_group(floatx4 (&acc)[RT][NF], const float* 
 #pragma unroll
       for (int u = 0; u < kW; ++u)
 #pragma unroll
-        for (int i = 0; i < NF; ++i)
+        for (int i = 0; i < NA; ++i)
           if (t0 + u < RT) acc[t0 + u][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][j], b[i][j], acc[t0 + u][i], 0, 0, 0);
     if (t0 + 2 < RT) __builtin_amdgcn_sched_barrier(0);
   }
@@ -739,9 +748,20 @@ struct BStream {
 // the epilogue's ~3 x 4 RT NF global stores came after them; vmcnt counts stores too, the
 // counter's range was exceeded, and hipcc waited for vmcnt(0) at every loop head: at c4 / c5 the
 // whole ring drained every P groups.)
+// full: every fragment of the wave is real; else its last one lies past CF and its MFMAs are skipped
+// (a wave-uniform branch per k group; fragment counts per SIMD are balanced by the plan, mlps_plan)
+template <int RT, int NF>
+__device__ __forceinline__ void mlps_group_any(floatx4 (&acc)[RT][NF], const float* As, int S, int g,
+                                               const floatx4 (&b)[NF], bool full) {
+  if (NF == 1 || full)
+    mlps_group<RT, NF, NF>(acc, As, S, g, b);
+  else
+    mlps_group<RT, NF, (NF > 1 ? NF - 1 : 1)>(acc, As, S, g, b);
+}
+
 template <int RT, int NF, int P>
 __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring)[P][NF], BStream<NF>& bs, const float* As,
-                                          int S, int G) {
+                                          int S, int G, bool full) {
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -749,7 +769,7 @@ __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring
   for (int g0 = 0; g0 < G - P; g0 += P) {
 #pragma unroll
     for (int q = 0; q < P; ++q) {
-      mlps_group<RT, NF>(acc, As, S, g0 + q, ring[q]);
+      mlps_group_any<RT, NF>(acc, As, S, g0 + q, ring[q], full);
       // refill the slot only after its MFMAs have read it: the load then targets the same registers
       // (a refill issued before the last read needs fresh registers and a copy at the loop's back
       // edge, and copying a register with a load in flight waits for that load)
@@ -759,7 +779,7 @@ __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring
   }
 #pragma unroll
   for (int q = 0; q < P; ++q) {
-    mlps_group<RT, NF>(acc, As, S, G - P + q, ring[q]);
+    mlps_group_any<RT, NF>(acc, As, S, G - P + q, ring[q], full);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -816,13 +836,15 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
     fok[i] = wave + i * nw < CF && 16 * (wave + i * nw) + lr < D;
     fr[i] = min(wave + i * nw, CF - 1);
   }
+  // all NF fragments real (wave-uniform: readfirstlane)
+  const bool full = __builtin_amdgcn_readfirstlane(wave + (NF - 1) * nw) < CF;
   const float scale = drop_scale(p.drop_p);
   const uint64_t seed = p.drop ? (uint64_t)*p.seed : 0;
   // the last block's residual operands as buffer loads (an absent x reads 0: no branch per load)
   const __amdgpu_buffer_rsrc_t rug = mlp_rsrc(p.ug, (uint32_t)(4 * N * 2 * D));
   const __amdgpu_buffer_rsrc_t rx_ = mlp_rsrc(p.x, p.x ? (uint32_t)(4 * ((N - 1) * p.ldx + D)) : 0u);
-  // k padding of both tiles (the chunk loads and the epilogues write columns < D only)
-  for (int e = threadIdx.x; e < 2 * R * S; e += blockDim.x) Xa[e] = 0.f;
+  // k padding (columns D .. 16 G) of both tiles: the chunk loads and the epilogues write columns < D only
+  mlps_zero_pad(Xa, 2 * R, S, D, 16 * G);
   MLPS_STAMP(0, 1);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
@@ -861,7 +883,7 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
             }
           }
       }
-      mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G);
+      mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G, full);
       MLPS_STAMP(0, 3 + 3 * ph);
       // everything the epilogue addresses derives from these opaque copies, so none of it is
       // computed ahead of the GEMM and held across it
@@ -958,8 +980,10 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
     fok[i] = wave + i * nw < CF && 16 * (wave + i * nw) + lr < D;
     fr[i] = min(wave + i * nw, CF - 1);
   }
+  // all NF fragments real (wave-uniform: readfirstlane)
+  const bool full = __builtin_amdgcn_readfirstlane(wave + (NF - 1) * nw) < CF;
   const float scale = drop_scale(p.drop_p);
-  for (int e = threadIdx.x; e < 2 * R * S; e += blockDim.x) DA[e] = 0.f;  // k padding of DA and DV
+  mlps_zero_pad(DA, 2 * R, S, D, 16 * G);  // k padding of DA and DV
   MLPS_STAMP(1, 1);
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
@@ -997,7 +1021,7 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
             }
           }
       }
-      mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G);
+      mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G, full);
       MLPS_STAMP(1, 3 + 3 * ph);
       int lo = lane;  // opaque copies: see k_mlps_fwd
       asm volatile("" : "+s"(r0), "+v"(lo));
@@ -1109,7 +1133,27 @@ MlpsPlan mlps_plan(int64_t N, int64_t D) {
   MlpsPlan pl{};
   const int CF = (int)cdiv(D, 16);
   if (D < 1 || CF > 24) return pl;  // beyond 2 fragments per wave: the per-GEMM path
-  pl.NF = CF <= 12 ? 1 : 2;
+  // waves and fragments per wave: wave w owns fragments w, w + nw, ...; the SIMD running waves
+  // s, s + 4, ... carries the sum of their fragment counts. One fragment per wave up to 12; above,
+  // two per wave with as many waves (<= 12) as leave the busiest SIMD the fewest fragments (c5's
+  // 20: 12 waves, 8 of two fragments and 4 of one -> 5 per SIMD, where 10 waves of two put 6 on two
+  // SIMDs and 4 on the others); a wave whose second fragment lies past CF skips its MFMAs
+  auto busiest = [&](int nw) {
+    int m = 0;
+    for (int sd = 0; sd < 4; ++sd) {
+      int f = 0;
+      for (int w = sd; w < nw; w += 4) f += (int)cdiv(std::max(CF - w, 0), nw);
+      m = std::max(m, f);
+    }
+    return m;
+  };
+  int nw = CF;
+  if (CF > 12) {
+    int best = 1 << 30;
+    for (int cand = (int)cdiv(CF, 2); cand <= kSMaxThreads / 64; ++cand)
+      if (busiest(cand) < best) best = busiest(cand), nw = cand;
+  }
+  pl.NF = (int)cdiv(CF, nw);
   pl.geo.CF = CF;
   // ring depth P in {5, 4}: the k groups per GEMM rounded up to a multiple of it (fewer zero groups
   // first, then the deeper ring)
@@ -1117,11 +1161,13 @@ MlpsPlan mlps_plan(int64_t N, int64_t D) {
   pl.P = g5 <= g4 ? 5 : 4;
   pl.geo.G = std::min(g5, g4);
   pl.geo.S = 16 * pl.geo.G + 4;
-  pl.geo.nw = (int)cdiv(CF, pl.NF);
+  pl.geo.nw = nw;
   // workgroups per CU: 2 where a workgroup has <= 10 waves of one fragment each (two fragments
   // per wave need more than the 96 VGPRs of 5 waves per SIMD); A/B: AIMX_MLPS_OCC=1|2
+  // (measured: c4 step 2.894 ms with two, 2.888 with one — a workgroup alone on its CU finishes
+  // sooner, but 430 chunks of 3 row tiles leave the CUs holding two of them the busiest; default 1)
   const bool occ2_ok = pl.NF == 1 && 64 * pl.geo.nw <= kSOcc2Threads;
-  int occ = occ2_ok ? 2 : 1;
+  int occ = 1;
   if (const char* e = getenv("AIMX_MLPS_OCC")) occ = (atoi(e) == 2 && occ2_ok) ? 2 : 1;
   const int rt_max = occ == 2 ? 4 : (pl.NF == 1 ? 7 : 3);
   // enough rows per chunk that the chunks fit one round of occ workgroups per CU
