@@ -759,9 +759,12 @@ __device__ __forceinline__ void mlps_group_any(floatx4 (&acc)[RT][NF], const flo
     mlps_group<RT, NF, (NF > 1 ? NF - 1 : 1)>(acc, As, S, g, b);
 }
 
-template <int RT, int NF, int P>
+// tail(): the epilogue's operand loads, issued before the last P k groups, which load nothing
+// themselves — issued before the GEMM they queued ahead of the ring's loads and slowed every k group
+// (c4: the GEMMs carrying them took 4-5 us longer)
+template <int RT, int NF, int P, class Tail>
 __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring)[P][NF], BStream<NF>& bs, const float* As,
-                                          int S, int G, bool full) {
+                                          int S, int G, bool full, Tail&& tail) {
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -777,6 +780,8 @@ __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  tail();
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int q = 0; q < P; ++q) {
     mlps_group_any<RT, NF>(acc, As, S, G - P + q, ring[q], full);
@@ -864,26 +869,29 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
       asm volatile("" : "+s"(r0));
       const int k = ph >> 1;
       const bool w1 = (ph & 1) == 0, last = ph == nph - 1;
-      // epilogue operands, in flight during the GEMM (consumed only in the epilogue: an add here
-      // would wait for the loads at once): bias; after the last block g and x
+      // epilogue operands, in flight during the GEMM's last k groups (consumed only in the epilogue:
+      // an add there would wait for the loads at once): bias; after the last block g and x (every
+      // other GEMM points them past the buffers' extents: no branch around loads)
       float bia[NF], rg[RT][NF][4], rx[RT][NF][4];
 #pragma unroll
       for (int i = 0; i < NF; ++i) bia[i] = Bia[ph * 16 * CF + 16 * fr[i] + lr];
-      if (kPre && last) {
+      auto tail = [&]() {
+        if constexpr (kPre) {
 #pragma unroll
-        for (int t = 0; t < RT; ++t)
+          for (int t = 0; t < RT; ++t)
 #pragma unroll
-          for (int i = 0; i < NF; ++i) {
-            const int c = min(16 * fr[i] + lr, D - 1);
+            for (int i = 0; i < NF; ++i) {
+              const int c = min(16 * fr[i] + lr, D - 1);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t gr = (uint32_t)min(r0 + 16 * t + lq + r, N - 1);
-              rg[t][i][r] = bload(rug, 4u * (gr * (uint32_t)(2 * D) + (uint32_t)(D + c)));
-              rx[t][i][r] = bload(rx_, 4u * (gr * (uint32_t)p.ldx + (uint32_t)c));  // 0 without x
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t gr = (uint32_t)min(r0 + 16 * t + lq + r, N - 1);
+                rg[t][i][r] = bload(rug, last ? 4u * (gr * (uint32_t)(2 * D) + (uint32_t)(D + c)) : 0xFFFFFFF0u);
+                rx[t][i][r] = bload(rx_, last ? 4u * (gr * (uint32_t)p.ldx + (uint32_t)c) : 0xFFFFFFF0u);  // 0 without x
+              }
             }
-          }
-      }
-      mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G, full);
+        }
+      };
+      mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G, full, tail);
       MLPS_STAMP(0, 3 + 3 * ph);
       // everything the epilogue addresses derives from these opaque copies, so none of it is
       // computed ahead of the GEMM and held across it
@@ -966,7 +974,8 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
   extern __shared__ __attribute__((aligned(16))) float lds[];
   MLPS_STAMP(1, 0);
   constexpr int R = 16 * RT;
-  constexpr bool kPre = OCC == 1 && (NF == 1 || RT <= 2);  // as in k_mlps_fwd
+  // as in k_mlps_fwd; v and mask held through the last k groups: up to RT = 5 (above, spills)
+  constexpr bool kPre = OCC == 1 && (NF == 1 ? RT <= 5 : RT <= 2);
   const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
   float* DA = lds;          // gradient w.r.t. the current block output [R][S]
   float* DV = lds + R * S;  // dV_k                                     [R][S]
@@ -1001,27 +1010,31 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
       asm volatile("" : "+s"(r0));
       const int k = nm - 1 - (ph >> 1);
       const bool dv = (ph & 1) == 0;
-      // epilogue operands, in flight during the GEMM (raw: any arithmetic here would wait for the
-      // loads at once): dV: v and the dropout mask; dA of block 0: u
+      // epilogue operands, in flight during the GEMM's last k groups (raw: any arithmetic there
+      // would wait for the loads at once): dV: v and the dropout mask; dA of block 0: u. Loaded
+      // unconditionally (address selects: element 0 where unused; the mask is read only with dropout)
       float ev[RT][NF][4];
       uint32_t em[RT][NF][4];
-      if (kPre && (dv || k == 0)) {
-        const gfloat* V = (const gfloat*)(dv ? pick8(p.V, k) : p.u);
-        const gu8* M = (const gu8*)pick8(p.M, k);
+      auto tail = [&]() {
+        if constexpr (kPre) {
+          const bool need = dv || k == 0;
+          const gfloat* V = (const gfloat*)(dv ? pick8(p.V, k) : p.u);
+          const gu8* M = p.drop ? (const gu8*)pick8(p.M, k) : (const gu8*)V;
 #pragma unroll
-        for (int t = 0; t < RT; ++t)
+          for (int t = 0; t < RT; ++t)
 #pragma unroll
-          for (int i = 0; i < NF; ++i) {
-            const uint32_t c = (uint32_t)min(16 * fr[i] + lr, D - 1);
+            for (int i = 0; i < NF; ++i) {
+              const uint32_t c = (uint32_t)min(16 * fr[i] + lr, D - 1);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t o = (uint32_t)min(r0 + 16 * t + lq + r, N - 1) * (uint32_t)D + c;
-              ev[t][i][r] = V[o];
-              em[t][i][r] = (dv && p.drop) ? (uint32_t)M[o] : 1u;
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t o = (uint32_t)min(r0 + 16 * t + lq + r, N - 1) * (uint32_t)D + c;
+                ev[t][i][r] = V[need ? o : 0u];
+                em[t][i][r] = (uint32_t)M[dv ? o : 0u];
+              }
             }
-          }
-      }
-      mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G, full);
+        }
+      };
+      mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G, full, tail);
       MLPS_STAMP(1, 3 + 3 * ph);
       int lo = lane;  // opaque copies: see k_mlps_fwd
       asm volatile("" : "+s"(r0), "+v"(lo));
