@@ -146,6 +146,14 @@ __device__ __forceinline__ float mlp_bload(__amdgpu_buffer_rsrc_t r, uint32_t of
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off) { return mlp_bload(r, off); }
+// buffer stores: an offset past the extent drops the store (rows past N without a branch per element)
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore_u8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, r, off, 0, 0);
+}
+constexpr uint32_t kDrop = 0xFFFFFFF0u;  // a buffer offset past every extent
 
 template <bool TR>
 __device__ __forceinline__ void fill_lds(float* Wl, const float* const* wtab, int nmat, int D, int Kp, int S,
@@ -898,10 +906,10 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
       int lo = lane;
       asm volatile("" : "+s"(r0), "+v"(lo));
       const int lr = lo & 15, lq = 4 * (lo >> 4);
+      const uint32_t nd = (uint32_t)(N * D);
       if (w1) {  // v = a W1^T + b1 ; r = dropout(act(v))
-        gfloat* V = (gfloat*)pick8(p.V, k);
-        gfloat* Rk = (gfloat*)pick8(p.R, k);
-        gu8* M = (gu8*)pick8(p.M, k);
+        const __amdgpu_buffer_rsrc_t rV = mlp_rsrc(pick8(p.V, k), 4u * nd), rR = mlp_rsrc(pick8(p.R, k), 4u * nd);
+        const __amdgpu_buffer_rsrc_t rM = mlp_rsrc(pick8(p.M, k), p.drop ? nd : 0u);
         const uint32_t salt = (uint32_t)(p.salt0 + k);
 #pragma unroll
         for (int t = 0; t < RT; ++t)
@@ -914,22 +922,23 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
               const int row = 16 * t + lq + r;
               const int64_t gr = r0 + row;
               const uint32_t o = (uint32_t)gr * (uint32_t)D + (uint32_t)c;
+              const bool in = gr < N;
               const float v = acc[t][i][r] + bia[i];
               float a = act_fwd(p.act, v);
               if (p.drop) {
                 const bool keep = hash_uniform(seed, salt, (uint64_t)o) >= p.drop_p;
                 a = keep ? a * scale : 0.f;
-                if (gr < N) M[o] = keep ? 1 : 0;
+                bstore_u8(rM, in ? o : kDrop, keep ? 1u : 0u);
               }
               Hb[row * S + c] = a;
-              if (gr < N) {
-                V[o] = v;
-                Rk[o] = a;
-              }
+              bstore(rV, in ? 4u * o : kDrop, v);
+              bstore(rR, in ? 4u * o : kDrop, a);
             }
           }
       } else {  // a_{k+1} = r W2^T + b2 + a_k (+ g + x after the last block)
-        gfloat* Ak = (gfloat*)pick8(p.A, k);
+        const uint32_t ldo = last ? (uint32_t)p.ldo : (uint32_t)D;
+        const __amdgpu_buffer_rsrc_t rO = last ? mlp_rsrc(p.out, 4u * (uint32_t)((N - 1) * p.ldo + D))
+                                               : mlp_rsrc(pick8(p.A, k), 4u * nd);
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -951,12 +960,7 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
                 }
               }
               Xa[row * S + c] = a;
-              if (gr < N) {
-                if (last)
-                  p.out[(uint32_t)gr * (uint32_t)p.ldo + (uint32_t)c] = a;
-                else
-                  Ak[(uint32_t)gr * (uint32_t)D + (uint32_t)c] = a;
-              }
+              bstore(rO, gr < N ? 4u * ((uint32_t)gr * ldo + (uint32_t)c) : kDrop, a);
             }
           }
       }
@@ -1039,8 +1043,9 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
       int lo = lane;  // opaque copies: see k_mlps_fwd
       asm volatile("" : "+s"(r0), "+v"(lo));
       const int lr = lo & 15, lq = 4 * (lo >> 4);
+      const uint32_t nd = (uint32_t)(N * D);
       if (dv) {  // dV = (dA W2) * mask/(1-p) * act'(v)
-        gfloat* dVk = (gfloat*)pick8(p.dV, k);
+        const __amdgpu_buffer_rsrc_t rdV = mlp_rsrc(pick8(p.dV, k), 4u * nd);
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -1061,11 +1066,12 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
               const float m = p.drop ? (mk ? scale : 0.f) : 1.f;
               const float d = (gr < N) ? acc[t][i][r] * m * act_grad(p.act, v) : 0.f;
               DV[row * S + c] = d;
-              if (gr < N) dVk[(uint32_t)gr * (uint32_t)D + (uint32_t)c] = d;
+              bstore(rdV, gr < N ? 4u * ((uint32_t)gr * (uint32_t)D + (uint32_t)c) : kDrop, d);
             }
           }
       } else {  // dA_k = dA_{k+1} + dV W1 ; k == 0: du = dA_0 act'(u) -> dUG[:, :D]
-        gfloat* dAk = (gfloat*)pick8(p.dA, max(k - 1, 0));
+        const uint32_t ldd = k > 0 ? (uint32_t)D : (uint32_t)(2 * D);
+        const __amdgpu_buffer_rsrc_t rdA = k > 0 ? mlp_rsrc(pick8(p.dA, k - 1), 4u * nd) : mlp_rsrc(p.dug, 8u * nd);
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -1078,13 +1084,11 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
               const int64_t gr = r0 + row;
               const float da = DA[row * S + c] + acc[t][i][r];
               DA[row * S + c] = da;
-              if (gr < N) {
-                if (k > 0)
-                  dAk[(uint32_t)gr * (uint32_t)D + (uint32_t)c] = da;
-                else
-                  p.dug[(uint32_t)gr * (uint32_t)(2 * D) + (uint32_t)c] =
-                      da * act_grad(p.act, kPre ? ev[t][i][r] : p.u[(uint32_t)gr * (uint32_t)D + (uint32_t)c]);
-              }
+              float o = da;
+              if (k == 0)
+                o = da * act_grad(p.act, kPre ? ev[t][i][r]
+                                              : p.u[(uint32_t)min(gr, N - 1) * (uint32_t)D + (uint32_t)c]);
+              bstore(rdA, gr < N ? 4u * ((uint32_t)gr * ldd + (uint32_t)c) : kDrop, o);
             }
           }
       }

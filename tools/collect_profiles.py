@@ -55,3 +55,24 @@ for cfgname in ("c2", "c4", "c5"):
             f.write(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_summary.py"),
                                     os.path.join(src, f"{cfgname}_mfma"), "15"], capture_output=True, text=True,
                                    check=True).stdout)
+# step kernel sequences (default bench command = c2, c4, c5), the parity report, the DDP lines,
+# the k_mlps phase stamps and the GPU suite's summary (part c)
+for name, out in (("bench_step_seq.txt", "c2_step_seq.txt"), ("c4_trace_step_seq.txt", "c4_step_seq.txt"),
+                  ("c5_trace_step_seq.txt", "c5_step_seq.txt"), ("parity.json", "parity.json"),
+                  ("mlps_trace_c4.log", "mlps_trace_c4.txt"), ("mlps_trace_c5.log", "mlps_trace_c5.txt")):
+    p = os.path.join(src, name)
+    if os.path.exists(p):
+        with open(p) as fi, open(os.path.join(dst, f"{tag}_{out}"), "w") as fo:
+            fo.write("".join(ln for ln in fi if "amdgpu.ids" not in ln))
+for name in ("bench_ddp_world1", "bench_dp2_gloo"):
+    p = os.path.join(src, f"{name}.log")
+    if os.path.exists(p):
+        lines = [ln for ln in open(p) if ln.startswith("{")]
+        if lines:
+            with open(os.path.join(dst, f"{tag}_{name}.json"), "w") as f:
+                f.write(lines[-1])
+p = os.path.join(src, "tests.log")
+if os.path.exists(p):
+    tail = [ln for ln in open(p) if "passed" in ln or "failed" in ln or ln.startswith("FAILED")]
+    with open(os.path.join(dst, f"{tag}_gpu_tests.txt"), "w") as f:
+        f.write("".join(tail[-20:]))

@@ -1,29 +1,49 @@
 #!/bin/bash
-# Round profile set (run on the GPU box): kernel trace + stats of the default bench command, the
-# hop roofline launches alone, and the two PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic.
+# Round profile set (run on the GPU box), in parts that each fit one gpurun call:
+#   a: kernel trace + stats of the default bench command, the hop roofline launches alone, the two
+#      PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic, the default bench line;
+#   b: c3/c4/c5 bench lines (fp32, AMP for c2/c4/c5), step traces of c4/c5, MFMA-busy PMC passes on
+#      c2, c4 and c5 (whole-step MFMA utilisation against chip peak);
+#   c: the per-tensor parity report, the DDP lines (world-size-1 RCCL with the DDP-wrapped autograph
+#      leg; two gloo ranks sharing the GPU), the k_mlps phase stamps, smoke and the whole -m gpu suite.
 # Outputs under gpurun_out/round/; tools/collect_profiles.py copies the summaries into profiles/.
-# Extra (after the core set): the c3/c4/c5 bench lines (fp32 and AMP) and MFMA-busy PMC passes on
-# c2, c4 and c5 (whole-step MFMA utilisation against chip peak).
+# usage: tools/profile_round.sh a|b|c
 set -o pipefail
-# usage: tools/profile_round.sh [FIRST]  (FIRST: 0-based index of the first step to run, to resume)
 R=gpurun_out/round
 mkdir -p $R
-STEPS=(
+A=(
   "900 round/bench.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/bench -- python3 bench.py --no-cpu-baseline"
   "600 round/roof.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/roof -- python3 bench.py --roofline-only"
   "600 round/pmc_fetch.log rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/pmc_fetch -- python3 bench.py --roofline-only"
   "600 round/pmc_write.log rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/pmc_write -- python3 bench.py --roofline-only"
   "900 round/bench_plain.log python3 bench.py"
+)
+B=(
   "300 round/bench_c3.log python3 bench.py --config c3 --no-cpu-baseline --no-roofline --no-eager"
   "300 round/bench_c4.log python3 bench.py --config c4 --no-cpu-baseline"
   "300 round/bench_c5.log python3 bench.py --config c5 --no-cpu-baseline"
   "300 round/bench_c2_amp.log python3 bench.py --amp --no-cpu-baseline --no-roofline"
   "300 round/bench_c4_amp.log python3 bench.py --config c4 --amp --no-cpu-baseline --no-roofline"
   "300 round/bench_c5_amp.log python3 bench.py --config c5 --amp --no-cpu-baseline --no-roofline"
-  "120 round/counters.log rocprofv3 -L"
   "600 round/c4_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/c4_trace -- python3 bench.py --config c4 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
+  "600 round/c5_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/c5_trace -- python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
+  "120 round/seq.log bash -c 'for c in bench c4_trace c5_trace; do python3 tools/step_seq.py $R/\$c > $R/\${c}_step_seq.txt; done'"
   "600 round/c2_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c2_mfma -- python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
   "600 round/c4_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c4_mfma -- python3 bench.py --config c4 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
   "600 round/c5_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c5_mfma -- python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
 )
-tools/gpu_steps.sh "${STEPS[@]:${1:-0}}"
+C=(
+  "600 round/parity_report.log python3 -u tools/parity_report.py --out $R/parity.json"
+  "300 round/bench_ddp_world1.log python3 bench.py --ddp-world1 --no-cpu-baseline --no-roofline"
+  "300 round/bench_dp2_gloo.log python3 bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-eager"
+  "120 round/mlps_trace_c4.log python3 -u tools/mlps_trace.py c4"
+  "120 round/mlps_trace_c5.log python3 -u tools/mlps_trace.py c5"
+  "300 round/smoke.log python3 -c 'import __graft_entry__ as g; g.smoke()'"
+  "?900 round/tests.log python3 -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread"
+)
+case "$1" in
+  a) tools/gpu_steps.sh "${A[@]}" ;;
+  b) tools/gpu_steps.sh "${B[@]}" ;;
+  c) tools/gpu_steps.sh "${C[@]}" ;;
+  *) echo "usage: $0 a|b|c" >&2; exit 2 ;;
+esac
