@@ -1064,6 +1064,19 @@ struct WbTable {
   int32_t xcd;  // XCD-aware work order (AIMX_WGRAD_XCD=0: launch order, for A/B)
 };
 
+#ifdef AIMX_WB_TRACE  // diagnostics build only: per-wave shader-clock totals of k_wgrad_lds phases
+// [traced workgroup][wave][phase: put (waits for the fill's loads), fetch (issue), compute, barrier, total]
+__device__ long long g_wb_trace[4][10][5];
+#define WBT(slot, stmt)                                         \
+  do {                                                          \
+    const long long t0_ = (long long)__builtin_readcyclecounter(); \
+    stmt;                                                       \
+    wbt[slot] += (long long)__builtin_readcyclecounter() - t0_; \
+  } while (0)
+#else
+#define WBT(slot, stmt) stmt
+#endif
+
 // DB: two LDS buffers per operand (80-wide blocks only: 40 KiB, four workgroups fill a CU's
 // 160 KiB). Fill s + 1 is written to the idle buffer while fill s computes from the other, so each
 // fill costs one workgroup barrier instead of two and the LDS writes overlap other waves' MFMAs.
@@ -1219,6 +1232,10 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
     }
 #endif
   };
+#ifdef AIMX_WB_TRACE
+  long long wbt[5] = {0, 0, 0, 0, 0};
+  const long long wbt0 = (long long)__builtin_readcyclecounter();
+#endif
 #pragma unroll
   for (int d = 0; d < kWbD; ++d)
     fetch(kb + d * kWbK, ring[d]);
@@ -1226,25 +1243,25 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
     static_assert(kWbD == 2, "the double-buffered schedule keeps two fills in registers");
     // fill s computes from buffer s & 1; fill s + 1 (loaded two compute periods earlier) goes to
     // the other buffer first, and its register slot is refilled with fill s + 3
-    put(ring[0], kb, sA, sB);
-    fetch(kb + 2 * kWbK, ring[0]);
-    __syncthreads();
+    WBT(0, put(ring[0], kb, sA, sB));
+    WBT(1, fetch(kb + 2 * kWbK, ring[0]));
+    WBT(3, __syncthreads());
     // put and fetch run unconditionally (fills past the slice are zeros, put into the idle
     // buffer): with them under a condition, the paths into the loop head differ in their pending
     // loads and hipcc waits for all of them there (vmcnt(0)), ending every fill's prefetch
     // (sched_barrier: the fills' loads issue before the compute; hipcc would sink them below it)
     for (int s0 = 0; s0 < nsub; s0 += 2) {
-      put(ring[1], kb + (s0 + 1) * kWbK, sA + kBuf, sB + kBuf);
-      fetch(kb + (s0 + 3) * kWbK, ring[1]);
+      WBT(0, put(ring[1], kb + (s0 + 1) * kWbK, sA + kBuf, sB + kBuf));
+      WBT(1, fetch(kb + (s0 + 3) * kWbK, ring[1]));
       __builtin_amdgcn_sched_barrier(0);
-      compute(sA, sB);
-      __syncthreads();  // fill s0 + 1 visible; every read of buffer 0 done before it is refilled
+      WBT(2, compute(sA, sB));
+      WBT(3, __syncthreads());  // fill s0 + 1 visible; every read of buffer 0 done before it is refilled
       if (s0 + 1 >= nsub) break;
-      put(ring[0], kb + (s0 + 2) * kWbK, sA, sB);
-      fetch(kb + (s0 + 4) * kWbK, ring[0]);
+      WBT(0, put(ring[0], kb + (s0 + 2) * kWbK, sA, sB));
+      WBT(1, fetch(kb + (s0 + 4) * kWbK, ring[0]));
       __builtin_amdgcn_sched_barrier(0);
-      compute(sA + kBuf, sB + kBuf);
-      __syncthreads();
+      WBT(2, compute(sA + kBuf, sB + kBuf));
+      WBT(3, __syncthreads());
     }
   } else {
     // kWbD fills in flight: fill s lands in register slot s % kWbD, is copied to LDS kWbD - 1
@@ -1263,6 +1280,14 @@ __global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, fl
     }
   }
 
+#ifdef AIMX_WB_TRACE
+  {
+    const int slot = blockIdx.x == 0 ? 0 : blockIdx.x == 777 ? 1 : blockIdx.x == 2222 ? 2 : blockIdx.x == 4444 ? 3 : -1;
+    wbt[4] = (long long)__builtin_readcyclecounter() - wbt0;
+    if (slot >= 0 && lane == 0 && w < 10)
+      for (int i = 0; i < 5; ++i) __builtin_nontemporal_store(wbt[i], &g_wb_trace[slot][w][i]);
+  }
+#endif
   if (S > 1) {
     const __amdgpu_buffer_rsrc_t rws = make_rsrc(ws + t.ws_off[q], (uint32_t)(4 * (int64_t)S * nb * G::Slab));
     const uint32_t own = 16u * (uint32_t)((w * kWbF) * 64 + lane);
@@ -1791,3 +1816,9 @@ extern "C" int aimx_gemm(const AimxGemmArgs* a, aimx_stream_t stream) {
   if (!a) return AIMX_EARG;
   return aimx::launch_gemm(*a, (hipStream_t)stream);
 }
+
+#ifdef AIMX_WB_TRACE
+extern "C" int aimx_wb_trace_read(long long* out) {  // 4 x 10 x 5 shader-clock totals
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(aimx::g_wb_trace), sizeof(long long) * 4 * 10 * 5) == hipSuccess ? 0 : -1;
+}
+#endif
