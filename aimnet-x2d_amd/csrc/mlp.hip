@@ -640,9 +640,6 @@ namespace {
 // per row tile feeds 4 MFMAs). Epilogues, dropout hash, salts and outputs (V, R, M, A, out / dV, dA,
 // dUG) are the per-GEMM path's.
 constexpr int kSMaxThreads = 768;                // <= 12 waves: up to 170 VGPRs per lane
-// two workgroups per CU (OCC = 2): <= 10 waves each, 5 per SIMD, <= 102 VGPRs per lane, half the LDS
-// each, so one workgroup's chunk load, epilogues and barriers overlap the other's MFMA phases
-constexpr int kSOcc2Threads = 640;
 constexpr int kMlpsDynLds = 160 * 1024 - 1024;   // + the static pointer tables
 
 #ifdef AIMX_MLPS_TRACE  // diagnostics build only: per-wave phase timestamps of two workgroups
@@ -767,12 +764,9 @@ __device__ __forceinline__ void mlps_group_any(floatx4 (&acc)[RT][NF], const flo
     mlps_group<RT, NF, (NF > 1 ? NF - 1 : 1)>(acc, As, S, g, b);
 }
 
-// tail(): the epilogue's operand loads, issued before the last P k groups, which load nothing
-// themselves — issued before the GEMM they queued ahead of the ring's loads and slowed every k group
-// (c4: the GEMMs carrying them took 4-5 us longer)
-template <int RT, int NF, int P, class Tail>
+template <int RT, int NF, int P>
 __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring)[P][NF], BStream<NF>& bs, const float* As,
-                                          int S, int G, bool full, Tail&& tail) {
+                                          int S, int G, bool full) {
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -788,8 +782,6 @@ __device__ __forceinline__ void mlps_gemm(floatx4 (&acc)[RT][NF], floatx4 (&ring
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  tail();
-  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int q = 0; q < P; ++q) {
     mlps_group_any<RT, NF>(acc, As, S, G - P + q, ring[q], full);
@@ -821,15 +813,13 @@ __device__ __forceinline__ T pick8(T const (&a)[8], int k) {
   return r;
 }
 
-template <int RT, int NF, int P, int OCC>
-__global__ __launch_bounds__(OCC == 1 ? kSMaxThreads : kSOcc2Threads) __attribute__((amdgpu_waves_per_eu(OCC == 1 ? 1 : 5)))
-void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo) {
+template <int RT, int NF, int P>
+__global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   MLPS_STAMP(0, 0);
   constexpr int R = 16 * RT;
   // epilogue operands prefetched into registers during the GEMM where they fit (else loaded in the
   // epilogue): 8 RT NF VGPRs
-  constexpr bool kPre = OCC == 1 && (NF == 1 || RT <= 2);  // two per CU: the other workgroup hides the loads
   const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
   float* Xa = lds;              // block input a_k [R][S]
   float* Hb = lds + R * S;      // r_k             [R][S]
@@ -877,29 +867,10 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
       asm volatile("" : "+s"(r0));
       const int k = ph >> 1;
       const bool w1 = (ph & 1) == 0, last = ph == nph - 1;
-      // epilogue operands, in flight during the GEMM's last k groups (consumed only in the epilogue:
-      // an add there would wait for the loads at once): bias; after the last block g and x (every
-      // other GEMM points them past the buffers' extents: no branch around loads)
-      float bia[NF], rg[RT][NF][4], rx[RT][NF][4];
+      float bia[NF];
 #pragma unroll
       for (int i = 0; i < NF; ++i) bia[i] = Bia[ph * 16 * CF + 16 * fr[i] + lr];
-      auto tail = [&]() {
-        if constexpr (kPre) {
-#pragma unroll
-          for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int i = 0; i < NF; ++i) {
-              const int c = min(16 * fr[i] + lr, D - 1);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const uint32_t gr = (uint32_t)min(r0 + 16 * t + lq + r, N - 1);
-                rg[t][i][r] = bload(rug, last ? 4u * (gr * (uint32_t)(2 * D) + (uint32_t)(D + c)) : 0xFFFFFFF0u);
-                rx[t][i][r] = bload(rx_, last ? 4u * (gr * (uint32_t)p.ldx + (uint32_t)c) : 0xFFFFFFF0u);  // 0 without x
-              }
-            }
-        }
-      };
-      mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G, full, tail);
+      mlps_gemm<RT, NF, P>(acc, ring, bs, w1 ? Xa : Hb, S, G, full);
       MLPS_STAMP(0, 3 + 3 * ph);
       // everything the epilogue addresses derives from these opaque copies, so none of it is
       // computed ahead of the GEMM and held across it
@@ -939,30 +910,38 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
         const uint32_t ldo = last ? (uint32_t)p.ldo : (uint32_t)D;
         const __amdgpu_buffer_rsrc_t rO = last ? mlp_rsrc(p.out, 4u * (uint32_t)((N - 1) * p.ldo + D))
                                                : mlp_rsrc(pick8(p.A, k), 4u * nd);
+        // the last block's residual operands g and x, a fragment's loads all issued before their
+        // first use (one round trip per fragment). Loaded during the GEMM instead, they slowed its k
+        // loop by more (queued ahead of the weight ring's loads, or stalling the MFMAs' issue in a
+        // burst: c4 +4-5 us); all fragments at once held too many registers for NF = 2
 #pragma unroll
-        for (int t = 0; t < RT; ++t)
+        for (int i = 0; i < NF; ++i) {
+          float rg[RT][4], rx[RT][4];
+          if (last) {
+            const int c = min(16 * fr[i] + lr, D - 1);
 #pragma unroll
-          for (int i = 0; i < NF; ++i) {
-            if (!fok[i]) continue;
-            const int c = 16 * fr[i] + lr;
+            for (int t = 0; t < RT; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t gq = (uint32_t)min(r0 + 16 * t + lq + r, N - 1);
+                rg[t][r] = bload(rug, 4u * (gq * (uint32_t)(2 * D) + (uint32_t)(D + c)));
+                rx[t][r] = bload(rx_, 4u * (gq * (uint32_t)p.ldx + (uint32_t)c));  // 0 without x
+              }
+          }
+          if (!fok[i]) continue;
+          const int c = 16 * fr[i] + lr;
+#pragma unroll
+          for (int t = 0; t < RT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int row = 16 * t + lq + r;
               const int64_t gr = r0 + row;
               float a = (acc[t][i][r] + bia[i]) + Xa[row * S + c];
-              if (last) {
-                if (kPre) {
-                  a = (a + rg[t][i][r]) + rx[t][i][r];
-                } else {
-                  const uint32_t gq = (uint32_t)min(gr, N - 1);
-                  a = (a + bload(rug, 4u * (gq * (uint32_t)(2 * D) + (uint32_t)(D + c)))) +
-                      bload(rx_, 4u * (gq * (uint32_t)p.ldx + (uint32_t)c));
-                }
-              }
+              if (last) a = (a + rg[t][r]) + rx[t][r];
               Xa[row * S + c] = a;
               bstore(rO, gr < N ? 4u * ((uint32_t)gr * ldo + (uint32_t)c) : kDrop, a);
             }
-          }
+        }
       }
       MLPS_STAMP(0, 4 + 3 * ph);
       mlps_refill<NF, P>(ring, bs);
@@ -972,14 +951,11 @@ void k_mlps_fwd(const MlpFwd p, const floatx4* __restrict__ img, const SGeom geo
   }
 }
 
-template <int RT, int NF, int P, int OCC>
-__global__ __launch_bounds__(OCC == 1 ? kSMaxThreads : kSOcc2Threads) __attribute__((amdgpu_waves_per_eu(OCC == 1 ? 1 : 5)))
-void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo) {
+template <int RT, int NF, int P>
+__global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   MLPS_STAMP(1, 0);
   constexpr int R = 16 * RT;
-  // as in k_mlps_fwd; v and mask held through the last k groups: up to RT = 5 (above, spills)
-  constexpr bool kPre = OCC == 1 && (NF == 1 ? RT <= 5 : RT <= 2);
   const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
   float* DA = lds;          // gradient w.r.t. the current block output [R][S]
   float* DV = lds + R * S;  // dV_k                                     [R][S]
@@ -1014,82 +990,55 @@ void k_mlps_bwd(const MlpBwd p, const floatx4* __restrict__ img, const SGeom geo
       asm volatile("" : "+s"(r0));
       const int k = nm - 1 - (ph >> 1);
       const bool dv = (ph & 1) == 0;
-      // epilogue operands, in flight during the GEMM's last k groups (raw: any arithmetic there
-      // would wait for the loads at once): dV: v and the dropout mask; dA of block 0: u. Loaded
-      // unconditionally (address selects: element 0 where unused; the mask is read only with dropout)
-      float ev[RT][NF][4];
-      uint32_t em[RT][NF][4];
-      auto tail = [&]() {
-        if constexpr (kPre) {
-          const bool need = dv || k == 0;
-          const gfloat* V = (const gfloat*)(dv ? pick8(p.V, k) : p.u);
-          const gu8* M = p.drop ? (const gu8*)pick8(p.M, k) : (const gu8*)V;
-#pragma unroll
-          for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int i = 0; i < NF; ++i) {
-              const uint32_t c = (uint32_t)min(16 * fr[i] + lr, D - 1);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const uint32_t o = (uint32_t)min(r0 + 16 * t + lq + r, N - 1) * (uint32_t)D + c;
-                ev[t][i][r] = V[need ? o : 0u];
-                em[t][i][r] = (uint32_t)M[dv ? o : 0u];
-              }
-            }
-        }
-      };
-      mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G, full, tail);
+      mlps_gemm<RT, NF, P>(acc, ring, bs, dv ? DA : DV, S, G, full);
       MLPS_STAMP(1, 3 + 3 * ph);
       int lo = lane;  // opaque copies: see k_mlps_fwd
       asm volatile("" : "+s"(r0), "+v"(lo));
       const int lr = lo & 15, lq = 4 * (lo >> 4);
       const uint32_t nd = (uint32_t)(N * D);
-      if (dv) {  // dV = (dA W2) * mask/(1-p) * act'(v)
-        const __amdgpu_buffer_rsrc_t rdV = mlp_rsrc(pick8(p.dV, k), 4u * nd);
+      // per fragment: the epilogue's operands (dV: v and the dropout mask; dA of block 0: u), every
+      // load issued before the first use (one round trip per fragment, see k_mlps_fwd), then its
+      // outputs
+      const uint32_t ldd = dv ? (uint32_t)D : k > 0 ? (uint32_t)D : (uint32_t)(2 * D);
+      const __amdgpu_buffer_rsrc_t rout = dv      ? mlp_rsrc(pick8(p.dV, k), 4u * nd)
+                                          : k > 0 ? mlp_rsrc(pick8(p.dA, k - 1), 4u * nd)
+                                                  : mlp_rsrc(p.dug, 8u * nd);
+      const gfloat* V = (const gfloat*)(dv ? pick8(p.V, k) : p.u);
+      const gu8* M = (dv && p.drop) ? (const gu8*)pick8(p.M, k) : (const gu8*)V;
 #pragma unroll
-        for (int t = 0; t < RT; ++t)
+      for (int i = 0; i < NF; ++i) {
+        float ev[RT][4];
+        uint32_t em[RT][4];
+        if (dv || k == 0) {
+          const uint32_t c = (uint32_t)min(16 * fr[i] + lr, D - 1);
 #pragma unroll
-          for (int i = 0; i < NF; ++i) {
-            if (!fok[i]) continue;
-            const int c = 16 * fr[i] + lr;
+          for (int t = 0; t < RT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int row = 16 * t + lq + r;
-              const int64_t gr = r0 + row;
-              float v = ev[t][i][r];
-              uint32_t mk = em[t][i][r];
-              if (!kPre) {
-                const uint32_t o = (uint32_t)min(gr, N - 1) * (uint32_t)D + (uint32_t)c;
-                v = ((const gfloat*)pick8(p.V, k))[o];
-                mk = p.drop ? (uint32_t)((const gu8*)pick8(p.M, k))[o] : 1u;
-              }
-              const float m = p.drop ? (mk ? scale : 0.f) : 1.f;
-              const float d = (gr < N) ? acc[t][i][r] * m * act_grad(p.act, v) : 0.f;
-              DV[row * S + c] = d;
-              bstore(rdV, gr < N ? 4u * ((uint32_t)gr * (uint32_t)D + (uint32_t)c) : kDrop, d);
+              const uint32_t o = (uint32_t)min(r0 + 16 * t + lq + r, N - 1) * (uint32_t)D + c;
+              ev[t][r] = V[o];
+              em[t][r] = (uint32_t)M[o];  // used only with dropout (else a byte of V: ignored)
             }
-          }
-      } else {  // dA_k = dA_{k+1} + dV W1 ; k == 0: du = dA_0 act'(u) -> dUG[:, :D]
-        const uint32_t ldd = k > 0 ? (uint32_t)D : (uint32_t)(2 * D);
-        const __amdgpu_buffer_rsrc_t rdA = k > 0 ? mlp_rsrc(pick8(p.dA, k - 1), 4u * nd) : mlp_rsrc(p.dug, 8u * nd);
+        }
+        if (!fok[i]) continue;
+        const int c = 16 * fr[i] + lr;
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
-          for (int i = 0; i < NF; ++i) {
-            if (!fok[i]) continue;
-            const int c = 16 * fr[i] + lr;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = 16 * t + lq + r;
-              const int64_t gr = r0 + row;
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * t + lq + r;
+            const int64_t gr = r0 + row;
+            float o;
+            if (dv) {  // dV = (dA W2) * mask/(1-p) * act'(v)
+              const float m = p.drop ? (em[t][r] ? scale : 0.f) : 1.f;
+              o = (gr < N) ? acc[t][i][r] * m * act_grad(p.act, ev[t][r]) : 0.f;
+              DV[row * S + c] = o;
+            } else {  // dA_k = dA_{k+1} + dV W1 ; k == 0: du = dA_0 act'(u) -> dUG[:, :D]
               const float da = DA[row * S + c] + acc[t][i][r];
               DA[row * S + c] = da;
-              float o = da;
-              if (k == 0)
-                o = da * act_grad(p.act, kPre ? ev[t][i][r]
-                                              : p.u[(uint32_t)min(gr, N - 1) * (uint32_t)D + (uint32_t)c]);
-              bstore(rdA, gr < N ? 4u * ((uint32_t)gr * ldd + (uint32_t)c) : kDrop, o);
+              o = k == 0 ? da * act_grad(p.act, ev[t][r]) : da;
             }
+            bstore(rout, gr < N ? 4u * ((uint32_t)gr * ldd + (uint32_t)c) : kDrop, o);
           }
       }
       MLPS_STAMP(1, 4 + 3 * ph);
@@ -1140,7 +1089,7 @@ bool mlpw_lds_ok(int64_t D, int64_t nm) {
 // ---- weight-streamed geometry and launches ----
 struct MlpsPlan {
   bool ok;
-  int RT, NF, P, OCC;
+  int RT, NF, P;
   SGeom geo;
   unsigned blocks;
   size_t lds;
@@ -1179,24 +1128,18 @@ MlpsPlan mlps_plan(int64_t N, int64_t D) {
   pl.geo.G = std::min(g5, g4);
   pl.geo.S = 16 * pl.geo.G + 4;
   pl.geo.nw = nw;
-  // workgroups per CU: 2 where a workgroup has <= 10 waves of one fragment each (two fragments
-  // per wave need more than the 96 VGPRs of 5 waves per SIMD); A/B: AIMX_MLPS_OCC=1|2
-  // (measured: c4 step 2.894 ms with two, 2.888 with one — a workgroup alone on its CU finishes
-  // sooner, but 430 chunks of 3 row tiles leave the CUs holding two of them the busiest; default 1)
-  const bool occ2_ok = pl.NF == 1 && 64 * pl.geo.nw <= kSOcc2Threads;
-  int occ = 1;
-  if (const char* e = getenv("AIMX_MLPS_OCC")) occ = (atoi(e) == 2 && occ2_ok) ? 2 : 1;
-  const int rt_max = occ == 2 ? 4 : (pl.NF == 1 ? 7 : 3);
-  // enough rows per chunk that the chunks fit one round of occ workgroups per CU
-  const int64_t slots = (int64_t)occ * g_num_cus();
+  // (two workgroups per CU, 5 waves per SIMD at <= 96 VGPRs, measured no faster at c4: 2.894 vs
+  // 2.888 ms — 430 chunks of 3 row tiles leave the CUs holding two the busiest — and removed)
+  const int rt_max = pl.NF == 1 ? 7 : 3;
+  // enough rows per chunk that the chunks fit one round of one workgroup per CU
+  const int64_t slots = g_num_cus();
   int rt = (int)std::min<int64_t>(rt_max, std::max<int64_t>(1, cdiv(cdiv(std::max<int64_t>(N, 1), slots), 16)));
   if (const char* e = getenv("AIMX_MLPS_RT")) rt = std::max(1, std::min(rt_max, atoi(e)));  // A/B experiments only
   // two activation tiles + the forward's bias table (2 nm x 16 CF floats, nm <= 8), per workgroup
   auto lds = [&](int r) { return sizeof(float) * (size_t)(2 * 16 * r * pl.geo.S + 2 * 8 * 16 * CF); };
-  const size_t cap = occ == 2 ? (size_t)(kMlpsDynLds / 2 - 1024) : (size_t)kMlpsDynLds;
+  const size_t cap = (size_t)kMlpsDynLds;
   while (rt > 1 && lds(rt) > cap) --rt;
   if (lds(rt) > cap) return pl;
-  pl.OCC = occ;
   pl.RT = rt;
   pl.lds = lds(rt);
   pl.blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(N, 16 * rt), slots));
@@ -1204,35 +1147,31 @@ MlpsPlan mlps_plan(int64_t N, int64_t D) {
   return pl;
 }
 
-template <int RT, int NF, int P, int OCC>
+template <int RT, int NF, int P>
 int mlps_launch(const MlpsPlan& pl, const MlpFwd* pf, const MlpBwd* pb, const float* img, hipStream_t st) {
   static const bool set = [] {
-    (void)hipFuncSetAttribute((const void*)k_mlps_fwd<RT, NF, P, OCC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kMlpsDynLds / OCC);
-    (void)hipFuncSetAttribute((const void*)k_mlps_bwd<RT, NF, P, OCC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kMlpsDynLds / OCC);
+    (void)hipFuncSetAttribute((const void*)k_mlps_fwd<RT, NF, P>, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpsDynLds);
+    (void)hipFuncSetAttribute((const void*)k_mlps_bwd<RT, NF, P>, hipFuncAttributeMaxDynamicSharedMemorySize, kMlpsDynLds);
     return true;
   }();
   (void)set;
   const dim3 grid(pl.blocks), block(64 * pl.geo.nw);
   if (pf)
-    hipLaunchKernelGGL((k_mlps_fwd<RT, NF, P, OCC>), grid, block, pl.lds, st, *pf,
-                       reinterpret_cast<const floatx4*>(img), pl.geo);
+    hipLaunchKernelGGL((k_mlps_fwd<RT, NF, P>), grid, block, pl.lds, st, *pf, reinterpret_cast<const floatx4*>(img),
+                       pl.geo);
   else
-    hipLaunchKernelGGL((k_mlps_bwd<RT, NF, P, OCC>), grid, block, pl.lds, st, *pb,
-                       reinterpret_cast<const floatx4*>(img), pl.geo);
+    hipLaunchKernelGGL((k_mlps_bwd<RT, NF, P>), grid, block, pl.lds, st, *pb, reinterpret_cast<const floatx4*>(img),
+                       pl.geo);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
 
 int mlps_dispatch(const MlpsPlan& pl, const MlpFwd* pf, const MlpBwd* pb, const float* img, hipStream_t st) {
-#define AIMX_MLPS_CASE(rt, nf, occ)                                                                 \
-  if (pl.RT == rt && pl.NF == nf && pl.OCC == occ)                                                  \
-    return pl.P == 5 ? mlps_launch<rt, nf, 5, occ>(pl, pf, pb, img, st) : mlps_launch<rt, nf, 4, occ>(pl, pf, pb, img, st);
-  AIMX_MLPS_CASE(1, 1, 1) AIMX_MLPS_CASE(2, 1, 1) AIMX_MLPS_CASE(3, 1, 1) AIMX_MLPS_CASE(4, 1, 1)
-  AIMX_MLPS_CASE(5, 1, 1) AIMX_MLPS_CASE(6, 1, 1) AIMX_MLPS_CASE(7, 1, 1) AIMX_MLPS_CASE(1, 2, 1)
-  AIMX_MLPS_CASE(2, 2, 1) AIMX_MLPS_CASE(3, 2, 1)
-  AIMX_MLPS_CASE(1, 1, 2) AIMX_MLPS_CASE(2, 1, 2) AIMX_MLPS_CASE(3, 1, 2) AIMX_MLPS_CASE(4, 1, 2)
+#define AIMX_MLPS_CASE(rt, nf)                                                          \
+  if (pl.RT == rt && pl.NF == nf)                                                       \
+    return pl.P == 5 ? mlps_launch<rt, nf, 5>(pl, pf, pb, img, st) : mlps_launch<rt, nf, 4>(pl, pf, pb, img, st);
+  AIMX_MLPS_CASE(1, 1) AIMX_MLPS_CASE(2, 1) AIMX_MLPS_CASE(3, 1) AIMX_MLPS_CASE(4, 1) AIMX_MLPS_CASE(5, 1)
+  AIMX_MLPS_CASE(6, 1) AIMX_MLPS_CASE(7, 1) AIMX_MLPS_CASE(1, 2) AIMX_MLPS_CASE(2, 2) AIMX_MLPS_CASE(3, 2)
 #undef AIMX_MLPS_CASE
   return AIMX_EARG;
 }
