@@ -824,7 +824,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
   float* Xa = lds;              // block input a_k [R][S]
   float* Hb = lds + R * S;      // r_k             [R][S]
   float* Bia = lds + 2 * R * S;  // b1_k at 2k, b2_k at 2k+1: [16 CF] each
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = 4 * (lane >> 4);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15;
   for (int e = threadIdx.x; e < 2 * nm * 16 * CF; e += blockDim.x) {
     const int m = e / (16 * CF), c = e - m * (16 * CF);
     const float* bb = pick8((m & 1) ? p.b2 : p.b1, m >> 1);
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
   const int D = (int)p.D, CF = geo.CF, G = geo.G, S = geo.S, nw = geo.nw, nm = p.nm;
   float* DA = lds;          // gradient w.r.t. the current block output [R][S]
   float* DV = lds + R * S;  // dV_k                                     [R][S]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lq = 4 * (lane >> 4);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15;
   const int64_t N = p.N, nchunk = cdiv(N, R);
   const int nph = 2 * nm;
   int fr[NF];
