@@ -1561,8 +1561,14 @@ bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
       a.mask_in || a.mask_out || a.act >= 0)
     return false;
   if (a.zc_rowptr && a.zc_dim != 1) return false;
-  const char* e = getenv("AIMX_WGRAD_LDS_GEMM");  // single long-K GEMMs too (opt-in: see DESIGN)
-  if (!e || atoi(e) == 0) return false;
+  // single long-K weight gradients: from M N K >= 2e9 (c4's 512-wide concat / embedding dW: step
+  // 2.873 -> 2.836 ms; c2's 256-wide ones measured +72 us this way, c5's 1024-wide neutral);
+  // AIMX_WGRAD_LDS_GEMM=0 / 1 forces either way (A/B)
+  static const int forced = [] {
+    const char* e = getenv("AIMX_WGRAD_LDS_GEMM");
+    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
+  }();
+  if (forced == 0 || (forced < 0 && (double)a.M * (double)a.N * (double)a.K < 2e9)) return false;
   pr = AimxWgradProblem{};
   pr.dY = a.A;
   pr.ld_dy = a.sak;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round profile set (run on the GPU box), in parts that each fit one gpurun call:
-#   a: kernel trace + stats of the default bench command, the hop roofline launches alone, the two
+#   a: the parity tests (a failure stops the set), kernel trace + stats of the default bench command, the hop roofline launches alone, the two
 #      PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic, the default bench line;
 #   b: c3/c4/c5 bench lines (fp32, AMP for c2/c4/c5), step traces of c4/c5, MFMA-busy PMC passes on
 #      c2, c4 and c5 (whole-step MFMA utilisation against chip peak);
@@ -12,6 +12,7 @@ set -o pipefail
 R=gpurun_out/round
 mkdir -p $R
 A=(
+  "300 round/parity.log python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hop_rows.py -q -x --timeout 200 --timeout-method thread"
   "900 round/bench.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/bench -- python3 bench.py --no-cpu-baseline"
   "600 round/roof.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/roof -- python3 bench.py --roofline-only"
   "600 round/pmc_fetch.log rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/pmc_fetch -- python3 bench.py --roofline-only"
