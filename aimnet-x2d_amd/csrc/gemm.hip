@@ -1083,12 +1083,15 @@ __device__ long long g_wb_trace[4][10][5];
 // VM: the operands' staging, 1 = 16-byte loads for every problem of the launch, 0 = dword loads for
 // every problem, 2 = per problem (WbTable.v4). With a per-problem branch inside each fetch the
 // paths into the fill loop's head carry different load counts and hipcc waits for all loads there.
+// 80-wide blocks: 5 waves per SIMD (<= 102 VGPRs), so that four workgroups (20 waves, all the LDS)
+// fit a CU; at 108-112 VGPRs only three did
 template <int BB, bool DB, int VM>
-__global__ __launch_bounds__(WbGeom<BB>::T) void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
+__global__ __launch_bounds__(WbGeom<BB>::T) __attribute__((amdgpu_waves_per_eu(BB == 80 ? 5 : 1)))
+void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
   using G = WbGeom<BB>;
   constexpr int kWbF = G::F, kWbT = G::T, kWbV = G::V, kLd = G::S;
   constexpr int kBuf = kWbK * kLd;  // floats per operand buffer
-  static_assert(!DB || BB == 80, "double-buffered LDS only for 80-wide blocks");
+  static_assert(!DB || BB <= 80, "double-buffered LDS only for 64- and 80-wide blocks");
   __shared__ __attribute__((aligned(16))) float sA[(DB ? 2 : 1) * kBuf];
   __shared__ __attribute__((aligned(16))) float sB[(DB ? 2 : 1) * kBuf];
   // the split-K arrival flag lives in sA: written only after the barrier that ends every LDS read
@@ -1521,7 +1524,10 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
     w.lds = true;
     const char* be = getenv("AIMX_WGRAD_BB");
     const int force = be ? atoi(be) : 0;
-    w.bb = force == 160 ? 160 : 80;
+    // 64-wide blocks (AIMX_WGRAD_BB=64, A/B): 4 waves, one per SIMD, so no SIMD carries two of a
+    // workgroup's waves into every fill barrier (80-wide: 5 waves; the barrier took 23-26 % of a
+    // wave's loop at c4 / c5, tools/wgrad_trace.py)
+    w.bb = force == 160 ? 160 : force == 64 ? 64 : 80;
     w.slab = (int64_t)w.bb * w.bb;
     w.tiles_x = (int)cdiv(p.M, w.bb);
     w.tiles_y = (int)cdiv(N, w.bb);
@@ -1731,14 +1737,20 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
         const int vm = nv4 == tb.n ? 1 : (nv4 == 0 ? 0 : 2);
         using WbFn = void (*)(const WbTable, float*, int32_t*);
         WbFn fn;
+        static const bool narrow = [] {
+          const char* e = getenv("AIMX_WGRAD_BB");
+          return e && atoi(e) == 64;
+        }();
         if (wide)
           fn = vm == 1 ? k_wgrad_lds<160, false, 1> : (vm == 0 ? k_wgrad_lds<160, false, 0> : k_wgrad_lds<160, false, 2>);
+        else if (narrow)
+          fn = vm == 1 ? k_wgrad_lds<64, true, 1> : (vm == 0 ? k_wgrad_lds<64, true, 0> : k_wgrad_lds<64, true, 2>);
         else if (dbuf)
           fn = vm == 1 ? k_wgrad_lds<80, true, 1> : (vm == 0 ? k_wgrad_lds<80, true, 0> : k_wgrad_lds<80, true, 2>);
         else
           fn = vm == 1 ? k_wgrad_lds<80, false, 1> : (vm == 0 ? k_wgrad_lds<80, false, 0> : k_wgrad_lds<80, false, 2>);
-        hipLaunchKernelGGL(fn, dim3((unsigned)blkb), dim3(wide ? WbGeom<160>::T : WbGeom<80>::T), 0, (hipStream_t)stream,
-                           tb, (float*)workspace, counters);
+        const int nthr = wide ? WbGeom<160>::T : narrow ? WbGeom<64>::T : WbGeom<80>::T;
+        hipLaunchKernelGGL(fn, dim3((unsigned)blkb), dim3(nthr), 0, (hipStream_t)stream, tb, (float*)workspace, counters);
       }
       tb = WbTable{};
       blkb = 0;

@@ -1,13 +1,13 @@
 #!/bin/bash
 # round-4 working call (overwritten per call)
 export PYTHONDONTWRITEBYTECODE=1
-R=gpurun_out/r4m
+R=gpurun_out/r4n
 tools/gpu_steps.sh \
- "300 r4m/parity.log python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hop_rows.py -q -x --timeout 200 --timeout-method thread" \
- "120 r4m/trace_c4.log python3 -u tools/mlps_trace.py c4" \
- "120 r4m/trace_c5.log python3 -u tools/mlps_trace.py c5" \
- "150 r4m/bench_c2.log python3 bench.py --config c2 --steps 100 --warmup 10 --no-cpu-baseline --no-roofline --no-eager" \
- "200 r4m/bench_c4.log python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline" \
- "200 r4m/bench_c4_wl.log env AIMX_WGRAD_LDS_GEMM=1 python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager" \
- "200 r4m/bench_c5.log python3 bench.py --config c5 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline" \
- "200 r4m/bench_c5_wl.log env AIMX_WGRAD_LDS_GEMM=1 python3 bench.py --config c5 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager"
+ "300 r4n/parity.log python3 -u -m pytest tests/test_gpu_parity.py -q -x --timeout 200 --timeout-method thread -k 'wgrad or model_case or full_size or gemm'" \
+ "120 r4n/wtrace_c4.log python3 -u tools/wgrad_trace.py c4" \
+ "150 r4n/bench_c2.log python3 bench.py --config c2 --steps 100 --warmup 10 --no-cpu-baseline --no-roofline --no-eager" \
+ "200 r4n/bench_c4.log python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager" \
+ "200 r4n/bench_c4_bb64.log env AIMX_WGRAD_BB=64 python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager" \
+ "200 r4n/bench_c5.log python3 bench.py --config c5 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager" \
+ "200 r4n/bench_c5_bb64.log env AIMX_WGRAD_BB=64 python3 bench.py --config c5 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager" \
+ "150 r4n/bench_c2_bb64.log env AIMX_WGRAD_BB=64 python3 bench.py --config c2 --steps 100 --warmup 10 --no-cpu-baseline --no-roofline --no-eager"
