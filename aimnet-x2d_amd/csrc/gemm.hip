@@ -1506,12 +1506,32 @@ namespace {
 struct WgPlan {
   int tiles_x, tiles_y, splits, kchunk;
   bool lds;    // k_wgrad_lds (bb x bb blocks) instead of k_wgrad_grouped (32 x 32 tiles)
-  int bb;      // k_wgrad_lds block edge: 80 or 160
+  int bb;      // k_wgrad_lds block edge: 64, 80 or 160 (wg_bb)
   int64_t slab;  // floats per split-K slab
 };
 // min_wgs > 0 (a lone long-K GEMM routed here): split K further until the launch has about that
 // many workgroups, so the LDS fills of a few blocks are spread over the whole chip
-WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
+// Block edge of one k_wgrad_lds launch: 64 (4 waves, one per SIMD: no SIMD carries two of a
+// workgroup's waves into every fill barrier; with 80-wide blocks' 5 waves the barrier took 23-26 %
+// of a wave's loop, tools/wgrad_trace.py) unless the 64-wide tiling pads the launch's long-K
+// problems to more than 1.25x the block area of 80-wide blocks (c2's 76-wide MLP weights: 2.6x).
+// Measured: c4 2.745 -> 2.635 ms, c5 4.025 -> 3.951 ms with 64; c2 0.722 -> 0.737 ms (kept at 80).
+// AIMX_WGRAD_BB=64 / 80 / 160 forces one (A/B).
+int wg_bb(const AimxWgradProblem* p, int32_t n) {
+  const char* e = getenv("AIMX_WGRAD_BB");  // read per call (a few per step): the parity tests switch it
+  const int force = e ? atoi(e) : 0;
+  if (force == 64 || force == 80 || force == 160) return force;
+  double a64 = 0, a80 = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if (p[i].K < 2048) continue;
+    const int64_t N = p[i].col_out ? p[i].N + 1 : p[i].N;
+    a64 += (double)cdiv(p[i].M, 64) * cdiv(N, 64) * 64 * 64;
+    a80 += (double)cdiv(p[i].M, 80) * cdiv(N, 80) * 80 * 80;
+  }
+  return a64 <= 1.25 * a80 ? 64 : 80;
+}
+
+WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs, int bb) {
   const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
   const bool no_lds = e && atoi(e) == 0;
   WgPlan w;
@@ -1522,12 +1542,7 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs = 0) {
     // c5 853 -> 880 us; steps c2 0.78 -> 0.90, c4 3.30 -> 3.37, c5 4.98 -> 5.11 ms (a quarter of
     // the workgroups, 109 VGPRs: 4 waves per SIMD; profiles/r03_gemm_ab.txt)
     w.lds = true;
-    const char* be = getenv("AIMX_WGRAD_BB");
-    const int force = be ? atoi(be) : 0;
-    // 64-wide blocks (AIMX_WGRAD_BB=64, A/B): 4 waves, one per SIMD, so no SIMD carries two of a
-    // workgroup's waves into every fill barrier (80-wide: 5 waves; the barrier took 23-26 % of a
-    // wave's loop at c4 / c5, tools/wgrad_trace.py)
-    w.bb = force == 160 ? 160 : force == 64 ? 64 : 80;
+    w.bb = bb;  // wg_bb
     w.slab = (int64_t)w.bb * w.bb;
     w.tiles_x = (int)cdiv(p.M, w.bb);
     w.tiles_y = (int)cdiv(N, w.bb);
@@ -1592,7 +1607,7 @@ bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
     pr.zc_chunks = a.zc_chunks;
     pr.zc_width = a.zc_width;
   }
-  return pr.N >= 1 && wg_valid(pr) && wg_plan(pr).lds;
+  return pr.N >= 1 && wg_valid(pr) && wg_plan(pr, 0, 80).lds;
 }
 }  // namespace
 
@@ -1608,7 +1623,7 @@ size_t gemm_workspace_floats(const AimxGemmArgs& a) {
   size_t f = tiled_workspace_floats(a);
   AimxWgradProblem pr;
   if (gemm_as_wgrad(a, pr)) {
-    const WgPlan w = wg_plan(pr, kLoneWgs);
+    const WgPlan w = wg_plan(pr, kLoneWgs, wg_bb(&pr, 1));
     if (w.splits > 1) f = std::max(f, (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab);
   }
   return f;
@@ -1632,7 +1647,7 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   {
     AimxWgradProblem pr;
     if (gemm_as_wgrad(a, pr)) {
-      const WgPlan w = wg_plan(pr, kLoneWgs);
+      const WgPlan w = wg_plan(pr, kLoneWgs, wg_bb(&pr, 1));
       const size_t need = w.splits > 1 ? sizeof(float) * w.splits * w.tiles_x * w.tiles_y * w.slab : 0;
       if ((w.splits == 1 || (a.workspace && a.workspace_bytes >= need)) && a.counters &&
           (int64_t)w.tiles_x * w.tiles_y <= a.n_counters)
@@ -1691,8 +1706,9 @@ namespace aimx {
 size_t wgrad_ws_bytes(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
   if (!p || n < 0) return 0;
   size_t f = 0;
+  const int bb = wg_bb(p, n);
   for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i], min_wgs);
+    const WgPlan w = wg_plan(p[i], min_wgs, bb);
     if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab;
   }
   return sizeof(float) * f;
@@ -1705,8 +1721,9 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
     if (!wg_valid(p[i])) return AIMX_EARG;
   if (workspace_bytes < wgrad_ws_bytes(p, n, min_wgs) || (workspace_bytes && !workspace)) return AIMX_EARG;
   int64_t ctiles = 0;
+  const int bb = wg_bb(p, n);
   for (int32_t i = 0; i < n; ++i) {
-    const WgPlan w = wg_plan(p[i], min_wgs);
+    const WgPlan w = wg_plan(p[i], min_wgs, bb);
     ctiles += (int64_t)w.tiles_x * w.tiles_y;
   }
   if (!counters || ctiles > n_counters) return AIMX_EARG;
@@ -1737,10 +1754,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
         const int vm = nv4 == tb.n ? 1 : (nv4 == 0 ? 0 : 2);
         using WbFn = void (*)(const WbTable, float*, int32_t*);
         WbFn fn;
-        static const bool narrow = [] {
-          const char* e = getenv("AIMX_WGRAD_BB");
-          return e && atoi(e) == 64;
-        }();
+        const bool narrow = bb == 64;
         if (wide)
           fn = vm == 1 ? k_wgrad_lds<160, false, 1> : (vm == 0 ? k_wgrad_lds<160, false, 0> : k_wgrad_lds<160, false, 2>);
         else if (narrow)
@@ -1765,7 +1779,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
-    const WgPlan w = wg_plan(pr, min_wgs);
+    const WgPlan w = wg_plan(pr, min_wgs, bb);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {
       const int wide = w.bb == 160;

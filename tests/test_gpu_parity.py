@@ -406,15 +406,18 @@ def test_gemm_weight_grad_forced_splits(splits):
     assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
 
 
-@pytest.mark.parametrize("bb", ["80", "160"])
+@pytest.mark.parametrize("bb", ["auto", "64", "80", "160"])
 def test_wgrad_grouped_matches_fp64(bb, monkeypatch):
     """aimx_wgrad_grouped over the stack's shapes (76 x 76 / 152 x 304 / c5's 307 x 307 and
-    614 x 614 with the bias column, long K: the LDS-block kernel, 80-wide blocks and the opt-in
-    160-wide ones under AIMX_WGRAD_BB=160), a short-K FFN shape, K = 1 and odd widths
-    (unaligned rows: the LDS kernel's dword loads): dW = dY^T X and db = sum_k dY against fp64,
-    deterministic, counters left at zero."""
+    614 x 614 with the bias column, long K: the LDS-block kernel with the block edge its rule picks,
+    or 64-, 80- or 160-wide blocks forced by AIMX_WGRAD_BB), a short-K FFN shape, K = 1 and odd
+    widths (unaligned rows: the LDS kernel's dword loads): dW = dY^T X and db = sum_k dY against
+    fp64, deterministic, counters left at zero."""
     from aimx import ops, _lib
-    monkeypatch.setenv("AIMX_WGRAD_BB", bb)
+    if bb == "auto":
+        monkeypatch.delenv("AIMX_WGRAD_BB", raising=False)
+    else:
+        monkeypatch.setenv("AIMX_WGRAD_BB", bb)
     g = torch.Generator().manual_seed(11)
     shapes = [(76, 76, 9170, True), (152, 304, 9170, True), (76, 76, 4099, False), (256, 256, 520, True),
               (36, 36, 1, True), (38, 38, 777, True), (8, 12, 64, False),

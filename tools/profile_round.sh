@@ -2,12 +2,12 @@
 # Round profile set (run on the GPU box), in parts that each fit one gpurun call:
 #   a: the parity tests (a failure stops the set), kernel trace + stats of the default bench command, the hop roofline launches alone, the two
 #      PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic, the default bench line;
-#   b: c3/c4/c5 bench lines (fp32, AMP for c2/c4/c5), step traces of c4/c5, MFMA-busy PMC passes on
-#      c2, c4 and c5 (whole-step MFMA utilisation against chip peak);
+#   b: the parity tests again, c3/c4/c5 bench lines, step traces of c4/c5, c4's MFMA-busy PMC pass;
+#   b2: AMP bench lines (c2/c4/c5), MFMA-busy PMC passes on c2 and c5 (whole-step MFMA against peak);
 #   c: the per-tensor parity report, the DDP lines (world-size-1 RCCL with the DDP-wrapped autograph
 #      leg; two gloo ranks sharing the GPU), the k_mlps phase stamps, smoke and the whole -m gpu suite.
 # Outputs under gpurun_out/round/; tools/collect_profiles.py copies the summaries into profiles/.
-# usage: tools/profile_round.sh a|b|c
+# usage: tools/profile_round.sh a|b|b2|c
 set -o pipefail
 R=gpurun_out/round
 mkdir -p $R
@@ -20,17 +20,20 @@ A=(
   "900 round/bench_plain.log python3 bench.py"
 )
 B=(
+  "400 round/parity_b.log python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hop_rows.py -q -x --timeout 200 --timeout-method thread"
   "300 round/bench_c3.log python3 bench.py --config c3 --no-cpu-baseline --no-roofline --no-eager"
   "300 round/bench_c4.log python3 bench.py --config c4 --no-cpu-baseline"
   "300 round/bench_c5.log python3 bench.py --config c5 --no-cpu-baseline"
-  "300 round/bench_c2_amp.log python3 bench.py --amp --no-cpu-baseline --no-roofline"
-  "300 round/bench_c4_amp.log python3 bench.py --config c4 --amp --no-cpu-baseline --no-roofline"
-  "300 round/bench_c5_amp.log python3 bench.py --config c5 --amp --no-cpu-baseline --no-roofline"
   "600 round/c4_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/c4_trace -- python3 bench.py --config c4 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
   "600 round/c5_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/c5_trace -- python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
   "120 round/seq.log bash -c 'for c in bench c4_trace c5_trace; do python3 tools/step_seq.py $R/\$c > $R/\${c}_step_seq.txt; done'"
-  "600 round/c2_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c2_mfma -- python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
   "600 round/c4_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c4_mfma -- python3 bench.py --config c4 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
+)
+B2=(
+  "300 round/bench_c2_amp.log python3 bench.py --amp --no-cpu-baseline --no-roofline"
+  "300 round/bench_c4_amp.log python3 bench.py --config c4 --amp --no-cpu-baseline --no-roofline"
+  "300 round/bench_c5_amp.log python3 bench.py --config c5 --amp --no-cpu-baseline --no-roofline"
+  "600 round/c2_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c2_mfma -- python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
   "600 round/c5_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c5_mfma -- python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
 )
 C=(
@@ -45,6 +48,7 @@ C=(
 case "$1" in
   a) tools/gpu_steps.sh "${A[@]}" ;;
   b) tools/gpu_steps.sh "${B[@]}" ;;
+  b2) tools/gpu_steps.sh "${B2[@]}" ;;
   c) tools/gpu_steps.sh "${C[@]}" ;;
   *) echo "usage: $0 a|b|c" >&2; exit 2 ;;
 esac
