@@ -57,7 +57,7 @@ for cfgname in ("c2", "c4", "c5"):
                                    check=True).stdout)
 # step kernel sequences (default bench command = c2, c4, c5), the parity report, the DDP lines,
 # the k_mlps phase stamps and the GPU suite's summary (part c)
-for name, out in (("bench_step_seq.txt", "c2_step_seq.txt"), ("c4_trace_step_seq.txt", "c4_step_seq.txt"),
+for name, out in (("c2_trace_step_seq.txt", "c2_step_seq.txt"), ("c4_trace_step_seq.txt", "c4_step_seq.txt"),
                   ("c5_trace_step_seq.txt", "c5_step_seq.txt"), ("parity.json", "parity.json"),
                   ("mlps_trace_c4.log", "mlps_trace_c4.txt"), ("mlps_trace_c5.log", "mlps_trace_c5.txt")):
     p = os.path.join(src, name)

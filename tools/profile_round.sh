@@ -37,6 +37,8 @@ B2=(
   "600 round/c5_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c5_mfma -- python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
 )
 C=(
+  "600 round/c2_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/c2_trace -- python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 20 --warmup 5"
+  "120 round/seq_c2.log bash -c 'python3 tools/step_seq.py $R/c2_trace > $R/c2_trace_step_seq.txt'"
   "600 round/parity_report.log python3 -u tools/parity_report.py --out $R/parity.json"
   "300 round/bench_ddp_world1.log python3 bench.py --ddp-world1 --no-cpu-baseline --no-roofline"
   "300 round/bench_dp2_gloo.log python3 bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-eager"
