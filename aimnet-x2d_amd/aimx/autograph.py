@@ -313,7 +313,14 @@ class _ReplayGrads(torch.autograd.Function):
         b.gout[:ctx.G].copy_(gout)
         b.g_bwd.replay()
         b.done = ctx.gen
-        return (None, None, None, *[sg for sg in b.grads if sg is not None])
+        # every .grad None (zero_grad(set_to_none=True), the default): fresh views of the static
+        # gradients, which the AccumulateGrad nodes take as they are (the parameters' .grad then
+        # alias the bucket's static gradients, as _Replay hands them out) instead of cloning each
+        # one — 73 launches per step at c2. Otherwise the static tensors themselves: the engine
+        # clones them, so accumulating onto an existing .grad never reads memory the next replay
+        # overwrites.
+        fresh = all(p.grad is None for p, sg in zip(b.params, b.grads) if sg is not None)
+        return (None, None, None, *[sg.view_as(sg) if fresh else sg for sg in b.grads if sg is not None])
 
 
 def _pick(st, N, E, G, dev, amp):
