@@ -44,7 +44,9 @@ constexpr int kRows = 8;      // molecules per workgroup (the most: head8_rows)
 constexpr int kWaves = 16;    // waves per workgroup
 constexpr int kNT = 64 * kWaves;
 constexpr int kRingMax = 8;   // B items (4 k each) in flight per wave (fewer when a GEMM has fewer)
-constexpr int kMaxF8 = 256;   // widest F (see head8_ok)
+// widest F (see head8_ok). 512 (c4) measured slower before the k4-interleaved images and the
+// 4-row tiles; with them c4 2.641 -> 2.589 ms (8-row tiles 2.697)
+constexpr int kMaxF8 = 512;
 constexpr int kMaxGemms = 2 * AIMX_HEAD_MAX_BLOCKS + 2;
 
 __device__ __forceinline__ float drop_scale8(float p) { return p < 1.f ? 1.f / (1.f - p) : 0.f; }
@@ -392,12 +394,7 @@ bool head8_ok(const AimxHead* h) {
   // (512 would fit too, but every workgroup streams all 2 + 2 nb F x F weights through its CU: at
   // F = 512 that is 9.4 MiB per workgroup, and the 65-workgroup launch ran 185 + 188 us at c4
   // against 139 + 143 us for head.hip's clustered kernels, profiles/r04_c4_step_seq.txt)
-  // AIMX_HEAD8_MAXF=512 admits F = 512 (c4) for A/B: measured slower there before the k4 images
-  static const int64_t max_f = [] {
-    const char* e = getenv("AIMX_HEAD8_MAXF");
-    return (e && atoi(e) == 512) ? (int64_t)512 : (int64_t)kMaxF8;
-  }();
-  if (F < 128 || F > max_f || kWaves % (F / 64) || F % 64 || h->H_in != F || h->nb < 1 || h->nb > AIMX_HEAD_MAX_BLOCKS)
+  if (F < 128 || F > kMaxF8 || kWaves % (F / 64) || F % 64 || h->H_in != F || h->nb < 1 || h->nb > AIMX_HEAD_MAX_BLOCKS)
     return false;
   return lds8_floats(geo8((int)F), kRows) * sizeof(float) <= 156 * 1024;
 }

@@ -1,11 +1,9 @@
 #!/bin/bash
 # round-4 working call (overwritten per call)
 export PYTHONDONTWRITEBYTECODE=1
-R=gpurun_out/r4p
-B="python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline --no-roofline --no-eager"
+R=gpurun_out/r4q
 tools/gpu_steps.sh \
- "200 r4p/head512.log env AIMX_HEAD8_MAXF=512 python3 -u -m pytest tests/test_gpu_parity.py -q --timeout 100 --timeout-method thread -k 'fused_head or head8'" \
- "200 r4p/c4_base.log $B" \
- "200 r4p/c4_h512.log env AIMX_HEAD8_MAXF=512 $B" \
- "200 r4p/c4_base2.log $B" \
- "200 r4p/c4_h512_r8.log env AIMX_HEAD8_MAXF=512 AIMX_HEAD8_ROWS=8 $B"
+ "?900 r4q/tests.log python3 -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread" \
+ "200 r4q/bench_c4.log python3 bench.py --config c4 --steps 30 --warmup 8 --no-cpu-baseline" \
+ "300 r4q/smoke.log python3 -c 'import __graft_entry__ as g; g.smoke()'" \
+ "200 r4q/bench_c2.log python3 bench.py --no-cpu-baseline"
