@@ -47,28 +47,85 @@ def _scale_for(key, ref64):
     return 0.0
 
 
-def parity_failures(ours, ref32, ref64, atol_rel=1e-5, factor=3.0):
-    """North-star tolerance, per tensor: err(ours vs fp64) <= max(1e-5, factor * err(ref fp32 vs fp64)).
+PIN_TOL = 1e-6
 
-    1e-5 norm-relative is the contract (BASELINE.json north_star). Where the reference's own fp32
-    result is further than that from the exact (fp64) value — measured per tensor, e.g. c3's
-    attention / partial charges at ~6e-5..9e-5 (tools/noise_floor.py) — the bound is `factor` times
-    the reference's own fp32 error instead: no fp32 implementation can be closer to the reference
-    than the reference is to the exact answer.
+
+def _rel(a, b, den):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    if a.shape != b.shape:
+        return float("inf")
+    return (np.abs(a - b).max() / den) if (b.size and den > 0) else 0.0
+
+
+def _den(key, b, scale_src):
+    b = np.asarray(b, np.float64)
+    return max(np.abs(b).max() if b.size else 0.0, _scale_for(key, scale_src))
+
+
+def pin_tol(key, r32, ref64, tol=PIN_TOL):
+    """PIN_TOL, widened only where the reference's own fp32 error vs exact is large: by 5 % of
+    that error (CPU reductions regrouped by the thread count move c3's pool gradients by 2e-6
+    where the reference itself is 1e-4 from exact). A systematic oracle bug of 1e-4 still fails."""
+    if ref64 is None or key not in ref64:
+        return tol
+    return max(tol, 0.05 * _rel(r32, ref64[key], _den(key, ref64[key], ref64)))
+
+
+def pin_failures(oracle32, ref32, ref64=None, tol=PIN_TOL):
+    """The oracle pin: the oracle's fp32 run against the reference's OWN fp32 tensors (a golden
+    fixture made by importing the reference, tests/golden/make_golden.py), per tensor,
+    norm-relative <= tol (1e-6). The oracle replays the reference's ATen ops in the reference's
+    order, so the two agree bit for bit on most cases and within 2.4e-7 on the rest (measured on
+    all 16 fixture cases; `pin_tol`). Returns [(key, err, tol)] for every tensor that misses (or
+    is missing)."""
+    bad = []
+    src = ref64 if ref64 is not None else ref32
+    for k, r in ref32.items():
+        if k not in oracle32:
+            bad.append((k, "missing", tol))
+            continue
+        err = _rel(oracle32[k], r, _den(k, r, src))
+        t = pin_tol(k, r, ref64, tol)
+        if not err <= t:
+            bad.append((k, err, t))
+    return bad
+
+
+def parity_failures(ours, ref32, ref64, atol_rel=1e-5, factor=3.0, oracle32=None):
+    """North-star tolerance, per tensor: err(ours vs fp64) <= max(1e-5, factor * floor).
+
+    1e-5 norm-relative is the contract (BASELINE.json north_star). The floor is the fp32 error of
+    the reference's own algorithm against the exact (fp64) value — e.g. c3's attention / partial
+    charges at ~6e-5..9e-5 (tools/noise_floor.py): no fp32 implementation can be closer to the
+    reference than the reference is to the exact answer. Where it comes from, per tensor k:
+
+    * k in `ref32` (the reference's own fp32 output, a golden fixture): its error vs fp64 — but
+      ONLY once the oracle pin holds for k, i.e. `oracle32[k]` (the oracle's fp32 run on the same
+      inputs) is within `pin_tol` of `ref32[k]` (`pin_failures`). A missed pin is itself a failure
+      (`("pin:" + k, err, PIN_TOL)`); without `oracle32` no floor is taken (tol = 1e-5).
+    * k only in `oracle32` (no reference output exists, e.g. config-sized batches): the oracle's
+      own fp32 error — the same ATen op sequence that `tests/test_oracle_golden.py` pins to the
+      reference on every fixture case.
+    * neither: no floor.
     """
     bad = []
     for k, v64 in ref64.items():
         if k not in ours:
             continue
-        sc = _scale_for(k, ref64)
-        a = np.asarray(ours[k], np.float64)
-        b = np.asarray(v64, np.float64)
-        den = max(np.abs(b).max() if b.size else 0.0, sc)
-        err = (np.abs(a - b).max() / den) if (b.size and den > 0) else 0.0
+        den = _den(k, v64, ref64)
+        err = _rel(ours[k], v64, den)
         floor = 0.0
         if ref32 is not None and k in ref32:
-            r = np.asarray(ref32[k], np.float64)
-            floor = (np.abs(r - b).max() / den) if (b.size and den > 0) else 0.0
+            if oracle32 is not None and k in oracle32:
+                pin = _rel(oracle32[k], ref32[k], _den(k, ref32[k], ref64))
+                ptol = pin_tol(k, ref32[k], ref64)
+                if not pin <= ptol:
+                    bad.append(("pin:" + k, pin, ptol))
+                else:
+                    floor = _rel(ref32[k], v64, den)
+        elif oracle32 is not None and k in oracle32:
+            floor = _rel(oracle32[k], v64, den)
         tol = max(atol_rel, factor * floor)
         if not err <= tol:
             bad.append((k, err, tol))

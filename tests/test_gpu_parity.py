@@ -529,7 +529,13 @@ def test_attention_pool_standalone():
     ((pp * torch.from_numpy(z["wp"]).double()).sum() + (aa * torch.from_numpy(z["wa"]).double()).sum()).backward()
     ref64 = {"pooled": pp.detach().numpy(), "attn": aa.detach().numpy(), "grad_x": x64.grad.numpy()}
     ref64.update({"grad." + k[5:]: v.grad.numpy() for k, v in p64.items()})
-    bad = parity_failures(ours, {k: z[k] for k in ours}, ref64)
+    p32 = {"pool." + k: v.clone().requires_grad_() for k, v in params.items()}
+    x32 = torch.from_numpy(z["x"]).requires_grad_()
+    pp, aa = om.attention_pool(p32, "pool.", x32, b, 4, int(b.max()) + 1)
+    ((pp * torch.from_numpy(z["wp"])).sum() + (aa * torch.from_numpy(z["wa"])).sum()).backward()
+    o32 = {"pooled": pp.detach().numpy(), "attn": aa.detach().numpy(), "grad_x": x32.grad.numpy()}
+    o32.update({"grad." + k[5:]: v.grad.numpy() for k, v in p32.items()})
+    bad = parity_failures(ours, {k: z[k] for k in ours}, ref64, oracle32=o32)
     assert not bad, bad
 
 
@@ -573,7 +579,7 @@ def test_attention_pool_shapes(C, H, strided):
         ref = {"pooled": pp.detach().numpy(), "attn": aa.detach().numpy(), "grad_x": xr.grad.numpy()}
         ref.update({"grad." + k[5:]: v.grad.numpy() for k, v in pd.items()})
         refs[dt] = ref
-    bad = parity_failures(ours, refs[torch.float32], refs[torch.float64])
+    bad = parity_failures(ours, None, refs[torch.float64], oracle32=refs[torch.float32])
     assert not bad, bad
 
 
@@ -671,7 +677,7 @@ def test_model_full_size(name):
     ref32 = _run_full(cfg, seed, inputs, loss_w, "cpu", torch.float32)
     ours = _run_full(cfg, seed, inputs, loss_w, "cuda")
     assert set(ours) == set(ref64), set(ours) ^ set(ref64)
-    bad = parity_failures(ours, ref32, ref64)
+    bad = parity_failures(ours, None, ref64, oracle32=ref32)
     assert not bad, bad
 
 
@@ -682,10 +688,10 @@ def test_model_case(name):
     ref64 = _oracle_run(z, cfg, inputs, torch.float64)
     ref32 = fixture_refs(z)
     must = set(ref32)
-    # tensors the fixture did not store: the oracle's fp32 CPU run (the reference's own ATen ops,
-    # pinned by tests/test_oracle_golden.py) stands in for the reference's fp32 error floor
-    for k, v in _oracle_run(z, cfg, inputs, torch.float32).items():
-        ref32.setdefault(k, v)
+    # the oracle's fp32 run on the same inputs: it must pin the fixture (conftest.pin_tol) before
+    # the fixture's own fp32 error becomes the floor; for tensors the fixture did not store it is
+    # the floor itself (the reference's ATen ops, pinned by tests/test_oracle_golden.py)
+    oracle32 = _oracle_run(z, cfg, inputs, torch.float32)
     model = _build_model(cfg, int(z["seed"]))
     af, edges, batch, tc = load_case(name, DEV)[2]
     out, attn, q = model(af, edges, batch, tc, *case_stereo(z, DEV))
@@ -702,7 +708,7 @@ def test_model_case(name):
     # every gradient the reference produced must be produced here too
     for k in must:
         assert k in ours, k
-    bad = parity_failures(ours, ref32, ref64)
+    bad = parity_failures(ours, ref32, ref64, oracle32=oracle32)
     assert not bad, bad
 
 
