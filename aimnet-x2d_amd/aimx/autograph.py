@@ -91,18 +91,20 @@ def wanted(model, args):
     return not st.forward_hooked(model)
 
 
+def _dist_initialized():
+    try:
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized()
+    except Exception:  # pragma: no cover
+        return False
+
+
 def _through_autograd(model):
     """Hand the gradients out through autograd (the parameters' AccumulateGrad nodes) instead of
     assigning .grad: whenever something may be watching them — a process group is initialised
     (DistributedDataParallel's reducer hooks every gradient accumulator, reference runner.py:703-707,
     and averages the buckets as they become ready), or a parameter carries gradient hooks."""
-    try:
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized():
-            return True
-    except Exception:  # pragma: no cover
-        return True
-    return _state(model).grad_hooked(model)
+    return _dist_initialized() or _state(model).grad_hooked(model)
 
 
 class _State:
@@ -214,8 +216,12 @@ class _Bucket:
                 del out, al
         cur.wait_stream(side)
         torch.cuda.synchronize(self.dev)
+        # under a process group, another thread (ProcessGroupNCCL's watchdog) may query its events
+        # while the capture is open: a global-mode capture would be invalidated by that query, a
+        # thread-local one only watches this thread (as GraphedTrainStep captures, train.py)
+        mode = "thread_local" if _dist_initialized() else "global"
         self.g_fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fwd):
+        with torch.cuda.graph(self.g_fwd, capture_error_mode=mode):
             with _aliased(model, live) as al:
                 self.outs = model._aimx_forward(*args)
         stand_ins = [al[id(p)] for p in live]
@@ -225,7 +231,7 @@ class _Bucket:
         # leaves behind could sit in blocks the forward graph used (and frees) for temporaries,
         # and the next forward replay would overwrite the caller's .grad
         self.g_bwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_bwd):
+        with torch.cuda.graph(self.g_bwd, capture_error_mode=mode):
             gs = torch.autograd.grad(self.outs[0], stand_ins, self.gout, allow_unused=True)
         del stand_ins
         by_id = {id(p): g for p, g in zip(live, gs)}
@@ -311,6 +317,13 @@ class _ReplayGrads(torch.autograd.Function):
                             "same shape bucket (or its backward already ran); run one backward per forward, or "
                             "set AIMX_AUTOGRAPH=0")
         b.gout[:ctx.G].copy_(gout)
+        # a .grad still aliasing its static gradient (handed out as a fresh view by an earlier step
+        # and not reset since: accumulation, DDP no_sync micro-batches) would be overwritten by the
+        # replay and then accumulated onto itself (2 g_new instead of g_old + g_new): move it out first
+        for p, sg in zip(b.params, b.grads):
+            if sg is not None and p.grad is not None and p.grad.untyped_storage().data_ptr() == \
+                    sg.untyped_storage().data_ptr():
+                p.grad = p.grad.clone()
         b.g_bwd.replay()
         b.done = ctx.gen
         # every .grad None (zero_grad(set_to_none=True), the default): fresh views of the static

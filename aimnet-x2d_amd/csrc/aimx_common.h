@@ -107,6 +107,27 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Raw buffer descriptor over [p, p + bytes) (stride 0, num_records in bytes, dword3 0x00020000 =
+// DATA_FORMAT 32): loads past the extent return 0 and stores past it are dropped, so an invalid
+// element is an ADDRESS select (offset >= bytes, or kBufDrop) instead of a branch around the access.
+// The inputs are made provably wave-uniform with readfirstlane so hipcc builds the descriptor in
+// SGPRs and does not waterfall the accesses (guide T8/T20).
+//
+// The halves MUST pass through uint32_t: __builtin_amdgcn_readfirstlane returns int, and
+// `((uint64_t)hi << 32) | readfirstlane(lo)` sign-extends the low half — a base whose bit 31 is set
+// becomes 0xFFFF'xxxxxxxx after the descriptor keeps the low 16 bits of the high dword (hipcc:
+// s_bfe_i64 + s_or_b64 into the base). That address faults; it is what made the round-4 attention
+// pool's two-round row loads fault on one allocation of one test and not on the others.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* q = (void*)(((uint64_t)hi << 32) | (uint64_t)lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+// A buffer offset past every extent (extents stay below 2^32 - 16, so offset + 12 does not wrap).
+constexpr uint32_t kBufDrop = 0xFFFFFFF0u;
+
 // Internal launchers shared across translation units.
 // The 8-molecule fused head (head8.hip); head.hip's entry points dispatch to it where it applies.
 bool head8_ok(const AimxHead* h);
@@ -132,7 +153,7 @@ int launch_charge_bwd(const float* x, int64_t ldx, int64_t N, int64_t D, const i
 // D > 128 takes the weight-streamed kernels, which read their weights from MFMA-fragment images:
 // mlp_pack_floats(s) floats (0: not needed) written by launch_mlp_pack once per call and direction,
 // passed as `pack` (nullptr: the weight-resident kernels).
-bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision);
+bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision, int64_t ld);
 size_t mlp_pack_floats(const AimxShellStack* s);
 int launch_mlp_pack(const AimxShellStack* s, bool bwd, float* dst, hipStream_t st);
 int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64_t ldx, float* out, int64_t ldo,

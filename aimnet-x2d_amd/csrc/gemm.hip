@@ -156,11 +156,7 @@ __device__ __forceinline__ void epilogue_n(const AimxGemmArgs& a, const int (&m)
 // padding), 32-bit byte offsets (fewer VGPRs than 64-bit flat addresses). Inputs are made
 // provably wave-uniform with readfirstlane so hipcc does not waterfall the loads (guide T8/T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* q = (void*)(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  return buffer_rsrc(p, bytes);  // aimx_common.h (the uint32_t halves matter)
 }
 
 __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {

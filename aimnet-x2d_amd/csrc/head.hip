@@ -59,11 +59,7 @@ struct Cluster {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* q = (void*)(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  return buffer_rsrc(p, bytes);  // aimx_common.h (the uint32_t halves matter)
 }
 
 // A value another workgroup of the cluster will read: sc1 (write-through) when clustered.

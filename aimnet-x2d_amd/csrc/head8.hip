@@ -383,17 +383,17 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
 
 }  // namespace
 
-// The 8-row kernels apply when every chain GEMM is F x F with F = 128 or 256
+// The 8-row kernels apply when every chain GEMM is F x F with F % 64 == 0 and 128 <= F <= kMaxF8
 // (H_in == F: the reference's defaults, ffn_hidden_dim = hidden_dim) and the LDS holds the tiles.
 bool head8_ok(const AimxHead* h) {
   if (const char* e = getenv("AIMX_HEAD8")) {
     if (atoi(e) == 0) return false;
   }
   const int64_t F = h->F;
-  // the 16 waves split into F / 64 column groups x 16 / (F / 64) k ranges exactly: F = 128, 256
-  // (512 would fit too, but every workgroup streams all 2 + 2 nb F x F weights through its CU: at
-  // F = 512 that is 9.4 MiB per workgroup, and the 65-workgroup launch ran 185 + 188 us at c4
-  // against 139 + 143 us for head.hip's clustered kernels, profiles/r04_c4_step_seq.txt)
+  // the 16 waves split into F / 64 column groups x 16 / (F / 64) k ranges exactly (F = 128, 256,
+  // 512). Every workgroup streams all 2 + 2 nb F x F weights through its CU (9.4 MiB at F = 512);
+  // F = 512 ran slower than head.hip's clustered kernels until the k4-interleaved images and the
+  // 4-row tiles (round 4: c4 2.641 -> 2.589 ms with head8 at F = 512, profiles/r04_ab.txt)
   if (F < 128 || F > kMaxF8 || kWaves % (F / 64) || F % 64 || h->H_in != F || h->nb < 1 || h->nb > AIMX_HEAD_MAX_BLOCKS)
     return false;
   return lds8_floats(geo8((int)F), kRows) * sizeof(float) <= 156 * 1024;

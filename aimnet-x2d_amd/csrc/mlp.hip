@@ -136,11 +136,7 @@ __device__ __forceinline__ void lds_sync() {
 // is a load from an address past the end (an ADDRESS select) — a value select after the load lets
 // hipcc branch around every load and wait for each one in turn (cdna_hip_programming.md §5 trap (c)).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* q = (void*)(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  return buffer_rsrc(p, bytes);  // aimx_common.h (the uint32_t halves matter)
 }
 __device__ __forceinline__ float mlp_bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
@@ -1202,13 +1198,23 @@ bool mlps_on(int64_t N, int64_t D, int64_t nm, int32_t precision) {
   return mlps_plan(N, D).ok;
 }
 
-bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision) {
+// The fused kernels address their row operands through raw buffer descriptors (buffer_rsrc): 32-bit
+// byte extents, kBufDrop past them. `ld` is the widest row stride of any operand of the call (the
+// stack's [x | F] rows, its output and upstream-gradient rows); larger batches take the per-GEMM path.
+static bool mlp_extent_ok(int64_t N, int64_t D, int64_t ld) {
+  return 4 * (std::max<int64_t>(N, 1) * std::max<int64_t>(ld, 2 * D) + 2 * D) < (int64_t)kBufDrop - 64;
+}
+
+bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision, int64_t ld) {
+  if (!mlp_extent_ok(N, D, ld)) return false;
   if (getenv("AIMX_MLPS") && atoi(getenv("AIMX_MLPS")) == 1) return mlps_on(N, D, nm, precision);
   return mlpw_on(D, nm) || mlps_on(N, D, nm, precision);
 }
 
 size_t mlp_pack_floats(const AimxShellStack* s) {
-  if (!mlps_on(s->N, s->D, s->num_mlp, s->precision)) return 0;
+  if (!mlps_on(s->N, s->D, s->num_mlp, s->precision) ||
+      !mlp_extent_ok(s->N, s->D, std::max(s->D * (s->num_hops + 1), s->out_ld)))
+    return 0;
   return (size_t)(s->num_layers * 2 * s->num_mlp * mlps_image_floats(s->D));
 }
 

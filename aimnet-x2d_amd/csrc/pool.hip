@@ -137,7 +137,7 @@ __device__ __forceinline__ void attn_fwd_body(const float* __restrict__ x, int64
   // 1) scores, centred on the first atom (fp64 dots; the softmax is shift invariant and the bias
   //    cancels: d_hj = (x_j - x_0) . W_h / tau, see attn_fwd_rows), a wave per atom, lanes over
   //    channels; d is kept in LDS or, for the largest molecules, in the scores array itself
-  const int64_t i0 = gperm[b];
+  const int64_t i0 = n > 0 ? gperm[b] : 0;  // (an empty molecule reads no row)
   for (int j = w; j < n; j += NW) {
     const int64_t i = gperm[b + j];
     double acc[kMaxH];
@@ -348,15 +348,36 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-// this wave's rows j = base + p + r*P of the molecule, lane channels c..c+3 (one burst)
+// The row-resident paths read x through a raw buffer descriptor (aimx_common.h buffer_rsrc): its
+// extent ends at the last row's C-th channel, so the 32-bit byte offsets need (N-1)·ldx + C < 2^30.
+__device__ __forceinline__ bool rows_addressable(int64_t N, int64_t ldx, int64_t C) {
+  return (N - 1) * ldx + C < ((int64_t)1 << 30) - 4;
+}
+__device__ __forceinline__ uint32_t rows_extent(int64_t N, int64_t ldx, int64_t C) {
+  return 4u * (uint32_t)max<int64_t>((N - 1) * ldx + C, 1);
+}
+
+typedef float pfloatx4 __attribute__((ext_vector_type(4)));
+
+// This wave's rows j = base + p + r*P of the molecule (n >= 1 atoms), lane channels c..c+3, in two
+// rounds: the R row indices (clamped into the molecule, so always valid loads), then the R rows; an
+// invalid row or channel is an ADDRESS select past the extent (reads 0). A value select per row
+// (`valid ? load : 0`) makes hipcc branch around each load and wait for it: R dependent round trips
+// instead of two. (Round 4 reverted this form after a fault; the cause was the descriptor's
+// sign-extended base, see buffer_rsrc, not these offsets.)
 template <int P, int R>
-__device__ __forceinline__ void load_rows(float4 (&xr)[R], const float* __restrict__ x, int64_t ldx,
+__device__ __forceinline__ void load_rows(float4 (&xr)[R], __amdgpu_buffer_rsrc_t rx, uint32_t xbytes, int64_t ldx,
                                           const int32_t* __restrict__ gperm, int32_t b, int n, int base, int p,
                                           int c, bool cv) {
+  int32_t q[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) q[r] = gperm[b + max(min(base + p + r * P, n - 1), 0)];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int j = base + p + r * P;
-    xr[r] = (cv && j < n) ? ld4(x + (int64_t)gperm[b + j] * ldx + c) : zero4();
+    const uint32_t off = (cv && j < n) ? 4u * (uint32_t)((int64_t)q[r] * ldx + c) : xbytes;
+    const pfloatx4 v = __builtin_bit_cast(pfloatx4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+    xr[r] = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -392,7 +413,9 @@ __device__ __forceinline__ void attn_fwd_rows(const float* __restrict__ x, int64
   const int c = s * 256 + lane * 4;
   const bool cv = c < C;
   const int nchunk = (n + CAPN - 1) / CAPN;
-  const float4 x0 = cv ? ld4(x + (int64_t)gperm[b] * ldx + c) : zero4();
+  const uint32_t xbytes = rows_extent(N, ldx, C);
+  const __amdgpu_buffer_rsrc_t rx = buffer_rsrc(x, xbytes);
+  const float4 x0 = (cv && n > 0) ? ld4(x + (int64_t)gperm[b] * ldx + c) : zero4();
   float4 wv[HM];
 #pragma unroll
   for (int h = 0; h < HM; ++h) wv[h] = (cv && h < H) ? ld4(W + (int64_t)h * C + c) : zero4();
@@ -400,7 +423,7 @@ __device__ __forceinline__ void attn_fwd_rows(const float* __restrict__ x, int64
   // 1) partial dots of this slice, reduced across the wave
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+    load_rows<P, R>(xr, rx, xbytes, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int q = 0; q < NCH; ++q) {
       float v[NVC];
@@ -457,7 +480,7 @@ __device__ __forceinline__ void attn_fwd_rows(const float* __restrict__ x, int64
   float4 acc = zero4();
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+    if (nchunk > 1) load_rows<P, R>(xr, rx, xbytes, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int j = base + p + r * P;
@@ -513,7 +536,9 @@ __device__ __forceinline__ void attn_bwd_rows(const float* __restrict__ x, int64
   const int c = s * 256 + lane * 4;
   const bool cv = c < C;
   const int nchunk = (n + CAPN - 1) / CAPN;
-  const float4 x0 = cv ? ld4(x + (int64_t)gperm[b] * ldx + c) : zero4();
+  const uint32_t xbytes = rows_extent(N, ldx, C);
+  const __amdgpu_buffer_rsrc_t rx = buffer_rsrc(x, xbytes);
+  const float4 x0 = (cv && n > 0) ? ld4(x + (int64_t)gperm[b] * ldx + c) : zero4();
   const float4 q = cv ? ld4(dpool + (int64_t)g * C + c) : zero4();
   float4 wv[HM];
 #pragma unroll
@@ -526,7 +551,7 @@ __device__ __forceinline__ void attn_bwd_rows(const float* __restrict__ x, int64
   // 1) centred dots with q and with each W_h for this slice, reduced across the wave
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+    load_rows<P, R>(xr, rx, xbytes, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int qq = 0; qq < NCH; ++qq) {
       float v[NVC];
@@ -602,7 +627,7 @@ __device__ __forceinline__ void attn_bwd_rows(const float* __restrict__ x, int64
   for (int h = 0; h < HM; ++h) dw[h] = zero4();
   for (int ch = 0; ch < nchunk; ++ch) {
     const int base = ch * CAPN;
-    if (nchunk > 1) load_rows<P, R>(xr, x, ldx, gperm, b, n, base, p, c, cv);
+    if (nchunk > 1) load_rows<P, R>(xr, rx, xbytes, ldx, gperm, b, n, base, p, c, cv);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int j = base + p + r * P;
@@ -672,7 +697,7 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_fwd(
   const int n = e - b;
   const float tau = *tau_p;
   const bool rows = n <= kMaxAtomsRows && H <= HM && C <= S * 256 && (C % 4) == 0 &&
-                    (ldx % 4) == 0 && al16(x) && al16(W) && al16(pooled);
+                    (ldx % 4) == 0 && al16(x) && al16(W) && al16(pooled) && rows_addressable(N, ldx, C);
   if (rows)
     attn_fwd_rows<S, P, R, HM>(x, ldx, N, C, W, bias, tau, H, b, n, gperm, g, pooled, attn, scores, smem);
   else if (n <= kCap)
@@ -703,7 +728,7 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_bwd(
   const float tau = *tau_p;
   const bool rows = n <= kMaxAtomsRows && H <= HM && C <= S * 256 && (C % 4) == 0 &&
                     (ldx % 4) == 0 && (lddx % 4) == 0 && al16(x) && al16(W) && al16(dx) && al16(dpool) &&
-                    al16(dW_part);
+                    al16(dW_part) && rows_addressable(N, ldx, C);
   if (rows)
     attn_bwd_rows<S, P, R, HM>(x, ldx, N, C, W, tau, H, b, n, gperm, g, attn, dpool, dattn, dx, lddx, dW_part, db_part,
                             dtau_part, smem);

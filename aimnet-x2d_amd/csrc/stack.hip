@@ -108,6 +108,35 @@ int copy2d(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows,
   return AIMX_OK;
 }
 
+// A shell layer without MLP blocks (shell_conv_num_mlp_layers = 0: cli.py:106-107 accepts it):
+// out = act(u) + g (layers.py:82-89, 106), + the outer residual x when stacked (gnn.py:302-306),
+// added in the reference's order. UG = [act(u) | g] (row stride 2D).
+__global__ void k_nomlp_fwd(const float* __restrict__ UG, int64_t D, const float* __restrict__ res, int64_t ldr,
+                            float* __restrict__ dst, int64_t ldd, int64_t N) {
+  const int64_t total = N * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / D, c = i - r * D;
+    float v = UG[r * 2 * D + c] + UG[r * 2 * D + D + c];
+    if (res) v = v + res[r * ldr + c];
+    dst[r * ldd + c] = v;
+  }
+}
+
+// Its backward: dUG = [dY * act'(u) | dY] (U = the saved pre-activation u). dY may be dUG's own
+// upper half (below the top layer the hop backward wrote it there): then only du is written.
+__global__ void k_nomlp_bwd(const float* __restrict__ dY, int64_t ldy, const float* __restrict__ U, int act,
+                            float* __restrict__ dUG, int64_t N, int64_t D, int copy_dy) {
+  const int64_t total = N * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / D, c = i - r * D;
+    const float y = dY[r * ldy + c];
+    dUG[r * 2 * D + c] = y * act_grad(act, U[r * D + c]);
+    if (copy_dy) dUG[r * 2 * D + D + c] = y;
+  }
+}
+
+int nomlp_blocks(int64_t N, int64_t D) { return (int)std::min<int64_t>(cdiv(N * D, 256), 8192); }
+
 struct Ws {
   float* p;
   size_t bytes;
@@ -151,7 +180,7 @@ void set_zc(AimxGemmArgs& a, const AimxShellStack* s, int dim) {
 }
 
 bool valid(const AimxShellStack* s) {
-  if (!s || s->N < 0 || s->D < 1 || s->num_hops < 1 || s->num_layers < 1 || s->num_mlp < 1) return false;
+  if (!s || s->N < 0 || s->D < 1 || s->num_hops < 1 || s->num_layers < 1 || s->num_mlp < 0) return false;
   if (s->mode_single && (s->num_layers != 1 || s->use_pc)) return false;
   if (s->use_pc && (s->D < 2 || !s->gptr || !s->gperm || !s->total_charges)) return false;
   return true;
@@ -232,7 +261,15 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
       RUN(run(a, ws, st));
     }
     // 4) MLP blocks: one fused launch for all of them (mlp.hip), or one GEMM per linear
-    if (mlp_fused_ok(N, D, nm, s->precision)) {
+    if (nm == 0) {  // no blocks: out = act(u) + g (+ x)
+      float* dst = (l == L - 1) ? s->out : s->use_pc ? s->X[l + 1] : s->F[l + 1];
+      const int64_t ldd = (l == L - 1) ? s->out_ld : s->use_pc ? D : K;
+      hipLaunchKernelGGL(k_nomlp_fwd, dim3((unsigned)nomlp_blocks(N, D)), dim3(256), 0, st, s->UG[l], D,
+                         s->mode_single ? nullptr : F, K, dst, ldd, N);
+      AIMX_CHECK_LAUNCH();
+      continue;
+    }
+    if (mlp_fused_ok(N, D, nm, s->precision, std::max(K, s->out_ld))) {
       float* dst;
       int64_t ldd;
       if (l == L - 1) {
@@ -425,7 +462,12 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     const float* dY = (l == L - 1) ? g->d_out : dUG + D;
     const int64_t ldy = (l == L - 1) ? g->d_out_ld : D2;
     // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
-    const bool fused = mlp_fused_ok(N, D, nm, s->precision);
+    const bool fused = nm > 0 && mlp_fused_ok(N, D, nm, s->precision, std::max({K, s->out_ld, g->d_out_ld}));
+    if (nm == 0) {  // no blocks: dUG = [dY * act'(u) | dY]
+      hipLaunchKernelGGL(k_nomlp_bwd, dim3((unsigned)nomlp_blocks(N, D)), dim3(256), 0, st, dY, ldy, s->U[l], s->act,
+                         dUG, N, D, dY != dUG + D ? 1 : 0);
+      AIMX_CHECK_LAUNCH();
+    }
     if (fused) {  // the whole chain + dUG = [du | dY] in one launch (mlp.hip)
       float* dVs[8];
       float* dAs[8];
@@ -467,7 +509,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       }
     }
     // dg = dY -> dUG[:, D:] (the fused chain writes it itself)
-    if (!fused && dY != dUG + D) RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
+    if (!fused && nm > 0 && dY != dUG + D) RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
     if (aux) {  // fork: this layer's weight gradients run beside the rest of the chain
       hipEvent_t ev = (hipEvent_t)g->events[l];
       AIMX_CHECK_HIP(hipEventRecord(ev, st));

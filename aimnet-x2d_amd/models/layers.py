@@ -22,7 +22,13 @@ class ShellConvolutionLayer(nn.Module):
     forward(x [N,D], target [E], src [E]) = a_L + global_skip, where
       F = [x | hop_1 | ... | hop_h] (hop_j = chunk j of scatter_add(x[src % N], target)),
       a_0 = act(input_proj(F)), a_{k+1} = linear_2(dropout(act(linear_1(a_k)))) + a_k,
-      global_skip = global_skip_proj(F).
+      global_skip = global_skip_proj(F), or a_0.clone() when the reference builds no
+      global_skip_proj (input_dim == output_dim, layers.py:61,86-89).
+
+    Every configuration the reference accepts runs on the HIP kernels: any number of MLP blocks
+    (0 included, cli.py:106-107) on the fused stack when the layer is square (atom_input_dim ==
+    output_dim, the GNN's layers), else the composed path (hop kernel, MFMA GEMMs with fused
+    epilogues, the fused LinearBlock operator; `_stacked`).
     """
 
     def __init__(self, atom_input_dim: int, output_dim: int, num_hops: int = 3, dropout: float = 0.00,
@@ -45,12 +51,18 @@ class ShellConvolutionLayer(nn.Module):
         self._output_dim = output_dim
 
     # -- kernel plumbing -------------------------------------------------------------------
+    def _stacked(self):
+        """The fused stack's layer shape (aimx_shell_stack_*): atom_input_dim == output_dim (so a
+        global_skip_proj exists) and at most 8 MLP blocks — every layer the reference GNN builds."""
+        return self.global_skip_proj is not None and self._atom_input_dim == self._output_dim and \
+            len(self.mlp_blocks) <= 8
+
     def _aimx_params(self):
         """[input_proj.W, global_skip_proj.W, input_proj.b, global_skip_proj.b, (w1, b1, w2, b2) per
         block]; the operator packs [Wi ; Wg] of all layers with one cat kernel."""
-        if self.global_skip_proj is None or self._atom_input_dim != self._output_dim or len(self.mlp_blocks) == 0:
-            raise NotImplementedError("aimx: ShellConvolutionLayer needs global_skip_proj, equal in/out width and "
-                                      ">= 1 MLP block (every reference configuration does)")
+        if not self._stacked():
+            raise ValueError("aimx: the fused message-passing stack takes square shell layers with a "
+                             "global_skip_proj (GNN layers); ShellConvolutionLayer.forward handles the rest")
         p = [self.input_proj.weight, self.global_skip_proj.weight, self.input_proj.bias, self.global_skip_proj.bias]
         for b in self.mlp_blocks:
             p += [b["linear_1"].weight, b["linear_1"].bias, b["linear_2"].weight, b["linear_2"].bias]
@@ -69,10 +81,27 @@ class ShellConvolutionLayer(nn.Module):
         if plan is None or plan.N != x.shape[0] or plan.num_hops != self.num_hops:
             plan = GraphPlan(x.shape[0], self.num_hops, target=target, src=src)
         training, p = self._aimx_dropout()
+        if not self._stacked():
+            return self._composed(plan, x, training, p)
         seed = torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64) if training else None
         return ops.message_passing_stack(plan, x, self._aimx_params(), num_hops=self.num_hops, num_layers=1,
                                          num_mlp=len(self.mlp_blocks), act=self._aimx_act(), training=training,
                                          drop_p=p, drop_seed=seed, single=True)
+
+    def _composed(self, plan, x, training, p):
+        """layers.py:75-108 for the shapes the fused stack does not take (rectangular layers, no
+        global_skip_proj): the hop kernel, MFMA GEMMs with the activation fused in the epilogue and
+        the fused LinearBlock operator (linear_1 -> act -> dropout -> linear_2 + skip, layers.py:92-103)."""
+        n = x.shape[0]
+        F = torch.cat([x] + list(torch.split(ops.hop(plan, x), n, dim=0)), dim=-1)
+        act = self._aimx_act()
+        a = ops.linear(F, self.input_proj.weight, self.input_proj.bias, act)
+        skip = ops.linear(F, self.global_skip_proj.weight, self.global_skip_proj.bias) \
+            if self.global_skip_proj is not None else a.clone()
+        for b in self.mlp_blocks:
+            a = ops.linear_block(a, b["linear_1"].weight, b["linear_1"].bias, b["linear_2"].weight, b["linear_2"].bias,
+                                 act, p, training, True)
+        return a + skip
 
     def message_passing(self, atom_features: torch.Tensor, target: torch.Tensor, src: torch.Tensor) -> List[torch.Tensor]:
         """Per-hop aggregated features (reference layers.py:133-167): chunk j of

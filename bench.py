@@ -612,48 +612,98 @@ def _free_port():
         return sk.getsockname()[1]
 
 
-def launch_ranks(n, argv, poll_s=0.2, script=None):
+def _pdeathsig():
+    """A preexec_fn for the rank processes: the kernel sends the rank SIGKILL when this launcher
+    dies for any reason (prctl(PR_SET_PDEATHSIG)), so a launcher killed by the driver's timeout
+    leaves no rank holding a GPU. libc's prctl is bound here, in the parent: the child (between fork
+    and exec, before anything touches a GPU) only calls it."""
+    import ctypes
+    import signal
+    prctl = ctypes.CDLL(None, use_errno=True).prctl
+    parent = os.getpid()
+
+    def setup():
+        prctl(1, int(signal.SIGKILL))  # PR_SET_PDEATHSIG
+        if os.getppid() != parent:  # the launcher died before the request took effect
+            os._exit(1)
+    return setup
+
+
+def launch_ranks(n, argv, poll_s=0.2, script=None, deadline_s=0.0, straggler_s=300.0):
     """`python bench.py --gpus N` without a launcher: start N rank processes of this same script
     (children, never an exec of this process) and wait for them. This process never touches the
     GPU. Rank 0's stdout is this command's stdout (the one JSON line); the others' stdout goes to
     stderr. The first rank to fail stops the rest, and its exit code is returned (a rank that dies
-    would otherwise leave its peers waiting in a collective)."""
+    would otherwise leave its peers waiting in a collective).
+
+    No rank outlives the launcher or hangs it: SIGTERM / SIGINT / SIGHUP to the launcher are
+    forwarded to every rank's process group (exit 128 + the signal), each rank gets a parent-death
+    SIGKILL (_pdeathsig: a launcher killed outright takes its ranks with it), and the launcher stops
+    every rank and exits 124 once `deadline_s` (> 0) has passed since the start, or `straggler_s`
+    since the first rank finished cleanly while others still run (a peer hung in a collective)."""
     import signal
     import subprocess
     port = _free_port()
     procs = []
-    for r in range(n):
-        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv),
-                                      env=rank_env(os.environ, r, n, port),
-                                      stdout=None if r == 0 else sys.stderr.fileno(), start_new_session=True))
+    got = []
+    sigs = (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)
+    old = {sg: signal.signal(sg, lambda sig, frame: got.append(sig)) for sg in sigs}
+    setup = _pdeathsig()
+    t0 = time.time()
+    first_ok = None
     rc = 0
     try:
+        for r in range(n):
+            procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv),
+                                          env=rank_env(os.environ, r, n, port),
+                                          stdout=None if r == 0 else sys.stderr.fileno(), start_new_session=True,
+                                          preexec_fn=setup))
         while True:
+            if got:
+                rc = 128 + int(got[0])
+                print(f"bench: launcher got signal {int(got[0])}; stopping every rank", file=sys.stderr)
+                break
             codes = [p.poll() for p in procs]
             bad = [c for c in codes if c not in (None, 0)]
             if bad:
                 rc = bad[0]
+                print(f"bench: a rank exited with {rc}; stopping the other ranks", file=sys.stderr)
                 break
             if all(c == 0 for c in codes):
                 break
+            now = time.time()
+            if first_ok is None and any(c == 0 for c in codes):
+                first_ok = now
+            if deadline_s and now - t0 > deadline_s:
+                rc = 124
+                print(f"bench: deadline of {deadline_s:g} s passed; stopping every rank", file=sys.stderr)
+                break
+            if first_ok is not None and straggler_s and now - first_ok > straggler_s:
+                rc = 124
+                print(f"bench: ranks still running {straggler_s:g} s after a peer finished (hung in a "
+                      "collective?); stopping them", file=sys.stderr)
+                break
             time.sleep(poll_s)
-    except KeyboardInterrupt:
-        rc = 130
-    if rc:
-        print(f"bench: a rank exited with {rc}; stopping the other ranks", file=sys.stderr)
-        for p in procs:
-            if p.poll() is None:
+    finally:
+        if rc or len(procs) < n:
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+            grace = time.time() + 10
+            for p in procs:
                 try:
-                    os.killpg(p.pid, signal.SIGTERM)
-                except ProcessLookupError:
-                    pass
-        deadline = time.time() + 30
-        for p in procs:
-            try:
-                p.wait(timeout=max(0.1, deadline - time.time()))
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
-                p.wait()
+                    p.wait(timeout=max(0.1, grace - time.time()))
+                except subprocess.TimeoutExpired:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+                    p.wait()
+        for sg, h in old.items():
+            signal.signal(sg, h)
     return 128 - rc if rc < 0 else rc
 
 
@@ -688,6 +738,12 @@ def main():
     ap.add_argument("--ddp-world1", action="store_true",
                     help="A/B of the data-parallel step on one GPU: a world-size-1 RCCL group with the bucket "
                          "all-reduces kept (GradientSync always=True); AIMX_DDP_GRAPH=capture|split picks the mode")
+    ap.add_argument("--deadline", type=float, default=0.0,
+                    help="self-launched ranks (--gpus N without torchrun): stop every rank and exit 124 after this "
+                         "many seconds (0: none)")
+    ap.add_argument("--straggler", type=float, default=300.0,
+                    help="self-launched ranks: stop the others and exit 124 this many seconds after the first rank "
+                         "finished cleanly (a peer hung in a collective)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
@@ -697,7 +753,7 @@ def main():
         sys.exit(2)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `python bench.py --gpus N`: start the N ranks here, before anything touches the GPU
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], deadline_s=args.deadline, straggler_s=args.straggler))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a {world}-rank run as "

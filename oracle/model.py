@@ -58,7 +58,8 @@ def shell_layer(p, pre, x, target, src, cfg, training=False):
     chunks = message_passing(x, target, src, cfg["num_shells"])
     feats = torch.cat([x] + chunks, dim=-1)
     h = act(a, linear(p, pre + "input_proj", feats))
-    skip = linear(p, pre + "global_skip_proj", feats)
+    # layers.py:61,86-89: no global_skip_proj when input_dim (= D_in (h+1)) == output_dim
+    skip = linear(p, pre + "global_skip_proj", feats) if pre + "global_skip_proj.weight" in p else h.clone()
     for k in range(cfg["shell_conv_num_mlp_layers"]):
         b = f"{pre}mlp_blocks.{k}."
         y = linear(p, b + "linear_1", h)

@@ -17,7 +17,7 @@ featuriser over the reference's sample split) and synthetic 40-atom molecules (a
 Weights: oracle.model.seeded_params(cfg, seed) loaded into the reference with load_state_dict.
 
 Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.npz)
-        python tests/golden/make_golden.py init_weights stereo large   (only those groups)
+        python tests/golden/make_golden.py init_weights stereo large shell   (only those groups)
 """
 import ast
 import os
@@ -354,6 +354,57 @@ def case_stereo():
              grads=("message_passing_layers.", "stereochemical_embedding_2.", "embedding_projection."))
 
 
+def _shell_layer_case(rng, layer, n, h, e, offset_targets):
+    """One standalone ShellConvolutionLayer (layers.py:17-167) record: seeded parameters, inputs,
+    y = layer(x, tgt, src) and every gradient of sum(y * w)."""
+    params = {}
+    for k, p in layer.named_parameters():
+        r = np.random.default_rng([5, len(k), sum(map(ord, k))])
+        params[k] = torch.tensor(r.standard_normal(tuple(p.shape)) / (np.sqrt(p.shape[1]) if p.dim() == 2 else 10.0),
+                                 dtype=torch.float32)
+    layer.load_state_dict(params)
+    layer.eval()
+    d = layer.input_proj.weight.shape[1] // (h + 1)
+    x = torch.tensor(rng.standard_normal((n, d)), dtype=torch.float32, requires_grad=True)
+    tgt = torch.tensor(rng.integers(0, (h if offset_targets else 1) * n, e), dtype=torch.long)
+    src = torch.tensor(rng.integers(-100, 300, e) if offset_targets else rng.integers(0, h * n, e), dtype=torch.long)
+    y = layer(x, tgt, src)
+    w = torch.tensor(rng.standard_normal(tuple(y.shape)), dtype=torch.float32)
+    (y * w).sum().backward()
+    rec = {"x": x.detach().numpy(), "tgt": tgt.numpy(), "src": src.numpy(), "y": y.detach().numpy(),
+           "w": w.numpy(), "grad_x": x.grad.numpy(), "dims": np.array([d, y.shape[1], h, len(layer.mlp_blocks)])}
+    for k, p in layer.named_parameters():
+        rec["param." + k] = params[k].numpy()
+        rec["grad." + k] = p.grad.numpy()
+    return rec
+
+
+def case_shell():
+    """The general ShellConvolutionLayer contract (layers.py:32-108, cli.py:106-107): GNNs with
+    shell_conv_num_mlp_layers 0 and 3, and standalone layers without MLP blocks, without a
+    global_skip_proj (input_dim == output_dim: global_skip = x.clone(), layers.py:61,86-89) and
+    with output_dim != atom_input_dim."""
+    asset = QM9Asset()
+    run_case("nm0", default_config(hidden_dim=128, num_shells=3, shell_conv_num_mlp_layers=0),
+             asset.molecules(range(144, 176)), seed=14)
+    run_case("nm3", default_config(hidden_dim=128, num_shells=3, shell_conv_num_mlp_layers=3),
+             asset.molecules(range(176, 208)), seed=15)
+    rng = np.random.default_rng(31)
+    rec = {}
+    for tag, layer, n, h, e, off in (
+            ("sq_nm0", ShellConvolutionLayer(38, 38, num_hops=3, num_mlp_layers=0), 50, 3, 400, True),
+            ("noproj", ShellConvolutionLayer(16, 64, num_hops=3, num_mlp_layers=2), 60, 3, 500, False),
+            ("noproj_nm0", ShellConvolutionLayer(20, 60, num_hops=2, num_mlp_layers=0), 40, 2, 300, True),
+            ("rect", ShellConvolutionLayer(38, 50, num_hops=3, num_mlp_layers=1), 50, 3, 400, False),
+            ("rect_nm3", ShellConvolutionLayer(24, 40, num_hops=4, num_mlp_layers=3), 45, 4, 500, True)):
+        assert (layer.global_skip_proj is None) == tag.startswith("noproj"), tag
+        for k, v in _shell_layer_case(rng, layer, n, h, e, off).items():
+            rec[f"{tag}.{k}"] = v
+    path = os.path.join(HERE, "shell_layers.npz")
+    np.savez_compressed(path, **rec)
+    print("shell_layers:", os.path.getsize(path))
+
+
 def case_large():
     c4 = default_config(hidden_dim=512, num_shells=3)
     run_case("c4s", c4, synth_molecules(64, seed=4), seed=4,
@@ -368,7 +419,7 @@ def main():
     only = sys.argv[1:]
     if only:
         for nm in only:
-            {"init_weights": case_init_weights, "stereo": case_stereo, "large": case_large}[nm]()
+            {"init_weights": case_init_weights, "stereo": case_stereo, "large": case_large, "shell": case_shell}[nm]()
         return
     asset = QM9Asset()
     case_edges()
@@ -385,6 +436,7 @@ def main():
     case_large()
     case_init_weights()
     case_stereo()
+    case_shell()
     for kind in ("mean", "max", "sum"):
         cfg = default_config(hidden_dim=128, num_shells=3, pooling_type=kind)
         run_case(f"pool_{kind}", cfg, asset.molecules(range(32, 64)), seed=6,

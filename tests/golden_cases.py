@@ -7,7 +7,8 @@ import torch
 from conftest import load_golden
 
 CASES = ["c1", "c2", "c3", "c4s", "c5s", "pool_mean", "pool_max", "pool_sum",
-         "act_relu", "act_leakyrelu", "act_elu", "act_gelu", "evidential", "noedges", "stereo", "stereo_pc"]
+         "act_relu", "act_leakyrelu", "act_elu", "act_gelu", "evidential", "noedges", "stereo", "stereo_pc",
+         "nm0", "nm3"]
 FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
 
 

@@ -82,3 +82,71 @@ def test_gpus_must_equal_world_size(world, gpus):
     assert p.returncode == 2, p.stderr
     assert f"--gpus {gpus} but WORLD_SIZE {world}" in p.stderr
     assert p.stdout == ""
+
+
+def _alive(pid):
+    """True while pid exists and is not a zombie."""
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            return not any(ln.startswith("State:") and "Z" in ln.split()[1] for ln in f)
+    except FileNotFoundError:
+        return False
+
+
+def _launcher(tmp_path, n, body, extra=""):
+    """A separate launcher process (python -> bench.launch_ranks) whose ranks write their pids."""
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    script = _script(tmp_path, f"open(os.path.join({str(pids)!r}, os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                     + body)
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+            f"sys.exit(bench.launch_ranks({n}, [], script={script!r}{extra}))")
+    p = subprocess.Popen([sys.executable, "-c", code], start_new_session=True)
+    t0 = time.time()
+    while len(os.listdir(pids)) < n and time.time() - t0 < 120:
+        time.sleep(0.05)
+    assert len(os.listdir(pids)) == n, "ranks did not start"
+    return p, [int((pids / f).read_text()) for f in sorted(os.listdir(pids))]
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGHUP", "SIGINT"])
+def test_launcher_signal_stops_every_rank(tmp_path, sig):
+    """The driver's timeout signals the launcher: every rank is gone within 5 s and the launcher
+    exits 128 + the signal."""
+    import signal
+    p, pids = _launcher(tmp_path, 3, "time.sleep(300)\n")
+    p.send_signal(getattr(signal, sig))
+    assert p.wait(timeout=30) == 128 + int(getattr(signal, sig))
+    t0 = time.time()
+    while any(_alive(q) for q in pids) and time.time() - t0 < 5:
+        time.sleep(0.05)
+    assert not any(_alive(q) for q in pids)
+
+
+def test_launcher_killed_outright_takes_its_ranks(tmp_path):
+    """SIGKILL cannot be forwarded: the ranks' parent-death signal ends them within 5 s."""
+    import signal
+    p, pids = _launcher(tmp_path, 2, "time.sleep(300)\n")
+    p.send_signal(signal.SIGKILL)
+    p.wait(timeout=30)
+    t0 = time.time()
+    while any(_alive(q) for q in pids) and time.time() - t0 < 5:
+        time.sleep(0.05)
+    assert not any(_alive(q) for q in pids)
+
+
+def test_hung_rank_with_finished_peer_hits_the_deadline(tmp_path):
+    """Rank 0 finishes, rank 1 hangs (a collective that never completes): the launcher stops it
+    and exits non-zero by the deadline (and by the straggler window, whichever comes first)."""
+    body = "if os.environ['RANK'] == '1':\n    time.sleep(300)\n"
+    for extra, limit in ((", deadline_s=3.0", 20), (", straggler_s=2.0", 20)):
+        sub = tmp_path / extra.strip(", =.").replace("=", "")
+        sub.mkdir()
+        t0 = time.time()
+        p, pids = _launcher(sub, 2, body, extra)
+        assert p.wait(timeout=60) == 124
+        assert time.time() - t0 < limit
+        t1 = time.time()
+        while any(_alive(q) for q in pids) and time.time() - t1 < 5:
+            time.sleep(0.05)
+        assert not any(_alive(q) for q in pids)

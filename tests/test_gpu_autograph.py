@@ -310,3 +310,38 @@ def test_autograph_grad_hooks_fire_through_autograd():
     finally:
         for h in hs:
             h.remove()
+
+
+def test_autograph_hooked_accumulation_without_zero_grad():
+    """through autograd (_ReplayGrads, here via a post-accumulate hook) the first
+    backward hands out fresh views of the bucket's static gradients. A second forward/backward
+    WITHOUT zero_grad (gradient accumulation, DDP no_sync micro-batches) replays into that same
+    memory: each .grad must end as g_old + g_new (eager), not 2 g_new. Two batches of the same
+    bucket, then a third step after zero_grad(set_to_none=False)."""
+    from aimx import autograph
+    bs = _batches(2, 17)
+    m1 = _model()
+    m2 = _model()
+    m2.load_state_dict(m1.state_dict())
+    autograph.enable(m2)
+    hs = [p.register_post_accumulate_grad_hook(lambda p: None) for p in m2.parameters()]
+    try:
+        for m in (m1, m2):
+            m.zero_grad(set_to_none=True)
+        for k, b in enumerate(bs + [bs[0]]):
+            if k == 2:
+                for m in (m1, m2):
+                    m.zero_grad(set_to_none=False)
+            for m in (m1, m2):
+                o, _, _ = m(*b.model_args())
+                (o.square().sum() + o.sum()).backward()
+            torch.cuda.synchronize()
+            assert autograph._state(m2).buckets, "the replay did not run"
+            for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+                if p1.grad is None:
+                    assert p2.grad is None, n
+                else:
+                    assert _rel(p2.grad, p1.grad) < 1e-5, (k, n, _rel(p2.grad, p1.grad))
+    finally:
+        for h in hs:
+            h.remove()

@@ -506,6 +506,35 @@ def test_shell_layer_standalone():
     assert not bad, bad
 
 
+@pytest.mark.parametrize("tag", ["sq_nm0", "noproj", "noproj_nm0", "rect", "rect_nm3"])
+def test_shell_layer_contract(tag):
+    """The general ShellConvolutionLayer contract against reference-generated fixtures
+    (shell_layers.npz, tests/golden/make_golden.py case_shell): no MLP blocks (cli.py:106-107),
+    no global_skip_proj (input_dim == output_dim: global_skip = x.clone(), layers.py:61,86-89),
+    output_dim != atom_input_dim, hop-offset and plain targets; outputs and every gradient vs the
+    fp64 oracle, the fixture's fp32 error as the floor once the fp32 oracle pins it."""
+    from models.layers import ShellConvolutionLayer
+    from test_oracle_golden import shell_layer_oracle
+    z = load_golden("shell_layers")
+    d, dout, h, nm = (int(v) for v in z[f"{tag}.dims"])
+    layer = ShellConvolutionLayer(d, dout, num_hops=h, num_mlp_layers=nm)
+    pre = f"{tag}.param."
+    layer.load_state_dict({k[len(pre):]: torch.from_numpy(z[k]) for k in z.files if k.startswith(pre)})
+    layer = layer.to(DEV).eval()
+    assert (layer.global_skip_proj is None) == tag.startswith("noproj")
+    x = torch.from_numpy(z[f"{tag}.x"]).to(DEV).requires_grad_()
+    y = layer(x, torch.from_numpy(z[f"{tag}.tgt"]).to(DEV), torch.from_numpy(z[f"{tag}.src"]).to(DEV))
+    (y * torch.from_numpy(z[f"{tag}.w"]).to(DEV)).sum().backward()
+    ours = {"y": y.detach().cpu().numpy(), "grad_x": x.grad.cpu().numpy()}
+    ours.update({"grad." + k: p.grad.cpu().numpy() for k, p in layer.named_parameters()})
+    torch.set_num_threads(8)
+    o32 = shell_layer_oracle(z, tag, torch.float32)
+    o64 = shell_layer_oracle(z, tag, torch.float64)
+    assert set(ours) == set(o64), set(ours) ^ set(o64)
+    bad = parity_failures(ours, {k: z[f"{tag}.{k}"] for k in ours}, o64, oracle32=o32)
+    assert not bad, bad
+
+
 def test_attention_pool_standalone():
     from models.pooling import MultiHeadAttentionPoolingLayer
     _, om = _oracle()

@@ -184,3 +184,36 @@ def test_init_weights_matches_reference(tag):
     assert list(sd.keys()) == keys
     for k in keys:
         assert np.array_equal(sd[k].numpy(), z[f"{tag}.{k}"]), k
+
+
+SHELL_TAGS = ["sq_nm0", "noproj", "noproj_nm0", "rect", "rect_nm3"]
+
+
+def shell_layer_oracle(z, tag, dtype):
+    """The oracle's ShellConvolutionLayer (oracle/model.py shell_layer) on a shell_layers.npz record:
+    (y, grad_x, {param grad})."""
+    d, dout, h, nm = (int(v) for v in z[f"{tag}.dims"])
+    pre = f"{tag}.param."
+    p = {"l." + k[len(pre):]: torch.from_numpy(z[k]).to(dtype).requires_grad_() for k in z.files if k.startswith(pre)}
+    x = torch.from_numpy(z[f"{tag}.x"]).to(dtype).requires_grad_()
+    cfg = {"activation": "silu", "num_shells": h, "shell_conv_num_mlp_layers": nm, "shell_conv_dropout": 0.0}
+    y = om.shell_layer(p, "l.", x, torch.from_numpy(z[f"{tag}.tgt"]), torch.from_numpy(z[f"{tag}.src"]), cfg)
+    (y * torch.from_numpy(z[f"{tag}.w"]).to(dtype)).sum().backward()
+    res = {"y": y.detach().numpy(), "grad_x": x.grad.numpy()}
+    res.update({"grad." + k[2:]: v.grad.numpy() for k, v in p.items()})
+    return res
+
+
+@pytest.mark.parametrize("tag", SHELL_TAGS)
+def test_shell_layer_contract(tag):
+    """Standalone ShellConvolutionLayer without MLP blocks, without global_skip_proj (input_dim ==
+    output_dim, layers.py:61,86-89) and with output_dim != atom_input_dim: the oracle pinned to the
+    reference's own fp32 outputs and gradients (shell_layers.npz)."""
+    torch.set_num_threads(8)
+    z = load_golden("shell_layers")
+    r32 = shell_layer_oracle(z, tag, torch.float32)
+    r64 = shell_layer_oracle(z, tag, torch.float64)
+    ref = {k: z[f"{tag}.{k}"] for k in r32}
+    assert (f"{tag}.param.global_skip_proj.weight" in z.files) == (not tag.startswith("noproj"))
+    bad = pin_failures(r32, ref, r64)
+    assert not bad, bad
