@@ -48,6 +48,34 @@ def _scale_for(key, ref64):
 
 
 PIN_TOL = 1e-6
+GOLDEN_HOST = os.path.join(GOLDEN, "HOST.json")
+
+
+def host_fingerprint():
+    """What decides ATen's fp32 CPU arithmetic: the CPU model (MKL / oneDNN pick their kernels by
+    vendor and ISA), the dispatch capability and the torch build."""
+    import torch
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"cpu": model, "capability": torch.backends.cpu.get_cpu_capability(), "torch": torch.__version__}
+
+
+def fixture_host():
+    """True on the host the golden fixtures were made on (tests/golden/HOST.json, written by
+    make_golden.py): there the oracle's fp32 run reproduces the reference's own fp32 tensors to
+    PIN_TOL. On another CPU (the MI355X boxes' AMD EPYC) ATen's fp32 GEMM / reduction kernels round
+    differently, and the same oracle code moves by up to ~1-3x the reference's own fp32 error
+    (measured: profiles/r05_pin_probe_box.json)."""
+    import json
+    try:
+        with open(GOLDEN_HOST) as f:
+            return json.load(f) == host_fingerprint()
+    except (OSError, ValueError):
+        return False
 
 
 def _rel(a, b, den):
@@ -63,30 +91,40 @@ def _den(key, b, scale_src):
     return max(np.abs(b).max() if b.size else 0.0, _scale_for(key, scale_src))
 
 
-def pin_tol(key, r32, ref64, tol=PIN_TOL):
-    """PIN_TOL, widened only where the reference's own fp32 error vs exact is large: by 5 % of
-    that error (CPU reductions regrouped by the thread count move c3's pool gradients by 2e-6
-    where the reference itself is 1e-4 from exact). A systematic oracle bug of 1e-4 still fails."""
-    if ref64 is None or key not in ref64:
-        return tol
-    return max(tol, 0.05 * _rel(r32, ref64[key], _den(key, ref64[key], ref64)))
+def pin_tol(key, r32, ref64, tol=PIN_TOL, same_host=None):
+    """The pin's bound for one tensor. On the fixture host: PIN_TOL, widened only where the
+    reference's own fp32 error vs exact is large, by 5 % of that error (CPU reductions regrouped by
+    the thread count move c3's pool gradients by 2e-6 where the reference itself is 1e-4 from exact).
+    Elsewhere (another CPU's ATen kernels, see fixture_host): max(3e-5, 5x the reference's own fp32
+    error) — a sanity bound on that host's own ATen rounding (the EPYC boxes' worst: 4.5x, the
+    attention pool's temperature gradient), not the pin: the code-level pin is the fixture host's,
+    run by the CPU suite every round. The floor the GPU tests then take, |fixture - fp64 oracle|, does
+    not depend on the host (the fp64 runs agree to ~1e-15)."""
+    own = _rel(r32, ref64[key], _den(key, ref64[key], ref64)) if (ref64 is not None and key in ref64) else 0.0
+    if same_host is None:
+        same_host = fixture_host()
+    if same_host:
+        return max(tol, 0.05 * own)
+    return max(3e-5, 5.0 * own)
 
 
-def pin_failures(oracle32, ref32, ref64=None, tol=PIN_TOL):
+def pin_failures(oracle32, ref32, ref64=None, tol=PIN_TOL, same_host=None):
     """The oracle pin: the oracle's fp32 run against the reference's OWN fp32 tensors (a golden
     fixture made by importing the reference, tests/golden/make_golden.py), per tensor,
-    norm-relative <= tol (1e-6). The oracle replays the reference's ATen ops in the reference's
-    order, so the two agree bit for bit on most cases and within 2.4e-7 on the rest (measured on
-    all 16 fixture cases; `pin_tol`). Returns [(key, err, tol)] for every tensor that misses (or
-    is missing)."""
+    norm-relative <= tol (1e-6) on the fixture host. The oracle replays the reference's ATen ops in
+    the reference's order, so there the two agree bit for bit on most cases and within 2.4e-7 on
+    the rest (measured on every fixture case; `pin_tol`). Returns [(key, err, tol)] for every tensor
+    that misses (or is missing)."""
     bad = []
     src = ref64 if ref64 is not None else ref32
+    if same_host is None:
+        same_host = fixture_host()
     for k, r in ref32.items():
         if k not in oracle32:
             bad.append((k, "missing", tol))
             continue
         err = _rel(oracle32[k], r, _den(k, r, src))
-        t = pin_tol(k, r, ref64, tol)
+        t = pin_tol(k, r, ref64, tol, same_host)
         if not err <= t:
             bad.append((k, err, t))
     return bad
@@ -101,14 +139,18 @@ def parity_failures(ours, ref32, ref64, atol_rel=1e-5, factor=3.0, oracle32=None
     reference than the reference is to the exact answer. Where it comes from, per tensor k:
 
     * k in `ref32` (the reference's own fp32 output, a golden fixture): its error vs fp64 — but
-      ONLY once the oracle pin holds for k, i.e. `oracle32[k]` (the oracle's fp32 run on the same
-      inputs) is within `pin_tol` of `ref32[k]` (`pin_failures`). A missed pin is itself a failure
-      (`("pin:" + k, err, PIN_TOL)`); without `oracle32` no floor is taken (tol = 1e-5).
+      ONLY once the oracle pin holds for k, i.e. the oracle's fp32 run on the same inputs is within
+      `pin_tol` of `ref32[k]` (`pin_failures`). A missed pin is itself a failure
+      (`("pin:" + k, err, tol)`); without `oracle32` no floor is taken (tol = 1e-5).
     * k only in `oracle32` (no reference output exists, e.g. config-sized batches): the oracle's
       own fp32 error — the same ATen op sequence that `tests/test_oracle_golden.py` pins to the
-      reference on every fixture case.
+      reference on every fixture case. `oracle32` may be a list of such runs (the same function
+      evaluated in different legitimate fp32 orders, golden_cases.reversed_molecules): the floor is
+      their largest error, a less noisy estimate of fp32 rounding than one draw.
     * neither: no floor.
     """
+    runs = oracle32 if isinstance(oracle32, (list, tuple)) else ([oracle32] if oracle32 is not None else [])
+    same_host = fixture_host() if (ref32 is not None and runs) else None
     bad = []
     for k, v64 in ref64.items():
         if k not in ours:
@@ -117,15 +159,15 @@ def parity_failures(ours, ref32, ref64, atol_rel=1e-5, factor=3.0, oracle32=None
         err = _rel(ours[k], v64, den)
         floor = 0.0
         if ref32 is not None and k in ref32:
-            if oracle32 is not None and k in oracle32:
-                pin = _rel(oracle32[k], ref32[k], _den(k, ref32[k], ref64))
-                ptol = pin_tol(k, ref32[k], ref64)
+            if runs and k in runs[0]:
+                pin = _rel(runs[0][k], ref32[k], _den(k, ref32[k], ref64))
+                ptol = pin_tol(k, ref32[k], ref64, same_host=same_host)
                 if not pin <= ptol:
                     bad.append(("pin:" + k, pin, ptol))
                 else:
                     floor = _rel(ref32[k], v64, den)
-        elif oracle32 is not None and k in oracle32:
-            floor = _rel(oracle32[k], v64, den)
+        else:
+            floor = max([_rel(r[k], v64, den) for r in runs if k in r], default=0.0)
         tol = max(atol_rel, factor * floor)
         if not err <= tol:
             bad.append((k, err, tol))

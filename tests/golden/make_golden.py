@@ -414,8 +414,21 @@ def case_large():
              grads=("message_passing_layers.", "pooling."), sketch_over=100_000)
 
 
+def write_host():
+    """The host the fixtures come from (tests/conftest.py fixture_host: the oracle pin is exact
+    only under the same CPU kernels)."""
+    import json
+    model = ""
+    with open("/proc/cpuinfo") as f:  # the same fields as tests/conftest.py host_fingerprint
+        model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    fp = {"cpu": model, "capability": torch.backends.cpu.get_cpu_capability(), "torch": torch.__version__}
+    with open(os.path.join(HERE, "HOST.json"), "w") as f:
+        json.dump(fp, f, indent=1)
+
+
 def main():
     torch.set_num_threads(8)
+    write_host()
     only = sys.argv[1:]
     if only:
         for nm in only:

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from conftest import add_sketches, fixture_refs, load_golden, norm_rel, parity_failures
-from golden_cases import CASES, case_stereo, load_case
+from golden_cases import CASES, case_stereo, load_case, reversed_molecules
 
 pytestmark = pytest.mark.gpu
 
@@ -695,8 +695,9 @@ def _run_full(cfg, seed, inputs, loss_w, device, dtype=torch.float32):
 def test_model_full_size(name):
     """c4 / c5 at their configured per-GPU batch (512 x 40-atom molecules h512 3 hops; 256 x
     40-atom h1024 6 hops): outputs, attention and every parameter gradient, element for element,
-    within the parity contract against the fp64 oracle (the floor: the oracle's own fp32 run, the
-    reference's ATen ops pinned by tests/test_oracle_golden.py). Exercises what the 64 / 32-molecule
+    within the parity contract against the fp64 oracle (the floor: the larger error of the oracle's
+    fp32 run on the batch and on the molecule-reversed batch — the reference's ATen ops, pinned by
+    tests/test_oracle_golden.py — golden_cases.reversed_molecules). Exercises what the 64 / 32-molecule
     fixtures cannot: the weight-streamed MLP at its 96 / 48-row chunks, full-K (~20 k atom) split-K
     weight gradients, multi-window hop tiling."""
     z, cfg, inputs, loss_w = full_size_case(name)
@@ -704,9 +705,11 @@ def test_model_full_size(name):
     seed = int(z["seed"])
     ref64 = _run_full(cfg, seed, inputs, loss_w, "cpu", torch.float64)
     ref32 = _run_full(cfg, seed, inputs, loss_w, "cpu", torch.float32)
+    rin, rlw, unperm = reversed_molecules(inputs, loss_w)
+    ref32r = unperm(_run_full(cfg, seed, rin, rlw, "cpu", torch.float32))
     ours = _run_full(cfg, seed, inputs, loss_w, "cuda")
     assert set(ours) == set(ref64), set(ours) ^ set(ref64)
-    bad = parity_failures(ours, None, ref64, oracle32=ref32)
+    bad = parity_failures(ours, None, ref64, oracle32=[ref32, ref32r])
     assert not bad, bad
 
 

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from conftest import parity_failures
-from golden_cases import FEATURE_KEYS, load_case
+from golden_cases import FEATURE_KEYS, load_case, reversed_molecules
 from test_gpu_parity import _build_model
 
 pytestmark = pytest.mark.gpu
@@ -78,8 +78,10 @@ def test_stream_6hop_feeds_gpu_model_at_parity(tmp_path, world, rank):
         tc = torch.zeros(B)
         ref64 = _oracle_grads(cfg, int(z["seed"]), af, edges, batch, tc, loss_w, torch.float64)
         ref32 = _oracle_grads(cfg, int(z["seed"]), af, edges, batch, tc, loss_w, torch.float32)
+        (raf, red, rb, rtc), rlw, unperm = reversed_molecules((af, edges, batch, tc), loss_w)
+        ref32r = unperm(_oracle_grads(cfg, int(z["seed"]), raf, red, rb, rtc, rlw, torch.float32))
         assert set(ours) == set(ref64), set(ours) ^ set(ref64)
-        bad = parity_failures(ours, None, ref64, oracle32=ref32)
+        bad = parity_failures(ours, None, ref64, oracle32=[ref32, ref32r])
         assert not bad, bad
         seen += 1
     assert seen == len(pos) // B >= 1
