@@ -22,6 +22,7 @@ c_ptr = ctypes.c_void_p
 c_size = ctypes.c_size_t
 
 ACT_KIND = {"relu": 0, "leakyrelu": 1, "elu": 2, "gelu": 3, "silu": 4}
+GATHER_SKIP_TAIL = 1  # AIMX_GATHER_SKIP_TAIL (include/aimx.h)
 
 
 class AimxError(RuntimeError):
@@ -186,6 +187,8 @@ _SIGS = {
     "aimx_csr_build_multi": (c_i32, [ctypes.POINTER(CsrSpec), c_i32, c_ptr, c_size, c_ptr, c_ptr]),
     "aimx_segment_gather_sum": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i64,
                                         c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "aimx_segment_gather_sum_ex": (c_i32, [c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_i64,
+                                           c_i64, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr]),
     "aimx_gemm_workspace_bytes": (c_size, [ctypes.POINTER(GemmArgs)]),
     "aimx_gemm": (c_i32, [ctypes.POINTER(GemmArgs), c_ptr]),
     "aimx_shell_stack_workspace_bytes": (c_size, [ctypes.POINTER(ShellStack)]),

@@ -629,3 +629,15 @@ extern "C" int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t
   return aimx::segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs,
                                   add0, add0_ld, add1, add1_ld, row_seg, row_seg_stride, (hipStream_t)stream, 0);
 }
+
+extern "C" int aimx_segment_gather_sum_ex(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs,
+                                          int64_t D, const int32_t* rowptr, const int32_t* col, int64_t rows,
+                                          float* out, int64_t out_ld, int64_t out_rpc, int64_t out_cs,
+                                          const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld,
+                                          const int64_t* row_seg, int64_t row_seg_stride, int32_t flags,
+                                          aimx_stream_t stream) {
+  if (flags & ~AIMX_GATHER_SKIP_TAIL) return AIMX_EARG;
+  return aimx::segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs,
+                                  add0, add0_ld, add1, add1_ld, row_seg, row_seg_stride, (hipStream_t)stream,
+                                  (flags & AIMX_GATHER_SKIP_TAIL) ? 1 : 0);
+}

@@ -322,7 +322,8 @@ def hop_in_step(batch, hops, hidden, device):
                 inputs, layers.py:154, so chunk 0 only), plus the chunk-0 gradient dF[:, :D] and
                 the outer residual dY (row stride 2 D) added, written into the next-lower layer's
                 dUG slot (row stride 2 D).
-    Algorithmic bytes: fwd 4 [N D + E + (h N + 1) + h N D] (every chunk written);
+    Algorithmic bytes: fwd 4 [N D + E + (h N + 1) + w N D], w = the chunks the step writes (the
+    stack skips the trailing edge-less ones, which its GEMMs trim: chunk 0 only for reference inputs);
     bwd 4 [N D (gathered rows) + E + (N + 1) + 2 N D (the residual reads) + N D (written)]."""
     from aimx import _lib
     from aimx.plan import GraphPlan
@@ -341,20 +342,24 @@ def hop_in_step(batch, hops, hidden, device):
     fl = 4  # bytes per float: column offsets as pointer arithmetic
     kern = "k_gather_sum" if d % 4 == 0 else "k_gather_rows"
 
-    def fwd():
-        assert lib.aimx_segment_gather_sum(P(F), K, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n,
-                                           P(F) + fl * d, K, n, d, None, 0, None, 0, seg, seg_st, s) == 0
+    def fwd():  # the stack's call: trailing edge-less chunks not written (AIMX_GATHER_SKIP_TAIL)
+        assert lib.aimx_segment_gather_sum_ex(P(F), K, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n,
+                                              P(F) + fl * d, K, n, d, None, 0, None, 0, seg, seg_st,
+                                              _lib.GATHER_SKIP_TAIL, s) == 0
 
     def bwd():
         assert lib.aimx_segment_gather_sum(P(dF) + fl * d, K, n, d, d, P(plan.bwd.rowptr), P(plan.bwd.col), n,
                                            P(nxt) + fl * d, 2 * d, 0, 0, P(dF), K, P(dUG) + fl * d, 2 * d,
                                            seg, seg_st, s) == 0
+    # chunks the step writes: up to the last one holding an edge (reference inputs: chunk 0 only)
+    rp = plan.fwd.rowptr.cpu()
+    written = max([k + 1 for k in range(hops) if int(rp[(k + 1) * n]) > int(rp[k * n])], default=0)
     torch.cuda.synchronize()
     tf, tb = cold_time_us(fwd, device), cold_time_us(bwd, device)
-    bf = 4 * (n * d + e + (hops * n + 1) + hops * n * d)
+    bf = 4 * (n * d + e + (hops * n + 1) + written * n * d)
     bb = 4 * (n * d + e + (n + 1) + 2 * n * d + n * d)
     note = "the stack's own layout (F column offset D, residual adds), cold MALL (512 MiB flush per launch)"
-    return {"atoms": n, "edges": e, "D": d, "hops": hops,
+    return {"atoms": n, "edges": e, "D": d, "hops": hops, "chunks_written": written,
             "fwd": _bw(kern + " (hop fwd, in-step layout)", bf, tf, timing=note),
             "bwd": _bw(kern + " (hop bwd + residual adds, in-step layout)", bb, tb, timing=note)}
 

@@ -111,6 +111,21 @@ int aimx_segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rows_p
                             const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld,
                             const int64_t* row_seg, int64_t row_seg_stride, aimx_stream_t stream);
 
+/* aimx_segment_gather_sum with flags. AIMX_GATHER_SKIP_TAIL: output chunks in the trailing run of
+ * edge-less chunks (out_rows_per_chunk > 0) are NOT written — their rows keep whatever the buffer
+ * held. For consumers that never read those chunks: the message-passing stack's hop (the reference's
+ * chunks >= 1 are empty, layers.py:154, and its GEMMs trim them exactly, AimxGemmArgs.zc_*). The
+ * call the stack makes per layer, exposed so that its cost can be timed on its own. */
+#define AIMX_GATHER_SKIP_TAIL 1
+int aimx_segment_gather_sum_ex(const float* src, int64_t src_ld, int64_t src_rows_per_chunk,
+                               int64_t src_chunk_stride, int64_t D,
+                               const int32_t* rowptr, const int32_t* col, int64_t rows,
+                               float* out, int64_t out_ld, int64_t out_rows_per_chunk,
+                               int64_t out_chunk_stride,
+                               const float* add0, int64_t add0_ld, const float* add1, int64_t add1_ld,
+                               const int64_t* row_seg, int64_t row_seg_stride, int32_t flags,
+                               aimx_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------
  * Fused fp32 GEMM on the matrix cores (v_mfma_f32_16x16x4_f32; exact f32 fmaf chains), the
  * building block of the node-update MLP (reference layers.py:82-106, nn.Linear/addmm):
