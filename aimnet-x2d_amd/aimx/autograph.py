@@ -103,8 +103,10 @@ def _through_autograd(model):
     """Hand the gradients out through autograd (the parameters' AccumulateGrad nodes) instead of
     assigning .grad: whenever something may be watching them — a process group is initialised
     (DistributedDataParallel's reducer hooks every gradient accumulator, reference runner.py:703-707,
-    and averages the buckets as they become ready), or a parameter carries gradient hooks."""
-    return _dist_initialized() or _state(model).grad_hooked(model)
+    and averages the buckets as they become ready), or a parameter carries gradient hooks. (Under
+    DDP with the model's own sync, run() takes _ReplayDDP instead unless other hooks exist.)"""
+    sync = model.__dict__.get("_aimx_sync")
+    return _dist_initialized() or _state(model).grad_hooked(model, sync.hook_ids if sync is not None else ())
 
 
 class _State:
@@ -117,9 +119,12 @@ class _State:
         """Forward hooks on a submodule: a replay cannot fire them (the eager path runs instead)."""
         return any(m._forward_hooks or m._forward_pre_hooks for m in model.modules() if m is not model)
 
-    def grad_hooked(self, model):
-        """Gradient hooks on a parameter: the replay then hands its gradients out through autograd."""
-        return any(getattr(p, "_post_accumulate_grad_hooks", None) or getattr(p, "_backward_hooks", None)
+    def grad_hooked(self, model, ignore=()):
+        """Gradient hooks on a parameter (other than the handles in `ignore`: the model's own
+        gradient sync): the replay then hands its gradients out through autograd."""
+        def hooked(d):
+            return bool(d) and any(k not in ignore for k in d)
+        return any(hooked(getattr(p, "_post_accumulate_grad_hooks", None)) or hooked(getattr(p, "_backward_hooks", None))
                    for p in model.parameters())
 
 
@@ -298,6 +303,48 @@ class _Replay(torch.autograd.Function):
         return None, None, None
 
 
+class _ReplayDDP(torch.autograd.Function):
+    """_Replay under DistributedDataParallel with the model's own gradient sync
+    (GNN._ddp_params_and_buffers_to_ignore): the anchor parameter, the one DDP's reducer keeps, gets
+    its gradient through autograd (DDP's hooks and end-of-backward bookkeeping run on it); every
+    other gradient is averaged across the ranks by the sync right after the backward replay (pack,
+    one all-reduce per bucket, unpack) and handed to .grad as _Replay does."""
+
+    @staticmethod
+    def forward(ctx, anchor, bucket, G, sync, p_anchor):
+        ctx.bucket, ctx.G, ctx.gen, ctx.sync, ctx.p_anchor = bucket, G, bucket.gen, sync, p_anchor
+        return bucket.outs[0][:G].clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        b, pa = ctx.bucket, ctx.p_anchor
+        if b.gen != ctx.gen or b.done == ctx.gen:
+            raise AimxError("aimx autograph: this output's saved state was overwritten by a later forward of the "
+                            "same shape bucket (or its backward already ran); run one backward per forward, or "
+                            "set AIMX_AUTOGRAPH=0")
+        b.gout[:ctx.G].copy_(gout)
+        keep = {}
+        for p, sg in zip(b.params, b.grads):
+            if sg is not None and p.grad is sg:
+                keep[id(p)] = sg.clone()
+        b.g_bwd.replay()
+        b.done = ctx.gen
+        ctx.sync.reduce_tensors({id(p): sg for p, sg in zip(b.params, b.grads) if sg is not None and p is not pa})
+        ga = None
+        for p, sg in zip(b.params, b.grads):
+            if sg is None:
+                continue
+            if p is pa:
+                ga = sg.clone()  # DDP's reducer averages this one (and may write into .grad)
+            elif p.grad is None:
+                p.grad = sg
+            elif p.grad is sg:
+                sg.add_(keep[id(p)])
+            else:
+                p.grad.add_(sg)
+        return None, None, None, None, ga
+
+
 class _ReplayGrads(torch.autograd.Function):
     """_Replay for watched gradients (_through_autograd): the parameters with a gradient are inputs,
     and the backward replay's static gradients come back as their gradients, so autograd's
@@ -379,7 +426,13 @@ def run(model, args):
     b.gen += 1
     if st.anchor is None or st.anchor.device != dev:
         st.anchor = torch.zeros((), device=dev, requires_grad=True)
-    if _through_autograd(model):
+    native = model._aimx_native_sync() if hasattr(model, "_aimx_native_sync") else None
+    p_anchor = None
+    if native is not None:
+        p_anchor = dict(model.named_parameters()).get(getattr(model, "_DDP_ANCHOR", ""))
+    if native is not None and p_anchor is not None and not st.grad_hooked(model, native.hook_ids):
+        out = _ReplayDDP.apply(st.anchor, b, G, native, p_anchor)
+    elif _through_autograd(model):
         out = _ReplayGrads.apply(st.anchor, b, G, *[p for p, sg in zip(b.params, b.grads) if sg is not None])
     else:
         out = _Replay.apply(st.anchor, b, G)

@@ -124,6 +124,8 @@ class GNN(nn.Module):
         args = (atom_features, multi_hop_edge_indices, batch_indices, total_charges, tetrahedral_indices,
                 cis_indices, trans_indices)
         _lib.require_device(multi_hop_edge_indices, batch_indices, total_charges)
+        if self.training and torch.is_grad_enabled():
+            self._aimx_native_sync()  # wrapped by DDP: our gradient sync exists before the backward
         if autograph.wanted(self, args):  # per-shape-bucket graph replay (aimx/autograph.py; AIMX_AUTOGRAPH=0: off)
             return autograph.run(self, args)
         return self._aimx_forward(*args)
@@ -339,6 +341,61 @@ class GNN(nn.Module):
                 nn.init.xavier_uniform_(head.weight)
                 if head.bias is not None:
                     nn.init.zeros_(head.bias)
+
+    # -- DistributedDataParallel (reference runner.py:703-707) -----------------------------------
+    # DDP's constructor reads `module._ddp_params_and_buffers_to_ignore` (the hook it offers modules
+    # for parameters whose gradients they synchronise themselves). Here it is a property: reading it
+    # is how the model learns it is being wrapped. It then keeps ONE used parameter (_DDP_ANCHOR) in
+    # DDP's reducer — DDP refuses a module with none, and that parameter's hook is what DDP's own
+    # end-of-backward bookkeeping runs on — and averages every other gradient itself
+    # (utils.distributed.GradientSync: bucketed RCCL all-reduce over our own communicator), which a
+    # graph replay can do in a handful of launches where DDP's reducer copies each of the 73
+    # gradients into its buckets and back. AIMX_NATIVE_DDP=0 leaves every parameter to DDP.
+    _DDP_ANCHOR = "output_layer.bias"
+
+    @property
+    def _ddp_params_and_buffers_to_ignore(self):
+        user = list(self.__dict__.get("_aimx_ddp_user_ignore", ()))
+        if os.environ.get("AIMX_NATIVE_DDP", "1") == "0":
+            if user:
+                return user
+            raise AttributeError("_ddp_params_and_buffers_to_ignore")
+        if not self.__dict__.get("_aimx_ddp_native", False):
+            self.__dict__["_aimx_ddp_native"] = True
+            # DDP's constructor broadcasts the start state of what it syncs; this is ours (the same
+            # collective order on every rank: every rank is inside DDP's constructor)
+            from utils.distributed import broadcast_parameters
+            broadcast_parameters([p for n, p in self.named_parameters() if n != self._DDP_ANCHOR and n not in user])
+        return [n for n, _ in self.named_parameters() if n != self._DDP_ANCHOR] + \
+            [n for n in user if n not in dict(self.named_parameters())]
+
+    @_ddp_params_and_buffers_to_ignore.setter
+    def _ddp_params_and_buffers_to_ignore(self, names):
+        # DistributedDataParallel._set_params_and_buffers_to_ignore_for_model(module, names)
+        self.__dict__["_aimx_ddp_user_ignore"] = list(names)
+
+    def _aimx_native_sync(self):
+        """The gradient sync of the parameters DDP was told to ignore (None unless wrapped)."""
+        if not self.__dict__.get("_aimx_ddp_native", False):
+            return None
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
+        sync = self.__dict__.get("_aimx_sync")
+        params = [p for n, p in self.named_parameters() if n != self._DDP_ANCHOR and
+                  n not in self.__dict__.get("_aimx_ddp_user_ignore", ())]
+        key = tuple((id(p), p.data_ptr()) for p in params)
+        if sync is None or self.__dict__.get("_aimx_sync_key") != key:
+            if sync is not None:
+                sync.remove()
+            from utils.distributed import GradientSync
+            # always: the collectives run at world size 1 too, as DDP's do; auto_finish: the
+            # reference trainer never calls finish() (DDP finalises in an engine callback)
+            sync = GradientSync(params, unused=self.unused_parameters(), always=True, broadcast_params=False,
+                                auto_finish=True)
+            self.__dict__["_aimx_sync"] = sync
+            self.__dict__["_aimx_sync_key"] = key
+        return sync
 
     def unused_parameters(self):
         """Parameters the forward never touches: long_range_projection (gnn.py:146) and, with

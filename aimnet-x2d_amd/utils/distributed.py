@@ -189,7 +189,8 @@ class GradientSync:
     """
 
     def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True,
-                 first_bucket_mb: float = 1.0, unused=(), always: bool = False, broadcast_params: bool = True):
+                 first_bucket_mb: float = 1.0, unused=(), always: bool = False, broadcast_params: bool = True,
+                 auto_finish: bool = False):
         params = list(params)
         unused = list(unused)
         if broadcast_params:
@@ -237,9 +238,15 @@ class GradientSync:
             self.comm = _lib.Comm(process_group, dev)
             self._stream = torch.cuda.Stream(device=dev)
             self._events = [(torch.cuda.Event(), torch.cuda.Event()) for _ in self.buckets]
+        # auto_finish: the first bucket hook of a backward queues finish() as an autograd-engine
+        # callback (what DDP's reducer does with its finalize), so a loop that never calls finish()
+        # — the reference trainer under DistributedDataParallel — still gets averaged gradients
+        self.auto_finish = auto_finish
+        self._queued = False
         if self.overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self.hook_ids = {h.id for h in self._hooks}
         self._reset()
 
     @property
@@ -302,10 +309,51 @@ class GradientSync:
             self._handles[i] = dist.all_reduce(flat, group=self.group, async_op=True)
 
     def _on_grad(self, p):
+        if self.auto_finish and not self._queued:
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finish_queued)
         i = self._bucket_of[id(p)]
         self._pending[i] -= 1
         if self._pending[i] == 0 and self._handles[i] is None:
             self._launch(i)
+
+    def _finish_queued(self):
+        self._queued = False
+        self.finish()
+
+    def reduce_tensors(self, grads):
+        """Average the gradients `grads` ({id(param): tensor}, this sync's parameters) across the
+        ranks in place, bucket by bucket on the current stream (pack, one all-reduce, unpack): the
+        gradients a graph replay produced without running the parameters' accumulators
+        (aimx.autograph). A parameter missing from `grads` counts as zeros."""
+        if not self.active:
+            return
+        for i, bucket in enumerate(self.buckets):
+            flat = self._flat[i]
+            if flat is None or flat.device != bucket[0].device:
+                flat = torch.empty(sum(p.numel() for p in bucket), dtype=bucket[0].dtype, device=bucket[0].device)
+                self._flat[i] = flat
+            pairs, back, off = [], [], 0
+            for p in bucket:
+                n = p.numel()
+                g = grads.get(id(p))
+                pairs.append((g.reshape(-1) if g is not None else None, flat[off:off + n]))
+                if g is not None:
+                    back.append((flat[off:off + n], g.reshape(-1)))
+                off += n
+            if self.comm is not None:
+                from aimx import _lib
+                _lib.multi_copy(pairs, flat.device)
+                self.comm.all_reduce(flat, average=True, stream=torch.cuda.current_stream(flat.device))
+                if back:
+                    _lib.multi_copy(back, flat.device)
+            else:
+                torch.cat([g if g is not None else torch.zeros_like(d) for g, d in pairs], out=flat)
+                dist.all_reduce(flat, group=self.group)
+                if self.world > 1:
+                    flat.div_(self.world)
+                if back:
+                    torch._foreach_copy_([d for _, d in back], [s_ for s_, _ in back])
 
     def finish(self):
         """Complete every bucket's all-reduce and write averaged gradients back into .grad."""

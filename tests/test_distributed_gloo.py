@@ -195,3 +195,34 @@ def test_broadcast_parameters_subgroup_source():
     out = _run("_subgroup_broadcast", world=3)
     assert out[0] == [0.0] * 4
     assert out[1] == [1.0] * 4 and out[2] == [1.0] * 4
+
+
+def _ddp_wrap_native(rank, world):
+    """The reference's wrap, unchanged (runner.py:703-707), around the GNN on CPU (construction only:
+    the forward needs the GPU): DDP reads GNN._ddp_params_and_buffers_to_ignore, keeps the anchor
+    parameter alone in its reducer, and the model broadcasts its own start state."""
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from models import GNN
+    from utils.distributed import replica_checksums
+    torch.manual_seed(100 + rank)  # different start states on the two ranks
+    m = GNN({"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}, 64, 1)
+    before = replica_checksums(m.parameters())[0]
+    ddp = DDP(m, find_unused_parameters=True)
+    kept = [n for n, _ in m.named_parameters() if n not in ddp.parameters_to_ignore]
+    after = replica_checksums(m.parameters())[0]
+    native = m.__dict__.get("_aimx_ddp_native", False)
+    os.environ["AIMX_NATIVE_DDP"] = "0"
+    m2 = GNN({"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}, 64, 1)
+    ddp2 = DDP(m2, find_unused_parameters=True)
+    plain_ignored = len(ddp2.parameters_to_ignore)
+    del os.environ["AIMX_NATIVE_DDP"]
+    return before, after, kept, native, plain_ignored, len(list(m.named_parameters()))
+
+
+def test_ddp_wrap_keeps_one_parameter_and_syncs_start_state():
+    out = _run("_ddp_wrap_native")
+    for r in (0, 1):
+        before, after, kept, native, plain_ignored, n = out[r]
+        assert not before and after  # rank 0's parameters everywhere after the wrap
+        assert kept == ["output_layer.bias"] and native and n == 73
+        assert plain_ignored == 0  # AIMX_NATIVE_DDP=0: DDP keeps every parameter

@@ -327,20 +327,25 @@ def test_rccl_capture_failure_falls_back_to_split():
     assert out["identical"] and out["ar_us"] > 0, out
 
 
-def _ddp_wrapped(rank, replay):
+def _ddp_wrapped(rank, replay, native=True):
     """The reference's own data-parallel wrapping, unchanged (runner.py:703-707):
     DistributedDataParallel(GNN, find_unused_parameters=True) over this GNN, two iterations of the
     unchanged loop (zero_grad(set_to_none) -> forward -> L1 -> backward). replay: the default
-    drop-in — the autograph replays the bucket's graphs and hands the gradients out through
-    autograd, so DDP's reducer averages them; else every operator eagerly."""
+    drop-in — the autograph replays the bucket's graphs; else every operator eagerly. native
+    (default): DDP keeps only GNN._DDP_ANCHOR and the model's own GradientSync averages the rest
+    (after the replay, or from its bucket hooks eagerly); AIMX_NATIVE_DDP=0: DDP's reducer takes
+    every gradient (the replay hands them out through autograd)."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     from aimx import autograph
     from models import L1Loss
+    if not native:
+        os.environ["AIMX_NATIVE_DDP"] = "0"
     b = _qm9_batch(np.arange(rank * B_HALF, (rank + 1) * B_HALF))
-    m = _model()
+    m = _model(seed=rank)  # different start states: the wrap must synchronise them
     autograph.enable(m, replay)
     assert autograph.wanted(m, b.model_args()) == replay
     ddp = DDP(m, device_ids=[0], find_unused_parameters=True)
+    assert len(ddp.parameters_to_ignore) == (72 if native else 0)
     for _ in range(2):  # the second iteration: DDP found its reduction finished, buckets replayed again
         for p in m.parameters():
             p.grad = None
@@ -359,20 +364,24 @@ def ddp_wrapped_eager(rank, world):
     return _ddp_wrapped(rank, False)
 
 
-@pytest.mark.parametrize("fn", ["ddp_wrapped", "ddp_wrapped_eager"])
+def ddp_wrapped_plain(rank, world):
+    return _ddp_wrapped(rank, True, native=False)
+
+
+@pytest.mark.parametrize("fn", ["ddp_wrapped", "ddp_wrapped_eager", "ddp_wrapped_plain"])
 def test_ddp_wrapped_drop_in_equals_full_batch(fn):
     """INTEGRATION.md's claim: the reference trainer's DDP wrapping still works on this GNN —
     with the autograph's graph replay (default) and eagerly — and two ranks' averaged gradients
     equal one process's full-batch gradients (1e-5 norm-relative)."""
     from models import L1Loss
     out = _run(fn)
-    m = _model()
+    m = _model(seed=0)  # rank 0's start state, which the wrap broadcast
     b = _qm9_batch(np.arange(2 * B_HALF))
     o, _, _ = m(*b.model_args())
     L1Loss()(o, b.targets).backward()
     full = _grads(m)
     for r in range(2):
-        assert out[r]["buckets"] == (1 if fn == "ddp_wrapped" else 0), out[r]["buckets"]
+        assert out[r]["buckets"] == (0 if fn == "ddp_wrapped_eager" else 1), out[r]["buckets"]
         assert out[r]["unused_grad_none"]
         got = out[r]["grads"]
         assert set(got) == set(full), r
