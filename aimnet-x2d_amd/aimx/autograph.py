@@ -109,23 +109,56 @@ def _through_autograd(model):
     return _dist_initialized() or _state(model).grad_hooked(model, sync.hook_ids if sync is not None else ())
 
 
+# Module-structure generation: bumped whenever a parameter or a submodule is registered anywhere
+# (nn.Module.__setattr__ / register_parameter / load_state_dict(assign=True) / a swapped submodule)
+# and by GNN._apply (.to(), .cuda(): parameters in new storage). The per-step checks below read a
+# cached parameter / module list while it is unchanged instead of walking the module tree (the walks
+# cost ~0.4 ms of host time per step — more than a c2 step's replay).
+_GEN = [0]
+
+
+def _bump(*_):
+    _GEN[0] += 1
+
+
+def bump_structure():
+    """Invalidate every model's cached parameter / module lists (GNN._apply calls it)."""
+    _bump()
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump)
+torch.nn.modules.module.register_module_module_registration_hook(_bump)
+
+
 class _State:
     def __init__(self):
         self.buckets = {}
         self.order = []
         self.anchor = None
+        self.gen = -1
+        self.params = self.modules = self.key = None
+
+    def structure(self, model):
+        """(parameters, submodules, parameter identity key), rebuilt only when _GEN moved."""
+        if self.gen != _GEN[0]:
+            self.params = list(model.parameters())
+            self.modules = [m for m in model.modules() if m is not model]
+            self.key = tuple((id(p), p.data_ptr()) for p in self.params)
+            self.gen = _GEN[0]
+        return self
 
     def forward_hooked(self, model):
         """Forward hooks on a submodule: a replay cannot fire them (the eager path runs instead)."""
-        return any(m._forward_hooks or m._forward_pre_hooks for m in model.modules() if m is not model)
+        return any(m._forward_hooks or m._forward_pre_hooks for m in self.structure(model).modules)
 
     def grad_hooked(self, model, ignore=()):
         """Gradient hooks on a parameter (other than the handles in `ignore`: the model's own
         gradient sync): the replay then hands its gradients out through autograd."""
-        def hooked(d):
-            return bool(d) and any(k not in ignore for k in d)
-        return any(hooked(getattr(p, "_post_accumulate_grad_hooks", None)) or hooked(getattr(p, "_backward_hooks", None))
-                   for p in model.parameters())
+        for p in self.structure(model).params:
+            for d in (p._post_accumulate_grad_hooks, p._backward_hooks):
+                if d and any(k not in ignore for k in d):
+                    return True
+        return False
 
 
 def _state(model):
@@ -150,7 +183,7 @@ def pad_mols_for(Np):
 def _param_key(model):
     """Identity and storage of the model's live parameters: a replaced Parameter object
     (load_state_dict(assign=True), a swapped submodule) or moved storage re-captures the bucket."""
-    return tuple((id(p), p.data_ptr()) for p in model.parameters())
+    return _state(model).structure(model).key
 
 
 def _amp_key():
@@ -177,7 +210,7 @@ class _Bucket:
             ptr(self.charges)
         a.Np, a.Ep, a.pad_mols = Np, Ep, self.pad_mols
         self.pad = a
-        self.params = [p for p in model.parameters()]
+        self.params = list(_state(model).structure(model).params)
         self.param_key = _param_key(model)
         self.gen = 0        # forward replays so far
         self.done = -1      # generation whose backward has run
@@ -427,9 +460,7 @@ def run(model, args):
     if st.anchor is None or st.anchor.device != dev:
         st.anchor = torch.zeros((), device=dev, requires_grad=True)
     native = model._aimx_native_sync() if hasattr(model, "_aimx_native_sync") else None
-    p_anchor = None
-    if native is not None:
-        p_anchor = dict(model.named_parameters()).get(getattr(model, "_DDP_ANCHOR", ""))
+    p_anchor = getattr(native, "anchor_param", None)
     if native is not None and p_anchor is not None and not st.grad_hooked(model, native.hook_ids):
         out = _ReplayDDP.apply(st.anchor, b, G, native, p_anchor)
     elif _through_autograd(model):

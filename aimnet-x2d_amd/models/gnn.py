@@ -95,6 +95,7 @@ class GNN(nn.Module):
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
         self._aimx_pack_ig()
+        autograph.bump_structure()  # parameters may now live in new storage
         return out
 
     def _create_embeddings(self, feature_sizes: Dict[str, int], embedding_dim: int):
@@ -382,19 +383,19 @@ class GNN(nn.Module):
         if not (dist.is_available() and dist.is_initialized()):
             return None
         sync = self.__dict__.get("_aimx_sync")
-        params = [p for n, p in self.named_parameters() if n != self._DDP_ANCHOR and
-                  n not in self.__dict__.get("_aimx_ddp_user_ignore", ())]
-        key = tuple((id(p), p.data_ptr()) for p in params)
-        if sync is None or self.__dict__.get("_aimx_sync_key") != key:
-            if sync is not None:
-                sync.remove()
+        if sync is None:
+            # built once: DDP itself holds the Parameter objects it wrapped, so a wrapped model's
+            # parameters are not replaced or moved afterwards (DDP would break first)
             from utils.distributed import GradientSync
+            named = dict(self.named_parameters())
+            params = [p for n, p in named.items() if n != self._DDP_ANCHOR and
+                      n not in self.__dict__.get("_aimx_ddp_user_ignore", ())]
             # always: the collectives run at world size 1 too, as DDP's do; auto_finish: the
             # reference trainer never calls finish() (DDP finalises in an engine callback)
             sync = GradientSync(params, unused=self.unused_parameters(), always=True, broadcast_params=False,
                                 auto_finish=True)
+            sync.anchor_param = named.get(self._DDP_ANCHOR)
             self.__dict__["_aimx_sync"] = sync
-            self.__dict__["_aimx_sync_key"] = key
         return sync
 
     def unused_parameters(self):
