@@ -95,16 +95,29 @@ def segment_softmax(scores, batch, num_graphs):
     return e / s.gather(1, idx)
 
 
-def attention_pool(p, pre, x, batch, num_heads, num_graphs):
-    """pooling.py:122-172 (MultiHeadAttentionPoolingLayer.forward), dropout p=0."""
+def attention_pool(p, pre, x, batch, num_heads, num_graphs, capture=None):
+    """pooling.py:122-172 (MultiHeadAttentionPoolingLayer.forward), dropout p=0. `capture` (dict)
+    receives the scores [H, N] (their .grad is retained) and tau: temperature_scale() below."""
     tau = p[pre + "temperature"]
     scores = torch.stack([linear(p, f"{pre}attention_weights.{i}", x).squeeze(-1) / tau
                           for i in range(num_heads)], 0)
+    if capture is not None and scores.requires_grad:
+        scores.retain_grad()
+        capture["pool_scores"], capture["pool_tau"] = scores, tau
     a = segment_softmax(scores, batch, num_graphs)
     weighted = x.unsqueeze(0).expand(num_heads, -1, -1) * a.unsqueeze(-1)
     idx = batch.view(1, -1, 1).expand_as(weighted)
     pooled = torch.zeros(num_heads, num_graphs, x.shape[1], dtype=x.dtype, device=x.device).scatter_add_(1, idx, weighted)
     return pooled.mean(dim=0), a
+
+
+def temperature_scale(capture):
+    """After backward: sum_hj |dL/ds_hj * s_hj| / |tau| — the magnitude of the terms whose signed sum
+    is dL/dtau (s = x.W_h / tau + ..., ds/dtau = -s / tau). The temperature gradient sums H*N terms of
+    both signs (softmax shift invariance makes them cancel to a few % of that magnitude), so its fp32
+    rounding is judged against this scale (tests/conftest.py _scale_for)."""
+    s = capture["pool_scores"]
+    return float((s.grad * s).detach().abs().sum() / capture["pool_tau"].detach().abs())
 
 
 def simple_pool(kind, x, batch, num_graphs):
@@ -241,7 +254,7 @@ def gnn_forward(p, cfg, atom_features, edges, batch, total_charges, training=Fal
         capture["pre_pool"] = x
     g = total_charges.shape[0]
     if cfg["pooling_type"] == "attention":
-        pooled, attn = attention_pool(p, "pooling.", x, batch, cfg["attention_num_heads"], g)
+        pooled, attn = attention_pool(p, "pooling.", x, batch, cfg["attention_num_heads"], g, capture=capture)
     else:
         pooled, attn = simple_pool(cfg["pooling_type"], x, batch, g), None
     x = linear(p, "post_pooling_projection", pooled)

@@ -39,7 +39,11 @@ def golden():
 
 def _scale_for(key, ref64):
     """Gradients whose exact value is 0 (softmax shift invariance: d/db_h of the attention bias,
-    pooling.py:136-145) are pure rounding noise; judge them against their sibling weight's scale."""
+    pooling.py:136-145) are pure rounding noise; judge them against their sibling weight's scale.
+    A gradient the fp64 oracle run gives a scale for (`"scale:" + key`: the attention temperature's,
+    oracle.model.temperature_scale — a signed sum of H*N terms) is judged against that scale."""
+    if "scale:" + key in ref64:
+        return float(ref64["scale:" + key])
     if ".attention_weights." in key and key.startswith("grad.") and key.endswith(".bias"):
         w = key[:-len("bias")] + "weight"
         if w in ref64:
