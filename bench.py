@@ -480,29 +480,24 @@ def cpu_info():
     return model, os.cpu_count(), affinity
 
 
-def cpu_baseline(cfg, seconds=10.0, max_steps=40, one_thread_seconds=6.0, all_cores_seconds=6.0):
+def cpu_baseline(cfg, seconds=10.0, max_steps=40, one_thread_seconds=6.0):
     """Oracle CPU restatement of the reference train step (fwd+bwd+clip+Adam, dropout on): on the
-    box's CPU share (min(16, cpu_count) threads, `value`), on torch.set_num_threads(os.cpu_count())
-    and on 1 thread (BASELINE.md CPU-baseline plan item 3); the port/reference ratio comes from
-    profiles/port_vs_reference.json (the reference itself only runs in the development container)."""
+    box's CPU share (min(16, cpu_count) threads: the box's cgroup quota is 16 CPUs' worth of time,
+    `value`) and on 1 thread (BASELINE.md CPU-baseline plan item 3); the port/reference ratio comes
+    from profiles/port_vs_reference.json (the reference itself only runs in the development
+    container). (Round 4's extra figure on os.cpu_count() threads oversubscribed that quota 16x and
+    measured the oversubscription, not the CPU; it is gone.)"""
     threads = min(16, os.cpu_count() or 1)
     res = _cpu_rate(cfg, threads, seconds, max_steps)
     res1 = _cpu_rate(cfg, 1, one_thread_seconds, 8)
     model, count, affinity = cpu_info()
-    if (count or 1) != threads:
-        resa = _cpu_rate(cfg, count or 1, all_cores_seconds, 10)
-        quota = None
-        try:  # cgroup v2 CPU quota: "max period" or "<quota> <period>" (CPUs' worth of time)
-            q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-            quota = None if q == "max" else round(int(q) / int(per), 2)
-        except (OSError, ValueError):
-            pass
-        res.update({"value_all_cores": resa["value"], "sample_all_cores": resa["sample"],
-                    "cgroup_cpu_quota": quota,
-                    "note_all_cores": f"torch.set_num_threads(os.cpu_count() = {count}) on a box process whose "
-                                      f"CPU affinity holds {affinity} CPUs"
-                                      + (f" but whose cgroup quota is {quota} CPUs' worth of time: the threads "
-                                         "oversubscribe it" if quota is not None and quota < (count or 1) else "")})
+    quota = None
+    try:  # cgroup v2 CPU quota: "max period" or "<quota> <period>" (CPUs' worth of time)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    res["cgroup_cpu_quota"] = quota
     res.update({"value_1thread": res1["value"], "sample_1thread": res1["sample"], "cpu_model": model,
                 "cpu_count": count, "cpu_affinity": affinity})
     pvr = os.path.join(ROOT, "profiles", "port_vs_reference.json")
