@@ -504,14 +504,27 @@ class Comm:
             self.handle = None
 
 
+def copy_items(pairs):
+    """The aimx_multi_copy item array of `pairs` (see multi_copy), built once for reuse: the caller
+    keeps every tensor alive while the array is in use."""
+    arr = (CopyItem * max(1, len(pairs)))()
+    for i, (src, dst) in enumerate(pairs):
+        arr[i].src = None if src is None else src.data_ptr()
+        arr[i].dst = dst.data_ptr()
+        arr[i].n = dst.numel()
+    return arr, len(pairs)
+
+
+def multi_copy_items(items, device):
+    """One aimx_multi_copy launch over a prebuilt copy_items() array, on the current stream."""
+    arr, n = items
+    if n:
+        check(load().aimx_multi_copy(arr, n, stream_ptr(device)), "multi_copy")
+
+
 def multi_copy(pairs, device):
     """pairs: [(src tensor or None, dst tensor)] of fp32 contiguous tensors: dst <- src (None: 0),
     one launch (aimx_multi_copy) on the current stream."""
     if not pairs:
         return
-    arr = (CopyItem * len(pairs))()
-    for i, (src, dst) in enumerate(pairs):
-        arr[i].src = None if src is None else src.data_ptr()
-        arr[i].dst = dst.data_ptr()
-        arr[i].n = dst.numel()
-    check(load().aimx_multi_copy(arr, len(pairs), stream_ptr(device)), "multi_copy")
+    multi_copy_items(copy_items(pairs), device)

@@ -336,6 +336,9 @@ class _Replay(torch.autograd.Function):
         return None, None, None
 
 
+_RT_KEYS = __import__("itertools").count()
+
+
 class _ReplayDDP(torch.autograd.Function):
     """_Replay under DistributedDataParallel with the model's own gradient sync
     (GNN._ddp_params_and_buffers_to_ignore): the anchor parameter, the one DDP's reducer keeps, gets
@@ -362,7 +365,11 @@ class _ReplayDDP(torch.autograd.Function):
                 keep[id(p)] = sg.clone()
         b.g_bwd.replay()
         b.done = ctx.gen
-        ctx.sync.reduce_tensors({id(p): sg for p, sg in zip(b.params, b.grads) if sg is not None and p is not pa})
+        rt = b.__dict__.get("_rt_grads")
+        if rt is None:  # the bucket's static gradients: the same tensors every replay
+            rt = b._rt_grads = {id(p): sg for p, sg in zip(b.params, b.grads) if sg is not None and p is not pa}
+            b._rt_key = next(_RT_KEYS)  # never reused (an id() could be, after the bucket is gone)
+        ctx.sync.reduce_tensors(rt, key=b._rt_key)
         ga = None
         for p, sg in zip(b.params, b.grads):
             if sg is None:

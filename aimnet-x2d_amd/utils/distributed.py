@@ -321,12 +321,44 @@ class GradientSync:
         self._queued = False
         self.finish()
 
-    def reduce_tensors(self, grads):
+    def reduce_tensors(self, grads, key=None):
         """Average the gradients `grads` ({id(param): tensor}, this sync's parameters) across the
         ranks in place, bucket by bucket on the current stream (pack, one all-reduce, unpack): the
         gradients a graph replay produced without running the parameters' accumulators
-        (aimx.autograph). A parameter missing from `grads` counts as zeros."""
+        (aimx.autograph). A parameter missing from `grads` counts as zeros. `key` (hashable): the
+        same tensors come back every call under it (a replay's static gradients), so the pack /
+        unpack launch descriptors are built once (and `grads` holds them alive meanwhile)."""
         if not self.active:
+            return
+        if key is not None and self.comm is not None:
+            cache = self.__dict__.setdefault("_rt_cache", {})
+            plan = cache.get(key)
+            if plan is None:
+                from aimx import _lib
+                plan = []
+                for i, bucket in enumerate(self.buckets):
+                    flat = self._flat[i]
+                    if flat is None or flat.device != bucket[0].device:
+                        flat = torch.empty(sum(p.numel() for p in bucket), dtype=bucket[0].dtype,
+                                           device=bucket[0].device)
+                        self._flat[i] = flat
+                    pairs, back, off = [], [], 0
+                    for p in bucket:
+                        n = p.numel()
+                        g = grads.get(id(p))
+                        pairs.append((g.reshape(-1) if g is not None else None, flat[off:off + n]))
+                        if g is not None:
+                            back.append((flat[off:off + n], g.reshape(-1)))
+                        off += n
+                    plan.append((flat, _lib.copy_items(pairs), _lib.copy_items(back), pairs, back))
+                if len(cache) > 8:
+                    cache.clear()
+                cache[key] = plan
+            from aimx import _lib
+            for flat, pack, unpack, _, _ in plan:
+                _lib.multi_copy_items(pack, flat.device)
+                self.comm.all_reduce(flat, average=True, stream=torch.cuda.current_stream(flat.device))
+                _lib.multi_copy_items(unpack, flat.device)
             return
         for i, bucket in enumerate(self.buckets):
             flat = self._flat[i]

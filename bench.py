@@ -68,7 +68,9 @@ def make_collated(cfg, n_batches, seed):
 
 
 PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from the loss)
-LAYOUT_QUANTUM = 128  # atoms: one-GPU static batches are padded to the next multiple (one graph each)
+# atoms: one-GPU static batches are padded to the next multiple (one graph each); AIMX_BENCH_QUANTUM
+# overrides (A/B)
+LAYOUT_QUANTUM = int(os.environ.get("AIMX_BENCH_QUANTUM", "128"))
 
 
 def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):

@@ -1,7 +1,15 @@
 #!/bin/bash
 # round-5 working call (overwritten per call)
 export PYTHONDONTWRITEBYTECODE=1
-T="python3 -u -m pytest -x -v --timeout 200 --timeout-method thread"
+B="python3 bench.py --no-cpu-baseline --no-roofline --steps 40 --warmup 8"
 tools/gpu_steps.sh \
- "?600 r5e/ddp.log $T tests/test_gpu_ddp.py tests/test_gpu_autograph.py tests/test_gpu_stream.py tests/test_gpu_parity.py -k 'ddp or autograph or stream or full_size'" \
- "200 r5e/bench_ddp1.log python3 bench.py --ddp-world1 --no-cpu-baseline --no-roofline"
+ "200 r5f/ddp1.log python3 bench.py --ddp-world1 --no-cpu-baseline --no-roofline" \
+ "200 r5f/c2_q128.log env AIMX_BENCH_QUANTUM=128 $B" \
+ "200 r5f/c2_q64.log env AIMX_BENCH_QUANTUM=64 $B" \
+ "200 r5f/c2_q32.log env AIMX_BENCH_QUANTUM=32 $B" \
+ "200 r5f/c5_q128.log env AIMX_BENCH_QUANTUM=128 $B --config c5" \
+ "200 r5f/c5_q64.log env AIMX_BENCH_QUANTUM=64 $B --config c5" \
+ "200 r5f/c5_q32.log env AIMX_BENCH_QUANTUM=32 $B --config c5" \
+ "200 r5f/c4_q128.log env AIMX_BENCH_QUANTUM=128 $B --config c4" \
+ "200 r5f/c4_q64.log env AIMX_BENCH_QUANTUM=64 $B --config c4" \
+ "200 r5f/c4_q32.log env AIMX_BENCH_QUANTUM=32 $B --config c4"
