@@ -39,8 +39,8 @@ CONFIGS = {
     "c1": dict(source="qm9", hidden=128, hops=3, batch=32, tasks=1, pc=False),
     "c2": dict(source="qm9", hidden=256, hops=3, batch=512, tasks=1, pc=False),
     "c3": dict(source="qm9", hidden=256, hops=4, batch=512, tasks=12, pc=True),
-    "c4": dict(source="synth40", hidden=512, hops=3, batch=512, tasks=1, pc=False),
-    "c5": dict(source="synth40", hidden=1024, hops=6, batch=256, tasks=1, pc=False),
+    "c4": dict(source="synth40", hidden=512, hops=3, batch=512, tasks=1, pc=False, quantum=32),
+    "c5": dict(source="synth40", hidden=1024, hops=6, batch=256, tasks=1, pc=False, quantum=32),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FS = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
@@ -68,9 +68,15 @@ def make_collated(cfg, n_batches, seed):
 
 
 PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from the loss)
-# atoms: one-GPU static batches are padded to the next multiple (one graph each); AIMX_BENCH_QUANTUM
-# overrides (A/B)
-LAYOUT_QUANTUM = int(os.environ.get("AIMX_BENCH_QUANTUM", "128"))
+# atoms: one-GPU static batches are padded to the next multiple (one graph each). c4 / c5 (device-
+# bound steps, no launch overhead for the graph to win back) use 32: every padded atom is paid in
+# full there (profiles/r05_quantum_ab.txt: c5 graphed 3.972 -> 3.952 ms, eager 3.965-3.975; c4
+# 2.600 -> 2.590); c2 keeps 128 (0.7249 vs 0.7324 ms with 32). AIMX_BENCH_QUANTUM overrides (A/B).
+LAYOUT_QUANTUM = 128
+
+
+def layout_quantum(cfg):
+    return int(os.environ.get("AIMX_BENCH_QUANTUM", cfg.get("quantum", LAYOUT_QUANTUM)))
 
 
 def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):
@@ -83,9 +89,11 @@ def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):
     if not pad:
         return [adata.DeviceBatch(c, device, targets=t, total_charges=q, csr_hops=cfg["hops"]) for c, t, q in cols]
 
+    q = layout_quantum(cfg)
+
     def bucket(c):
         n = c["batch"].shape[0]
-        return -(-(n + 2) // LAYOUT_QUANTUM) * LAYOUT_QUANTUM if buckets else 0
+        return -(-(n + 2) // q) * q if buckets else 0
     groups = {}
     for c, _, _ in cols:
         groups.setdefault(bucket(c), []).append(c)
@@ -940,7 +948,7 @@ def main():
                        "train step fwd+bwd+clip+Adam, dropout 0.05"
                        + (f", HIP-graph replay of padded static batches (+{pad_mols_used} padding molecules of"
                           " <= 64 atoms, excluded from the loss; "
-                          + (f"{graphed.layouts} captured layouts: {LAYOUT_QUANTUM}-atom buckets)" if sync is None
+                          + (f"{graphed.layouts} captured layouts: {layout_quantum(cfg)}-atom buckets)" if sync is None
                              else "one layout)") if args.graph else ", eager"),
                        "feed": ("resident pool of %d batches in HBM" % args.pool if feeder is None else
                                 "native C++ collate + pinned H2D per step (PCIe-inclusive; not the metric value)"
