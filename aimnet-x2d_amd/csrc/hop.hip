@@ -543,9 +543,14 @@ int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   // AIMX_HOP_ROWS=2 sends every width there (A/B)
   const HopEnv& E = hop_env();
   const int64_t rows_mode = E.rows_mode;
-  if ((vec < 4 && rows_mode == 1) || rows_mode == 2)
+  if ((vec < 4 && rows_mode == 1) || rows_mode == 2) {
+    if (row_seg && gather_regs_on() && launch_gather_regs(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out,
+                                                          out_ld, out_rpc, out_cs, add0, add0_ld, add1, add1_ld,
+                                                          row_seg, row_seg_stride, stream, skip_tail) == AIMX_OK)
+      return AIMX_OK;
     return launch_gather_rows(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
                               add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream, skip_tail);
+  }
   const int64_t upr_i = D / vec;
   // 32-bit thread indexing (rows * D / vec < 2^31) and int32 chunked row ids.
   if (rows * upr_i >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;

@@ -30,9 +30,21 @@ __device__ __forceinline__ int64_t row_off(uint32_t r, int64_t ld, const FastDiv
 }
 
 // The odd-width / unaligned-row hop (hop_rows.hip); same contract as aimx_segment_gather_sum.
+// windows = false: only the big tiles of the rows past the first output chunk (hop_regs.hip runs the
+// first chunk's rows).
 int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
                        int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
-                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream, int32_t skip_tail = 0);
+                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
+                       int32_t skip_tail = 0, bool windows = true);
+
+// The first output chunk's rows summed from the register file, molecule by molecule (hop_regs.hip);
+// needs row_seg. AIMX_HOP_REGS=0 turns it off (gather_regs_on).
+bool gather_regs_on();
+int launch_gather_regs(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
+                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
+                       int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
+                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
+                       int32_t skip_tail);
 
 }  // namespace aimx

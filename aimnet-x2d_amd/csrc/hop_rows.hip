@@ -575,7 +575,7 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
                        int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
                        int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
-                       int32_t skip_tail) {
+                       int32_t skip_tail, bool windows) {
   // 4-byte-aligned fp32 rows (the 16-byte fix-up works on float offsets)
   auto al4 = [](const void* p) { return ((uintptr_t)p & 3) == 0; };
   if (!al4(src) || !al4(out) || (add0 && !al4(add0)) || (add1 && !al4(add1))) return AIMX_EARG;
@@ -610,7 +610,7 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   const int64_t split = (out_rpc > 0 && out_rpc < rows) ? out_rpc : rows;
   const int64_t nwin = cdiv(split, win);
   const bool pass_split = passes > 1 && (split_env == 1 || (split_env == 2 && nwin < split_below));
-  const int64_t nsmall = nwin * (pass_split ? passes : 1);
+  const int64_t nsmall = windows ? nwin * (pass_split ? passes : 1) : 0;
   const int64_t big = std::max<int64_t>(cap, big_env);
   const int64_t nbig = cdiv(rows - split, big);
   RowsArgs a;

@@ -1,15 +1,10 @@
 #!/bin/bash
-# round-5 working call (overwritten per call)
+# round-5 working call (overwritten per call): register-file hop kernel, parity then speed
 export PYTHONDONTWRITEBYTECODE=1
-B="python3 bench.py --no-cpu-baseline --no-roofline --steps 40 --warmup 8"
+T="python3 -u -m pytest -x -v --timeout 120 --timeout-method thread"
+M="python3 tools/hop_cfg_micro.py --configs c4,c5"
 tools/gpu_steps.sh \
- "200 r5f/ddp1.log python3 bench.py --ddp-world1 --no-cpu-baseline --no-roofline" \
- "200 r5f/c2_q128.log env AIMX_BENCH_QUANTUM=128 $B" \
- "200 r5f/c2_q64.log env AIMX_BENCH_QUANTUM=64 $B" \
- "200 r5f/c2_q32.log env AIMX_BENCH_QUANTUM=32 $B" \
- "200 r5f/c5_q128.log env AIMX_BENCH_QUANTUM=128 $B --config c5" \
- "200 r5f/c5_q64.log env AIMX_BENCH_QUANTUM=64 $B --config c5" \
- "200 r5f/c5_q32.log env AIMX_BENCH_QUANTUM=32 $B --config c5" \
- "200 r5f/c4_q128.log env AIMX_BENCH_QUANTUM=128 $B --config c4" \
- "200 r5f/c4_q64.log env AIMX_BENCH_QUANTUM=64 $B --config c4" \
- "200 r5f/c4_q32.log env AIMX_BENCH_QUANTUM=32 $B --config c4"
+ "300 r5h/hop_tests.log $T tests/test_gpu_hop_rows.py" \
+ "200 r5h/regs.log $M" \
+ "200 r5h/rows.log env AIMX_HOP_REGS=0 $M" \
+ "400 r5h/model.log $T tests/test_gpu_parity.py -k 'full_size or c4s or c5s or stereo'"
