@@ -86,6 +86,16 @@ if len(sys.argv) > 1 and sys.argv[1] == "node":
             run(M, w, w, "NN", f"node bwd D={D} w={w}")
     sys.exit(0)
 
+if len(sys.argv) > 1 and sys.argv[1] == "head":
+    # c5's post-pool chain (F = 1024, 256 molecules + up to 2 padding): forward, input gradient,
+    # weight gradient, at the planner's choice and with forced splits
+    for M in (256, 258):
+        for sp in (0, 1, 2, 4, 8):
+            run(M, 1024, 1024, "NT", f"c5 head fwd splits={sp}", splits=sp)
+            run(M, 1024, 1024, "NN", f"c5 head dX splits={sp}", splits=sp, torch_ref=sp == 0)
+        run(1024, 1024, M, "TN", "c5 head dW")
+    sys.exit(0)
+
 if len(sys.argv) > 1 and sys.argv[1] == "splits":
     for M, N, K, lab in [(76, 77, 9170, "c2 dW mlp"), (152, 305, 9170, "c2 dW_ig"), (256, 257, 9170, "c2 concat dW")]:
         for sp in (0, 4, 8, 12, 16, 24, 32, 48, 64):
