@@ -769,6 +769,195 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   }
 }
 
+// ---- Skinny GEMM: few rows, wide and deep (the post-pool chain's F x F layers at F = 1024) -------
+// Y[M, N] = A[M, K] B with M <= 640 (molecules of one batch) and N, K >= 256 (c5's 258 x 1024 x 1024
+// forward and input-gradient GEMMs, gnn.py:252-258). On k_gemm these ran as 640 split-K blocks
+// with one 32-deep slice in flight each: every block paid ~7 dependent L2/MALL round trips and the
+// launch took 17-20 us for 0.54 GFLOP (16 % MFMA, profiles/r04_c5_step_seq.txt). Here a block owns
+// a 64 x 64 tile and a K range of ~256 (S splits chosen so the full row blocks fill the chip once),
+// and its whole K range is requested up front: LDS-DMA loads (buffer_load ... lds, no registers)
+// into a two-stage ring of 64-deep stages, so while stage s is multiplied stage s + 1 is already
+// landing and stage s + 2 is issued as soon as stage s is consumed (counted vmcnt, raw s_barrier:
+// no vmcnt(0) drain in the loop). One 256-B row per 64 k: the stage images are XOR-swizzled on
+// the SOURCE address (an LDS-DMA writes lane-linear):
+//  * k-contiguous operands ([m][k] or [n][k]): float4 column c of row r at position c ^ (r & 15),
+//    read as k-permuted 16-byte fragments (lane (l & 15, g = l >> 4) holds k = 16s + 4g + j of its
+//    row, MFMA j uses component j) — a 16-lane group covers all 16 positions: conflict-free;
+//  * n-contiguous B ([k][n], the input gradient's W): float4 column c of k row r at position
+//    c ^ (4 * ((r >> 2) & 3)), read as dwords (k rows 16s + 4g + j) — the 4 k-groups of a read land
+//    on disjoint bank quarters.
+// Wave w multiplies rows 16w..16w+15 of the tile by its 64 columns (4 accumulators); waves whose
+// rows are all past M (the last row block of a padded batch) skip the MFMAs. Blocks of full row
+// blocks are numbered first, so the light last row block lands on the CUs' second slots. Split-K
+// slabs are summed by the last-arriving block in slice order (sc1 hand-off as in k_gemm):
+// deterministic. Epilogue: k_gemm's (bias, residuals, activation, pre-activation, dropout).
+constexpr int kSkB = 64;                 // tile edge
+constexpr int kSkKC = 64;                // k per stage
+constexpr int kSkImg = kSkB * kSkKC;     // floats per operand image
+constexpr int kSkStage = 2 * kSkImg;     // floats per stage (A image, then B image)
+
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, float* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <bool BKC>
+__global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk, int nm_full, int nb,
+                                                uint32_t a_bytes, uint32_t b_bytes) {
+  // ONE shared array (a second __shared__ object can make hipcc drain the DMA before each read)
+  __shared__ __attribute__((aligned(16))) float smem[2 * kSkStage];  // 64 KiB: two blocks per CU
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = (int)a.M, N = (int)a.N, K = (int)a.K;
+  const int S = (int)gridDim.y;
+  int b = (int)blockIdx.x, mb, nbk;
+  if (b < nm_full * nb) {
+    mb = b % nm_full;
+    nbk = b / nm_full;
+  } else {
+    b -= nm_full * nb;
+    mb = nm_full;
+    nbk = b;
+  }
+  const int z = (int)blockIdx.y;
+  const int m0 = mb * kSkB, n0 = nbk * kSkB;
+  const int kb = z * kchunk, ke = min(K, kb + kchunk);
+  const int nst = ke > kb ? (ke - kb + kSkKC - 1) / kSkKC : 0;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.B, b_bytes);
+  const uint32_t sam = (uint32_t)a.sam, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
+  const int sub = lane >> 4, pos = lane & 15;
+
+  // stage st (k0 = kb + 64 st) into buffer buf: 8 LDS-DMA instructions per wave (4 A + 4 B, 1 KiB
+  // each = 4 image rows); invalid float4s point past the extent and read 0
+  auto fill = [&](int st, int buf) {
+    float* sa = smem + buf * kSkStage;
+    float* sb = sa + kSkImg;
+    const int k0 = kb + st * kSkKC;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = w * 4 + u, row = 4 * t + sub;
+      const int ca = pos ^ (row & 15);
+      const int ka = k0 + 4 * ca;
+      const uint32_t oa = (m0 + row < M && ka < ke) ? 4u * ((uint32_t)(m0 + row) * sam + (uint32_t)ka) : kBufDrop;
+      lds_dma16(ra, sa + t * 256, oa);
+      uint32_t ob;
+      if constexpr (BKC) {
+        ob = (n0 + row < N && ka < ke) ? 4u * ((uint32_t)(n0 + row) * sbn + (uint32_t)ka) : kBufDrop;
+      } else {
+        const int cb = pos ^ (((row >> 2) & 3) << 2);
+        const int kr = k0 + row, n = n0 + 4 * cb;
+        ob = (kr < ke && n < N) ? 4u * ((uint32_t)kr * sbk + (uint32_t)n) : kBufDrop;
+      }
+      lds_dma16(rb, sb + t * 256, ob);
+    }
+  };
+
+  floatx4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const bool active = m0 + 16 * w < M;
+  const int lm = lane & 15, g = lane >> 4;
+  auto compute = [&](int buf) {
+    const float* sa = smem + buf * kSkStage;
+    const float* sb = sa + kSkImg;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const floatx4 av = *reinterpret_cast<const floatx4*>(sa + (16 * w + lm) * kSkKC + (((4 * s + g) ^ lm) << 2));
+      floatx4 bv[4];
+#pragma unroll
+      for (int nf = 0; nf < 4; ++nf) {
+        if constexpr (BKC) {
+          bv[nf] = *reinterpret_cast<const floatx4*>(sb + (16 * nf + lm) * kSkKC + (((4 * s + g) ^ lm) << 2));
+        } else {
+          const int col = ((((4 * nf + (lm >> 2)) ^ (g << 2))) << 2) + (lm & 3);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) bv[nf][j] = sb[(16 * s + 4 * g + j) * kSkB + col];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[nf][j], acc[nf], 0, 0, 0);
+    }
+  };
+
+  if (nst > 0) fill(0, 0);
+  if (nst > 1) fill(1, 1);
+  for (int st = 0; st < nst; ++st) {
+    // this stage's 8 DMAs retired (the next stage's 8 may stay in flight), then every wave's
+    if (st + 1 < nst)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // (s_barrier alone does not order memory for the compiler)
+    if (active) compute(st & 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every read of the buffer done before it is refilled
+    asm volatile("" ::: "memory");
+    if (st + 2 < nst) fill(st + 2, st & 1);
+  }
+
+  if (S > 1) {
+    const int tile = mb * nb + nbk;
+    const int64_t ntiles = (int64_t)(nm_full + (M % kSkB ? 1 : 0)) * nb;
+    constexpr int TILE = kSkB * kSkB;
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(a.workspace, (uint32_t)(4 * (int64_t)S * ntiles * TILE));
+    const uint32_t slab0 = (uint32_t)(4 * (((int64_t)z * ntiles + tile) * TILE));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store_sc1(rws, slab0 + 16u * (uint32_t)(j * 256 + tid), acc[j]);
+    int* flag = reinterpret_cast<int*>(smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == S - 1);
+      if (last) __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    const uint32_t zstride = (uint32_t)(4 * ntiles * TILE);
+    const uint32_t tile0 = (uint32_t)(4 * (int64_t)tile * TILE);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t off = tile0 + 16u * (uint32_t)(j * 256 + tid);
+      floatx4 s = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int z0 = 0; z0 < S; z0 += 8) {
+        floatx4 t[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t[q] = load_sc1(rws, (uint32_t)min(z0 + q, S - 1) * zstride + off);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (z0 + q < S) s += t[q];
+      }
+      acc[j] = s;
+    }
+  }
+
+  // C tile through LDS (row-major, stride 65), then k_gemm's epilogue in chunks of 8 per thread
+  constexpr int CS = kSkB + 1;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) smem[(16 * w + 4 * g + r) * CS + 16 * j + lm] = acc[j][r];
+  __syncthreads();
+#pragma unroll
+  for (int q0 = 0; q0 < 16; q0 += 8) {
+    int qm[8], qn[8];
+    float ev[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + (q0 + u) * 256;
+      qm[u] = m0 + e / kSkB;
+      qn[u] = n0 + e % kSkB;
+      ev[u] = smem[(e / kSkB) * CS + e % kSkB];
+    }
+    epilogue_n<8>(a, qm, qn, ev);
+  }
+}
+
 // ---- Weight-gradient GEMM (K = atoms, small M x N): MFMA fragments straight from L2 ----------
 // dW = dY^T X: A = dY^T is m-contiguous (sam == 1), B = X is n-contiguous (sbn == 1), K is the atom
 // count. In that layout the 16x16x4 MFMA fragments ARE coalesced global rows (lane l reads A[k0 +
@@ -1356,7 +1545,26 @@ struct Plan {
   int bm, bn, splits;
   int64_t kchunk;
   bool wgrad;
+  bool skinny;  // k_skinny (64 x 64 tiles, deep LDS-DMA stages)
 };
+
+// k_skinny applies to fp32 products with few rows and a wide, deep right operand whose tiled grid
+// is short of the chip: A k-contiguous, B k- or n-contiguous, 16-byte rows, counters for the
+// in-launch split-K reduce. AIMX_SKINNY=0 turns it off (A/B).
+bool skinny_ok(const AimxGemmArgs& a) {
+  static const bool off = [] {
+    const char* e = getenv("AIMX_SKINNY");
+    return e && atoi(e) == 0;
+  }();
+  if (off || a.precision != AIMX_PREC_FP32 || a.ones_col || a.zc_rowptr) return false;
+  if (a.M < 1 || a.M > 640 || a.N < 256 || a.K < 256) return false;
+  if (a.sak != 1 || !(a.sbk == 1 || a.sbn == 1)) return false;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al(a.A) || !al(a.B) || a.K % 4 || a.sam % 4) return false;
+  if (a.sbk == 1 ? (a.sbn % 4 != 0) : (a.sbk % 4 != 0 || a.N % 4 != 0)) return false;
+  const int64_t tiles = cdiv(a.M, kSkB) * cdiv(a.N, kSkB);
+  return tiles < 256 && a.counters && tiles <= a.n_counters;
+}
 
 // Weight-gradient layout (A m-contiguous, B n-contiguous) with a long K: k_wgrad.
 inline bool is_wgrad(const AimxGemmArgs& a) {
@@ -1366,9 +1574,21 @@ inline bool is_wgrad(const AimxGemmArgs& a) {
   return !off && a.sam == 1 && a.sbn == 1 && a.sak != 1 && a.K >= 512;
 }
 
-Plan plan_gemm(const AimxGemmArgs& a) {
+Plan plan_gemm(const AimxGemmArgs& a, bool allow_skinny = true) {
   Plan p;
   p.wgrad = false;
+  p.skinny = false;
+  if (allow_skinny && !is_wgrad(a) && skinny_ok(a)) {
+    // splits so the full row blocks' tiles fill the chip about once, >= 128 of K per split
+    p.skinny = true;
+    p.bm = p.bn = kSkB;
+    const int64_t full = std::max<int64_t>(1, a.M / kSkB) * cdiv(a.N, kSkB);
+    int64_t sp = a.splits > 0 ? a.splits : std::max<int64_t>(1, (256 + full / 2) / full);
+    sp = std::max<int64_t>(1, std::min<int64_t>({sp, 64, a.K / 128}));
+    p.kchunk = cdiv(cdiv(a.K, sp), kSkKC) * kSkKC;
+    p.splits = (int)std::max<int64_t>(1, cdiv(a.K, p.kchunk));
+    return p;
+  }
   if (is_wgrad(a)) {
     // ~1536 waves in flight chip-wide, every wave keeping >= 2 load groups (2 x 32 k) of work
     p.wgrad = true;
@@ -1663,6 +1883,20 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   const uint32_t a_bytes = (uint32_t)std::max<int64_t>(a_ext, 4);
   const uint32_t b_bytes = (uint32_t)std::max<int64_t>(b_ext, 4);
   Plan p = plan_gemm(a);
+  if (p.skinny) {
+    const size_t need = p.splits > 1 ? sizeof(float) * (size_t)p.splits * cdiv(a.M, kSkB) * cdiv(a.N, kSkB) * kSkB * kSkB : 0;
+    if (p.splits == 1 || (a.workspace && a.workspace_bytes >= need)) {
+      const int nb = (int)cdiv(a.N, kSkB), nm_full = (int)(a.M / kSkB);
+      const dim3 grid((unsigned)(cdiv(a.M, kSkB) * nb), (unsigned)p.splits);
+      if (a.sbk == 1)
+        hipLaunchKernelGGL(k_skinny<true>, grid, dim3(256), 0, s, a, (int)p.kchunk, nm_full, nb, a_bytes, b_bytes);
+      else
+        hipLaunchKernelGGL(k_skinny<false>, grid, dim3(256), 0, s, a, (int)p.kchunk, nm_full, nb, a_bytes, b_bytes);
+      AIMX_CHECK_LAUNCH();
+      return AIMX_OK;
+    }
+    p = plan_gemm(a, false);
+  }
   if (p.splits > 1 && (!a.workspace || a.workspace_bytes < sizeof(float) * tiled_workspace_floats(a))) {
     p.splits = 1;
     p.kchunk = std::max<int64_t>(cdiv(a.K, kBK) * kBK, kBK);

@@ -254,6 +254,30 @@ def test_gemm_layouts(M, N, K, layout):
     assert err < 2e-6, err
 
 
+@pytest.mark.parametrize("M,N,K,layout,splits", [
+    (258, 1024, 1024, "NT", 0), (258, 1024, 1024, "NN", 0), (256, 512, 1000, "NT", 0), (1, 256, 256, "NN", 0),
+    (640, 260, 300, "NT", 0), (130, 1024, 4096, "NN", 0), (64, 256, 256, "NT", 0), (200, 516, 260, "NN", 0),
+    (258, 1024, 1024, "NT", 1), (258, 1024, 1024, "NN", 7), (77, 300, 1028, "NT", 64)])
+def test_gemm_skinny(M, N, K, layout, splits):
+    """k_skinny (few rows, wide and deep: c5's post-pool F = 1024 layers and their input gradient):
+    padded row blocks, N and K tails inside a 64-wide tile and a 64-deep stage, one split and more
+    splits than stages; against fp64, deterministic (bitwise) and counters left at zero."""
+    from aimx import _lib
+    C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True, splits=splits)
+    err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    C2, _, _, _, _ = _gemm(M, N, K, layout, bias=True, res=True, splits=splits)
+    assert torch.equal(C, C2)
+    assert int(_lib.counters(DEV).abs().sum().item()) == 0
+
+
+def test_gemm_skinny_activation_epilogue():
+    C, _, pre, ref, _ = _gemm(258, 1024, 1024, "NT", bias=True, act=4)
+    assert (pre.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    fr = torch.nn.functional.silu(ref)
+    assert (C.double() - fr).abs().max().item() / fr.abs().max().item() < 2e-6
+
+
 def _gemm_raw(M, N, K, layout, off, pa, pb, ones=False):
     """aimx_gemm on operands that start `off` floats into their buffers with row strides padded by
     pa / pb floats; returns (C, bias-gradient column, fp64 reference)."""
