@@ -800,32 +800,54 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, float* lds, 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
 }
 
-template <bool BKC>
-__global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk, int nm_full, int nb,
-                                                uint32_t a_bytes, uint32_t b_bytes) {
+// Tile order: the full (64 x 64) tiles first, then the partial ones (the last column block, e.g. a
+// weight gradient's lone ones column, then the last row block), so light tiles take the CUs' second
+// slots. Tile index t = mb * nb + nbk is the split-K counter / slab index.
+__device__ __forceinline__ void skinny_tile(int b, int M, int N, int& mb, int& nbk) {
+  const int nmF = M / kSkB, nnF = N / kSkB, nm = (M + kSkB - 1) / kSkB;
+  if (b < nmF * nnF) {
+    mb = b % nmF;
+    nbk = b / nmF;
+    return;
+  }
+  b -= nmF * nnF;
+  if (N % kSkB) {  // the partial column block, every row block
+    if (b < nm) {
+      mb = b;
+      nbk = nnF;
+      return;
+    }
+    b -= nm;
+  }
+  mb = nmF;  // the partial row block, full column blocks
+  nbk = b;
+}
+
+// AK: A k-contiguous ([m][k], sak == 1) or m-contiguous ([k][m], sam == 1: a weight gradient's dY^T);
+// BKC: B k-contiguous ([n][k]) or n-contiguous ([k][n]). a.ones_col (weight gradients, !BKC only):
+// column N - 1 of B is an implicit ones column (the bias gradient), written into the stage image
+// after its DMA has landed.
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
   // ONE shared array (a second __shared__ object can make hipcc drain the DMA before each read)
   __shared__ __attribute__((aligned(16))) float smem[2 * kSkStage];  // 64 KiB: two blocks per CU
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = (int)a.M, N = (int)a.N, K = (int)a.K;
+  const int Nreal = a.ones_col ? N - 1 : N;
   const int S = (int)gridDim.y;
-  int b = (int)blockIdx.x, mb, nbk;
-  if (b < nm_full * nb) {
-    mb = b % nm_full;
-    nbk = b / nm_full;
-  } else {
-    b -= nm_full * nb;
-    mb = nm_full;
-    nbk = b;
-  }
+  const int nb = (N + kSkB - 1) / kSkB;
+  int mb, nbk;
+  skinny_tile((int)blockIdx.x, M, N, mb, nbk);
   const int z = (int)blockIdx.y;
   const int m0 = mb * kSkB, n0 = nbk * kSkB;
   const int kb = z * kchunk, ke = min(K, kb + kchunk);
   const int nst = ke > kb ? (ke - kb + kSkKC - 1) / kSkKC : 0;
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.B, b_bytes);
-  const uint32_t sam = (uint32_t)a.sam, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
+  const uint32_t sam = (uint32_t)a.sam, sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
   const int sub = lane >> 4, pos = lane & 15;
+  const bool ones_here = a.ones_col && Nreal >= n0 && Nreal < n0 + kSkB;
 
   // stage st (k0 = kb + 64 st) into buffer buf: 8 LDS-DMA instructions per wave (4 A + 4 B, 1 KiB
   // each = 4 image rows); invalid float4s point past the extent and read 0
@@ -836,19 +858,28 @@ __global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int t = w * 4 + u, row = 4 * t + sub;
-      const int ca = pos ^ (row & 15);
-      const int ka = k0 + 4 * ca;
-      const uint32_t oa = (m0 + row < M && ka < ke) ? 4u * ((uint32_t)(m0 + row) * sam + (uint32_t)ka) : kBufDrop;
+      const int ck = pos ^ (row & 15), kk = k0 + 4 * ck;             // k-contiguous image
+      const int cr = pos ^ (((row >> 2) & 3) << 2), kr = k0 + row;   // k-row image
+      uint32_t oa, ob;
+      if constexpr (AK)
+        oa = (m0 + row < M && kk < ke) ? 4u * ((uint32_t)(m0 + row) * sam + (uint32_t)kk) : kBufDrop;
+      else
+        oa = (kr < ke && m0 + 4 * cr < M) ? 4u * ((uint32_t)kr * sak + (uint32_t)(m0 + 4 * cr)) : kBufDrop;
       lds_dma16(ra, sa + t * 256, oa);
-      uint32_t ob;
-      if constexpr (BKC) {
-        ob = (n0 + row < N && ka < ke) ? 4u * ((uint32_t)(n0 + row) * sbn + (uint32_t)ka) : kBufDrop;
-      } else {
-        const int cb = pos ^ (((row >> 2) & 3) << 2);
-        const int kr = k0 + row, n = n0 + 4 * cb;
-        ob = (kr < ke && n < N) ? 4u * ((uint32_t)kr * sbk + (uint32_t)n) : kBufDrop;
-      }
+      if constexpr (BKC)
+        ob = (n0 + row < Nreal && kk < ke) ? 4u * ((uint32_t)(n0 + row) * sbn + (uint32_t)kk) : kBufDrop;
+      else
+        ob = (kr < ke && n0 + 4 * cr < Nreal) ? 4u * ((uint32_t)kr * sbk + (uint32_t)(n0 + 4 * cr)) : kBufDrop;
       lds_dma16(rb, sb + t * 256, ob);
+    }
+  };
+  // the implicit ones column of stage st's B image (k rows past the range read 0)
+  auto put_ones = [&](int st, int buf) {
+    float* sb = smem + buf * kSkStage + kSkImg;
+    const int k0 = kb + st * kSkKC, cn = Nreal - n0;
+    if (tid < kSkKC) {
+      const int r = tid;
+      sb[r * kSkB + (((cn >> 2) ^ (((r >> 2) & 3) << 2)) << 2) + (cn & 3)] = (k0 + r < ke) ? 1.f : 0.f;
     }
   };
 
@@ -856,13 +887,21 @@ __global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const bool active = m0 + 16 * w < M;
+  const int nfa = min(4, (N - n0 + 15) / 16);  // column fragments holding a column < N
   const int lm = lane & 15, g = lane >> 4;
   auto compute = [&](int buf) {
     const float* sa = smem + buf * kSkStage;
     const float* sb = sa + kSkImg;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const floatx4 av = *reinterpret_cast<const floatx4*>(sa + (16 * w + lm) * kSkKC + (((4 * s + g) ^ lm) << 2));
+      floatx4 av;
+      if constexpr (AK) {
+        av = *reinterpret_cast<const floatx4*>(sa + (16 * w + lm) * kSkKC + (((4 * s + g) ^ lm) << 2));
+      } else {
+        const int col = ((((4 * w + (lm >> 2)) ^ (g << 2))) << 2) + (lm & 3);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) av[j] = sa[(16 * s + 4 * g + j) * kSkB + col];
+      }
       floatx4 bv[4];
 #pragma unroll
       for (int nf = 0; nf < 4; ++nf) {
@@ -874,10 +913,19 @@ __global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk
           for (int j = 0; j < 4; ++j) bv[nf][j] = sb[(16 * s + 4 * g + j) * kSkB + col];
         }
       }
+      if (nfa == 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int nf = 0; nf < 4; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[nf][j], acc[nf], 0, 0, 0);
+          for (int nf = 0; nf < 4; ++nf)
+            acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[nf][j], acc[nf], 0, 0, 0);
+      } else {  // a partial column block: only its fragments below N (wave-uniform)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int nf = 0; nf < 4; ++nf)
+            if (nf < nfa) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[nf][j], acc[nf], 0, 0, 0);
+      }
     }
   };
 
@@ -891,6 +939,12 @@ __global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // (s_barrier alone does not order memory for the compiler)
+    if (ones_here) {  // after every wave's DMA of the stage has landed
+      put_ones(st, st & 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     if (active) compute(st & 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every read of the buffer done before it is refilled
@@ -900,7 +954,7 @@ __global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk
 
   if (S > 1) {
     const int tile = mb * nb + nbk;
-    const int64_t ntiles = (int64_t)(nm_full + (M % kSkB ? 1 : 0)) * nb;
+    const int64_t ntiles = (int64_t)((M + kSkB - 1) / kSkB) * nb;
     constexpr int TILE = kSkB * kSkB;
     const __amdgpu_buffer_rsrc_t rws = make_rsrc(a.workspace, (uint32_t)(4 * (int64_t)S * ntiles * TILE));
     const uint32_t slab0 = (uint32_t)(4 * (((int64_t)z * ntiles + tile) * TILE));
@@ -1548,22 +1602,27 @@ struct Plan {
   bool skinny;  // k_skinny (64 x 64 tiles, deep LDS-DMA stages)
 };
 
-// k_skinny applies to fp32 products with few rows and a wide, deep right operand whose tiled grid
-// is short of the chip: A k-contiguous, B k- or n-contiguous, 16-byte rows, counters for the
-// in-launch split-K reduce. AIMX_SKINNY=0 turns it off (A/B).
+// k_skinny applies to fp32 products whose tiled grid is short of the chip: few rows and a wide,
+// deep right operand (A k-contiguous: the post-pool chain's forward / input gradient, M <= 640), or
+// a short-K weight gradient (A m-contiguous, K <= 1024 rows, M and N >= 256), with 16-byte rows
+// and counters for the in-launch split-K reduce. AIMX_SKINNY=0 turns it off (A/B).
 bool skinny_ok(const AimxGemmArgs& a) {
   static const bool off = [] {
     const char* e = getenv("AIMX_SKINNY");
     return e && atoi(e) == 0;
   }();
-  if (off || a.precision != AIMX_PREC_FP32 || a.ones_col || a.zc_rowptr) return false;
-  if (a.M < 1 || a.M > 640 || a.N < 256 || a.K < 256) return false;
-  if (a.sak != 1 || !(a.sbk == 1 || a.sbn == 1)) return false;
+  if (off || a.precision != AIMX_PREC_FP32 || a.zc_rowptr) return false;
+  const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
+  const bool ak = a.sak == 1, bkc = a.sbk == 1;
+  if (!(ak || a.sam == 1) || !(bkc || a.sbn == 1) || (a.ones_col && bkc)) return false;
+  if (ak ? (a.M < 1 || a.M > 640 || Nreal < 256 || a.K < 256) : (a.K < 1 || a.K > 1024 || a.M < 256 || Nreal < 256))
+    return false;
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (!al(a.A) || !al(a.B) || a.K % 4 || a.sam % 4) return false;
-  if (a.sbk == 1 ? (a.sbn % 4 != 0) : (a.sbk % 4 != 0 || a.N % 4 != 0)) return false;
+  if (!al(a.A) || !al(a.B)) return false;
+  if (ak ? (a.sam % 4 != 0 || a.K % 4 != 0) : (a.sak % 4 != 0 || a.M % 4 != 0)) return false;
+  if (bkc ? (a.sbn % 4 != 0 || a.K % 4 != 0) : (a.sbk % 4 != 0 || Nreal % 4 != 0)) return false;
   const int64_t tiles = cdiv(a.M, kSkB) * cdiv(a.N, kSkB);
-  return tiles < 256 && a.counters && tiles <= a.n_counters;
+  return tiles <= 320 && a.counters && tiles <= a.n_counters;
 }
 
 // Weight-gradient layout (A m-contiguous, B n-contiguous) with a long K: k_wgrad.
@@ -1578,7 +1637,7 @@ Plan plan_gemm(const AimxGemmArgs& a, bool allow_skinny = true) {
   Plan p;
   p.wgrad = false;
   p.skinny = false;
-  if (allow_skinny && !is_wgrad(a) && skinny_ok(a)) {
+  if (allow_skinny && skinny_ok(a)) {
     // splits so the full row blocks' tiles fill the chip about once, >= 128 of K per split
     p.skinny = true;
     p.bm = p.bn = kSkB;
@@ -1827,6 +1886,33 @@ bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
 }
 }  // namespace
 
+// A weight-gradient problem as one unsplit k_skinny launch (no workspace needed), when it applies
+bool wgrad_as_skinny(const AimxWgradProblem& pr, int32_t* counters, int64_t n_counters, AimxGemmArgs& a) {
+  if (pr.zc_rowptr || pr.K < 1) return false;
+  a = AimxGemmArgs{};
+  a.M = pr.M;
+  a.N = pr.col_out ? pr.N + 1 : pr.N;
+  a.K = pr.K;
+  a.A = pr.dY;
+  a.sam = 1;
+  a.sak = pr.ld_dy;
+  a.B = pr.X;
+  a.sbk = pr.ld_x;
+  a.sbn = 1;
+  a.C = pr.dW;
+  a.ldc = pr.ld_dw;
+  a.act = -1;
+  a.dact_kind = -1;
+  a.ones_col = pr.col_out ? 1 : 0;
+  a.col_out = pr.col_out;
+  a.precision = AIMX_PREC_FP32;
+  a.counters = counters;
+  a.n_counters = n_counters;
+  if (!skinny_ok(a)) return false;
+  const Plan p = plan_gemm(a);
+  return p.skinny && p.splits == 1;
+}
+
 // workspace of the tiled kernels' split-K plan
 size_t tiled_workspace_floats(const AimxGemmArgs& a) {
   const Plan p = plan_gemm(a);
@@ -1886,12 +1972,11 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   if (p.skinny) {
     const size_t need = p.splits > 1 ? sizeof(float) * (size_t)p.splits * cdiv(a.M, kSkB) * cdiv(a.N, kSkB) * kSkB * kSkB : 0;
     if (p.splits == 1 || (a.workspace && a.workspace_bytes >= need)) {
-      const int nb = (int)cdiv(a.N, kSkB), nm_full = (int)(a.M / kSkB);
-      const dim3 grid((unsigned)(cdiv(a.M, kSkB) * nb), (unsigned)p.splits);
-      if (a.sbk == 1)
-        hipLaunchKernelGGL(k_skinny<true>, grid, dim3(256), 0, s, a, (int)p.kchunk, nm_full, nb, a_bytes, b_bytes);
-      else
-        hipLaunchKernelGGL(k_skinny<false>, grid, dim3(256), 0, s, a, (int)p.kchunk, nm_full, nb, a_bytes, b_bytes);
+      const dim3 grid((unsigned)(cdiv(a.M, kSkB) * cdiv(a.N, kSkB)), (unsigned)p.splits);
+      const bool ak = a.sak == 1, bkc = a.sbk == 1;
+      auto fn = ak ? (bkc ? k_skinny<true, true> : k_skinny<true, false>)
+                   : (bkc ? k_skinny<false, true> : k_skinny<false, false>);
+      hipLaunchKernelGGL(fn, grid, dim3(256), 0, s, a, (int)p.kchunk, a_bytes, b_bytes);
       AIMX_CHECK_LAUNCH();
       return AIMX_OK;
     }
@@ -2009,6 +2094,14 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
+    {  // short-K, wide weight gradients (the post-pool chain's F x F at F >= 256): one k_skinny launch
+      AimxGemmArgs ga;
+      if (wgrad_as_skinny(pr, counters, n_counters, ga)) {
+        const int rc = launch_gemm(ga, (hipStream_t)stream);
+        if (rc != AIMX_OK) return rc;
+        continue;
+      }
+    }
     const WgPlan w = wg_plan(pr, min_wgs, bb);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {

@@ -271,6 +271,21 @@ def test_gemm_skinny(M, N, K, layout, splits):
     assert int(_lib.counters(DEV).abs().sum().item()) == 0
 
 
+@pytest.mark.parametrize("M,N,K,ones", [(1024, 1024, 258, True), (1024, 1024, 258, False), (512, 512, 516, True),
+                                        (260, 300, 1000, True), (1024, 256, 61, True), (256, 1020, 7, False)])
+def test_gemm_skinny_weight_gradient(M, N, K, ones):
+    """k_skinny's short-K weight-gradient layout (dW = dY^T X: A m-contiguous, B n-contiguous) with
+    the implicit ones column (bias gradient) written into the stage image: K tails inside a stage,
+    a partial last column block holding only the ones column; fp64, bitwise deterministic."""
+    C, col, _, ref, Am = _gemm(M, N, K, "TN", ones=ones)
+    assert (C.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    if ones:
+        rs = Am.double().sum(1)
+        assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
+    C2, col2, _, _, _ = _gemm(M, N, K, "TN", ones=ones)
+    assert torch.equal(C, C2) and torch.equal(col, col2)
+
+
 def test_gemm_skinny_activation_epilogue():
     C, _, pre, ref, _ = _gemm(258, 1024, 1024, "NT", bias=True, act=4)
     assert (pre.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6

@@ -4,7 +4,7 @@ export PYTHONDONTWRITEBYTECODE=1
 T="python3 -u -m pytest -x -v --timeout 120 --timeout-method thread"
 M="python3 tools/hop_cfg_micro.py --configs c4,c5"
 tools/gpu_steps.sh \
- "?200 r5h/skinny_tests.log $T tests/test_gpu_parity.py -k 'skinny or gemm_layouts or activation_epilogue'" \
+ "?200 r5h/skinny_tests.log $T tests/test_gpu_parity.py -k 'skinny or gemm or wgrad or activation_epilogue or linear'" \
  "?300 r5h/hop_tests.log $T tests/test_gpu_hop_rows.py" \
  "200 r5h/regs.log $M" \
  "200 r5h/rows.log env AIMX_HOP_REGS=0 $M" \
