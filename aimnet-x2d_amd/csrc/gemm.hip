@@ -827,10 +827,25 @@ __device__ __forceinline__ void skinny_tile(int b, int M, int N, int& mb, int& n
 // BKC: B k-contiguous ([n][k]) or n-contiguous ([k][n]). a.ones_col (weight gradients, !BKC only):
 // column N - 1 of B is an implicit ones column (the bias gradient), written into the stage image
 // after its DMA has landed.
-template <bool AK, bool BKC>
+// NS: stages in the ring (2: 64 KiB, two blocks per CU; 4: 128 KiB, a block's whole ~256-deep K
+// range in flight at once).
+template <int NS>
+__device__ __forceinline__ void skinny_wait(int in_flight_after) {
+  // vmcnt = 8 DMAs per stage still allowed in flight behind the stage about to be read
+  if (NS > 3 && in_flight_after >= 3)
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (NS > 2 && in_flight_after == 2)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (in_flight_after >= 1)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool AK, bool BKC, int NS>
 __global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
   // ONE shared array (a second __shared__ object can make hipcc drain the DMA before each read)
-  __shared__ __attribute__((aligned(16))) float smem[2 * kSkStage];  // 64 KiB: two blocks per CU
+  __shared__ __attribute__((aligned(16))) float smem[NS * kSkStage];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = (int)a.M, N = (int)a.N, K = (int)a.K;
@@ -929,27 +944,25 @@ __global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk
     }
   };
 
-  if (nst > 0) fill(0, 0);
-  if (nst > 1) fill(1, 1);
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+    if (q < nst) fill(q, q);
   for (int st = 0; st < nst; ++st) {
-    // this stage's 8 DMAs retired (the next stage's 8 may stay in flight), then every wave's
-    if (st + 1 < nst)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this stage's 8 DMAs retired (the later stages' may stay in flight), then every wave's
+    skinny_wait<NS>(min(NS - 1, nst - 1 - st));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // (s_barrier alone does not order memory for the compiler)
     if (ones_here) {  // after every wave's DMA of the stage has landed
-      put_ones(st, st & 1);
+      put_ones(st, st % NS);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    if (active) compute(st & 1);
+    if (active) compute(st % NS);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every read of the buffer done before it is refilled
     asm volatile("" ::: "memory");
-    if (st + 2 < nst) fill(st + 2, st & 1);
+    if (st + NS < nst) fill(st + NS, st % NS);
   }
 
   if (S > 1) {
@@ -1638,11 +1651,11 @@ Plan plan_gemm(const AimxGemmArgs& a, bool allow_skinny = true) {
   p.wgrad = false;
   p.skinny = false;
   if (allow_skinny && skinny_ok(a)) {
-    // splits so the full row blocks' tiles fill the chip about once, >= 128 of K per split
+    // splits so the blocks fill the chip at most once (one 128-KiB block per CU), >= 128 of K each
     p.skinny = true;
     p.bm = p.bn = kSkB;
-    const int64_t full = std::max<int64_t>(1, a.M / kSkB) * cdiv(a.N, kSkB);
-    int64_t sp = a.splits > 0 ? a.splits : std::max<int64_t>(1, (256 + full / 2) / full);
+    const int64_t tiles = cdiv(a.M, kSkB) * cdiv(a.N, kSkB);
+    int64_t sp = a.splits > 0 ? a.splits : std::max<int64_t>(1, 256 / tiles);
     sp = std::max<int64_t>(1, std::min<int64_t>({sp, 64, a.K / 128}));
     p.kchunk = cdiv(cdiv(a.K, sp), kSkKC) * kSkKC;
     p.splits = (int)std::max<int64_t>(1, cdiv(a.K, p.kchunk));
@@ -1974,8 +1987,15 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
     if (p.splits == 1 || (a.workspace && a.workspace_bytes >= need)) {
       const dim3 grid((unsigned)(cdiv(a.M, kSkB) * cdiv(a.N, kSkB)), (unsigned)p.splits);
       const bool ak = a.sak == 1, bkc = a.sbk == 1;
-      auto fn = ak ? (bkc ? k_skinny<true, true> : k_skinny<true, false>)
-                   : (bkc ? k_skinny<false, true> : k_skinny<false, false>);
+      // stages in flight: AIMX_SKINNY_NS=2 / 4 (A/B; default 4)
+      static const int ns = [] {
+        const char* e = getenv("AIMX_SKINNY_NS");
+        return (e && atoi(e) == 2) ? 2 : 4;
+      }();
+      auto fn = ns == 4 ? (ak ? (bkc ? k_skinny<true, true, 4> : k_skinny<true, false, 4>)
+                              : (bkc ? k_skinny<false, true, 4> : k_skinny<false, false, 4>))
+                        : (ak ? (bkc ? k_skinny<true, true, 2> : k_skinny<true, false, 2>)
+                              : (bkc ? k_skinny<false, true, 2> : k_skinny<false, false, 2>));
       hipLaunchKernelGGL(fn, grid, dim3(256), 0, s, a, (int)p.kchunk, a_bytes, b_bytes);
       AIMX_CHECK_LAUNCH();
       return AIMX_OK;

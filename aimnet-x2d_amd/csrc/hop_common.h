@@ -39,7 +39,7 @@ int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_
                        int32_t skip_tail = 0, bool windows = true);
 
 // The first output chunk's rows summed from the register file, molecule by molecule (hop_regs.hip);
-// needs row_seg. AIMX_HOP_REGS=0 turns it off (gather_regs_on).
+// needs row_seg. Opt-in: AIMX_HOP_REGS=1 (gather_regs_on; measured slower, see hop_regs.hip).
 bool gather_regs_on();
 int launch_gather_regs(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,

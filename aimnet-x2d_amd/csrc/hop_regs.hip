@@ -188,10 +188,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 
 }  // namespace
 
+// Opt-in (AIMX_HOP_REGS=1): bit-exact, but measured 4-12x SLOWER than hop_rows.hip in the step's
+// own layout (c4 forward 123.7 vs 30.3 us, c5 519.5 vs 42.3 us; profiles/r05_hop_regs_ab.txt):
+// every source is a dependent chain (LDS index read -> readfirstlane -> s_set_gpr_idx -> v_mov)
+// of one wave per SIMD, with nothing to overlap it. Kept for the record and its tests.
 bool gather_regs_on() {
   static const bool on = [] {
     const char* e = getenv("AIMX_HOP_REGS");
-    return !e || atoi(e) != 0;
+    return e && atoi(e) != 0;
   }();
   return on;
 }

@@ -104,12 +104,12 @@ def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):
         e_max = max(c["edges"].shape[0] for c in cs) + (64 if k else 256)
         shape[k] = (n_max, e_max, adata.pad_mols_for(n_max, n_min, 64, 1) if k else pad_mols_for(n_max, n_min))
     out = []
-    for c, t, q in cols:
+    for c, t, chg in cols:
         n_max, e_max, pm = shape[bucket(c)]
         real_atoms, real_edges = c["batch"].shape[0], c["edges"].shape[0]
         pc = adata.pad_collated(c, n_max, e_max, cfg["batch"], pm)
         tg = np.concatenate([t, np.zeros((pm, t.shape[1]), np.float32)])
-        qq = np.concatenate([q, np.zeros(pm, np.float32)])
+        qq = np.concatenate([chg, np.zeros(pm, np.float32)])
         b = adata.DeviceBatch(pc, device, targets=tg, total_charges=qq, csr_hops=cfg["hops"])
         b.real_atoms, b.real_edges, b.real_graphs = real_atoms, real_edges, cfg["batch"]
         out.append(b)

@@ -8,6 +8,7 @@ import sys
 import time
 
 import pytest
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -150,3 +151,21 @@ def test_hung_rank_with_finished_peer_hits_the_deadline(tmp_path):
         while any(_alive(q) for q in pids) and time.time() - t1 < 5:
             time.sleep(0.05)
         assert not any(_alive(q) for q in pids)
+
+
+@pytest.mark.parametrize("config,buckets", [("c2", True), ("c5", True), ("c4", False)])
+def test_padded_static_layouts_on_cpu(config, buckets):
+    """bench.make_batches' static graph layouts (the default bench path): every batch padded to its
+    bucket's atom count (a multiple of the config's layout quantum), padding molecules appended and
+    excluded from the loss by real_graphs, charges and targets padded with zeros."""
+    cfg = dict(bench.CONFIGS[config])
+    cfg["batch"] = 12
+    q = bench.layout_quantum(cfg)
+    bs = bench.make_batches(cfg, 3, 7, torch.device("cpu"), pad=True, buckets=buckets)
+    assert len(bs) == 3
+    for b in bs:
+        n = b.batch.shape[0]
+        if buckets:
+            assert n % q == 0 and n >= b.real_atoms + 2
+        assert b.real_graphs == 12 and b.total_charges.shape[0] > 12
+        assert not b.total_charges[12:].any()
