@@ -154,6 +154,11 @@ int launch_charge_bwd(const float* x, int64_t ldx, int64_t N, int64_t D, const i
 // mlp_pack_floats(s) floats (0: not needed) written by launch_mlp_pack once per call and direction,
 // passed as `pack` (nullptr: the weight-resident kernels).
 bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision, int64_t ld);
+// the stack's F / UG row strides (AimxShellStack.ld_f / ld_ug; 0 = dense)
+inline int64_t stack_ld_f(const AimxShellStack* s) {
+  return s->ld_f > 0 ? s->ld_f : s->D * (s->num_hops + 1);
+}
+inline int64_t stack_ld_ug(const AimxShellStack* s) { return s->ld_ug > 0 ? s->ld_ug : 2 * s->D; }
 size_t mlp_pack_floats(const AimxShellStack* s);
 int launch_mlp_pack(const AimxShellStack* s, bool bwd, float* dst, hipStream_t st);
 int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64_t ldx, float* out, int64_t ldo,

@@ -1618,11 +1618,14 @@ struct Plan {
 // k_skinny applies to fp32 products whose tiled grid is short of the chip: few rows and a wide,
 // deep right operand (A k-contiguous: the post-pool chain's forward / input gradient, M <= 640), or
 // a short-K weight gradient (A m-contiguous, K <= 1024 rows, M and N >= 256), with 16-byte rows
-// and counters for the in-launch split-K reduce. AIMX_SKINNY=0 turns it off (A/B).
+// and counters for the in-launch split-K reduce. Opt-in (AIMX_SKINNY=1): measured slower than the
+// tiled path at c5 (head forward 18.8-22.7 vs 15.2 us, step 4.115 vs 3.931 ms;
+// profiles/r05_skinny_ab.txt) — one wave per SIMD and two barriers per 64-deep stage leave the
+// MFMA pipe idle between stages. Kept, with its parity tests, for the record.
 bool skinny_ok(const AimxGemmArgs& a) {
   static const bool off = [] {
     const char* e = getenv("AIMX_SKINNY");
-    return e && atoi(e) == 0;
+    return !(e && atoi(e) == 1);
   }();
   if (off || a.precision != AIMX_PREC_FP32 || a.zc_rowptr) return false;
   const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;

@@ -39,7 +39,8 @@ struct MlpFwd {
   int32_t nm, act, drop, salt0;
   float drop_p;
   const int64_t* seed;
-  const float* ug;  // [N, 2D]: a0 = act(u), g
+  const float* ug;  // [N, 2D] (row stride ldug): a0 = act(u), g
+  int64_t ldug;
   const float* x;   // outer residual (nullable), ld ldx
   int64_t ldx;
   const float* w1[8];
@@ -68,7 +69,8 @@ struct MlpBwd {
   const uint8_t* M[8];
   float* dV[8];
   float* dA[8];     // dA_k for k = 1..nm-1 (the gradient w.r.t. block k's input), index k - 1
-  float* dug;       // [N, 2D]: [du | dY]
+  float* dug;       // [N, 2D] (row stride ldug): [du | dY]
+  int64_t ldug;
   int32_t v4;       // fill with 16-byte loads (D, lddy and every weight / dy pointer 4-float aligned)
 };
 
@@ -386,9 +388,9 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, in
     bv[u] = btab[m][c];
   }
   if (p.v4)
-    fill_lds_v4<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, 2 * p.D, (int64_t)blockIdx.x * R, R, N);
+    fill_lds_v4<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, p.ldug, (int64_t)blockIdx.x * R, R, N);
   else
-    fill_lds<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, 2 * p.D, (int64_t)blockIdx.x * R, R, N);
+    fill_lds<false>(W, wtab, 2 * nm, D, Kp, S, Xa, p.ug, p.ldug, (int64_t)blockIdx.x * R, R, N);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int e = threadIdx.x + u * (int)blockDim.x;
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, in
     const int64_t r0 = ch * R;
     if (ch != (int64_t)blockIdx.x) {
       __syncthreads();  // the previous chunk's last epilogue reads of Xa are done
-      load_rows(Xa, S, p.ug, 2 * p.D, r0, R, D, Kp, N);
+      load_rows(Xa, S, p.ug, p.ldug, r0, R, D, Kp, N);
       __syncthreads();
     }
     MLPW_STAMP(st++);
@@ -430,7 +432,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, in
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int64_t gc = min(r0 + 16 * t + 4 * (lane >> 4) + i, N - 1);
-            resid[i] = p.ug[gc * 2 * p.D + p.D + cc];
+            resid[i] = p.ug[gc * p.ldug + p.D + cc];
             if (p.x) resid[i] += p.x[gc * p.ldx + cc];
           }
         }
@@ -472,7 +474,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, in
               add[i] += resid[i];
             } else {
               const int64_t gc = min(r0 + 16 * t + 4 * (lane >> 4) + i, N - 1);
-              float rr = p.ug[gc * 2 * p.D + p.D + cc];
+              float rr = p.ug[gc * p.ldug + p.D + cc];
               if (p.x) rr += p.x[gc * p.ldx + cc];
               add[i] += rr;
             }
@@ -551,7 +553,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
     MLPW_STAMP(sb++);
     for (int e = threadIdx.x; e < R * D; e += blockDim.x) {  // dg = dY (from the LDS copy)
       const int r = e / D, c = e - r * D;
-      if (r0 + r < N) p.dug[(r0 + r) * 2 * p.D + p.D + c] = DA[r * S + c];
+      if (r0 + r < N) p.dug[(r0 + r) * p.ldug + p.D + c] = DA[r * S + c];
     }
     float uu[4] = {0.f, 0.f, 0.f, 0.f};  // act'(u) input for block 0's dA phase
     for (int k = nm - 1; k >= 0; --k) {
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
               if (k > 0)
                 dAk[g * D + c] = da;
               else
-                p.dug[g * 2 * p.D + c] = da * act_grad(p.act, uu[i]);
+                p.dug[g * p.ldug + c] = da * act_grad(p.act, uu[i]);
             }
           }
         }
@@ -840,7 +842,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
   const float scale = drop_scale(p.drop_p);
   const uint64_t seed = p.drop ? (uint64_t)*p.seed : 0;
   // the last block's residual operands as buffer loads (an absent x reads 0: no branch per load)
-  const __amdgpu_buffer_rsrc_t rug = mlp_rsrc(p.ug, (uint32_t)(4 * N * 2 * D));
+  const __amdgpu_buffer_rsrc_t rug = mlp_rsrc(p.ug, (uint32_t)(4 * N * p.ldug));
   const __amdgpu_buffer_rsrc_t rx_ = mlp_rsrc(p.x, p.x ? (uint32_t)(4 * ((N - 1) * p.ldx + D)) : 0u);
   // k padding (columns D .. 16 G) of both tiles: the chunk loads and the epilogues write columns < D only
   mlps_zero_pad(Xa, 2 * R, S, D, 16 * G);
@@ -848,7 +850,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
     __syncthreads();  // the previous chunk's last reads of Xa are done
-    load_chunk<4 * RT * NF>(Xa, S, p.ug, 2 * p.D, r0c, R, D, N);  // a0 = act(u) = UG[:, :D]; zero beyond N
+    load_chunk<4 * RT * NF>(Xa, S, p.ug, p.ldug, r0c, R, D, N);  // a0 = act(u) = UG[:, :D]; zero beyond N
     __syncthreads();
     MLPS_STAMP(0, 2);
     BStream<NF> bs;
@@ -920,7 +922,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const uint32_t gq = (uint32_t)min(r0 + 16 * t + lq + r, N - 1);
-                rg[t][r] = bload(rug, 4u * (gq * (uint32_t)(2 * D) + (uint32_t)(D + c)));
+                rg[t][r] = bload(rug, 4u * (gq * (uint32_t)p.ldug + (uint32_t)(D + c)));
                 rx[t][r] = bload(rx_, 4u * (gq * (uint32_t)p.ldx + (uint32_t)c));  // 0 without x
               }
           }
@@ -973,7 +975,7 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
   for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
     const int64_t r0c = ch * R;
     __syncthreads();
-    load_chunk<4 * RT * NF>(DA, S, p.dy, p.lddy, r0c, R, D, N, p.dug + p.D, 2 * p.D);  // and dg = dY
+    load_chunk<4 * RT * NF>(DA, S, p.dy, p.lddy, r0c, R, D, N, p.dug + p.D, p.ldug);  // and dg = dY
     __syncthreads();
     MLPS_STAMP(1, 2);
     BStream<NF> bs;
@@ -995,10 +997,10 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
       // per fragment: the epilogue's operands (dV: v and the dropout mask; dA of block 0: u), every
       // load issued before the first use (one round trip per fragment, see k_mlps_fwd), then its
       // outputs
-      const uint32_t ldd = dv ? (uint32_t)D : k > 0 ? (uint32_t)D : (uint32_t)(2 * D);
+      const uint32_t ldd = dv ? (uint32_t)D : k > 0 ? (uint32_t)D : (uint32_t)p.ldug;
       const __amdgpu_buffer_rsrc_t rout = dv      ? mlp_rsrc(pick8(p.dV, k), 4u * nd)
                                           : k > 0 ? mlp_rsrc(pick8(p.dA, k - 1), 4u * nd)
-                                                  : mlp_rsrc(p.dug, 8u * nd);
+                                                  : mlp_rsrc(p.dug, 4u * (uint32_t)(N * p.ldug));
       const gfloat* V = (const gfloat*)(dv ? pick8(p.V, k) : p.u);
       const gu8* M = (dv && p.drop) ? (const gu8*)pick8(p.M, k) : (const gu8*)V;
 #pragma unroll
@@ -1213,7 +1215,7 @@ bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision, int64_t l
 
 size_t mlp_pack_floats(const AimxShellStack* s) {
   if (!mlps_on(s->N, s->D, s->num_mlp, s->precision) ||
-      !mlp_extent_ok(s->N, s->D, std::max(s->D * (s->num_hops + 1), s->out_ld)))
+      !mlp_extent_ok(s->N, s->D, std::max({stack_ld_f(s), stack_ld_ug(s), s->out_ld})))
     return 0;
   return (size_t)(s->num_layers * 2 * s->num_mlp * mlps_image_floats(s->D));
 }
@@ -1257,6 +1259,7 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
   p.drop_p = p.drop ? s->drop_p : 0.f;
   p.seed = s->drop_seed;
   p.ug = s->UG[l];
+  p.ldug = stack_ld_ug(s);
   p.x = x_res;
   p.ldx = ldx;
   for (int64_t k = 0; k < nm; ++k) {
@@ -1274,7 +1277,7 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
   p.ldo = ldo;
   {
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
-    bool v4 = s->D % 4 == 0 && al(p.ug);
+    bool v4 = s->D % 4 == 0 && p.ldug % 4 == 0 && al(p.ug);
     for (int64_t k = 0; k < nm; ++k) v4 = v4 && al(p.w1[k]) && al(p.w2[k]);
     p.v4 = (v4 && !getenv("AIMX_MLPW_FILL1")) ? 1 : 0;  // AIMX_MLPW_FILL1: dword fill (A/B)
   }
@@ -1315,6 +1318,7 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
     p.dA[k] = (k < nm - 1) ? dA[k] : nullptr;
   }
   p.dug = dug;
+  p.ldug = stack_ld_ug(s);
   {
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     bool v4 = s->D % 4 == 0 && lddy % 4 == 0 && al(dy);

@@ -111,12 +111,12 @@ int copy2d(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows,
 // A shell layer without MLP blocks (shell_conv_num_mlp_layers = 0: cli.py:106-107 accepts it):
 // out = act(u) + g (layers.py:82-89, 106), + the outer residual x when stacked (gnn.py:302-306),
 // added in the reference's order. UG = [act(u) | g] (row stride 2D).
-__global__ void k_nomlp_fwd(const float* __restrict__ UG, int64_t D, const float* __restrict__ res, int64_t ldr,
-                            float* __restrict__ dst, int64_t ldd, int64_t N) {
+__global__ void k_nomlp_fwd(const float* __restrict__ UG, int64_t ldug, int64_t D, const float* __restrict__ res,
+                            int64_t ldr, float* __restrict__ dst, int64_t ldd, int64_t N) {
   const int64_t total = N * D;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / D, c = i - r * D;
-    float v = UG[r * 2 * D + c] + UG[r * 2 * D + D + c];
+    float v = UG[r * ldug + c] + UG[r * ldug + D + c];
     if (res) v = v + res[r * ldr + c];
     dst[r * ldd + c] = v;
   }
@@ -125,13 +125,13 @@ __global__ void k_nomlp_fwd(const float* __restrict__ UG, int64_t D, const float
 // Its backward: dUG = [dY * act'(u) | dY] (U = the saved pre-activation u). dY may be dUG's own
 // upper half (below the top layer the hop backward wrote it there): then only du is written.
 __global__ void k_nomlp_bwd(const float* __restrict__ dY, int64_t ldy, const float* __restrict__ U, int act,
-                            float* __restrict__ dUG, int64_t N, int64_t D, int copy_dy) {
+                            float* __restrict__ dUG, int64_t ldug, int64_t N, int64_t D, int copy_dy) {
   const int64_t total = N * D;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / D, c = i - r * D;
     const float y = dY[r * ldy + c];
-    dUG[r * 2 * D + c] = y * act_grad(act, U[r * D + c]);
-    if (copy_dy) dUG[r * 2 * D + D + c] = y;
+    dUG[r * ldug + c] = y * act_grad(act, U[r * D + c]);
+    if (copy_dy) dUG[r * ldug + D + c] = y;
   }
 }
 
@@ -181,6 +181,9 @@ void set_zc(AimxGemmArgs& a, const AimxShellStack* s, int dim) {
 
 bool valid(const AimxShellStack* s) {
   if (!s || s->N < 0 || s->D < 1 || s->num_hops < 1 || s->num_layers < 1 || s->num_mlp < 0) return false;
+  if (s->ld_f < 0 || s->ld_ug < 0 || (s->ld_f > 0 && s->ld_f < s->D * (s->num_hops + 1)) ||
+      (s->ld_ug > 0 && s->ld_ug < 2 * s->D))
+    return false;
   if (s->mode_single && (s->num_layers != 1 || s->use_pc)) return false;
   if (s->use_pc && (s->D < 2 || !s->gptr || !s->gperm || !s->total_charges)) return false;
   return true;
@@ -222,6 +225,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
   if (!valid(s)) return AIMX_EARG;
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
+  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s);  // F / UG row strides
   if (N == 0) return AIMX_OK;
   const size_t split = fwd_split_floats(s), npack = mlp_pack_floats(s);
   float* pack = nullptr;
@@ -239,19 +243,19 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
     if (s->use_pc) {
       const float* raw = (l == 0) ? s->x_in : s->X[l];
       const int64_t ldr = (l == 0) ? s->x_in_ld : D;
-      RUN(launch_charge_fwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, F, K, st));
+      RUN(launch_charge_fwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, F, LF, st));
     } else if (l == 0) {
-      RUN(copy2d(s->x_in, s->x_in_ld, F, K, N, D, st));
+      RUN(copy2d(s->x_in, s->x_in_ld, F, LF, N, D, st));
     }
     // 2) hop: chunks 1..h of F = scatter_add(x[src % N], target) in edge order. The trailing
     //    edge-less chunks (all but the first for reference inputs, layers.py:154) are not written:
     //    every GEMM over F trims them exactly (zc_*: the input projection's k loop stops before
     //    them, the weight gradient reads them as zero), so their zeros would be dead stores
-    RUN(gather(s, F, K, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, K, N, D, nullptr, 0, nullptr, 0, st,
+    RUN(gather(s, F, LF, 0, 0, D, s->fwd_rowptr, s->fwd_col, N * h, F + D, LF, N, D, nullptr, 0, nullptr, 0, st,
                zc_on() ? 1 : 0));
     // 3) [u | g] = F [Wi ; Wg]^T + [bi ; bg], a0 = act(u)
     {
-      AimxGemmArgs a = linear_fwd(N, K, D2, F, K, s->w_ig[l], s->UG[l], D2);
+      AimxGemmArgs a = linear_fwd(N, K, D2, F, LF, s->w_ig[l], s->UG[l], LUG);
       set_zc(a, s, 0);
       a.bias = s->b_ig[l];
       a.act = s->act;
@@ -263,13 +267,13 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
     // 4) MLP blocks: one fused launch for all of them (mlp.hip), or one GEMM per linear
     if (nm == 0) {  // no blocks: out = act(u) + g (+ x)
       float* dst = (l == L - 1) ? s->out : s->use_pc ? s->X[l + 1] : s->F[l + 1];
-      const int64_t ldd = (l == L - 1) ? s->out_ld : s->use_pc ? D : K;
-      hipLaunchKernelGGL(k_nomlp_fwd, dim3((unsigned)nomlp_blocks(N, D)), dim3(256), 0, st, s->UG[l], D,
-                         s->mode_single ? nullptr : F, K, dst, ldd, N);
+      const int64_t ldd = (l == L - 1) ? s->out_ld : s->use_pc ? D : LF;
+      hipLaunchKernelGGL(k_nomlp_fwd, dim3((unsigned)nomlp_blocks(N, D)), dim3(256), 0, st, s->UG[l], LUG, D,
+                         s->mode_single ? nullptr : F, LF, dst, ldd, N);
       AIMX_CHECK_LAUNCH();
       continue;
     }
-    if (mlp_fused_ok(N, D, nm, s->precision, std::max(K, s->out_ld))) {
+    if (mlp_fused_ok(N, D, nm, s->precision, std::max({LF, LUG, s->out_ld}))) {
       float* dst;
       int64_t ldd;
       if (l == L - 1) {
@@ -280,15 +284,15 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
         ldd = D;
       } else {
         dst = s->F[l + 1];
-        ldd = K;
+        ldd = LF;
       }
-      RUN(launch_mlp_fwd(s, l, s->mode_single ? nullptr : F, K, dst, ldd, pack, st));
+      RUN(launch_mlp_fwd(s, l, s->mode_single ? nullptr : F, LF, dst, ldd, pack, st));
       continue;
     }
     for (int64_t k = 0; k < nm; ++k) {
       const int64_t idx = l * nm + k;
       const float* in = (k == 0) ? s->UG[l] : s->A[idx - 1];
-      const int64_t ldin = (k == 0) ? D2 : D;
+      const int64_t ldin = (k == 0) ? LUG : D;
       {
         AimxGemmArgs a = linear_fwd(N, D, D, in, ldin, s->w1[idx], s->R[idx], D);
         a.bias = s->b1[idx];
@@ -320,7 +324,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
           ldd = D;
         } else {
           dst = s->F[l + 1];
-          ldd = K;
+          ldd = LF;
         }
         AimxGemmArgs a = linear_fwd(N, D, D, s->R[idx], D, s->w2[idx], dst, ldd);
         a.bias = s->b2[idx];
@@ -328,10 +332,10 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
         a.ldres[0] = ldin;
         if (last) {
           a.res[1] = s->UG[l] + D;  // global skip (layers.py:106)
-          a.ldres[1] = D2;
+          a.ldres[1] = LUG;
           if (!s->mode_single) {
             a.res[2] = F;  // outer residual x (gnn.py:302-306), after partial charges
-            a.ldres[2] = K;
+            a.ldres[2] = LF;
           }
         }
         RUN(run(a, ws, st));
@@ -359,13 +363,14 @@ int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, c
                          AimxWgradProblem* out) {
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
+  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s);
   int n = 0;
   for (int64_t l = L - 1; l >= 0; --l) {
     const float* dYl = nullptr;
     int64_t ldy = D;
     if (base) {  // below the top layer, dY lives in the upper half of the layer's dUG (see backward)
-      dYl = (l == L - 1) ? g->d_out : base + L_->dUG + l * N * D2 + D;
-      ldy = (l == L - 1) ? g->d_out_ld : D2;
+      dYl = (l == L - 1) ? g->d_out : base + L_->dUG + l * N * LUG + D;
+      ldy = (l == L - 1) ? g->d_out_ld : LUG;
     }
     for (int64_t k = nm - 1; k >= 0; --k) {
       const int64_t idx = l * nm + k;
@@ -374,12 +379,12 @@ int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, c
       AimxWgradProblem w2 = {da, lda, base ? s->R[idx] : nullptr, D, g ? g->d_w2[idx] : nullptr, D,
                              g ? g->d_b2[idx] : nullptr, D, D, N};
       const float* in = base ? ((k == 0) ? s->UG[l] : s->A[idx - 1]) : nullptr;
-      AimxWgradProblem w1 = {base ? base + L_->dV + idx * N * D : nullptr, D, in, (k == 0) ? D2 : D,
+      AimxWgradProblem w1 = {base ? base + L_->dV + idx * N * D : nullptr, D, in, (k == 0) ? LUG : D,
                              g ? g->d_w1[idx] : nullptr, D, g ? g->d_b1[idx] : nullptr, D, D, N};
       out[n++] = w2;
       out[n++] = w1;
     }
-    AimxWgradProblem wig = {base ? base + L_->dUG + l * N * D2 : nullptr, D2, base ? s->F[l] : nullptr, K,
+    AimxWgradProblem wig = {base ? base + L_->dUG + l * N * LUG : nullptr, LUG, base ? s->F[l] : nullptr, LF,
                             g ? g->d_w_ig[l] : nullptr, K, g ? g->d_b_ig[l] : nullptr, D2, K, N};
     if (zc_on() && s->fwd_rowptr) {  // weight columns of empty chunks get an exact zero gradient
       wig.zc_rowptr = s->fwd_rowptr;
@@ -399,8 +404,8 @@ BwdLayout bwd_layout(const AimxShellStack* s) {
   b.nA = L * (nm - 1);
   b.nY = std::max<int64_t>(L - 1, 0);
   int64_t o = 0;
-  b.dF = o, o += al64(N * K);
-  b.dUG = o, o += al64(L * N * 2 * D);
+  b.dF = o, o += al64(N * stack_ld_f(s));
+  b.dUG = o, o += al64(L * N * stack_ld_ug(s));
   b.dV = o, o += al64(L * nm * N * D);
   b.dA = o, o += al64(std::max<int64_t>(b.nA, 1) * N * D);
   b.dY = o, o += al64(std::max<int64_t>(b.nY, 1) * N * D);
@@ -429,6 +434,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   if (!valid(s) || !g) return AIMX_EARG;
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
+  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s);
   if (N == 0) return AIMX_OK;
   const BwdLayout lay = bwd_layout(s);
   if (!g->workspace || g->workspace_bytes < sizeof(float) * (size_t)lay.total) return AIMX_EARG;
@@ -458,14 +464,14 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   for (int64_t l = L - 1; l >= 0; --l) {
     // dUG = [du | dg] with dg = dY: below the top layer the hop backward of layer l + 1 already
     // wrote dY into dUG's upper half (ld 2D), so only the top layer copies its upstream gradient
-    float* dUG = base + lay.dUG + l * N * D2;
+    float* dUG = base + lay.dUG + l * N * LUG;
     const float* dY = (l == L - 1) ? g->d_out : dUG + D;
-    const int64_t ldy = (l == L - 1) ? g->d_out_ld : D2;
+    const int64_t ldy = (l == L - 1) ? g->d_out_ld : LUG;
     // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
-    const bool fused = nm > 0 && mlp_fused_ok(N, D, nm, s->precision, std::max({K, s->out_ld, g->d_out_ld}));
+    const bool fused = nm > 0 && mlp_fused_ok(N, D, nm, s->precision, std::max({LF, LUG, s->out_ld, g->d_out_ld}));
     if (nm == 0) {  // no blocks: dUG = [dY * act'(u) | dY]
       hipLaunchKernelGGL(k_nomlp_bwd, dim3((unsigned)nomlp_blocks(N, D)), dim3(256), 0, st, dY, ldy, s->U[l], s->act,
-                         dUG, N, D, dY != dUG + D ? 1 : 0);
+                         dUG, LUG, N, D, dY != dUG + D ? 1 : 0);
       AIMX_CHECK_LAUNCH();
     }
     if (fused) {  // the whole chain + dUG = [du | dY] in one launch (mlp.hip)
@@ -496,7 +502,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       }
       {  // da_in = da_out + dV W1 ; for k == 0 also * act'(u) -> du into dUG[:, :D]
         float* dst = (k == 0) ? dUG : base + lay.dA + (l * (nm - 1) + k - 1) * N * D;
-        const int64_t ldd = (k == 0) ? D2 : D;
+        const int64_t ldd = (k == 0) ? LUG : D;
         AimxGemmArgs a = linear_dx(N, D, D, dV, D, s->w1[idx], dst, ldd);
         a.res[0] = da_out;
         a.ldres[0] = ld_out;
@@ -509,7 +515,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       }
     }
     // dg = dY -> dUG[:, D:] (the fused chain writes it itself)
-    if (!fused && nm > 0 && dY != dUG + D) RUN(copy2d(dY, ldy, dUG + D, D2, N, D, st));
+    if (!fused && nm > 0 && dY != dUG + D) RUN(copy2d(dY, ldy, dUG + D, LUG, N, D, st));
     if (aux) {  // fork: this layer's weight gradients run beside the rest of the chain
       hipEvent_t ev = (hipEvent_t)g->events[l];
       AIMX_CHECK_HIP(hipEventRecord(ev, st));
@@ -519,17 +525,17 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     }
     {  // dF = dUG [Wi ; Wg]; tiles wholly in the trailing empty chunks are not computed nor stored:
        // the hop backward gathers only from chunks that hold targets (zc_dim 2)
-      AimxGemmArgs a = linear_dx(N, K, D2, dUG, D2, s->w_ig[l], dF, K);
+      AimxGemmArgs a = linear_dx(N, K, D2, dUG, LUG, s->w_ig[l], dF, LF);
       set_zc(a, s, 2);
       RUN(run(a, ws, st));
     }
     // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]
     const bool first = (l == 0);
-    float* nxt = first ? g->d_x_in : base + lay.dUG + (l - 1) * N * D2 + D;  // layer l-1's dY slot
-    const int64_t ldn = first ? g->d_x_in_ld : D2;
+    float* nxt = first ? g->d_x_in : base + lay.dUG + (l - 1) * N * LUG + D;  // layer l-1's dY slot
+    const int64_t ldn = first ? g->d_x_in_ld : LUG;
     float* dst = s->use_pc ? base + lay.T0 : nxt;
     const int64_t ldd = s->use_pc ? D : ldn;
-    RUN(gather(s, dF + D, K, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, dF, K,
+    RUN(gather(s, dF + D, LF, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, dF, LF,
                s->mode_single ? nullptr : dY, ldy, st));
     if (s->use_pc) {
       const float* raw = first ? s->x_in : s->X[l];

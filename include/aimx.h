@@ -216,6 +216,10 @@ typedef struct AimxShellStack {
   float* workspace; size_t workspace_bytes;
   int32_t* counters; int64_t n_counters; /* as in AimxGemmArgs */
   int32_t precision; /* AIMX_PREC_*: of the stack's node-update GEMMs (weight gradients stay fp32) */
+  /* row strides (floats) of the F [N, D(h+1)] and UG [N, 2D] buffers and of their backward
+   * counterparts (0: dense, K and 2D). Rounded up to 4 floats they make every row 16-byte aligned, so
+   * the weight gradients over them take 16-byte loads at odd D (c4 / c5: D = 153 / 307) */
+  int64_t ld_f, ld_ug;
 } AimxShellStack;
 
 typedef struct AimxShellStackGrad {

@@ -1,11 +1,12 @@
 #!/bin/bash
-# round-5 working call (overwritten per call): skinny GEMM stages A/B
+# round-5 working call (overwritten per call): padded F / UG row strides (16-byte rows) — parity, then A/B
 export PYTHONDONTWRITEBYTECODE=1
-T="python3 -u -m pytest -x -v --timeout 120 --timeout-method thread"
+T="python3 -u -m pytest -x -v --timeout 200 --timeout-method thread"
+B="python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 30 --warmup 8"
 tools/gpu_steps.sh \
- "?200 r5i/skinny_tests.log $T tests/test_gpu_parity.py -k 'skinny or gemm or wgrad or linear'" \
- "200 r5i/head_ns4.log python3 tools/gemm_micro.py head" \
- "200 r5i/head_ns2.log env AIMX_SKINNY_NS=2 python3 tools/gemm_micro.py head" \
- "200 r5i/head_off.log env AIMX_SKINNY=0 python3 tools/gemm_micro.py head" \
- "300 r5i/c5_ns4.log python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 30 --warmup 8" \
- "300 r5i/c5_off.log env AIMX_SKINNY=0 python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 30 --warmup 8"
+ "400 r5l/parity.log $T tests/test_gpu_parity.py -k 'full_size or c4s or c5s or shell_layer or mlp or stack or case'" \
+ "300 r5l/c5_pad.log $B --config c5" \
+ "300 r5l/c5_dense.log env AIMX_STACK_PAD=0 $B --config c5" \
+ "300 r5l/c4_pad.log $B --config c4" \
+ "300 r5l/c4_dense.log env AIMX_STACK_PAD=0 $B --config c4" \
+ "300 r5l/c2_pad.log $B"

@@ -2,7 +2,7 @@
 (torch.mm -> hipBLASLt / rocBLAS, fp32) on the same dW = dY^T X problems, graph-timed.
 Problems per layer: dW_ig (2D x (h+1)D, the untrimmed input projection) and 4 x dW_mlp (D x D);
 bias columns excluded on the vendor side (a column sum, timed separately).
-usage: python tools/wgrad_lib_ab.py [c4|c5]"""
+usage: python tools/wgrad_lib_ab.py [c4|c5] [pad]   (pad: row strides rounded up to 4 floats, 16-byte rows)"""
 import ctypes
 import json
 import os
@@ -41,17 +41,19 @@ def main():
     dev = torch.device("cuda")
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c5"
     K, D, h = {"c4": (20480, 153, 3), "c5": (10240, 307, 6)}[cfg]
+    pad = len(sys.argv) > 2 and sys.argv[2] == "pad"
     groups = {"wig": [(2 * D, (h + 1) * D)] * 3, "mlp": [(D, D)] * 12}
     groups["all"] = groups["wig"] + groups["mlp"]
-    res = {"config": cfg, "K": K, "D": D, "hops": h}
+    res = {"config": cfg, "K": K, "D": D, "hops": h, "pad": pad}
     for name, shapes in groups.items():
         flops = sum(2 * M * N * K for M, N in shapes)
         ops, arr = [], (_lib.WgradProblem * len(shapes))()
         for i, (M, N) in enumerate(shapes):
-            dy, x = torch.randn(K, M, device=dev), torch.randn(K, N, device=dev)
+            lm, ln = (-(-M // 4) * 4, -(-N // 4) * 4) if pad else (M, N)
+            dy, x = torch.randn(K, lm, device=dev)[:, :M], torch.randn(K, ln, device=dev)[:, :N]
             dw, db = torch.empty(M, N, device=dev), torch.empty(M, device=dev)
             ops.append((dy, x, dw, db))
-            arr[i].dY, arr[i].ld_dy, arr[i].X, arr[i].ld_x = dy.data_ptr(), M, x.data_ptr(), N
+            arr[i].dY, arr[i].ld_dy, arr[i].X, arr[i].ld_x = dy.data_ptr(), lm, x.data_ptr(), ln
             arr[i].dW, arr[i].ld_dw, arr[i].col_out = dw.data_ptr(), N, db.data_ptr()
             arr[i].M, arr[i].N, arr[i].K = M, N, K
         n = len(shapes)
