@@ -99,6 +99,7 @@ class ShellStack(ctypes.Structure):
         ("out", c_ptr), ("out_ld", c_i64),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
         ("counters", c_ptr), ("n_counters", c_i64), ("precision", c_i32), ("ld_f", c_i64), ("ld_ug", c_i64),
+        ("ld_act", c_i64),
     ]
 
 

@@ -61,7 +61,7 @@ class _MPStack(torch.autograd.Function):
         dev = x_in.device
         n, d, h, nl, nm = spec["N"], spec["D"], spec["num_hops"], spec["num_layers"], spec["num_mlp"]
         k = d * (h + 1)
-        lf, lug = _stack_strides(d, k)
+        lf, lug, la = _stack_strides(d, k)
         x_in, x_ld = _rows(x_in)
         ar = Arena(dev)
         iF = [ar.add(n, lf) for _ in range(nl)]
@@ -69,8 +69,8 @@ class _MPStack(torch.autograd.Function):
         iUG = [ar.add(n, lug) for _ in range(nl)]
         iU = [ar.add(n, d) for _ in range(nl)]
         iV = [ar.add(n, d) for _ in range(nl * nm)]
-        iR = [ar.add(n, d) for _ in range(nl * nm)]
-        iA = [ar.add(n, d) if (j % nm) != nm - 1 else None for j in range(nl * nm)]
+        iR = [ar.add(n, la) for _ in range(nl * nm)]
+        iA = [ar.add(n, la) if (j % nm) != nm - 1 else None for j in range(nl * nm)]
         buf, views = ar.alloc()
         F = [views[i] for i in iF]
         X = [views[i] if i is not None else None for i in iX]
@@ -98,7 +98,7 @@ class _MPStack(torch.autograd.Function):
         s.N, s.D, s.num_hops, s.num_layers, s.num_mlp = n, d, h, nl, nm
         s.act, s.use_pc, s.training, s.mode_single = spec["act"], int(spec["use_pc"]), int(drop), int(spec["single"])
         s.precision = spec["prec"]
-        s.ld_f, s.ld_ug = lf, lug
+        s.ld_f, s.ld_ug, s.ld_act = lf, lug, la
         s.drop_p = float(spec["drop_p"]) if drop else 0.0
         s.drop_seed = ptr(drop_seed) if drop else None
         s.fwd_rowptr, s.fwd_col = ptr(plan.fwd.rowptr), ptr(plan.fwd.col)
@@ -123,7 +123,7 @@ class _MPStack(torch.autograd.Function):
         # inputs go through save_for_backward; only forward-internal buffers live on ctx
         ctx.save_for_backward(x_in, total_charges, drop_seed, *params)
         ctx.state = dict(buf=buf, M=M, F=F, X=X, UG=UG, U=U, V=V, R=R, A=A, x_ld=x_ld, ws=ws, drop=drop,
-                         packed=packed, w_ig=w_ig, b_ig=b_ig, lf=lf, lug=lug)
+                         packed=packed, w_ig=w_ig, b_ig=b_ig, lf=lf, lug=lug, la=la)
         return out
 
     @staticmethod
@@ -154,7 +154,7 @@ class _MPStack(torch.autograd.Function):
         s.N, s.D, s.num_hops, s.num_layers, s.num_mlp = n, d, h, nl, nm
         s.act, s.use_pc, s.training, s.mode_single = spec["act"], int(spec["use_pc"]), int(st["drop"]), int(spec["single"])
         s.precision = spec["prec"]
-        s.ld_f, s.ld_ug = st["lf"], st["lug"]
+        s.ld_f, s.ld_ug, s.ld_act = st["lf"], st["lug"], st["la"]
         s.drop_p = float(spec["drop_p"]) if st["drop"] else 0.0
         s.drop_seed = ptr(st["seed"]) if st["drop"] else None
         s.fwd_rowptr, s.fwd_col = ptr(plan.fwd.rowptr), ptr(plan.fwd.col)
@@ -205,12 +205,13 @@ _PAD = {}
 
 
 def _stack_strides(d, k):
-    """Row strides of the stack's F [N, K] and UG [N, 2D] buffers: rounded up to 4 floats, so every
-    row is 16-byte aligned and the weight gradients over them take 16-byte loads at odd D (c4 / c5:
-    D = 153 / 307; profiles/r05_wgrad_rows_ab.txt). AIMX_STACK_PAD=0: dense (A/B)."""
+    """Row strides of the stack's F [N, K], UG [N, 2D] and MLP activation (R, A) buffers: rounded up
+    to 4 floats, so every row is 16-byte aligned and the weight gradients over them take 16-byte loads
+    at odd D (c4 / c5: D = 153 / 307; profiles/r05_wgrad_rows_ab.txt). AIMX_STACK_PAD=0: dense (A/B)."""
+    r4 = lambda v: -(-v // 4) * 4  # noqa: E731
     if os.environ.get("AIMX_STACK_PAD", "1") == "0":
-        return k, 2 * d
-    return -(-k // 4) * 4, -(-(2 * d) // 4) * 4
+        return k, 2 * d, d
+    return r4(k), r4(2 * d), r4(d)
 
 
 def _ig_in_place(heads, d, k, blk):

@@ -159,6 +159,8 @@ inline int64_t stack_ld_f(const AimxShellStack* s) {
   return s->ld_f > 0 ? s->ld_f : s->D * (s->num_hops + 1);
 }
 inline int64_t stack_ld_ug(const AimxShellStack* s) { return s->ld_ug > 0 ? s->ld_ug : 2 * s->D; }
+// row stride of the MLP blocks' R / A activations and of their gradients dV / dA (ld_act; 0 = D)
+inline int64_t stack_ld_act(const AimxShellStack* s) { return s->ld_act > 0 ? s->ld_act : s->D; }
 size_t mlp_pack_floats(const AimxShellStack* s);
 int launch_mlp_pack(const AimxShellStack* s, bool bwd, float* dst, hipStream_t st);
 int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64_t ldx, float* out, int64_t ldo,

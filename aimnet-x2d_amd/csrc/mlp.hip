@@ -41,6 +41,7 @@ struct MlpFwd {
   const int64_t* seed;
   const float* ug;  // [N, 2D] (row stride ldug): a0 = act(u), g
   int64_t ldug;
+  int64_t lda;      // row stride of R and A (V, M: D)
   const float* x;   // outer residual (nullable), ld ldx
   int64_t ldx;
   const float* w1[8];
@@ -71,6 +72,7 @@ struct MlpBwd {
   float* dA[8];     // dA_k for k = 1..nm-1 (the gradient w.r.t. block k's input), index k - 1
   float* dug;       // [N, 2D] (row stride ldug): [du | dY]
   int64_t ldug;
+  int64_t lda;      // row stride of dV and dA (V, M, u: D)
   int32_t v4;       // fill with 16-byte loads (D, lddy and every weight / dy pointer 4-float aligned)
 };
 
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, in
             Hb[r * S + c] = a;
             if (g < N) {
               V[g * D + c] = v;
-              Rk[g * D + c] = a;
+              Rk[g * p.lda + c] = a;
             }
           }
         }
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_fwd(const MlpFwd p, in
               if (last)
                 p.out[g * p.ldo + c] = a;
               else
-                Ak[g * D + c] = a;
+                Ak[g * p.lda + c] = a;
             }
           }
         }
@@ -576,7 +578,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
             const int64_t g = r0 + r;
             const float dv = (g < N) ? acc[i] * mf[i] * act_grad(p.act, ag[i]) : 0.f;
             DV[r * S + c] = dv;
-            if (g < N) dVk[g * D + c] = dv;
+            if (g < N) dVk[g * p.lda + c] = dv;
           }
         }
       }
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(64 * kWMaxWaves) void k_mlpw_bwd(const MlpBwd p, in
             DA[r * S + c] = da;
             if (g < N) {
               if (k > 0)
-                dAk[g * D + c] = da;
+                dAk[g * p.lda + c] = da;
               else
                 p.dug[g * p.ldug + c] = da * act_grad(p.act, uu[i]);
             }
@@ -877,7 +879,8 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
       const int lr = lo & 15, lq = 4 * (lo >> 4);
       const uint32_t nd = (uint32_t)(N * D);
       if (w1) {  // v = a W1^T + b1 ; r = dropout(act(v))
-        const __amdgpu_buffer_rsrc_t rV = mlp_rsrc(pick8(p.V, k), 4u * nd), rR = mlp_rsrc(pick8(p.R, k), 4u * nd);
+        const __amdgpu_buffer_rsrc_t rV = mlp_rsrc(pick8(p.V, k), 4u * nd);
+        const __amdgpu_buffer_rsrc_t rR = mlp_rsrc(pick8(p.R, k), 4u * (uint32_t)(N * p.lda));
         const __amdgpu_buffer_rsrc_t rM = mlp_rsrc(pick8(p.M, k), p.drop ? nd : 0u);
         const uint32_t salt = (uint32_t)(p.salt0 + k);
 #pragma unroll
@@ -901,13 +904,13 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_fwd(const MlpFwd p, const
               }
               Hb[row * S + c] = a;
               bstore(rV, in ? 4u * o : kDrop, v);
-              bstore(rR, in ? 4u * o : kDrop, a);
+              bstore(rR, in ? 4u * ((uint32_t)gr * (uint32_t)p.lda + (uint32_t)c) : kDrop, a);
             }
           }
       } else {  // a_{k+1} = r W2^T + b2 + a_k (+ g + x after the last block)
-        const uint32_t ldo = last ? (uint32_t)p.ldo : (uint32_t)D;
+        const uint32_t ldo = last ? (uint32_t)p.ldo : (uint32_t)p.lda;
         const __amdgpu_buffer_rsrc_t rO = last ? mlp_rsrc(p.out, 4u * (uint32_t)((N - 1) * p.ldo + D))
-                                               : mlp_rsrc(pick8(p.A, k), 4u * nd);
+                                               : mlp_rsrc(pick8(p.A, k), 4u * (uint32_t)(N * p.lda));
         // the last block's residual operands g and x, a fragment's loads all issued before their
         // first use (one round trip per fragment). Loaded during the GEMM instead, they slowed its k
         // loop by more (queued ahead of the weight ring's loads, or stalling the MFMAs' issue in a
@@ -997,9 +1000,9 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
       // per fragment: the epilogue's operands (dV: v and the dropout mask; dA of block 0: u), every
       // load issued before the first use (one round trip per fragment, see k_mlps_fwd), then its
       // outputs
-      const uint32_t ldd = dv ? (uint32_t)D : k > 0 ? (uint32_t)D : (uint32_t)p.ldug;
-      const __amdgpu_buffer_rsrc_t rout = dv      ? mlp_rsrc(pick8(p.dV, k), 4u * nd)
-                                          : k > 0 ? mlp_rsrc(pick8(p.dA, k - 1), 4u * nd)
+      const uint32_t ldd = dv ? (uint32_t)p.lda : k > 0 ? (uint32_t)p.lda : (uint32_t)p.ldug;
+      const __amdgpu_buffer_rsrc_t rout = dv      ? mlp_rsrc(pick8(p.dV, k), 4u * (uint32_t)(N * p.lda))
+                                          : k > 0 ? mlp_rsrc(pick8(p.dA, k - 1), 4u * (uint32_t)(N * p.lda))
                                                   : mlp_rsrc(p.dug, 4u * (uint32_t)(N * p.ldug));
       const gfloat* V = (const gfloat*)(dv ? pick8(p.V, k) : p.u);
       const gu8* M = (dv && p.drop) ? (const gu8*)pick8(p.M, k) : (const gu8*)V;
@@ -1215,7 +1218,7 @@ bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision, int64_t l
 
 size_t mlp_pack_floats(const AimxShellStack* s) {
   if (!mlps_on(s->N, s->D, s->num_mlp, s->precision) ||
-      !mlp_extent_ok(s->N, s->D, std::max({stack_ld_f(s), stack_ld_ug(s), s->out_ld})))
+      !mlp_extent_ok(s->N, s->D, std::max({stack_ld_f(s), stack_ld_ug(s), stack_ld_act(s), s->out_ld})))
     return 0;
   return (size_t)(s->num_layers * 2 * s->num_mlp * mlps_image_floats(s->D));
 }
@@ -1260,6 +1263,7 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
   p.seed = s->drop_seed;
   p.ug = s->UG[l];
   p.ldug = stack_ld_ug(s);
+  p.lda = stack_ld_act(s);
   p.x = x_res;
   p.ldx = ldx;
   for (int64_t k = 0; k < nm; ++k) {
@@ -1319,6 +1323,7 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
   }
   p.dug = dug;
   p.ldug = stack_ld_ug(s);
+  p.lda = stack_ld_act(s);
   {
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     bool v4 = s->D % 4 == 0 && lddy % 4 == 0 && al(dy);

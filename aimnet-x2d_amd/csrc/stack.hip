@@ -181,8 +181,8 @@ void set_zc(AimxGemmArgs& a, const AimxShellStack* s, int dim) {
 
 bool valid(const AimxShellStack* s) {
   if (!s || s->N < 0 || s->D < 1 || s->num_hops < 1 || s->num_layers < 1 || s->num_mlp < 0) return false;
-  if (s->ld_f < 0 || s->ld_ug < 0 || (s->ld_f > 0 && s->ld_f < s->D * (s->num_hops + 1)) ||
-      (s->ld_ug > 0 && s->ld_ug < 2 * s->D))
+  if (s->ld_f < 0 || s->ld_ug < 0 || s->ld_act < 0 || (s->ld_f > 0 && s->ld_f < s->D * (s->num_hops + 1)) ||
+      (s->ld_ug > 0 && s->ld_ug < 2 * s->D) || (s->ld_act > 0 && s->ld_act < s->D))
     return false;
   if (s->mode_single && (s->num_layers != 1 || s->use_pc)) return false;
   if (s->use_pc && (s->D < 2 || !s->gptr || !s->gperm || !s->total_charges)) return false;
@@ -225,7 +225,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
   if (!valid(s)) return AIMX_EARG;
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
-  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s);  // F / UG row strides
+  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s), LA = stack_ld_act(s);  // F / UG / R, A row strides
   if (N == 0) return AIMX_OK;
   const size_t split = fwd_split_floats(s), npack = mlp_pack_floats(s);
   float* pack = nullptr;
@@ -273,7 +273,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
       AIMX_CHECK_LAUNCH();
       continue;
     }
-    if (mlp_fused_ok(N, D, nm, s->precision, std::max({LF, LUG, s->out_ld}))) {
+    if (mlp_fused_ok(N, D, nm, s->precision, std::max({LF, LUG, LA, s->out_ld}))) {
       float* dst;
       int64_t ldd;
       if (l == L - 1) {
@@ -292,9 +292,9 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
     for (int64_t k = 0; k < nm; ++k) {
       const int64_t idx = l * nm + k;
       const float* in = (k == 0) ? s->UG[l] : s->A[idx - 1];
-      const int64_t ldin = (k == 0) ? LUG : D;
+      const int64_t ldin = (k == 0) ? LUG : LA;
       {
-        AimxGemmArgs a = linear_fwd(N, D, D, in, ldin, s->w1[idx], s->R[idx], D);
+        AimxGemmArgs a = linear_fwd(N, D, D, in, ldin, s->w1[idx], s->R[idx], LA);
         a.bias = s->b1[idx];
         a.act = s->act;
         a.act_ncols = D;
@@ -315,7 +315,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
         int64_t ldd;
         if (!last) {
           dst = s->A[idx];
-          ldd = D;
+          ldd = LA;
         } else if (l == L - 1) {
           dst = s->out;
           ldd = s->out_ld;
@@ -326,7 +326,7 @@ extern "C" int aimx_shell_stack_forward(const AimxShellStack* s, aimx_stream_t s
           dst = s->F[l + 1];
           ldd = LF;
         }
-        AimxGemmArgs a = linear_fwd(N, D, D, s->R[idx], D, s->w2[idx], dst, ldd);
+        AimxGemmArgs a = linear_fwd(N, D, D, s->R[idx], LA, s->w2[idx], dst, ldd);
         a.bias = s->b2[idx];
         a.res[0] = in;  // per-block skip (layers.py:103)
         a.ldres[0] = ldin;
@@ -363,23 +363,23 @@ int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, c
                          AimxWgradProblem* out) {
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
-  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s);
+  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s), LA = stack_ld_act(s);
   int n = 0;
   for (int64_t l = L - 1; l >= 0; --l) {
     const float* dYl = nullptr;
     int64_t ldy = D;
-    if (base) {  // below the top layer, dY lives in the upper half of the layer's dUG (see backward)
-      dYl = (l == L - 1) ? g->d_out : base + L_->dUG + l * N * LUG + D;
-      ldy = (l == L - 1) ? g->d_out_ld : LUG;
+    if (base) {  // below the top layer, dY is the hop backward's output (its own 16-byte rows)
+      dYl = (l == L - 1) ? g->d_out : base + L_->dY + l * N * LA;
+      ldy = (l == L - 1) ? g->d_out_ld : LA;
     }
     for (int64_t k = nm - 1; k >= 0; --k) {
       const int64_t idx = l * nm + k;
-      const float* da = (k == nm - 1) ? dYl : (base ? base + L_->dA + (l * (nm - 1) + k) * N * D : nullptr);
-      const int64_t lda = (k == nm - 1) ? ldy : D;
-      AimxWgradProblem w2 = {da, lda, base ? s->R[idx] : nullptr, D, g ? g->d_w2[idx] : nullptr, D,
+      const float* da = (k == nm - 1) ? dYl : (base ? base + L_->dA + (l * (nm - 1) + k) * N * LA : nullptr);
+      const int64_t lda = (k == nm - 1) ? ldy : LA;
+      AimxWgradProblem w2 = {da, lda, base ? s->R[idx] : nullptr, LA, g ? g->d_w2[idx] : nullptr, D,
                              g ? g->d_b2[idx] : nullptr, D, D, N};
       const float* in = base ? ((k == 0) ? s->UG[l] : s->A[idx - 1]) : nullptr;
-      AimxWgradProblem w1 = {base ? base + L_->dV + idx * N * D : nullptr, D, in, (k == 0) ? LUG : D,
+      AimxWgradProblem w1 = {base ? base + L_->dV + idx * N * LA : nullptr, LA, in, (k == 0) ? LUG : LA,
                              g ? g->d_w1[idx] : nullptr, D, g ? g->d_b1[idx] : nullptr, D, D, N};
       out[n++] = w2;
       out[n++] = w1;
@@ -406,9 +406,9 @@ BwdLayout bwd_layout(const AimxShellStack* s) {
   int64_t o = 0;
   b.dF = o, o += al64(N * stack_ld_f(s));
   b.dUG = o, o += al64(L * N * stack_ld_ug(s));
-  b.dV = o, o += al64(L * nm * N * D);
-  b.dA = o, o += al64(std::max<int64_t>(b.nA, 1) * N * D);
-  b.dY = o, o += al64(std::max<int64_t>(b.nY, 1) * N * D);
+  b.dV = o, o += al64(L * nm * N * stack_ld_act(s));
+  b.dA = o, o += al64(std::max<int64_t>(b.nA, 1) * N * stack_ld_act(s));
+  b.dY = o, o += al64(std::max<int64_t>(b.nY, 1) * N * stack_ld_act(s));  // dY of layers 0..L-2
   b.T0 = o, o += al64(N * D);
   b.pk = o, o += al64((int64_t)mlp_pack_floats(s));
   b.wg = o;
@@ -434,7 +434,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   if (!valid(s) || !g) return AIMX_EARG;
   const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
   const int64_t K = D * (h + 1), D2 = 2 * D;
-  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s);
+  const int64_t LF = stack_ld_f(s), LUG = stack_ld_ug(s), LA = stack_ld_act(s);
   if (N == 0) return AIMX_OK;
   const BwdLayout lay = bwd_layout(s);
   if (!g->workspace || g->workspace_bytes < sizeof(float) * (size_t)lay.total) return AIMX_EARG;
@@ -462,13 +462,15 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     RUN(launch_mlp_pack(s, true, pack, st));
   }
   for (int64_t l = L - 1; l >= 0; --l) {
-    // dUG = [du | dg] with dg = dY: below the top layer the hop backward of layer l + 1 already
-    // wrote dY into dUG's upper half (ld 2D), so only the top layer copies its upstream gradient
+    // dUG = [du | dg] with dg = dY. dY: the upstream gradient (top layer) or the hop backward's
+    // output of layer l + 1, in a buffer of its own with 16-byte rows (the weight gradient of the
+    // last MLP block reads it with 16-byte loads; dUG's upper half starts at the odd offset D); the
+    // MLP chain copies it into dUG's upper half as it stages it
     float* dUG = base + lay.dUG + l * N * LUG;
-    const float* dY = (l == L - 1) ? g->d_out : dUG + D;
-    const int64_t ldy = (l == L - 1) ? g->d_out_ld : LUG;
+    const float* dY = (l == L - 1) ? g->d_out : base + lay.dY + l * N * LA;
+    const int64_t ldy = (l == L - 1) ? g->d_out_ld : LA;
     // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
-    const bool fused = nm > 0 && mlp_fused_ok(N, D, nm, s->precision, std::max({LF, LUG, s->out_ld, g->d_out_ld}));
+    const bool fused = nm > 0 && mlp_fused_ok(N, D, nm, s->precision, std::max({LF, LUG, LA, s->out_ld, g->d_out_ld}));
     if (nm == 0) {  // no blocks: dUG = [dY * act'(u) | dY]
       hipLaunchKernelGGL(k_nomlp_bwd, dim3((unsigned)nomlp_blocks(N, D)), dim3(256), 0, st, dY, ldy, s->U[l], s->act,
                          dUG, LUG, N, D, dY != dUG + D ? 1 : 0);
@@ -478,18 +480,18 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       float* dVs[8];
       float* dAs[8];
       for (int64_t k = 0; k < nm; ++k) {
-        dVs[k] = base + lay.dV + (l * nm + k) * N * D;
-        dAs[k] = (k < nm - 1) ? base + lay.dA + (l * (nm - 1) + k) * N * D : nullptr;
+        dVs[k] = base + lay.dV + (l * nm + k) * N * LA;
+        dAs[k] = (k < nm - 1) ? base + lay.dA + (l * (nm - 1) + k) * N * LA : nullptr;
       }
       RUN(launch_mlp_bwd(s, l, dY, ldy, dVs, dAs, dUG, pack, st));
     }
     for (int64_t k = nm - 1; k >= 0 && !fused; --k) {
       const int64_t idx = l * nm + k;
-      const float* da_out = (k == nm - 1) ? dY : base + lay.dA + (l * (nm - 1) + k) * N * D;
-      const int64_t ld_out = (k == nm - 1) ? ldy : D;
-      float* dV = base + lay.dV + idx * N * D;
+      const float* da_out = (k == nm - 1) ? dY : base + lay.dA + (l * (nm - 1) + k) * N * LA;
+      const int64_t ld_out = (k == nm - 1) ? ldy : LA;
+      float* dV = base + lay.dV + idx * N * LA;
       {  // dV = (da_out W2) * mask/(1-p) * act'(V)
-        AimxGemmArgs a = linear_dx(N, D, D, da_out, ld_out, s->w2[idx], dV, D);
+        AimxGemmArgs a = linear_dx(N, D, D, da_out, ld_out, s->w2[idx], dV, LA);
         if (drop) {
           a.drop_p = s->drop_p;
           a.mask_in = s->M[idx];
@@ -501,9 +503,9 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
         RUN(run(a, ws, st));
       }
       {  // da_in = da_out + dV W1 ; for k == 0 also * act'(u) -> du into dUG[:, :D]
-        float* dst = (k == 0) ? dUG : base + lay.dA + (l * (nm - 1) + k - 1) * N * D;
-        const int64_t ldd = (k == 0) ? LUG : D;
-        AimxGemmArgs a = linear_dx(N, D, D, dV, D, s->w1[idx], dst, ldd);
+        float* dst = (k == 0) ? dUG : base + lay.dA + (l * (nm - 1) + k - 1) * N * LA;
+        const int64_t ldd = (k == 0) ? LUG : LA;
+        AimxGemmArgs a = linear_dx(N, D, D, dV, LA, s->w1[idx], dst, ldd);
         a.res[0] = da_out;
         a.ldres[0] = ld_out;
         if (k == 0) {
@@ -531,8 +533,8 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     }
     // hop backward + chunk-0 gradient + outer residual: dx = dF[:, :D] + dY + sum_{e: src%N == j} dF_agg[target_e]
     const bool first = (l == 0);
-    float* nxt = first ? g->d_x_in : base + lay.dUG + (l - 1) * N * LUG + D;  // layer l-1's dY slot
-    const int64_t ldn = first ? g->d_x_in_ld : LUG;
+    float* nxt = first ? g->d_x_in : base + lay.dY + (l - 1) * N * LA;  // layer l-1's dY
+    const int64_t ldn = first ? g->d_x_in_ld : LA;
     float* dst = s->use_pc ? base + lay.T0 : nxt;
     const int64_t ldd = s->use_pc ? D : ldn;
     RUN(gather(s, dF + D, LF, N, D, D, s->bwd_rowptr, s->bwd_col, N, dst, ldd, 0, 0, dF, LF,

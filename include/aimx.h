@@ -220,6 +220,8 @@ typedef struct AimxShellStack {
    * counterparts (0: dense, K and 2D). Rounded up to 4 floats they make every row 16-byte aligned, so
    * the weight gradients over them take 16-byte loads at odd D (c4 / c5: D = 153 / 307) */
   int64_t ld_f, ld_ug;
+  /* row stride of the R [N, D] and A [N, D] buffers (and of the backward's dV / dA): 0 = D */
+  int64_t ld_act;
 } AimxShellStack;
 
 typedef struct AimxShellStackGrad {
