@@ -358,6 +358,14 @@ struct BwdLayout {
 
 int64_t al64(int64_t x) { return (x + 63) / 64 * 64; }
 
+// The top layer's upstream gradient as the stack reads it: an external view whose rows are not
+// 16-byte aligned (c5: the x_other columns of the concat's input gradient) is copied once into the
+// dY slot of layer L-1 (16-byte rows), so the weight gradient of its last MLP block does not force
+// the grouped launch onto its per-problem load path.
+bool top_dy_copied(const AimxShellStack* s, const AimxShellStackGrad* g) {
+  return stack_ld_act(s) % 4 == 0 && g->d_out && ((g->d_out_ld % 4) != 0 || ((uintptr_t)g->d_out & 15) != 0);
+}
+
 // one AimxWgradProblem per weight gradient of the stack, in launch order
 int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, const float* base, const BwdLayout* L_,
                          AimxWgradProblem* out) {
@@ -369,8 +377,9 @@ int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, c
     const float* dYl = nullptr;
     int64_t ldy = D;
     if (base) {  // below the top layer, dY is the hop backward's output (its own 16-byte rows)
-      dYl = (l == L - 1) ? g->d_out : base + L_->dY + l * N * LA;
-      ldy = (l == L - 1) ? g->d_out_ld : LA;
+      const bool ext = l == L - 1 && !top_dy_copied(s, g);
+      dYl = ext ? g->d_out : base + L_->dY + l * N * LA;
+      ldy = ext ? g->d_out_ld : LA;
     }
     for (int64_t k = nm - 1; k >= 0; --k) {
       const int64_t idx = l * nm + k;
@@ -402,13 +411,13 @@ BwdLayout bwd_layout(const AimxShellStack* s) {
   const int64_t K = D * (h + 1);
   BwdLayout b;
   b.nA = L * (nm - 1);
-  b.nY = std::max<int64_t>(L - 1, 0);
+  b.nY = L;  // layers 0..L-2: the hop backward's output; L-1: top_dy's aligned copy
   int64_t o = 0;
   b.dF = o, o += al64(N * stack_ld_f(s));
   b.dUG = o, o += al64(L * N * stack_ld_ug(s));
   b.dV = o, o += al64(L * nm * N * stack_ld_act(s));
   b.dA = o, o += al64(std::max<int64_t>(b.nA, 1) * N * stack_ld_act(s));
-  b.dY = o, o += al64(std::max<int64_t>(b.nY, 1) * N * stack_ld_act(s));  // dY of layers 0..L-2
+  b.dY = o, o += al64(std::max<int64_t>(b.nY, 1) * N * stack_ld_act(s));
   b.T0 = o, o += al64(N * D);
   b.pk = o, o += al64((int64_t)mlp_pack_floats(s));
   b.wg = o;
@@ -461,14 +470,16 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     pack = base + lay.pk;
     RUN(launch_mlp_pack(s, true, pack, st));
   }
+  if (top_dy_copied(s, g)) RUN(copy2d(g->d_out, g->d_out_ld, base + lay.dY + (L - 1) * N * LA, LA, N, D, st));
   for (int64_t l = L - 1; l >= 0; --l) {
     // dUG = [du | dg] with dg = dY. dY: the upstream gradient (top layer) or the hop backward's
     // output of layer l + 1, in a buffer of its own with 16-byte rows (the weight gradient of the
     // last MLP block reads it with 16-byte loads; dUG's upper half starts at the odd offset D); the
     // MLP chain copies it into dUG's upper half as it stages it
     float* dUG = base + lay.dUG + l * N * LUG;
-    const float* dY = (l == L - 1) ? g->d_out : base + lay.dY + l * N * LA;
-    const int64_t ldy = (l == L - 1) ? g->d_out_ld : LA;
+    const bool ext = l == L - 1 && !top_dy_copied(s, g);
+    const float* dY = ext ? g->d_out : base + lay.dY + l * N * LA;
+    const int64_t ldy = ext ? g->d_out_ld : LA;
     // MLP blocks, last to first: only the activation-gradient chain here (weights deferred)
     const bool fused = nm > 0 && mlp_fused_ok(N, D, nm, s->precision, std::max({LF, LUG, LA, s->out_ld, g->d_out_ld}));
     if (nm == 0) {  // no blocks: dUG = [dY * act'(u) | dY]
