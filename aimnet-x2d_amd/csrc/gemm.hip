@@ -1710,9 +1710,16 @@ Plan plan_gemm(const AimxGemmArgs& a, bool allow_skinny = true) {
       p.bn = fn;
     }
   }
+  // Few rows, deep K (c5's post-pool F = 1024 chain, 258 x 1024 x 1024, 16 launches per step): 32 x 32
+  // tiles split to ~1700 workgroups beat 64 x 32 split 4 (forward 15.8 -> 13.6 us, input gradient
+  // 16.4 -> 14.1 us; the 3 x 8 tile / split sweep in profiles/r05_head_gemm_sweep.txt)
+  const bool deep_few = getenv("AIMX_GEMM_TILE") == nullptr && tiles(64, 32) < 256 && a.K >= 1024 && a.M <= 1024;
+  if (deep_few) p.bm = p.bn = 32;
   const int64_t t = tiles(p.bm, p.bn);
   int64_t splits = a.splits;
-  if (splits <= 0) {
+  if (splits <= 0 && deep_few) {
+    splits = std::max<int64_t>(1, std::min<int64_t>((1728 + t / 2) / t, a.K / (4 * kBK)));
+  } else if (splits <= 0) {
     splits = 1;
     // Split K only for grids short of one block per CU with a long K (weight gradients: K =
     // atoms; c5's head GEMMs: 264 x 1024 x 1024 ran as 160 64 x 32 blocks of 32 BK steps each, ~35

@@ -667,25 +667,27 @@ struct SGeom {
 };
 
 struct MlpPack {
-  const float* w[32];
+  const float* w[32];           // layer-major: layer l's matrices at [l * nmat, (l + 1) * nmat)
   int32_t nmat, D, CF, G, tr;  // tr: image of W^T (backward: B(k, n) = W[k][n])
-  floatx4* dst;                 // one layer's block: CF * nmat * G * 64 float4s
+  int32_t nl;                   // layers packed by this launch
+  floatx4* dst;                 // the layers' blocks, consecutive: CF * nmat * G * 64 float4s each
 };
 
 __global__ void k_mlps_pack(const MlpPack p) {
   // images of one layer: [f][phase][g][lane] (BStream); p.nmat = 2 nm phases of one layer
-  const int64_t total = (int64_t)p.CF * p.nmat * p.G * 64;
+  const int64_t per = (int64_t)p.CF * p.nmat * p.G * 64, total = per * p.nl;
   __shared__ const float* tab[32];
   if (threadIdx.x < 32) tab[threadIdx.x] = p.w[threadIdx.x];
   __syncthreads();
   for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < total; u += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(u & 63);
-    const int64_t q = u >> 6;
+    const int64_t l = u / per, uv = u - l * per;
+    const int lane = (int)(uv & 63);
+    const int64_t q = uv >> 6;
     const int g = (int)(q % p.G);
     const int m = (int)((q / p.G) % p.nmat);
     const int f = (int)(q / ((int64_t)p.G * p.nmat));
     const int n = 16 * f + (lane & 15), k0 = 16 * g + 4 * (lane >> 4);
-    const float* W = tab[m];
+    const float* W = tab[l * p.nmat + m];
     floatx4 v;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1225,24 +1227,30 @@ size_t mlp_pack_floats(const AimxShellStack* s) {
 
 // Every layer's MLP weights as MFMA-fragment images (k_mlps_pack), in the order the chain reads
 // them: forward W1_0, W2_0, W1_1, ... per layer; backward (transposed) W2_{nm-1}, W1_{nm-1}, ..., W1_0.
+// As many layers per launch as their 2 nm matrices fit the 32-entry table (c4 / c5: all 3 layers in
+// one launch instead of one per layer: 3 x 4.7 us -> one).
 int launch_mlp_pack(const AimxShellStack* s, bool bwd, float* dst, hipStream_t st) {
   const int64_t nm = s->num_mlp, L = s->num_layers, D = s->D;
   const MlpsPlan pl = mlps_plan(1, D);
   const int64_t per = 2 * nm * mlps_image_floats(D) / 4;  // float4s per layer block
-  for (int64_t l = 0; l < L; ++l) {
+  const int64_t lpl = std::max<int64_t>(1, 32 / (2 * nm));  // layers per launch
+  for (int64_t l0 = 0; l0 < L; l0 += lpl) {
+    const int64_t nl = std::min(lpl, L - l0);
     MlpPack p{};
     p.nmat = (int32_t)(2 * nm);
-    for (int64_t j = 0; j < 2 * nm; ++j) {
-      const int64_t k = bwd ? nm - 1 - (j >> 1) : (j >> 1);
-      const bool w2 = bwd ? (j & 1) == 0 : (j & 1) == 1;
-      p.w[j] = w2 ? s->w2[l * nm + k] : s->w1[l * nm + k];
-    }
+    for (int64_t l = l0; l < l0 + nl; ++l)
+      for (int64_t j = 0; j < 2 * nm; ++j) {
+        const int64_t k = bwd ? nm - 1 - (j >> 1) : (j >> 1);
+        const bool w2 = bwd ? (j & 1) == 0 : (j & 1) == 1;
+        p.w[(l - l0) * 2 * nm + j] = w2 ? s->w2[l * nm + k] : s->w1[l * nm + k];
+      }
     p.D = (int32_t)D;
     p.CF = pl.geo.CF;
     p.G = pl.geo.G;
     p.tr = bwd ? 1 : 0;
-    p.dst = reinterpret_cast<floatx4*>(dst) + l * per;
-    const int64_t blocks = std::min<int64_t>(cdiv(per, 256), 2048);
+    p.nl = (int32_t)nl;
+    p.dst = reinterpret_cast<floatx4*>(dst) + l0 * per;
+    const int64_t blocks = std::min<int64_t>(cdiv(per * nl, 256), 4096);
     hipLaunchKernelGGL(k_mlps_pack, dim3((unsigned)blocks), dim3(256), 0, st, p);
     AIMX_CHECK_LAUNCH();
   }

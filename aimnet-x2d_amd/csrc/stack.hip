@@ -91,19 +91,18 @@ AimxGemmArgs linear_dw(int64_t rows, int64_t in, int64_t out, const float* dY, i
 
 // Strided 2-D copy as a kernel: dst[r*ldd + c] = src[r*lds + c]. (hipMemcpy2DAsync D2D nodes
 // crashed the HIP runtime at stream-capture end on ROCm 7.2; a kernel node is also cheaper.)
+// Rows go to workgroups (grid-stride), columns to threads: no per-element division (the flat-index
+// form spent most of its 9.3 us on 64-bit div/mod at c5's 10 k x 307).
 __global__ void k_copy2d(const float* __restrict__ src, int64_t lds, float* __restrict__ dst, int64_t ldd,
                          int64_t rows, int64_t cols) {
-  const int64_t total = rows * cols;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / cols, c = i - r * cols;
-    dst[r * ldd + c] = src[r * lds + c];
-  }
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
+    for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) dst[r * ldd + c] = src[r * lds + c];
 }
 
 int copy2d(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int64_t cols, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return AIMX_OK;
-  const int64_t blocks = std::min<int64_t>(cdiv(rows * cols, 256), 4096);
-  hipLaunchKernelGGL(k_copy2d, dim3((unsigned)blocks), dim3(256), 0, s, src, lds, dst, ldd, rows, cols);
+  const int64_t blocks = std::min<int64_t>(rows, 8192);
+  hipLaunchKernelGGL(k_copy2d, dim3((unsigned)blocks), dim3(cols > 128 ? 256 : 128), 0, s, src, lds, dst, ldd, rows, cols);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
