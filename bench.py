@@ -326,12 +326,13 @@ def cold_time_us(fn, device, launches=20, flush_mb=512):
 def hop_in_step(batch, hops, hidden, device):
     """The hop forward and backward exactly as one train step's stack runs them per layer
     (stack.hip), at the config's own batch, through the C ABI, cold MALL (cold_time_us):
-      forward : src F[:, :D] (row stride K = D (h+1)), output written into F's columns
+      forward : src F[:, :D] (row stride LF = K = D (h+1) rounded up to 4 floats, as
+                aimx.ops._stack_strides lays the stack out), output written into F's columns
                 [D, K) (hop chunk j at column offset D + j D);
       backward: the gathered rows dF[:, D:] at the targets (every target is < N for reference
                 inputs, layers.py:154, so chunk 0 only), plus the chunk-0 gradient dF[:, :D] and
-                the outer residual dY (row stride 2 D) added, written into the next-lower layer's
-                dUG slot (row stride 2 D).
+                the outer residual dY (row stride LA = D rounded up to 4) added, written into the
+                next-lower layer's dY buffer (row stride LA).
     Algorithmic bytes: fwd 4 [N D + E + (h N + 1) + w N D], w = the chunks the step writes (the
     stack skips the trailing edge-less ones, which its GEMMs trim: chunk 0 only for reference inputs);
     bwd 4 [N D (gathered rows) + E + (N + 1) + 2 N D (the residual reads) + N D (written)]."""
@@ -339,28 +340,29 @@ def hop_in_step(batch, hops, hidden, device):
     from aimx.plan import GraphPlan
     lib = _lib.load()
     P = _lib.ptr
+    from aimx import ops
     n, d = batch.num_atoms, int(0.3 * hidden)
     K = d * (hops + 1)
+    LF, _, LA = ops._stack_strides(d, K)
     plan = GraphPlan(n, hops, edges=batch.edges, batch=batch.batch, num_graphs=batch.num_graphs)
     e = plan.E
-    F = torch.randn(n, K, device=device)
-    dF = torch.randn(n, K, device=device)
-    dUG = torch.randn(n, 2 * d, device=device)   # dY in the upper half (row stride 2 D)
-    nxt = torch.empty(n, 2 * d, device=device)  # the next-lower layer's dUG slot
+    F = torch.randn(n, LF, device=device)
+    dF = torch.randn(n, LF, device=device)
+    dY = torch.randn(n, LA, device=device)    # the layer's upstream gradient (the outer residual)
+    nxt = torch.empty(n, LA, device=device)  # the next-lower layer's dY buffer
     seg, seg_st = plan.row_seg()
     s = _lib.stream_ptr(device)
     fl = 4  # bytes per float: column offsets as pointer arithmetic
     kern = "k_gather_sum" if d % 4 == 0 else "k_gather_rows"
 
     def fwd():  # the stack's call: trailing edge-less chunks not written (AIMX_GATHER_SKIP_TAIL)
-        assert lib.aimx_segment_gather_sum_ex(P(F), K, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n,
-                                              P(F) + fl * d, K, n, d, None, 0, None, 0, seg, seg_st,
+        assert lib.aimx_segment_gather_sum_ex(P(F), LF, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n,
+                                              P(F) + fl * d, LF, n, d, None, 0, None, 0, seg, seg_st,
                                               _lib.GATHER_SKIP_TAIL, s) == 0
 
     def bwd():
-        assert lib.aimx_segment_gather_sum(P(dF) + fl * d, K, n, d, d, P(plan.bwd.rowptr), P(plan.bwd.col), n,
-                                           P(nxt) + fl * d, 2 * d, 0, 0, P(dF), K, P(dUG) + fl * d, 2 * d,
-                                           seg, seg_st, s) == 0
+        assert lib.aimx_segment_gather_sum(P(dF) + fl * d, LF, n, d, d, P(plan.bwd.rowptr), P(plan.bwd.col), n,
+                                           P(nxt), LA, 0, 0, P(dF), LF, P(dY), LA, seg, seg_st, s) == 0
     # chunks the step writes: up to the last one holding an edge (reference inputs: chunk 0 only)
     rp = plan.fwd.rowptr.cpu()
     written = max([k + 1 for k in range(hops) if int(rp[(k + 1) * n]) > int(rp[k * n])], default=0)
@@ -368,7 +370,8 @@ def hop_in_step(batch, hops, hidden, device):
     tf, tb = cold_time_us(fwd, device), cold_time_us(bwd, device)
     bf = 4 * (n * d + e + (hops * n + 1) + written * n * d)
     bb = 4 * (n * d + e + (n + 1) + 2 * n * d + n * d)
-    note = "the stack's own layout (F column offset D, residual adds), cold MALL (512 MiB flush per launch)"
+    note = (f"the stack's own layout (F row stride {LF}, chunk column offset D; dY / output row stride {LA}; "
+            "residual adds), cold MALL (512 MiB flush per launch)")
     return {"atoms": n, "edges": e, "D": d, "hops": hops, "chunks_written": written,
             "fwd": _bw(kern + " (hop fwd, in-step layout)", bf, tf, timing=note),
             "bwd": _bw(kern + " (hop bwd + residual adds, in-step layout)", bb, tb, timing=note)}

@@ -1,10 +1,9 @@
 #!/bin/bash
-# round-5 working call (overwritten per call): head tiles 32x32, one MLP pack launch per direction, row copy
+# round-5 working call (overwritten per call): whole GPU suite, smoke, default bench line, c4/c5 lines
 export PYTHONDONTWRITEBYTECODE=1
-T="python3 -u -m pytest -x -v --timeout 200 --timeout-method thread"
-B="python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 30 --warmup 8"
 tools/gpu_steps.sh \
- "400 r5q/parity.log $T tests/test_gpu_parity.py -k 'full_size or c4s or c5s or shell_layer or stack or case or gemm or head'" \
- "300 r5q/c5.log $B --config c5" \
- "300 r5q/c4.log $B --config c4" \
- "300 r5q/c2.log $B"
+ "?900 r5r/tests.log python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread" \
+ "300 r5r/smoke.log python3 -c 'import __graft_entry__ as g; g.smoke()'" \
+ "600 r5r/bench_plain.log python3 bench.py" \
+ "300 r5r/bench_c4.log python3 bench.py --config c4 --no-cpu-baseline" \
+ "300 r5r/bench_c5.log python3 bench.py --config c5 --no-cpu-baseline"
