@@ -1,9 +1,6 @@
 #!/bin/bash
-# round-5 working call (overwritten per call): whole GPU suite, smoke, default bench line, c4/c5 lines
+# round-5 working call (overwritten per call): c4 HDF5 stream line (1 M-molecule file), c2 native feed line
 export PYTHONDONTWRITEBYTECODE=1
 tools/gpu_steps.sh \
- "?900 r5r/tests.log python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread" \
- "300 r5r/smoke.log python3 -c 'import __graft_entry__ as g; g.smoke()'" \
- "600 r5r/bench_plain.log python3 bench.py" \
- "300 r5r/bench_c4.log python3 bench.py --config c4 --no-cpu-baseline" \
- "300 r5r/bench_c5.log python3 bench.py --config c5 --no-cpu-baseline"
+ "600 r5s/c4_stream.log python3 bench.py --config c4 --feed stream --stream-mols 1000000 --steps 400 --warmup 20 --no-cpu-baseline --no-roofline --no-eager" \
+ "300 r5s/c2_native.log python3 bench.py --feed native --steps 200 --warmup 20 --no-cpu-baseline --no-roofline --no-eager"
