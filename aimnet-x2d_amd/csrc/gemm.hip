@@ -1669,7 +1669,14 @@ Plan plan_gemm(const AimxGemmArgs& a, bool allow_skinny = true) {
     p.wgrad = true;
     p.bm = p.bn = 32;
     const int64_t t = cdiv(a.M, 32) * cdiv(a.N, 32);
-    int64_t splits = a.splits > 0 ? a.splits : cdiv(384, t);
+    // ~1150 workgroups (round 5, c2's 256 x 257 x 9170 concat dW: 6 splits 32.7 us, 16 splits
+    // 27.1 us; the 76 x 77 ones 17.8 -> 15.9 us; profiles/r05_lone_wgrad_splits.txt); AIMX_WGRAD_WGS
+    // overrides the target (A/B)
+    static const int64_t target = [] {
+      const char* e = getenv("AIMX_WGRAD_WGS");
+      return e ? std::max(64, atoi(e)) : 1152;
+    }();
+    int64_t splits = a.splits > 0 ? a.splits : cdiv(target, t);
     splits = std::max<int64_t>(1, std::min<int64_t>({splits, 64, a.K / 256}));
     p.kchunk = cdiv(cdiv(a.K, splits), 16) * 16;
     p.splits = (int)std::max<int64_t>(1, cdiv(a.K, p.kchunk));

@@ -15,6 +15,7 @@ starts = [i for i, r in enumerate(tr) if "k_embed_gather" in r["Kernel_Name"]]
 a, b = starts[-3], starts[-2]
 prev = None
 tot = 0.0
+t_first = int(tr[a]["Start_Timestamp"])
 for r in tr[a:b]:
     n = r["Kernel_Name"].replace("void ", "").replace("aimx::(anonymous namespace)::", "")
     if n.startswith("at::native::"):  # keep the kernel and its functor, drop the template noise
@@ -27,5 +28,5 @@ for r in tr[a:b]:
     prev = e
     wgs = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]) // max(1, int(r["Workgroup_Size_X"]))
     tot += (e - s) / 1e3
-    print(f"{(e - s) / 1e3:7.1f} gap {gap:5.1f} wgs {wgs:7d}  {n}")
+    print(f"{(e - s) / 1e3:7.1f} gap {gap:5.1f} at {(s - t_first) / 1e3:7.1f} wgs {wgs:7d}  {n}")
 print(f"{b - a} kernels, {tot:.1f} us busy, span {(int(tr[b - 1]['End_Timestamp']) - int(tr[a]['Start_Timestamp'])) / 1e3:.1f} us")
