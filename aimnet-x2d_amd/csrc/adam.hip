@@ -1,4 +1,4 @@
-// Fused global-norm gradient clipping + Adam over a list of tensors (three launches per step).
+// Fused global-norm gradient clipping + Adam over a list of tensors (two launches per step).
 //
 // Reference: the trainer's step, src/training/trainer.py:163-164
 //   torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0); optimizer.step()
@@ -7,15 +7,15 @@
 // 3-5 us launches per step for this model. Here:
 //   1. k_adam_sumsq   : per-(tensor, slice) partial sums of g^2 (fp64)  -> workspace
 // (each tensor's own step counter, torch.optim.Adam's per-parameter state['step'], is advanced by
-// the first workgroup of that tensor in launch 1 and read by launch 3 for its bias corrections:
+// the first workgroup of that tensor in launch 1 and read by launch 2 for its bias corrections:
 // a parameter without a gradient in a step keeps its count, as in torch)
-//   2. k_adam_fold    : one workgroup folds the partials in a fixed order: total norm, clip
-//                       coefficient (no arrival atomics: deterministic, no serialised tail)
-//   3. k_adam_update  : g *= coef (in place, as clip_grad_norm_ leaves it), [g += wd * p],
+//   2. k_adam_update  : every workgroup first folds the partials in one fixed order (total norm,
+//                       clip coefficient: deterministic, no arrival atomics, the same bits in every
+//                       workgroup), then g *= coef (in place, as clip_grad_norm_ leaves it), [g += wd * p],
 //                       m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
 //                       p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // The tensor table travels in the kernel arguments (chunks of kAdamChunk tensors), so nothing is
-// copied host->device and the three launches capture into a HIP graph as plain kernel nodes. The
+// copied host->device and the two launches capture into a HIP graph as plain kernel nodes. The
 // sum-of-squares slice (one workgroup) is 2048 elements or more, sized so a call makes about
 // kTargetSlices partials (c5's ~15M parameters: 16384-element slices, ~1,000 partials instead of
 // 7,284, each of which used to end in an atomic arrival on one counter: a serialised ~80 us tail);
@@ -55,15 +55,14 @@ __device__ __forceinline__ int find_tensor(const AdamTable& t, int b) {
   return i;
 }
 
-// Launch 2: the clip coefficient from every slice's partial sum of squares, by one workgroup:
-// thread t sums partials t, t + 256, ... in that order with 8 loads in flight, then the threads'
-// sums are combined in a fixed order. Deterministic: the same bits every call.
-// scal[0] = clip coefficient, scal[3] = total gradient norm (the value clip_grad_norm_ returns)
-__global__ __launch_bounds__(kAdamThreads) void k_adam_fold(const double* __restrict__ partial, int64_t n_partial,
-                                                            float max_norm, float* __restrict__ scal,
-                                                            float* __restrict__ norm_out) {
+// The clip coefficient from every slice's partial sum of squares, by one workgroup: thread t sums
+// partials t, t + 256, ... in that order with 8 loads in flight, then the threads' sums are
+// combined in a fixed order. Deterministic: the same bits every call and in every workgroup that
+// runs it — the update's workgroups each fold the partials themselves (round 5: one launch fewer
+// per step; the partials are ~0.5-1k doubles, L2-resident). Returns (coef, total norm).
+__device__ __forceinline__ float2 fold_partials(const double* __restrict__ partial, int64_t n_partial, float max_norm,
+                                                double* red) {
   constexpr int kInFlight = 8;
-  __shared__ double red[kAdamThreads / kWave];
   double s = 0.0;
   for (int64_t j0 = threadIdx.x; j0 < n_partial; j0 += (int64_t)kInFlight * kAdamThreads) {
     double v[kInFlight];
@@ -79,16 +78,12 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_fold(const double* __rest
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < kAdamThreads / kWave; ++w) t += red[w];
-    const float total = (float)sqrt(t);
-    float coef = 1.f;
-    if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
-    scal[0] = coef;
-    scal[3] = total;
-    if (norm_out) *norm_out = total;
-  }
+  double t = 0.0;
+  for (int w = 0; w < kAdamThreads / kWave; ++w) t += red[w];
+  const float total = (float)sqrt(t);
+  float coef = 1.f;
+  if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
+  return make_float2(coef, total);
 }
 
 // Launch 1: the partial sum of squares of each slice (fp64; the first workgroup of each tensor
@@ -130,12 +125,23 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_sumsq(const AdamTable t, 
   }
 }
 
-// Launch 3.
-__global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t, const float* __restrict__ scal,
+// Launch 2.
+// scal[0] = clip coefficient, scal[3] = total gradient norm (the value clip_grad_norm_ returns),
+// written by the first launch's workgroup 0
+__global__ __launch_bounds__(kAdamThreads) void k_adam_update(const AdamTable t, const double* __restrict__ partial,
+                                                              int64_t n_partial, float max_norm, float* __restrict__ scal,
+                                                              float* __restrict__ norm_out, int32_t first,
                                                               int64_t slice, const float* __restrict__ steps,
                                                               const float* __restrict__ lr, float beta1, float omb1,
                                                               float beta2, float omb2, float eps, float wd) {
-  const float coef = scal[0];
+  __shared__ double red[kAdamThreads / kWave];
+  const float2 cn = fold_partials(partial, n_partial, max_norm, red);
+  const float coef = cn.x;
+  if (first && blockIdx.x == 0 && threadIdx.x == 0) {
+    scal[0] = coef;
+    scal[3] = cn.y;
+    if (norm_out) *norm_out = cn.y;
+  }
   const int i = find_tensor(t, blockIdx.x);
   const int64_t s0 = (int64_t)(blockIdx.x - t.blk0[i]) * slice;
   const int64_t s1 = min(t.numel[i], s0 + slice);
@@ -260,13 +266,11 @@ extern "C" int aimx_fused_adam(const AimxAdamTensor* tensors, int32_t n, const A
     return AIMX_OK;
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(k_adam_fold, dim3(1), dim3(kAdamThreads), 0, s, (const double*)partial, total_blocks,
-                     h->max_grad_norm, scal, norm_out);
-  AIMX_CHECK_LAUNCH();
-  return for_chunks(kSliceElems, [&](const AdamTable& t, int32_t nb, int64_t) -> int {
-    hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const float*)scal,
-                       kSliceElems, (const float*)step, lr, h->beta1, h->one_minus_beta1, h->beta2,
-                       h->one_minus_beta2, h->eps, h->weight_decay);
+  return for_chunks(kSliceElems, [&](const AdamTable& t, int32_t nb, int64_t blk) -> int {
+    hipLaunchKernelGGL(k_adam_update, dim3((unsigned)nb), dim3(kAdamThreads), 0, s, t, (const double*)partial,
+                       total_blocks, h->max_grad_norm, scal, norm_out, blk == 0 ? 1 : 0, kSliceElems,
+                       (const float*)step, lr, h->beta1, h->one_minus_beta1, h->beta2, h->one_minus_beta2, h->eps,
+                       h->weight_decay);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
   });

@@ -1,11 +1,9 @@
 #!/bin/bash
-# round-5 working call (overwritten per call): lone weight-gradient split target A/B on the c2 step
+# round-5 working call (overwritten per call): Adam with the clip fold inside the update
 export PYTHONDONTWRITEBYTECODE=1
+T="python3 -u -m pytest -x -q --timeout 200 --timeout-method thread"
 B="python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 200 --warmup 20"
 tools/gpu_steps.sh \
- "300 r5v/c2_1152.log $B" \
- "300 r5v/c2_384.log env AIMX_WGRAD_WGS=384 $B" \
- "300 r5v/c2_768.log env AIMX_WGRAD_WGS=768 $B" \
- "300 r5v/c2_2048.log env AIMX_WGRAD_WGS=2048 $B" \
- "300 r5v/c4_1152.log $B --config c4" \
- "300 r5v/c4_384.log env AIMX_WGRAD_WGS=384 $B --config c4"
+ "400 r5w/tests.log $T tests/test_gpu_train.py tests/test_gpu_autograph.py tests/test_gpu_parity.py -k 'adam or trajectory or clip or train or graph'" \
+ "300 r5w/c2.log $B" \
+ "300 r5w/c5.log $B --config c5"
