@@ -548,6 +548,9 @@ int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_
                                                           out_ld, out_rpc, out_cs, add0, add0_ld, add1, add1_ld,
                                                           row_seg, row_seg_stride, stream, skip_tail) == AIMX_OK)
       return AIMX_OK;
+    if (gather_unal_on())
+      return launch_gather_unal(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs,
+                                add0, add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream, skip_tail);
     return launch_gather_rows(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
                               add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream, skip_tail);
   }

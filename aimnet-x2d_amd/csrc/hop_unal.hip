@@ -1,0 +1,836 @@
+// The hop for rows that are not runs of 16-byte-ALIGNED vectors (odd widths D = int(0.3 * hidden):
+// 153 / 307 at hidden 512 / 1024, reference src/models/gnn.py:100; hop chunks at column offset D of
+// the concatenated [x | chunk_0 | ...] matrix, layers.py:76-79), by 16-byte vectors at 4-byte-aligned
+// addresses. Same contract and bit-exact result as hop.hip / hop_rows.hip (the ordered edge-order sum
+// of CPU scatter_add_, layers.py:133-167).
+//
+// gfx950 executes global_load/store_dwordx4 at any 4-byte-aligned address (LLVM emits them for a
+// 4-byte-aligned 16-byte struct on this target; tools/micro/unal_copy.hip checks the copy bit for bit
+// and its rate). A row is then read and written as units of 4 columns [4g, 4g + 4) from the row's
+// own start, whatever its alignment: only the last unit of an odd-width row takes dword accesses.
+// In LDS the staged units sit 16-byte aligned, so the sum is ds_read_b128 throughout, and there is
+// no realignment tile (hop_rows.hip's column pass: stage -> sum -> shift through LDS -> store, four
+// barriers per 80-column pass run in sequence inside one workgroup).
+//
+// Work split, as hop.hip's: a workgroup owns a segment-aligned tile (the molecules that start in its
+// nominal window; sources are then the tile's own rows, staged by a speculative load issued together
+// with the col slice: two dependent global round trips per tile) and ONE column slice of it. The
+// slices of one tile are separate workgroups on one XCD (same L2 for the shared row pointers and col
+// slice, the only bytes read twice), so a wide row costs parallel workgroups, not sequential passes.
+// Hop chunks >= 1 (no edges for reference inputs) are big streaming tiles spread among the windows.
+#include <algorithm>
+#include <climits>
+#include <cstdlib>
+
+#include "aimx_common.h"
+#include "hop_common.h"
+
+namespace aimx {
+namespace {
+
+constexpr int kUT = 256;          // threads per workgroup
+constexpr int kUMaxTile = 64;     // nominal rows per tile (upper bound)
+constexpr int kUAlignWin = 64;    // a segment-aligned cut moves at most this many rows
+constexpr int kUMaxRows = kUMaxTile + kUAlignWin;
+constexpr int kUHead = 136;       // ints ahead of the col slice: row pointers [129] + misc [4], 16-byte multiple
+constexpr int kUMisc = 129;       // misc words: [0] lo / cut0, [1] hi / cut1, [2] spec lo, [3] spec hi
+constexpr int kUGroup = 4;        // LDS reads in flight per thread
+
+// Workgroup barrier for LDS hand-offs: waits for this wave's LDS operations only. __syncthreads()'s
+// fence also waits vmcnt(0), draining every global load in flight (the pipelined kernel's prefetch);
+// no thread here reads another thread's global writes, and an LDS store of loaded data already
+// waits for that load.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct __attribute__((packed, aligned(4))) F4u {
+  float x, y, z, w;
+};
+
+__device__ __forceinline__ float4 f4z() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ void f4acc(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+
+// Columns [c, c + 4) of a row of width D (c < D): one 16-byte load at the row's 4-byte alignment,
+// or dwords for the row's last, partial unit (never past the row's end).
+__device__ __forceinline__ float4 ld_unit(const float* row, uint32_t c, uint32_t D) {
+  if (c + 4 <= D) {
+    const F4u v = *reinterpret_cast<const F4u*>(row + c);
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  float4 v = f4z();
+  v.x = row[c];
+  if (c + 1 < D) v.y = row[c + 1];
+  if (c + 2 < D) v.z = row[c + 2];
+  return v;
+}
+// The 16 bytes of a row at columns [min(c, D - 4), +4) (D >= 4: always inside the row), as one load:
+// all four lanes are consumed unconditionally (put_unit), so the compiler neither splits nor
+// predicates it, and a batch of them stays in flight together.
+__device__ __forceinline__ float4 ld_raw(const float* row, uint32_t c, uint32_t D) {
+  const F4u v = *reinterpret_cast<const F4u*>(row + min(c, D - 4));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+// ld_raw's 16 bytes into a staged row d (slice column 0 at d[0]) at slice column min(c, D - 4) - 4 u0:
+// a full unit lands on its own 16 bytes; the last, partial unit of an odd-width row lands shifted
+// down, rewriting the same values over columns of the unit before it (identical bytes).
+__device__ __forceinline__ void put_raw(float* d, uint32_t c, uint32_t D, uint32_t u0, const float4& v) {
+  float* q = d + (min(c, D - 4) - 4 * u0);
+  q[0] = v.x;
+  q[1] = v.y;
+  q[2] = v.z;
+  q[3] = v.w;
+}
+__device__ __forceinline__ void st_unit(float* row, uint32_t c, uint32_t D, const float4& v) {
+  if (c + 4 <= D) {
+    *reinterpret_cast<F4u*>(row + c) = F4u{v.x, v.y, v.z, v.w};
+    return;
+  }
+  row[c] = v.x;
+  if (c + 1 < D) row[c + 1] = v.y;
+  if (c + 2 < D) row[c + 2] = v.z;
+}
+
+struct UnalArgs {
+  const float* src;
+  int64_t src_ld, src_cs;
+  FastDiv src_rpc;
+  const int32_t* rowptr;
+  const int32_t* col;
+  uint32_t D, upr;            // row width; units (4 columns) per row
+  uint32_t slices, cu;        // column slices per tile; units per slice (the last may be shorter)
+  uint32_t pitch, pitch_l2;   // staged row stride in units (a power of two, >= cu, a multiple of 16)
+  int32_t compact;            // thread t owns unit t % cs.d of row t / cs.d instead (row stride cu units)
+  FastDiv cu_full, cu_last;   // units of a full / the last slice
+  FastDiv upr_f;              // units of a whole row (big tiles)
+  uint32_t rows, split;       // tiles cover rows [0, split); big tiles rows [split, rows)
+  uint32_t tile_rows, ntiles, nsmall;
+  uint32_t big_rows, nbig;
+  uint32_t col_cap, xcap;     // staged col entries; staged rows (incl. the zero row) per workgroup
+  int32_t interleave, flat_zero, skip_tail;
+  float* out;
+  int64_t out_ld, out_cs;
+  FastDiv out_rpc;
+  const float* add0;
+  int64_t add0_ld;
+  const float* add1;
+  int64_t add1_ld;
+  const int64_t* seg;  // molecule id per row of [0, split) (optional)
+  int64_t seg_stride;
+};
+
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ const float* src_row(const UnalArgs& a, uint32_t q) {
+  if (!SRC_CHUNKED) return a.src + (int64_t)q * a.src_ld;
+  const uint32_t k = fdiv(q, a.src_rpc);
+  return a.src + (int64_t)(q - k * a.src_rpc.d) * a.src_ld + (int64_t)k * a.src_cs;
+}
+
+// The residual terms and the store of unit (row r, columns c..c+3): out = add0 + sum + add1 (the
+// order hop.hip uses).
+__device__ __forceinline__ void finish_unit(const UnalArgs& a, uint32_t r, uint32_t c, float4 acc) {
+  if (a.add0) {
+    float4 s = ld_unit(a.add0 + (int64_t)r * a.add0_ld, c, a.D);
+    f4acc(s, acc);
+    acc = s;
+  }
+  if (a.add1) f4acc(acc, ld_unit(a.add1 + (int64_t)r * a.add1_ld, c, a.D));
+  st_unit(a.out + row_off(r, a.out_ld, a.out_rpc, a.out_cs), c, a.D, acc);
+}
+
+// Rows [r0, r0 + nr), units [u0, u0 + cs.d) of the slice, summed straight from global memory (tiles
+// whose col slice or source span does not fit LDS, and edge-less tiles: cols == nullptr).
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ void rows_global(const UnalArgs& a, const int32_t* P, const int32_t* cols, int32_t base,
+                                            uint32_t r0, uint32_t nr, uint32_t u0, const FastDiv& cs) {
+  const uint32_t units = nr * cs.d;
+  for (uint32_t t = threadIdx.x; t < units; t += kUT) {
+    const uint32_t rl = fdiv(t, cs);
+    const uint32_t c = 4 * (u0 + t - rl * cs.d);
+    float4 acc = f4z();
+    if (cols) {
+      const int32_t b = P[rl] - base, e = P[rl + 1] - base;
+      for (int32_t k = b; k < e; ++k) f4acc(acc, ld_unit(src_row<SRC_CHUNKED>(a, (uint32_t)cols[k]), c, a.D));
+    }
+    finish_unit(a, r0 + rl, c, acc);
+  }
+}
+
+// Rows [first, first + span) of the slice into s_x (row stride 4 * cu floats, 16-byte aligned),
+// plus an all-zero row at index span. kSB units per thread per batch: every load of a batch is issued
+// (clamped, always valid addresses) before the first LDS store waits for one. (D >= 4 takes ld_raw /
+// put_raw: the launcher keeps a partial last unit out of a slice of its own.)
+constexpr int kSB = 6;
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ void stage(const UnalArgs& a, float* s_x, uint32_t first, uint32_t span, uint32_t u0,
+                                      const FastDiv& cs) {
+  const uint32_t ws = 4 * a.pitch;
+  for (uint32_t t = threadIdx.x; t < a.pitch; t += kUT) reinterpret_cast<float4*>(s_x + span * ws)[t] = f4z();
+  const uint32_t units = span * cs.d;
+  if (a.D < 4) {
+    for (uint32_t t = threadIdx.x; t < units; t += kUT) {
+      const uint32_t rl = fdiv(t, cs);
+      const uint32_t k = t - rl * cs.d;
+      *reinterpret_cast<float4*>(s_x + rl * ws + 4 * k) = ld_unit(src_row<SRC_CHUNKED>(a, first + rl), 4 * (u0 + k), a.D);
+    }
+    return;
+  }
+  for (uint32_t t0 = 0; t0 < units; t0 += kSB * kUT) {
+    float4 v[kSB];
+#pragma unroll
+    for (int b = 0; b < kSB; ++b) {
+      const uint32_t t = min(t0 + threadIdx.x + (uint32_t)b * kUT, units - 1);
+      const uint32_t rl = fdiv(t, cs);
+      v[b] = ld_raw(src_row<SRC_CHUNKED>(a, first + rl), 4 * (u0 + t - rl * cs.d), a.D);
+    }
+#pragma unroll
+    for (int b = 0; b < kSB; ++b) {
+      const uint32_t t = t0 + threadIdx.x + (uint32_t)b * kUT;
+      if (t < units) {
+        const uint32_t rl = fdiv(t, cs);
+        put_raw(s_x + rl * ws, 4 * (u0 + t - rl * cs.d), a.D, u0, v[b]);
+      }
+    }
+  }
+}
+
+// Rows [r0, r0 + nr) of the slice, summed from the staged rows: P[0..nr] their row pointers, col
+// entries from P[0] = pbase on as byte offsets into xb (cb), an all-zero staged row at byte offset
+// *(cb + zb). Thread t owns unit t % pitch of row t / pitch (lanes past the slice's units idle):
+// with a 16-unit multiple pitch and a 256-byte multiple row stride every unit k sits in 16-byte slot
+// k % 16 = lane % 16 of the LDS banks, whatever row its source is, so each ds_read_b128 lane group
+// ({0-3,12-15,20-27}, ...: distinct lane % 16) reads distinct slots: no bank conflict.
+__device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, int32_t pbase, const char* cb,
+                                         const char* xb, int32_t zb, uint32_t r0, uint32_t nr, uint32_t u0,
+                                         const FastDiv& cs) {
+  const uint32_t units = a.compact ? nr * cs.d : nr << a.pitch_l2;
+  for (uint32_t t = threadIdx.x; t < units; t += kUT) {
+    const uint32_t rl = a.compact ? fdiv(t, cs) : t >> a.pitch_l2;
+    const uint32_t k = a.compact ? t - rl * cs.d : t & (a.pitch - 1);
+    if (k >= cs.d) continue;
+    const uint32_t ub = 16 * k;
+    const int32_t bb = (P[rl] - pbase) * 4, eb = (P[rl + 1] - pbase) * 4;
+    float4 acc = f4z();
+    // slots past the segment read the zero row through an ADDRESS select (+0.0f leaves the sum,
+    // which starts at +0.0f, bit-identical), so the group's reads issue back to back
+    for (int32_t kb = bb; kb < eb; kb += 4 * kUGroup) {
+      float4 x[kUGroup];
+#pragma unroll
+      for (int q = 0; q < kUGroup; ++q) {
+        const int32_t off = *reinterpret_cast<const int32_t*>(cb + ((kb + 4 * q < eb) ? kb + 4 * q : zb));
+        x[q] = *reinterpret_cast<const float4*>(xb + off + ub);
+      }
+#pragma unroll
+      for (int q = 0; q < kUGroup; ++q) f4acc(acc, x[q]);
+    }
+    finish_unit(a, r0 + rl, 4 * (u0 + k), acc);
+  }
+}
+
+// One tile of rows [r0, r0 + nr) whose row pointers P[0..nr] are in LDS, one column slice. spec: the
+// tile is segment-aligned (whole molecules), so its own rows are staged while the first col piece
+// loads. A tile whose col slice overflows the col_cap LDS slots runs in row pieces that fit, all
+// summed from the same staged source rows (a molecule's pieces share its rows; a piece whose sources
+// leave the staged span restages). Called by the whole workgroup after the barrier that published P;
+// leaves every LDS region except the row pointers reusable.
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_t* s_misc, int32_t* s_col, float* s_x,
+                                     uint32_t r0, uint32_t nr, bool spec, uint32_t u0, const FastDiv& cs) {
+  const int32_t base = P[0];
+  if (P[nr] == base) {
+    rows_global<SRC_CHUNKED>(a, P, nullptr, base, r0, nr, u0, cs);
+    return;
+  }
+  const int32_t rb = (int32_t)(16 * a.pitch);  // bytes per staged row
+  const char* xb = reinterpret_cast<const char*>(s_x);
+  const char* cb = reinterpret_cast<const char*>(s_col);
+  bool have = spec && nr + 1 <= a.xcap;  // s_x holds rows [first, first + span)
+  uint32_t first = r0, span = nr;
+  bool staging = have;  // the speculative stage is issued with the first piece's col loads
+  for (uint32_t pr = 0; pr < nr;) {
+    // rows [pr, pe) of the tile: the longest run from pr whose col entries fit (plus the sentinel)
+    uint32_t pe = nr;
+    while (pe > pr + 1 && (uint32_t)(P[pe] - P[pr]) >= a.col_cap) pe = pr + (pe - pr) / 2;
+    const int32_t pb = P[pr] - base;
+    const int32_t ncols = P[pe] - P[pr];
+    if ((uint32_t)ncols >= a.col_cap) {  // one row longer than the slots: from global
+      rows_global<SRC_CHUNKED>(a, P + pr, a.col + base + pb, base + pb, r0 + pr, pe - pr, u0, cs);
+      pr = pe;
+      continue;
+    }
+    int32_t lo = INT_MAX, hi = INT_MIN;
+    for (int32_t i = threadIdx.x; i < ncols; i += kUT) {
+      const int32_t c = a.col[base + pb + i];
+      s_col[i] = c;
+      lo = min(lo, c);
+      hi = max(hi, c);
+    }
+    if (staging) stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs);
+    staging = false;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, __shfl_xor(lo, o, 64));
+      hi = max(hi, __shfl_xor(hi, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicMin(&s_misc[2], lo);
+      atomicMax(&s_misc[3], hi);
+    }
+    lds_barrier();
+    lo = s_misc[2];
+    hi = s_misc[3];
+    if (!(have && lo >= (int32_t)first && hi < (int32_t)(first + span))) {
+      if ((uint32_t)(hi - lo) + 1 >= a.xcap) {  // sources too far apart to stage: from global
+        lds_barrier();                         // every lo / hi read before the reset below
+        if (threadIdx.x == 0) {
+          s_misc[2] = INT_MAX;
+          s_misc[3] = INT_MIN;
+        }
+        rows_global<SRC_CHUNKED>(a, P + pr, s_col, base + pb, r0 + pr, pe - pr, u0, cs);
+        lds_barrier();  // s_col read before the next piece rewrites it
+        pr = pe;
+        continue;
+      }
+      // (the barrier above ordered every earlier stage write and staged-row read before this)
+      first = (uint32_t)lo;
+      span = (uint32_t)(hi - lo + 1);
+      have = true;
+      stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs);
+    }
+    // col entries as byte offsets of the staged rows; each thread rewrites the entries it stored
+    for (int32_t i = threadIdx.x; i < ncols; i += kUT) s_col[i] = (s_col[i] - (int32_t)first) * rb;
+    if (threadIdx.x == 0) s_col[ncols] = (int32_t)span * rb;
+    lds_barrier();
+    if (threadIdx.x == 0) {  // every lo / hi read is behind the barrier above
+      s_misc[2] = INT_MAX;
+      s_misc[3] = INT_MIN;
+    }
+    sum_rows(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0, cs);
+    pr = pe;
+    if (pr < nr) lds_barrier();  // s_col (and a restage of s_x) are rewritten by the next piece
+  }
+}
+
+// Big tile bbig of the rows [split, rows) (hop chunks >= 1): skipped (skip_tail), a streaming zero
+// fill, the residual terms alone, or (general CSR inputs only) a gather from global. Called by the
+// whole workgroup; s_ptr / s_misc are scratch; ends with every LDS read done.
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ void big_tile(const UnalArgs& a, uint32_t bbig, int32_t* s_ptr, int32_t* s_misc) {
+  const uint32_t R0 = a.split + bbig * a.big_rows;
+  const uint32_t NR = min(a.big_rows, a.rows - R0);
+  if (threadIdx.x == 0) {
+    s_misc[0] = a.rowptr[R0];
+    s_misc[1] = a.rowptr[R0 + NR];
+    // skip_tail: no edge from the start of R0's chunk to the end (every consumer trims those chunks)
+    s_misc[2] = a.skip_tail && a.out_rpc.d > 0 && a.rowptr[fdiv(R0, a.out_rpc) * a.out_rpc.d] == a.rowptr[a.rows];
+  }
+  lds_barrier();
+  const bool skip = s_misc[2] != 0, empty = s_misc[0] == s_misc[1];
+  lds_barrier();  // s_misc is scratch again for the caller
+  if (skip) return;
+  if (empty) {
+    if (a.flat_zero) {
+      // the big tile's rows are one contiguous [NR, D] region: dword head, aligned float4 body, tail
+      float* o = a.out + row_off(R0, a.out_ld, a.out_rpc, a.out_cs);
+      const uint32_t n = NR * a.D;
+      const uint32_t head = min(n, (uint32_t)((4u - (((uintptr_t)o >> 2) & 3u)) & 3u));
+      if (threadIdx.x < head) o[threadIdx.x] = 0.f;
+      const uint32_t body = (n - head) / 4;
+      float4* ob = reinterpret_cast<float4*>(o + head);
+      for (uint32_t t = threadIdx.x; t < body; t += kUT) ob[t] = f4z();
+      const uint32_t tail = (n - head) - 4 * body;
+      if (threadIdx.x < tail) o[head + 4 * body + threadIdx.x] = 0.f;
+      return;
+    }
+    rows_global<SRC_CHUNKED>(a, nullptr, nullptr, 0, R0, NR, 0, a.upr_f);
+    return;
+  }
+  // a big tile with edges (general CSR inputs only): its rows in tiles of tile_rows, whole width
+  for (uint32_t r0 = R0; r0 < R0 + NR; r0 += a.tile_rows) {
+    const uint32_t nr = min(a.tile_rows, R0 + NR - r0);
+    for (uint32_t t = threadIdx.x; t <= nr; t += kUT) s_ptr[t] = a.rowptr[r0 + t];
+    if (threadIdx.x == 0) {
+      s_misc[2] = INT_MAX;
+      s_misc[3] = INT_MIN;
+    }
+    lds_barrier();
+    const int32_t base = s_ptr[0];
+    rows_global<SRC_CHUNKED>(a, s_ptr, a.col + base, base, r0, nr, 0, a.upr_f);
+    lds_barrier();
+  }
+}
+
+template <bool SRC_CHUNKED>
+__global__ __launch_bounds__(kUT) void k_gather_unal(const UnalArgs a) {
+  // [row pointers | misc | pad] [col_cap col entries] [xcap staged rows of 4 * cu floats]
+  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
+  int32_t* s_ptr = s_dyn;
+  int32_t* s_misc = s_dyn + kUMisc;
+  int32_t* s_col = s_dyn + kUHead;
+  float* s_x = reinterpret_cast<float*>(s_dyn + kUHead + a.col_cap);
+  // block order: big (zero-fill) tiles spread evenly among the tile workgroups (hop.hip)
+  uint32_t bsmall = blockIdx.x, bbig = 0;
+  bool is_small = blockIdx.x < a.nsmall;
+  if (a.interleave) {
+    const uint64_t total = (uint64_t)gridDim.x, nbig = total - a.nsmall;
+    const uint32_t c1 = (uint32_t)(((uint64_t)blockIdx.x + 1) * nbig / total);
+    const uint32_t c0 = (uint32_t)((uint64_t)blockIdx.x * nbig / total);
+    is_small = (c1 == c0);
+    bsmall = blockIdx.x - c1;
+    bbig = c1 - 1;
+  } else if (!is_small) {
+    bbig = blockIdx.x - a.nsmall;
+  }
+  if (threadIdx.x == 0) {
+    s_misc[2] = INT_MAX;
+    s_misc[3] = INT_MIN;
+  }
+  if (is_small) {
+    // the slices of one tile on one XCD: small blocks b and b + 8 k share an XCD (round-robin
+    // dispatch), so tile = (b / (8 S)) * 8 + b % 8, slice = (b / 8) % S
+    const uint32_t S = a.slices;
+    const uint32_t grp = bsmall / (8 * S), in = bsmall - grp * 8 * S;
+    const uint32_t ti = grp * 8 + (in & 7), sl = in >> 3;
+    if (ti >= a.ntiles) return;
+    const FastDiv cs = sl + 1 == S ? a.cu_last : a.cu_full;
+    const uint32_t u0 = sl * a.cu;
+    const uint32_t c0 = ti * a.tile_rows;
+    const uint32_t c1 = min(c0 + a.tile_rows, a.split);
+    if (!a.seg) {
+      for (uint32_t t = threadIdx.x; t <= c1 - c0; t += kUT) s_ptr[t] = a.rowptr[c0 + t];
+      lds_barrier();
+      tile<SRC_CHUNKED>(a, s_ptr, s_misc, s_col, s_x, c0, c1 - c0, false, u0, cs);
+      return;
+    }
+    // segment-aligned cuts: each nominal cut c moves to the first molecule start in [c, c + 64) (c
+    // itself if none); both cuts are the same function of c, so the tiles partition the rows
+    const uint32_t pend = min(c1 + (uint32_t)kUAlignWin, a.split);
+    for (uint32_t t = threadIdx.x; t <= pend - c0; t += kUT) s_ptr[t] = a.rowptr[c0 + t];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {
+      const uint32_t c = w ? c1 : c0;
+      uint32_t cut = c;
+      if (c > 0 && c < a.split) {
+        const uint32_t q = min(c + lane, a.split - 1);
+        const int64_t sq = a.seg[(int64_t)q * a.seg_stride], sp = a.seg[(int64_t)(q - 1) * a.seg_stride];
+        const unsigned long long m = __ballot((c + lane < a.split) && sq != sp);
+        if (m) cut = c + (uint32_t)__builtin_ctzll(m);
+      }
+      if (lane == 0) s_misc[w] = (int32_t)cut;
+    }
+    lds_barrier();
+    const uint32_t r0 = (uint32_t)s_misc[0], r1 = (uint32_t)s_misc[1];
+    if (r1 <= r0) return;
+    tile<SRC_CHUNKED>(a, s_ptr + (r0 - c0), s_misc, s_col, s_x, r0, r1 - r0, true, u0, cs);
+    return;
+  }
+  big_tile<SRC_CHUNKED>(a, bbig, s_ptr, s_misc);
+}
+
+
+// ---- persistent, software-pipelined variant (segment-aligned tiles) --------------------------------
+// A workgroup walks items j, j + G, j + 2G, ... (G = the resident grid). While it sums item j from LDS,
+// the global loads of the next item's col slice and staged rows (registers) and of the item after
+// that's row pointers and molecule cuts are in flight, so each item costs one exposed round trip at
+// most instead of two back to back. Items: the small (tile, column slice) items and the big tiles of
+// the rows past the first chunk, interleaved as the one-shot kernel's blocks are.
+constexpr int kPMeta = 136;  // ints per meta buffer: row pointers [129] + misc [7]
+constexpr int kPRegU = 6;    // staged units per thread held in registers between load and commit
+constexpr int kPRegC = 8;    // col entries per thread held in registers
+// misc words (at kUMisc): [0] r0, [1] r1 (the cuts), [2] lo, [3] hi (col range), [4] c0 (row of P[0]),
+// [5] kind (0 none, 1 small, 2 big), [6] slice (small) / big tile index (big)
+
+struct ARegs {
+  int32_t rp;
+  int64_t sq, sp;
+};
+struct BRegs {
+  float4 x[kPRegU];
+  int32_t c[kPRegC];
+};
+
+__device__ __forceinline__ void item_of(const UnalArgs& a, uint32_t j, uint32_t total, bool& big, uint32_t& idx) {
+  if (a.interleave) {
+    const uint64_t nbig = total - a.nsmall;
+    const uint32_t c1 = (uint32_t)(((uint64_t)j + 1) * nbig / total);
+    const uint32_t c0 = (uint32_t)((uint64_t)j * nbig / total);
+    big = c1 != c0;
+    idx = big ? c1 - 1 : j - c1;
+  } else {
+    big = j >= a.nsmall;
+    idx = big ? j - a.nsmall : j;
+  }
+}
+__device__ __forceinline__ void small_of(const UnalArgs& a, uint32_t idx, uint32_t& ti, uint32_t& sl) {
+  const uint32_t S = a.slices;
+  const uint32_t grp = idx / (8 * S), in = idx - grp * 8 * S;
+  ti = grp * 8 + (in & 7);
+  sl = in >> 3;
+}
+
+// Item j's row pointers and molecule-start words into registers (loads only).
+__device__ __forceinline__ void load_a(const UnalArgs& a, uint32_t j, uint32_t total, ARegs& r) {
+  r.rp = 0;
+  r.sq = r.sp = 0;
+  if (j >= total) return;
+  bool big;
+  uint32_t idx, ti, sl;
+  item_of(a, j, total, big, idx);
+  if (big) return;
+  small_of(a, idx, ti, sl);
+  if (ti >= a.ntiles) return;
+  const uint32_t c0 = ti * a.tile_rows, c1 = min(c0 + a.tile_rows, a.split);
+  const uint32_t pend = min(c1 + (uint32_t)kUAlignWin, a.split);
+  if (threadIdx.x <= pend - c0) r.rp = a.rowptr[c0 + threadIdx.x];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < 2) {
+    const uint32_t c = w ? c1 : c0;
+    if (c > 0 && c < a.split) {
+      const uint32_t q = min(c + lane, a.split - 1);
+      r.sq = a.seg[(int64_t)q * a.seg_stride];
+      r.sp = a.seg[(int64_t)(q - 1) * a.seg_stride];
+    }
+  }
+}
+
+// Item j's meta buffer from the registers of load_a: row pointers, cuts, kind, a reset col range.
+// Prefetched registers are laundered through an empty asm at their commit point: the compiler may
+// not move their first use (and the wait for the load) up to the load itself.
+__device__ __forceinline__ void launder(int32_t& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void launder(int64_t& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void launder(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
+__device__ __forceinline__ void commit_a(const UnalArgs& a, uint32_t j, uint32_t total, ARegs r, int32_t* M) {
+  launder(r.rp);
+  launder(r.sq);
+  launder(r.sp);
+  int32_t* m = M + kUMisc;
+  bool big = false;
+  uint32_t idx = 0, ti = 0, sl = 0;
+  int kind = 0;
+  if (j < total) {
+    item_of(a, j, total, big, idx);
+    if (big) {
+      kind = 2;
+    } else {
+      small_of(a, idx, ti, sl);
+      kind = ti < a.ntiles ? 1 : 0;
+    }
+  }
+  if (kind == 1) {
+    const uint32_t c0 = ti * a.tile_rows, c1 = min(c0 + a.tile_rows, a.split);
+    const uint32_t pend = min(c1 + (uint32_t)kUAlignWin, a.split);
+    if (threadIdx.x <= pend - c0) M[threadIdx.x] = r.rp;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {  // wave-uniform: the whole wave takes part in the ballot
+      const uint32_t c = w ? c1 : c0;
+      const bool st = c > 0 && c < a.split && c + lane < a.split && r.sq != r.sp;
+      const unsigned long long mk = __ballot(st);
+      const uint32_t cut = (c > 0 && c < a.split && mk) ? c + (uint32_t)__builtin_ctzll(mk) : c;
+      if (lane == 0) m[w] = (int32_t)cut;
+    }
+    if (threadIdx.x == 128) {
+      m[4] = (int32_t)c0;
+      m[6] = (int32_t)sl;
+    }
+  } else if (threadIdx.x == 0) {
+    m[0] = m[1] = 0;
+    m[6] = (int32_t)idx;
+  }
+  if (threadIdx.x == 192) {
+    m[2] = INT_MAX;
+    m[3] = INT_MIN;
+    m[5] = kind;
+  }
+}
+
+// The small item in meta M: its tile, whether its col slice and its own rows (+ the zero row) fit the
+// prefetch registers and LDS (then the loads go out now, into r).
+template <bool SRC_CHUNKED>
+__device__ __forceinline__ bool load_b(const UnalArgs& a, const int32_t* M, BRegs& r) {
+  const int32_t* m = M + kUMisc;
+  if (m[5] != 1) return false;
+  const uint32_t r0 = (uint32_t)m[0], r1 = (uint32_t)m[1];
+  if (r1 <= r0) return false;
+  const int32_t* P = M + (r0 - (uint32_t)m[4]);
+  const uint32_t nr = r1 - r0;
+  const int32_t base = P[0], ncols = P[nr] - base;
+  const uint32_t sl = (uint32_t)m[6];
+  const FastDiv cs = sl + 1 == a.slices ? a.cu_last : a.cu_full;
+  const uint32_t u0 = sl * a.cu;
+  const uint32_t units = nr * cs.d;
+  if (!(ncols > 0 && (uint32_t)ncols < a.col_cap && ncols <= kPRegC * kUT && nr + 1 <= a.xcap &&
+        units <= (uint32_t)(kPRegU * kUT) && a.D >= 4))
+    return false;
+#pragma unroll
+  for (int k = 0; k < kPRegC; ++k) {
+    const int32_t i = threadIdx.x + k * kUT;
+    r.c[k] = i < ncols ? a.col[base + i] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kPRegU; ++k) {  // clamped, unconditional loads (commit_b writes the zero row)
+    const uint32_t u = min(threadIdx.x + k * kUT, units - 1);
+    const uint32_t rl = fdiv(u, cs);
+    r.x[k] = ld_raw(src_row<SRC_CHUNKED>(a, r0 + rl), 4 * (u0 + u - rl * cs.d), a.D);
+  }
+  return true;
+}
+
+// The prefetched col slice and rows into LDS, and the col range into the meta's lo / hi.
+__device__ __forceinline__ void commit_b(const UnalArgs& a, int32_t* M, BRegs r, int32_t* s_col, float* s_x) {
+#pragma unroll
+  for (int k = 0; k < kPRegC; ++k) launder(r.c[k]);
+#pragma unroll
+  for (int k = 0; k < kPRegU; ++k) launder(r.x[k]);
+  int32_t* m = M + kUMisc;
+  const uint32_t r0 = (uint32_t)m[0], r1 = (uint32_t)m[1];
+  const int32_t* P = M + (r0 - (uint32_t)m[4]);
+  const uint32_t nr = r1 - r0;
+  const int32_t ncols = P[nr] - P[0];
+  const uint32_t sl = (uint32_t)m[6];
+  const FastDiv cs = sl + 1 == a.slices ? a.cu_last : a.cu_full;
+  const uint32_t units = nr * cs.d;
+  const uint32_t ws = 4 * a.pitch;
+  const uint32_t u0 = sl * a.cu;
+  for (uint32_t t = threadIdx.x; t < a.pitch; t += kUT) reinterpret_cast<float4*>(s_x + nr * ws)[t] = f4z();
+  int32_t lo = INT_MAX, hi = INT_MIN;
+#pragma unroll
+  for (int k = 0; k < kPRegC; ++k) {
+    const int32_t i = threadIdx.x + k * kUT;
+    if (i < ncols) {
+      s_col[i] = r.c[k];
+      lo = min(lo, r.c[k]);
+      hi = max(hi, r.c[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kPRegU; ++k) {
+    const uint32_t u = threadIdx.x + k * kUT;
+    if (u < units) {
+      const uint32_t rl = fdiv(u, cs);
+      put_raw(s_x + rl * ws, 4 * (u0 + u - rl * cs.d), a.D, u0, r.x[k]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o, 64));
+    hi = max(hi, __shfl_xor(hi, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&m[2], lo);
+    atomicMax(&m[3], hi);
+  }
+}
+
+template <bool SRC_CHUNKED>
+__global__ __launch_bounds__(kUT) void k_gather_unal_pipe(const UnalArgs a, uint32_t total) {
+  // [meta 0 | meta 1] [col_cap col entries] [xcap staged rows of 4 * cu floats]
+  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
+  int32_t* s_col = s_dyn + 2 * kPMeta;
+  float* s_x = reinterpret_cast<float*>(s_dyn + 2 * kPMeta + a.col_cap);
+  const uint32_t G = gridDim.x;
+  uint32_t j = blockIdx.x;
+  if (j >= total) return;
+  int cur = 0;
+  ARegs ar;
+  BRegs br;
+  load_a(a, j, total, ar);
+  commit_a(a, j, total, ar, s_dyn);
+  lds_barrier();
+  bool pf = load_b<SRC_CHUNKED>(a, s_dyn, br);
+  load_a(a, j + G, total, ar);
+  if (pf) commit_b(a, s_dyn, br, s_col, s_x);
+  commit_a(a, j + G, total, ar, s_dyn + kPMeta);
+  lds_barrier();
+  for (; j < total; j += G) {
+    int32_t* M = s_dyn + cur * kPMeta;
+    int32_t* N = s_dyn + (1 - cur) * kPMeta;
+    const int32_t* m = M + kUMisc;
+    const int kind = m[5];
+    const uint32_t r0 = (uint32_t)m[0], r1 = (uint32_t)m[1], c0 = (uint32_t)m[4], sl = (uint32_t)m[6];
+    const int32_t lo = m[2], hi = m[3];
+    const bool own = pf && lo >= (int32_t)r0 && hi < (int32_t)r1;
+    const uint32_t nr = r1 > r0 ? r1 - r0 : 0;
+    const int32_t* P = M + (r0 - c0);
+    const int32_t rb = (int32_t)(16 * a.pitch);
+    if (own) {  // col entries as byte offsets of the staged rows (each thread its own entries)
+      const int32_t ncols = P[nr] - P[0];
+#pragma unroll
+      for (int k = 0; k < kPRegC; ++k) {
+        const int32_t i = threadIdx.x + k * kUT;
+        if (i < ncols) s_col[i] = (s_col[i] - (int32_t)r0) * rb;
+      }
+      if (threadIdx.x == 0) s_col[ncols] = (int32_t)nr * rb;
+    }
+    // the next items' loads go out before this item's sum
+    const bool pfn = load_b<SRC_CHUNKED>(a, N, br);
+    load_a(a, j + 2 * G, total, ar);
+    lds_barrier();
+    if (kind == 2) {
+      big_tile<SRC_CHUNKED>(a, (uint32_t)m[6], M, M + kUMisc);
+    } else if (kind == 1 && nr > 0) {
+      const FastDiv cs = sl + 1 == a.slices ? a.cu_last : a.cu_full;
+      const uint32_t u0 = sl * a.cu;
+      if (own) {
+        sum_rows(a, P, P[0], reinterpret_cast<const char*>(s_col), reinterpret_cast<const char*>(s_x),
+                 (P[nr] - P[0]) * 4, r0, nr, u0, cs);
+      } else {
+        if (pf) {  // prefetched, but the sources leave the tile: the general path (col range reset)
+          if (threadIdx.x == 0) {
+            M[kUMisc + 2] = INT_MAX;
+            M[kUMisc + 3] = INT_MIN;
+          }
+          lds_barrier();
+        }
+        tile<SRC_CHUNKED>(a, P, M + kUMisc, s_col, s_x, r0, nr, true, u0, cs);
+      }
+    }
+    lds_barrier();
+    if (pfn) commit_b(a, N, br, s_col, s_x);
+    commit_a(a, j + 2 * G, total, ar, M);
+    lds_barrier();
+    cur = 1 - cur;
+    pf = pfn;
+  }
+}
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  return e ? std::max<int64_t>(0, atoll(e)) : dflt;
+}
+
+}  // namespace
+
+bool gather_unal_on() {
+  static const bool on = env_i64("AIMX_HOP_UNAL", 1) != 0;
+  return on;
+}
+
+int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
+                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
+                       int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
+                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
+                       int32_t skip_tail) {
+  auto al4 = [](const void* p) { return ((uintptr_t)p & 3) == 0; };
+  if (!al4(src) || !al4(out) || (add0 && !al4(add0)) || (add1 && !al4(add1))) return AIMX_EARG;
+  if (rows >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;
+  // knobs, read once per process
+  // slice width (floats): 64 = one 16-unit pitch per staged row (conflict-free ds_read_b128, sum_rows)
+  static const int64_t w_max = std::max<int64_t>(4, env_i64("AIMX_HOPU_W", 80) / 4 * 4);
+  static const int64_t pitch_env = [] {  // staged row pitch in units: 0 compact, else a power of two >= 16
+    const int64_t e = env_i64("AIMX_HOPU_PITCH", 0);
+    if (!e) return (int64_t)0;
+    int64_t p = 16;
+    while (p < e) p *= 2;
+    return p;
+  }();
+  static const int64_t tr_env = std::max<int64_t>(1, std::min<int64_t>(kUMaxTile, env_i64("AIMX_HOPU_TILE", 32)));
+  static const int64_t col_cap_env = (std::max<int64_t>(64, env_i64("AIMX_HOPU_COL_CAP", 1024)) + 3) / 4 * 4;
+  static const int64_t stage_env = std::max<int64_t>(1024, env_i64("AIMX_HOPU_STAGE", 20 * 1024));
+  static const int64_t big_env = env_i64("AIMX_HOPU_BIG", 256);
+  static const int32_t interleave = env_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
+  static const bool no_seg = env_i64("AIMX_HOP_NO_SEG", 0) != 0;
+  static const int64_t pipe = env_i64("AIMX_HOPU_PIPE", 0);  // persistent pipelined kernel (opt-in: slower)
+  static const int64_t pipe_waves = std::max<int64_t>(1, env_i64("AIMX_HOPU_PIPE_WAVES", 1));  // grid = waves x resident
+  const int64_t upr = cdiv(D, 4);
+  // slices of cu units; the last slice must hold more than a partial last unit (put_raw writes that
+  // unit shifted down over the unit before it, which must be in the same slice)
+  int64_t slices = cdiv(upr * 4, w_max), cu = 0, cu_last = 0;
+  for (;; ++slices) {
+    cu = cdiv(upr, slices);
+    slices = cdiv(upr, cu);
+    cu_last = upr - (slices - 1) * cu;
+    if (D % 4 == 0 || D < 4 || slices == 1 || cu_last >= 2) break;
+  }
+  if (cu_last <= 0) return AIMX_EARG;
+  const int64_t split = (out_rpc > 0 && out_rpc < rows) ? out_rpc : rows;
+  // with few tiles (small batches) shorter nominal tiles keep the CUs busy
+  int64_t tr = tr_env;
+  while (tr > 8 && cdiv(split, tr) * slices < 2048) tr /= 2;
+  const int64_t ntiles = cdiv(split, tr);
+  const int64_t nsmall = cdiv(ntiles, 8) * 8 * slices;  // whole groups of 8 tiles (XCD order)
+  const int64_t big = std::max<int64_t>(tr, big_env);
+  const int64_t nbig = cdiv(rows - split, big);
+  int64_t pitch = pitch_env;
+  while (pitch_env && pitch < cu) pitch *= 2;
+  if (!pitch_env) pitch = cu;  // compact: no idle lanes, rows of cu units
+  int64_t pitch_l2 = 0;
+  while (pitch_env && (1ll << pitch_l2) < pitch) ++pitch_l2;
+  const int64_t xcap = std::min<int64_t>(kUMaxRows + 1, stage_env / (16 * pitch));
+  const size_t dyn = (size_t)(kUHead + col_cap_env) * 4 + (size_t)xcap * 16 * pitch;
+  UnalArgs a;
+  a.src = src;
+  a.src_ld = src_ld;
+  a.src_cs = src_cs;
+  a.src_rpc = make_fastdiv(src_rpc > 0 ? (uint32_t)src_rpc : 0);
+  a.rowptr = rowptr;
+  a.col = col;
+  a.D = (uint32_t)D;
+  a.upr = (uint32_t)upr;
+  a.slices = (uint32_t)slices;
+  a.cu = (uint32_t)cu;
+  a.pitch = (uint32_t)pitch;
+  a.pitch_l2 = (uint32_t)pitch_l2;
+  a.compact = pitch_env ? 0 : 1;
+  a.cu_full = make_fastdiv((uint32_t)cu);
+  a.cu_last = make_fastdiv((uint32_t)cu_last);
+  a.upr_f = make_fastdiv((uint32_t)upr);
+  a.rows = (uint32_t)rows;
+  a.split = (uint32_t)split;
+  a.tile_rows = (uint32_t)tr;
+  a.ntiles = (uint32_t)ntiles;
+  a.nsmall = (uint32_t)nsmall;
+  a.big_rows = (uint32_t)big;
+  a.nbig = (uint32_t)nbig;
+  a.col_cap = (uint32_t)col_cap_env;
+  a.xcap = (uint32_t)xcap;
+  a.out = out;
+  a.out_ld = out_ld;
+  a.out_cs = out_cs;
+  a.out_rpc = make_fastdiv(out_rpc > 0 ? (uint32_t)out_rpc : 0);
+  a.add0 = add0;
+  a.add0_ld = add0_ld;
+  a.add1 = add1;
+  a.add1_ld = add1_ld;
+  a.seg = (row_seg && !no_seg) ? row_seg : nullptr;
+  a.seg_stride = row_seg_stride;
+  const bool contiguous = out_ld == D && (out_rpc <= 0 || out_cs == out_rpc * out_ld);
+  a.flat_zero = (contiguous && !add0 && !add1) ? 1 : 0;
+  a.interleave = interleave;
+  a.skip_tail = skip_tail;
+  const int64_t blocks = nsmall + nbig;
+  if (blocks <= 0) return AIMX_OK;
+  if (blocks >= (int64_t)INT32_MAX) return AIMX_EARG;
+  if (a.seg && pipe) {
+    using PFn = void (*)(const UnalArgs, uint32_t);
+    PFn fn = src_rpc > 0 ? k_gather_unal_pipe<true> : k_gather_unal_pipe<false>;
+    const size_t pdyn = dyn - (size_t)kUHead * 4 + (size_t)2 * kPMeta * 4;
+    // the resident grid: workgroups per CU at this LDS size (queried once per size) x CUs
+    static int cus = 0;
+    static size_t occ_dyn = 0;
+    static int occ = 0;
+    if (!cus) {
+      int dev = 0;
+      AIMX_CHECK_HIP(hipGetDevice(&dev));
+      AIMX_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (occ_dyn != pdyn) {
+      AIMX_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kUT, pdyn));
+      occ_dyn = pdyn;
+    }
+    const int64_t grid = std::min<int64_t>(blocks, (int64_t)std::max(1, occ) * cus * pipe_waves);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kUT), pdyn, stream, a, (uint32_t)blocks);
+    AIMX_CHECK_LAUNCH();
+    return AIMX_OK;
+  }
+  using KFn = void (*)(const UnalArgs);
+  KFn fn = src_rpc > 0 ? k_gather_unal<true> : k_gather_unal<false>;
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kUT), dyn, stream, a);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
+}
+
+}  // namespace aimx
