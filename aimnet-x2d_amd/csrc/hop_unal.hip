@@ -122,6 +122,15 @@ struct UnalArgs {
   int64_t seg_stride;
 };
 
+// make_fastdiv on the device (d < 2^31)
+__device__ __forceinline__ FastDiv fastdiv_dev(uint32_t d) {
+  FastDiv f{d, 0, 0};
+  if (d == 0) return f;
+  while ((1u << f.l) < d) ++f.l;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << f.l) - d)) / d) + 1);
+  return f;
+}
+
 template <bool SRC_CHUNKED>
 __device__ __forceinline__ const float* src_row(const UnalArgs& a, uint32_t q) {
   if (!SRC_CHUNKED) return a.src + (int64_t)q * a.src_ld;
@@ -159,18 +168,19 @@ __device__ __forceinline__ void rows_global(const UnalArgs& a, const int32_t* P,
   }
 }
 
-// Rows [first, first + span) of the slice into s_x (row stride 4 * cu floats, 16-byte aligned),
-// plus an all-zero row at index span. kSB units per thread per batch: every load of a batch is issued
+// Rows [first, first + span), units [u0, u0 + cs.d) into s_x (row stride wsu units, 16-byte aligned),
+// plus an all-zero row at index span. dwords: ld_unit for every unit (a sub-slice may start at the
+// partial last unit, which put_raw would write in front of the row). kSB units per thread per batch: every load of a batch is issued
 // (clamped, always valid addresses) before the first LDS store waits for one. (D >= 4 takes ld_raw /
 // put_raw: the launcher keeps a partial last unit out of a slice of its own.)
 constexpr int kSB = 6;
 template <bool SRC_CHUNKED>
 __device__ __forceinline__ void stage(const UnalArgs& a, float* s_x, uint32_t first, uint32_t span, uint32_t u0,
-                                      const FastDiv& cs) {
-  const uint32_t ws = 4 * a.pitch;
-  for (uint32_t t = threadIdx.x; t < a.pitch; t += kUT) reinterpret_cast<float4*>(s_x + span * ws)[t] = f4z();
+                                      const FastDiv& cs, uint32_t wsu, bool dwords) {
+  const uint32_t ws = 4 * wsu;
+  for (uint32_t t = threadIdx.x; t < wsu; t += kUT) reinterpret_cast<float4*>(s_x + span * ws)[t] = f4z();
   const uint32_t units = span * cs.d;
-  if (a.D < 4) {
+  if (a.D < 4 || dwords) {
     for (uint32_t t = threadIdx.x; t < units; t += kUT) {
       const uint32_t rl = fdiv(t, cs);
       const uint32_t k = t - rl * cs.d;
@@ -205,11 +215,11 @@ __device__ __forceinline__ void stage(const UnalArgs& a, float* s_x, uint32_t fi
 // ({0-3,12-15,20-27}, ...: distinct lane % 16) reads distinct slots: no bank conflict.
 __device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, int32_t pbase, const char* cb,
                                          const char* xb, int32_t zb, uint32_t r0, uint32_t nr, uint32_t u0,
-                                         const FastDiv& cs) {
-  const uint32_t units = a.compact ? nr * cs.d : nr << a.pitch_l2;
+                                         const FastDiv& cs, bool compact) {
+  const uint32_t units = compact ? nr * cs.d : nr << a.pitch_l2;
   for (uint32_t t = threadIdx.x; t < units; t += kUT) {
-    const uint32_t rl = a.compact ? fdiv(t, cs) : t >> a.pitch_l2;
-    const uint32_t k = a.compact ? t - rl * cs.d : t & (a.pitch - 1);
+    const uint32_t rl = compact ? fdiv(t, cs) : t >> a.pitch_l2;
+    const uint32_t k = compact ? t - rl * cs.d : t & (a.pitch - 1);
     if (k >= cs.d) continue;
     const uint32_t ub = 16 * k;
     const int32_t bb = (P[rl] - pbase) * 4, eb = (P[rl + 1] - pbase) * 4;
@@ -268,7 +278,7 @@ __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_
       lo = min(lo, c);
       hi = max(hi, c);
     }
-    if (staging) stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs);
+    if (staging) stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs, a.pitch, false);
     staging = false;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -283,14 +293,30 @@ __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_
     lo = s_misc[2];
     hi = s_misc[3];
     if (!(have && lo >= (int32_t)first && hi < (int32_t)(first + span))) {
-      if ((uint32_t)(hi - lo) + 1 >= a.xcap) {  // sources too far apart to stage: from global
-        lds_barrier();                         // every lo / hi read before the reset below
+      if ((uint32_t)(hi - lo) + 1 >= a.xcap) {
+        // sources too far apart to stage the whole slice: narrower sub-slices of the span that fit
+        lds_barrier();  // every lo / hi read before the reset below
         if (threadIdx.x == 0) {
           s_misc[2] = INT_MAX;
           s_misc[3] = INT_MIN;
         }
-        rows_global<SRC_CHUNKED>(a, P + pr, s_col, base + pb, r0 + pr, pe - pr, u0, cs);
+        const uint32_t sp = (uint32_t)(hi - lo) + 1;
+        const uint32_t su = min(cs.d, a.xcap * a.pitch / (sp + 1));  // units per sub-slice
+        if (su == 0) {  // not even one unit of the span fits: from global
+          rows_global<SRC_CHUNKED>(a, P + pr, s_col, base + pb, r0 + pr, pe - pr, u0, cs);
+        } else {
+          for (int32_t i = threadIdx.x; i < ncols; i += kUT) s_col[i] = (s_col[i] - lo) * (int32_t)(16 * su);
+          if (threadIdx.x == 0) s_col[ncols] = (int32_t)(sp * 16 * su);
+          for (uint32_t j0 = 0; j0 < cs.d; j0 += su) {
+            const FastDiv fw = fastdiv_dev(min(su, cs.d - j0));
+            stage<SRC_CHUNKED>(a, s_x, (uint32_t)lo, sp, u0 + j0, fw, su, true);
+            lds_barrier();
+            sum_rows(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0 + j0, fw, true);
+            lds_barrier();  // staged rows read before the next sub-slice restages
+          }
+        }
         lds_barrier();  // s_col read before the next piece rewrites it
+        have = false;   // s_x no longer holds a whole-slice stage
         pr = pe;
         continue;
       }
@@ -298,7 +324,7 @@ __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_
       first = (uint32_t)lo;
       span = (uint32_t)(hi - lo + 1);
       have = true;
-      stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs);
+      stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs, a.pitch, false);
     }
     // col entries as byte offsets of the staged rows; each thread rewrites the entries it stored
     for (int32_t i = threadIdx.x; i < ncols; i += kUT) s_col[i] = (s_col[i] - (int32_t)first) * rb;
@@ -308,7 +334,7 @@ __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_
       s_misc[2] = INT_MAX;
       s_misc[3] = INT_MIN;
     }
-    sum_rows(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0, cs);
+    sum_rows(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0, cs, a.compact);
     pr = pe;
     if (pr < nr) lds_barrier();  // s_col (and a restage of s_x) are rewritten by the next piece
   }
@@ -676,7 +702,7 @@ __global__ __launch_bounds__(kUT) void k_gather_unal_pipe(const UnalArgs a, uint
       const uint32_t u0 = sl * a.cu;
       if (own) {
         sum_rows(a, P, P[0], reinterpret_cast<const char*>(s_col), reinterpret_cast<const char*>(s_x),
-                 (P[nr] - P[0]) * 4, r0, nr, u0, cs);
+                 (P[nr] - P[0]) * 4, r0, nr, u0, cs, a.compact);
       } else {
         if (pf) {  // prefetched, but the sources leave the tile: the general path (col range reset)
           if (threadIdx.x == 0) {
