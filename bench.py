@@ -208,6 +208,14 @@ def build_model(cfg, device):
     return m.to(device).train()
 
 
+def hop_kernel(d):
+    """The hop kernel that runs for width d: hop.hip for 16-byte rows, else hop_unal.hip (hop_rows.hip
+    with AIMX_HOP_UNAL=0)."""
+    if d % 4 == 0:
+        return "k_gather_sum"
+    return "k_gather_rows" if os.environ.get("AIMX_HOP_UNAL", "1") == "0" else "k_gather_unal"
+
+
 def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launches=20):
     """Time the hop kernel alone on a QM9-shaped graph of ~target_atoms atoms (tiled copies of a
     real collated batch), with HIP events on the stream it is launched on."""
@@ -249,7 +257,7 @@ def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launch
     if os.path.exists(tp):
         try:
             rec = json.load(open(tp))
-            if rec.get("atoms") == n and rec.get("edges") == e:
+            if rec.get("atoms") == n and rec.get("edges") == e and rec.get("kernel", hop_kernel(d)) == hop_kernel(d):
                 traffic = rec.get("hbm_bytes_per_launch")
                 bwd_traffic = (rec.get("bwd") or {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
@@ -264,7 +272,7 @@ def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launch
                                "command (bench.py --roofline-only), per launch, gfx950 corrections applied; not "
                                "measured inside this run") if traffic is not None else None,
             "bwd": bwd,
-            "kernel": ("k_gather_sum" if d % 4 == 0 else "k_gather_rows") + " (hop fwd)", "atoms": n, "edges": e,
+            "kernel": hop_kernel(d) + " (hop fwd)", "atoms": n, "edges": e,
             "D": d, "hops": hops,
             "algorithmic_bytes_per_launch": alg_bytes, "ms_per_launch": round(ms, 4)}
 
@@ -353,7 +361,7 @@ def hop_in_step(batch, hops, hidden, device):
     seg, seg_st = plan.row_seg()
     s = _lib.stream_ptr(device)
     fl = 4  # bytes per float: column offsets as pointer arithmetic
-    kern = "k_gather_sum" if d % 4 == 0 else "k_gather_rows"
+    kern = hop_kernel(d)
 
     def fwd():  # the stack's call: trailing edge-less chunks not written (AIMX_GATHER_SKIP_TAIL)
         assert lib.aimx_segment_gather_sum_ex(P(F), LF, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n,
@@ -401,7 +409,7 @@ def hop_bwd_roofline(plan, n, d, hops, device, launches=20):
     t1.synchronize()
     us = t0.elapsed_time(t1) / launches * 1e3
     # bytes: the gathered rows (chunk 0 only for reference inputs) + col + rowptr + dx written
-    return _bw(("k_gather_sum" if d % 4 == 0 else "k_gather_rows") + " (hop bwd)",
+    return _bw(hop_kernel(d) + " (hop bwd)",
                4 * (n * d + plan.E + (n + 1) + n * d), us)
 
 

@@ -7,7 +7,7 @@ coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE * 10
 16-B-per-lane streaming stores.
 
 usage: python tools/hop_traffic.py <fetch_dir> <write_dir> <roofline_json_log> [out.json]
-       [--kernel k_gather_sum|k_gather_rows]
+       [--kernel k_gather_sum|k_gather_unal|k_gather_rows]
 """
 import argparse
 import csv
