@@ -205,6 +205,45 @@ struct HopLds {
 };
 constexpr int kLdsHead = 136;  // ints ahead of the col slice: ptr (129) + lohi (2), padded to 16 B
 
+// Rows [first, first + span) of src into s_x (row stride D floats), plus an all-zero row at index
+// span. kStageB units per thread per batch: every load of a batch is issued (clamped indices, always
+// valid addresses) before the first LDS store waits for one; a load behind the row guard would make
+// the compiler wait for each load at the guard's join (one memory round trip per unit per thread).
+constexpr int kStageB = 3;
+// An empty asm that reads a loaded value: the loads of a batch cannot be sunk past it to their LDS
+// stores (the 64-VGPR budget otherwise makes the scheduler interleave load, wait, store per unit).
+__device__ __forceinline__ void hold(const float& v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void hold(const float2& v) { asm volatile("" ::"v"(v.x), "v"(v.y)); }
+__device__ __forceinline__ void hold(const float4& v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
+template <int VEC, bool SRC_CHUNKED>
+__device__ __forceinline__ void stage_span(const HopArgs& a, float* s_x, uint32_t first, uint32_t span) {
+  using T = typename VecT<VEC>::T;
+  const int32_t D = (int32_t)(a.upr.d * VEC);
+  for (uint32_t t = threadIdx.x; t < a.upr.d; t += blockDim.x)
+    *reinterpret_cast<T*>(s_x + span * D + t * VEC) = vzero<T>();
+  const uint32_t units = span * a.upr.d;
+  for (uint32_t t0 = 0; t0 < units; t0 += kStageB * blockDim.x) {
+    T v[kStageB];
+#pragma unroll
+    for (int b = 0; b < kStageB; ++b) {
+      const uint32_t t = min(t0 + threadIdx.x + (uint32_t)b * blockDim.x, units - 1);
+      const uint32_t rl = fdiv(t, a.upr);
+      v[b] = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>(first + rl, a.src_ld, a.src_rpc, a.src_cs) +
+                                         (t - rl * a.upr.d) * VEC);
+    }
+#pragma unroll
+    for (int b = 0; b < kStageB; ++b) hold(v[b]);
+#pragma unroll
+    for (int b = 0; b < kStageB; ++b) {
+      const uint32_t t = t0 + threadIdx.x + (uint32_t)b * blockDim.x;
+      if (t < units) {
+        const uint32_t rl = fdiv(t, a.upr);
+        *reinterpret_cast<T*>(s_x + rl * D + (t - rl * a.upr.d) * VEC) = v[b];
+      }
+    }
+  }
+}
+
 // One tile of nr <= tile_rows rows at r0 (called by the whole workgroup; leaves LDS reusable).
 template <int VEC, bool SRC_CHUNKED>
 // s_col / s_x point into the dynamic LDS (col_cap entries, then the staged rows). They are passed
@@ -259,16 +298,7 @@ __device__ __forceinline__ void process_tile(const HopArgs& a, HopLds& L, int32_
         // each thread rewrites the col entries it staged as byte offsets of the staged rows
         for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) s_col[i] = (s_col[i] - lo) * D * 4;
         if (threadIdx.x == 0) s_col[ncols] = span * D * 4;
-        const uint32_t units = (uint32_t)(span + 1) * a.upr.d;
-        for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
-          const uint32_t rl = fdiv(t, a.upr);
-          const uint32_t u = (t - rl * a.upr.d) * VEC;
-          T v = vzero<T>();
-          if (rl < (uint32_t)span)
-            v = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>((uint32_t)lo + rl, a.src_ld, a.src_rpc,
-                                                                         a.src_cs) + u);
-          *reinterpret_cast<T*>(s_x + rl * D + u) = v;
-        }
+        stage_span<VEC, SRC_CHUNKED>(a, s_x, (uint32_t)lo, (uint32_t)span);
         __syncthreads();
         tile_body_staged<VEC>(s_x, a.upr, L.ptr, s_col, ncols, base, r0, nr, a.out, a.out_ld, a.out_rpc, a.out_cs,
                               a.add0, a.add0_ld, a.add1, a.add1_ld);
@@ -337,16 +367,7 @@ __device__ __forceinline__ void process_tile_seg(const HopArgs& a, HopLds& L, in
     lo = min(lo, c);
     hi = max(hi, c);
   }
-  {  // speculative stage of rows [r0, r0 + nr) plus the zero row, loads in flight with the cols'
-    const uint32_t units = (nr + 1) * a.upr.d;
-    for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
-      const uint32_t rl = fdiv(t, a.upr);
-      const uint32_t u = (t - rl * a.upr.d) * VEC;
-      T v = vzero<T>();
-      if (rl < nr) v = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>(r0 + rl, a.src_ld, a.src_rpc, a.src_cs) + u);
-      *reinterpret_cast<T*>(s_x + rl * D + u) = v;
-    }
-  }
+  stage_span<VEC, SRC_CHUNKED>(a, s_x, r0, nr);  // speculative: loads in flight with the cols'
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     lo = min(lo, __shfl_xor(lo, o, 64));
@@ -365,14 +386,7 @@ __device__ __forceinline__ void process_tile_seg(const HopArgs& a, HopLds& L, in
     __syncthreads();
     first = (uint32_t)lo;
     span = (uint32_t)(hi - lo + 1);
-    const uint32_t units = (span + 1) * a.upr.d;
-    for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
-      const uint32_t rl = fdiv(t, a.upr);
-      const uint32_t u = (t - rl * a.upr.d) * VEC;
-      T v = vzero<T>();
-      if (rl < span) v = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>(first + rl, a.src_ld, a.src_rpc, a.src_cs) + u);
-      *reinterpret_cast<T*>(s_x + rl * D + u) = v;
-    }
+    stage_span<VEC, SRC_CHUNKED>(a, s_x, first, span);
     staged = true;
   }
   if (staged) {

@@ -173,7 +173,21 @@ __device__ __forceinline__ void rows_global(const UnalArgs& a, const int32_t* P,
 // partial last unit, which put_raw would write in front of the row). kSB units per thread per batch: every load of a batch is issued
 // (clamped, always valid addresses) before the first LDS store waits for one. (D >= 4 takes ld_raw /
 // put_raw: the launcher keeps a partial last unit out of a slice of its own.)
-constexpr int kSB = 6;
+#ifndef AIMX_HOPU_SB
+#define AIMX_HOPU_SB 4
+#endif
+#ifndef AIMX_HOPU_CB
+#define AIMX_HOPU_CB 4
+#endif
+#ifndef AIMX_HOPU_COMB
+#define AIMX_HOPU_COMB 0
+#endif
+constexpr int kSB = AIMX_HOPU_SB;
+constexpr int kCB = AIMX_HOPU_CB;  // col entries per thread per batch (tile)
+// An empty asm that reads a loaded value: a batch's loads cannot be sunk past it to their uses, so
+// they stay in flight together instead of one wait per load.
+__device__ __forceinline__ void hold(const int32_t& v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void hold(const float4& v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
 template <bool SRC_CHUNKED>
 __device__ __forceinline__ void stage(const UnalArgs& a, float* s_x, uint32_t first, uint32_t span, uint32_t u0,
                                       const FastDiv& cs, uint32_t wsu, bool dwords) {
@@ -196,6 +210,8 @@ __device__ __forceinline__ void stage(const UnalArgs& a, float* s_x, uint32_t fi
       const uint32_t rl = fdiv(t, cs);
       v[b] = ld_raw(src_row<SRC_CHUNKED>(a, first + rl), 4 * (u0 + t - rl * cs.d), a.D);
     }
+#pragma unroll
+    for (int b = 0; b < kSB; ++b) hold(v[b]);
 #pragma unroll
     for (int b = 0; b < kSB; ++b) {
       const uint32_t t = t0 + threadIdx.x + (uint32_t)b * kUT;
@@ -272,13 +288,58 @@ __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_
       continue;
     }
     int32_t lo = INT_MAX, hi = INT_MIN;
-    for (int32_t i = threadIdx.x; i < ncols; i += kUT) {
-      const int32_t c = a.col[base + pb + i];
-      s_col[i] = c;
-      lo = min(lo, c);
-      hi = max(hi, c);
+    // the col slice in batches of kCB loads per thread; with the speculative stage, each col batch
+    // goes out together with a stage batch (one round trip for both)
+    const bool spec_now = AIMX_HOPU_COMB && staging && a.D >= 4;
+    const uint32_t sunits = spec_now ? span * cs.d : 0;
+    const uint32_t ws = 4 * a.pitch;
+    if (spec_now)
+      for (uint32_t t = threadIdx.x; t < a.pitch; t += kUT) reinterpret_cast<float4*>(s_x + span * ws)[t] = f4z();
+    for (uint32_t k = 0; (int32_t)(k * kCB * kUT) < ncols || k * kSB * kUT < sunits; ++k) {
+      const int32_t i0 = (int32_t)(k * kCB * kUT);
+      const uint32_t t0 = k * kSB * kUT;
+      const bool cb_on = i0 < ncols, sb_on = t0 < sunits;  // workgroup-uniform
+      int32_t c[kCB];
+      float4 v[kSB];
+      if (cb_on) {
+#pragma unroll
+        for (int b = 0; b < kCB; ++b) c[b] = a.col[base + pb + min(i0 + (int32_t)threadIdx.x + b * kUT, ncols - 1)];
+      }
+      if (sb_on) {
+#pragma unroll
+        for (int b = 0; b < kSB; ++b) {
+          const uint32_t t = min(t0 + threadIdx.x + (uint32_t)b * kUT, sunits - 1);
+          const uint32_t rl = fdiv(t, cs);
+          v[b] = ld_raw(src_row<SRC_CHUNKED>(a, first + rl), 4 * (u0 + t - rl * cs.d), a.D);
+        }
+      }
+      if (cb_on) {
+#pragma unroll
+        for (int b = 0; b < kCB; ++b) hold(c[b]);
+#pragma unroll
+        for (int b = 0; b < kCB; ++b) {
+          const int32_t i = i0 + (int32_t)threadIdx.x + b * kUT;
+          if (i < ncols) {
+            s_col[i] = c[b];
+            lo = min(lo, c[b]);
+            hi = max(hi, c[b]);
+          }
+        }
+      }
+      if (sb_on) {
+#pragma unroll
+        for (int b = 0; b < kSB; ++b) hold(v[b]);
+#pragma unroll
+        for (int b = 0; b < kSB; ++b) {
+          const uint32_t t = t0 + threadIdx.x + (uint32_t)b * kUT;
+          if (t < sunits) {
+            const uint32_t rl = fdiv(t, cs);
+            put_raw(s_x + rl * ws, 4 * (u0 + t - rl * cs.d), a.D, u0, v[b]);
+          }
+        }
+      }
     }
-    if (staging) stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs, a.pitch, false);
+    if (staging && !spec_now) stage<SRC_CHUNKED>(a, s_x, first, span, u0, cs, a.pitch, false);
     staging = false;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
