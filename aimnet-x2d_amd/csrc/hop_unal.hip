@@ -74,6 +74,20 @@ __device__ __forceinline__ float4 ld_raw(const float* row, uint32_t c, uint32_t 
   const F4u v = *reinterpret_cast<const F4u*>(row + min(c, D - 4));
   return make_float4(v.x, v.y, v.z, v.w);
 }
+// ld_raw's 16 bytes as columns c.. of the row: lanes moved down by sh = c - min(c, D - 4) (0 for a
+// full unit; the lanes past the row's end then hold other columns, never stored)
+// (two-level selects on the shift's bits: a select chain on sh == 0 / 1 / 2 becomes a private-memory
+// table indexed by sh)
+__device__ __forceinline__ float4 shift_down(const float4 v, uint32_t sh) {
+  const bool b1 = (sh & 1u) != 0, b2 = (sh & 2u) != 0;
+  const float x = v.x, y = v.y, z = v.z, w = v.w;  // scalars: a select of member addresses keeps v in memory
+  float4 r;
+  r.x = b2 ? (b1 ? w : z) : (b1 ? y : x);
+  r.y = b2 ? w : (b1 ? z : y);
+  r.z = (b1 || b2) ? w : z;
+  r.w = w;
+  return r;
+}
 // ld_raw's 16 bytes into a staged row d (slice column 0 at d[0]) at slice column min(c, D - 4) - 4 u0:
 // a full unit lands on its own 16 bytes; the last, partial unit of an odd-width row lands shifted
 // down, rewriting the same values over columns of the unit before it (identical bytes).
@@ -120,6 +134,11 @@ struct UnalArgs {
   int64_t add1_ld;
   const int64_t* seg;  // molecule id per row of [0, split) (optional)
   int64_t seg_stride;
+  // the residual rows for the prefetching sum (ADDS): add0 / add1, or src row 0 (never used) when absent
+  const float* q0;
+  int64_t q0_ld;
+  const float* q1;
+  int64_t q1_ld;
 };
 
 // make_fastdiv on the device (d < 2^31)
@@ -229,14 +248,26 @@ __device__ __forceinline__ void stage(const UnalArgs& a, float* s_x, uint32_t fi
 // with a 16-unit multiple pitch and a 256-byte multiple row stride every unit k sits in 16-byte slot
 // k % 16 = lane % 16 of the LDS banks, whatever row its source is, so each ds_read_b128 lane group
 // ({0-3,12-15,20-27}, ...: distinct lane % 16) reads distinct slots: no bank conflict.
+template <bool ADDS>
 __device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, int32_t pbase, const char* cb,
                                          const char* xb, int32_t zb, uint32_t r0, uint32_t nr, uint32_t u0,
                                          const FastDiv& cs, bool compact) {
   const uint32_t units = compact ? nr * cs.d : nr << a.pitch_l2;
+  constexpr bool pre = ADDS;  // residual terms prefetched (the launcher: D >= 4 and a term present)
   for (uint32_t t = threadIdx.x; t < units; t += kUT) {
     const uint32_t rl = compact ? fdiv(t, cs) : t >> a.pitch_l2;
     const uint32_t k = compact ? t - rl * cs.d : t & (a.pitch - 1);
     if (k >= cs.d) continue;
+    const uint32_t c = 4 * (u0 + k);
+    const uint32_t r = r0 + rl;
+    // the residual rows' 16 bytes go out before the LDS sum and are consumed after it: unconditional
+    // loads (a missing term reads src row 0 instead, set up by the launcher, and is dropped), so no
+    // branch joins them to a wait
+    float4 q0, q1;
+    if (pre) {
+      q0 = ld_raw(a.q0 + (int64_t)r * a.q0_ld, c, a.D);
+      q1 = ld_raw(a.q1 + (int64_t)r * a.q1_ld, c, a.D);
+    }
     const uint32_t ub = 16 * k;
     const int32_t bb = (P[rl] - pbase) * 4, eb = (P[rl + 1] - pbase) * 4;
     float4 acc = f4z();
@@ -252,7 +283,18 @@ __device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, in
 #pragma unroll
       for (int q = 0; q < kUGroup; ++q) f4acc(acc, x[q]);
     }
-    finish_unit(a, r0 + rl, 4 * (u0 + k), acc);
+    if (pre) {
+      const uint32_t sh = c - min(c, a.D - 4);  // the partial last unit's shift (0 otherwise)
+      float4 s0 = shift_down(q0, sh);
+      f4acc(s0, acc);
+      if (a.add0) acc = s0;
+      float4 s1 = acc;
+      f4acc(s1, shift_down(q1, sh));
+      if (a.add1) acc = s1;
+      st_unit(a.out + row_off(r, a.out_ld, a.out_rpc, a.out_cs), c, a.D, acc);
+    } else {
+      finish_unit(a, r, c, acc);
+    }
   }
 }
 
@@ -262,7 +304,7 @@ __device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, in
 // summed from the same staged source rows (a molecule's pieces share its rows; a piece whose sources
 // leave the staged span restages). Called by the whole workgroup after the barrier that published P;
 // leaves every LDS region except the row pointers reusable.
-template <bool SRC_CHUNKED>
+template <bool SRC_CHUNKED, bool ADDS>
 __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_t* s_misc, int32_t* s_col, float* s_x,
                                      uint32_t r0, uint32_t nr, bool spec, uint32_t u0, const FastDiv& cs) {
   const int32_t base = P[0];
@@ -372,7 +414,7 @@ __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_
             const FastDiv fw = fastdiv_dev(min(su, cs.d - j0));
             stage<SRC_CHUNKED>(a, s_x, (uint32_t)lo, sp, u0 + j0, fw, su, true);
             lds_barrier();
-            sum_rows(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0 + j0, fw, true);
+            sum_rows<ADDS>(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0 + j0, fw, true);
             lds_barrier();  // staged rows read before the next sub-slice restages
           }
         }
@@ -395,7 +437,7 @@ __device__ __forceinline__ void tile(const UnalArgs& a, const int32_t* P, int32_
       s_misc[2] = INT_MAX;
       s_misc[3] = INT_MIN;
     }
-    sum_rows(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0, cs, a.compact);
+    sum_rows<ADDS>(a, P + pr, P[pr], cb, xb, ncols * 4, r0 + pr, pe - pr, u0, cs, a.compact);
     pr = pe;
     if (pr < nr) lds_barrier();  // s_col (and a restage of s_x) are rewritten by the next piece
   }
@@ -450,7 +492,7 @@ __device__ __forceinline__ void big_tile(const UnalArgs& a, uint32_t bbig, int32
   }
 }
 
-template <bool SRC_CHUNKED>
+template <bool SRC_CHUNKED, bool ADDS>
 __global__ __launch_bounds__(kUT) void k_gather_unal(const UnalArgs a) {
   // [row pointers | misc | pad] [col_cap col entries] [xcap staged rows of 4 * cu floats]
   extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
@@ -489,7 +531,7 @@ __global__ __launch_bounds__(kUT) void k_gather_unal(const UnalArgs a) {
     if (!a.seg) {
       for (uint32_t t = threadIdx.x; t <= c1 - c0; t += kUT) s_ptr[t] = a.rowptr[c0 + t];
       lds_barrier();
-      tile<SRC_CHUNKED>(a, s_ptr, s_misc, s_col, s_x, c0, c1 - c0, false, u0, cs);
+      tile<SRC_CHUNKED, ADDS>(a, s_ptr, s_misc, s_col, s_x, c0, c1 - c0, false, u0, cs);
       return;
     }
     // segment-aligned cuts: each nominal cut c moves to the first molecule start in [c, c + 64) (c
@@ -511,7 +553,7 @@ __global__ __launch_bounds__(kUT) void k_gather_unal(const UnalArgs a) {
     lds_barrier();
     const uint32_t r0 = (uint32_t)s_misc[0], r1 = (uint32_t)s_misc[1];
     if (r1 <= r0) return;
-    tile<SRC_CHUNKED>(a, s_ptr + (r0 - c0), s_misc, s_col, s_x, r0, r1 - r0, true, u0, cs);
+    tile<SRC_CHUNKED, ADDS>(a, s_ptr + (r0 - c0), s_misc, s_col, s_x, r0, r1 - r0, true, u0, cs);
     return;
   }
   big_tile<SRC_CHUNKED>(a, bbig, s_ptr, s_misc);
@@ -762,7 +804,7 @@ __global__ __launch_bounds__(kUT) void k_gather_unal_pipe(const UnalArgs a, uint
       const FastDiv cs = sl + 1 == a.slices ? a.cu_last : a.cu_full;
       const uint32_t u0 = sl * a.cu;
       if (own) {
-        sum_rows(a, P, P[0], reinterpret_cast<const char*>(s_col), reinterpret_cast<const char*>(s_x),
+        sum_rows<false>(a, P, P[0], reinterpret_cast<const char*>(s_col), reinterpret_cast<const char*>(s_x),
                  (P[nr] - P[0]) * 4, r0, nr, u0, cs, a.compact);
       } else {
         if (pf) {  // prefetched, but the sources leave the tile: the general path (col range reset)
@@ -772,7 +814,7 @@ __global__ __launch_bounds__(kUT) void k_gather_unal_pipe(const UnalArgs a, uint
           }
           lds_barrier();
         }
-        tile<SRC_CHUNKED>(a, P, M + kUMisc, s_col, s_x, r0, nr, true, u0, cs);
+        tile<SRC_CHUNKED, false>(a, P, M + kUMisc, s_col, s_x, r0, nr, true, u0, cs);
       }
     }
     lds_barrier();
@@ -883,6 +925,10 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   a.add1 = add1;
   a.add1_ld = add1_ld;
   a.seg = (row_seg && !no_seg) ? row_seg : nullptr;
+  a.q0 = add0 ? add0 : src;
+  a.q0_ld = add0 ? add0_ld : 0;
+  a.q1 = add1 ? add1 : src;
+  a.q1_ld = add1 ? add1_ld : 0;
   a.seg_stride = row_seg_stride;
   const bool contiguous = out_ld == D && (out_rpc <= 0 || out_cs == out_rpc * out_ld);
   a.flat_zero = (contiguous && !add0 && !add1) ? 1 : 0;
@@ -914,7 +960,9 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
     return AIMX_OK;
   }
   using KFn = void (*)(const UnalArgs);
-  KFn fn = src_rpc > 0 ? k_gather_unal<true> : k_gather_unal<false>;
+  const bool adds = D >= 4 && (add0 || add1);
+  KFn fn = src_rpc > 0 ? (adds ? k_gather_unal<true, true> : k_gather_unal<true, false>)
+                       : (adds ? k_gather_unal<false, true> : k_gather_unal<false, false>);
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kUT), dyn, stream, a);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
