@@ -141,6 +141,39 @@ __device__ __forceinline__ void tile_body_staged(const float* s_x, const FastDiv
   const char* xb = reinterpret_cast<const char*>(s_x);
   const char* cb = reinterpret_cast<const char*>(cols);
   const int32_t zb = zslot * 4;
+  if (add0 || add1) {
+    // the residual terms' loads go out before the LDS sum and are consumed after it: unconditional
+    // (an absent term reads the output row, dropped below), so no branch joins them to a wait
+    for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
+      const uint32_t rl = fdiv(t, upr);
+      const uint32_t ub = (t - rl * upr.d) * VEC * 4;
+      const uint32_t u = ub / 4;
+      const uint32_t r = r0 + rl;
+      float* orow = out + row_off(r, out_ld, out_rpc, out_cs);
+      const T q0 = *reinterpret_cast<const T*>((add0 ? add0 + (int64_t)r * add0_ld : orow) + u);
+      const T q1 = *reinterpret_cast<const T*>((add1 ? add1 + (int64_t)r * add1_ld : orow) + u);
+      const int32_t bb = (s_ptr[rl] - base) * 4, eb = (s_ptr[rl + 1] - base) * 4;
+      T acc = vzero<T>();
+      for (int32_t kb = bb; kb < eb; kb += 4 * kU) {
+        T v[kU];
+#pragma unroll
+        for (int j = 0; j < kU; ++j) {
+          const int32_t off = *reinterpret_cast<const int32_t*>(cb + ((kb + 4 * j < eb) ? kb + 4 * j : zb));
+          v[j] = *reinterpret_cast<const T*>(xb + off + ub);
+        }
+#pragma unroll
+        for (int j = 0; j < kU; ++j) vadd(acc, v[j]);
+      }
+      T s0 = q0;  // add0 + sum, then + add1: the order below
+      vadd(s0, acc);
+      if (add0) acc = s0;
+      T s1 = acc;
+      vadd(s1, q1);
+      if (add1) acc = s1;
+      *reinterpret_cast<T*>(orow + u) = acc;
+    }
+    return;
+  }
   for (uint32_t t = threadIdx.x; t < units; t += blockDim.x) {
     const uint32_t rl = fdiv(t, upr);
     const uint32_t ub = (t - rl * upr.d) * VEC * 4;
