@@ -749,12 +749,35 @@ __global__ __launch_bounds__(S * P * 64) void k_attn_bwd(
 // lane, then the 4 wave sums in order) into a slice slab; k_attn_reduce2 sums the slices in order.
 constexpr int kRedSlice = 64;
 
-__device__ __forceinline__ double partial_at(int64_t t, int64_t g, int64_t nw, int H, const float* __restrict__ dW_part,
-                                             const double* __restrict__ db_part,
-                                             const double* __restrict__ dtau_part) {
-  if (t < nw) return (double)dW_part[g * nw + t];
-  if (t < nw + H) return db_part[g * H + (t - nw)];
-  return dtau_part[g];
+// Column t of [dW (H*C) | db (H) | dtau] summed over molecules g0 .. g0 + kRedSlice / 4 - 1 (those < G),
+// in that order. Every load
+// of the column is issued unconditionally (the molecule index clamped, out-of-range terms zeroed
+// after an empty asm holds the loads), so the 16 loads per lane are in flight together; a guarded
+// load per term made the compiler wait for each one at its branch's join.
+__device__ __forceinline__ void hold_d(const double& v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ double slice_sum(int64_t t, int64_t g0, int64_t G, int64_t nw, int H,
+                                            const float* __restrict__ dW_part, const double* __restrict__ db_part,
+                                            const double* __restrict__ dtau_part) {
+  constexpr int K = kRedSlice / 4;
+  double v[K];
+  if (t < nw) {
+    float f[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) f[k] = dW_part[min(g0 + k, G - 1) * nw + t];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = (double)f[k];
+  } else {
+    const double* p = t < nw + H ? db_part + (t - nw) : dtau_part;
+    const int64_t st = t < nw + H ? H : 1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = p[min(g0 + k, G - 1) * st];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) hold_d(v[k]);
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) s += g0 + k < G ? v[k] : 0.0;
+  return s;
 }
 
 __global__ __launch_bounds__(256) void k_attn_reduce1(int64_t G, int H, int64_t C, const float* __restrict__ dW_part,
@@ -766,14 +789,7 @@ __global__ __launch_bounds__(256) void k_attn_reduce1(int64_t G, int H, int64_t 
   const int64_t t = (int64_t)blockIdx.x * 64 + lane;
   const int64_t g0 = (int64_t)blockIdx.y * kRedSlice + w * (kRedSlice / 4);
   double s = 0.0;
-  if (t < tot) {
-    double v[kRedSlice / 4];
-#pragma unroll
-    for (int k = 0; k < kRedSlice / 4; ++k)
-      v[k] = g0 + k < G ? partial_at(t, g0 + k, nw, H, dW_part, db_part, dtau_part) : 0.0;
-#pragma unroll
-    for (int k = 0; k < kRedSlice / 4; ++k) s += v[k];
-  }
+  if (t < tot && g0 < G) s = slice_sum(t, g0, G, nw, H, dW_part, db_part, dtau_part);
   red[w][lane] = s;
   __syncthreads();
   if (w == 0 && t < tot) slab[(int64_t)blockIdx.y * tot + t] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
@@ -813,14 +829,7 @@ __global__ __launch_bounds__(256) void k_attn_reduce(int64_t G, int H, int64_t C
   const int64_t t = (int64_t)blockIdx.x * 64 + lane;
   const int64_t g0 = (int64_t)blockIdx.y * kRedSlice + w * (kRedSlice / 4);
   double s = 0.0;
-  if (t < tot) {
-    double v[kRedSlice / 4];
-#pragma unroll
-    for (int k = 0; k < kRedSlice / 4; ++k)
-      v[k] = g0 + k < G ? partial_at(t, g0 + k, nw, H, dW_part, db_part, dtau_part) : 0.0;
-#pragma unroll
-    for (int k = 0; k < kRedSlice / 4; ++k) s += v[k];
-  }
+  if (t < tot && g0 < G) s = slice_sum(t, g0, G, nw, H, dW_part, db_part, dtau_part);
   red[w][lane] = s;
   __syncthreads();
   if (w == 0 && t < tot) {
