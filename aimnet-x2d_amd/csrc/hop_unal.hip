@@ -118,6 +118,7 @@ struct UnalArgs {
   uint32_t slices, cu;        // column slices per tile; units per slice (the last may be shorter)
   uint32_t pitch, pitch_l2;   // staged row stride in units (a power of two, >= cu, a multiple of 16)
   int32_t compact;            // thread t owns unit t % cs.d of row t / cs.d instead (row stride cu units)
+  int32_t pair;               // compact: two units of a row per thread (sum_rows_pair)
   FastDiv cu_full, cu_last;   // units of a full / the last slice
   FastDiv upr_f;              // units of a whole row (big tiles)
   uint32_t rows, split;       // tiles cover rows [0, split); big tiles rows [split, rows)
@@ -248,10 +249,77 @@ __device__ __forceinline__ void stage(const UnalArgs& a, float* s_x, uint32_t fi
 // with a 16-unit multiple pitch and a 256-byte multiple row stride every unit k sits in 16-byte slot
 // k % 16 = lane % 16 of the LDS banks, whatever row its source is, so each ds_read_b128 lane group
 // ({0-3,12-15,20-27}, ...: distinct lane % 16) reads distinct slots: no bank conflict.
+// The residual terms and the store of unit c of row r from a prefetched pair of raw loads (ADDS).
+__device__ __forceinline__ void finish_pre(const UnalArgs& a, uint32_t r, uint32_t c, const float4& q0,
+                                           const float4& q1, float4 acc) {
+  const uint32_t sh = c - min(c, a.D - 4);  // the partial last unit's shift (0 otherwise)
+  float4 s0 = shift_down(q0, sh);
+  f4acc(s0, acc);
+  if (a.add0) acc = s0;
+  float4 s1 = acc;
+  f4acc(s1, shift_down(q1, sh));
+  if (a.add1) acc = s1;
+  st_unit(a.out + row_off(r, a.out_ld, a.out_rpc, a.out_cs), c, a.D, acc);
+}
+
+// sum_rows with two units of a row per thread (k and k + ceil(w / 2), compact layout): one col-offset
+// read from LDS serves two ds_read_b128 (LDS cycles per gathered unit 6 -> 5).
+template <bool ADDS>
+__device__ __forceinline__ void sum_rows_pair(const UnalArgs& a, const int32_t* P, int32_t pbase, const char* cb,
+                                              const char* xb, int32_t zb, uint32_t r0, uint32_t nr, uint32_t u0,
+                                              const FastDiv& cs) {
+  const uint32_t half = (cs.d + 1) >> 1;
+  const FastDiv hf = fastdiv_dev(half);
+  const uint32_t units = nr * half;
+  for (uint32_t t = threadIdx.x; t < units; t += kUT) {
+    const uint32_t rl = fdiv(t, hf);
+    const uint32_t k = t - rl * half;
+    const bool has2 = k + half < cs.d;
+    const uint32_t k2 = has2 ? k + half : k;
+    const uint32_t c = 4 * (u0 + k), c2 = 4 * (u0 + k2);
+    const uint32_t r = r0 + rl;
+    float4 q0, q1, q2, q3;
+    if (ADDS) {
+      q0 = ld_raw(a.q0 + (int64_t)r * a.q0_ld, c, a.D);
+      q1 = ld_raw(a.q1 + (int64_t)r * a.q1_ld, c, a.D);
+      q2 = ld_raw(a.q0 + (int64_t)r * a.q0_ld, c2, a.D);
+      q3 = ld_raw(a.q1 + (int64_t)r * a.q1_ld, c2, a.D);
+    }
+    const uint32_t ub = 16 * k, ub2 = 16 * k2;
+    const int32_t bb = (P[rl] - pbase) * 4, eb = (P[rl + 1] - pbase) * 4;
+    float4 acc = f4z(), acc2 = f4z();
+    for (int32_t kb = bb; kb < eb; kb += 4 * kUGroup) {
+      float4 x[kUGroup], y[kUGroup];
+#pragma unroll
+      for (int q = 0; q < kUGroup; ++q) {
+        const int32_t off = *reinterpret_cast<const int32_t*>(cb + ((kb + 4 * q < eb) ? kb + 4 * q : zb));
+        x[q] = *reinterpret_cast<const float4*>(xb + off + ub);
+        y[q] = *reinterpret_cast<const float4*>(xb + off + ub2);
+      }
+#pragma unroll
+      for (int q = 0; q < kUGroup; ++q) {
+        f4acc(acc, x[q]);
+        f4acc(acc2, y[q]);
+      }
+    }
+    if (ADDS) {
+      finish_pre(a, r, c, q0, q1, acc);
+      if (has2) finish_pre(a, r, c2, q2, q3, acc2);
+    } else {
+      finish_unit(a, r, c, acc);
+      if (has2) finish_unit(a, r, c2, acc2);
+    }
+  }
+}
+
 template <bool ADDS>
 __device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, int32_t pbase, const char* cb,
                                          const char* xb, int32_t zb, uint32_t r0, uint32_t nr, uint32_t u0,
                                          const FastDiv& cs, bool compact) {
+  if (compact && a.pair && cs.d >= 2) {
+    sum_rows_pair<ADDS>(a, P, pbase, cb, xb, zb, r0, nr, u0, cs);
+    return;
+  }
   const uint32_t units = compact ? nr * cs.d : nr << a.pitch_l2;
   constexpr bool pre = ADDS;  // residual terms prefetched (the launcher: D >= 4 and a term present)
   for (uint32_t t = threadIdx.x; t < units; t += kUT) {
@@ -284,14 +352,7 @@ __device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, in
       for (int q = 0; q < kUGroup; ++q) f4acc(acc, x[q]);
     }
     if (pre) {
-      const uint32_t sh = c - min(c, a.D - 4);  // the partial last unit's shift (0 otherwise)
-      float4 s0 = shift_down(q0, sh);
-      f4acc(s0, acc);
-      if (a.add0) acc = s0;
-      float4 s1 = acc;
-      f4acc(s1, shift_down(q1, sh));
-      if (a.add1) acc = s1;
-      st_unit(a.out + row_off(r, a.out_ld, a.out_rpc, a.out_cs), c, a.D, acc);
+      finish_pre(a, r, c, q0, q1, acc);
     } else {
       finish_unit(a, r, c, acc);
     }
@@ -862,6 +923,7 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   static const int64_t big_env = env_i64("AIMX_HOPU_BIG", 256);
   static const int32_t interleave = env_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
   static const bool no_seg = env_i64("AIMX_HOP_NO_SEG", 0) != 0;
+  static const int64_t pair_env = env_i64("AIMX_HOPU_PAIR", 0);  // two units per col-offset read (opt-in: slower)
   static const int64_t pipe = env_i64("AIMX_HOPU_PIPE", 0);  // persistent pipelined kernel (opt-in: slower)
   static const int64_t pipe_waves = std::max<int64_t>(1, env_i64("AIMX_HOPU_PIPE_WAVES", 1));  // grid = waves x resident
   const int64_t upr = cdiv(D, 4);
@@ -904,6 +966,7 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   a.pitch = (uint32_t)pitch;
   a.pitch_l2 = (uint32_t)pitch_l2;
   a.compact = pitch_env ? 0 : 1;
+  a.pair = pair_env ? 1 : 0;
   a.cu_full = make_fastdiv((uint32_t)cu);
   a.cu_last = make_fastdiv((uint32_t)cu_last);
   a.upr_f = make_fastdiv((uint32_t)upr);
