@@ -7,17 +7,21 @@
 // gfx950 executes global_load/store_dwordx4 at any 4-byte-aligned address (LLVM emits them for a
 // 4-byte-aligned 16-byte struct on this target; tools/micro/unal_copy.hip checks the copy bit for bit
 // and its rate). A row is then read and written as units of 4 columns [4g, 4g + 4) from the row's
-// own start, whatever its alignment: only the last unit of an odd-width row takes dword accesses.
-// In LDS the staged units sit 16-byte aligned, so the sum is ds_read_b128 throughout, and there is
-// no realignment tile (hop_rows.hip's column pass: stage -> sum -> shift through LDS -> store, four
-// barriers per 80-column pass run in sequence inside one workgroup).
+// own start, whatever its alignment: the 16 bytes at min(c, D - 4) are always inside the row, and
+// the last, partial unit's lanes are moved into place (staging: written shifted into LDS; residual
+// terms: selects); its stores take dwords. In LDS the staged units sit 16-byte aligned, so the sum
+// is ds_read_b128 throughout, and there is no realignment tile (hop_rows.hip's column pass: stage ->
+// sum -> shift through LDS -> store, four barriers per 80-column pass in sequence in one workgroup).
 //
 // Work split, as hop.hip's: a workgroup owns a segment-aligned tile (the molecules that start in its
-// nominal window; sources are then the tile's own rows, staged by a speculative load issued together
-// with the col slice: two dependent global round trips per tile) and ONE column slice of it. The
-// slices of one tile are separate workgroups on one XCD (same L2 for the shared row pointers and col
-// slice, the only bytes read twice), so a wide row costs parallel workgroups, not sequential passes.
-// Hop chunks >= 1 (no edges for reference inputs) are big streaming tiles spread among the windows.
+// nominal window; sources are then the tile's own rows, staged speculatively) and ONE column slice
+// of it. The slices of one tile are separate workgroups on one XCD (same L2 for the shared row
+// pointers and col slice, the only bytes read twice), so a wide row costs parallel workgroups, not
+// sequential passes. Round trips per workgroup: row pointers + molecule cuts, the col slice, the
+// stage; each a batch of unconditional loads held in registers until all are out (a guarded load
+// per entry made hipcc wait for each one). The backward's residual terms are loaded before the LDS
+// sum. Hop chunks >= 1 (no edges for reference inputs) are big streaming tiles among the windows.
+// Measured variants and why the defaults: DESIGN.md §3 "the odd-width hop", profiles/r05_hop_unal_ab.txt.
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
