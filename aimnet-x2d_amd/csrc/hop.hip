@@ -248,14 +248,17 @@ constexpr int kStageB = 3;
 __device__ __forceinline__ void hold(const float& v) { asm volatile("" ::"v"(v)); }
 __device__ __forceinline__ void hold(const float2& v) { asm volatile("" ::"v"(v.x), "v"(v.y)); }
 __device__ __forceinline__ void hold(const float4& v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
+__device__ __forceinline__ void hold(const int32_t& v) { asm volatile("" ::"v"(v)); }
+// (t_begin: units below it were staged by the caller; the zero row is always written here)
 template <int VEC, bool SRC_CHUNKED>
-__device__ __forceinline__ void stage_span(const HopArgs& a, float* s_x, uint32_t first, uint32_t span) {
+__device__ __forceinline__ void stage_span(const HopArgs& a, float* s_x, uint32_t first, uint32_t span,
+                                           uint32_t t_begin = 0) {
   using T = typename VecT<VEC>::T;
   const int32_t D = (int32_t)(a.upr.d * VEC);
   for (uint32_t t = threadIdx.x; t < a.upr.d; t += blockDim.x)
     *reinterpret_cast<T*>(s_x + span * D + t * VEC) = vzero<T>();
   const uint32_t units = span * a.upr.d;
-  for (uint32_t t0 = 0; t0 < units; t0 += kStageB * blockDim.x) {
+  for (uint32_t t0 = t_begin; t0 < units; t0 += kStageB * blockDim.x) {
     T v[kStageB];
 #pragma unroll
     for (int b = 0; b < kStageB; ++b) {
@@ -394,13 +397,53 @@ __device__ __forceinline__ void process_tile_seg(const HopArgs& a, HopLds& L, in
   }
   const int32_t D = (int32_t)(a.upr.d * VEC);
   int32_t lo = INT32_MAX, hi = INT32_MIN;
-  for (int32_t i = threadIdx.x; i < ncols; i += blockDim.x) {
+  // the first kColB col entries and the first kStageB units of the speculative stage (rows [r0,
+  // r0 + nr)) per thread go out together, unconditionally (clamped), held until all are issued: one
+  // round trip for both; what is left (long col slices, tall tiles) follows in batches
+  constexpr int kColB = 2;
+  {
+    using T = typename VecT<VEC>::T;
+    const uint32_t bd = blockDim.x, units = nr * a.upr.d;
+    int32_t cv[kColB];
+    T sv[kStageB];
+#pragma unroll
+    for (int b = 0; b < kColB; ++b) cv[b] = a.col[base + min((int32_t)(threadIdx.x + b * bd), ncols - 1)];
+#pragma unroll
+    for (int b = 0; b < kStageB; ++b) {
+      const uint32_t t = min(threadIdx.x + (uint32_t)b * bd, units - 1);
+      const uint32_t rl = fdiv(t, a.upr);
+      sv[b] = *reinterpret_cast<const T*>(a.src + src_off<SRC_CHUNKED>(r0 + rl, a.src_ld, a.src_rpc, a.src_cs) +
+                                          (t - rl * a.upr.d) * VEC);
+    }
+#pragma unroll
+    for (int b = 0; b < kColB; ++b) hold(cv[b]);
+#pragma unroll
+    for (int b = 0; b < kStageB; ++b) hold(sv[b]);
+#pragma unroll
+    for (int b = 0; b < kColB; ++b) {
+      const int32_t i = (int32_t)(threadIdx.x + b * bd);
+      if (i < ncols) {
+        s_col[i] = cv[b];
+        lo = min(lo, cv[b]);
+        hi = max(hi, cv[b]);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < kStageB; ++b) {
+      const uint32_t t = threadIdx.x + (uint32_t)b * bd;
+      if (t < units) {
+        const uint32_t rl = fdiv(t, a.upr);
+        *reinterpret_cast<T*>(s_x + rl * D + (t - rl * a.upr.d) * VEC) = sv[b];
+      }
+    }
+  }
+  for (int32_t i = threadIdx.x + kColB * blockDim.x; i < ncols; i += blockDim.x) {
     const int32_t c = a.col[base + i];
     s_col[i] = c;
     lo = min(lo, c);
     hi = max(hi, c);
   }
-  stage_span<VEC, SRC_CHUNKED>(a, s_x, r0, nr);  // speculative: loads in flight with the cols'
+  stage_span<VEC, SRC_CHUNKED>(a, s_x, r0, nr, kStageB * blockDim.x);  // the rest and the zero row
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     lo = min(lo, __shfl_xor(lo, o, 64));
