@@ -242,7 +242,10 @@ constexpr int kLdsHead = 136;  // ints ahead of the col slice: ptr (129) + lohi 
 // span. kStageB units per thread per batch: every load of a batch is issued (clamped indices, always
 // valid addresses) before the first LDS store waits for one; a load behind the row guard would make
 // the compiler wait for each load at the guard's join (one memory round trip per unit per thread).
-constexpr int kStageB = 3;
+#ifndef AIMX_HOP_STAGEB
+#define AIMX_HOP_STAGEB 3
+#endif
+constexpr int kStageB = AIMX_HOP_STAGEB;
 // An empty asm that reads a loaded value: the loads of a batch cannot be sunk past it to their LDS
 // stores (the 64-VGPR budget otherwise makes the scheduler interleave load, wait, store per unit).
 __device__ __forceinline__ void hold(const float& v) { asm volatile("" ::"v"(v)); }
@@ -400,7 +403,10 @@ __device__ __forceinline__ void process_tile_seg(const HopArgs& a, HopLds& L, in
   // the first kColB col entries and the first kStageB units of the speculative stage (rows [r0,
   // r0 + nr)) per thread go out together, unconditionally (clamped), held until all are issued: one
   // round trip for both; what is left (long col slices, tall tiles) follows in batches
-  constexpr int kColB = 2;
+#ifndef AIMX_HOP_COLB
+#define AIMX_HOP_COLB 2
+#endif
+  constexpr int kColB = AIMX_HOP_COLB;
   {
     using T = typename VecT<VEC>::T;
     const uint32_t bd = blockDim.x, units = nr * a.upr.d;
