@@ -136,14 +136,13 @@ class _State:
         self.order = []
         self.anchor = None
         self.gen = -1
-        self.params = self.modules = self.key = None
+        self.params = self.modules = None
 
     def structure(self, model):
         """(parameters, submodules, parameter identity key), rebuilt only when _GEN moved."""
         if self.gen != _GEN[0]:
             self.params = list(model.parameters())
             self.modules = [m for m in model.modules() if m is not model]
-            self.key = tuple((id(p), p.data_ptr()) for p in self.params)
             self.gen = _GEN[0]
         return self
 
@@ -182,8 +181,11 @@ def pad_mols_for(Np):
 
 def _param_key(model):
     """Identity and storage of the model's live parameters: a replaced Parameter object
-    (load_state_dict(assign=True), a swapped submodule) or moved storage re-captures the bucket."""
-    return _state(model).structure(model).key
+    (load_state_dict(assign=True), a swapped submodule) or moved storage re-captures the bucket.
+    The parameter list is cached (rebuilt when _GEN moves), the storage pointers are read every
+    call: `p.data = ...` (vector_to_parameters, an EMA / SWA swap) or a submodule's .to() / .half()
+    moves a parameter's storage without registering anything."""
+    return tuple((id(p), p.data_ptr()) for p in _state(model).structure(model).params)
 
 
 def _amp_key():
@@ -316,12 +318,7 @@ class _Replay(torch.autograd.Function):
                             "same shape bucket (or its backward already ran); run one backward per forward, or "
                             "set AIMX_AUTOGRAPH=0")
         b.gout[:ctx.G].copy_(gout)
-        # the replay overwrites the static gradient tensors: keep what a caller that did not
-        # set .grad to None expects to accumulate onto
-        keep = {}
-        for p, sg in zip(b.params, b.grads):
-            if sg is not None and p.grad is sg:
-                keep[id(p)] = sg.clone()
+        _move_aliased_grads(b)
         b.g_bwd.replay()
         b.done = ctx.gen
         for p, sg in zip(b.params, b.grads):
@@ -329,14 +326,23 @@ class _Replay(torch.autograd.Function):
                 continue
             if p.grad is None:
                 p.grad = sg                      # zero_grad(set_to_none=True): the fast path
-            elif p.grad is sg:
-                sg.add_(keep[id(p)])
             else:
                 p.grad.add_(sg)
         return None, None, None
 
 
 _RT_KEYS = __import__("itertools").count()
+
+
+def _move_aliased_grads(b):
+    """A .grad still sharing storage with its static gradient (handed out as the tensor itself or a
+    view of it by an earlier step and not reset since: accumulation, DDP no_sync micro-batches)
+    would be overwritten by the replay and then accumulated onto itself (2 g_new instead of
+    g_old + g_new): move it out first."""
+    for p, sg in zip(b.params, b.grads):
+        if sg is not None and p.grad is not None and p.grad.untyped_storage().data_ptr() == \
+                sg.untyped_storage().data_ptr():
+            p.grad = p.grad.clone()
 
 
 class _ReplayDDP(torch.autograd.Function):
@@ -359,18 +365,21 @@ class _ReplayDDP(torch.autograd.Function):
                             "same shape bucket (or its backward already ran); run one backward per forward, or "
                             "set AIMX_AUTOGRAPH=0")
         b.gout[:ctx.G].copy_(gout)
-        keep = {}
-        for p, sg in zip(b.params, b.grads):
-            if sg is not None and p.grad is sg:
-                keep[id(p)] = sg.clone()
+        _move_aliased_grads(b)
         b.g_bwd.replay()
         b.done = ctx.gen
-        rt = b.__dict__.get("_rt_grads")
-        if rt is None:  # the bucket's static gradients: the same tensors every replay
-            rt = b._rt_grads = {id(p): sg for p, sg in zip(b.params, b.grads) if sg is not None and p is not pa}
-            b._rt_key = next(_RT_KEYS)  # never reused (an id() could be, after the bucket is gone)
-        ctx.sync.reduce_tensors(rt, key=b._rt_key)
+        sync = ctx.sync
+        fresh = all(p.grad is None for p, sg in zip(b.params, b.grads) if sg is not None and p is not pa)
+        if fresh and sync.syncing():
+            # the fast path (zero_grad(set_to_none=True), every backward synced): average the
+            # replay's static gradients in place, then hand them out
+            rt = b.__dict__.get("_rt_grads")
+            if rt is None:  # the bucket's static gradients: the same tensors every replay
+                rt = b._rt_grads = {id(p): sg for p, sg in zip(b.params, b.grads) if sg is not None and p is not pa}
+                b._rt_key = next(_RT_KEYS)  # never reused (an id() could be, after the bucket is gone)
+            sync.reduce_tensors(rt, key=b._rt_key)
         ga = None
+        acc = {}
         for p, sg in zip(b.params, b.grads):
             if sg is None:
                 continue
@@ -378,10 +387,14 @@ class _ReplayDDP(torch.autograd.Function):
                 ga = sg.clone()  # DDP's reducer averages this one (and may write into .grad)
             elif p.grad is None:
                 p.grad = sg
-            elif p.grad is sg:
-                sg.add_(keep[id(p)])
             else:
                 p.grad.add_(sg)
+            if p is not pa:
+                acc[id(p)] = p.grad
+        if not fresh and sync.syncing():
+            # accumulation (earlier micro-batches' gradients, e.g. under ddp.no_sync()): DDP averages
+            # the ACCUMULATED gradient at the synced backward, so this sums first and averages after
+            sync.reduce_tensors(acc)
         return None, None, None, None, ga
 
 
@@ -404,13 +417,7 @@ class _ReplayGrads(torch.autograd.Function):
                             "same shape bucket (or its backward already ran); run one backward per forward, or "
                             "set AIMX_AUTOGRAPH=0")
         b.gout[:ctx.G].copy_(gout)
-        # a .grad still aliasing its static gradient (handed out as a fresh view by an earlier step
-        # and not reset since: accumulation, DDP no_sync micro-batches) would be overwritten by the
-        # replay and then accumulated onto itself (2 g_new instead of g_old + g_new): move it out first
-        for p, sg in zip(b.params, b.grads):
-            if sg is not None and p.grad is not None and p.grad.untyped_storage().data_ptr() == \
-                    sg.untyped_storage().data_ptr():
-                p.grad = p.grad.clone()
+        _move_aliased_grads(b)
         b.g_bwd.replay()
         b.done = ctx.gen
         # every .grad None (zero_grad(set_to_none=True), the default): fresh views of the static

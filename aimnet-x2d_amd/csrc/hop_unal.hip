@@ -933,12 +933,18 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   const int64_t upr = cdiv(D, 4);
   // slices of cu units; the last slice must hold more than a partial last unit (put_raw writes that
   // unit shifted down over the unit before it, which must be in the same slice)
-  int64_t slices = cdiv(upr * 4, w_max), cu = 0, cu_last = 0;
-  for (;; ++slices) {
-    cu = cdiv(upr, slices);
-    slices = cdiv(upr, cu);
-    cu_last = upr - (slices - 1) * cu;
-    if (D % 4 == 0 || D < 4 || slices == 1 || cu_last >= 2) break;
+  // (the requested count s grows monotonically — the realised count cdiv(upr, cu) may be smaller,
+  // so stepping that instead could revisit the same split forever — and a split never found ends
+  // at one slice, which always qualifies)
+  int64_t slices = 1, cu = upr, cu_last = upr;
+  for (int64_t s = cdiv(upr * 4, w_max); s > 1 && s <= upr; ++s) {
+    const int64_t c = cdiv(upr, s), n = cdiv(upr, c), last = upr - (n - 1) * c;
+    if (D % 4 == 0 || D < 4 || n == 1 || last >= 2) {
+      slices = n;
+      cu = c;
+      cu_last = last;
+      break;
+    }
   }
   if (cu_last <= 0) return AIMX_EARG;
   const int64_t split = (out_rpc > 0 && out_rpc < rows) ? out_rpc : rows;

@@ -16,6 +16,8 @@ the reference computes it (gnn.py:288-306): the [x | cis/trans | tetrahedral] fe
 operator (ops.stereo_features, csrc/stereo.hip) feeding stereochemical_embedding_2.
 """
 import os
+import sys
+import weakref
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -31,6 +33,33 @@ from .pooling import create_pooling_layer
 
 
 _FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
+
+
+def _calling_ddp():
+    """The DistributedDataParallel whose constructor is reading GNN._ddp_params_and_buffers_to_ignore
+    (its `self`, a few frames up: the property is read by hasattr/getattr inside DDP.__init__, after
+    DDP has set its process_group), or None when something else reads it."""
+    try:
+        from torch.nn.parallel import DistributedDataParallel
+    except ImportError:  # pragma: no cover
+        return None
+    f = sys._getframe(2)
+    for _ in range(8):
+        if f is None:
+            break
+        s = f.f_locals.get("self")
+        if isinstance(s, DistributedDataParallel):
+            return s
+        f = f.f_back
+    return None
+
+
+def _nondefault_group(pg):
+    """None for the default (world) process group, else the group itself."""
+    import torch.distributed as dist
+    if pg is None or not (dist.is_available() and dist.is_initialized()):
+        return None
+    return None if pg == dist.distributed_c10d._get_default_group() else pg
 
 
 class GNN(nn.Module):
@@ -126,7 +155,9 @@ class GNN(nn.Module):
                 cis_indices, trans_indices)
         _lib.require_device(multi_hop_edge_indices, batch_indices, total_charges)
         if self.training and torch.is_grad_enabled():
-            self._aimx_native_sync()  # wrapped by DDP: our gradient sync exists before the backward
+            sync = self._aimx_native_sync()  # wrapped by DDP: our gradient sync exists before the backward
+            if sync is not None:
+                sync.new_step()
         if autograph.wanted(self, args):  # per-shape-bucket graph replay (aimx/autograph.py; AIMX_AUTOGRAPH=0: off)
             return autograph.run(self, args)
         return self._aimx_forward(*args)
@@ -362,11 +393,19 @@ class GNN(nn.Module):
                 return user
             raise AttributeError("_ddp_params_and_buffers_to_ignore")
         if not self.__dict__.get("_aimx_ddp_native", False):
+            # the wrapper whose constructor is asking: its process group is the one to average over
+            # (DDP(module, process_group=subgroup)) and its require_backward_grad_sync flag says
+            # whether a backward syncs at all (ddp.no_sync() micro-batches)
+            ddp = _calling_ddp()
+            group = _nondefault_group(ddp.process_group) if ddp is not None else None
             self.__dict__["_aimx_ddp_native"] = True
+            self.__dict__["_aimx_ddp_group"] = group
+            self.__dict__["_aimx_ddp_ref"] = weakref.ref(ddp) if ddp is not None else None
             # DDP's constructor broadcasts the start state of what it syncs; this is ours (the same
-            # collective order on every rank: every rank is inside DDP's constructor)
+            # collective order on every member: every member is inside DDP's constructor)
             from utils.distributed import broadcast_parameters
-            broadcast_parameters([p for n, p in self.named_parameters() if n != self._DDP_ANCHOR and n not in user])
+            broadcast_parameters([p for n, p in self.named_parameters() if n != self._DDP_ANCHOR and n not in user],
+                                 0, group)
         return [n for n, _ in self.named_parameters() if n != self._DDP_ANCHOR] + \
             [n for n in user if n not in dict(self.named_parameters())]
 
@@ -382,6 +421,14 @@ class GNN(nn.Module):
         import torch.distributed as dist
         if not (dist.is_available() and dist.is_initialized()):
             return None
+        ref = self.__dict__.get("_aimx_ddp_ref")
+        ddp = ref() if ref is not None else None
+        join = getattr(ddp, "_join_config", None)
+        if join is not None and join.enable:
+            raise _lib.AimxError(
+                "aimx native DDP: DistributedDataParallel.join() (uneven inputs) is not supported by the "
+                "model's own gradient sync; construct the model with AIMX_NATIVE_DDP=0 to let DDP's reducer "
+                "sync every parameter")
         sync = self.__dict__.get("_aimx_sync")
         if sync is None:
             # built once: DDP itself holds the Parameter objects it wrapped, so a wrapped model's
@@ -391,9 +438,12 @@ class GNN(nn.Module):
             params = [p for n, p in named.items() if n != self._DDP_ANCHOR and
                       n not in self.__dict__.get("_aimx_ddp_user_ignore", ())]
             # always: the collectives run at world size 1 too, as DDP's do; auto_finish: the
-            # reference trainer never calls finish() (DDP finalises in an engine callback)
-            sync = GradientSync(params, unused=self.unused_parameters(), always=True, broadcast_params=False,
-                                auto_finish=True)
+            # reference trainer never calls finish() (DDP finalises in an engine callback); the
+            # wrapper's group, and its no_sync() flag as the gate of every backward's sync
+            gate = (lambda r=ref: (r() is None) or bool(r().require_backward_grad_sync)) if ref is not None else None
+            sync = GradientSync(params, process_group=self.__dict__.get("_aimx_ddp_group"),
+                                unused=self.unused_parameters(), always=True, broadcast_params=False,
+                                auto_finish=True, gate=gate)
             sync.anchor_param = named.get(self._DDP_ANCHOR)
             self.__dict__["_aimx_sync"] = sync
         return sync

@@ -190,7 +190,7 @@ class GradientSync:
 
     def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True,
                  first_bucket_mb: float = 1.0, unused=(), always: bool = False, broadcast_params: bool = True,
-                 auto_finish: bool = False):
+                 auto_finish: bool = False, gate=None):
         params = list(params)
         unused = list(unused)
         if broadcast_params:
@@ -243,6 +243,10 @@ class GradientSync:
         # — the reference trainer under DistributedDataParallel — still gets averaged gradients
         self.auto_finish = auto_finish
         self._queued = False
+        # gate: called at a backward's first gradient; False skips that backward's sync altogether
+        # (DistributedDataParallel.no_sync(): the gradients accumulate locally, and the next synced
+        # backward's hooks see — and average — the accumulated .grad, as DDP's reducer does)
+        self.gate = gate
         if self.overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -308,10 +312,25 @@ class GradientSync:
         else:
             self._handles[i] = dist.all_reduce(flat, group=self.group, async_op=True)
 
+    def new_step(self):
+        """Forget a backward that never finished (it raised after its first bucket hook, so the
+        engine dropped the queued finish()): called at every training forward of a wrapped model."""
+        if self._queued or any(h is not None for h in self._handles):
+            self._queued = False
+            self._reset()
+
+    def syncing(self):
+        """Whether the current backward is synced (the gate, DDP's require_backward_grad_sync)."""
+        return self.gate is None or bool(self.gate())
+
     def _on_grad(self, p):
         if self.auto_finish and not self._queued:
+            if not self.syncing():  # a no_sync() backward: every hook of it returns here
+                return
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finish_queued)
+        elif not self.auto_finish and not self.syncing():
+            return
         i = self._bucket_of[id(p)]
         self._pending[i] -= 1
         if self._pending[i] == 0 and self._handles[i] is None:
@@ -389,7 +408,7 @@ class GradientSync:
 
     def finish(self):
         """Complete every bucket's all-reduce and write averaged gradients back into .grad."""
-        if not self.active:
+        if not self.active or not self.syncing():
             self._reset()
             return
         for i in range(len(self.buckets)):

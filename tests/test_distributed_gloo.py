@@ -226,3 +226,71 @@ def test_ddp_wrap_keeps_one_parameter_and_syncs_start_state():
         assert not before and after  # rank 0's parameters everywhere after the wrap
         assert kept == ["output_layer.bias"] and native and n == 73
         assert plain_ignored == 0  # AIMX_NATIVE_DDP=0: DDP keeps every parameter
+
+
+def _fake_backward(params, scale):
+    """A backward whose gradient of every parameter is `scale` (ones · scale): fires the sync's
+    post-accumulate-grad hooks exactly as a model backward does."""
+    loss = sum((p * scale).sum() for p in params)
+    loss.backward()
+
+
+def _ddp_subgroup_and_no_sync(rank, world):
+    """DDP(model, process_group=subgroup) on ranks 1 and 2 of 3: the native sync follows the
+    wrapper's group (start state from the GROUP's rank 0, gradients averaged over the group only),
+    and ddp.no_sync() micro-batches accumulate locally; the next synced backward averages the
+    accumulated gradients (DDP's semantics)."""
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from models import GNN
+    grp = dist.new_group([1, 2])
+    if rank not in (1, 2):
+        dist.barrier()
+        return None
+    torch.manual_seed(100 + rank)
+    m = GNN({"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}, 64, 1)
+    ddp = DDP(m, process_group=grp, find_unused_parameters=True)
+    sync = m._aimx_native_sync()
+    assert sync.group is grp and sync.world == 2
+    params = sync.params
+    # two no_sync micro-batches (local scale rank, then 2*rank), then one synced (3*rank)
+    with ddp.no_sync():
+        sync.new_step()
+        _fake_backward(params, float(rank))
+        sync.new_step()
+        _fake_backward(params, 2.0 * rank)
+    local = params[0].grad.flatten()[0].item()
+    sync.new_step()
+    _fake_backward(params, 3.0 * rank)
+    synced = params[0].grad.flatten()[0].item()
+    try:  # uneven inputs (DDP.join) are refused with a clear error, not silently mis-synced
+        with ddp.join():
+            m._aimx_native_sync()
+        joined = "no error"
+    except Exception as e:
+        joined = type(e).__name__
+    dist.barrier()
+    return local, synced, joined, [p.detach().flatten()[:8].tolist() for p in list(m.parameters())[:2]]
+
+
+def test_ddp_native_sync_follows_group_and_no_sync():
+    out = _run("_ddp_subgroup_and_no_sync", world=3)
+    assert out[0] is None
+    l1, s1, j1, p1 = out[1]
+    l2, s2, j2, p2 = out[2]
+    assert j1 == j2 == "AimxError"
+    assert l1 == 3.0 and l2 == 6.0                 # no_sync: local sums only (1+2, 2+4)
+    assert s1 == s2 == (6.0 + 12.0) / 2            # synced: the accumulated sums averaged over {1, 2}
+    assert p1 == p2  # start state from the group's rank 0
+
+
+def test_param_key_sees_storage_swaps():
+    """autograph re-captures when a parameter's storage moves without any registration
+    (`p.data = ...`: torch.nn.utils.vector_to_parameters, EMA / SWA swaps)."""
+    from aimx import autograph
+    from models import GNN
+    m = GNN({"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}, 64, 1)
+    k0 = autograph._param_key(m)
+    assert autograph._param_key(m) == k0
+    p = next(m.parameters())
+    p.data = p.data.clone()
+    assert autograph._param_key(m) != k0

@@ -237,6 +237,39 @@ def test_autograph_amp_state_and_replaced_parameters():
     assert all(p.grad is not None for n, p in m2.named_parameters() if "long_range" not in n)
 
 
+def test_autograph_recaptures_after_storage_swap():
+    """`p.data = ...` on the same Parameter objects (torch.nn.utils.vector_to_parameters, EMA / SWA
+    weight swaps) registers nothing, but moves the storage a captured graph reads: the next step
+    must re-capture, not replay stale (possibly freed) parameter memory."""
+    from torch.nn.utils import parameters_to_vector, vector_to_parameters
+    from aimx import autograph
+    b = _batches(1, 67)[0]
+    m1 = _model()
+    m2 = _model()
+    m2.load_state_dict(m1.state_dict())
+    autograph.enable(m2)
+    for _ in range(2):  # capture, then replay
+        m2.zero_grad(set_to_none=True)
+        m2(*b.model_args())[0].sum().backward()
+    st = m2.__dict__["_aimx_autograph_state"]
+    old = {id(bk) for bk in st.buckets.values()}
+    with torch.no_grad():
+        vec = parameters_to_vector(m2.parameters()) * 1.25
+        vector_to_parameters(vec, m2.parameters())
+        m1.load_state_dict({k: v * 1.25 for k, v in m1.state_dict().items()})
+    for m in (m1, m2):
+        m.zero_grad(set_to_none=True)
+    o1 = m1(*b.model_args())[0]
+    o2 = m2(*b.model_args())[0]
+    assert not old & {id(bk) for bk in st.buckets.values()}  # the bucket was re-captured
+    assert _rel(o2.detach(), o1.detach()) < 1e-5
+    o1.sum().backward()
+    o2.sum().backward()
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        if p1.grad is not None:
+            assert _rel(p2.grad, p1.grad) < 1e-5, n
+
+
 @pytest.mark.parametrize("slack", [1, 7, 8, 9, 300])
 def test_pad_batch_matches_pad_collated(slack):
     """aimx_pad_batch (one launch) builds exactly aimx.data.pad_collated's static layout: real rows

@@ -360,6 +360,39 @@ def ddp_wrapped(rank, world):
     return _ddp_wrapped(rank, True)
 
 
+def _ddp_no_sync(rank, replay):
+    """Gradient accumulation under the unchanged wrapper: this rank's half batch as two quarter
+    micro-batches, the first under ddp.no_sync() (no collective; local accumulation), the second
+    synced, .grad never reset in between. DDP averages the ACCUMULATED gradient at the synced
+    backward, so the result is twice the full-batch gradient (L1 is a mean per micro-batch)."""
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from aimx import autograph
+    from models import L1Loss
+    q = B_HALF // 2
+    bs = [_qm9_batch(np.arange(rank * B_HALF + i * q, rank * B_HALF + (i + 1) * q)) for i in range(2)]
+    m = _model(seed=rank)
+    autograph.enable(m, replay)
+    ddp = DDP(m, device_ids=[0], find_unused_parameters=True)
+    for p in m.parameters():
+        p.grad = None
+    with ddp.no_sync():
+        out, _, _ = ddp(*bs[0].model_args())
+        L1Loss()(out, bs[0].targets).backward()
+    out, _, _ = ddp(*bs[1].model_args())
+    L1Loss()(out, bs[1].targets).backward()
+    torch.cuda.synchronize()
+    return {"grads": _grads(m), "buckets": len(autograph._state(m).buckets),
+            "unused_grad_none": m.long_range_projection.weight.grad is None}
+
+
+def ddp_no_sync(rank, world):
+    return _ddp_no_sync(rank, True)
+
+
+def ddp_no_sync_eager(rank, world):
+    return _ddp_no_sync(rank, False)
+
+
 def ddp_wrapped_eager(rank, world):
     return _ddp_wrapped(rank, False)
 
@@ -368,7 +401,8 @@ def ddp_wrapped_plain(rank, world):
     return _ddp_wrapped(rank, True, native=False)
 
 
-@pytest.mark.parametrize("fn", ["ddp_wrapped", "ddp_wrapped_eager", "ddp_wrapped_plain"])
+@pytest.mark.parametrize("fn", ["ddp_wrapped", "ddp_wrapped_eager", "ddp_wrapped_plain", "ddp_no_sync",
+                                "ddp_no_sync_eager"])
 def test_ddp_wrapped_drop_in_equals_full_batch(fn):
     """INTEGRATION.md's claim: the reference trainer's DDP wrapping still works on this GNN —
     with the autograph's graph replay (default) and eagerly — and two ranks' averaged gradients
@@ -380,8 +414,11 @@ def test_ddp_wrapped_drop_in_equals_full_batch(fn):
     o, _, _ = m(*b.model_args())
     L1Loss()(o, b.targets).backward()
     full = _grads(m)
+    if "no_sync" in fn:  # two micro-batches' L1 means accumulated: twice the full-batch mean's gradient
+        full = {k: 2 * v for k, v in full.items()}
     for r in range(2):
-        assert out[r]["buckets"] == (0 if fn == "ddp_wrapped_eager" else 1), out[r]["buckets"]
+        if "no_sync" not in fn:
+            assert out[r]["buckets"] == (0 if fn == "ddp_wrapped_eager" else 1), out[r]["buckets"]
         assert out[r]["unused_grad_none"]
         got = out[r]["grads"]
         assert set(got) == set(full), r

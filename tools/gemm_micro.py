@@ -36,16 +36,23 @@ def bench(fn, it=50):
     return t0.elapsed_time(t1) / (5 * it) * 1e3
 
 
-def run(M, N, K, layout, label, splits=0, torch_ref=True, counters=True):
-    A = torch.randn(M, K, device=dev) if layout[0] == "N" else torch.randn(K, M, device=dev)
-    B = torch.randn(K, N, device=dev) if layout[1] == "N" else torch.randn(N, K, device=dev)
+def run(M, N, K, layout, label, splits=0, torch_ref=True, counters=True, lda=None, ldb=None):
+    """lda / ldb: row strides of A / B as stored (the step's padded or odd strides; default dense)."""
+    if layout[0] == "N":
+        A = torch.randn(M, lda or K, device=dev)[:, :K]
+    else:
+        A = torch.randn(K, lda or M, device=dev)[:, :M]
+    if layout[1] == "N":
+        B = torch.randn(K, ldb or N, device=dev)[:, :N]
+    else:
+        B = torch.randn(N, ldb or K, device=dev)[:, :K]
     C = torch.empty(M, N, device=dev)
     a = _lib.GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.A = A.data_ptr()
-    a.sam, a.sak = (K, 1) if layout[0] == "N" else (1, M)
+    a.sam, a.sak = (A.stride(0), 1) if layout[0] == "N" else (1, A.stride(0))
     a.B = B.data_ptr()
-    a.sbk, a.sbn = (N, 1) if layout[1] == "N" else (1, K)
+    a.sbk, a.sbn = (B.stride(0), 1) if layout[1] == "N" else (1, B.stride(0))
     a.C, a.ldc = C.data_ptr(), N
     a.act, a.dact_kind = -1, -1
     a.splits = splits
@@ -62,6 +69,22 @@ def run(M, N, K, layout, label, splits=0, torch_ref=True, counters=True):
     print(f"{label:28s} M={M:6d} N={N:5d} K={K:6d} {layout}: ours {t_ours:7.1f} us ({fl / t_ours / 1e6:6.1f} TF/s)"
           f"  torch {t_torch:7.1f} us ({fl / t_torch / 1e6:6.1f} TF/s)")
 
+
+if len(sys.argv) > 1 and sys.argv[1] == "big":
+    # the c4 / c5 MFMA-bound GEMMs in the step's layouts (hipBLASLt as a yardstick only): embedding
+    # projection, [Wi; Wg] input projection (K trimmed to the non-empty chunks, weight rows of the
+    # full D(h+1)), its input gradient, the node-update D x D, the concat and its input gradient
+    for M, D, h, H in ((20480, 153, 3, 512), (10240, 307, 6, 1024)):
+        K_ig = D * (h + 1)
+        run(M, H, 256, "NT", f"h{H} embed proj")
+        run(M, 2 * D, 2 * D, "NT", f"h{H} [u|g] fwd (zc)", lda=(K_ig + 3) // 4 * 4, ldb=K_ig)
+        run(M, 2 * D, 2 * D, "NN", f"h{H} [u|g] dF (zc)", lda=(2 * D + 3) // 4 * 4, ldb=K_ig)
+        run(M, D, D, "NT", f"h{H} node fwd")
+        run(M, D, D, "NN", f"h{H} node dX")
+        run(M, H, H, "NT", f"h{H} concat fwd")
+        run(M, H, H, "NN", f"h{H} concat dX")
+        run(H, H + 1, M, "TN", f"h{H} concat dW")
+    sys.exit(0)
 
 if len(sys.argv) > 1 and sys.argv[1] == "slices":
     # per-slice latency: one split, few tiles, K swept (no reduction, idle chip)
