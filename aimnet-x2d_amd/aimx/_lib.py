@@ -241,6 +241,8 @@ _SIGS = {
     "aimx_comm_init": (c_i32, [ctypes.POINTER(c_ptr), c_ptr, c_size, c_i32, c_i32]),
     "aimx_comm_allreduce": (c_i32, [c_ptr, c_ptr, c_i64, c_i32, c_ptr]),
     "aimx_comm_destroy": (c_i32, [c_ptr]),
+    "aimx_comm_version": (c_i32, [ctypes.POINTER(c_i32)]),
+    "aimx_comm_count": (c_i32, [c_ptr, ctypes.POINTER(c_i32)]),
     "aimx_fused_adam": (c_i32, [ctypes.POINTER(AdamTensor), c_i32, ctypes.POINTER(AdamHyper), c_ptr, c_ptr, c_ptr,
                                 c_ptr, c_size, c_ptr]),
 }
@@ -490,6 +492,15 @@ class Comm:
         with torch.cuda.device(dev):
             check(lib.aimx_comm_init(ctypes.byref(h), uid, COMM_ID_BYTES, self.world, self.rank), "comm_init")
         self.handle = h
+        # what the transport itself reports (the bench line's ddp.rccl): RCCL's version and the
+        # communicator's rank count, which must equal the group's world size
+        v, n = c_i32(0), c_i32(0)
+        check(lib.aimx_comm_version(ctypes.byref(v)), "comm_version")
+        check(lib.aimx_comm_count(h, ctypes.byref(n)), "comm_count")
+        if n.value != self.world:
+            raise AimxError(f"aimx.Comm: RCCL communicator has {n.value} ranks, the process group {self.world}")
+        self.info = {"version": f"{v.value // 10000}.{v.value // 100 % 100}.{v.value % 100}",
+                     "nranks": n.value, "library": rccl_path()}
 
     def all_reduce(self, buf, average=True, stream=None):
         """In-place fp32 all-reduce of `buf` on `stream` (default: the current stream)."""

@@ -25,6 +25,8 @@ struct Rccl {
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*get_version)(int*) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
 };
 
 Rccl g_rccl;
@@ -51,7 +53,8 @@ extern "C" int aimx_comm_load(const char* rccl_path) {
   Rccl r;
   r.handle = h;
   if (!bind(h, "ncclGetUniqueId", r.get_unique_id) || !bind(h, "ncclCommInitRank", r.comm_init_rank) ||
-      !bind(h, "ncclAllReduce", r.all_reduce) || !bind(h, "ncclCommDestroy", r.comm_destroy)) {
+      !bind(h, "ncclAllReduce", r.all_reduce) || !bind(h, "ncclCommDestroy", r.comm_destroy) ||
+      !bind(h, "ncclGetVersion", r.get_version) || !bind(h, "ncclCommCount", r.comm_count)) {
     dlclose(h);
     return AIMX_EARG;
   }
@@ -84,6 +87,22 @@ extern "C" int aimx_comm_allreduce(void* comm, float* buf, int64_t count, int32_
   if (count == 0) return AIMX_OK;
   return rc(g_rccl.all_reduce(buf, buf, (size_t)count, ncclFloat32, op == 1 ? ncclAvg : ncclSum, (ncclComm_t)comm,
                               (hipStream_t)stream));
+}
+
+extern "C" int aimx_comm_version(int32_t* version_out) {
+  if (!g_rccl.handle || !version_out) return AIMX_EARG;
+  int v = 0;
+  const int r = rc(g_rccl.get_version(&v));
+  *version_out = v;
+  return r;
+}
+
+extern "C" int aimx_comm_count(void* comm, int32_t* nranks_out) {
+  if (!g_rccl.handle || !comm || !nranks_out) return AIMX_EARG;
+  int n = 0;
+  const int r = rc(g_rccl.comm_count((ncclComm_t)comm, &n));
+  *nranks_out = n;
+  return r;
 }
 
 extern "C" int aimx_comm_destroy(void* comm) {

@@ -650,6 +650,46 @@ def _pdeathsig():
     return setup
 
 
+DEFAULT_DEADLINE_S = 600.0
+
+
+def resolve_deadline(gpus, given):
+    """--deadline as given, else DEFAULT_DEADLINE_S for a multi-GPU run and none at one GPU."""
+    if given is not None:
+        return float(given)
+    return DEFAULT_DEADLINE_S if gpus > 1 else 0.0
+
+
+def exit_code(ddp_check, capture_error):
+    """The command's status after the line is printed: 3 when data-parallel replicas diverged (the
+    numbers are not those of a correct run); 0 otherwise — also when the RCCL all-reduce capture fell
+    back to split graphs, which is a correct run of the split mode that the line labels as such."""
+    if ddp_check is not None and not ddp_check["replicas_identical"]:
+        print("bench: data-parallel replicas diverged (parameter checksums differ across ranks)", file=sys.stderr)
+        return 3
+    if capture_error is not None:
+        print(f"bench: warning: the RCCL all-reduce capture fell back to split graphs ({capture_error}); "
+              "the line reports the split-graph step", file=sys.stderr)
+    return 0
+
+
+def rank_watchdog(deadline_s):
+    """Exit this rank with 124 once `deadline_s` seconds have passed (a daemon timer; a rank that
+    finishes first never hears from it). A collective hung on a lost peer then ends the rank, and its
+    launcher (torchrun, or launch_ranks) stops the others, instead of every rank waiting for the
+    outer timeout. os._exit ends the process where it stands: nothing is exec'd."""
+    import threading
+
+    def expire():
+        print(f"bench: rank {os.environ.get('RANK', '?')}: deadline of {deadline_s:g} s passed (hung collective?); "
+              "exiting 124", file=sys.stderr, flush=True)
+        os._exit(124)
+    t = threading.Timer(deadline_s, expire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def launch_ranks(n, argv, poll_s=0.2, script=None, deadline_s=0.0, straggler_s=300.0):
     """`python bench.py --gpus N` without a launcher: start N rank processes of this same script
     (children, never an exec of this process) and wait for them. This process never touches the
@@ -759,9 +799,11 @@ def main():
     ap.add_argument("--ddp-world1", action="store_true",
                     help="A/B of the data-parallel step on one GPU: a world-size-1 RCCL group with the bucket "
                          "all-reduces kept (GradientSync always=True); AIMX_DDP_GRAPH=capture|split picks the mode")
-    ap.add_argument("--deadline", type=float, default=0.0,
-                    help="self-launched ranks (--gpus N without torchrun): stop every rank and exit 124 after this "
-                         "many seconds (0: none)")
+    ap.add_argument("--deadline", type=float, default=None,
+                    help="multi-GPU runs: every rank exits 124 this many seconds after it started (a hung "
+                         "collective must not wait for an outer timeout), and a self-launched run (--gpus N without "
+                         "torchrun) stops every rank then; 0: none. Default: %g s when --gpus > 1, none at one GPU"
+                         % DEFAULT_DEADLINE_S)
     ap.add_argument("--straggler", type=float, default=300.0,
                     help="self-launched ranks: stop the others and exit 124 this many seconds after the first rank "
                          "finished cleanly (a peer hung in a collective)")
@@ -772,10 +814,15 @@ def main():
     if args.gpus < 1:
         print(f"bench: --gpus {args.gpus} must be >= 1", file=sys.stderr)
         sys.exit(2)
+    args.deadline = resolve_deadline(args.gpus, args.deadline)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        # `python bench.py --gpus N`: start the N ranks here, before anything touches the GPU
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:], deadline_s=args.deadline, straggler_s=args.straggler))
+        # `python bench.py --gpus N`: start the N ranks here, before anything touches the GPU (the
+        # launcher's own deadline a little after the ranks', so a rank's own exit is what it reports)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], deadline_s=args.deadline + 30 if args.deadline else 0.0,
+                              straggler_s=args.straggler))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and args.deadline:
+        rank_watchdog(args.deadline)
     if world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a {world}-rank run as "
               f"{args.gpus} GPUs", file=sys.stderr)
@@ -985,6 +1032,9 @@ def main():
             line["ddp"] = {"world_size_reported": dist.get_world_size(), "backend": dist.get_backend(),
                            "graph_mode": graphed.mode if graphed is not None else "eager",
                            "capture_fallback": graphed is not None and graphed.capture_error is not None,
+                           "capture_error": (str(graphed.capture_error)[:300] if graphed is not None and
+                                             graphed.capture_error is not None else None),
+                           "rccl": getattr(sync.comm, "info", None),
                            "buckets": len(sync.buckets),
                            "bucket_mb": [round(sum(p.numel() for p in bk) * 4 / 2 ** 20, 3) for bk in sync.buckets],
                            **ddp_check}
@@ -995,16 +1045,10 @@ def main():
         if ddp_check is not None and not ddp_check["replicas_identical"]:
             line["invalid"] = "data-parallel replicas diverged"
         print(json.dumps(line), flush=True)
-    # a data-parallel run that diverged, or whose RCCL capture fell back to split graphs, is reported
-    # above and then fails the command (every rank knows both facts)
-    rc = 0
-    if ddp_check is not None and not ddp_check["replicas_identical"]:
-        print("bench: data-parallel replicas diverged (parameter checksums differ across ranks)", file=sys.stderr)
-        rc = 3
-    elif graphed is not None and graphed.capture_error is not None:
-        print(f"bench: the RCCL all-reduce capture fell back to split graphs ({graphed.capture_error})",
-              file=sys.stderr)
-        rc = 4
+    # a data-parallel run that diverged is reported above and then fails the command (every rank knows
+    # it). An RCCL capture that fell back to split graphs is a valid measurement of the split mode: the
+    # line says so (ddp.graph_mode "split", ddp.capture_error) and the command succeeds
+    rc = exit_code(ddp_check, graphed.capture_error if graphed is not None else None)
     if dist.is_initialized():
         dist.destroy_process_group()
     if rc:

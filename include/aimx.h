@@ -596,6 +596,10 @@ int aimx_comm_unique_id(void* id_out, size_t bytes);
 int aimx_comm_init(void** comm_out, const void* id, size_t bytes, int32_t nranks, int32_t rank);
 int aimx_comm_allreduce(void* comm, float* buf, int64_t count, int32_t op, aimx_stream_t stream);
 int aimx_comm_destroy(void* comm);
+/* The bound RCCL's version (ncclGetVersion: major*10000 + minor*100 + patch) and a communicator's
+ * rank count (ncclCommCount): the bench line reports what the transport itself says. */
+int aimx_comm_version(int32_t* version_out);
+int aimx_comm_count(void* comm, int32_t* nranks_out);
 
 #ifdef __cplusplus
 }

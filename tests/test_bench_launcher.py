@@ -169,3 +169,34 @@ def test_padded_static_layouts_on_cpu(config, buckets):
             assert n % q == 0 and n >= b.real_atoms + 2
         assert b.real_graphs == 12 and b.total_charges.shape[0] > 12
         assert not b.total_charges[12:].any()
+
+
+def test_multi_gpu_runs_get_a_default_deadline():
+    assert bench.resolve_deadline(1, None) == 0.0
+    assert bench.resolve_deadline(8, None) == bench.DEFAULT_DEADLINE_S > 0
+    assert bench.resolve_deadline(8, 0) == 0.0 and bench.resolve_deadline(2, 45) == 45.0
+
+
+def test_rank_watchdog_ends_a_hung_rank(tmp_path):
+    """A rank stuck in a collective (here: a sleep) exits 124 at its own deadline, so torchrun (or
+    launch_ranks) sees a failure and stops its peers; a rank that finishes first exits normally."""
+    hung = _script(tmp_path, f"sys.path.insert(0, {ROOT!r}); import bench; bench.rank_watchdog(1.0); time.sleep(60)\n")
+    t0 = time.time()
+    p = subprocess.run([sys.executable, hung], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 124 and time.time() - t0 < 30
+    assert "deadline of 1 s passed" in p.stderr
+    ok = tmp_path / "ok.py"
+    ok.write_text(f"import sys; sys.path.insert(0, {ROOT!r}); import bench; bench.rank_watchdog(30.0); print('done')\n")
+    p = subprocess.run([sys.executable, str(ok)], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and p.stdout.strip() == "done"
+
+
+def test_exit_codes_after_the_line(capsys):
+    """Diverged replicas fail the command (3); an RCCL capture that fell back to split graphs is a
+    valid split-mode measurement (0, with a warning) — the first 8-GPU driver run must yield a record."""
+    assert bench.exit_code(None, None) == 0
+    assert bench.exit_code({"replicas_identical": True}, None) == 0
+    assert bench.exit_code({"replicas_identical": True}, RuntimeError("capture failed")) == 0
+    assert "fell back to split graphs" in capsys.readouterr().err
+    assert bench.exit_code({"replicas_identical": False}, None) == 3
+    assert bench.exit_code({"replicas_identical": False}, RuntimeError("x")) == 3
