@@ -109,8 +109,6 @@ class ShellStackGrad(ctypes.Structure):
         ("d_x_in", c_ptr), ("d_x_in_ld", c_i64),
         ("d_w_ig", c_ptr), ("d_b_ig", c_ptr), ("d_w1", c_ptr), ("d_b1", c_ptr), ("d_w2", c_ptr), ("d_b2", c_ptr),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
-        ("aux_stream", c_ptr), ("events", c_ptr), ("n_events", c_i32),
-        ("aux_mode", c_i32), ("aux_counters", c_ptr), ("n_aux_counters", c_i64),
     ]
 
 
@@ -230,12 +228,12 @@ _SIGS = {
                                       c_ptr]),
     "aimx_l1_loss_backward_padded": (c_i32, [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr,
                                              c_ptr, c_i64, c_ptr]),
-    "aimx_events_create": (c_i32, [c_i32, c_ptr]),
-    "aimx_events_destroy": (c_i32, [c_i32, c_ptr]),
     "aimx_wgrad_grouped_workspace_bytes": (c_size, [ctypes.POINTER(WgradProblem), c_i32]),
     "aimx_wgrad_grouped": (c_i32, [ctypes.POINTER(WgradProblem), c_i32, c_ptr, c_size, c_ptr, c_i64, c_ptr]),
     "aimx_fused_adam_workspace_bytes": (c_size, [ctypes.POINTER(AdamTensor), c_i32]),
     "aimx_multi_copy": (c_i32, [ctypes.POINTER(CopyItem), c_i32, c_ptr]),
+    "aimx_set_option": (c_i32, [ctypes.c_char_p, c_i64]),
+    "aimx_clear_options": (c_i32, []),
     "aimx_comm_load": (c_i32, [ctypes.c_char_p]),
     "aimx_comm_unique_id": (c_i32, [c_ptr, c_size]),
     "aimx_comm_init": (c_i32, [ctypes.POINTER(c_ptr), c_ptr, c_size, c_i32, c_i32]),
@@ -303,64 +301,14 @@ def stream_ptr(device=None):
     return torch.cuda.current_stream(device).cuda_stream
 
 
-_AUX = {}
-N_EVENTS = 64
-
-
-def aux_stream(device):
-    """Per-device auxiliary stream + event handles for the fork/join of independent work (weight
-    gradients beside the activation-gradient chain). Returns (torch stream, ctypes event array).
-    Opt-in (AIMX_AUX=1): measured on MI355X at c2 the forked weight gradients made the captured
-    train step slower (1389 vs 1216 us; c4 3886 vs 3781 us) — the latency-bound activation-gradient
-    chain loses more to the co-running work than the weight gradients gain — so by default
-    (None, None) is returned and the stack runs its single grouped weight-gradient launch."""
-    if os.environ.get("AIMX_AUX", "0") != "1":
-        return None, None
-    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
-    hit = _AUX.get(key)
-    if hit is None:
-        lib = load()
-        ev = (c_ptr * N_EVENTS)()
-        check(lib.aimx_events_create(N_EVENTS, ev), "events_create")
-        hit = (torch.cuda.Stream(device=torch.device("cuda", key)), ev)
-        _AUX[key] = hit
-    return hit
-
-
-_SIDE = {}
-
-
-def side_stream(device):
-    """Per-device side stream + event handles on which the backward's weight gradients run beside
-    the activation-gradient chain (ops.side_fork). Opt-in (AIMX_SIDE_WGRAD=1), single process only:
-    measured on MI355X (profiles/r02_side_wgrad_ab.txt) the forked graph is SLOWER at every config
-    (c2 0.979 -> 1.053 ms, c4 3.53 -> 3.59, c5 5.28 -> 5.35): the activation-gradient chain's
-    kernels already occupy the CUs, so the weight gradients only time-share them and the fork/join
-    costs ~70 us per step."""
-    if os.environ.get("AIMX_SIDE_WGRAD", "0") != "1":
-        return None
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        return None
-    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
-    hit = _SIDE.get(key)
-    if hit is None:
-        lib = load()
-        ev = (c_ptr * N_EVENTS)()
-        check(lib.aimx_events_create(N_EVENTS, ev), "events_create")
-        hit = (torch.cuda.Stream(device=torch.device("cuda", key)), ev)
-        _SIDE[key] = hit
-    return hit
-
-
 _COUNTERS = {}
 N_COUNTERS = 1 << 16
 
 
 def counters(device, slot=0):
-    """Per-device split-K arrival counters: zeroed once, kept zero by the kernels themselves.
-    slot 1: a second array for kernels running concurrently on the side stream (ops.side_fork), so
-    two streams' split-K tickets never share a counter."""
+    """Per-device split-K arrival counters: zeroed once, kept zero by the kernels themselves. A
+    different slot is a separate array (for kernels a caller runs concurrently on another stream:
+    two streams' split-K tickets must never share a counter)."""
     key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
     buf = _COUNTERS.get((key, slot))
     if buf is None:
@@ -400,6 +348,9 @@ def head_sync_timed_out(device):
     return buf is not None and int(buf[0].item()) != 0
 
 
+HEAD_CLUSTER_FORCE = None
+
+
 def head_cluster(F=256):
     """Workgroups per 16-molecule tile of the fused head (F: the ffn width).
 
@@ -410,10 +361,10 @@ def head_cluster(F=256):
     still gives up poisons that launch's outputs with NaN (head.hip cluster_poisoned), so the
     per-step NaN count of the train loop sees it on the step it happens. At F = 512 (c4) the
     chain is 4x the work per tile and 4 workgroups per tile measured best (c4 step 3.278 ms vs
-    3.337 / 3.558 / 3.416 ms with 2 / 1 / 8; profiles/r03_head_f512_ab.txt)."""
-    env = os.environ.get("AIMX_HEAD_CLUSTER")
-    if env is not None:
-        return int(env)
+    3.337 / 3.558 / 3.416 ms with 2 / 1 / 8; profiles/r03_head_f512_ab.txt). HEAD_CLUSTER_FORCE (a
+    module attribute, tests and A/Bs) overrides both."""
+    if HEAD_CLUSTER_FORCE is not None:
+        return int(HEAD_CLUSTER_FORCE)
     if not head_cluster_allowed():
         return 1
     return 4 if F > 256 else 2
@@ -422,7 +373,6 @@ def head_cluster(F=256):
 def head_cluster_allowed():
     """False when other kernels may share the CUs with the clustered head.
 
-    * AIMX_AUX=1: the stack's weight gradients run on an auxiliary stream beside the backward.
     * Several ranks on one GPU (the gloo rehearsal, spawned test ranks): two processes' clustered
       launches can each hold part of the CUs while their partners wait for the rest.
     Data parallelism with one GPU per rank (torchrun: LOCAL_WORLD_SIZE <= the visible GPUs, this
@@ -432,8 +382,6 @@ def head_cluster_allowed():
     optimizer, ahead of the next forward's head (stream order in eager steps, graph edges in
     captured ones). Other ranks' kernels run on other GPUs. A cluster that still times out poisons
     its outputs (see head_cluster)."""
-    if os.environ.get("AIMX_AUX", "0") == "1":
-        return False
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
         return True
@@ -540,3 +488,32 @@ def multi_copy(pairs, device):
     if not pairs:
         return
     multi_copy_items(copy_items(pairs), device)
+
+
+class options:
+    """Set library path options (include/aimx.h aimx_set_option: test hooks such as AIMX_MLPW=0 for
+    the per-GEMM MLP path) for the duration of a with-block; the previous table is restored on exit.
+    The product library reads no environment variable for them."""
+
+    _active = {}
+
+    def __init__(self, **kw):
+        self.kw = {k: int(v) for k, v in kw.items()}
+
+    def __enter__(self):
+        self.saved = dict(options._active)
+        options._active.update(self.kw)
+        _apply_options()
+        return self
+
+    def __exit__(self, *exc):
+        options._active = self.saved
+        _apply_options()
+        return False
+
+
+def _apply_options():
+    lib = load()
+    check(lib.aimx_clear_options(), "clear_options")
+    for k, v in options._active.items():
+        check(lib.aimx_set_option(k.encode(), v), f"set_option {k}")

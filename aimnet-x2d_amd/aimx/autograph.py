@@ -64,7 +64,7 @@ def enable(model, on=True):
 # CSR build cost more than the launches saved (c4: 4.00 vs 3.29 ms eager, c5: 5.64 vs 5.14 ms;
 # profiles/r02_bench_c4.json, r02_bench_c5.json). Gate: atoms x hidden width of the batch (c2 / c3
 # 2.4 M, c4 / c5 10.4 M); an explicit enable(model, True) replays whatever the size.
-MAX_WORK = int(float(os.environ.get("AIMX_AUTOGRAPH_MAX_WORK", "6e6")))
+MAX_WORK = 6_000_000
 
 
 def wanted(model, args):

@@ -64,6 +64,8 @@ def load_h5():
     lib.aimx_h5_open.restype = c_i32
     lib.aimx_h5_open.argtypes = [ctypes.c_char_p, P(c_ptr)]
     lib.aimx_h5_close.argtypes = [c_ptr]
+    lib.aimx_h5_set_direct.restype = None
+    lib.aimx_h5_set_direct.argtypes = [c_i32]
     lib.aimx_h5_info.restype = c_i32
     lib.aimx_h5_info.argtypes = [c_ptr, P(H5Info)]
     lib.aimx_h5_read_store.restype = c_i32

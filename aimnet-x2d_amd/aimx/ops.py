@@ -178,17 +178,6 @@ class _MPStack(torch.autograd.Function):
         gwsb = lib.aimx_shell_stack_backward_workspace_bytes(s)
         buf = torch.empty(max(gwsb // 4, 1), dtype=_F32, device=dev)
         g.workspace, g.workspace_bytes = ptr(buf), buf.numel() * 4
-        aux, events = _lib.aux_stream(dev)
-        side_hit = _lib.side_stream(dev) if aux is None else None
-        if aux is not None and nl + 1 <= _lib.N_EVENTS:
-            g.aux_stream, g.events, g.n_events = aux.cuda_stream, _ct_addr(events), _lib.N_EVENTS
-        elif side_hit is not None:
-            # the stack's grouped weight-gradient launch forks onto the side stream at the end of
-            # the chain (aux_mode 1); the end-of-backward join (side_fork) completes it
-            side = side_fork(dev, buf, st["buf"], d_packed, *dw1, *db1, *dw2, *db2)
-            g.aux_stream, g.events, g.n_events = side.cuda_stream, _ct_addr(side_hit[1]), _lib.N_EVENTS
-            g.aux_mode = 1
-            g.aux_counters, g.n_aux_counters = ptr(_lib.counters(dev, 1)), _lib.N_COUNTERS
         check(lib.aimx_shell_stack_backward(s, g, stream_ptr(dev)), "shell_stack_backward")
         grads = []
         for l in range(nl):
@@ -207,10 +196,8 @@ _PAD = {}
 def _stack_strides(d, k):
     """Row strides of the stack's F [N, K], UG [N, 2D] and MLP activation (R, A) buffers: rounded up
     to 4 floats, so every row is 16-byte aligned and the weight gradients over them take 16-byte loads
-    at odd D (c4 / c5: D = 153 / 307; profiles/r05_wgrad_rows_ab.txt). AIMX_STACK_PAD=0: dense (A/B)."""
+    at odd D (c4 / c5: D = 153 / 307; profiles/r05_wgrad_rows_ab.txt)."""
     r4 = lambda v: -(-v // 4) * 4  # noqa: E731
-    if os.environ.get("AIMX_STACK_PAD", "1") == "0":
-        return k, 2 * d, d
     return r4(k), r4(2 * d), r4(d)
 
 
@@ -615,40 +602,6 @@ def amp_precision():
     return PREC_BF16 if torch.is_autocast_enabled("cuda") else PREC_FP32
 
 
-# ---------------------------------------------------------------------------------------------
-# Weight gradients beside the activation-gradient chain. No weight gradient feeds anything before
-# the optimizer step, so the backward's dW launches (the concat / embedding projections, the
-# stack's grouped launch, the head's grouped launch) run on a side stream forked from the
-# backward's stream, and one join at the END of the backward (an autograd engine callback, so
-# eager steps, captured graphs and DDP hooks all see complete gradients) restores the order.
-# Tensors a side launch reads or writes are record_stream()-ed on the side stream.
-# ---------------------------------------------------------------------------------------------
-_SIDE_PENDING = set()
-
-
-def side_fork(dev, *tensors):
-    """The side stream, made to wait for the current stream; None if side launches are off. The
-    end-of-backward join is queued on the first fork of a backward pass."""
-    hit = _lib.side_stream(dev)
-    if hit is None:
-        return None
-    side, _ = hit
-    cur = torch.cuda.current_stream(dev)
-    side.wait_stream(cur)
-    for t in tensors:
-        if t is not None:
-            t.record_stream(side)
-    key = (torch.device(dev).index, cur.cuda_stream)
-    if key not in _SIDE_PENDING:
-        _SIDE_PENDING.add(key)
-
-        def join(cur=cur, side=side, key=key):
-            cur.wait_stream(side)
-            _SIDE_PENDING.discard(key)
-        torch.autograd.Variable._execution_engine.queue_callback(join)
-    return side
-
-
 def _gemm_args(M, N, K, prec=PREC_FP32):
     a = _lib.GemmArgs()
     a.M, a.N, a.K = M, N, K
@@ -657,20 +610,16 @@ def _gemm_args(M, N, K, prec=PREC_FP32):
     return a
 
 
-def _run_gemm(a, dev, stream=None):
-    """stream: a side stream (ops.side_fork) — the launch then uses the side counter array and its
-    workspace is recorded on that stream."""
+def _run_gemm(a, dev):
     import ctypes
     lib = _lib.load()
-    a.counters, a.n_counters = ptr(_lib.counters(dev, 0 if stream is None else 1)), _lib.N_COUNTERS
+    a.counters, a.n_counters = ptr(_lib.counters(dev)), _lib.N_COUNTERS
     wsb = lib.aimx_gemm_workspace_bytes(ctypes.byref(a))
     ws = None
     if wsb:
         ws = torch.empty(wsb // 4 + 1, dtype=_F32, device=dev)
         a.workspace, a.workspace_bytes = ws.data_ptr(), wsb
-        if stream is not None:
-            ws.record_stream(stream)
-    check(lib.aimx_gemm(ctypes.byref(a), stream.cuda_stream if stream is not None else stream_ptr(dev)), "gemm")
+    check(lib.aimx_gemm(ctypes.byref(a), stream_ptr(dev)), "gemm")
     return ws
 
 
@@ -690,9 +639,8 @@ def gemm_linear_fwd(x, ldx, W, b, out, ldo, act=-1, pre=None, prec=PREC_FP32):
     return _run_gemm(a, x.device)
 
 
-def gemm_linear_bwd(dy, ldy, x, ldx, W, dx, dW, db, prec=PREC_FP32, side=False):
-    """dx = dy W ; dW = dy^T x ; db = sum_rows dy (ones-column fusion, split-K).
-    side: dW/db on the side stream (side_fork; only from inside a backward pass)."""
+def gemm_linear_bwd(dy, ldy, x, ldx, W, dx, dW, db, prec=PREC_FP32):
+    """dx = dy W ; dW = dy^T x ; db = sum_rows dy (ones-column fusion, split-K)."""
     M, n_out = dy.shape
     n_in = W.shape[1]
     dev = dy.device
@@ -707,7 +655,7 @@ def gemm_linear_bwd(dy, ldy, x, ldx, W, dx, dW, db, prec=PREC_FP32, side=False):
     a.B, a.sbk, a.sbn = ptr(x), ldx, 1
     a.C, a.ldc = ptr(dW), n_in
     a.ones_col, a.col_out = 1, ptr(db)
-    _run_gemm(a, dev, side_fork(dev, dy, x, dW, db) if side else None)
+    _run_gemm(a, dev)
 
 
 def act_backward(kind, dy, pre):
@@ -744,7 +692,7 @@ class _Linear(torch.autograd.Function):
         dx = torch.empty(x2.shape[0], W.shape[1], dtype=_F32, device=dy.device) if ctx.needs_input_grad[0] else None
         dW = torch.empty_like(W)
         db = torch.empty(W.shape[0], dtype=_F32, device=dy.device)
-        gemm_linear_bwd(dy2, ldy, x2, ctx.ldx, W.contiguous(), dx, dW, db, ctx.prec, side=True)
+        gemm_linear_bwd(dy2, ldy, x2, ctx.ldx, W.contiguous(), dx, dW, db, ctx.prec)
         dx = dx.view(*ctx.shape[:-1], W.shape[1]) if dx is not None else None
         return dx, dW, (db if ctx.has_b else None), None
 
@@ -839,7 +787,7 @@ class _EmbedProject(torch.autograd.Function):
         dE = torch.empty_like(E)
         dW = torch.empty_like(W)
         db = torch.empty(W.shape[0], dtype=_F32, device=dev)
-        gemm_linear_bwd(dpre, dpre.shape[1], E, E.shape[1], W.contiguous(), dE, dW, db, ctx.prec, side=True)
+        gemm_linear_bwd(dpre, dpre.shape[1], E, E.shape[1], W.contiguous(), dE, dW, db, ctx.prec)
         grads = [torch.empty_like(t) for t in tables]
         ts = _tables_struct(ctx.idx, tables, grads)
         wsb = lib.aimx_embedding_backward_workspace_bytes(ctypes.byref(ts), E.shape[0])
@@ -862,15 +810,13 @@ def embed_project(indices, tables, W, b, act=None, split=None, seeds=None):
 # ---------------------------------------------------------------------------------------------
 # Grouped weight gradients (aimx_wgrad_grouped) and the fused LinearBlock (layers.py:170-219)
 # ---------------------------------------------------------------------------------------------
-def wgrad_grouped(problems, side=False):
+def wgrad_grouped(problems):
     """problems: list of (dY [K, M] (ld), X [K, N] (ld), dW [M, N] out, db [M] out or None), all on one
-    device; every dW = dY^T X (and db = sum_k dY) in one launch (side: on the side stream, from
-    inside a backward pass; see side_fork)."""
+    device; every dW = dY^T X (and db = sum_k dY) in one launch."""
     lib = _lib.load()
     n = len(problems)
     arr = (_lib.WgradProblem * n)()
     dev = problems[0][0].device
-    stream = side_fork(dev, *[t for pr in problems for t in pr]) if side else None
     for i, (dy, x, dw, db) in enumerate(problems):
         dy, ldy = _rows(dy)
         x, ldx = _rows(x)
@@ -959,7 +905,7 @@ class _LinearBlock(torch.autograd.Function):
             dx = dx.view(*ctx.shape[:-1], n_in)
         dW1, db1 = torch.empty_like(W1), torch.empty(n_out, dtype=_F32, device=dev)
         dW2, db2 = torch.empty_like(W2), torch.empty(n_out, dtype=_F32, device=dev)
-        wgrad_grouped([(dY, H, dW2, db2), (dV, x2, dW1, db1)], side=True)
+        wgrad_grouped([(dY, H, dW2, db2), (dV, x2, dW1, db1)])
         return dx, dW1, db1, dW2, db2, None, None, None, None
 
 
@@ -1055,8 +1001,8 @@ def l1_loss(pred, target, weights=None, per_sample=False, rows=None, accum=None,
 # ---------------------------------------------------------------------------------------------
 # Fused post-pool head (gnn.py:252-258; MultiLayerPerceptron / LinearBlock layers.py:170-267)
 # ---------------------------------------------------------------------------------------------
-# widest ffn the fused head takes (head.hip kMaxF = 512); AIMX_HEAD_MAX_F lowers it (A/B)
-HEAD_MAX_F = min(512, int(os.environ.get("AIMX_HEAD_MAX_F", "512")))
+# widest ffn the fused head takes (head.hip kMaxF = 512)
+HEAD_MAX_F = 512
 
 
 class _Head(torch.autograd.Function):
@@ -1166,7 +1112,7 @@ class _Head(torch.autograd.Function):
         cat = views[st["icat"]]
         probs.append((gv[ids], views[st["iz"][nb - 1]], grads[2 + 4 * nb], grads[3 + 4 * nb]))
         probs.append((d_out, cat, grads[4 + 4 * nb], grads[5 + 4 * nb]))
-        ws = wgrad_grouped(probs, side=True)
+        ws = wgrad_grouped(probs)
         del ws, gbuf, hws
         return (None, None, d_x0, *grads)
 

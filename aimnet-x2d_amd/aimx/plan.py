@@ -19,8 +19,8 @@ import torch
 from . import _lib
 
 _VALIDATE = os.environ.get("AIMX_VALIDATE", "0") == "1"
-# use the CSR views a DeviceBatch carries from the batch builder (AIMX_HOST_CSR=0: always build)
-_HOST_CSR = os.environ.get("AIMX_HOST_CSR", "1") != "0"
+# use the CSR views a DeviceBatch carries from the batch builder (False: always build on the device)
+_HOST_CSR = True
 _ZERO = {}
 
 

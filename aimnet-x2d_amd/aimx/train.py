@@ -83,6 +83,11 @@ def _restore(saved, optimizer):
             cur.zero_()
 
 
+# test hook (tests/test_gpu_ddp.py sets it inside a rank process): GraphedTrainStep's "capture"
+# attempt raises as a failing RCCL capture would, to exercise the split fallback on any box
+INJECT_CAPTURE_FAILURE = False
+
+
 class GraphedTrainStep:
     """The train step captured as HIP graphs on a static padded batch (see module docstring).
 
@@ -98,8 +103,7 @@ class GraphedTrainStep:
     optimizer state, communicators) and then rewinds the parameters, the optimizer state and the
     dropout counter, so the first call is the reference loop's first step.
 
-    Data-parallel modes (`sync`: a utils.distributed.GradientSync; `ddp_graph` or the
-    AIMX_DDP_GRAPH environment variable picks one):
+    Data-parallel modes (`sync`: a utils.distributed.GradientSync; `ddp_graph` picks one):
       "capture" (default over RCCL): ONE graph holds forward, backward, the bucketed RCCL
           all-reduces (issued by the gradient hooks as their buckets fill, on RCCL's stream, so they
           overlap the rest of the backward — DDP's reducer, reference runner.py:703-707), the
@@ -115,7 +119,7 @@ class GraphedTrainStep:
         # test hook (tests/test_gpu_ddp.py): make the "capture" attempt raise as a failing RCCL build
         # would, to exercise the split fallback on any box
         if inject_capture_failure is None:
-            inject_capture_failure = os.environ.get("AIMX_TEST_CAPTURE_FAIL", "0") == "1"
+            inject_capture_failure = INJECT_CAPTURE_FAILURE
         self.capture_error = None
         self.model, self.criterion, self.optimizer, self.sync = model, criterion, optimizer, sync
         self.warmup = warmup
@@ -147,7 +151,7 @@ class GraphedTrainStep:
                 self.steps.add_(1)
 
         self._fwd_bwd = fwd_bwd
-        mode = ddp_graph or os.environ.get("AIMX_DDP_GRAPH") or "capture"
+        mode = ddp_graph or "capture"
         if mode not in ("capture", "split"):
             raise ValueError(f"ddp_graph must be 'capture' or 'split', not {mode!r}")
         if sync is None or not sync.active:
@@ -325,7 +329,7 @@ def train_epoch(model, batches: Iterable, criterion, optimizer, device, sync=Non
     s, c, n, tmo = t.tolist()
     if tmo != 0:
         raise RuntimeError("aimx: a clustered head launch timed out waiting for its cluster this epoch "
-                           "(results invalid; set AIMX_HEAD_CLUSTER=1)")
+                           "(results invalid; set aimx._lib.HEAD_CLUSTER_FORCE = 1)")
     return (s / c if c > 0 else 0.0), int(n)
 
 

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/aimx.h"
 
@@ -19,6 +20,12 @@ namespace aimx {
 constexpr int kWave = 64;  // CDNA wavefront
 
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Path options (version.hip). The product library reads no environment: an option is its default
+// unless a test set it through aimx_set_option (include/aimx.h: the alternative-path parity tests),
+// and only the tuning build (`make tune`: -DAIMX_TUNING -> lib/libaimx_tune.so, loaded by the tools'
+// A/B runs through AIMX_LIB_PATH) also reads the environment variable of the same name.
+int64_t opt_i64(const char* name, int64_t dflt);
 
 // Activation kinds (reference: src/utils/activation.py:9-34).
 enum Act : int { ACT_NONE = -1, ACT_RELU = 0, ACT_LEAKYRELU = 1, ACT_ELU = 2, ACT_GELU = 3, ACT_SILU = 4 };

@@ -36,10 +36,6 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 32;
-#ifndef AIMX_LDS_PIPE
-#define AIMX_LDS_PIPE 0  // 1: software-pipelined LDS fragment reads (k_wgrad_lds, k_gemm) — measured
-                         // neutral to slower (profiles/r03_lds_pipe_ab.txt), kept for A/B builds
-#endif
 
 // Epilogue over the NE outputs a thread owns, in two phases. epi_load issues every global load
 // the epilogue needs (C for beta, bias, residuals, act' pre-activation, dropout mask) and folds
@@ -215,17 +211,8 @@ __device__ __forceinline__ void zero_tile(const AimxGemmArgs& a, int m0, int n0,
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-// VU (fp32, !V4): the k-contiguous operands whose rows are not 16-byte aligned (c4/c5's D = 153 /
-// 307 activations and weights) are staged with 16-byte loads anyway: each row's 32-k slice is the
-// 9 aligned float4s covering it (descriptor based at the operand's 16-byte-aligned floor), and
-// each float4's components go to their shifted LDS columns, so per slice a thread issues ~2-3
-// 16-byte loads instead of 8 dword loads (the dword path is address-rate bound). Components
-// outside the slice or past K read as zero. The aligned 16-byte granules around valid elements
-// are always mapped, and the descriptor's extent is the granule-rounded end of the operand.
-template <int BM, int BN, bool AK, bool BKC, bool V4, bool BF, bool VU = false>
+template <int BM, int BN, bool AK, bool BKC, bool V4, bool BF>
 __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
-  static_assert(!VU || (!V4 && !BF), "VU is the fp32 dword-path replacement");
-  constexpr bool VUA = VU && AK, VUB = VU && BKC;
   constexpr int BK = kBK;
   constexpr int SH = BK + 8;                       // BF: bf16 row stride of both LDS images
   constexpr int LAH = BM * SH, LBH = BN * SH;      // BF: bf16 elements per stage and operand
@@ -255,13 +242,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       return;
     }
   }
-  // VU: descriptors from the 16-byte-aligned floor of each operand (mis_* floats below it)
-  const uint32_t mis_a = VUA ? (uint32_t)(((uintptr_t)a.A >> 2) & 3) : 0u;
-  const uint32_t mis_b = VUB ? (uint32_t)(((uintptr_t)a.B >> 2) & 3) : 0u;
-  const __amdgpu_buffer_rsrc_t ra_ =
-      VUA ? make_rsrc(a.A - mis_a, (a_bytes + 4u * mis_a + 15u) & ~15u) : make_rsrc(a.A, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb_ =
-      VUB ? make_rsrc(a.B - mis_b, (b_bytes + 4u * mis_b + 15u) & ~15u) : make_rsrc(a.B, b_bytes);
+  const __amdgpu_buffer_rsrc_t ra_ = make_rsrc(a.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb_ = make_rsrc(a.B, b_bytes);
   const uint32_t sam = (uint32_t)a.sam, sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
 
   // Per-thread fixed coordinates of the staging pattern.
@@ -301,38 +283,15 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   }
 
   constexpr int NA4 = V4 ? BM * BK / 1024 : 1, NB4 = V4 ? BN * BK / 1024 : 1;
-  // VU: float4 q (< rows * 9) of an operand's slice is (row q / 9, aligned float4 q % 9)
-  constexpr int VQ = BK / 4 + 1;
-  constexpr int NVA = VUA ? (BM * VQ + 255) / 256 : 1, NVB = VUB ? (BN * VQ + 255) / 256 : 1;
   struct Regs {
-    float a[VUA ? 1 : NA];
-    float b[VUB ? 1 : NB];
-    floatx4 va[NVA];
-    floatx4 vb[NVB];
-    int k0;  // the slice's first k (VU: sets each row's shift at the LDS store)
+    float a[NA];
+    float b[NB];
+    int k0;  // the slice's first k
   };
   auto load_slice = [&](int k0, bool tail, Regs& R) {
-    float(&ra)[VUA ? 1 : NA] = R.a;
-    float(&rb)[VUB ? 1 : NB] = R.b;
+    float(&ra)[NA] = R.a;
+    float(&rb)[NB] = R.b;
     R.k0 = k0;
-    if constexpr (VUA) {
-#pragma unroll
-      for (int i = 0; i < NVA; ++i) {
-        const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
-        const uint32_t p0 = mis_a + (uint32_t)(m0 + row) * sam + (uint32_t)k0;
-        const bool ok = q < BM * VQ;
-        R.va[i] = bload4(ra_, ok ? 4u * ((p0 & ~3u) + 4u * (uint32_t)j) : 0xFFFFFFF0u, 0);
-      }
-    }
-    if constexpr (VUB) {
-#pragma unroll
-      for (int i = 0; i < NVB; ++i) {
-        const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
-        const uint32_t p0 = mis_b + (uint32_t)(n0 + row) * sbn + (uint32_t)k0;
-        const bool ok = q < BN * VQ;
-        R.vb[i] = bload4(rb_, ok ? 4u * ((p0 & ~3u) + 4u * (uint32_t)j) : 0xFFFFFFF0u, 0);
-      }
-    }
     if constexpr (V4) {
 #pragma unroll
       for (int i = 0; i < NA4; ++i) {
@@ -363,8 +322,7 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
     }
     (void)tail;
     // A
-    if constexpr (VUA) {
-    } else if (AK) {
+    if (AK) {
       const uint32_t voff = 4u * ((uint32_t)(m0 + a_m) * sam + (uint32_t)(k0 + a_k));
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
@@ -378,8 +336,7 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
       }
     }
     // B
-    if constexpr (VUB) {
-    } else if (BKC) {
+    if (BKC) {
       const uint32_t voff = 4u * ((uint32_t)(n0 + b_n) * sbn + (uint32_t)(k0 + b_k));
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -398,7 +355,7 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   // hop chunk begins) are made here, where the data is needed anyway: in load_slice hipcc placed
   // them right after the loads and waited for each load at issue.
   auto store_slice = [&](const Regs& R, int stage) {
-    float ra[VUA ? 1 : NA], rb[VUB ? 1 : NB];
+    float ra[NA], rb[NB];
     {
       const int k0 = R.k0;
       const bool tail = k0 + BK > kend;
@@ -424,77 +381,23 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
           }
         }
       } else {
-        if constexpr (!VUA) {
-#pragma unroll
-          for (int i = 0; i < NA; ++i) {
-            const bool ok = AK ? (!tail || k0 + a_k < kend) : (a_m_ok && (!tail || k0 + a_k + i * A_STEP < kend));
-            ra[i] = ok ? R.a[i] : 0.f;
-          }
-        }
-        if constexpr (!VUB) {
-#pragma unroll
-          for (int i = 0; i < NB; ++i) {
-            if (BKC) {
-              const bool kok = !tail || k0 + b_k < kend;
-              const bool one = a.ones_col && (n0 + b_n + i * B_STEP == N - 1);
-              rb[i] = kok ? (one ? 1.f : R.b[i]) : 0.f;
-            } else {
-              const bool kok = !tail || k0 + b_k + i * B_STEP < kend;
-              rb[i] = kok ? (b_n_one ? 1.f : (b_n_ok ? R.b[i] : 0.f)) : 0.f;
-            }
-          }
-        }
-      }
-    }
-    if constexpr (VU) {
-      float* As = smem + stage * (LA + LB);
-      float* Bs = As + LA;
-      const int kend_rel = kend;  // components at k >= kend are zero
-      const int cur_k0 = R.k0;
-      if constexpr (VUA) {
-#pragma unroll
-        for (int i = 0; i < NVA; ++i) {
-          const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
-          if (q < BM * VQ) {
-            const int m = (int)((mis_a + (uint32_t)(m0 + row) * sam + (uint32_t)cur_k0) & 3u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int kc = 4 * j + e - m;
-              if (kc >= 0 && kc < BK) As[row * SA + kc] = (cur_k0 + kc < kend_rel) ? R.va[i][e] : 0.f;
-            }
-          }
-        }
-      } else {
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
-          const int mm = AK ? a_m + i * A_STEP : a_m;
-          const int kk = AK ? a_k : a_k + i * A_STEP;
-          As[AK ? (mm * SA + kk) : (kk * SA + mm)] = ra[i];
+          const bool ok = AK ? (!tail || k0 + a_k < kend) : (a_m_ok && (!tail || k0 + a_k + i * A_STEP < kend));
+          ra[i] = ok ? R.a[i] : 0.f;
         }
-      }
-      if constexpr (VUB) {
-#pragma unroll
-        for (int i = 0; i < NVB; ++i) {
-          const int q = tid + i * 256, row = q / VQ, j = q - row * VQ;
-          if (q < BN * VQ) {
-            const int m = (int)((mis_b + (uint32_t)(n0 + row) * sbn + (uint32_t)cur_k0) & 3u);
-            const bool one = a.ones_col && (n0 + row == N - 1);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int kc = 4 * j + e - m;
-              if (kc >= 0 && kc < BK) Bs[row * SB + kc] = (cur_k0 + kc < kend_rel) ? (one ? 1.f : R.vb[i][e]) : 0.f;
-            }
-          }
-        }
-      } else {
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
-          const int nn = BKC ? b_n + i * B_STEP : b_n;
-          const int kk = BKC ? b_k : b_k + i * B_STEP;
-          Bs[BKC ? (nn * SB + kk) : (kk * SB + nn)] = rb[i];
+          if (BKC) {
+            const bool kok = !tail || k0 + b_k < kend;
+            const bool one = a.ones_col && (n0 + b_n + i * B_STEP == N - 1);
+            rb[i] = kok ? (one ? 1.f : R.b[i]) : 0.f;
+          } else {
+            const bool kok = !tail || k0 + b_k + i * B_STEP < kend;
+            rb[i] = kok ? (b_n_one ? 1.f : (b_n_ok ? R.b[i] : 0.f)) : 0.f;
+          }
         }
       }
-      return;
     }
     if constexpr (BF) {
       __bf16* Ah = reinterpret_cast<__bf16*>(smem) + stage * (LAH + LBH);
@@ -618,23 +521,6 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
         bf[j] = Bs[BKC ? (nn * SB + kr) : (kr * SB + nn)];
       }
     };
-#if AIMX_LDS_PIPE
-    // fragments of k step s + 1 read before the MFMAs of step s (see k_wgrad_lds)
-    float af[2][TM], bf[2][TN];
-    rd(0, af[0], bf[0]);
-#pragma unroll
-    for (int s = 0; s < BK / 4; ++s) {
-      const int c = s & 1;
-      if (s + 1 < BK / 4) rd(s + 1, af[c ^ 1], bf[c ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[c][i], bf[c][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#else
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       float af[TM], bf[TN];
@@ -644,7 +530,6 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-#endif
   };
 
   // Software pipeline: two register sets and two LDS stages. While slice s is multiplied from
@@ -769,257 +654,238 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   }
 }
 
-// ---- Skinny GEMM: few rows, wide and deep (the post-pool chain's F x F layers at F = 1024) -------
-// Y[M, N] = A[M, K] B with M <= 640 (molecules of one batch) and N, K >= 256 (c5's 258 x 1024 x 1024
-// forward and input-gradient GEMMs, gnn.py:252-258). On k_gemm these ran as 640 split-K blocks
-// with one 32-deep slice in flight each: every block paid ~7 dependent L2/MALL round trips and the
-// launch took 17-20 us for 0.54 GFLOP (16 % MFMA, profiles/r04_c5_step_seq.txt). Here a block owns
-// a 64 x 64 tile and a K range of ~256 (S splits chosen so the full row blocks fill the chip once),
-// and its whole K range is requested up front: LDS-DMA loads (buffer_load ... lds, no registers)
-// into a two-stage ring of 64-deep stages, so while stage s is multiplied stage s + 1 is already
-// landing and stage s + 2 is issued as soon as stage s is consumed (counted vmcnt, raw s_barrier:
-// no vmcnt(0) drain in the loop). One 256-B row per 64 k: the stage images are XOR-swizzled on
-// the SOURCE address (an LDS-DMA writes lane-linear):
-//  * k-contiguous operands ([m][k] or [n][k]): float4 column c of row r at position c ^ (r & 15),
-//    read as k-permuted 16-byte fragments (lane (l & 15, g = l >> 4) holds k = 16s + 4g + j of its
-//    row, MFMA j uses component j) — a 16-lane group covers all 16 positions: conflict-free;
-//  * n-contiguous B ([k][n], the input gradient's W): float4 column c of k row r at position
-//    c ^ (4 * ((r >> 2) & 3)), read as dwords (k rows 16s + 4g + j) — the 4 k-groups of a read land
-//    on disjoint bank quarters.
-// Wave w multiplies rows 16w..16w+15 of the tile by its 64 columns (4 accumulators); waves whose
-// rows are all past M (the last row block of a padded batch) skip the MFMAs. Blocks of full row
-// blocks are numbered first, so the light last row block lands on the CUs' second slots. Split-K
-// slabs are summed by the last-arriving block in slice order (sc1 hand-off as in k_gemm):
-// deterministic. Epilogue: k_gemm's (bias, residuals, activation, pre-activation, dropout).
-constexpr int kSkB = 64;                 // tile edge
-constexpr int kSkKC = 64;                // k per stage
-constexpr int kSkImg = kSkB * kSkKC;     // floats per operand image
-constexpr int kSkStage = 2 * kSkImg;     // floats per stage (A image, then B image)
+// ---- Large-tile GEMM (round 6): the MFMA-bound products of c4 / c5 --------------------------------
+// Y[M, N] = epi(A[M, K] B) with M = atoms (1e4-2e4) and N, K = 256-1024: the embedding projection,
+// the stack's [Wi; Wg] input projections and their input gradients, the concat and its input
+// gradient (gnn.py:224-246, layers.py:82-87). k_gemm's 64 x 64 blocks give each wave a 32 x 32 tile
+// of 16 x 16 x 4 products: two operand reads per MFMA pair and every operand re-read by twice as
+// many blocks — 47-60 % of the fp32 matrix rate at c5. Here:
+//  * a 128 x BN block (BN = 128 or 64), 4 waves in 2 x 2, each wave 64 x BN/2 as 32 x 32 tiles of
+//    v_mfma_f32_32x32x2_f32 (exact fp32, 64 cycles, 16 accumulators per tile);
+//  * operands staged through LDS as k-contiguous rows of 36 floats ([m][k] and [n][k]; an
+//    n-contiguous B is transposed by the staging writes), 32 k per slice, two LDS stages and one
+//    barrier per slice, the next slice's global loads in flight through the current slice's MFMAs;
+//  * fragments by ds_read_b128 in a k-permuted order: lane (r, h) of k-group g reads k = 8g + 4h
+//    .. 8g + 4h + 3 of its row and MFMA j takes component j (A and B agree on the permutation, so
+//    every product pairs the same k; the stride of 36 floats puts a 16-lane group on 16 distinct
+//    4-bank groups);
+//  * 16-byte global loads at any 4-byte alignment (gfx950 executes dwordx4 at 4-byte-aligned
+//    addresses: odd widths such as the D = 307 weight rows need no dword path), 64-bit addressing
+//    (no 2 GiB operand limit); rows / columns past M / N read a clamped valid row (their outputs
+//    are never stored), k past the end of the slice (K, or the non-empty hop chunks) is zeroed;
+//  * blocks walk the N tiles of one row block on one XCD (shared A rows in that XCD's L2);
+//  * k_gemm's epilogue (bias, residuals, activation, pre-activation, dropout, act', masks) through
+//    an LDS transpose of the tile.
+// No split K (M alone fills the chip), no ones column, fp32 only (the AMP path stays on k_gemm).
+struct __attribute__((packed, aligned(4))) GbF4 {
+  float x, y, z, w;
+};
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int kGbBM = 128, kGbBK = 32, kGbS = kGbBK + 4;
 
-__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, float* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+__device__ __forceinline__ floatx4 gb_load(const float* p) {
+  const GbF4 v = *reinterpret_cast<const GbF4*>(p);
+  return floatx4{v.x, v.y, v.z, v.w};
 }
 
-// Tile order: the full (64 x 64) tiles first, then the partial ones (the last column block, e.g. a
-// weight gradient's lone ones column, then the last row block), so light tiles take the CUs' second
-// slots. Tile index t = mb * nb + nbk is the split-K counter / slab index.
-__device__ __forceinline__ void skinny_tile(int b, int M, int N, int& mb, int& nbk) {
-  const int nmF = M / kSkB, nnF = N / kSkB, nm = (M + kSkB - 1) / kSkB;
-  if (b < nmF * nnF) {
-    mb = b % nmF;
-    nbk = b / nmF;
-    return;
-  }
-  b -= nmF * nnF;
-  if (N % kSkB) {  // the partial column block, every row block
-    if (b < nm) {
-      mb = b;
-      nbk = nnF;
+// component e of v, 0 for e outside 0..3 (selects only: a branch here would make hipcc wait for the
+// loads one by one)
+__device__ __forceinline__ float gb_pick(const floatx4& v, int e) {
+  const float lo = (e & 1) ? v[1] : v[0], hi = (e & 1) ? v[3] : v[2];
+  const float x = (e & 2) ? hi : lo;
+  return (unsigned)e < 4u ? x : 0.f;
+}
+
+template <int BN, int NW, bool BKC>
+__global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int tiles_n, int ntiles) {
+  constexpr int BM = kGbBM, BK = kGbBK, S = kGbS, NT = 64 * NW;
+  constexpr int WR = NW / 2;                      // wave rows (2 or 4); two wave columns
+  constexpr int FM = BM / (32 * WR), FN = BN / 64;  // 32 x 32 tiles per wave along m / n
+  constexpr int LA = BM * S, LB = BN * S;         // floats per stage and operand
+  constexpr int NA = BM * BK / 4 / NT;            // A float4s per thread per slice
+  constexpr int NB = BN * BK / 4 / NT;            // B float4s per thread per slice
+  constexpr int RS = NT / 8;                      // k-contiguous rows staged per pass
+  __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
+  static_assert(BM * (BN + 1) <= 2 * (LA + LB), "C tile must fit the staging LDS");
+  static_assert(NA >= 1 && NB >= 1 && FM >= 1 && FN >= 1, "tile geometry");
+
+  // XCD-aware tile order: the blocks one XCD runs (b % 8 equal under round-robin dispatch) take a
+  // contiguous range of tiles, row block major (bijective for any grid size)
+  const int bid = blockIdx.x, nb = (int)gridDim.x;
+  const int q = nb / 8, rr = nb % 8, xcd = bid % 8, loc = bid / 8;
+  const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  if (tile >= ntiles) return;
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int M = (int)a.M, N = (int)a.N;
+  int kend = (int)a.K;
+  if (a.zc_rowptr) {
+    const int zE = zc_extent(a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width);
+    if (a.zc_dim == 0) {
+      kend = min(kend, zE);
+    } else if (n0 >= zE) {
+      if (a.zc_dim == 1)
+        for (int e = tid; e < BM * BN; e += NT) {
+          const int m = m0 + e / BN, n = n0 + e % BN;
+          if (m < M && n < N) a.C[(int64_t)m * a.ldc + n] = 0.f;
+        }
       return;
     }
-    b -= nm;
   }
-  mb = nmF;  // the partial row block, full column blocks
-  nbk = b;
-}
 
-// AK: A k-contiguous ([m][k], sak == 1) or m-contiguous ([k][m], sam == 1: a weight gradient's dY^T);
-// BKC: B k-contiguous ([n][k]) or n-contiguous ([k][n]). a.ones_col (weight gradients, !BKC only):
-// column N - 1 of B is an implicit ones column (the bias gradient), written into the stage image
-// after its DMA has landed.
-// NS: stages in the ring (2: 64 KiB, two blocks per CU; 4: 128 KiB, a block's whole ~256-deep K
-// range in flight at once).
-template <int NS>
-__device__ __forceinline__ void skinny_wait(int in_flight_after) {
-  // vmcnt = 8 DMAs per stage still allowed in flight behind the stage about to be read
-  if (NS > 3 && in_flight_after >= 3)
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if (NS > 2 && in_flight_after == 2)
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (in_flight_after >= 1)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <bool AK, bool BKC, int NS>
-__global__ __launch_bounds__(256) void k_skinny(const AimxGemmArgs a, int kchunk, uint32_t a_bytes, uint32_t b_bytes) {
-  // ONE shared array (a second __shared__ object can make hipcc drain the DMA before each read)
-  __shared__ __attribute__((aligned(16))) float smem[NS * kSkStage];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int M = (int)a.M, N = (int)a.N, K = (int)a.K;
-  const int Nreal = a.ones_col ? N - 1 : N;
-  const int S = (int)gridDim.y;
-  const int nb = (N + kSkB - 1) / kSkB;
-  int mb, nbk;
-  skinny_tile((int)blockIdx.x, M, N, mb, nbk);
-  const int z = (int)blockIdx.y;
-  const int m0 = mb * kSkB, n0 = nbk * kSkB;
-  const int kb = z * kchunk, ke = min(K, kb + kchunk);
-  const int nst = ke > kb ? (ke - kb + kSkKC - 1) / kSkKC : 0;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.B, b_bytes);
-  const uint32_t sam = (uint32_t)a.sam, sak = (uint32_t)a.sak, sbk = (uint32_t)a.sbk, sbn = (uint32_t)a.sbn;
-  const int sub = lane >> 4, pos = lane & 15;
-  const bool ones_here = a.ones_col && Nreal >= n0 && Nreal < n0 + kSkB;
-
-  // stage st (k0 = kb + 64 st) into buffer buf: 8 LDS-DMA instructions per wave (4 A + 4 B, 1 KiB
-  // each = 4 image rows); invalid float4s point past the extent and read 0
-  auto fill = [&](int st, int buf) {
-    float* sa = smem + buf * kSkStage;
-    float* sb = sa + kSkImg;
-    const int k0 = kb + st * kSkKC;
+  // staging coordinates. k-contiguous operands: thread t loads float4 (t & 7) of rows t / 8 + RS i
+  // (8 lanes cover one row's 128 bytes of the slice).
+  const int a_c = tid & 7, a_r = tid >> 3;
+  const float* __restrict__ Ap = a.A;
+  const float* __restrict__ Bp = a.B;
+  const int64_t sam = a.sam, sbn = a.sbn, sbk = a.sbk;
+  int64_t a_row[NA];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = w * 4 + u, row = 4 * t + sub;
-      const int ck = pos ^ (row & 15), kk = k0 + 4 * ck;             // k-contiguous image
-      const int cr = pos ^ (((row >> 2) & 3) << 2), kr = k0 + row;   // k-row image
-      uint32_t oa, ob;
-      if constexpr (AK)
-        oa = (m0 + row < M && kk < ke) ? 4u * ((uint32_t)(m0 + row) * sam + (uint32_t)kk) : kBufDrop;
-      else
-        oa = (kr < ke && m0 + 4 * cr < M) ? 4u * ((uint32_t)kr * sak + (uint32_t)(m0 + 4 * cr)) : kBufDrop;
-      lds_dma16(ra, sa + t * 256, oa);
-      if constexpr (BKC)
-        ob = (n0 + row < Nreal && kk < ke) ? 4u * ((uint32_t)(n0 + row) * sbn + (uint32_t)kk) : kBufDrop;
-      else
-        ob = (kr < ke && n0 + 4 * cr < Nreal) ? 4u * ((uint32_t)kr * sbk + (uint32_t)(n0 + 4 * cr)) : kBufDrop;
-      lds_dma16(rb, sb + t * 256, ob);
+  for (int i = 0; i < NA; ++i) a_row[i] = (int64_t)min(m0 + a_r + RS * i, M - 1) * sam;
+  // BKC: B rows are n (the pattern of A). !BKC: float4 q = tid + NT i is k row (q & 7) +
+  // 8 ((q >> 3) / NC), columns 4 ((q >> 3) % NC): a wave covers 8 k rows x 8 float4 columns, 128
+  // contiguous bytes per k row.
+  constexpr int NC = BN / 4;                      // float4 columns of a k row (!BKC)
+  int64_t b_row[NB];
+  int b_kr[NB], b_nc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    if constexpr (BKC) {
+      b_row[i] = (int64_t)min(n0 + a_r + RS * i, N - 1) * sbn;
+      b_kr[i] = 0;
+      b_nc[i] = 0;
+    } else {
+      const int qq = tid + NT * i;
+      b_kr[i] = (qq & 7) + 8 * (qq / (8 * NC));
+      b_nc[i] = 4 * ((qq >> 3) % NC);
+      b_row[i] = 0;
     }
-  };
-  // the implicit ones column of stage st's B image (k rows past the range read 0)
-  auto put_ones = [&](int st, int buf) {
-    float* sb = smem + buf * kSkStage + kSkImg;
-    const int k0 = kb + st * kSkKC, cn = Nreal - n0;
-    if (tid < kSkKC) {
-      const int r = tid;
-      sb[r * kSkB + (((cn >> 2) ^ (((r >> 2) & 3) << 2)) << 2) + (cn & 3)] = (k0 + r < ke) ? 1.f : 0.f;
-    }
-  };
+  }
 
-  floatx4 acc[4];
+  floatx4 ra[NA], rb[NB];
+  auto load_slice = [&](int k0) {
+    const int kk = min(k0 + 4 * a_c, kend - 4);  // a run that would cross kend starts 4 before it
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const bool active = m0 + 16 * w < M;
-  const int nfa = min(4, (N - n0 + 15) / 16);  // column fragments holding a column < N
-  const int lm = lane & 15, g = lane >> 4;
-  auto compute = [&](int buf) {
-    const float* sa = smem + buf * kSkStage;
-    const float* sb = sa + kSkImg;
+    for (int i = 0; i < NA; ++i) ra[i] = gb_load(Ap + a_row[i] + kk);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      floatx4 av;
-      if constexpr (AK) {
-        av = *reinterpret_cast<const floatx4*>(sa + (16 * w + lm) * kSkKC + (((4 * s + g) ^ lm) << 2));
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (BKC) {
+        rb[i] = gb_load(Bp + b_row[i] + kk);
       } else {
-        const int col = ((((4 * w + (lm >> 2)) ^ (g << 2))) << 2) + (lm & 3);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) av[j] = sa[(16 * s + 4 * g + j) * kSkB + col];
+        const int k = min(k0 + b_kr[i], kend - 1);
+        const int n = min(n0 + b_nc[i], N - 4);     // a run past N starts 4 before it (N >= 4)
+        rb[i] = gb_load(Bp + (int64_t)k * sbk + n);
       }
-      floatx4 bv[4];
+    }
+  };
+  auto store_slice = [&](int k0, int stage) {
+    float* As = smem + stage * (LA + LB);
+    float* Bs = As + LA;
+    const bool ktail = k0 + BK > kend;  // block-uniform
+    const int kk = k0 + 4 * a_c;
+    const int sh = kk - min(kk, kend - 4);  // 0, or how far the run was moved back (4+: all past kend)
 #pragma unroll
-      for (int nf = 0; nf < 4; ++nf) {
-        if constexpr (BKC) {
-          bv[nf] = *reinterpret_cast<const floatx4*>(sb + (16 * nf + lm) * kSkKC + (((4 * s + g) ^ lm) << 2));
-        } else {
-          const int col = ((((4 * nf + (lm >> 2)) ^ (g << 2))) << 2) + (lm & 3);
+    for (int i = 0; i < NA; ++i) {
+      floatx4 v = ra[i];
+      if (ktail) v = floatx4{gb_pick(ra[i], sh), gb_pick(ra[i], sh + 1), gb_pick(ra[i], sh + 2), gb_pick(ra[i], sh + 3)};
+      *reinterpret_cast<floatx4*>(&As[(a_r + RS * i) * S + 4 * a_c]) = v;
+    }
 #pragma unroll
-          for (int j = 0; j < 4; ++j) bv[nf][j] = sb[(16 * s + 4 * g + j) * kSkB + col];
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (BKC) {
+        floatx4 v = rb[i];
+        if (ktail) v = floatx4{gb_pick(rb[i], sh), gb_pick(rb[i], sh + 1), gb_pick(rb[i], sh + 2), gb_pick(rb[i], sh + 3)};
+        *reinterpret_cast<floatx4*>(&Bs[(a_r + RS * i) * S + 4 * a_c]) = v;
+      } else {
+        const int nn = n0 + b_nc[i];
+        const int shn = nn - min(nn, N - 4);
+        const bool kin = k0 + b_kr[i] < kend;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = shn ? gb_pick(rb[i], shn + e) : rb[i][e];
+          Bs[(b_nc[i] + e) * S + b_kr[i]] = kin ? x : 0.f;
         }
       }
-      if (nfa == 4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int nf = 0; nf < 4; ++nf)
-            acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[nf][j], acc[nf], 0, 0, 0);
-      } else {  // a partial column block: only its fragments below N (wave-uniform)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int nf = 0; nf < 4; ++nf)
-            if (nf < nfa) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[nf][j], acc[nf], 0, 0, 0);
-      }
     }
   };
 
+  floatx16 acc[FM][FN];
 #pragma unroll
-  for (int q = 0; q < NS; ++q)
-    if (q < nst) fill(q, q);
-  for (int st = 0; st < nst; ++st) {
-    // this stage's 8 DMAs retired (the later stages' may stay in flight), then every wave's
-    skinny_wait<NS>(min(NS - 1, nst - 1 - st));
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");  // (s_barrier alone does not order memory for the compiler)
-    if (ones_here) {  // after every wave's DMA of the stage has landed
-      put_ones(st, st % NS);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int l32 = lane & 31, h = lane >> 5;
+  auto compute_slice = [&](int stage) {
+    const float* As = smem + stage * (LA + LB);
+    const float* Bs = As + LA;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      floatx4 af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const floatx4*>(&As[(wr * (BM / WR) + i * 32 + l32) * S + 8 * g + 4 * h]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bf[j] = *reinterpret_cast<const floatx4*>(&Bs[(wc * (BN / 2) + j * 32 + l32) * S + 8 * g + 4 * h]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
     }
-    if (active) compute(st % NS);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every read of the buffer done before it is refilled
-    asm volatile("" ::: "memory");
-    if (st + NS < nst) fill(st + NS, st % NS);
+  };
+
+  // one register stage, two LDS stages, one barrier per slice. The loads run unconditionally (a
+  // slice past the end reloads valid addresses and is never stored) so the wait before each store
+  // sees one pending set (see k_gemm).
+  const int nsl = (kend + BK - 1) / BK;
+  if (nsl > 0) {
+    load_slice(0);
+    store_slice(0, 0);
+  }
+  __syncthreads();
+  for (int sl = 0; sl < nsl; ++sl) {
+    const int kn = min(sl + 1, nsl - 1) * BK;
+    load_slice(kn);
+    // the loads stay ahead of the MFMAs (hipcc would otherwise sink them to their use, after the
+    // compute, and every slice would wait one full memory round trip)
+    __builtin_amdgcn_sched_barrier(0);
+    compute_slice(sl & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (sl + 1 < nsl) store_slice(kn, (sl + 1) & 1);
+    __syncthreads();
   }
 
-  if (S > 1) {
-    const int tile = mb * nb + nbk;
-    const int64_t ntiles = (int64_t)((M + kSkB - 1) / kSkB) * nb;
-    constexpr int TILE = kSkB * kSkB;
-    const __amdgpu_buffer_rsrc_t rws = make_rsrc(a.workspace, (uint32_t)(4 * (int64_t)S * ntiles * TILE));
-    const uint32_t slab0 = (uint32_t)(4 * (((int64_t)z * ntiles + tile) * TILE));
+  // C/D of 32x32: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5); transposed through
+  // LDS so the epilogue walks rows with consecutive lanes on consecutive columns
+  constexpr int CS = BN + 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) store_sc1(rws, slab0 + 16u * (uint32_t)(j * 256 + tid), acc[j]);
-    int* flag = reinterpret_cast<int*>(smem);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == S - 1);
-      if (last) __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    const uint32_t zstride = (uint32_t)(4 * ntiles * TILE);
-    const uint32_t tile0 = (uint32_t)(4 * (int64_t)tile * TILE);
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t off = tile0 + 16u * (uint32_t)(j * 256 + tid);
-      floatx4 s = floatx4{0.f, 0.f, 0.f, 0.f};
-      for (int z0 = 0; z0 < S; z0 += 8) {
-        floatx4 t[8];
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) t[q] = load_sc1(rws, (uint32_t)min(z0 + q, S - 1) * zstride + off);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (z0 + q < S) s += t[q];
-      }
-      acc[j] = s;
-    }
-  }
-
-  // C tile through LDS (row-major, stride 65), then k_gemm's epilogue in chunks of 8 per thread
-  constexpr int CS = kSkB + 1;
+      for (int r = 0; r < 16; ++r)
+        smem[(wr * (BM / WR) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CS + wc * (BN / 2) + j * 32 + l32] =
+            acc[i][j][r];
   __syncthreads();
+  constexpr int NE = BM * BN / NT;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) smem[(16 * w + 4 * g + r) * CS + 16 * j + lm] = acc[j][r];
-  __syncthreads();
-#pragma unroll
-  for (int q0 = 0; q0 < 16; q0 += 8) {
+  for (int q0 = 0; q0 < NE; q0 += 8) {
     int qm[8], qn[8];
     float ev[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int e = tid + (q0 + u) * 256;
-      qm[u] = m0 + e / kSkB;
-      qn[u] = n0 + e % kSkB;
-      ev[u] = smem[(e / kSkB) * CS + e % kSkB];
+      const int e = tid + (q0 + u) * NT;
+      qm[u] = m0 + e / BN;
+      qn[u] = n0 + e % BN;
+      ev[u] = smem[(e / BN) * CS + e % BN];
     }
     epilogue_n<8>(a, qm, qn, ev);
   }
@@ -1277,24 +1143,19 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(const WgradTable t, float
               tile, nt, ws + t.ws_off[q], counters ? counters + t.cnt_off[q] : nullptr, red);
 }
 
-// ---- Long-K weight gradients through LDS: 80 x 80 or 160 x 160 output blocks ------------------
+// ---- Long-K weight gradients through LDS: 64 x 64 or 80 x 80 output blocks ---------------------
 // k_wgrad_grouped's waves load their MFMA fragments straight from global memory: one dword load
 // per MFMA, re-read by every 32 x 32 tile of the output, which leaves that kernel address-rate
 // bound (~30 % MFMA issue). Here a workgroup owns a BB x BB block (80: a whole 76 x 76 + bias MLP
-// weight of c2, or a quarter of its input projection; 160: c4's 153 x 154 weight whole, c5's
-// 307 x 308 in four) and a K slice: 32 k rows of dY and X are staged in LDS by 16-byte loads (each
-// element read once per block), prefetched into registers while the previous rows compute; wave w
-// (of BB / 16) owns fragment row w and runs its BB / 16 MFMAs per k step from LDS (A read once,
-// reused across the row). The 160-wide block halves the operand bytes per MFMA (global loads and
-// LDS writes per flop) and gives each wave 10 MFMAs per k step against 11 LDS reads. LDS row
-// strides 80 / 176 floats put the 4 k rows of a fragment read on bank offsets 0/16/32/48:
+// weight of c2, or a quarter of its input projection; 64: four waves, one per SIMD) and a K slice:
+// 32 k rows of dY and X are staged in LDS by 16-byte loads (each element read once per block) in two
+// LDS buffers, prefetched into registers while the previous rows compute; wave w (of BB / 16) owns
+// fragment row w and runs its BB / 16 MFMAs per k step from LDS (A read once, reused across the
+// row). LDS row strides of 80 floats put the 4 k rows of a fragment read on bank offsets 0/16/32/48:
 // conflict-free. Split-K slices are summed as in k_wgrad_grouped (sc1 slabs, last arriver adds
 // them in slice order): deterministic.
 constexpr int kWbK = 32;                             // k rows per LDS fill
-#ifndef AIMX_WBD
-#define AIMX_WBD 2
-#endif
-constexpr int kWbD = AIMX_WBD;                       // LDS fills in flight (register ring)
+constexpr int kWbD = 2;                              // LDS fills in flight (register ring)
 template <int BB>
 struct WbGeom {
   static constexpr int F = BB / 16;                  // fragments per edge = waves per workgroup
@@ -1313,7 +1174,7 @@ struct WbTable {
   uint32_t a_bytes[kWgMaxProb], b_bytes[kWgMaxProb];
   int64_t ws_off[kWgMaxProb], cnt_off[kWgMaxProb];
   AimxWgradProblem p[kWgMaxProb];
-  int32_t xcd;  // XCD-aware work order (AIMX_WGRAD_XCD=0: launch order, for A/B)
+  int32_t xcd;  // XCD-aware work order
 };
 
 #ifdef AIMX_WB_TRACE  // diagnostics build only: per-wave shader-clock totals of k_wgrad_lds phases
@@ -1329,23 +1190,21 @@ __device__ long long g_wb_trace[4][10][5];
 #define WBT(slot, stmt) stmt
 #endif
 
-// DB: two LDS buffers per operand (80-wide blocks only: 40 KiB, four workgroups fill a CU's
-// 160 KiB). Fill s + 1 is written to the idle buffer while fill s computes from the other, so each
+// Two LDS buffers per operand (40 KiB at 80 wide: four workgroups fill a CU's 160 KiB). Fill s + 1 is written to the idle buffer while fill s computes from the other, so each
 // fill costs one workgroup barrier instead of two and the LDS writes overlap other waves' MFMAs.
 // VM: the operands' staging, 1 = 16-byte loads for every problem of the launch, 0 = dword loads for
 // every problem, 2 = per problem (WbTable.v4). With a per-problem branch inside each fetch the
 // paths into the fill loop's head carry different load counts and hipcc waits for all loads there.
 // 80-wide blocks: 5 waves per SIMD (<= 102 VGPRs), so that four workgroups (20 waves, all the LDS)
 // fit a CU; at 108-112 VGPRs only three did
-template <int BB, bool DB, int VM>
+template <int BB, int VM>
 __global__ __launch_bounds__(WbGeom<BB>::T) __attribute__((amdgpu_waves_per_eu(BB == 80 ? 5 : 1)))
 void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
   using G = WbGeom<BB>;
   constexpr int kWbF = G::F, kWbT = G::T, kWbV = G::V, kLd = G::S;
   constexpr int kBuf = kWbK * kLd;  // floats per operand buffer
-  static_assert(!DB || BB <= 80, "double-buffered LDS only for 64- and 80-wide blocks");
-  __shared__ __attribute__((aligned(16))) float sA[(DB ? 2 : 1) * kBuf];
-  __shared__ __attribute__((aligned(16))) float sB[(DB ? 2 : 1) * kBuf];
+  __shared__ __attribute__((aligned(16))) float sA[2 * kBuf];
+  __shared__ __attribute__((aligned(16))) float sB[2 * kBuf];
   // the split-K arrival flag lives in sA: written only after the barrier that ends every LDS read
   int& flag = *reinterpret_cast<int*>(sA);
   int q = 0;
@@ -1453,28 +1312,6 @@ void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
   };
   // the kWbK k rows staged in (sa, sb) into this wave's accumulators
   auto compute = [&](const float* sa, const float* sb) {
-#if AIMX_LDS_PIPE
-    // the fragments of k step k4 + 1 are read from LDS before the MFMAs of step k4 issue (two
-    // register sets; sched_barriers keep that order), so each step's MFMAs wait only for reads
-    // issued one step earlier instead of a full LDS round trip per step
-    float av[2], bv[2][kWbF];
-    auto rd = [&](int k4, int sl) {
-      const int r = (k4 * 4 + lk) * kLd + lm;
-      av[sl] = sa[r + w * 16];
-#pragma unroll
-      for (int j = 0; j < kWbF; ++j) bv[sl][j] = sb[r + j * 16];
-    };
-    rd(0, 0);
-#pragma unroll
-    for (int k4 = 0; k4 < kWbK / 4; ++k4) {
-      const int c = k4 & 1;
-      if (k4 + 1 < kWbK / 4) rd(k4 + 1, c ^ 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], bv[c][j], acc[j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#else
 #pragma unroll
     for (int k4 = 0; k4 < kWbK / 4; ++k4) {
       const int r = (k4 * 4 + lk) * kLd + lm;
@@ -1485,7 +1322,6 @@ void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
 #pragma unroll
       for (int j = 0; j < kWbF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[j], acc[j], 0, 0, 0);
     }
-#endif
   };
 #ifdef AIMX_WB_TRACE
   long long wbt[5] = {0, 0, 0, 0, 0};
@@ -1494,45 +1330,28 @@ void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
 #pragma unroll
   for (int d = 0; d < kWbD; ++d)
     fetch(kb + d * kWbK, ring[d]);
-  if constexpr (DB) {
-    static_assert(kWbD == 2, "the double-buffered schedule keeps two fills in registers");
-    // fill s computes from buffer s & 1; fill s + 1 (loaded two compute periods earlier) goes to
-    // the other buffer first, and its register slot is refilled with fill s + 3
-    WBT(0, put(ring[0], kb, sA, sB));
-    WBT(1, fetch(kb + 2 * kWbK, ring[0]));
+  static_assert(kWbD == 2, "the double-buffered schedule keeps two fills in registers");
+  // fill s computes from buffer s & 1; fill s + 1 (loaded two compute periods earlier) goes to
+  // the other buffer first, and its register slot is refilled with fill s + 3
+  WBT(0, put(ring[0], kb, sA, sB));
+  WBT(1, fetch(kb + 2 * kWbK, ring[0]));
+  WBT(3, __syncthreads());
+  // put and fetch run unconditionally (fills past the slice are zeros, put into the idle
+  // buffer): with them under a condition, the paths into the loop head differ in their pending
+  // loads and hipcc waits for all of them there (vmcnt(0)), ending every fill's prefetch
+  // (sched_barrier: the fills' loads issue before the compute; hipcc would sink them below it)
+  for (int s0 = 0; s0 < nsub; s0 += 2) {
+    WBT(0, put(ring[1], kb + (s0 + 1) * kWbK, sA + kBuf, sB + kBuf));
+    WBT(1, fetch(kb + (s0 + 3) * kWbK, ring[1]));
+    __builtin_amdgcn_sched_barrier(0);
+    WBT(2, compute(sA, sB));
+    WBT(3, __syncthreads());  // fill s0 + 1 visible; every read of buffer 0 done before it is refilled
+    if (s0 + 1 >= nsub) break;
+    WBT(0, put(ring[0], kb + (s0 + 2) * kWbK, sA, sB));
+    WBT(1, fetch(kb + (s0 + 4) * kWbK, ring[0]));
+    __builtin_amdgcn_sched_barrier(0);
+    WBT(2, compute(sA + kBuf, sB + kBuf));
     WBT(3, __syncthreads());
-    // put and fetch run unconditionally (fills past the slice are zeros, put into the idle
-    // buffer): with them under a condition, the paths into the loop head differ in their pending
-    // loads and hipcc waits for all of them there (vmcnt(0)), ending every fill's prefetch
-    // (sched_barrier: the fills' loads issue before the compute; hipcc would sink them below it)
-    for (int s0 = 0; s0 < nsub; s0 += 2) {
-      WBT(0, put(ring[1], kb + (s0 + 1) * kWbK, sA + kBuf, sB + kBuf));
-      WBT(1, fetch(kb + (s0 + 3) * kWbK, ring[1]));
-      __builtin_amdgcn_sched_barrier(0);
-      WBT(2, compute(sA, sB));
-      WBT(3, __syncthreads());  // fill s0 + 1 visible; every read of buffer 0 done before it is refilled
-      if (s0 + 1 >= nsub) break;
-      WBT(0, put(ring[0], kb + (s0 + 2) * kWbK, sA, sB));
-      WBT(1, fetch(kb + (s0 + 4) * kWbK, ring[0]));
-      __builtin_amdgcn_sched_barrier(0);
-      WBT(2, compute(sA + kBuf, sB + kBuf));
-      WBT(3, __syncthreads());
-    }
-  } else {
-    // kWbD fills in flight: fill s lands in register slot s % kWbD, is copied to LDS kWbD - 1
-    // compute periods after its loads were issued, and the slot is refilled with fill s + kWbD
-    for (int s0 = 0; s0 < nsub; s0 += kWbD) {
-#pragma unroll
-      for (int d = 0; d < kWbD; ++d) {
-        const int s = s0 + d;
-        if (s >= nsub) break;
-        __syncthreads();  // the previous rows' MFMA reads are done
-        put(ring[d], kb + s * kWbK, sA, sB);
-        __syncthreads();
-        if (s + kWbD < nsub) fetch(kb + (s + kWbD) * kWbK, ring[d]);
-        compute(sA, sB);
-      }
-    }
   }
 
 #ifdef AIMX_WB_TRACE
@@ -1612,70 +1431,26 @@ struct Plan {
   int bm, bn, splits;
   int64_t kchunk;
   bool wgrad;
-  bool skinny;  // k_skinny (64 x 64 tiles, deep LDS-DMA stages)
 };
-
-// k_skinny applies to fp32 products whose tiled grid is short of the chip: few rows and a wide,
-// deep right operand (A k-contiguous: the post-pool chain's forward / input gradient, M <= 640), or
-// a short-K weight gradient (A m-contiguous, K <= 1024 rows, M and N >= 256), with 16-byte rows
-// and counters for the in-launch split-K reduce. Opt-in (AIMX_SKINNY=1): measured slower than the
-// tiled path at c5 (head forward 18.8-22.7 vs 15.2 us, step 4.115 vs 3.931 ms;
-// profiles/r05_skinny_ab.txt) — one wave per SIMD and two barriers per 64-deep stage leave the
-// MFMA pipe idle between stages. Kept, with its parity tests, for the record.
-bool skinny_ok(const AimxGemmArgs& a) {
-  static const bool off = [] {
-    const char* e = getenv("AIMX_SKINNY");
-    return !(e && atoi(e) == 1);
-  }();
-  if (off || a.precision != AIMX_PREC_FP32 || a.zc_rowptr) return false;
-  const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
-  const bool ak = a.sak == 1, bkc = a.sbk == 1;
-  if (!(ak || a.sam == 1) || !(bkc || a.sbn == 1) || (a.ones_col && bkc)) return false;
-  if (ak ? (a.M < 1 || a.M > 640 || Nreal < 256 || a.K < 256) : (a.K < 1 || a.K > 1024 || a.M < 256 || Nreal < 256))
-    return false;
-  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (!al(a.A) || !al(a.B)) return false;
-  if (ak ? (a.sam % 4 != 0 || a.K % 4 != 0) : (a.sak % 4 != 0 || a.M % 4 != 0)) return false;
-  if (bkc ? (a.sbn % 4 != 0 || a.K % 4 != 0) : (a.sbk % 4 != 0 || Nreal % 4 != 0)) return false;
-  const int64_t tiles = cdiv(a.M, kSkB) * cdiv(a.N, kSkB);
-  return tiles <= 320 && a.counters && tiles <= a.n_counters;
-}
 
 // Weight-gradient layout (A m-contiguous, B n-contiguous) with a long K: k_wgrad.
 inline bool is_wgrad(const AimxGemmArgs& a) {
-  static const bool off = getenv("AIMX_GEMM_NO_WGRAD") != nullptr;  // A/B experiments only
   // (also under AIMX_PREC_BF16: long-K weight gradients stay exact fp32 on k_wgrad — the tiled
   // kernel at these shapes, ~150 workgroups, measured 3-5x slower: profiles/r02_c4_amp_seq.txt)
-  return !off && a.sam == 1 && a.sbn == 1 && a.sak != 1 && a.K >= 512;
+  return a.sam == 1 && a.sbn == 1 && a.sak != 1 && a.K >= 512;
 }
 
-Plan plan_gemm(const AimxGemmArgs& a, bool allow_skinny = true) {
+Plan plan_gemm(const AimxGemmArgs& a) {
   Plan p;
   p.wgrad = false;
-  p.skinny = false;
-  if (allow_skinny && skinny_ok(a)) {
-    // splits so the blocks fill the chip at most once (one 128-KiB block per CU), >= 128 of K each
-    p.skinny = true;
-    p.bm = p.bn = kSkB;
-    const int64_t tiles = cdiv(a.M, kSkB) * cdiv(a.N, kSkB);
-    int64_t sp = a.splits > 0 ? a.splits : std::max<int64_t>(1, 256 / tiles);
-    sp = std::max<int64_t>(1, std::min<int64_t>({sp, 64, a.K / 128}));
-    p.kchunk = cdiv(cdiv(a.K, sp), kSkKC) * kSkKC;
-    p.splits = (int)std::max<int64_t>(1, cdiv(a.K, p.kchunk));
-    return p;
-  }
   if (is_wgrad(a)) {
     // ~1536 waves in flight chip-wide, every wave keeping >= 2 load groups (2 x 32 k) of work
     p.wgrad = true;
     p.bm = p.bn = 32;
     const int64_t t = cdiv(a.M, 32) * cdiv(a.N, 32);
     // ~1150 workgroups (round 5, c2's 256 x 257 x 9170 concat dW: 6 splits 32.7 us, 16 splits
-    // 27.1 us; the 76 x 77 ones 17.8 -> 15.9 us; profiles/r05_lone_wgrad_splits.txt); AIMX_WGRAD_WGS
-    // overrides the target (A/B)
-    static const int64_t target = [] {
-      const char* e = getenv("AIMX_WGRAD_WGS");
-      return e ? std::max(64, atoi(e)) : 1152;
-    }();
+    // 27.1 us; the 76 x 77 ones 17.8 -> 15.9 us; profiles/r05_lone_wgrad_splits.txt)
+    static const int64_t target = std::max<int64_t>(64, opt_i64("AIMX_WGRAD_WGS", 1152));
     int64_t splits = a.splits > 0 ? a.splits : cdiv(target, t);
     splits = std::max<int64_t>(1, std::min<int64_t>({splits, 64, a.K / 256}));
     p.kchunk = cdiv(cdiv(a.K, splits), 16) * 16;
@@ -1710,17 +1485,10 @@ Plan plan_gemm(const AimxGemmArgs& a, bool allow_skinny = true) {
   // 64 x 64, and K >= 1024 products (c5's head GEMMs) on 64 x 64 with split K — per-GEMM step
   // traces in profiles/r02_gemm_tile_ab.txt)
   if (a.M * a.N * a.K < (int64_t)750000000 && a.K < 1024) p.bm = p.bn = 32;
-  if (const char* f = getenv("AIMX_GEMM_TILE")) {  // A/B experiments only: "64x64", "64x32", "32x32"
-    const int fm = atoi(f), fn = atoi(strchr(f, 'x') ? strchr(f, 'x') + 1 : f);
-    if ((fm == 64 && (fn == 64 || fn == 32)) || (fm == 32 && fn == 32)) {
-      p.bm = fm;
-      p.bn = fn;
-    }
-  }
   // Few rows, deep K (c5's post-pool F = 1024 chain, 258 x 1024 x 1024, 16 launches per step): 32 x 32
   // tiles split to ~1700 workgroups beat 64 x 32 split 4 (forward 15.8 -> 13.6 us, input gradient
   // 16.4 -> 14.1 us; the 3 x 8 tile / split sweep in profiles/r05_head_gemm_sweep.txt)
-  const bool deep_few = getenv("AIMX_GEMM_TILE") == nullptr && tiles(64, 32) < 256 && a.K >= 1024 && a.M <= 1024;
+  const bool deep_few = tiles(64, 32) < 256 && a.K >= 1024 && a.M <= 1024;
   if (deep_few) p.bm = p.bn = 32;
   const int64_t t = tiles(p.bm, p.bn);
   int64_t splits = a.splits;
@@ -1765,29 +1533,9 @@ void launch_tile_v(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t 
     hipLaunchKernelGGL((k_gemm<BM, BN, false, false, V4, BF>), grid, dim3(256), 0, s, a, kc, ab, bb);
 }
 
-// The VU staging (k_gemm) for fp32 operands that fail v4_ok with at least one k-contiguous operand:
-// opt-in (AIMX_GEMM_VU=1). Bit-identical to the dword path but measured slower: c4 step 3.34 ->
-// 3.56 ms, c5 4.99 -> 5.86 ms, c3 unchanged (profiles/r03_gemm_vu_ab.txt) — the dword loads were
-// not what bounds these tiles; the shifted dword LDS writes and ~20 more VGPRs cost more.
-bool vu_on() {
-  const char* e = getenv("AIMX_GEMM_VU");  // read per call: tests switch it in one process
-  return e && atoi(e) == 1;
-}
-
 template <int BM, int BN>
 void launch_tile(const AimxGemmArgs& a, const Plan& p, dim3 grid, hipStream_t s, uint32_t ab, uint32_t bb) {
   const bool bf = a.precision == AIMX_PREC_BF16;
-  if (!bf && !v4_ok(a) && (a.sak == 1 || a.sbk == 1) && vu_on()) {
-    const bool ak = (a.sak == 1), bk = (a.sbk == 1);
-    const int kc = (int)p.kchunk;
-    if (ak && bk)
-      hipLaunchKernelGGL((k_gemm<BM, BN, true, true, false, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
-    else if (ak)
-      hipLaunchKernelGGL((k_gemm<BM, BN, true, false, false, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
-    else
-      hipLaunchKernelGGL((k_gemm<BM, BN, false, true, false, false, true>), grid, dim3(256), 0, s, a, kc, ab, bb);
-    return;
-  }
   if (v4_ok(a)) {
     if (bf)
       launch_tile_v<BM, BN, true, true>(a, p, grid, s, ab, bb);
@@ -1811,7 +1559,7 @@ namespace {
 struct WgPlan {
   int tiles_x, tiles_y, splits, kchunk;
   bool lds;    // k_wgrad_lds (bb x bb blocks) instead of k_wgrad_grouped (32 x 32 tiles)
-  int bb;      // k_wgrad_lds block edge: 64, 80 or 160 (wg_bb)
+  int bb;      // k_wgrad_lds block edge: 64 or 80 (wg_bb)
   int64_t slab;  // floats per split-K slab
 };
 // min_wgs > 0 (a lone long-K GEMM routed here): split K further until the launch has about that
@@ -1821,11 +1569,10 @@ struct WgPlan {
 // of a wave's loop, tools/wgrad_trace.py) unless the 64-wide tiling pads the launch's long-K
 // problems to more than 1.25x the block area of 80-wide blocks (c2's 76-wide MLP weights: 2.6x).
 // Measured: c4 2.745 -> 2.635 ms, c5 4.025 -> 3.951 ms with 64; c2 0.722 -> 0.737 ms (kept at 80).
-// AIMX_WGRAD_BB=64 / 80 / 160 forces one (A/B).
+// The test hook AIMX_WGRAD_BB (aimx_set_option) forces 64 or 80.
 int wg_bb(const AimxWgradProblem* p, int32_t n) {
-  const char* e = getenv("AIMX_WGRAD_BB");  // read per call (a few per step): the parity tests switch it
-  const int force = e ? atoi(e) : 0;
-  if (force == 64 || force == 80 || force == 160) return force;
+  const int64_t force = opt_i64("AIMX_WGRAD_BB", 0);  // test hook (aimx_set_option): 64 or 80 forced
+  if (force == 64 || force == 80) return (int)force;
   double a64 = 0, a80 = 0;
   for (int32_t i = 0; i < n; ++i) {
     if (p[i].K < 2048) continue;
@@ -1837,22 +1584,18 @@ int wg_bb(const AimxWgradProblem* p, int32_t n) {
 }
 
 WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs, int bb) {
-  const char* e = getenv("AIMX_WGRAD_LDS");  // =0: A/B experiments only (read per call: graph A/Bs)
-  const bool no_lds = e && atoi(e) == 0;
   WgPlan w;
   const int64_t N = p.col_out ? p.N + 1 : p.N;
-  if (!no_lds && p.K >= 2048) {
+  if (p.K >= 2048) {
     // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks.
-    // 160-wide blocks (AIMX_WGRAD_BB=160, opt-in) measured slower: wgrad launch c4 472 -> 490 us,
-    // c5 853 -> 880 us; steps c2 0.78 -> 0.90, c4 3.30 -> 3.37, c5 4.98 -> 5.11 ms (a quarter of
-    // the workgroups, 109 VGPRs: 4 waves per SIMD; profiles/r03_gemm_ab.txt)
+    // (160-wide blocks measured slower: wgrad launch c4 472 -> 490 us, c5 853 -> 880 us, a quarter
+    // of the workgroups at 109 VGPRs; profiles/r03_gemm_ab.txt — removed in round 6)
     w.lds = true;
     w.bb = bb;  // wg_bb
     w.slab = (int64_t)w.bb * w.bb;
     w.tiles_x = (int)cdiv(p.M, w.bb);
     w.tiles_y = (int)cdiv(N, w.bb);
-    const char* kp = getenv("AIMX_WGRAD_KPER");  // atoms per workgroup (tuning experiments)
-    const int64_t kper = kp ? std::max(64, atoi(kp)) : 512;
+    const int64_t kper = 512;  // atoms per workgroup
     int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
     if (min_wgs > 0)
       sp = std::max(sp, std::min<int64_t>({64, p.K / 128, cdiv(min_wgs, (int64_t)w.tiles_x * w.tiles_y)}));
@@ -1889,12 +1632,7 @@ bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
   if (a.zc_rowptr && a.zc_dim != 1) return false;
   // single long-K weight gradients: from M N K >= 2e9 (c4's 512-wide concat / embedding dW: step
   // 2.873 -> 2.836 ms; c2's 256-wide ones measured +72 us this way, c5's 1024-wide neutral);
-  // AIMX_WGRAD_LDS_GEMM=0 / 1 forces either way (A/B)
-  static const int forced = [] {
-    const char* e = getenv("AIMX_WGRAD_LDS_GEMM");
-    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
-  }();
-  if (forced == 0 || (forced < 0 && (double)a.M * (double)a.N * (double)a.K < 2e9)) return false;
+  if ((double)a.M * (double)a.N * (double)a.K < 2e9) return false;
   pr = AimxWgradProblem{};
   pr.dY = a.A;
   pr.ld_dy = a.sak;
@@ -1916,31 +1654,41 @@ bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
 }
 }  // namespace
 
-// A weight-gradient problem as one unsplit k_skinny launch (no workspace needed), when it applies
-bool wgrad_as_skinny(const AimxWgradProblem& pr, int32_t* counters, int64_t n_counters, AimxGemmArgs& a) {
-  if (pr.zc_rowptr || pr.K < 1) return false;
-  a = AimxGemmArgs{};
-  a.M = pr.M;
-  a.N = pr.col_out ? pr.N + 1 : pr.N;
-  a.K = pr.K;
-  a.A = pr.dY;
-  a.sam = 1;
-  a.sak = pr.ld_dy;
-  a.B = pr.X;
-  a.sbk = pr.ld_x;
-  a.sbn = 1;
-  a.C = pr.dW;
-  a.ldc = pr.ld_dw;
-  a.act = -1;
-  a.dact_kind = -1;
-  a.ones_col = pr.col_out ? 1 : 0;
-  a.col_out = pr.col_out;
-  a.precision = AIMX_PREC_FP32;
-  a.counters = counters;
-  a.n_counters = n_counters;
-  if (!skinny_ok(a)) return false;
-  const Plan p = plan_gemm(a);
-  return p.skinny && p.splits == 1;
+// k_gemm_big applies to the large fp32 products with a k-contiguous A (see the kernel): the tile
+// edge BN (128 or 64) minimises the busiest CU's work, ceil(tiles / CUs) x BN, ties to 128 (fewer
+// operand re-reads). Returns 0 when the product stays on k_gemm.
+int big_bn(const AimxGemmArgs& a) {
+  const int64_t mode = opt_i64("AIMX_GEMM_BIG", 1);  // test hook / tuning build: 0 off, 64 / 128 forced
+  if (mode == 0) return 0;
+  if (a.precision != AIMX_PREC_FP32 || a.ones_col || a.splits > 1) return 0;
+  if (a.sak != 1 || !(a.sbk == 1 || a.sbn == 1)) return 0;
+  if (a.M < 4096 || a.N < 128 || a.K < 128 || a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31))
+    return 0;
+  if (a.zc_rowptr && a.zc_width < kGbBK) return 0;
+  if ((double)a.M * (double)a.N * (double)a.K < 1.5e9) return 0;
+  if (mode == 64 || mode == 128) return (int)mode;
+  const int64_t tm = cdiv(a.M, kGbBM);
+  const int64_t w128 = cdiv(tm * cdiv(a.N, 128), 256) * 128, w64 = cdiv(tm * cdiv(a.N, 64), 256) * 64;
+  return w64 < w128 ? 64 : 128;
+}
+
+int launch_big(const AimxGemmArgs& a, int bn, hipStream_t s) {
+  const int tn = (int)cdiv(a.N, bn);
+  const int nt = (int)(cdiv(a.M, kGbBM) * tn);
+  const bool bkc = a.sbk == 1;
+  // waves per workgroup (test hook / tuning build AIMX_GEMM_BIG_W: 4 or 8)
+  const int nw = opt_i64("AIMX_GEMM_BIG_W", 8) == 4 ? 4 : 8;
+  using Fn = void (*)(const AimxGemmArgs, int, int);
+  Fn fn;
+  if (nw == 8)
+    fn = bn == 128 ? (bkc ? k_gemm_big<128, 8, true> : k_gemm_big<128, 8, false>)
+                   : (bkc ? k_gemm_big<64, 8, true> : k_gemm_big<64, 8, false>);
+  else
+    fn = bn == 128 ? (bkc ? k_gemm_big<128, 4, true> : k_gemm_big<128, 4, false>)
+                   : (bkc ? k_gemm_big<64, 4, true> : k_gemm_big<64, 4, false>);
+  hipLaunchKernelGGL(fn, dim3((unsigned)nt), dim3(64 * nw), 0, s, a, tn, nt);
+  AIMX_CHECK_LAUNCH();
+  return AIMX_OK;
 }
 
 // workspace of the tiled kernels' split-K plan
@@ -1986,6 +1734,7 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
         return wgrad_grouped_run(&pr, 1, a.workspace, a.workspace_bytes, a.counters, a.n_counters, s, kLoneWgs);
     }
   }
+  if (const int bn = big_bn(a)) return launch_big(a, bn, s);
   // operand layouts: each operand must be contiguous along k or along m/n; byte extents < 2 GiB
   if (!(a.sak == 1 || a.sam == 1) || !(a.sbk == 1 || a.sbn == 1)) return AIMX_EARG;
   const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
@@ -1999,26 +1748,6 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   const uint32_t a_bytes = (uint32_t)std::max<int64_t>(a_ext, 4);
   const uint32_t b_bytes = (uint32_t)std::max<int64_t>(b_ext, 4);
   Plan p = plan_gemm(a);
-  if (p.skinny) {
-    const size_t need = p.splits > 1 ? sizeof(float) * (size_t)p.splits * cdiv(a.M, kSkB) * cdiv(a.N, kSkB) * kSkB * kSkB : 0;
-    if (p.splits == 1 || (a.workspace && a.workspace_bytes >= need)) {
-      const dim3 grid((unsigned)(cdiv(a.M, kSkB) * cdiv(a.N, kSkB)), (unsigned)p.splits);
-      const bool ak = a.sak == 1, bkc = a.sbk == 1;
-      // stages in flight: AIMX_SKINNY_NS=2 / 4 (A/B; default 4)
-      static const int ns = [] {
-        const char* e = getenv("AIMX_SKINNY_NS");
-        return (e && atoi(e) == 2) ? 2 : 4;
-      }();
-      auto fn = ns == 4 ? (ak ? (bkc ? k_skinny<true, true, 4> : k_skinny<true, false, 4>)
-                              : (bkc ? k_skinny<false, true, 4> : k_skinny<false, false, 4>))
-                        : (ak ? (bkc ? k_skinny<true, true, 2> : k_skinny<true, false, 2>)
-                              : (bkc ? k_skinny<false, true, 2> : k_skinny<false, false, 2>));
-      hipLaunchKernelGGL(fn, grid, dim3(256), 0, s, a, (int)p.kchunk, a_bytes, b_bytes);
-      AIMX_CHECK_LAUNCH();
-      return AIMX_OK;
-    }
-    p = plan_gemm(a, false);
-  }
   if (p.splits > 1 && (!a.workspace || a.workspace_bytes < sizeof(float) * tiled_workspace_floats(a))) {
     p.splits = 1;
     p.kchunk = std::max<int64_t>(cdiv(a.K, kBK) * kBK, kBK);
@@ -2083,39 +1812,25 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   // problems per launch each); workspace slabs and counters are laid out in problem order
   int64_t ws_off = 0, cnt_off = 0;
   WgradTable t{};
-  WbTable tbs[2] = {};  // 80- and 160-wide problems: one launch family each
-  int32_t blk = 0, blkbs[2] = {0, 0};
-  auto flush = [&](bool lds, int wide = 0) {
+  WbTable tb{};
+  int32_t blk = 0, blkb = 0;
+  auto flush = [&](bool lds) {
     if (lds) {
-      WbTable& tb = tbs[wide];
-      int32_t& blkb = blkbs[wide];
       tb.blk0[tb.n] = blkb;
-      {
-        const char* e = getenv("AIMX_WGRAD_XCD");  // =0: launch order (A/B experiments only)
-        tb.xcd = (e && atoi(e) == 0) ? 0 : 1;
-      }
+      tb.xcd = 1;
       if (blkb > 0) {
-        // double-buffered LDS: 0.5-1.5 % faster at c4 / c5, neutral at c2 (16 fills per workgroup;
-        // profiles/r03_wgrad_dbuf_ab.txt). AIMX_WGRAD_DBUF=0: single-buffered (A/B only; read once)
-        static const bool dbuf = [] {
-          const char* e = getenv("AIMX_WGRAD_DBUF");
-          return !(e && atoi(e) == 0);
-        }();
         int nv4 = 0;
         for (int k = 0; k < tb.n; ++k) nv4 += tb.v4[k] != 0;
         const int vm = nv4 == tb.n ? 1 : (nv4 == 0 ? 0 : 2);
         using WbFn = void (*)(const WbTable, float*, int32_t*);
         WbFn fn;
         const bool narrow = bb == 64;
-        if (wide)
-          fn = vm == 1 ? k_wgrad_lds<160, false, 1> : (vm == 0 ? k_wgrad_lds<160, false, 0> : k_wgrad_lds<160, false, 2>);
-        else if (narrow)
-          fn = vm == 1 ? k_wgrad_lds<64, true, 1> : (vm == 0 ? k_wgrad_lds<64, true, 0> : k_wgrad_lds<64, true, 2>);
-        else if (dbuf)
-          fn = vm == 1 ? k_wgrad_lds<80, true, 1> : (vm == 0 ? k_wgrad_lds<80, true, 0> : k_wgrad_lds<80, true, 2>);
+        // double-buffered LDS (0.5-1.5 % faster at c4 / c5, neutral at c2; profiles/r03_wgrad_dbuf_ab.txt)
+        if (narrow)
+          fn = vm == 1 ? k_wgrad_lds<64, 1> : (vm == 0 ? k_wgrad_lds<64, 0> : k_wgrad_lds<64, 2>);
         else
-          fn = vm == 1 ? k_wgrad_lds<80, false, 1> : (vm == 0 ? k_wgrad_lds<80, false, 0> : k_wgrad_lds<80, false, 2>);
-        const int nthr = wide ? WbGeom<160>::T : narrow ? WbGeom<64>::T : WbGeom<80>::T;
+          fn = vm == 1 ? k_wgrad_lds<80, 1> : (vm == 0 ? k_wgrad_lds<80, 0> : k_wgrad_lds<80, 2>);
+        const int nthr = narrow ? WbGeom<64>::T : WbGeom<80>::T;
         hipLaunchKernelGGL(fn, dim3((unsigned)blkb), dim3(nthr), 0, (hipStream_t)stream, tb, (float*)workspace, counters);
       }
       tb = WbTable{};
@@ -2131,20 +1846,9 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
-    {  // short-K, wide weight gradients (the post-pool chain's F x F at F >= 256): one k_skinny launch
-      AimxGemmArgs ga;
-      if (wgrad_as_skinny(pr, counters, n_counters, ga)) {
-        const int rc = launch_gemm(ga, (hipStream_t)stream);
-        if (rc != AIMX_OK) return rc;
-        continue;
-      }
-    }
     const WgPlan w = wg_plan(pr, min_wgs, bb);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {
-      const int wide = w.bb == 160;
-      WbTable& tb = tbs[wide];
-      int32_t& blkb = blkbs[wide];
       const int k = tb.n++;
       const int64_t Kr = std::max<int64_t>(pr.K, 1) - 1;
       const bool v4 = pr.ld_dy % 4 == 0 && pr.ld_x % 4 == 0 && (uintptr_t)pr.dY % 16 == 0 && (uintptr_t)pr.X % 16 == 0;
@@ -2164,7 +1868,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
       tb.ws_off[k] = ws_off;
       tb.cnt_off[k] = cnt_off;
       blkb += w.splits * nt;
-      if (tb.n == kWgMaxProb) flush(true, wide);
+      if (tb.n == kWgMaxProb) flush(true);
     } else {
       const int k = t.n++;
       t.p[k] = pr;
@@ -2184,8 +1888,7 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
     cnt_off += nt;
   }
   if (t.n) flush(false);
-  if (tbs[0].n) flush(true, 0);
-  if (tbs[1].n) flush(true, 1);
+  if (tb.n) flush(true);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }

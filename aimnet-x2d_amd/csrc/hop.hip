@@ -578,30 +578,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 
 inline bool aligned(const void* p, int bytes) { return ((uintptr_t)p % bytes) == 0; }
 
-int64_t env_i64(const char* name, int64_t dflt) {
-  const char* e = getenv(name);
-  return e ? std::max<int64_t>(0, atoll(e)) : dflt;
-}
-
-// The launcher's A/B knobs, read from the environment once per process (an eager step calls the
-// launcher ~6 times; -1: unset, the launcher's own default applies)
+// The launcher's tuning knobs (opt_i64: defaults in the product library; -1 = the launcher's own
+// default), read once per process (an eager step calls the launcher ~6 times)
 struct HopEnv {
-  int64_t rows_mode, tile_units, big_mul, col_cap, stage_bytes, flat, nt, interleave, spec;
+  int64_t tile_units, big_mul, col_cap, stage_bytes, flat, nt, interleave, spec;
   bool no_seg;
 };
 const HopEnv& hop_env() {
   static const HopEnv e = [] {
     HopEnv v;
-    v.rows_mode = env_i64("AIMX_HOP_ROWS", 1);
-    v.tile_units = env_i64("AIMX_HOP_TILE_UNITS", -1);
-    v.big_mul = env_i64("AIMX_HOP_BIG_MUL", -1);
-    v.col_cap = env_i64("AIMX_HOP_COL_CAP", -1);
-    v.stage_bytes = env_i64("AIMX_HOP_STAGE_BYTES", -1);
-    v.flat = env_i64("AIMX_HOP_FLAT", 1);
-    v.nt = env_i64("AIMX_HOP_NT", 0);
-    v.interleave = env_i64("AIMX_HOP_INTERLEAVE", 1);
-    v.spec = env_i64("AIMX_HOP_SPEC", 1);
-    v.no_seg = getenv("AIMX_HOP_NO_SEG") != nullptr;
+    v.tile_units = opt_i64("AIMX_HOP_TILE_UNITS", -1);
+    v.big_mul = opt_i64("AIMX_HOP_BIG_MUL", -1);
+    v.col_cap = opt_i64("AIMX_HOP_COL_CAP", -1);
+    v.stage_bytes = opt_i64("AIMX_HOP_STAGE_BYTES", -1);
+    v.flat = opt_i64("AIMX_HOP_FLAT", 1);
+    v.nt = opt_i64("AIMX_HOP_NT", 0);
+    v.interleave = opt_i64("AIMX_HOP_INTERLEAVE", 1);
+    v.spec = opt_i64("AIMX_HOP_SPEC", 1);
+    v.no_seg = opt_i64("AIMX_HOP_NO_SEG", 0) != 0;
     return v;
   }();
   return e;
@@ -634,22 +628,12 @@ int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_
     return true;
   };
   const int vec = ok(4) ? 4 : (ok(2) ? 2 : 1);
-  // rows that are not runs of 16-byte vectors (odd D, unaligned chunk offsets) go through LDS to
-  // aligned 16-byte accesses (hop_rows.hip); AIMX_HOP_ROWS=0 keeps them here (dword lanes),
-  // AIMX_HOP_ROWS=2 sends every width there (A/B)
+  // rows that are not runs of 16-byte-aligned vectors (odd D, unaligned chunk offsets) take the
+  // 16-byte-at-4-byte-alignment kernel (hop_unal.hip)
   const HopEnv& E = hop_env();
-  const int64_t rows_mode = E.rows_mode;
-  if ((vec < 4 && rows_mode == 1) || rows_mode == 2) {
-    if (row_seg && gather_regs_on() && launch_gather_regs(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out,
-                                                          out_ld, out_rpc, out_cs, add0, add0_ld, add1, add1_ld,
-                                                          row_seg, row_seg_stride, stream, skip_tail) == AIMX_OK)
-      return AIMX_OK;
-    if (gather_unal_on())
-      return launch_gather_unal(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs,
-                                add0, add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream, skip_tail);
-    return launch_gather_rows(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs, add0,
-                              add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream, skip_tail);
-  }
+  if (vec < 4)
+    return launch_gather_unal(src, src_ld, src_rpc, src_cs, D, rowptr, col, rows, out, out_ld, out_rpc, out_cs,
+                              add0, add0_ld, add1, add1_ld, row_seg, row_seg_stride, stream, skip_tail);
   const int64_t upr_i = D / vec;
   // 32-bit thread indexing (rows * D / vec < 2^31) and int32 chunked row ids.
   if (rows * upr_i >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;

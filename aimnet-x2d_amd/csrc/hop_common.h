@@ -1,4 +1,4 @@
-// Helpers shared by the two hop kernels (hop.hip: 16-byte-aligned rows; hop_rows.hip: any row
+// Helpers shared by the two hop kernels (hop.hip: 16-byte-aligned rows; hop_unal.hip: any row
 // alignment / odd widths). Reference op: ShellConvolutionLayer.message_passing,
 // src/models/layers.py:133-167.
 #pragma once
@@ -29,28 +29,9 @@ __device__ __forceinline__ int64_t row_off(uint32_t r, int64_t ld, const FastDiv
   return (int64_t)(r - q * rpc.d) * ld + (int64_t)q * cstride;
 }
 
-// The odd-width / unaligned-row hop (hop_rows.hip); same contract as aimx_segment_gather_sum.
-// windows = false: only the big tiles of the rows past the first output chunk (hop_regs.hip runs the
-// first chunk's rows).
-int launch_gather_rows(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
-                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
-                       int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
-                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
-                       int32_t skip_tail = 0, bool windows = true);
-
 // The odd-width / unaligned-row hop by 16-byte vectors at 4-byte-aligned addresses (hop_unal.hip);
-// same contract. Default for those rows (AIMX_HOP_UNAL=0: hop_rows.hip).
-bool gather_unal_on();
+// same contract as aimx_segment_gather_sum.
 int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
-                       const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
-                       int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
-                       int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,
-                       int32_t skip_tail);
-
-// The first output chunk's rows summed from the register file, molecule by molecule (hop_regs.hip);
-// needs row_seg. Opt-in: AIMX_HOP_REGS=1 (gather_regs_on; measured slower, see hop_regs.hip).
-bool gather_regs_on();
-int launch_gather_regs(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
                        int64_t out_rpc, int64_t out_cs, const float* add0, int64_t add0_ld, const float* add1,
                        int64_t add1_ld, const int64_t* row_seg, int64_t row_seg_stride, hipStream_t stream,

@@ -1,7 +1,7 @@
 // The hop for rows that are not runs of 16-byte-ALIGNED vectors (odd widths D = int(0.3 * hidden):
 // 153 / 307 at hidden 512 / 1024, reference src/models/gnn.py:100; hop chunks at column offset D of
 // the concatenated [x | chunk_0 | ...] matrix, layers.py:76-79), by 16-byte vectors at 4-byte-aligned
-// addresses. Same contract and bit-exact result as hop.hip / hop_rows.hip (the ordered edge-order sum
+// addresses. Same contract and bit-exact result as hop.hip (the ordered edge-order sum
 // of CPU scatter_add_, layers.py:133-167).
 //
 // gfx950 executes global_load/store_dwordx4 at any 4-byte-aligned address (LLVM emits them for a
@@ -10,8 +10,8 @@
 // own start, whatever its alignment: the 16 bytes at min(c, D - 4) are always inside the row, and
 // the last, partial unit's lanes are moved into place (staging: written shifted into LDS; residual
 // terms: selects); its stores take dwords. In LDS the staged units sit 16-byte aligned, so the sum
-// is ds_read_b128 throughout, and there is no realignment tile (hop_rows.hip's column pass: stage ->
-// sum -> shift through LDS -> store, four barriers per 80-column pass in sequence in one workgroup).
+// is ds_read_b128 throughout, and there is no realignment tile (round 3's hop_rows.hip, removed in round
+// 6: stage -> sum -> shift through LDS -> store, four barriers per 80-column pass in sequence).
 //
 // Work split, as hop.hip's: a workgroup owns a segment-aligned tile (the molecules that start in its
 // nominal window; sources are then the tile's own rows, staged speculatively) and ONE column slice
@@ -41,7 +41,7 @@ constexpr int kUMisc = 129;       // misc words: [0] lo / cut0, [1] hi / cut1, [
 constexpr int kUGroup = 4;        // LDS reads in flight per thread
 
 // Workgroup barrier for LDS hand-offs: waits for this wave's LDS operations only. __syncthreads()'s
-// fence also waits vmcnt(0), draining every global load in flight (the pipelined kernel's prefetch);
+// fence also waits vmcnt(0), draining every global load in flight (loads in flight);
 // no thread here reads another thread's global writes, and an LDS store of loaded data already
 // waits for that load.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -122,7 +122,6 @@ struct UnalArgs {
   uint32_t slices, cu;        // column slices per tile; units per slice (the last may be shorter)
   uint32_t pitch, pitch_l2;   // staged row stride in units (a power of two, >= cu, a multiple of 16)
   int32_t compact;            // thread t owns unit t % cs.d of row t / cs.d instead (row stride cu units)
-  int32_t pair;               // compact: two units of a row per thread (sum_rows_pair)
   FastDiv cu_full, cu_last;   // units of a full / the last slice
   FastDiv upr_f;              // units of a whole row (big tiles)
   uint32_t rows, split;       // tiles cover rows [0, split); big tiles rows [split, rows)
@@ -266,64 +265,10 @@ __device__ __forceinline__ void finish_pre(const UnalArgs& a, uint32_t r, uint32
   st_unit(a.out + row_off(r, a.out_ld, a.out_rpc, a.out_cs), c, a.D, acc);
 }
 
-// sum_rows with two units of a row per thread (k and k + ceil(w / 2), compact layout): one col-offset
-// read from LDS serves two ds_read_b128 (LDS cycles per gathered unit 6 -> 5).
-template <bool ADDS>
-__device__ __forceinline__ void sum_rows_pair(const UnalArgs& a, const int32_t* P, int32_t pbase, const char* cb,
-                                              const char* xb, int32_t zb, uint32_t r0, uint32_t nr, uint32_t u0,
-                                              const FastDiv& cs) {
-  const uint32_t half = (cs.d + 1) >> 1;
-  const FastDiv hf = fastdiv_dev(half);
-  const uint32_t units = nr * half;
-  for (uint32_t t = threadIdx.x; t < units; t += kUT) {
-    const uint32_t rl = fdiv(t, hf);
-    const uint32_t k = t - rl * half;
-    const bool has2 = k + half < cs.d;
-    const uint32_t k2 = has2 ? k + half : k;
-    const uint32_t c = 4 * (u0 + k), c2 = 4 * (u0 + k2);
-    const uint32_t r = r0 + rl;
-    float4 q0, q1, q2, q3;
-    if (ADDS) {
-      q0 = ld_raw(a.q0 + (int64_t)r * a.q0_ld, c, a.D);
-      q1 = ld_raw(a.q1 + (int64_t)r * a.q1_ld, c, a.D);
-      q2 = ld_raw(a.q0 + (int64_t)r * a.q0_ld, c2, a.D);
-      q3 = ld_raw(a.q1 + (int64_t)r * a.q1_ld, c2, a.D);
-    }
-    const uint32_t ub = 16 * k, ub2 = 16 * k2;
-    const int32_t bb = (P[rl] - pbase) * 4, eb = (P[rl + 1] - pbase) * 4;
-    float4 acc = f4z(), acc2 = f4z();
-    for (int32_t kb = bb; kb < eb; kb += 4 * kUGroup) {
-      float4 x[kUGroup], y[kUGroup];
-#pragma unroll
-      for (int q = 0; q < kUGroup; ++q) {
-        const int32_t off = *reinterpret_cast<const int32_t*>(cb + ((kb + 4 * q < eb) ? kb + 4 * q : zb));
-        x[q] = *reinterpret_cast<const float4*>(xb + off + ub);
-        y[q] = *reinterpret_cast<const float4*>(xb + off + ub2);
-      }
-#pragma unroll
-      for (int q = 0; q < kUGroup; ++q) {
-        f4acc(acc, x[q]);
-        f4acc(acc2, y[q]);
-      }
-    }
-    if (ADDS) {
-      finish_pre(a, r, c, q0, q1, acc);
-      if (has2) finish_pre(a, r, c2, q2, q3, acc2);
-    } else {
-      finish_unit(a, r, c, acc);
-      if (has2) finish_unit(a, r, c2, acc2);
-    }
-  }
-}
-
 template <bool ADDS>
 __device__ __forceinline__ void sum_rows(const UnalArgs& a, const int32_t* P, int32_t pbase, const char* cb,
                                          const char* xb, int32_t zb, uint32_t r0, uint32_t nr, uint32_t u0,
                                          const FastDiv& cs, bool compact) {
-  if (compact && a.pair && cs.d >= 2) {
-    sum_rows_pair<ADDS>(a, P, pbase, cb, xb, zb, r0, nr, u0, cs);
-    return;
-  }
   const uint32_t units = compact ? nr * cs.d : nr << a.pitch_l2;
   constexpr bool pre = ADDS;  // residual terms prefetched (the launcher: D >= 4 and a term present)
   for (uint32_t t = threadIdx.x; t < units; t += kUT) {
@@ -625,283 +570,9 @@ __global__ __launch_bounds__(kUT) void k_gather_unal(const UnalArgs a) {
 }
 
 
-// ---- persistent, software-pipelined variant (segment-aligned tiles) --------------------------------
-// A workgroup walks items j, j + G, j + 2G, ... (G = the resident grid). While it sums item j from LDS,
-// the global loads of the next item's col slice and staged rows (registers) and of the item after
-// that's row pointers and molecule cuts are in flight, so each item costs one exposed round trip at
-// most instead of two back to back. Items: the small (tile, column slice) items and the big tiles of
-// the rows past the first chunk, interleaved as the one-shot kernel's blocks are.
-constexpr int kPMeta = 136;  // ints per meta buffer: row pointers [129] + misc [7]
-constexpr int kPRegU = 6;    // staged units per thread held in registers between load and commit
-constexpr int kPRegC = 8;    // col entries per thread held in registers
-// misc words (at kUMisc): [0] r0, [1] r1 (the cuts), [2] lo, [3] hi (col range), [4] c0 (row of P[0]),
-// [5] kind (0 none, 1 small, 2 big), [6] slice (small) / big tile index (big)
-
-struct ARegs {
-  int32_t rp;
-  int64_t sq, sp;
-};
-struct BRegs {
-  float4 x[kPRegU];
-  int32_t c[kPRegC];
-};
-
-__device__ __forceinline__ void item_of(const UnalArgs& a, uint32_t j, uint32_t total, bool& big, uint32_t& idx) {
-  if (a.interleave) {
-    const uint64_t nbig = total - a.nsmall;
-    const uint32_t c1 = (uint32_t)(((uint64_t)j + 1) * nbig / total);
-    const uint32_t c0 = (uint32_t)((uint64_t)j * nbig / total);
-    big = c1 != c0;
-    idx = big ? c1 - 1 : j - c1;
-  } else {
-    big = j >= a.nsmall;
-    idx = big ? j - a.nsmall : j;
-  }
-}
-__device__ __forceinline__ void small_of(const UnalArgs& a, uint32_t idx, uint32_t& ti, uint32_t& sl) {
-  const uint32_t S = a.slices;
-  const uint32_t grp = idx / (8 * S), in = idx - grp * 8 * S;
-  ti = grp * 8 + (in & 7);
-  sl = in >> 3;
-}
-
-// Item j's row pointers and molecule-start words into registers (loads only).
-__device__ __forceinline__ void load_a(const UnalArgs& a, uint32_t j, uint32_t total, ARegs& r) {
-  r.rp = 0;
-  r.sq = r.sp = 0;
-  if (j >= total) return;
-  bool big;
-  uint32_t idx, ti, sl;
-  item_of(a, j, total, big, idx);
-  if (big) return;
-  small_of(a, idx, ti, sl);
-  if (ti >= a.ntiles) return;
-  const uint32_t c0 = ti * a.tile_rows, c1 = min(c0 + a.tile_rows, a.split);
-  const uint32_t pend = min(c1 + (uint32_t)kUAlignWin, a.split);
-  if (threadIdx.x <= pend - c0) r.rp = a.rowptr[c0 + threadIdx.x];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (w < 2) {
-    const uint32_t c = w ? c1 : c0;
-    if (c > 0 && c < a.split) {
-      const uint32_t q = min(c + lane, a.split - 1);
-      r.sq = a.seg[(int64_t)q * a.seg_stride];
-      r.sp = a.seg[(int64_t)(q - 1) * a.seg_stride];
-    }
-  }
-}
-
-// Item j's meta buffer from the registers of load_a: row pointers, cuts, kind, a reset col range.
-// Prefetched registers are laundered through an empty asm at their commit point: the compiler may
-// not move their first use (and the wait for the load) up to the load itself.
-__device__ __forceinline__ void launder(int32_t& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void launder(int64_t& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void launder(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
-
-__device__ __forceinline__ void commit_a(const UnalArgs& a, uint32_t j, uint32_t total, ARegs r, int32_t* M) {
-  launder(r.rp);
-  launder(r.sq);
-  launder(r.sp);
-  int32_t* m = M + kUMisc;
-  bool big = false;
-  uint32_t idx = 0, ti = 0, sl = 0;
-  int kind = 0;
-  if (j < total) {
-    item_of(a, j, total, big, idx);
-    if (big) {
-      kind = 2;
-    } else {
-      small_of(a, idx, ti, sl);
-      kind = ti < a.ntiles ? 1 : 0;
-    }
-  }
-  if (kind == 1) {
-    const uint32_t c0 = ti * a.tile_rows, c1 = min(c0 + a.tile_rows, a.split);
-    const uint32_t pend = min(c1 + (uint32_t)kUAlignWin, a.split);
-    if (threadIdx.x <= pend - c0) M[threadIdx.x] = r.rp;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (w < 2) {  // wave-uniform: the whole wave takes part in the ballot
-      const uint32_t c = w ? c1 : c0;
-      const bool st = c > 0 && c < a.split && c + lane < a.split && r.sq != r.sp;
-      const unsigned long long mk = __ballot(st);
-      const uint32_t cut = (c > 0 && c < a.split && mk) ? c + (uint32_t)__builtin_ctzll(mk) : c;
-      if (lane == 0) m[w] = (int32_t)cut;
-    }
-    if (threadIdx.x == 128) {
-      m[4] = (int32_t)c0;
-      m[6] = (int32_t)sl;
-    }
-  } else if (threadIdx.x == 0) {
-    m[0] = m[1] = 0;
-    m[6] = (int32_t)idx;
-  }
-  if (threadIdx.x == 192) {
-    m[2] = INT_MAX;
-    m[3] = INT_MIN;
-    m[5] = kind;
-  }
-}
-
-// The small item in meta M: its tile, whether its col slice and its own rows (+ the zero row) fit the
-// prefetch registers and LDS (then the loads go out now, into r).
-template <bool SRC_CHUNKED>
-__device__ __forceinline__ bool load_b(const UnalArgs& a, const int32_t* M, BRegs& r) {
-  const int32_t* m = M + kUMisc;
-  if (m[5] != 1) return false;
-  const uint32_t r0 = (uint32_t)m[0], r1 = (uint32_t)m[1];
-  if (r1 <= r0) return false;
-  const int32_t* P = M + (r0 - (uint32_t)m[4]);
-  const uint32_t nr = r1 - r0;
-  const int32_t base = P[0], ncols = P[nr] - base;
-  const uint32_t sl = (uint32_t)m[6];
-  const FastDiv cs = sl + 1 == a.slices ? a.cu_last : a.cu_full;
-  const uint32_t u0 = sl * a.cu;
-  const uint32_t units = nr * cs.d;
-  if (!(ncols > 0 && (uint32_t)ncols < a.col_cap && ncols <= kPRegC * kUT && nr + 1 <= a.xcap &&
-        units <= (uint32_t)(kPRegU * kUT) && a.D >= 4))
-    return false;
-#pragma unroll
-  for (int k = 0; k < kPRegC; ++k) {
-    const int32_t i = threadIdx.x + k * kUT;
-    r.c[k] = i < ncols ? a.col[base + i] : 0;
-  }
-#pragma unroll
-  for (int k = 0; k < kPRegU; ++k) {  // clamped, unconditional loads (commit_b writes the zero row)
-    const uint32_t u = min(threadIdx.x + k * kUT, units - 1);
-    const uint32_t rl = fdiv(u, cs);
-    r.x[k] = ld_raw(src_row<SRC_CHUNKED>(a, r0 + rl), 4 * (u0 + u - rl * cs.d), a.D);
-  }
-  return true;
-}
-
-// The prefetched col slice and rows into LDS, and the col range into the meta's lo / hi.
-__device__ __forceinline__ void commit_b(const UnalArgs& a, int32_t* M, BRegs r, int32_t* s_col, float* s_x) {
-#pragma unroll
-  for (int k = 0; k < kPRegC; ++k) launder(r.c[k]);
-#pragma unroll
-  for (int k = 0; k < kPRegU; ++k) launder(r.x[k]);
-  int32_t* m = M + kUMisc;
-  const uint32_t r0 = (uint32_t)m[0], r1 = (uint32_t)m[1];
-  const int32_t* P = M + (r0 - (uint32_t)m[4]);
-  const uint32_t nr = r1 - r0;
-  const int32_t ncols = P[nr] - P[0];
-  const uint32_t sl = (uint32_t)m[6];
-  const FastDiv cs = sl + 1 == a.slices ? a.cu_last : a.cu_full;
-  const uint32_t units = nr * cs.d;
-  const uint32_t ws = 4 * a.pitch;
-  const uint32_t u0 = sl * a.cu;
-  for (uint32_t t = threadIdx.x; t < a.pitch; t += kUT) reinterpret_cast<float4*>(s_x + nr * ws)[t] = f4z();
-  int32_t lo = INT_MAX, hi = INT_MIN;
-#pragma unroll
-  for (int k = 0; k < kPRegC; ++k) {
-    const int32_t i = threadIdx.x + k * kUT;
-    if (i < ncols) {
-      s_col[i] = r.c[k];
-      lo = min(lo, r.c[k]);
-      hi = max(hi, r.c[k]);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kPRegU; ++k) {
-    const uint32_t u = threadIdx.x + k * kUT;
-    if (u < units) {
-      const uint32_t rl = fdiv(u, cs);
-      put_raw(s_x + rl * ws, 4 * (u0 + u - rl * cs.d), a.D, u0, r.x[k]);
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = min(lo, __shfl_xor(lo, o, 64));
-    hi = max(hi, __shfl_xor(hi, o, 64));
-  }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMin(&m[2], lo);
-    atomicMax(&m[3], hi);
-  }
-}
-
-template <bool SRC_CHUNKED>
-__global__ __launch_bounds__(kUT) void k_gather_unal_pipe(const UnalArgs a, uint32_t total) {
-  // [meta 0 | meta 1] [col_cap col entries] [xcap staged rows of 4 * cu floats]
-  extern __shared__ __attribute__((aligned(16))) int32_t s_dyn[];
-  int32_t* s_col = s_dyn + 2 * kPMeta;
-  float* s_x = reinterpret_cast<float*>(s_dyn + 2 * kPMeta + a.col_cap);
-  const uint32_t G = gridDim.x;
-  uint32_t j = blockIdx.x;
-  if (j >= total) return;
-  int cur = 0;
-  ARegs ar;
-  BRegs br;
-  load_a(a, j, total, ar);
-  commit_a(a, j, total, ar, s_dyn);
-  lds_barrier();
-  bool pf = load_b<SRC_CHUNKED>(a, s_dyn, br);
-  load_a(a, j + G, total, ar);
-  if (pf) commit_b(a, s_dyn, br, s_col, s_x);
-  commit_a(a, j + G, total, ar, s_dyn + kPMeta);
-  lds_barrier();
-  for (; j < total; j += G) {
-    int32_t* M = s_dyn + cur * kPMeta;
-    int32_t* N = s_dyn + (1 - cur) * kPMeta;
-    const int32_t* m = M + kUMisc;
-    const int kind = m[5];
-    const uint32_t r0 = (uint32_t)m[0], r1 = (uint32_t)m[1], c0 = (uint32_t)m[4], sl = (uint32_t)m[6];
-    const int32_t lo = m[2], hi = m[3];
-    const bool own = pf && lo >= (int32_t)r0 && hi < (int32_t)r1;
-    const uint32_t nr = r1 > r0 ? r1 - r0 : 0;
-    const int32_t* P = M + (r0 - c0);
-    const int32_t rb = (int32_t)(16 * a.pitch);
-    if (own) {  // col entries as byte offsets of the staged rows (each thread its own entries)
-      const int32_t ncols = P[nr] - P[0];
-#pragma unroll
-      for (int k = 0; k < kPRegC; ++k) {
-        const int32_t i = threadIdx.x + k * kUT;
-        if (i < ncols) s_col[i] = (s_col[i] - (int32_t)r0) * rb;
-      }
-      if (threadIdx.x == 0) s_col[ncols] = (int32_t)nr * rb;
-    }
-    // the next items' loads go out before this item's sum
-    const bool pfn = load_b<SRC_CHUNKED>(a, N, br);
-    load_a(a, j + 2 * G, total, ar);
-    lds_barrier();
-    if (kind == 2) {
-      big_tile<SRC_CHUNKED>(a, (uint32_t)m[6], M, M + kUMisc);
-    } else if (kind == 1 && nr > 0) {
-      const FastDiv cs = sl + 1 == a.slices ? a.cu_last : a.cu_full;
-      const uint32_t u0 = sl * a.cu;
-      if (own) {
-        sum_rows<false>(a, P, P[0], reinterpret_cast<const char*>(s_col), reinterpret_cast<const char*>(s_x),
-                 (P[nr] - P[0]) * 4, r0, nr, u0, cs, a.compact);
-      } else {
-        if (pf) {  // prefetched, but the sources leave the tile: the general path (col range reset)
-          if (threadIdx.x == 0) {
-            M[kUMisc + 2] = INT_MAX;
-            M[kUMisc + 3] = INT_MIN;
-          }
-          lds_barrier();
-        }
-        tile<SRC_CHUNKED, false>(a, P, M + kUMisc, s_col, s_x, r0, nr, true, u0, cs);
-      }
-    }
-    lds_barrier();
-    if (pfn) commit_b(a, N, br, s_col, s_x);
-    commit_a(a, j + 2 * G, total, ar, M);
-    lds_barrier();
-    cur = 1 - cur;
-    pf = pfn;
-  }
-}
-
-int64_t env_i64(const char* name, int64_t dflt) {
-  const char* e = getenv(name);
-  return e ? std::max<int64_t>(0, atoll(e)) : dflt;
-}
 
 }  // namespace
 
-bool gather_unal_on() {
-  static const bool on = env_i64("AIMX_HOP_UNAL", 1) != 0;
-  return on;
-}
 
 int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_t src_cs, int64_t D,
                        const int32_t* rowptr, const int32_t* col, int64_t rows, float* out, int64_t out_ld,
@@ -913,23 +584,20 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   if (rows >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;
   // knobs, read once per process
   // slice width (floats): 64 = one 16-unit pitch per staged row (conflict-free ds_read_b128, sum_rows)
-  static const int64_t w_max = std::max<int64_t>(4, env_i64("AIMX_HOPU_W", 80) / 4 * 4);
+  static const int64_t w_max = std::max<int64_t>(4, opt_i64("AIMX_HOPU_W", 80) / 4 * 4);
   static const int64_t pitch_env = [] {  // staged row pitch in units: 0 compact, else a power of two >= 16
-    const int64_t e = env_i64("AIMX_HOPU_PITCH", 0);
+    const int64_t e = opt_i64("AIMX_HOPU_PITCH", 0);
     if (!e) return (int64_t)0;
     int64_t p = 16;
     while (p < e) p *= 2;
     return p;
   }();
-  static const int64_t tr_env = std::max<int64_t>(1, std::min<int64_t>(kUMaxTile, env_i64("AIMX_HOPU_TILE", 32)));
-  static const int64_t col_cap_env = (std::max<int64_t>(64, env_i64("AIMX_HOPU_COL_CAP", 1024)) + 3) / 4 * 4;
-  static const int64_t stage_env = std::max<int64_t>(1024, env_i64("AIMX_HOPU_STAGE", 20 * 1024));
-  static const int64_t big_env = env_i64("AIMX_HOPU_BIG", 256);
-  static const int32_t interleave = env_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
-  static const bool no_seg = env_i64("AIMX_HOP_NO_SEG", 0) != 0;
-  static const int64_t pair_env = env_i64("AIMX_HOPU_PAIR", 0);  // two units per col-offset read (opt-in: slower)
-  static const int64_t pipe = env_i64("AIMX_HOPU_PIPE", 0);  // persistent pipelined kernel (opt-in: slower)
-  static const int64_t pipe_waves = std::max<int64_t>(1, env_i64("AIMX_HOPU_PIPE_WAVES", 1));  // grid = waves x resident
+  static const int64_t tr_env = std::max<int64_t>(1, std::min<int64_t>(kUMaxTile, opt_i64("AIMX_HOPU_TILE", 32)));
+  static const int64_t col_cap_env = (std::max<int64_t>(64, opt_i64("AIMX_HOPU_COL_CAP", 1024)) + 3) / 4 * 4;
+  static const int64_t stage_env = std::max<int64_t>(1024, opt_i64("AIMX_HOPU_STAGE", 20 * 1024));
+  static const int64_t big_env = opt_i64("AIMX_HOPU_BIG", 256);
+  static const int32_t interleave = opt_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
+  static const bool no_seg = opt_i64("AIMX_HOP_NO_SEG", 0) != 0;
   const int64_t upr = cdiv(D, 4);
   // slices of cu units; the last slice must hold more than a partial last unit (put_raw writes that
   // unit shifted down over the unit before it, which must be in the same slice)
@@ -976,7 +644,6 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   a.pitch = (uint32_t)pitch;
   a.pitch_l2 = (uint32_t)pitch_l2;
   a.compact = pitch_env ? 0 : 1;
-  a.pair = pair_env ? 1 : 0;
   a.cu_full = make_fastdiv((uint32_t)cu);
   a.cu_last = make_fastdiv((uint32_t)cu_last);
   a.upr_f = make_fastdiv((uint32_t)upr);
@@ -1010,28 +677,6 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   const int64_t blocks = nsmall + nbig;
   if (blocks <= 0) return AIMX_OK;
   if (blocks >= (int64_t)INT32_MAX) return AIMX_EARG;
-  if (a.seg && pipe) {
-    using PFn = void (*)(const UnalArgs, uint32_t);
-    PFn fn = src_rpc > 0 ? k_gather_unal_pipe<true> : k_gather_unal_pipe<false>;
-    const size_t pdyn = dyn - (size_t)kUHead * 4 + (size_t)2 * kPMeta * 4;
-    // the resident grid: workgroups per CU at this LDS size (queried once per size) x CUs
-    static int cus = 0;
-    static size_t occ_dyn = 0;
-    static int occ = 0;
-    if (!cus) {
-      int dev = 0;
-      AIMX_CHECK_HIP(hipGetDevice(&dev));
-      AIMX_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    if (occ_dyn != pdyn) {
-      AIMX_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kUT, pdyn));
-      occ_dyn = pdyn;
-    }
-    const int64_t grid = std::min<int64_t>(blocks, (int64_t)std::max(1, occ) * cus * pipe_waves);
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kUT), pdyn, stream, a, (uint32_t)blocks);
-    AIMX_CHECK_LAUNCH();
-    return AIMX_OK;
-  }
   using KFn = void (*)(const UnalArgs);
   const bool adds = D >= 4 && (add0 || add1);
   KFn fn = src_rpc > 0 ? (adds ? k_gather_unal<true, true> : k_gather_unal<true, false>)

@@ -404,8 +404,12 @@ struct aimx_h5_writer {
 // Map the file for the direct path when /data is one contiguous run of 16-byte descriptors in an
 // 8-byte-address file, and keep it only if the records it finds equal H5Dread's for a sample of
 // elements (first, last and spread between). Any doubt leaves the H5Dread path in place.
+static std::atomic<int> g_allow_direct{1};
+
+extern "C" void aimx_h5_set_direct(int32_t allow) { g_allow_direct.store(allow ? 1 : 0); }
+
 static void try_direct(aimx_h5_reader* r, const char* path) {
-  if (const char* e = std::getenv("AIMX_H5_DIRECT"); e && e[0] == '0') return;
+  if (!g_allow_direct.load()) return;
   if (r->n_records <= 0) return;
   hid_t fcpl = H5Fget_create_plist(r->file);
   size_t sa = 0, ss = 0;

@@ -1073,7 +1073,7 @@ int mlpw_rt(int64_t N, int64_t D, int64_t nm) {
   const int CF = pad16((int)D) / 16;
   const int64_t tiles = (N + 15) / 16;
   int rt = (int)std::min<int64_t>(4, std::max<int64_t>(1, (tiles + g_num_cus() - 1) / g_num_cus()));
-  if (const char* e = getenv("AIMX_MLPW_RT")) rt = std::max(1, std::min(4, atoi(e)));  // A/B experiments only
+  if (const int64_t f = opt_i64("AIMX_MLPW_RT", 0)) rt = (int)std::max<int64_t>(1, std::min<int64_t>(4, f));  // tuning build only
   while (rt > 1 && (rt * CF > 2 * kWMaxWaves || mlpw_lds_bytes(D, nm, rt) > (size_t)kMlpwDynLds)) --rt;
   return rt;
 }
@@ -1137,7 +1137,7 @@ MlpsPlan mlps_plan(int64_t N, int64_t D) {
   // enough rows per chunk that the chunks fit one round of one workgroup per CU
   const int64_t slots = g_num_cus();
   int rt = (int)std::min<int64_t>(rt_max, std::max<int64_t>(1, cdiv(cdiv(std::max<int64_t>(N, 1), slots), 16)));
-  if (const char* e = getenv("AIMX_MLPS_RT")) rt = std::max(1, std::min(rt_max, atoi(e)));  // A/B experiments only
+  if (const int64_t f = opt_i64("AIMX_MLPS_RT", 0)) rt = (int)std::max<int64_t>(1, std::min<int64_t>(rt_max, f));  // test hook
   // two activation tiles + the forward's bias table (2 nm x 16 CF floats, nm <= 8), per workgroup
   auto lds = [&](int r) { return sizeof(float) * (size_t)(2 * 16 * r * pl.geo.S + 2 * 8 * 16 * CF); };
   const size_t cap = (size_t)kMlpsDynLds;
@@ -1187,19 +1187,15 @@ int64_t mlps_image_floats(int64_t D) {
 
 }  // namespace
 
-// The weight-resident kernels: default for D <= 128 whose weights fit the LDS (AIMX_MLPW=0 turns
-// them off). Read per call (~6 calls per train step): tests switch the paths inside one process.
-bool mlpw_on(int64_t D, int64_t nm) {
-  const char* e = getenv("AIMX_MLPW");
-  return (!e || atoi(e) != 0) && mlpw_lds_ok(D, nm);
-}
+// The weight-resident kernels: default for D <= 128 whose weights fit the LDS (the test hook
+// AIMX_MLPW = 0 turns them off: the per-GEMM path's parity tests). Read per call.
+bool mlpw_on(int64_t D, int64_t nm) { return opt_i64("AIMX_MLPW", 1) != 0 && mlpw_lds_ok(D, nm); }
 
 // The weight-streamed kernels: everything the weight-resident ones do not take, in fp32 (AMP keeps
-// the per-GEMM path's bf16 operands), up to D = 384 and 8 blocks. AIMX_MLPS=0 turns them off (the
-// per-GEMM path), AIMX_MLPS=1 makes them take small D too (tests).
+// the per-GEMM path's bf16 operands), up to D = 384 and 8 blocks. Test hook AIMX_MLPS: 0 turns them off
+// (the per-GEMM path), 1 makes them take small D too.
 bool mlps_on(int64_t N, int64_t D, int64_t nm, int32_t precision) {
-  const char* e = getenv("AIMX_MLPS");
-  const int mode = e ? atoi(e) : -1;
+  const int64_t mode = opt_i64("AIMX_MLPS", -1);
   if (mode == 0 || precision == AIMX_PREC_BF16 || nm < 1 || nm > 8) return false;
   if (mode != 1 && mlpw_on(D, nm)) return false;
   return mlps_plan(N, D).ok;
@@ -1214,7 +1210,7 @@ static bool mlp_extent_ok(int64_t N, int64_t D, int64_t ld) {
 
 bool mlp_fused_ok(int64_t N, int64_t D, int64_t nm, int32_t precision, int64_t ld) {
   if (!mlp_extent_ok(N, D, ld)) return false;
-  if (getenv("AIMX_MLPS") && atoi(getenv("AIMX_MLPS")) == 1) return mlps_on(N, D, nm, precision);
+  if (opt_i64("AIMX_MLPS", -1) == 1) return mlps_on(N, D, nm, precision);
   return mlpw_on(D, nm) || mlps_on(N, D, nm, precision);
 }
 
@@ -1291,7 +1287,7 @@ int launch_mlp_fwd(const AimxShellStack* s, int64_t l, const float* x_res, int64
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     bool v4 = s->D % 4 == 0 && p.ldug % 4 == 0 && al(p.ug);
     for (int64_t k = 0; k < nm; ++k) v4 = v4 && al(p.w1[k]) && al(p.w2[k]);
-    p.v4 = (v4 && !getenv("AIMX_MLPW_FILL1")) ? 1 : 0;  // AIMX_MLPW_FILL1: dword fill (A/B)
+    p.v4 = v4 ? 1 : 0;
   }
   if (!pack && mlpw_on(s->D, nm)) {
     const int rt = mlpw_rt(s->N, s->D, nm);
@@ -1336,7 +1332,7 @@ int launch_mlp_bwd(const AimxShellStack* s, int64_t l, const float* dy, int64_t 
     auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     bool v4 = s->D % 4 == 0 && lddy % 4 == 0 && al(dy);
     for (int64_t k = 0; k < nm; ++k) v4 = v4 && al(p.w1[k]) && al(p.w2[k]);
-    p.v4 = (v4 && !getenv("AIMX_MLPW_FILL1")) ? 1 : 0;
+    p.v4 = v4 ? 1 : 0;
   }
   if (!pack && mlpw_on(s->D, nm)) {
     const int rt = mlpw_rt(s->N, s->D, nm);

@@ -163,11 +163,7 @@ int gather(const AimxShellStack* st, const float* src, int64_t src_ld, int64_t s
 
 // Empty hop chunks (AimxGemmArgs.zc_*): every GEMM over F's columns trims the all-zero chunks the
 // reference's hop leaves (layers.py:154), detected on the device from the forward CSR row pointers.
-// AIMX_NO_ZC=1 disables it (A/B experiments).
-bool zc_on() {
-  static const bool off = getenv("AIMX_NO_ZC") != nullptr;
-  return !off;
-}
+bool zc_on() { return opt_i64("AIMX_NO_ZC", 0) == 0; }  // tuning build: AIMX_NO_ZC=1 disables it
 
 void set_zc(AimxGemmArgs& a, const AimxShellStack* s, int dim) {
   if (!zc_on() || !s->fwd_rowptr) return;
@@ -452,15 +448,7 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
   const int per_layer = (int)(2 * nm + 1);
   std::vector<AimxWgradProblem> pr(L * per_layer);
   const int n_pr = stack_wgrad_problems(s, g, base, &lay, pr.data());
-  // with an auxiliary stream, each layer's weight gradients fork off as soon as its activation
-  // gradients exist; the two streams split the counter array so their split-K tickets never meet
-  const bool tail = g->aux_mode == 1 && g->aux_stream && g->events && g->n_events >= 1 && g->aux_counters;
-  const bool aux = !tail && g->aux_stream && g->events && g->n_events >= L + 1 && s->counters && s->n_counters >= 2;
-  hipStream_t ast = (hipStream_t)g->aux_stream;
-  const int64_t main_counters = aux ? s->n_counters / 2 : s->n_counters;
-  const Ws ws{s->workspace, s->workspace_bytes, s->counters, main_counters, s->precision};
-  int32_t* aux_cnt = aux ? s->counters + main_counters : nullptr;
-  const int64_t aux_ncnt = aux ? s->n_counters - main_counters : 0;
+  const Ws ws{s->workspace, s->workspace_bytes, s->counters, s->n_counters, s->precision};
   float* wg_ws = base + lay.wg;
   const size_t wg_bytes = sizeof(float) * (size_t)(lay.total - lay.wg);
   const bool drop = s->training && s->drop_p > 0.f;
@@ -528,13 +516,6 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
     }
     // dg = dY -> dUG[:, D:] (the fused chain writes it itself)
     if (!fused && nm > 0 && dY != dUG + D) RUN(copy2d(dY, ldy, dUG + D, LUG, N, D, st));
-    if (aux) {  // fork: this layer's weight gradients run beside the rest of the chain
-      hipEvent_t ev = (hipEvent_t)g->events[l];
-      AIMX_CHECK_HIP(hipEventRecord(ev, st));
-      AIMX_CHECK_HIP(hipStreamWaitEvent(ast, ev, 0));
-      RUN(aimx_wgrad_grouped(pr.data() + (L - 1 - l) * per_layer, per_layer, wg_ws, wg_bytes, aux_cnt, aux_ncnt,
-                             (aimx_stream_t)ast));
-    }
     {  // dF = dUG [Wi ; Wg]; tiles wholly in the trailing empty chunks are not computed nor stored:
        // the hop backward gathers only from chunks that hold targets (zc_dim 2)
       AimxGemmArgs a = linear_dx(N, K, D2, dUG, LUG, s->w_ig[l], dF, LF);
@@ -554,19 +535,6 @@ extern "C" int aimx_shell_stack_backward(const AimxShellStack* s, const AimxShel
       const int64_t ldr = first ? s->x_in_ld : D;
       RUN(launch_charge_bwd(raw, ldr, N, D, s->gptr, s->gperm, s->G, s->total_charges, dst, D, nxt, ldn, st));
     }
-  }
-  if (aux) {  // join
-    hipEvent_t ev = (hipEvent_t)g->events[L];
-    AIMX_CHECK_HIP(hipEventRecord(ev, ast));
-    AIMX_CHECK_HIP(hipStreamWaitEvent(st, ev, 0));
-    return AIMX_OK;
-  }
-  if (tail) {  // fork the grouped weight gradients; the caller joins (AimxShellStackGrad.aux_mode)
-    hipEvent_t ev = (hipEvent_t)g->events[0];
-    AIMX_CHECK_HIP(hipEventRecord(ev, st));
-    AIMX_CHECK_HIP(hipStreamWaitEvent(ast, ev, 0));
-    return aimx_wgrad_grouped(pr.data(), n_pr, wg_ws, wg_bytes, g->aux_counters, g->n_aux_counters,
-                              (aimx_stream_t)ast);
   }
   // every weight and bias gradient of the stack in one grouped launch
   return aimx_wgrad_grouped(pr.data(), n_pr, wg_ws, wg_bytes, s->counters, s->n_counters, stream_);

@@ -33,6 +33,8 @@ from .pooling import create_pooling_layer
 
 
 _FEATURE_KEYS = ("atom_type", "hydrogen_count", "degree", "hybridization")
+# the fused post-pool head (aimx.ops.head) where it applies; False: the module path (tests, A/Bs)
+FUSED_HEAD = True
 
 
 def _calling_ddp():
@@ -228,8 +230,9 @@ class GNN(nn.Module):
     def _aimx_head_ok(self) -> bool:
         """The fused head covers the reference's post-pool chain when every LinearBlock is F -> F
         with one activation and one dropout setting, F <= 512 (above 256 only where clustered
-        launches are allowed), F and the input width multiples of 32 (AIMX_NO_FUSED_HEAD=1 disables)."""
-        if os.environ.get("AIMX_NO_FUSED_HEAD", "0") == "1":
+        launches are allowed), F and the input width multiples of 32 (FUSED_HEAD = False, a module
+        attribute for tests and A/Bs, disables it)."""
+        if not FUSED_HEAD:
             return False
         pp, blocks = self.post_pooling_projection, list(self.ffn.layers)
         F = pp.out_features
@@ -249,7 +252,12 @@ class GNN(nn.Module):
                     b.linear2.out_features != F or type(b.activation) is not type(b0.activation) or \
                     b.dropout.p != b0.dropout.p or b.dropout.training != b0.dropout.training:
                 return False
-        return True
+        # the fused kernels read the weight matrices with 16-byte loads: weights moved into other
+        # storage (torch.nn.utils.vector_to_parameters puts them at arbitrary float offsets of one
+        # vector) take the module path, which accepts any alignment
+        ws = [pp.weight, self.skip_transform.weight, self.output_layer.weight]
+        ws += [w for b in blocks for w in (b.linear1.weight, b.linear2.weight)]
+        return all(w.data_ptr() % 16 == 0 and w.is_contiguous() for w in ws)
 
     def _embed_atomic_features(self, atom_features: Dict[str, torch.Tensor]) -> torch.Tensor:
         return torch.cat([
@@ -298,11 +306,7 @@ class GNN(nn.Module):
     # -- stereochemistry (plain PyTorch; reference gnn.py:310-509) ----------------------------
     def _apply_stereochemistry(self, x_other, tetrahedral_indices, cis_indices, trans_indices):
         # [x | cis/trans | tetrahedral] in one HIP op (csrc/stereo.hip) forward and backward; the
-        # two methods below keep the reference's PyTorch formulation (AIMX_STEREO_TORCH=1 uses them)
-        if os.environ.get("AIMX_STEREO_TORCH", "0") == "1":
-            ct = self._cis_trans_calculation(x_other, cis_indices, trans_indices)
-            tet = self._tetrahedral_feature_calculation_physics_inspired(x_other, tetrahedral_indices)
-            return self.stereochemical_embedding_2(torch.cat([x_other, ct, tet], dim=-1))
+        # two methods below keep the reference's PyTorch formulation as module API
         return self.stereochemical_embedding_2(ops.stereo_features(x_other, tetrahedral_indices, cis_indices,
                                                                    trans_indices))
 

@@ -190,7 +190,7 @@ class GradientSync:
 
     def __init__(self, params, bucket_mb: float = 25.0, process_group=None, overlap: bool = True,
                  first_bucket_mb: float = 1.0, unused=(), always: bool = False, broadcast_params: bool = True,
-                 auto_finish: bool = False, gate=None):
+                 auto_finish: bool = False, gate=None, side_stream=None):
         params = list(params)
         unused = list(unused)
         if broadcast_params:
@@ -225,10 +225,9 @@ class GradientSync:
         # MI355X with a world-size-1 RCCL group (profiles/r02_ddp_ab.txt), the forked graph costs
         # ~20 us per c2 step (3.3 MB of gradients: an 8-GPU all-reduce of them is only tens of us)
         # and nothing at c5 (63 MB, where an 8-GPU all-reduce takes ~0.3 ms and overlap pays).
-        # AIMX_DDP_SIDE=1 / 0 forces it on / off.
+        # side_stream=True / False forces it on / off.
         total = sum(p.numel() for p in self.params) * 4
-        env = os.environ.get("AIMX_DDP_SIDE")
-        self.side_stream = (env == "1") if env is not None else total >= 16 * 2 ** 20
+        self.side_stream = bool(side_stream) if side_stream is not None else total >= 16 * 2 ** 20
         self.comm = None
         self._stream = None
         self._events = []
@@ -276,13 +275,8 @@ class GradientSync:
             flat = torch.empty(sum(p.numel() for p in bucket), dtype=bucket[0].dtype, device=bucket[0].device)
             self._flat[i] = flat
         if self.comm is not None:
-            # pack every gradient (zeros for a missing one) into the flat buffer: one launch. Weight
-            # gradients may still be in flight on the backward's side stream (aimx.ops.side_fork):
-            # the pack waits for them (an event, no host sync)
+            # pack every gradient (zeros for a missing one) into the flat buffer: one launch
             from aimx import _lib
-            hit = _lib.side_stream(flat.device)
-            if hit is not None:
-                torch.cuda.current_stream(flat.device).wait_stream(hit[0])
             pairs, off = [], 0
             for p in bucket:
                 n = p.numel()
@@ -292,11 +286,6 @@ class GradientSync:
                 off += n
             _lib.multi_copy(pairs, flat.device)
         else:
-            if flat.is_cuda:
-                from aimx import _lib
-                hit = _lib.side_stream(flat.device)
-                if hit is not None:
-                    torch.cuda.current_stream(flat.device).wait_stream(hit[0])
             grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket]
             torch.cat(grads, out=flat)
         if self.comm is not None:

@@ -71,12 +71,13 @@ PAD_MOLS = 8  # padding molecules appended to each static batch (excluded from t
 # atoms: one-GPU static batches are padded to the next multiple (one graph each). c4 / c5 (device-
 # bound steps, no launch overhead for the graph to win back) use 32: every padded atom is paid in
 # full there (profiles/r05_quantum_ab.txt: c5 graphed 3.972 -> 3.952 ms, eager 3.965-3.975; c4
-# 2.600 -> 2.590); c2 keeps 128 (0.7249 vs 0.7324 ms with 32). AIMX_BENCH_QUANTUM overrides (A/B).
+# 2.600 -> 2.590); c2 keeps 128 (0.7249 vs 0.7324 ms with 32). --quantum overrides (A/B).
 LAYOUT_QUANTUM = 128
+QUANTUM_OVERRIDE = None
 
 
 def layout_quantum(cfg):
-    return int(os.environ.get("AIMX_BENCH_QUANTUM", cfg.get("quantum", LAYOUT_QUANTUM)))
+    return int(QUANTUM_OVERRIDE or cfg.get("quantum", LAYOUT_QUANTUM))
 
 
 def make_batches(cfg, n_batches, seed, device, pad=False, buckets=False):
@@ -209,11 +210,8 @@ def build_model(cfg, device):
 
 
 def hop_kernel(d):
-    """The hop kernel that runs for width d: hop.hip for 16-byte rows, else hop_unal.hip (hop_rows.hip
-    with AIMX_HOP_UNAL=0)."""
-    if d % 4 == 0:
-        return "k_gather_sum"
-    return "k_gather_rows" if os.environ.get("AIMX_HOP_UNAL", "1") == "0" else "k_gather_unal"
+    """The hop kernel that runs for width d: hop.hip for 16-byte rows, else hop_unal.hip."""
+    return "k_gather_sum" if d % 4 == 0 else "k_gather_unal"
 
 
 def hop_roofline(batch, hops, device, hidden=256, target_atoms=4_000_000, launches=20):
@@ -798,7 +796,11 @@ def main():
     ap.add_argument("--eager-steps", type=int, default=20)
     ap.add_argument("--ddp-world1", action="store_true",
                     help="A/B of the data-parallel step on one GPU: a world-size-1 RCCL group with the bucket "
-                         "all-reduces kept (GradientSync always=True); AIMX_DDP_GRAPH=capture|split picks the mode")
+                         "all-reduces kept (GradientSync always=True); --ddp-graph picks the mode")
+    ap.add_argument("--ddp-graph", default="capture", choices=["capture", "split"],
+                    help="data-parallel graph mode of GraphedTrainStep (capture: the RCCL all-reduces inside the "
+                         "step graph; split: eager all-reduces between captured halves)")
+    ap.add_argument("--quantum", type=int, default=None, help="atoms per static-layout bucket (A/B; default per config)")
     ap.add_argument("--deadline", type=float, default=None,
                     help="multi-GPU runs: every rank exits 124 this many seconds after it started (a hung "
                          "collective must not wait for an outer timeout), and a self-launched run (--gpus N without "
@@ -810,6 +812,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
+    global QUANTUM_OVERRIDE
+    QUANTUM_OVERRIDE = args.quantum
 
     if args.gpus < 1:
         print(f"bench: --gpus {args.gpus} must be >= 1", file=sys.stderr)
@@ -893,7 +897,7 @@ def main():
         # Adam; each timed step copies a fresh resident batch into the static inputs and replays.
         from aimx.train import GraphedTrainStep
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.amp):  # captured in the context
-            graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync,
+            graphed = GraphedTrainStep(model, loss_fn, opt, batches[0], n_real=B, sync=sync, ddp_graph=args.ddp_graph,
                                        max_layouts=8 if sync is None else 1)
             graphed.prepare(batches)
 
@@ -955,7 +959,7 @@ def main():
         dist.all_reduce(tmo, op=dist.ReduceOp.MAX)
     head_timeout = bool(tmo.item() != 0)
     if head_timeout:
-        print("bench: a clustered head launch timed out (AIMX_HEAD_CLUSTER); results invalid", file=sys.stderr)
+        print("bench: a clustered head launch timed out; results invalid", file=sys.stderr)
     atoms = sum(getattr(b, "real_atoms", b.num_atoms) for b in batches) / len(batches)
     edges = sum(getattr(b, "real_edges", b.edges.shape[0]) for b in batches) / len(batches)
     mol = cfg["batch"] * world * args.steps

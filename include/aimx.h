@@ -41,10 +41,16 @@ typedef void* aimx_stream_t; /* hipStream_t */
 /* Library identity (for load checks): returns "aimx/<version>/gfx950". */
 const char* aimx_version(void);
 
-/* Event handles (hipEvent_t, timing disabled) for the fork/join of auxiliary streams
- * (AimxShellStackGrad.aux_stream). Created once by the caller and reused across calls. */
-int aimx_events_create(int32_t n, void** events);
-int aimx_events_destroy(int32_t n, void** events);
+/* Path options: test hooks, not a tuning surface. The product library reads no environment
+ * variable; every launcher uses its defaults unless an option of the same name was set here (the
+ * alternative-path parity tests: "AIMX_MLPW" 0 = per-GEMM node-update MLP, "AIMX_MLPS" 0 / 1 =
+ * weight-streamed MLP off / for every width, "AIMX_MLPS_RT" row tiles per chunk, "AIMX_WGRAD_BB"
+ * 64 / 80 weight-gradient block edge, "AIMX_GEMM_BIG" 0 / 64 / 128 large-tile GEMM off / forced
+ * tile, "AIMX_GEMM_BIG_W" 4 / 8 waves, "AIMX_HEAD8" 0 = 16-molecule head kernels). The tuning build
+ * (make tune -> lib/libaimx_tune.so) also reads these names, and its A/B knobs, from the
+ * environment. aimx_set_option returns AIMX_EARG for a name longer than 47 bytes or past 16 names. */
+int aimx_set_option(const char* name, int64_t value);
+int aimx_clear_options(void);
 
 /* ------------------------------------------------------------------------------------------
  * Stable CSR build (device): rows sorted by key, ties kept in ascending item order — exactly the
@@ -233,20 +239,6 @@ typedef struct AimxShellStackGrad {
    * per-block activation gradients are kept until the weight gradients of the whole stack run
    * as ONE grouped launch at the end (aimx_wgrad_grouped) */
   void* workspace; size_t workspace_bytes;
-  /* optional concurrency: when aux_stream != NULL and n_events >= num_layers + 1, each layer's
-   * weight gradients are launched on aux_stream as soon as that layer's activation gradients
-   * exist (event fork), overlapping the rest of the activation-gradient chain on `stream`; the
-   * call returns with `stream` joined on aux_stream (event join), so graph capture and eager
-   * execution see the same dependencies. aux_stream uses the upper half of the counter array.
-   * events: hipEvent_t handles from aimx_events_create. */
-  aimx_stream_t aux_stream; void* const* events; int32_t n_events;
-  /* aux_mode 1 ("tail fork"): instead of the per-layer forks above, the stack's single grouped
-   * weight-gradient launch runs on aux_stream after an event fork (events[0]) at the end of the
-   * activation-gradient chain, and the call returns WITHOUT joining: the caller joins aux_stream
-   * before it reads a weight gradient or releases the workspace / activations. The launch uses
-   * aux_counters (a counter array of its own, as in AimxGemmArgs), so the two streams' split-K
-   * tickets never meet. */
-  int32_t aux_mode; int32_t* aux_counters; int64_t n_aux_counters;
 } AimxShellStackGrad;
 
 size_t aimx_shell_stack_workspace_bytes(const AimxShellStack* s);

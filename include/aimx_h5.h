@@ -39,6 +39,9 @@ typedef struct aimx_h5_writer aimx_h5_writer;
 
 /* Open for reading; loads /index_map (identity when absent, as molecular.py:138-142). */
 int aimx_h5_open(const char* path, aimx_h5_reader** out);
+/* Test hook: allow (1, default) or forbid (0) the direct memory-mapped record path in later
+ * aimx_h5_open calls (AimxH5Info.direct_read), so both read paths can be compared. */
+void aimx_h5_set_direct(int32_t allow);
 void aimx_h5_close(aimx_h5_reader* r);
 int aimx_h5_info(const aimx_h5_reader* r, AimxH5Info* out);
 

@@ -258,10 +258,10 @@ def test_gemm_layouts(M, N, K, layout):
     (258, 1024, 1024, "NT", 0), (258, 1024, 1024, "NN", 0), (256, 512, 1000, "NT", 0), (1, 256, 256, "NN", 0),
     (640, 260, 300, "NT", 0), (130, 1024, 4096, "NN", 0), (64, 256, 256, "NT", 0), (200, 516, 260, "NN", 0),
     (258, 1024, 1024, "NT", 1), (258, 1024, 1024, "NN", 7), (77, 300, 1028, "NT", 64)])
-def test_gemm_skinny(M, N, K, layout, splits):
-    """k_skinny (few rows, wide and deep: c5's post-pool F = 1024 layers and their input gradient):
-    padded row blocks, N and K tails inside a 64-wide tile and a 64-deep stage, one split and more
-    splits than stages; against fp64, deterministic (bitwise) and counters left at zero."""
+def test_gemm_few_rows_deep_k(M, N, K, layout, splits):
+    """Few rows, wide and deep (c5's post-pool F = 1024 layers and their input gradient: 32 x 32
+    tiles split over K): padded row blocks, N and K tails, one split and forced split counts;
+    against fp64, deterministic (bitwise) and counters left at zero."""
     from aimx import _lib
     C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True, splits=splits)
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
@@ -273,10 +273,10 @@ def test_gemm_skinny(M, N, K, layout, splits):
 
 @pytest.mark.parametrize("M,N,K,ones", [(1024, 1024, 258, True), (1024, 1024, 258, False), (512, 512, 516, True),
                                         (260, 300, 1000, True), (1024, 256, 61, True), (256, 1020, 7, False)])
-def test_gemm_skinny_weight_gradient(M, N, K, ones):
-    """k_skinny's short-K weight-gradient layout (dW = dY^T X: A m-contiguous, B n-contiguous) with
-    the implicit ones column (bias gradient) written into the stage image: K tails inside a stage,
-    a partial last column block holding only the ones column; fp64, bitwise deterministic."""
+def test_gemm_short_k_weight_gradient(M, N, K, ones):
+    """Short-K weight gradients (dW = dY^T X: A m-contiguous, B n-contiguous; the post-pool chain's
+    F x F at K = molecules) with the implicit ones column (bias gradient): K tails, a partial last
+    column block holding only the ones column; fp64, bitwise deterministic."""
     C, col, _, ref, Am = _gemm(M, N, K, "TN", ones=ones)
     assert (C.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
     if ones:
@@ -286,7 +286,7 @@ def test_gemm_skinny_weight_gradient(M, N, K, ones):
     assert torch.equal(C, C2) and torch.equal(col, col2)
 
 
-def test_gemm_skinny_activation_epilogue():
+def test_gemm_deep_k_activation_epilogue():
     C, _, pre, ref, _ = _gemm(258, 1024, 1024, "NT", bias=True, act=4)
     assert (pre.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
     fr = torch.nn.functional.silu(ref)
@@ -335,14 +335,11 @@ def _gemm_raw(M, N, K, layout, off, pa, pb, ones=False):
     (2049, 153, 153, "NT", 1, 0, 0, False), (2049, 153, 153, "NN", 2, 3, 0, False), (1003, 307, 307, "NT", 3, 0, 1, False),
     (1003, 307, 306, "NN", 0, 1, 2, False), (517, 77, 153, "NT", 1, 0, 0, True), (33, 5, 3, "NT", 2, 0, 0, False),
     (700, 153, 31, "NT", 3, 2, 0, False), (64, 160, 614, "NT", 1, 1, 3, False), (300, 45, 153, "TT", 2, 1, 0, False)])
-def test_gemm_unaligned_vector_staging_equals_dword_path(M, N, K, layout, off, pa, pb, ones, monkeypatch):
-    """The 16-byte staging of unaligned k-contiguous operands (k_gemm VU: c4/c5's D = 153 / 307
-    rows; opt-in AIMX_GEMM_VU=1) fills the same LDS tiles as the dword path, so the two results are
-    bit-identical: odd widths and row strides, every base misalignment, K tails shorter than a
-    slice, the ones column; and within 2e-6 of fp64."""
-    monkeypatch.setenv("AIMX_GEMM_VU", "1")
+def test_gemm_unaligned_rows_ones_column(M, N, K, layout, off, pa, pb, ones):
+    """The dword staging of unaligned k-contiguous operands (c4/c5's D = 153 / 307 rows): odd widths
+    and row strides, every base misalignment, K tails shorter than a slice, the ones column; within
+    2e-6 of fp64 and bitwise deterministic."""
     C1, col1, ref, Am = _gemm_raw(M, N, K, layout, off, pa, pb, ones)
-    monkeypatch.setenv("AIMX_GEMM_VU", "0")
     C0, col0, _, _ = _gemm_raw(M, N, K, layout, off, pa, pb, ones)
     assert torch.equal(C1, C0) and torch.equal(col1, col0)
     err = (C1.double() - ref).abs().max().item() / ref.abs().max().item()
@@ -390,6 +387,56 @@ def test_gemm_unaligned_rows_and_bases(M, N, K, layout, off):
     ref = Am.double() @ Bm.double()
     err = (C.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-6, err
+
+
+@pytest.mark.parametrize("M,N,K,layout,off,pa,pb", [
+    (10240, 614, 614, "NT", 0, 1538, 1535),   # c5 [u|g]: F rows of ld 2152, weight rows of 2149 (odd)
+    (10241, 2149, 614, "NN", 1, 2, 0),         # c5 input gradient: B n-contiguous, N tail, odd base
+    (10240, 1024, 1024, "NT", 0, 0, 0),        # c5 concat
+    (20481, 306, 306, "NT", 3, 306, 306),      # c4 [u|g] (K tail inside a float4 and a slice)
+    (9999, 512, 257, "NN", 2, 1, 3),           # K % 32 = 1, every base misaligned
+    (4096, 130, 3000, "NT", 1, 0, 1)])         # deep K, a 2-column tail tile
+def test_gemm_big_tiles(M, N, K, layout, off, pa, pb):
+    """k_gemm_big (128-row blocks of 32 x 32 x 2 fp32 MFMA: the c4 / c5 projections and input
+    gradients): odd row strides and bases (16-byte loads at 4-byte alignment), M / N / K tails, both B
+    layouts; within 2e-6 of fp64 and bitwise deterministic."""
+    C, _, ref, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
+    assert torch.isfinite(C).all()
+    err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    C2, _, _, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
+    assert torch.equal(C, C2)
+
+
+def test_gemm_big_tiles_epilogue_and_trimming():
+    """k_gemm_big's fused epilogue (bias, residual, SiLU with the pre-activation store) and the
+    empty-hop-chunk trimming at c5 size: forward k loop stopped at E (NaN past it is never read) equals
+    the untrimmed product bitwise; the input gradient's tiles past E are skipped (zc_dim 2) and every
+    column < E is bitwise the untrimmed one."""
+    n, d, h = 10240, 307, 6
+    K = d * (h + 1)
+    C, _, pre, ref, _ = _gemm(n, 2 * d, 1024, "NT", bias=True, act=4, res=True)
+    assert (pre.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    fr = torch.nn.functional.silu(ref)  # bias and residual enter the pre-activation (epi_apply)
+    assert (C.double() - fr).abs().max().item() / fr.abs().max().item() < 2e-6
+    counts = torch.zeros(h * n, dtype=torch.int32)
+    counts[0:n:5] = 3
+    rowptr = torch.cat([torch.zeros(1, dtype=torch.int32), counts.cumsum(0).to(torch.int32)]).to(DEV)
+    E = 2 * d
+    g = torch.Generator().manual_seed(9)
+    F = torch.randn(n, K, generator=g)
+    F[:, E:] = 0
+    Fnan = F.clone()
+    Fnan[:, E:] = float("nan")
+    W = torch.randn(2 * d, K, generator=g)
+    full, _, _, ref2, _ = _gemm(n, 2 * d, K, "NT", A=F, B=W)
+    trim, _, _, _, _ = _gemm(n, 2 * d, K, "NT", A=Fnan, B=W, zc=(rowptr, n, h, d, 0))
+    assert torch.equal(full, trim)
+    assert (trim.double() - ref2).abs().max().item() / ref2.abs().max().item() < 2e-6
+    dUG = torch.randn(n, 2 * d, generator=g)
+    full, _, _, _, _ = _gemm(n, K, 2 * d, "NN", A=dUG, B=W)
+    trim, _, _, _, _ = _gemm(n, K, 2 * d, "NN", A=dUG, B=W, zc=(rowptr, n, h, d, 2))
+    assert torch.equal(full[:, :E], trim[:, :E])
 
 
 @pytest.mark.parametrize("d", [76, 153])
@@ -445,18 +492,20 @@ def test_gemm_weight_grad_forced_splits(splits):
     assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
 
 
-@pytest.mark.parametrize("bb", ["auto", "64", "80", "160"])
-def test_wgrad_grouped_matches_fp64(bb, monkeypatch):
+@pytest.mark.parametrize("bb", ["auto", "64", "80"])
+def test_wgrad_grouped_matches_fp64(bb):
     """aimx_wgrad_grouped over the stack's shapes (76 x 76 / 152 x 304 / c5's 307 x 307 and
     614 x 614 with the bias column, long K: the LDS-block kernel with the block edge its rule picks,
-    or 64-, 80- or 160-wide blocks forced by AIMX_WGRAD_BB), a short-K FFN shape, K = 1 and odd
+    or 64- or 80-wide blocks forced by the AIMX_WGRAD_BB option), a short-K FFN shape, K = 1 and odd
     widths (unaligned rows: the LDS kernel's dword loads): dW = dY^T X and db = sum_k dY against
     fp64, deterministic, counters left at zero."""
     from aimx import ops, _lib
-    if bb == "auto":
-        monkeypatch.delenv("AIMX_WGRAD_BB", raising=False)
-    else:
-        monkeypatch.setenv("AIMX_WGRAD_BB", bb)
+    with _lib.options(**({} if bb == "auto" else {"AIMX_WGRAD_BB": int(bb)})):
+        _wgrad_grouped_case()
+
+
+def _wgrad_grouped_case():
+    from aimx import ops, _lib
     g = torch.Generator().manual_seed(11)
     shapes = [(76, 76, 9170, True), (152, 304, 9170, True), (76, 76, 4099, False), (256, 256, 520, True),
               (36, 36, 1, True), (38, 38, 777, True), (8, 12, 64, False),
@@ -919,28 +968,6 @@ def test_fused_adam_add_param_group_after_steps():
         assert norm_rel(a.detach().cpu().numpy(), b.detach().cpu().numpy()) < 1e-6
 
 
-def test_aux_stream_weight_gradients_identical(monkeypatch):
-    """AIMX_AUX=1 (weight gradients forked onto an auxiliary stream, event fork/join) gives the
-    same gradients bit for bit as the single grouped launch (eager execution)."""
-    z, cfg, _ = load_case("c2")
-    af, edges, batch, tc = load_case("c2", DEV)[2]
-    e_empty = torch.empty(0, 2, dtype=torch.long, device=DEV)
-    w = torch.from_numpy(z["loss_w"]).to(DEV)
-
-    def grads(aux):
-        monkeypatch.setenv("AIMX_AUX", "1" if aux else "0")
-        model = _build_model(cfg, int(z["seed"]))
-        out, _, _ = model(af, edges, batch, tc, torch.empty(0, 4, dtype=torch.long, device=DEV), e_empty, e_empty)
-        (out * w).sum().backward()
-        torch.cuda.synchronize()
-        return {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
-
-    a, b = grads(False), grads(True)
-    assert a.keys() == b.keys()
-    for k in a:
-        assert torch.equal(a[k], b[k]), k
-
-
 def test_hop_segment_aligned_tiles_bit_exact():
     """Molecule ids (row_seg) only move the hop's tile cuts: forward and backward are bit-identical
     with and without them, on a large multi-molecule graph (thousands of tiles, cuts both aligned
@@ -1058,8 +1085,9 @@ def test_fused_head_matches_module_path(name, monkeypatch):
     e_empty = torch.empty(0, 2, dtype=torch.long, device=DEV)
     w = torch.from_numpy(z["loss_w"]).to(DEV)
     res = []
+    import models.gnn as mg
     for off in ("0", "1"):
-        monkeypatch.setenv("AIMX_NO_FUSED_HEAD", off)
+        monkeypatch.setattr(mg, "FUSED_HEAD", off == "0")
         model = _build_model(cfg, int(z["seed"]))
         assert model._aimx_head_ok() == (off == "0")
         out, _, _ = model(af, edges, batch, tc, torch.empty(0, 4, dtype=torch.long, device=DEV), e_empty, e_empty)
@@ -1153,7 +1181,7 @@ def test_fused_head_clusters_bit_identical(G, monkeypatch):
     seed = torch.tensor([11], device=DEV)
     res = {}
     for S in ("1", "2", "4", "8"):
-        monkeypatch.setenv("AIMX_HEAD_CLUSTER", S)
+        monkeypatch.setattr(_lib, "HEAD_CLUSTER_FORCE", int(S))
         t = [b.to(DEV).requires_grad_() for b in base]
         x, wp, bp = t[:3]
         blocks = [tuple(t[3 + 4 * i:7 + 4 * i]) for i in range(2)]
@@ -1172,17 +1200,20 @@ def test_fused_head_clusters_bit_identical(G, monkeypatch):
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "act_gelu", "stereo"])
 def test_streamed_mlp_forced_parity(name, monkeypatch):
-    """AIMX_MLPS=1 (the weight-streamed node-update chain, mlp.hip k_mlps_*, the default for D > 128)
-    forced onto the small-D cases keeps the model within the parity contract."""
-    monkeypatch.setenv("AIMX_MLPS", "1")
-    test_model_case(name)
+    """The AIMX_MLPS = 1 option (the weight-streamed node-update chain, mlp.hip k_mlps_*, the default
+    for D > 128) forced onto the small-D cases keeps the model within the parity contract."""
+    from aimx import _lib
+    with _lib.options(AIMX_MLPS=1):
+        test_model_case(name)
 
 
 @pytest.mark.parametrize("name", ["c4s", "c5s"])
 def test_per_gemm_mlp_path_parity_wide(name, monkeypatch):
-    """AIMX_MLPS=0 (one GEMM per MLP linear) at D = 153 / 307 stays within the parity contract."""
-    monkeypatch.setenv("AIMX_MLPS", "0")
-    test_model_case(name)
+    """The AIMX_MLPS = 0 option (one GEMM per MLP linear) at D = 153 / 307 stays within the parity
+    contract."""
+    from aimx import _lib
+    with _lib.options(AIMX_MLPS=0):
+        test_model_case(name)
 
 
 def _stack_case(hidden, hops, mols, seed=0):
@@ -1217,17 +1248,18 @@ def test_streamed_mlp_matches_per_gemm(hidden, hops, mols, rt, monkeypatch):
     kw = dict(num_hops=hops, num_layers=3, num_mlp=2, act="silu", training=True, drop_p=0.05, drop_seed=seed)
     w = torch.randn(n, d, device=DEV)
     res = {}
+    from aimx import _lib
     for mode in ("0", "1"):
-        monkeypatch.setenv("AIMX_MLPS", mode)
+        opts = {"AIMX_MLPS": int(mode)}
         if rt is not None and mode == "1":
-            monkeypatch.setenv("AIMX_MLPS_RT", rt)
-        xs = x.clone().requires_grad_()
-        ps = [p.detach().clone().requires_grad_() for p in params]
-        y = ops.message_passing_stack(plan, xs, ps, **kw)
-        (y * w).sum().backward()
-        torch.cuda.synchronize()
+            opts["AIMX_MLPS_RT"] = int(rt)
+        with _lib.options(**opts):
+            xs = x.clone().requires_grad_()
+            ps = [p.detach().clone().requires_grad_() for p in params]
+            y = ops.message_passing_stack(plan, xs, ps, **kw)
+            (y * w).sum().backward()
+            torch.cuda.synchronize()
         res[mode] = [y.detach()] + [xs.grad] + [p.grad for p in ps]
-        monkeypatch.delenv("AIMX_MLPS_RT", raising=False)
     for i, (a, b) in enumerate(zip(res["1"], res["0"])):
         assert a is not None and b is not None, i
         assert torch.isfinite(a).all(), i
@@ -1237,10 +1269,11 @@ def test_streamed_mlp_matches_per_gemm(hidden, hops, mols, rt, monkeypatch):
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "act_gelu", "stereo"])
 def test_per_gemm_mlp_path_parity(name, monkeypatch):
-    """AIMX_MLPW=0 (one GEMM per MLP linear, the path D > 128 always takes) keeps the small-D cases
-    within the parity contract too (the default there is the weight-resident fused chain)."""
-    monkeypatch.setenv("AIMX_MLPW", "0")
-    test_model_case(name)
+    """The AIMX_MLPW = 0 option (one GEMM per MLP linear) keeps the small-D cases within the parity
+    contract too (the default there is the weight-resident fused chain)."""
+    from aimx import _lib
+    with _lib.options(AIMX_MLPW=0):
+        test_model_case(name)
 
 
 # ------------------------------------------------------------------------------- stereochemistry

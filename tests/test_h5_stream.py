@@ -172,15 +172,12 @@ def test_stream_batches_span_chunks():
 
 
 def _read_all(path, pos, hops, direct, threads=3):
-    old = os.environ.get("AIMX_H5_DIRECT")
-    os.environ["AIMX_H5_DIRECT"] = "1" if direct else "0"
+    lib = h5.load_h5()
+    lib.aimx_h5_set_direct(1 if direct else 0)  # test hook: the direct path allowed or not
     try:
         f = h5.H5File(path)
     finally:
-        if old is None:
-            del os.environ["AIMX_H5_DIRECT"]
-        else:
-            os.environ["AIMX_H5_DIRECT"] = old
+        lib.aimx_h5_set_direct(1)
     assert f.direct_read == direct
     store, kept = f.read_store(pos, hops, 1, threads)
     return _collate_h(store, hops), kept

@@ -118,13 +118,14 @@ def test_fused_adam_has_no_cpu_path():
 
 def test_head_cluster_rule(monkeypatch):
     """Clustered head launches: a lone process and data parallelism with one GPU per rank keep them;
-    ranks sharing a GPU, an unknown launcher layout and the auxiliary stream drop to 1 workgroup
-    per tile (aimx/_lib.py head_cluster_allowed)."""
+    ranks sharing a GPU and an unknown launcher layout drop to 1 workgroup per tile
+    (aimx/_lib.py head_cluster_allowed); HEAD_CLUSTER_FORCE overrides."""
     import torch.distributed as dist
 
     from aimx import _lib
-    for k in ("AIMX_HEAD_CLUSTER", "AIMX_AUX", "LOCAL_WORLD_SIZE", "LOCAL_RANK"):
+    for k in ("LOCAL_WORLD_SIZE", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(_lib, "HEAD_CLUSTER_FORCE", None)
     assert _lib.head_cluster(256) == 2 and _lib.head_cluster(512) == 4  # lone process
     monkeypatch.setattr(dist, "is_initialized", lambda: True)
     monkeypatch.setattr(dist, "get_world_size", lambda group=None: 8)
@@ -139,8 +140,5 @@ def test_head_cluster_rule(monkeypatch):
     monkeypatch.setenv("LOCAL_RANK", "3")
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
     assert _lib.head_cluster(256) == 1  # 8 ranks share one GPU (rehearsal)
-    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
-    monkeypatch.setenv("AIMX_AUX", "1")
-    assert _lib.head_cluster(256) == 1
-    monkeypatch.setenv("AIMX_HEAD_CLUSTER", "4")
+    monkeypatch.setattr(_lib, "HEAD_CLUSTER_FORCE", 4)
     assert _lib.head_cluster(256) == 4  # explicit override

@@ -1,9 +1,18 @@
 #!/bin/bash
-# round-5 working call (overwritten per call): Adam with the clip fold inside the update
+# round-6 working call (overwritten per call): full -m gpu suite after the knob pruning + the
+# large-tile GEMM, then the big-GEMM variants (tuning build) and c2 / c5 bench lines
 export PYTHONDONTWRITEBYTECODE=1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 T="python3 -u -m pytest -x -q --timeout 200 --timeout-method thread"
-B="python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 200 --warmup 20"
+TL=aimnet-x2d_amd/lib/libaimx_tune.so
 tools/gpu_steps.sh \
- "400 r5w/tests.log $T tests/test_gpu_train.py tests/test_gpu_autograph.py tests/test_gpu_parity.py -k 'adam or trajectory or clip or train or graph'" \
- "300 r5w/c2.log $B" \
- "300 r5w/c5.log $B --config c5"
+ "900 r6b/tests.log $T tests -m gpu" \
+ "300 r6b/gemm_old.log AIMX_LIB_PATH=$TL AIMX_GEMM_BIG=0 python3 tools/gemm_micro.py big" \
+ "300 r6b/gemm_w8.log AIMX_LIB_PATH=$TL AIMX_GEMM_BIG_W=8 python3 tools/gemm_micro.py big" \
+ "300 r6b/gemm_w4.log AIMX_LIB_PATH=$TL AIMX_GEMM_BIG_W=4 python3 tools/gemm_micro.py big" \
+ "300 r6b/gemm_w8_128.log AIMX_LIB_PATH=$TL AIMX_GEMM_BIG_W=8 AIMX_GEMM_BIG=128 python3 tools/gemm_micro.py big" \
+ "300 r6b/gemm_w8_64.log AIMX_LIB_PATH=$TL AIMX_GEMM_BIG_W=8 AIMX_GEMM_BIG=64 python3 tools/gemm_micro.py big" \
+ "300 r6b/c5.log python3 bench.py --config c5 --no-cpu-baseline --no-eager --no-roofline" \
+ "300 r6b/c5_old.log AIMX_LIB_PATH=$TL AIMX_GEMM_BIG=0 python3 bench.py --config c5 --no-cpu-baseline --no-eager --no-roofline" \
+ "300 r6b/c4.log python3 bench.py --config c4 --no-cpu-baseline --no-eager --no-roofline" \
+ "300 r6b/c2.log python3 bench.py --no-cpu-baseline --no-eager --no-roofline"
