@@ -80,7 +80,7 @@ class GemmArgs(ctypes.Structure):
         ("splits", c_i32), ("workspace", c_ptr), ("workspace_bytes", c_size),
         ("counters", c_ptr), ("n_counters", c_i64),
         ("zc_rowptr", c_ptr), ("zc_rows", c_i64), ("zc_chunks", c_i32), ("zc_width", c_i64), ("zc_dim", c_i32),
-        ("precision", c_i32),
+        ("precision", c_i32), ("m_base", c_i64),
     ]
 
 

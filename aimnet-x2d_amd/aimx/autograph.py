@@ -246,6 +246,15 @@ class _Bucket:
         cur = torch.cuda.current_stream(self.dev)
         side = torch.cuda.Stream(device=self.dev)
         side.wait_stream(cur)
+        # the post-pool head runs on the G real molecules only (GNN._aimx_head_rows): the replay
+        # hands out outs[0][:G], the padding molecules' rows are never read
+        model.__dict__["_aimx_head_rows"] = self.G
+        try:
+            self._capture(model, warmup, params, live, args, cur, side)
+        finally:
+            model.__dict__.pop("_aimx_head_rows", None)
+
+    def _capture(self, model, warmup, params, live, args, cur, side):
         with torch.cuda.stream(side):  # warm-up: plans, workspaces, allocator pools, seed state
             for _ in range(warmup):
                 with _aliased(model, live) as al:

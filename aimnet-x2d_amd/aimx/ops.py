@@ -827,11 +827,8 @@ def wgrad_grouped(problems):
         arr[i].M, arr[i].N, arr[i].K = dy.shape[1], x.shape[1], dy.shape[0]
     wsb = lib.aimx_wgrad_grouped_workspace_bytes(arr, n)
     ws = torch.empty(max(wsb // 4, 1), dtype=_F32, device=dev)
-    if stream is not None:
-        ws.record_stream(stream)
-    check(lib.aimx_wgrad_grouped(arr, n, ptr(ws), ws.numel() * 4, ptr(_lib.counters(dev, 0 if stream is None else 1)),
-                                 _lib.N_COUNTERS, stream.cuda_stream if stream is not None else stream_ptr(dev)),
-          "wgrad_grouped")
+    check(lib.aimx_wgrad_grouped(arr, n, ptr(ws), ws.numel() * 4, ptr(_lib.counters(dev)), _lib.N_COUNTERS,
+                                 stream_ptr(dev)), "wgrad_grouped")
     return ws
 
 

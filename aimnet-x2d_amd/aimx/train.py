@@ -115,7 +115,6 @@ class GraphedTrainStep:
 
     def __init__(self, model, criterion, optimizer, example_batch, n_real=None, sync=None, warmup=3,
                  ddp_graph=None, inject_capture_failure=None, max_layouts=1):
-        import os
         # test hook (tests/test_gpu_ddp.py): make the "capture" attempt raise as a failing RCCL build
         # would, to exercise the split fallback on any box
         if inject_capture_failure is None:
@@ -136,7 +135,13 @@ class GraphedTrainStep:
         self.eager_steps = 0
 
         def fwd_bwd(batch):
-            out, _, _ = model(*batch.model_args())
+            # the post-pool head runs on the B real molecules only (their rows are the loss's; the
+            # padding molecules' outputs are never read): GNN._aimx_head_rows
+            model.__dict__["_aimx_head_rows"] = B
+            try:
+                out, _, _ = model(*batch.model_args())
+            finally:
+                model.__dict__.pop("_aimx_head_rows", None)
             if padded is not None:
                 # fused L1: the padding rows' zero gradient in the loss's backward launch, and the
                 # step's loss sum / NaN flag / step count in its forward launch

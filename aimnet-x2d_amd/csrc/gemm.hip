@@ -125,7 +125,8 @@ __device__ __forceinline__ void epi_apply(const AimxGemmArgs& a, const int (&m)[
     const uint64_t seed = (uint64_t)*a.drop_seed;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
-      const bool keep = hash_uniform(seed, a.drop_salt, (uint64_t)m[e] * (uint64_t)a.N + (uint64_t)n[e]) >= a.drop_p;
+      const bool keep =
+          hash_uniform(seed, a.drop_salt, (uint64_t)(m[e] + a.m_base) * (uint64_t)a.N + (uint64_t)n[e]) >= a.drop_p;
       x[e] = keep ? x[e] * scale : 0.f;
       if (ok[e] & !ones[e]) a.mask_out[m[e] * a.ldmask + n[e]] = keep ? 1 : 0;
     }
@@ -1252,9 +1253,11 @@ void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
   const int kb = z * t.kchunk[q];
   const int kend = min((int)pr.K, kb + t.kchunk[q]);
   const int nsub = kend > kb ? (kend - kb + kWbK - 1) / kWbK : 0;
+  // descriptors over this split's K rows only (32-bit offsets from the split's first row: a problem
+  // of any K stays addressable; wg_plan keeps one split's rows under 2 GiB)
   const uint32_t ab = t.a_bytes[q], bb = t.b_bytes[q];
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(pr.dY, ab);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(pr.X, bb);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(pr.dY + (int64_t)kb * pr.ld_dy, ab);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(pr.X + (int64_t)kb * pr.ld_x, bb);
   const uint32_t lda = (uint32_t)pr.ld_dy, ldb = (uint32_t)pr.ld_x;
   const bool v4 = VM == 2 ? t.v4[q] != 0 : VM == 1;
 
@@ -1270,18 +1273,18 @@ void k_wgrad_lds(const WbTable t, float* ws, int32_t* counters) {
       const bool isb = u >= kWbV / 2;
       const int f = tid + (isb ? u - kWbV / 2 : u) * kWbT;
       const int row = f / (BB / 4), c = 4 * (f % (BB / 4));
-      const int k = k0 + row;
+      const int k = k0 + row, kr = k - kb;  // kr: row within the split (the descriptors' base)
       const int col = (isb ? n0 : m0) + c, lim = isb ? zlim : M;
       const uint32_t ld = isb ? ldb : lda, bytes = isb ? bb : ab;
       const __amdgpu_buffer_rsrc_t r = isb ? rb : ra;
       const bool kok = k < kend;
       floatx4 v;
       if (v4) {
-        v = bload4(r, kok && col < lim ? 4u * ((uint32_t)k * ld + (uint32_t)col) : bytes, 0);
+        v = bload4(r, kok && col < lim ? 4u * ((uint32_t)kr * ld + (uint32_t)col) : bytes, 0);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          v[i] = bload(r, kok && col + i < lim ? 4u * ((uint32_t)k * ld + (uint32_t)(col + i)) : bytes, 0);
+          v[i] = bload(r, kok && col + i < lim ? 4u * ((uint32_t)kr * ld + (uint32_t)(col + i)) : bytes, 0);
       }
       stage[u] = v;
     }
@@ -1600,6 +1603,10 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs, int bb) {
     if (min_wgs > 0)
       sp = std::max(sp, std::min<int64_t>({64, p.K / 128, cdiv(min_wgs, (int64_t)w.tiles_x * w.tiles_y)}));
     w.kchunk = (int)(cdiv(cdiv(p.K, sp), kWbK) * kWbK);
+    // one split's rows of either operand under 2 GiB (its descriptors start at its first row): a
+    // very long K (a large inference-time batch) takes more splits instead of a refusal
+    const int64_t ld = std::max(p.ld_dy, p.ld_x), rows_max = ((1ll << 31) / 4 - 2 * ld) / ld;
+    if (w.kchunk > rows_max) w.kchunk = (int)std::max<int64_t>(kWbK, rows_max / kWbK * kWbK);
     w.splits = (int)std::max<int64_t>(1, cdiv(p.K, w.kchunk));
     return w;
   }
@@ -1618,6 +1625,10 @@ bool wg_valid(const AimxWgradProblem& p) {
   if (p.M < 1 || p.N < 1 || p.K < 0 || !p.dY || !p.X || !p.dW) return false;
   if (p.ld_dy < p.M || p.ld_x < p.N || p.ld_dw < p.N) return false;
   if (p.zc_rowptr && (p.zc_chunks < 0 || p.zc_rows < 0 || p.zc_width < 0)) return false;
+  if (p.K >= (1ll << 31) || p.M >= (1ll << 31) || p.N >= (1ll << 31)) return false;
+  // the LDS-block kernel addresses each split from its first row (wg_plan bounds a split's rows);
+  // the short-K kernel addresses the whole operand
+  if (p.K >= 2048) return 4 * 64 * std::max(p.ld_dy, p.ld_x) < (1ll << 31);
   const int64_t a_ext = 4 * ((p.K - 1) * p.ld_dy + p.M), b_ext = 4 * ((p.K - 1) * p.ld_x + p.N);
   return p.K == 0 || (a_ext < (1ll << 31) && b_ext < (1ll << 31));
 }
@@ -1740,6 +1751,29 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
   const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;
   const int64_t a_ext = 4 * ((a.M - 1) * a.sam + (a.K - 1) * a.sak + 1);
   const int64_t b_ext = Nreal > 0 ? 4 * ((a.K - 1) * a.sbk + (Nreal - 1) * a.sbn + 1) : 4;
+  if (a.K > 0 && a_ext >= (1ll << 31) && a.sak == 1 && a.M > 1) {
+    // A's rows past 2 GiB (a very large batch: ~250 k atoms at c5's F-row stride): consecutive row
+    // chunks of the product, each its own launch over offset row pointers (rows are independent;
+    // the epilogue operands are row-indexed, the dropout hash keyed by the global row)
+    const int64_t rows = std::max<int64_t>(1, ((1ll << 31) / 4 - a.K - 64) / std::max<int64_t>(a.sam, 1));
+    for (int64_t m0 = 0; m0 < a.M; m0 += rows) {
+      AimxGemmArgs c = a;
+      c.M = std::min(rows, a.M - m0);
+      c.m_base = a.m_base + m0;
+      c.A = a.A + m0 * a.sam;
+      c.C = a.C + m0 * a.ldc;
+      if (a.pre) c.pre = a.pre + m0 * a.ldpre;
+      if (a.dact_pre) c.dact_pre = a.dact_pre + m0 * a.lddact;
+      for (int r = 0; r < 3; ++r)
+        if (a.res[r]) c.res[r] = a.res[r] + m0 * a.ldres[r];
+      if (a.mask_in) c.mask_in = a.mask_in + m0 * a.ldmask;
+      if (a.mask_out) c.mask_out = a.mask_out + m0 * a.ldmask;
+      if (a.col_out) c.col_out = a.col_out + m0;
+      const int rc = launch_gemm(c, s);
+      if (rc != AIMX_OK) return rc;
+    }
+    return AIMX_OK;
+  }
   if (a.K > 0 && (a_ext >= (1ll << 31) || b_ext >= (1ll << 31))) return AIMX_EARG;
   if (a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31)) return AIMX_EARG;
   // descriptor byte counts = the operand's true extent: every in-range element is readable, loads
@@ -1863,8 +1897,9 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
       // rounded width long), so its valid components are never cut by the range check
       const int64_t am = v4 ? std::min<int64_t>(pr.ld_dy, cdiv(pr.M, 4) * 4) : pr.M;
       const int64_t bm = v4 ? std::min<int64_t>(pr.ld_x, cdiv(pr.N, 4) * 4) : pr.N;
-      tb.a_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * (Kr * pr.ld_dy + am));
-      tb.b_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * (Kr * pr.ld_x + bm));
+      const int64_t Ks = std::min<int64_t>(Kr, w.kchunk - 1);  // rows of one split past its first
+      tb.a_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * (Ks * pr.ld_dy + am));
+      tb.b_bytes[k] = (uint32_t)std::max<int64_t>(4, 4 * (Ks * pr.ld_x + bm));
       tb.ws_off[k] = ws_off;
       tb.cnt_off[k] = cnt_off;
       blkb += w.splits * nt;

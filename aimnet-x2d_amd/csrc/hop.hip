@@ -628,6 +628,32 @@ int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_
     return true;
   };
   const int vec = ok(4) ? 4 : (ok(2) ? 2 : 1);
+  // Launch size: the kernels index threads and rows in 32 bits. A call past that (a very large
+  // inference batch) runs as consecutive row ranges, each inside one output chunk: a range's row
+  // pointers, output rows, residual rows and molecule ids are offsets of the caller's (rows are
+  // independent sums, so the result is the one-launch result, bit for bit).
+  {
+    const int64_t upr_v = cdiv(D, vec);
+    int64_t cap = std::max<int64_t>(1, ((int64_t)INT32_MAX - 1) / std::max<int64_t>(upr_v, 1) / 2);
+    if (const int64_t f = opt_i64("AIMX_HOP_MAX_ROWS", 0)) cap = std::min(cap, f);  // test hook
+    const int64_t rpc = (out_rpc > 0 && out_rpc < rows) ? out_rpc : rows;
+    if (rows > cap) {
+      for (int64_t r0 = 0; r0 < rows;) {
+        const int64_t in_chunk = rpc - r0 % rpc;              // rows left in r0's output chunk
+        const int64_t n = std::min<int64_t>({cap, in_chunk, rows - r0});
+        float* o = out + (r0 % rpc) * out_ld + (r0 / rpc) * (rpc < rows ? out_cs : 0);
+        const bool first = r0 < rpc;                             // row_seg covers the first chunk
+        const int rc = segment_gather_sum(src, src_ld, src_rpc, src_cs, D, rowptr + r0, col, n, o, out_ld, 0, 0,
+                                          add0 ? add0 + r0 * add0_ld : nullptr, add0_ld,
+                                          add1 ? add1 + r0 * add1_ld : nullptr, add1_ld,
+                                          first && row_seg ? row_seg + r0 * row_seg_stride : nullptr, row_seg_stride,
+                                          stream, 0);
+        if (rc != AIMX_OK) return rc;
+        r0 += n;
+      }
+      return AIMX_OK;
+    }
+  }
   // rows that are not runs of 16-byte-aligned vectors (odd D, unaligned chunk offsets) take the
   // 16-byte-at-4-byte-alignment kernel (hop_unal.hip)
   const HopEnv& E = hop_env();

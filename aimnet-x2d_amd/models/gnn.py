@@ -207,6 +207,12 @@ class GNN(nn.Module):
         finally:
             self.pooling._aimx_plan = None
 
+        # a caller that reads only the first rows of the output (GraphedTrainStep, the autograph: the
+        # rows after them are padding molecules) sets _aimx_head_rows, and the post-pool chain
+        # (gnn.py:252-258: a per-molecule function) runs on those rows alone
+        rows = self.__dict__.get("_aimx_head_rows")
+        if rows is not None and 0 < rows < x_pooled.shape[0]:
+            x_pooled = x_pooled[:rows]
         try:
             if self._aimx_head_ok():
                 # gnn.py:252-258 as one fused operator forward and backward (aimx.ops.head)

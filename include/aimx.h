@@ -46,7 +46,8 @@ const char* aimx_version(void);
  * alternative-path parity tests: "AIMX_MLPW" 0 = per-GEMM node-update MLP, "AIMX_MLPS" 0 / 1 =
  * weight-streamed MLP off / for every width, "AIMX_MLPS_RT" row tiles per chunk, "AIMX_WGRAD_BB"
  * 64 / 80 weight-gradient block edge, "AIMX_GEMM_BIG" 0 / 64 / 128 large-tile GEMM off / forced
- * tile, "AIMX_GEMM_BIG_W" 4 / 8 waves, "AIMX_HEAD8" 0 = 16-molecule head kernels). The tuning build
+ * tile, "AIMX_GEMM_BIG_W" 4 / 8 waves, "AIMX_HEAD8" 0 = 16-molecule head kernels, "AIMX_HOP_MAX_ROWS"
+ * n = the hop's row-range splitting at n rows per launch instead of its 2^31 limit). The tuning build
  * (make tune -> lib/libaimx_tune.so) also reads these names, and its A/B knobs, from the
  * environment. aimx_set_option returns AIMX_EARG for a name longer than 47 bytes or past 16 names. */
 int aimx_set_option(const char* name, int64_t value);
@@ -183,6 +184,10 @@ typedef struct AimxGemmArgs {
    * (v_mfma_f32_16x16x32_bf16); C, the epilogue and every other tensor stay fp32. Long-K
    * weight-gradient GEMMs (A m-contiguous, B n-contiguous, K >= 512) stay exact fp32. */
   int32_t precision;
+  /* Row offset of this call's row 0 in a larger product (the dropout hash is keyed by the global row
+   * m_base + m, so a product run as row chunks draws the masks of the one-launch product); 0 for a
+   * caller's own calls. */
+  int64_t m_base;
 } AimxGemmArgs;
 #define AIMX_PREC_FP32 0
 #define AIMX_PREC_BF16 1

@@ -198,3 +198,34 @@ def test_hop_rows_long_molecule_bit_exact():
     assert np.array_equal(outs[0][0], _fwd_ref(x, edges[:, 0], edges[:, 1], 3))
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert np.array_equal(outs[0][1], _bwd_ref(g.cpu().numpy(), edges[:, 0], edges[:, 1], n))
+
+
+@pytest.mark.parametrize("d,hops,cap", [(76, 3, 37), (153, 3, 101), (307, 6, 64)])
+def test_hop_row_range_split_bit_exact(d, hops, cap):
+    """A hop launch past the kernels' 32-bit row / thread indexing runs as consecutive row ranges
+    inside each output chunk (hop.hip; forced here at `cap` rows per launch through the
+    AIMX_HOP_MAX_ROWS option): forward into the stack's chunked F layout and the backward with its
+    residual terms are bit-identical to one launch."""
+    from aimx import _lib
+    lib, P, S = _abi()
+    n, edges, batch = _graph("synth40", 30, hops, seed=d)
+    plan = _plan(n, hops, edges, batch)
+    seg, seg_st = plan.row_seg()
+    K = d * (hops + 1)
+    rng = np.random.default_rng(3)
+    F0 = torch.from_numpy(rng.standard_normal((n, K)).astype(np.float32)).to(DEV)
+    dF = torch.from_numpy(rng.standard_normal((n, K)).astype(np.float32)).to(DEV)
+    dY = torch.from_numpy(rng.standard_normal((n, 2 * d)).astype(np.float32)).to(DEV)
+    res = []
+    for opts in ({}, {"AIMX_HOP_MAX_ROWS": cap}):
+        with _lib.options(**opts):
+            F = F0.clone()
+            assert lib.aimx_segment_gather_sum(P(F), K, 0, 0, d, P(plan.fwd.rowptr), P(plan.fwd.col), hops * n,
+                                               P(F) + 4 * d, K, n, d, None, 0, None, 0, seg, seg_st, S(DEV)) == 0
+            dst = torch.zeros((n, 2 * d), device=DEV)
+            assert lib.aimx_segment_gather_sum(P(dF) + 4 * d, K, n, d, d, P(plan.bwd.rowptr), P(plan.bwd.col), n,
+                                               P(dst) + 4 * d, 2 * d, 0, 0, P(dF), K, P(dY) + 4 * d, 2 * d, seg,
+                                               seg_st, S(DEV)) == 0
+            torch.cuda.synchronize()
+            res.append((F, dst))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])

@@ -273,3 +273,50 @@ def test_l1_loss_gradient_in_forward_launch():
         half = torch.full((), 0.5, device=DEV)
         ops.l1_loss(p3, y, weights, per_sample, rows=32, accum=acc(), grad_of=one).backward(half)
         assert torch.equal(p3.grad, 0.5 * p1.grad)
+
+
+def test_large_batch_past_2gib_equals_two_batches():
+    """A batch past every 32-bit operand extent (reference predictors take any batch_size,
+    inference/pipeline.py:559): GNN forward + backward at hidden 1024 / 6 hops on 6,400 40-atom
+    molecules (~265 k atoms; the stack's F = [x | hop chunks] rows of 2,152 floats are 2.3 GB, the
+    weight gradients' K = atoms spans more). The GEMMs address such operands in 64 bits or run as row
+    chunks, the weight gradients split K so each split's descriptors stay under 2 GiB. Equals the same
+    molecules as two batches: outputs row for row, gradients summed (loss = sum(out * w) is additive
+    over molecules), within 1e-5 norm-relative."""
+    from aimx import autograph
+    from aimx import data as adata
+    from aimx.synth import synth_molecules
+    from models import GNN
+    hops, n_mols = 6, 6400
+    mols = synth_molecules(n_mols, seed=17)
+    rng = np.random.default_rng(5)
+    w = rng.standard_normal((n_mols, 1)).astype(np.float32)
+    torch.manual_seed(3)
+    fs = {"atom_type": 119, "hydrogen_count": 9, "degree": 7, "hybridization": 7}
+    m = GNN(fs, 1024, 1, num_shells=hops, shell_conv_dropout=0.0, ffn_dropout=0.0).to("cuda").train()
+    autograph.enable(m, False)
+
+    def run(lo, hi):
+        col = adata.collate(mols[lo:hi], hops)
+        b = adata.DeviceBatch(col, "cuda", total_charges=np.zeros(hi - lo, np.float32))
+        m.zero_grad(set_to_none=True)
+        out, _, _ = m(*b.model_args())
+        (out * torch.from_numpy(w[lo:hi]).cuda()).sum().backward()
+        torch.cuda.synchronize()
+        return out.detach().cpu(), {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()
+                                    if p.grad is not None}, col["batch"].shape[0]
+
+    o_big, g_big, n_big = run(0, n_mols)
+    assert n_big * 2152 * 4 > 2 ** 31
+    o1, g1, _ = run(0, n_mols // 2)
+    o2, g2, _ = run(n_mols // 2, n_mols)
+    o_ref = torch.cat([o1, o2])
+    assert torch.isfinite(o_big).all()
+    assert ((o_big - o_ref).norm() / o_ref.norm()).item() < 1e-5
+    assert g_big.keys() == g1.keys() == g2.keys()
+    for k in g_big:
+        ref = g1[k] + g2[k]
+        den = ref.norm()
+        if ".attention_weights." in k and k.endswith(".bias"):  # exactly 0 (softmax shift invariance)
+            den = (g1[k[:-4] + "weight"] + g2[k[:-4] + "weight"]).norm()
+        assert ((g_big[k] - ref).norm() / den.clamp_min(1e-30)).item() < 1e-5, k
