@@ -1673,11 +1673,11 @@ int big_bn(const AimxGemmArgs& a) {
   if (mode == 0) return 0;
   if (a.precision != AIMX_PREC_FP32 || a.ones_col || a.splits > 1) return 0;
   if (a.sak != 1 || !(a.sbk == 1 || a.sbn == 1)) return 0;
-  if (a.M < 4096 || a.N < 128 || a.K < 128 || a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31))
+  if (a.M < 256 || a.N < 64 || a.K < 64 || a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31))
     return 0;
   if (a.zc_rowptr && a.zc_width < kGbBK) return 0;
-  if ((double)a.M * (double)a.N * (double)a.K < 1.5e9) return 0;
-  if (mode == 64 || mode == 128) return (int)mode;
+  if (mode == 64 || mode == 128) return (int)mode;  // forced (tests, tuning build): any size
+  if (a.M < 4096 || a.N < 128 || a.K < 128 || (double)a.M * (double)a.N * (double)a.K < 1.5e9) return 0;
   const int64_t tm = cdiv(a.M, kGbBM);
   const int64_t w128 = cdiv(tm * cdiv(a.N, 128), 256) * 128, w64 = cdiv(tm * cdiv(a.N, 64), 256) * 64;
   return w64 < w128 ? 64 : 128;

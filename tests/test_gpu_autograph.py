@@ -252,7 +252,7 @@ def test_autograph_recaptures_after_storage_swap():
         m2.zero_grad(set_to_none=True)
         m2(*b.model_args())[0].sum().backward()
     st = m2.__dict__["_aimx_autograph_state"]
-    old = {id(bk) for bk in st.buckets.values()}
+    old = list(st.buckets.values())  # held: a freed bucket's id() could be reused by its successor
     with torch.no_grad():
         vec = parameters_to_vector(m2.parameters()) * 1.25
         vector_to_parameters(vec, m2.parameters())
@@ -261,7 +261,7 @@ def test_autograph_recaptures_after_storage_swap():
         m.zero_grad(set_to_none=True)
     o1 = m1(*b.model_args())[0]
     o2 = m2(*b.model_args())[0]
-    assert not old & {id(bk) for bk in st.buckets.values()}  # the bucket was re-captured
+    assert not any(bk is o for bk in st.buckets.values() for o in old)  # the bucket was re-captured
     assert _rel(o2.detach(), o1.detach()) < 1e-5
     o1.sum().backward()
     o2.sum().backward()

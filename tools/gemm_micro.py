@@ -74,7 +74,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "big":
     # the c4 / c5 MFMA-bound GEMMs in the step's layouts (hipBLASLt as a yardstick only): embedding
     # projection, [Wi; Wg] input projection (K trimmed to the non-empty chunks, weight rows of the
     # full D(h+1)), its input gradient, the node-update D x D, the concat and its input gradient
-    for M, D, h, H in ((20480, 153, 3, 512), (10240, 307, 6, 1024)):
+    for M, D, h, H in ((9170, 76, 3, 256), (20480, 153, 3, 512), (10240, 307, 6, 1024)):
         K_ig = D * (h + 1)
         run(M, H, 256, "NT", f"h{H} embed proj")
         run(M, 2 * D, 2 * D, "NT", f"h{H} [u|g] fwd (zc)", lda=(K_ig + 3) // 4 * 4, ldb=K_ig)
