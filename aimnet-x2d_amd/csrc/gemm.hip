@@ -697,8 +697,17 @@ __device__ __forceinline__ float gb_pick(const floatx4& v, int e) {
   return (unsigned)e < 4u ? x : 0.f;
 }
 
-template <int BN, int NW, bool BKC>
-__global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int tiles_n, int ntiles) {
+// AK: A k-contiguous ([m][k], the projections) or m-contiguous ([k][m]: a weight gradient's dY^T);
+// BKC: B k-contiguous ([n][k]) or n-contiguous ([k][n]). An m- / n-contiguous operand is staged by
+// 16-byte runs along m / n of 8 k rows per wave (128 bytes per k row) and transposed by the LDS
+// writes. A weight gradient (a.ones_col: column N - 1 of B is the implicit ones column, the bias
+// gradient; zc_dim 1: B's columns past the non-empty hop chunks read as 0) splits K over `splits`
+// blocks per tile: partial tiles go to sc1 slabs in accumulator order, and the last block of a tile
+// to arrive (agent-scope counter, self-resetting) sums them in split order (deterministic) and runs
+// the epilogue, as k_gemm's split-K path.
+template <int BN, int NW, bool AK, bool BKC>
+__global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int tiles_n, int ntiles, int kchunk,
+                                                     int splits) {
   constexpr int BM = kGbBM, BK = kGbBK, S = kGbS, NT = 64 * NW;
   constexpr int WR = NW / 2;                      // wave rows (2 or 4); two wave columns
   constexpr int FM = BM / (32 * WR), FN = BN / 64;  // 32 x 32 tiles per wave along m / n
@@ -710,53 +719,69 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int 
   static_assert(BM * (BN + 1) <= 2 * (LA + LB), "C tile must fit the staging LDS");
   static_assert(NA >= 1 && NB >= 1 && FM >= 1 && FN >= 1, "tile geometry");
 
-  // XCD-aware tile order: the blocks one XCD runs (b % 8 equal under round-robin dispatch) take a
-  // contiguous range of tiles, row block major (bijective for any grid size)
+  // XCD-aware order: the blocks one XCD runs (b % 8 equal under round-robin dispatch) take a
+  // contiguous range of (tile, split) items, row block major, a tile's splits adjacent (bijective
+  // for any grid size)
   const int bid = blockIdx.x, nb = (int)gridDim.x;
   const int q = nb / 8, rr = nb % 8, xcd = bid % 8, loc = bid / 8;
-  const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
-  if (tile >= ntiles) return;
+  const int item = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  if (item >= ntiles * splits) return;
+  const int tile = item / splits, z = item - tile * splits;
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int M = (int)a.M, N = (int)a.N;
-  int kend = (int)a.K;
+  const int Nreal = a.ones_col ? N - 1 : N;
+  int kend = (int)a.K, nlim = Nreal;  // nlim: B columns past it read as 0 (the ones column aside)
   if (a.zc_rowptr) {
     const int zE = zc_extent(a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width);
     if (a.zc_dim == 0) {
       kend = min(kend, zE);
-    } else if (n0 >= zE) {
-      if (a.zc_dim == 1)
+    } else if (n0 >= zE && !(a.ones_col && n0 + BN > Nreal)) {  // never the tile of the ones column
+      if (a.zc_dim == 1 && z == 0)
         for (int e = tid; e < BM * BN; e += NT) {
           const int m = m0 + e / BN, n = n0 + e % BN;
-          if (m < M && n < N) a.C[(int64_t)m * a.ldc + n] = 0.f;
+          if (m < M && n < Nreal) a.C[(int64_t)m * a.ldc + n] = 0.f;
         }
       return;
+    } else {
+      nlim = min(nlim, zE);
     }
   }
+  const int kbeg = z * kchunk;
+  const int kfin = min(kend, kbeg + kchunk);
 
   // staging coordinates. k-contiguous operands: thread t loads float4 (t & 7) of rows t / 8 + RS i
-  // (8 lanes cover one row's 128 bytes of the slice).
+  // (8 lanes cover one row's 128 bytes of the slice). m- / n-contiguous operands: float4 q = tid +
+  // NT i is k row (q & 7) + 8 ((q >> 3) / NC), columns 4 ((q >> 3) % NC): a wave covers 8 k rows x 8
+  // float4 columns, 128 contiguous bytes per k row.
   const int a_c = tid & 7, a_r = tid >> 3;
   const float* __restrict__ Ap = a.A;
   const float* __restrict__ Bp = a.B;
-  const int64_t sam = a.sam, sbn = a.sbn, sbk = a.sbk;
+  const int64_t sam = a.sam, sak = a.sak, sbn = a.sbn, sbk = a.sbk;
+  constexpr int NCA = BM / 4, NC = BN / 4;
   int64_t a_row[NA];
+  int a_kr[NA], a_mc[NA];
 #pragma unroll
-  for (int i = 0; i < NA; ++i) a_row[i] = (int64_t)min(m0 + a_r + RS * i, M - 1) * sam;
-  // BKC: B rows are n (the pattern of A). !BKC: float4 q = tid + NT i is k row (q & 7) +
-  // 8 ((q >> 3) / NC), columns 4 ((q >> 3) % NC): a wave covers 8 k rows x 8 float4 columns, 128
-  // contiguous bytes per k row.
-  constexpr int NC = BN / 4;                      // float4 columns of a k row (!BKC)
+  for (int i = 0; i < NA; ++i) {
+    if constexpr (AK) {
+      a_row[i] = (int64_t)min(m0 + a_r + RS * i, M - 1) * sam;
+      a_kr[i] = a_mc[i] = 0;
+    } else {
+      const int qq = tid + NT * i;
+      a_kr[i] = (qq & 7) + 8 * (qq / (8 * NCA));
+      a_mc[i] = 4 * ((qq >> 3) % NCA);
+      a_row[i] = 0;
+    }
+  }
   int64_t b_row[NB];
   int b_kr[NB], b_nc[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     if constexpr (BKC) {
       b_row[i] = (int64_t)min(n0 + a_r + RS * i, N - 1) * sbn;
-      b_kr[i] = 0;
-      b_nc[i] = 0;
+      b_kr[i] = b_nc[i] = 0;
     } else {
       const int qq = tid + NT * i;
       b_kr[i] = (qq & 7) + 8 * (qq / (8 * NC));
@@ -767,16 +792,24 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int 
 
   floatx4 ra[NA], rb[NB];
   auto load_slice = [&](int k0) {
-    const int kk = min(k0 + 4 * a_c, kend - 4);  // a run that would cross kend starts 4 before it
+    const int kk = min(k0 + 4 * a_c, kfin - 4);  // a run that would cross kfin starts 4 before it
 #pragma unroll
-    for (int i = 0; i < NA; ++i) ra[i] = gb_load(Ap + a_row[i] + kk);
+    for (int i = 0; i < NA; ++i) {
+      if constexpr (AK) {
+        ra[i] = gb_load(Ap + a_row[i] + kk);
+      } else {
+        const int k = min(k0 + a_kr[i], kfin - 1);
+        const int m = min(m0 + a_mc[i], M - 4);     // a run past M starts 4 before it (M >= 4)
+        ra[i] = gb_load(Ap + (int64_t)k * sak + m);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (BKC) {
         rb[i] = gb_load(Bp + b_row[i] + kk);
       } else {
-        const int k = min(k0 + b_kr[i], kend - 1);
-        const int n = min(n0 + b_nc[i], N - 4);     // a run past N starts 4 before it (N >= 4)
+        const int k = min(k0 + b_kr[i], kfin - 1);
+        const int n = min(n0 + b_nc[i], Nreal - 4);  // a run past B's columns starts 4 before their end
         rb[i] = gb_load(Bp + (int64_t)k * sbk + n);
       }
     }
@@ -784,14 +817,25 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int 
   auto store_slice = [&](int k0, int stage) {
     float* As = smem + stage * (LA + LB);
     float* Bs = As + LA;
-    const bool ktail = k0 + BK > kend;  // block-uniform
+    const bool ktail = k0 + BK > kfin;  // block-uniform
     const int kk = k0 + 4 * a_c;
-    const int sh = kk - min(kk, kend - 4);  // 0, or how far the run was moved back (4+: all past kend)
+    const int sh = kk - min(kk, kfin - 4);  // 0, or how far the run was moved back (4+: all past kfin)
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      floatx4 v = ra[i];
-      if (ktail) v = floatx4{gb_pick(ra[i], sh), gb_pick(ra[i], sh + 1), gb_pick(ra[i], sh + 2), gb_pick(ra[i], sh + 3)};
-      *reinterpret_cast<floatx4*>(&As[(a_r + RS * i) * S + 4 * a_c]) = v;
+      if constexpr (AK) {
+        floatx4 v = ra[i];
+        if (ktail) v = floatx4{gb_pick(ra[i], sh), gb_pick(ra[i], sh + 1), gb_pick(ra[i], sh + 2), gb_pick(ra[i], sh + 3)};
+        *reinterpret_cast<floatx4*>(&As[(a_r + RS * i) * S + 4 * a_c]) = v;
+      } else {
+        const int mm = m0 + a_mc[i];
+        const int shm = mm - min(mm, M - 4);
+        const bool kin = k0 + a_kr[i] < kfin;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = shm ? gb_pick(ra[i], shm + e) : ra[i][e];
+          As[(a_mc[i] + e) * S + a_kr[i]] = kin ? x : 0.f;
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -801,11 +845,13 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int 
         *reinterpret_cast<floatx4*>(&Bs[(a_r + RS * i) * S + 4 * a_c]) = v;
       } else {
         const int nn = n0 + b_nc[i];
-        const int shn = nn - min(nn, N - 4);
-        const bool kin = k0 + b_kr[i] < kend;
+        const int shn = nn - min(nn, Nreal - 4);
+        const bool kin = k0 + b_kr[i] < kfin;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float x = shn ? gb_pick(rb[i], shn + e) : rb[i][e];
+          float x = shn ? gb_pick(rb[i], shn + e) : rb[i][e];
+          x = nn + e < nlim ? x : 0.f;
+          if (a.ones_col) x = nn + e == Nreal ? 1.f : x;
           Bs[(b_nc[i] + e) * S + b_kr[i]] = kin ? x : 0.f;
         }
       }
@@ -846,14 +892,14 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int 
   // one register stage, two LDS stages, one barrier per slice. The loads run unconditionally (a
   // slice past the end reloads valid addresses and is never stored) so the wait before each store
   // sees one pending set (see k_gemm).
-  const int nsl = (kend + BK - 1) / BK;
+  const int nsl = kfin > kbeg ? (kfin - kbeg + BK - 1) / BK : 0;
   if (nsl > 0) {
-    load_slice(0);
-    store_slice(0, 0);
+    load_slice(kbeg);
+    store_slice(kbeg, 0);
   }
   __syncthreads();
   for (int sl = 0; sl < nsl; ++sl) {
-    const int kn = min(sl + 1, nsl - 1) * BK;
+    const int kn = kbeg + min(sl + 1, nsl - 1) * BK;
     load_slice(kn);
     // the loads stay ahead of the MFMAs (hipcc would otherwise sink them to their use, after the
     // compute, and every slice would wait one full memory round trip)
@@ -862,6 +908,56 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int 
     __builtin_amdgcn_sched_barrier(0);
     if (sl + 1 < nsl) store_slice(kn, (sl + 1) & 1);
     __syncthreads();
+  }
+
+  if (splits > 1) {
+    // partial tile -> slab in accumulator order (thread tid's 16-float run r of tile (i, j) at
+    // (((i * FN + j) * 4 + r4) * NT + tid) * 4 floats); the last block of the tile to arrive sums
+    // the slabs in split order (sc1 hand-off, MI355X_MICROARCH.md "Valid forms" row 1)
+    constexpr int TILE = BM * BN;
+    const __amdgpu_buffer_rsrc_t rws = make_rsrc(a.workspace, (uint32_t)(4 * (int64_t)splits * ntiles * TILE));
+    const uint32_t slab0 = (uint32_t)(4 * ((int64_t)z * ntiles + tile) * TILE);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          store_sc1(rws, slab0 + 16u * (uint32_t)(((i * FN + j) * 4 + r4) * NT + tid),
+                    floatx4{acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]});
+    int* flag = reinterpret_cast<int*>(smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == splits - 1);
+      if (last) __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    const uint32_t zstride = (uint32_t)(4 * (int64_t)ntiles * TILE);
+    const uint32_t tile0 = (uint32_t)(4 * (int64_t)tile * TILE);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const uint32_t off = tile0 + 16u * (uint32_t)(((i * FN + j) * 4 + r4) * NT + tid);
+          floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
+          for (int z0 = 0; z0 < splits; z0 += 8) {
+            floatx4 t[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) t[w] = load_sc1(rws, (uint32_t)min(z0 + w, splits - 1) * zstride + off);
+#pragma unroll
+            for (int w = 0; w < 8; ++w)
+              if (z0 + w < splits) sum += t[w];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * r4 + e] = sum[e];
+        }
+    __syncthreads();  // the flag word's readers are done before the C tile overwrites it
   }
 
   // C/D of 32x32: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5); transposed through
@@ -1665,39 +1761,73 @@ bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
 }
 }  // namespace
 
-// k_gemm_big applies to the large fp32 products with a k-contiguous A (see the kernel): the tile
-// edge BN (128 or 64) minimises the busiest CU's work, ceil(tiles / CUs) x BN, ties to 128 (fewer
-// operand re-reads). Returns 0 when the product stays on k_gemm.
-int big_bn(const AimxGemmArgs& a) {
+// k_gemm_big applies to the large fp32 products (see the kernel): the projections and input
+// gradients (A k-contiguous, one block per tile) and the long-K weight gradients (A m-contiguous, B
+// n-contiguous, K = atoms: K split over blocks). The tile edge BN (128 or 64) minimises the busiest
+// CU's work, ceil(items / CUs) x BN, ties to 128 (fewer operand re-reads). bn = 0: the product stays
+// on k_gemm / k_wgrad_lds.
+struct BigPlan {
+  int bn = 0, nw = 8, splits = 1, kchunk = 0, tiles = 0;
+};
+
+BigPlan big_plan(const AimxGemmArgs& a) {
+  BigPlan p;
   const int64_t mode = opt_i64("AIMX_GEMM_BIG", 1);  // test hook / tuning build: 0 off, 64 / 128 forced
-  if (mode == 0) return 0;
-  if (a.precision != AIMX_PREC_FP32 || a.ones_col || a.splits > 1) return 0;
-  if (a.sak != 1 || !(a.sbk == 1 || a.sbn == 1)) return 0;
-  if (a.M < 256 || a.N < 64 || a.K < 64 || a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31))
-    return 0;
-  if (a.zc_rowptr && a.zc_width < kGbBK) return 0;
-  if (mode == 64 || mode == 128) return (int)mode;  // forced (tests, tuning build): any size
-  if (a.M < 4096 || a.N < 128 || a.K < 128 || (double)a.M * (double)a.N * (double)a.K < 1.5e9) return 0;
+  if (mode == 0 || a.precision != AIMX_PREC_FP32 || a.splits > 1) return p;
+  const bool ak = a.sak == 1, wgrad = a.sam == 1 && a.sbn == 1 && a.sak != 1;
+  if (!(ak && (a.sbk == 1 || a.sbn == 1)) && !wgrad) return p;
+  if (a.ones_col && !wgrad) return p;
+  if (a.M < 128 || a.N < 64 || a.K < 64 || a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31)) return p;
+  if (a.zc_rowptr && a.zc_width < kGbBK) return p;
+  const bool forced = mode == 64 || mode == 128;
+  if (!forced) {
+    if (ak && (a.M < 4096 || a.N < 128 || a.K < 128 || (double)a.M * (double)a.N * (double)a.K < 1.5e9)) return p;
+    if (wgrad && (a.M < 256 || a.N < 256 || a.K < 2048 || (double)a.M * (double)a.N * (double)a.K < 2e9)) return p;
+  }
   const int64_t tm = cdiv(a.M, kGbBM);
-  const int64_t w128 = cdiv(tm * cdiv(a.N, 128), 256) * 128, w64 = cdiv(tm * cdiv(a.N, 64), 256) * 64;
-  return w64 < w128 ? 64 : 128;
+  auto items = [&](int bn, int sp) { return tm * cdiv(a.N, bn) * sp; };
+  auto splits_for = [&](int bn) -> int {
+    if (!wgrad) return 1;  // rows alone fill the chip
+    // ~512 blocks (two per CU), each >= 512 atoms of K
+    return (int)std::max<int64_t>(1, std::min<int64_t>({cdiv(512, tm * cdiv(a.N, bn)), 64, a.K / 512}));
+  };
+  if (forced) {
+    p.bn = (int)mode;
+  } else {
+    const int s128 = splits_for(128), s64 = splits_for(64);
+    const int64_t w128 = cdiv(items(128, s128), 256) * 128 * cdiv(a.K, s128);
+    const int64_t w64 = cdiv(items(64, s64), 256) * 64 * cdiv(a.K, s64);
+    p.bn = w64 < w128 ? 64 : 128;
+  }
+  p.splits = splits_for(p.bn);
+  p.kchunk = (int)(cdiv(cdiv(a.K, p.splits), kGbBK) * kGbBK);
+  p.splits = (int)cdiv(a.K, p.kchunk);
+  p.tiles = (int)(tm * cdiv(a.N, p.bn));
+  p.nw = opt_i64("AIMX_GEMM_BIG_W", 8) == 4 ? 4 : 8;  // waves per workgroup (test hook / tuning build)
+  if (p.splits > 1 && (!a.counters || p.tiles > a.n_counters)) p.bn = 0;  // no counters: k_wgrad_lds
+  return p;
 }
 
-int launch_big(const AimxGemmArgs& a, int bn, hipStream_t s) {
-  const int tn = (int)cdiv(a.N, bn);
-  const int nt = (int)(cdiv(a.M, kGbBM) * tn);
-  const bool bkc = a.sbk == 1;
-  // waves per workgroup (test hook / tuning build AIMX_GEMM_BIG_W: 4 or 8)
-  const int nw = opt_i64("AIMX_GEMM_BIG_W", 8) == 4 ? 4 : 8;
-  using Fn = void (*)(const AimxGemmArgs, int, int);
-  Fn fn;
-  if (nw == 8)
-    fn = bn == 128 ? (bkc ? k_gemm_big<128, 8, true> : k_gemm_big<128, 8, false>)
-                   : (bkc ? k_gemm_big<64, 8, true> : k_gemm_big<64, 8, false>);
+size_t big_workspace_floats(const BigPlan& p) {
+  return p.bn && p.splits > 1 ? (size_t)p.splits * p.tiles * kGbBM * p.bn : 0;
+}
+
+template <int BN, int NW>
+void launch_big_t(const AimxGemmArgs& a, const BigPlan& p, hipStream_t s) {
+  using Fn = void (*)(const AimxGemmArgs, int, int, int, int);
+  const bool ak = a.sak == 1, bkc = a.sbk == 1;
+  const Fn fn = ak ? (bkc ? k_gemm_big<BN, NW, true, true> : k_gemm_big<BN, NW, true, false>)
+                   : k_gemm_big<BN, NW, false, false>;
+  const int tn = (int)cdiv(a.N, BN);
+  hipLaunchKernelGGL(fn, dim3((unsigned)(p.tiles * p.splits)), dim3(64 * NW), 0, s, a, tn, p.tiles, p.kchunk,
+                     p.splits);
+}
+
+int launch_big(const AimxGemmArgs& a, const BigPlan& p, hipStream_t s) {
+  if (p.nw == 8)
+    p.bn == 128 ? launch_big_t<128, 8>(a, p, s) : launch_big_t<64, 8>(a, p, s);
   else
-    fn = bn == 128 ? (bkc ? k_gemm_big<128, 4, true> : k_gemm_big<128, 4, false>)
-                   : (bkc ? k_gemm_big<64, 4, true> : k_gemm_big<64, 4, false>);
-  hipLaunchKernelGGL(fn, dim3((unsigned)nt), dim3(64 * nw), 0, s, a, tn, nt);
+    p.bn == 128 ? launch_big_t<128, 4>(a, p, s) : launch_big_t<64, 4>(a, p, s);
   AIMX_CHECK_LAUNCH();
   return AIMX_OK;
 }
@@ -1712,6 +1842,7 @@ size_t tiled_workspace_floats(const AimxGemmArgs& a) {
 // needs counters, so a caller without them falls back to the tiled plan)
 size_t gemm_workspace_floats(const AimxGemmArgs& a) {
   size_t f = tiled_workspace_floats(a);
+  f = std::max(f, big_workspace_floats(big_plan(a)));
   AimxWgradProblem pr;
   if (gemm_as_wgrad(a, pr)) {
     const WgPlan w = wg_plan(pr, kLoneWgs, wg_bb(&pr, 1));
@@ -1736,6 +1867,11 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
       return AIMX_EARG;
   }
   {
+    const BigPlan bp = big_plan(a);
+    if (bp.bn && (bp.splits == 1 || (a.workspace && a.workspace_bytes >= sizeof(float) * big_workspace_floats(bp))))
+      return launch_big(a, bp, s);
+  }
+  {
     AimxWgradProblem pr;
     if (gemm_as_wgrad(a, pr)) {
       const WgPlan w = wg_plan(pr, kLoneWgs, wg_bb(&pr, 1));
@@ -1745,7 +1881,6 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
         return wgrad_grouped_run(&pr, 1, a.workspace, a.workspace_bytes, a.counters, a.n_counters, s, kLoneWgs);
     }
   }
-  if (const int bn = big_bn(a)) return launch_big(a, bn, s);
   // operand layouts: each operand must be contiguous along k or along m/n; byte extents < 2 GiB
   if (!(a.sak == 1 || a.sam == 1) || !(a.sbk == 1 || a.sbn == 1)) return AIMX_EARG;
   const int64_t Nreal = a.ones_col ? a.N - 1 : a.N;

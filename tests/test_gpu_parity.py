@@ -408,6 +408,53 @@ def test_gemm_big_tiles(M, N, K, layout, off, pa, pb):
     assert torch.equal(C, C2)
 
 
+@pytest.mark.parametrize("M,N,K,ones,force", [(1024, 1024, 10240, True, 0), (512, 512, 20480, True, 0),
+                                              (307, 307, 4099, True, 64), (307, 307, 4099, True, 128),
+                                              (130, 70, 2049, False, 64), (256, 257, 9170, True, 128)])
+def test_gemm_big_weight_gradient(M, N, K, ones, force):
+    """k_gemm_big's weight-gradient layout (dW = dY^T X: A m-contiguous, B n-contiguous, K = atoms split
+    over blocks with an ordered slab reduction by the last block of each tile) with the implicit ones
+    column (the bias gradient): the c4 / c5 concat and embedding shapes by the rule, c5's 307-wide MLP
+    weights and small odd shapes forced onto 64- or 128-wide tiles (the AIMX_GEMM_BIG option);
+    within 2e-6 of fp64, bitwise deterministic, counters left at zero."""
+    from aimx import _lib
+    with _lib.options(**({"AIMX_GEMM_BIG": force} if force else {})):
+        C, col, _, ref, Am = _gemm(M, N, K, "TN", ones=ones)
+        C2, col2, _, _, _ = _gemm(M, N, K, "TN", ones=ones)
+    assert torch.isfinite(C).all()
+    assert (C.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    if ones:
+        rs = Am.double().sum(1)
+        assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
+    assert torch.equal(C, C2) and torch.equal(col, col2)
+    assert int(_lib.counters(DEV).abs().sum().item()) == 0
+
+
+def test_gemm_big_weight_gradient_trimming():
+    """The weight gradient over F with empty hop chunks (zc_dim 1) on k_gemm_big: blocks wholly past
+    E are written as zeros without loads, the block straddling E reads F's columns past E as 0 (they
+    hold NaN here: the stack's hop leaves them unwritten); equal to the untrimmed product bitwise."""
+    from aimx import _lib
+    n, d, h = 12000, 307, 6
+    K = d * (h + 1)
+    counts = torch.zeros(h * n, dtype=torch.int32)
+    counts[0:n:5] = 3
+    rowptr = torch.cat([torch.zeros(1, dtype=torch.int32), counts.cumsum(0).to(torch.int32)]).to(DEV)
+    E = 2 * d
+    g = torch.Generator().manual_seed(13)
+    F = torch.randn(n, K, generator=g)
+    F[:, E:] = 0
+    Fnan = F.clone()
+    Fnan[:, E:] = float("nan")
+    dY = torch.randn(n, 2 * d, generator=g)
+    with _lib.options(AIMX_GEMM_BIG=128):
+        full, fcol, _, ref, _ = _gemm(2 * d, K, n, "TN", A=dY, B=F, ones=True)
+        trim, tcol, _, _, _ = _gemm(2 * d, K, n, "TN", A=dY, B=Fnan, ones=True, zc=(rowptr, n, h, d, 1))
+    assert torch.equal(full, trim) and torch.equal(fcol, tcol)
+    assert not trim[:, E:].any()
+    assert (full.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+
+
 def test_gemm_big_tiles_epilogue_and_trimming():
     """k_gemm_big's fused epilogue (bias, residual, SiLU with the pre-activation store) and the
     empty-hop-chunk trimming at c5 size: forward k loop stopped at E (NaN past it is never read) equals
