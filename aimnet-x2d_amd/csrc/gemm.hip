@@ -1953,11 +1953,53 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
 
 
 namespace aimx {
+// A weight-gradient problem of a grouped call as a k_gemm_big launch of its own (the long-K
+// products big_plan takes: c5's [Wi; Wg] 614 x 615, K = atoms); bp.bn = 0 when it stays grouped.
+AimxGemmArgs wgrad_args(const AimxWgradProblem& pr) {
+  AimxGemmArgs a{};
+  a.M = pr.M;
+  a.N = pr.col_out ? pr.N + 1 : pr.N;
+  a.K = pr.K;
+  a.A = pr.dY;
+  a.sam = 1;
+  a.sak = pr.ld_dy;
+  a.B = pr.X;
+  a.sbk = pr.ld_x;
+  a.sbn = 1;
+  a.C = pr.dW;
+  a.ldc = pr.ld_dw;
+  a.act = -1;
+  a.dact_kind = -1;
+  a.ones_col = pr.col_out ? 1 : 0;
+  a.col_out = pr.col_out;
+  a.precision = AIMX_PREC_FP32;
+  if (pr.zc_rowptr) {
+    a.zc_rowptr = pr.zc_rowptr;
+    a.zc_rows = pr.zc_rows;
+    a.zc_chunks = pr.zc_chunks;
+    a.zc_width = pr.zc_width;
+    a.zc_dim = 1;
+  }
+  a.counters = reinterpret_cast<int32_t*>(1);  // placeholder: big_plan only checks for counters
+  a.n_counters = INT64_MAX;
+  return a;
+}
+
+BigPlan wgrad_big_plan(const AimxWgradProblem& pr) {
+  if (pr.K < 2048) return BigPlan{};
+  return big_plan(wgrad_args(pr));
+}
+
 size_t wgrad_ws_bytes(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
   if (!p || n < 0) return 0;
   size_t f = 0;
   const int bb = wg_bb(p, n);
   for (int32_t i = 0; i < n; ++i) {
+    const BigPlan bp = wgrad_big_plan(p[i]);
+    if (bp.bn) {
+      f += big_workspace_floats(bp);
+      continue;
+    }
     const WgPlan w = wg_plan(p[i], min_wgs, bb);
     if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab;
   }
@@ -1973,6 +2015,11 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   int64_t ctiles = 0;
   const int bb = wg_bb(p, n);
   for (int32_t i = 0; i < n; ++i) {
+    const BigPlan bp = wgrad_big_plan(p[i]);
+    if (bp.bn) {
+      ctiles += bp.tiles;
+      continue;
+    }
     const WgPlan w = wg_plan(p[i], min_wgs, bb);
     ctiles += (int64_t)w.tiles_x * w.tiles_y;
   }
@@ -2015,6 +2062,21 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
+    {  // the large long-K problems: k_gemm_big launches of their own (slabs / counters in problem order)
+      const BigPlan bp = wgrad_big_plan(pr);
+      if (bp.bn) {
+        AimxGemmArgs ga = wgrad_args(pr);
+        ga.workspace = (float*)workspace + ws_off;
+        ga.workspace_bytes = sizeof(float) * big_workspace_floats(bp);
+        ga.counters = counters + cnt_off;
+        ga.n_counters = bp.tiles;
+        const int rc = launch_big(ga, bp, (hipStream_t)stream);
+        if (rc != AIMX_OK) return rc;
+        ws_off += (int64_t)big_workspace_floats(bp);
+        cnt_off += bp.tiles;
+        continue;
+      }
+    }
     const WgPlan w = wg_plan(pr, min_wgs, bb);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {

@@ -266,8 +266,8 @@ def test_autograph_recaptures_after_storage_swap():
     o1.sum().backward()
     o2.sum().backward()
     for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
-        if p1.grad is not None:
-            assert _rel(p2.grad, p1.grad) < 1e-5, n
+        if p1.grad is not None:  # absolute floor: the pool's softmax-logit bias has an exactly-zero gradient
+            assert (p2.grad - p1.grad).norm().item() <= 1e-5 * max(p1.grad.norm().item(), 1e-9), n
 
 
 @pytest.mark.parametrize("slack", [1, 7, 8, 9, 300])

@@ -539,15 +539,18 @@ def test_gemm_weight_grad_forced_splits(splits):
     assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
 
 
-@pytest.mark.parametrize("bb", ["auto", "64", "80"])
+@pytest.mark.parametrize("bb", ["auto", "64", "80", "nobig"])
 def test_wgrad_grouped_matches_fp64(bb):
     """aimx_wgrad_grouped over the stack's shapes (76 x 76 / 152 x 304 / c5's 307 x 307 and
     614 x 614 with the bias column, long K: the LDS-block kernel with the block edge its rule picks,
     or 64- or 80-wide blocks forced by the AIMX_WGRAD_BB option), a short-K FFN shape, K = 1 and odd
-    widths (unaligned rows: the LDS kernel's dword loads): dW = dY^T X and db = sum_k dY against
-    fp64, deterministic, counters left at zero."""
+    widths (unaligned rows: the LDS kernel's dword loads); the c5 [Wi; Wg] product (614 x 615, K =
+    10240) and a 512 x 384 one go to k_gemm_big launches of their own inside the grouped call unless
+    the AIMX_GEMM_BIG option is 0 ("nobig"): dW = dY^T X and db = sum_k dY against fp64,
+    deterministic, counters left at zero."""
     from aimx import ops, _lib
-    with _lib.options(**({} if bb == "auto" else {"AIMX_WGRAD_BB": int(bb)})):
+    opts = {} if bb == "auto" else ({"AIMX_GEMM_BIG": 0} if bb == "nobig" else {"AIMX_WGRAD_BB": int(bb)})
+    with _lib.options(**opts):
         _wgrad_grouped_case()
 
 
@@ -557,7 +560,8 @@ def _wgrad_grouped_case():
     shapes = [(76, 76, 9170, True), (152, 304, 9170, True), (76, 76, 4099, False), (256, 256, 520, True),
               (36, 36, 1, True), (38, 38, 777, True), (8, 12, 64, False),
               (153, 153, 5000, True), (77, 45, 2500, False), (160, 81, 2048, True),  # LDS path: dword loads
-              (307, 307, 10240, True), (614, 614, 4096, True), (145, 301, 3001, False), (163, 150, 2048, True)]
+              (307, 307, 10240, True), (614, 614, 4096, True), (145, 301, 3001, False), (163, 150, 2048, True),
+              (614, 614, 10240, True), (512, 384, 12000, False)]
     probs, refs = [], []
     for M, N, K, bias in shapes:
         dy = torch.randn(K, M, generator=g)
