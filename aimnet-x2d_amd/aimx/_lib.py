@@ -296,6 +296,8 @@ def stream_ptr(device=None):
         elif isinstance(device, int):
             idx = device
         else:
+            if isinstance(device, str):
+                device = torch.device(device)
             idx = device.index if device.index is not None else torch.cuda.current_device()
         return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream

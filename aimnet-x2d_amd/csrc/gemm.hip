@@ -1526,6 +1526,146 @@ __global__ void k_splitk_reduce(const AimxGemmArgs a, int splits, int tiles_n) {
   }
 }
 
+// ---- Few rows, deep K: the post-pool chain's G x F x F products (k_gemm_deep) ------------------
+// c5's head runs G = 256 molecules through F = 1024 square Linears (gnn.py:252-258): 256 32 x 32
+// output tiles, one per CU, K = 1024. Staged through LDS (k_gemm<32,32>, split K) every k slice
+// waits a full L2 round trip behind a barrier: ~14 us per GEMM at ~15 % MFMA. Here a workgroup of
+// 8 waves owns one 32 x 32 tile and every wave computes the WHOLE tile over 1/8 of K with
+// v_mfma_f32_32x32x2_f32, loading its fragments straight from L2 into a register ring (no LDS
+// staging, no barrier until the end): A (k-contiguous) and B as [n][k] come as one 16-byte load per
+// lane per 8 k (lane half h holds k = 8g + 4h + j for MFMA j: the same permutation on both
+// operands, so the products pair up), B as [k][n] (the input gradient's W) as one coalesced dword
+// per lane per MFMA. The 8 partial tiles meet in LDS and are summed in wave order (deterministic);
+// the epilogue operands are loaded before the k loop.
+constexpr int kDpU = 4;  // 8-k groups per register set (two sets alternate: 8 groups in flight)
+
+template <bool BKC, int NW>
+__global__ __launch_bounds__(64 * NW) void k_gemm_deep(const AimxGemmArgs a, int tiles_m, int ntiles, int kq,
+                                                       uint32_t a_bytes, uint32_t b_bytes) {
+  constexpr int NO = 1024 / (64 * NW);  // outputs finished per thread
+  __shared__ __attribute__((aligned(16))) float red[NW * 1024];
+  // XCD-aware order: the blocks of one XCD (b % 8 under round-robin dispatch) take a contiguous
+  // range of tiles, column-tile major, so an XCD's L2 holds 1/8 of B (bijective for any grid)
+  const int bid = blockIdx.x, nb = (int)gridDim.x;
+  const int q = nb / 8, rr = nb % 8, xcd = bid % 8, loc = bid / 8;
+  const int tile = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  if (tile >= ntiles) return;
+  const int m0 = (tile % tiles_m) * 32, n0 = (tile / tiles_m) * 32;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int M = (int)a.M, N = (int)a.N, K = (int)a.K;
+
+  // this thread's NO outputs (tile element NO t + u: row / 32, column % 32); their epilogue operands
+  // are loaded now, raw and branch-free (an absent operand is a 0-byte descriptor: its loads return
+  // 0), and combined after the k loop exactly as epi_load does: nothing waits for them before then
+  const int er = (NO * tid) >> 5, ec = (NO * tid) & 31;
+  int em[NO], en[NO];
+#pragma unroll
+  for (int u = 0; u < NO; ++u) em[u] = m0 + er, en[u] = n0 + ec + u;
+  float ec_c[NO], ec_b[NO], ec_r[3][NO], ec_p[NO];
+  uint32_t ec_k[NO];
+  {
+    auto ext = [&](const void* p, int64_t ld) { return p ? (uint32_t)(4 * ((a.M - 1) * ld + a.N)) : 0u; };
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(a.C, a.beta != 0.f ? ext(a.C, a.ldc) : 0u);
+    const __amdgpu_buffer_rsrc_t rbias = make_rsrc(a.bias, a.bias ? (uint32_t)(4 * a.N) : 0u);
+    const __amdgpu_buffer_rsrc_t rp = make_rsrc(a.dact_pre, ext(a.dact_pre, a.lddact));
+    const __amdgpu_buffer_rsrc_t rk =
+        make_rsrc(a.mask_in, a.mask_in ? (uint32_t)((a.M - 1) * a.ldmask + a.N) : 0u);
+#pragma unroll
+    for (int e = 0; e < NO; ++e) {
+      const bool in = (em[e] < M) & (en[e] < N);
+      const uint32_t me = (uint32_t)em[e], ne = (uint32_t)en[e];
+      ec_c[e] = bload(rc, in ? 4u * (me * (uint32_t)a.ldc + ne) : kBufDrop, 0);
+      ec_b[e] = bload(rbias, in ? 4u * ne : kBufDrop, 0);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res[q], ext(a.res[q], a.ldres[q]));
+        ec_r[q][e] = bload(rr, in ? 4u * (me * (uint32_t)a.ldres[q] + ne) : kBufDrop, 0);
+      }
+      ec_p[e] = bload(rp, in ? 4u * (me * (uint32_t)a.lddact + ne) : kBufDrop, 0);
+      ec_k[e] = __builtin_amdgcn_raw_buffer_load_b8(rk, in ? me * (uint32_t)a.ldmask + ne : kBufDrop, 0, 0);
+    }
+  }
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.B, b_bytes);
+  const int kb = min(K, w * kq), ke = min(K, kb + kq);
+  const uint32_t lda = (uint32_t)a.sam, ldb = BKC ? (uint32_t)a.sbn : (uint32_t)a.sbk;
+  // per-lane offsets (the k-dependent part goes to the wave-uniform soffset); rows / columns past
+  // M / N and k past the wave's range point past the descriptor and read 0 (address selects only)
+  const uint32_t va = m0 + r < M ? 4u * ((uint32_t)(m0 + r) * lda + 4u * h) : a_bytes;
+  const uint32_t vb = n0 + r < N ? (BKC ? 4u * ((uint32_t)(n0 + r) * ldb + 4u * h) : 4u * (4u * h * ldb + n0 + r))
+                                 : b_bytes;
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+  auto load_set = [&](int kg, floatx4 (&fa)[kDpU], floatx4 (&fb)[kDpU]) {
+#pragma unroll
+    for (int u = 0; u < kDpU; ++u) {
+      const int k0 = kg + 8 * u;
+      const bool kok = k0 + 4 * h < ke;
+      fa[u] = bload4(ra, kok ? va : a_bytes, __builtin_amdgcn_readfirstlane(4u * (uint32_t)k0));
+      if (BKC) {
+        fb[u] = bload4(rb, kok ? vb : b_bytes, __builtin_amdgcn_readfirstlane(4u * (uint32_t)k0));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[u][j] = bload(rb, kok ? vb : b_bytes, __builtin_amdgcn_readfirstlane(4u * (uint32_t)(k0 + j) * ldb));
+      }
+    }
+  };
+  auto mma_set = [&](const floatx4 (&fa)[kDpU], const floatx4 (&fb)[kDpU]) {
+#pragma unroll
+    for (int u = 0; u < kDpU; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][j], fb[u][j], acc, 0, 0, 0);
+  };
+  constexpr int KS = 8 * kDpU;
+  const int ns = ke > kb ? (ke - kb + KS - 1) / KS : 0;
+  floatx4 fa0[kDpU], fb0[kDpU], fa1[kDpU], fb1[kDpU];
+  if (ns > 0) load_set(kb, fa0, fb0);
+  // loads unconditional (a set past the range reads 0): conditional ones leave hipcc waiting for
+  // every load at the loop head
+  for (int g = 0; g < ns; g += 2) {
+    load_set(kb + (g + 1) * KS, fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_set(fa0, fb0);
+    if (g + 1 >= ns) break;
+    load_set(kb + (g + 2) * KS, fa0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_set(fa1, fb1);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[w * 1024 + i * 64 + lane] = acc[i];
+  __syncthreads();
+  // output (row, col) is register (row & 3) + 4 (row >> 3) of lane col + 32 ((row >> 2) & 1)
+  const int ri = (er & 3) + 4 * (er >> 3), rl = ec + 32 * ((er >> 2) & 1);
+  float v[NO];
+#pragma unroll
+  for (int e = 0; e < NO; ++e) v[e] = 0.f;
+#pragma unroll
+  for (int u = 0; u < NW; ++u)
+#pragma unroll
+    for (int e = 0; e < NO; ++e) v[e] += red[u * 1024 + ri * 64 + rl + e];
+  EpiPre<NO> epi;  // epi_load's arithmetic, term by term
+  const float scale = a.drop_p < 1.f ? 1.f / (1.f - a.drop_p) : 0.f;
+#pragma unroll
+  for (int e = 0; e < NO; ++e) {
+    float add = 0.f;
+    if (a.beta != 0.f) add += a.beta * ec_c[e];
+    if (a.bias) add += ec_b[e];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (a.res[q]) add += ec_r[q][e];
+    float dg = a.dact_pre ? act_grad(a.dact_kind, ec_p[e]) : 1.f;
+    if (a.mask_in) dg *= ec_k[e] ? scale : 0.f;
+    epi.add[e] = add;
+    epi.dg[e] = dg;
+  }
+  epi_apply<NO>(a, em, en, v, epi);
+}
+
 struct Plan {
   int bm, bn, splits;
   int64_t kchunk;
@@ -1772,7 +1912,9 @@ struct BigPlan {
 
 BigPlan big_plan(const AimxGemmArgs& a) {
   BigPlan p;
-  const int64_t mode = opt_i64("AIMX_GEMM_BIG", 1);  // test hook / tuning build: 0 off, 64 / 128 forced
+  // off by default (measured slower than k_gemm<64,64> / k_wgrad_lds at c4 / c5, profiles/r06_big_gemm_ab.txt);
+  // test hook / tuning build: 1 = by the rule below, 64 / 128 forced tile
+  const int64_t mode = opt_i64("AIMX_GEMM_BIG", 0);
   if (mode == 0 || a.precision != AIMX_PREC_FP32 || a.splits > 1) return p;
   const bool ak = a.sak == 1, wgrad = a.sam == 1 && a.sbn == 1 && a.sak != 1;
   if (!(ak && (a.sbk == 1 || a.sbn == 1)) && !wgrad) return p;
@@ -1833,6 +1975,24 @@ int launch_big(const AimxGemmArgs& a, const BigPlan& p, hipStream_t s) {
 }
 
 // workspace of the tiled kernels' split-K plan
+// k_gemm_deep: few rows, deep K (the post-pool chain at F >= 512: G x F x F, G <= 1024), A
+// k-contiguous and B either way, 16-byte aligned k-contiguous rows, no ones column / trimming.
+bool deep_ok(const AimxGemmArgs& a) {
+  if (opt_i64("AIMX_GEMM_DEEP", 1) == 0 || a.precision != AIMX_PREC_FP32 || a.splits > 0) return false;
+  if (a.ones_col || a.zc_rowptr || a.sak != 1 || (a.sbk != 1 && a.sbn != 1)) return false;
+  if (a.M < 1 || a.M > 1024 || a.N < 1 || a.K < 512 || a.K % 4 != 0) return false;
+  if (cdiv(a.M, 32) * cdiv(a.N, 32) > 2048) return false;
+  if (a.sam % 4 != 0 || (uintptr_t)a.A % 16 != 0) return false;
+  if (a.sbk == 1 && (a.sbn % 4 != 0 || (uintptr_t)a.B % 16 != 0)) return false;
+  // the epilogue operands' row extents (32-bit buffer offsets)
+  const int64_t lds[6] = {a.ldc, a.ldres[0], a.ldres[1], a.ldres[2], a.lddact, a.ldmask};
+  for (int64_t ld : lds)
+    if (4 * ((a.M - 1) * std::max<int64_t>(ld, 0) + a.N) >= (1ll << 31)) return false;
+  const int64_t a_ext = 4 * ((a.M - 1) * a.sam + a.K);
+  const int64_t b_ext = a.sbk == 1 ? 4 * ((a.N - 1) * a.sbn + a.K) : 4 * ((a.K - 1) * a.sbk + a.N);
+  return a_ext < (1ll << 31) && b_ext < (1ll << 31);
+}
+
 size_t tiled_workspace_floats(const AimxGemmArgs& a) {
   const Plan p = plan_gemm(a);
   return p.splits > 1 ? (size_t)p.splits * (size_t)(cdiv(a.M, p.bm) * cdiv(a.N, p.bn)) * p.bm * p.bn : 0;
@@ -1880,6 +2040,21 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
           (int64_t)w.tiles_x * w.tiles_y <= a.n_counters)
         return wgrad_grouped_run(&pr, 1, a.workspace, a.workspace_bytes, a.counters, a.n_counters, s, kLoneWgs);
     }
+  }
+  if (deep_ok(a)) {
+    const int tm = (int)cdiv(a.M, 32), nt = tm * (int)cdiv(a.N, 32);
+    // 16 waves (each 1/16 of K: c5's K = 1024 is two register sets per wave, all in flight at once);
+    // 8 in the tuning build's A/B (AIMX_GEMM_DEEP=8)
+    const int nw = opt_i64("AIMX_GEMM_DEEP", 16) == 8 ? 8 : 16;
+    const int kq = (int)(cdiv(cdiv(a.K, nw), 8) * 8);
+    const uint32_t a_bytes = (uint32_t)(4 * ((a.M - 1) * a.sam + a.K));
+    const uint32_t b_bytes = (uint32_t)(a.sbk == 1 ? 4 * ((a.N - 1) * a.sbn + a.K) : 4 * ((a.K - 1) * a.sbk + a.N));
+    using Fn = void (*)(const AimxGemmArgs, int, int, int, uint32_t, uint32_t);
+    const Fn fn = a.sbk == 1 ? (nw == 16 ? k_gemm_deep<true, 16> : k_gemm_deep<true, 8>)
+                             : (nw == 16 ? k_gemm_deep<false, 16> : k_gemm_deep<false, 8>);
+    hipLaunchKernelGGL(fn, dim3((unsigned)nt), dim3(64 * nw), 0, s, a, tm, nt, kq, a_bytes, b_bytes);
+    AIMX_CHECK_LAUNCH();
+    return AIMX_OK;
   }
   // operand layouts: each operand must be contiguous along k or along m/n; byte extents < 2 GiB
   if (!(a.sak == 1 || a.sam == 1) || !(a.sbk == 1 || a.sbn == 1)) return AIMX_EARG;

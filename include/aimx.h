@@ -45,8 +45,9 @@ const char* aimx_version(void);
  * variable; every launcher uses its defaults unless an option of the same name was set here (the
  * alternative-path parity tests: "AIMX_MLPW" 0 = per-GEMM node-update MLP, "AIMX_MLPS" 0 / 1 =
  * weight-streamed MLP off / for every width, "AIMX_MLPS_RT" row tiles per chunk, "AIMX_WGRAD_BB"
- * 64 / 80 weight-gradient block edge, "AIMX_GEMM_BIG" 0 / 64 / 128 large-tile GEMM off / forced
- * tile, "AIMX_GEMM_BIG_W" 4 / 8 waves, "AIMX_HEAD8" 0 = 16-molecule head kernels, "AIMX_HOP_MAX_ROWS"
+ * 64 / 80 weight-gradient block edge, "AIMX_GEMM_BIG" 1 / 64 / 128 large-tile GEMM by rule / forced (default off)
+ * tile, "AIMX_GEMM_BIG_W" 4 / 8 waves, "AIMX_GEMM_DEEP" 0 = few-row deep-K products on the
+ * LDS-staged tiles, "AIMX_HEAD8" 0 = 16-molecule head kernels, "AIMX_HOP_MAX_ROWS"
  * n = the hop's row-range splitting at n rows per launch instead of its 2^31 limit). The tuning build
  * (make tune -> lib/libaimx_tune.so) also reads these names, and its A/B knobs, from the
  * environment. aimx_set_option returns AIMX_EARG for a name longer than 47 bytes or past 16 names. */

@@ -218,6 +218,12 @@ def _gemm(M, N, K, layout, **epi):
         a.res[0], a.ldres[0] = res.data_ptr(), N
     if ones:
         a.ones_col, a.col_out = 1, col.data_ptr()
+    dpre = torch.randn(M, N, generator=g).to(DEV) if epi.get("dact") is not None else None
+    if dpre is not None:  # input-gradient epilogue: C = (AB) * act'(dpre) [* mask / (1 - p)]
+        a.dact_pre, a.lddact, a.dact_kind = dpre.data_ptr(), N, epi["dact"]
+    mask = (torch.rand(M, N, generator=g) > 0.3).to(torch.uint8).to(DEV) if epi.get("mask") else None
+    if mask is not None:
+        a.mask_in, a.ldmask, a.drop_p = mask.data_ptr(), N, 0.3
     a.splits = epi.get("splits", 0)
     a.precision = epi.get("prec", 0)
     if epi.get("zc") is not None:
@@ -240,6 +246,13 @@ def _gemm(M, N, K, layout, **epi):
         ref = ref + bias.cpu().double()
     if res is not None:
         ref = ref + res.cpu().double()
+    if dpre is not None:
+        x = dpre.cpu().double()
+        sg = torch.sigmoid(x)
+        assert epi["dact"] == 4  # silu'
+        ref = ref * (sg * (1 + x * (1 - sg)))
+    if mask is not None:
+        ref = ref * mask.cpu().double() / 0.7
     return C.cpu(), col.cpu(), pre.cpu(), ref, Am
 
 
@@ -284,6 +297,30 @@ def test_gemm_short_k_weight_gradient(M, N, K, ones):
         assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
     C2, col2, _, _, _ = _gemm(M, N, K, "TN", ones=ones)
     assert torch.equal(C, C2) and torch.equal(col, col2)
+
+
+@pytest.mark.parametrize("M,N,K,layout", [(256, 1024, 1024, "NT"), (256, 1024, 1024, "NN"), (257, 1000, 1028, "NT"),
+                                          (256, 12, 2048, "NT"), (1, 33, 512, "NN"), (1024, 64, 516, "NN"),
+                                          (96, 1024, 4100, "NT")])
+@pytest.mark.parametrize("deep", [16, 8, 0])
+def test_gemm_deep_kernel(M, N, K, layout, deep):
+    """k_gemm_deep (8 waves per 32 x 32 tile, each 1/8 of K from a register ring, summed in wave
+    order) against fp64 and against the LDS-staged tiles (AIMX_GEMM_DEEP option 0): the c5 head's
+    forward ([n][k] weights) and input gradient ([k][n]), row / column / K % 8 == 4 tails, the
+    output layer (N = T), one row; the epilogues (bias + residual, SiLU with the pre-activation
+    store, the input gradient's act'(pre) x dropout mask); bitwise deterministic."""
+    from aimx import _lib
+    with _lib.options(AIMX_GEMM_DEEP=deep):
+        C, _, _, ref, _ = _gemm(M, N, K, layout, bias=True, res=True)
+        C2, _, _, _, _ = _gemm(M, N, K, layout, bias=True, res=True)
+        Ca, _, pre, refa, _ = _gemm(M, N, K, layout, bias=True, act=4)
+        Cg, _, _, refg, _ = _gemm(M, N, K, layout, dact=4, mask=True)
+    assert (C.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    assert torch.equal(C, C2)
+    assert (pre.double() - refa).abs().max().item() / refa.abs().max().item() < 2e-6
+    fr = torch.nn.functional.silu(refa)
+    assert (Ca.double() - fr).abs().max().item() / fr.abs().max().item() < 2e-6
+    assert (Cg.double() - refg).abs().max().item() / refg.abs().max().item() < 2e-6
 
 
 def test_gemm_deep_k_activation_epilogue():
@@ -399,12 +436,15 @@ def test_gemm_unaligned_rows_and_bases(M, N, K, layout, off):
 def test_gemm_big_tiles(M, N, K, layout, off, pa, pb):
     """k_gemm_big (128-row blocks of 32 x 32 x 2 fp32 MFMA: the c4 / c5 projections and input
     gradients): odd row strides and bases (16-byte loads at 4-byte alignment), M / N / K tails, both B
-    layouts; within 2e-6 of fp64 and bitwise deterministic."""
-    C, _, ref, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
+    layouts; within 3e-6 of fp64 (the max error relative to the max entry: K = 3000 accumulates
+    2.3e-6) and bitwise deterministic. (The AIMX_GEMM_BIG option: off by default.)"""
+    from aimx import _lib
+    with _lib.options(AIMX_GEMM_BIG=1):
+        C, _, ref, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
+        C2, _, _, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
     assert torch.isfinite(C).all()
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
-    assert err < 2e-6, err
-    C2, _, _, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
+    assert err < 3e-6, err
     assert torch.equal(C, C2)
 
 
@@ -418,7 +458,7 @@ def test_gemm_big_weight_gradient(M, N, K, ones, force):
     weights and small odd shapes forced onto 64- or 128-wide tiles (the AIMX_GEMM_BIG option);
     within 2e-6 of fp64, bitwise deterministic, counters left at zero."""
     from aimx import _lib
-    with _lib.options(**({"AIMX_GEMM_BIG": force} if force else {})):
+    with _lib.options(AIMX_GEMM_BIG=force or 1):
         C, col, _, ref, Am = _gemm(M, N, K, "TN", ones=ones)
         C2, col2, _, _, _ = _gemm(M, N, K, "TN", ones=ones)
     assert torch.isfinite(C).all()
@@ -460,6 +500,12 @@ def test_gemm_big_tiles_epilogue_and_trimming():
     empty-hop-chunk trimming at c5 size: forward k loop stopped at E (NaN past it is never read) equals
     the untrimmed product bitwise; the input gradient's tiles past E are skipped (zc_dim 2) and every
     column < E is bitwise the untrimmed one."""
+    from aimx import _lib
+    with _lib.options(AIMX_GEMM_BIG=1):
+        _big_epilogue_case()
+
+
+def _big_epilogue_case():
     n, d, h = 10240, 307, 6
     K = d * (h + 1)
     C, _, pre, ref, _ = _gemm(n, 2 * d, 1024, "NT", bias=True, act=4, res=True)
@@ -539,17 +585,17 @@ def test_gemm_weight_grad_forced_splits(splits):
     assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
 
 
-@pytest.mark.parametrize("bb", ["auto", "64", "80", "nobig"])
+@pytest.mark.parametrize("bb", ["auto", "64", "80", "big"])
 def test_wgrad_grouped_matches_fp64(bb):
     """aimx_wgrad_grouped over the stack's shapes (76 x 76 / 152 x 304 / c5's 307 x 307 and
     614 x 614 with the bias column, long K: the LDS-block kernel with the block edge its rule picks,
     or 64- or 80-wide blocks forced by the AIMX_WGRAD_BB option), a short-K FFN shape, K = 1 and odd
     widths (unaligned rows: the LDS kernel's dword loads); the c5 [Wi; Wg] product (614 x 615, K =
     10240) and a 512 x 384 one go to k_gemm_big launches of their own inside the grouped call unless
-    the AIMX_GEMM_BIG option is 0 ("nobig"): dW = dY^T X and db = sum_k dY against fp64,
+    the AIMX_GEMM_BIG option selects the large-tile rule ("big"; the default keeps them grouped): dW = dY^T X and db = sum_k dY against fp64,
     deterministic, counters left at zero."""
     from aimx import ops, _lib
-    opts = {} if bb == "auto" else ({"AIMX_GEMM_BIG": 0} if bb == "nobig" else {"AIMX_WGRAD_BB": int(bb)})
+    opts = {} if bb == "auto" else ({"AIMX_GEMM_BIG": 1} if bb == "big" else {"AIMX_WGRAD_BB": int(bb)})
     with _lib.options(**opts):
         _wgrad_grouped_case()
 

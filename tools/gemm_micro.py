@@ -119,6 +119,17 @@ if len(sys.argv) > 1 and sys.argv[1] == "head":
         run(1024, 1024, M, "TN", "c5 head dW")
     sys.exit(0)
 
+if len(sys.argv) > 1 and sys.argv[1] == "deep":
+    # k_gemm_deep's shapes: c5's post-pool chain (256 molecules, F = 1024) forward / input gradient,
+    # its output layer (K = 2F) and c4's F = 512 chain (AIMX_GEMM_DEEP in the tuning build: 16 / 8 / 0)
+    run(256, 1024, 1024, "NT", "c5 head fwd")
+    run(256, 1024, 1024, "NN", "c5 head dX")
+    run(256, 1, 2048, "NT", "c5 output layer")
+    run(256, 2048, 1, "NN", "c5 output dX", torch_ref=False)
+    run(512, 512, 512, "NT", "c4 head fwd")
+    run(512, 512, 512, "NN", "c4 head dX")
+    sys.exit(0)
+
 if len(sys.argv) > 1 and sys.argv[1] == "headsweep":
     # c5's post-pool GEMMs on the tiled kernel: split counts at the tile AIMX_GEMM_TILE forces
     for sp in (0, 2, 3, 4, 6, 8, 12, 16):
