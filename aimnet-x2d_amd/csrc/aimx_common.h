@@ -26,6 +26,14 @@ __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 
 // and only the tuning build (`make tune`: -DAIMX_TUNING -> lib/libaimx_tune.so, loaded by the tools'
 // A/B runs through AIMX_LIB_PATH) also reads the environment variable of the same name.
 int64_t opt_i64(const char* name, int64_t dflt);
+// A tuning knob (an A/B of a measured variant): read from the environment in the tuning build
+// (make tune, -DAIMX_TUNING); the product library always takes the default, so its only
+// switchable paths are the opt_i64 options include/aimx.h documents.
+#ifdef AIMX_TUNING
+inline int64_t tune_i64(const char* name, int64_t dflt) { return opt_i64(name, dflt); }
+#else
+inline int64_t tune_i64(const char*, int64_t dflt) { return dflt; }
+#endif
 
 // Activation kinds (reference: src/utils/activation.py:9-34).
 enum Act : int { ACT_NONE = -1, ACT_RELU = 0, ACT_LEAKYRELU = 1, ACT_ELU = 2, ACT_GELU = 3, ACT_SILU = 4 };

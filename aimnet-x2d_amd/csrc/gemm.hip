@@ -1689,7 +1689,7 @@ Plan plan_gemm(const AimxGemmArgs& a) {
     const int64_t t = cdiv(a.M, 32) * cdiv(a.N, 32);
     // ~1150 workgroups (round 5, c2's 256 x 257 x 9170 concat dW: 6 splits 32.7 us, 16 splits
     // 27.1 us; the 76 x 77 ones 17.8 -> 15.9 us; profiles/r05_lone_wgrad_splits.txt)
-    static const int64_t target = std::max<int64_t>(64, opt_i64("AIMX_WGRAD_WGS", 1152));
+    static const int64_t target = std::max<int64_t>(64, tune_i64("AIMX_WGRAD_WGS", 1152));
     int64_t splits = a.splits > 0 ? a.splits : cdiv(target, t);
     splits = std::max<int64_t>(1, std::min<int64_t>({splits, 64, a.K / 256}));
     p.kchunk = cdiv(cdiv(a.K, splits), 16) * 16;
@@ -1945,7 +1945,7 @@ BigPlan big_plan(const AimxGemmArgs& a) {
   p.kchunk = (int)(cdiv(cdiv(a.K, p.splits), kGbBK) * kGbBK);
   p.splits = (int)cdiv(a.K, p.kchunk);
   p.tiles = (int)(tm * cdiv(a.N, p.bn));
-  p.nw = opt_i64("AIMX_GEMM_BIG_W", 8) == 4 ? 4 : 8;  // waves per workgroup (test hook / tuning build)
+  p.nw = tune_i64("AIMX_GEMM_BIG_W", 8) == 4 ? 4 : 8;  // waves per workgroup (test hook / tuning build)
   if (p.splits > 1 && (!a.counters || p.tiles > a.n_counters)) p.bn = 0;  // no counters: k_wgrad_lds
   return p;
 }

@@ -594,7 +594,7 @@ HeadLaunch head_launch(const AimxHead* h) {
   // 4w4 218 us forward+backward; 16 waves need more than the 128 VGPRs a 1024-thread workgroup
   // allows and spill)
   int waves = S <= 2 ? 8 : 4;
-  if (const int64_t f = opt_i64("AIMX_HEAD_WAVES", 0)) waves = f == 16 ? 16 : f == 4 ? 4 : 8;  // tuning build
+  if (const int64_t f = tune_i64("AIMX_HEAD_WAVES", 0)) waves = f == 16 ? 16 : f == 4 ? 4 : 8;  // tuning build
   if (S == 1) return HeadLaunch{(unsigned)ntiles, waves};
   static int cus[64] = {0};
   int dev = 0;

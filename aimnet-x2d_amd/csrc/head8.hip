@@ -386,7 +386,7 @@ __global__ __launch_bounds__(kNT) void k_head8_bwd(const AimxHead h, const AimxH
 // The 8-row kernels apply when every chain GEMM is F x F with F % 64 == 0 and 128 <= F <= kMaxF8
 // (H_in == F: the reference's defaults, ffn_hidden_dim = hidden_dim) and the LDS holds the tiles.
 bool head8_ok(const AimxHead* h) {
-  if (opt_i64("AIMX_HEAD8", 1) == 0) return false;  // test hook: the 16-molecule kernels
+  if (tune_i64("AIMX_HEAD8", 1) == 0) return false;  // test hook: the 16-molecule kernels
   const int64_t F = h->F;
   // the 16 waves split into F / 64 column groups x 16 / (F / 64) k ranges exactly (F = 128, 256,
   // 512). Every workgroup streams all 2 + 2 nb F x F weights through its CU (9.4 MiB at F = 512);
@@ -405,7 +405,7 @@ namespace {
 // AIMX_HEAD8_ROWS=4|8 forces one (c2, G = 520: 0.7275 ms with 4 vs 0.7678 ms with 8, r4e)
 int head8_rows(int64_t G) {
   static const int r = [] {
-    return (int)opt_i64("AIMX_HEAD8_ROWS", 0);  // tuning build
+    return (int)tune_i64("AIMX_HEAD8_ROWS", 0);  // tuning build
   }();
   if (r == 4 || r == 8) return r;
   return G >= 8 * 256 ? 8 : 4;

@@ -290,7 +290,6 @@ template <int VEC, bool SRC_CHUNKED>
 // and its reads become flat loads through the vector-memory pipe instead of ds_reads.
 __device__ __forceinline__ void process_tile(const HopArgs& a, HopLds& L, int32_t* s_col, float* s_x, uint32_t r0,
                                              uint32_t nr) {
-  using T = typename VecT<VEC>::T;
   if (threadIdx.x <= nr) L.ptr[threadIdx.x] = a.rowptr[r0 + threadIdx.x];
   if (threadIdx.x == 0) {
     L.lohi[0] = INT32_MAX;
@@ -359,7 +358,6 @@ __device__ __forceinline__ void process_tile(const HopArgs& a, HopLds& L, int32_
 template <int VEC, bool SRC_CHUNKED>
 __device__ __forceinline__ void process_tile_seg(const HopArgs& a, HopLds& L, int32_t* s_col, float* s_x,
                                                  uint32_t c0, uint32_t c1) {
-  using T = typename VecT<VEC>::T;
   int32_t* spec = L.lohi + 2;  // [lo, hi] of the col slice (LDS head padding, see kLdsHead)
   {
     const uint32_t pend = min(c1 + (uint32_t)kAlignWin, a.split_rows);  // last possible cut
@@ -587,15 +585,15 @@ struct HopEnv {
 const HopEnv& hop_env() {
   static const HopEnv e = [] {
     HopEnv v;
-    v.tile_units = opt_i64("AIMX_HOP_TILE_UNITS", -1);
-    v.big_mul = opt_i64("AIMX_HOP_BIG_MUL", -1);
-    v.col_cap = opt_i64("AIMX_HOP_COL_CAP", -1);
-    v.stage_bytes = opt_i64("AIMX_HOP_STAGE_BYTES", -1);
-    v.flat = opt_i64("AIMX_HOP_FLAT", 1);
-    v.nt = opt_i64("AIMX_HOP_NT", 0);
-    v.interleave = opt_i64("AIMX_HOP_INTERLEAVE", 1);
-    v.spec = opt_i64("AIMX_HOP_SPEC", 1);
-    v.no_seg = opt_i64("AIMX_HOP_NO_SEG", 0) != 0;
+    v.tile_units = tune_i64("AIMX_HOP_TILE_UNITS", -1);
+    v.big_mul = tune_i64("AIMX_HOP_BIG_MUL", -1);
+    v.col_cap = tune_i64("AIMX_HOP_COL_CAP", -1);
+    v.stage_bytes = tune_i64("AIMX_HOP_STAGE_BYTES", -1);
+    v.flat = tune_i64("AIMX_HOP_FLAT", 1);
+    v.nt = tune_i64("AIMX_HOP_NT", 0);
+    v.interleave = tune_i64("AIMX_HOP_INTERLEAVE", 1);
+    v.spec = tune_i64("AIMX_HOP_SPEC", 1);
+    v.no_seg = tune_i64("AIMX_HOP_NO_SEG", 0) != 0;
     return v;
   }();
   return e;
@@ -632,8 +630,12 @@ int segment_gather_sum(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   // inference batch) runs as consecutive row ranges, each inside one output chunk: a range's row
   // pointers, output rows, residual rows and molecule ids are offsets of the caller's (rows are
   // independent sums, so the result is the one-launch result, bit for bit).
+  // (the odd-width kernel indexes threads within a tile and rows in 32 bits: only rows < 2^31 bound
+  // it; the aligned kernel's flat thread index also spans rows x D / vec. A split call loses the
+  // chunked fast paths — zero-fill tiles, skip_tail — so the cap must not bite at configured sizes:
+  // c5's 6-hop forward at roofline size is 6.6 M rows of 307.)
   {
-    const int64_t upr_v = cdiv(D, vec);
+    const int64_t upr_v = vec < 4 ? 1 : cdiv(D, vec);
     int64_t cap = std::max<int64_t>(1, ((int64_t)INT32_MAX - 1) / std::max<int64_t>(upr_v, 1) / 2);
     if (const int64_t f = opt_i64("AIMX_HOP_MAX_ROWS", 0)) cap = std::min(cap, f);  // test hook
     const int64_t rpc = (out_rpc > 0 && out_rpc < rows) ? out_rpc : rows;

@@ -584,20 +584,20 @@ int launch_gather_unal(const float* src, int64_t src_ld, int64_t src_rpc, int64_
   if (rows >= (int64_t)INT32_MAX || src_rpc >= INT32_MAX || out_rpc >= INT32_MAX) return AIMX_EARG;
   // knobs, read once per process
   // slice width (floats): 64 = one 16-unit pitch per staged row (conflict-free ds_read_b128, sum_rows)
-  static const int64_t w_max = std::max<int64_t>(4, opt_i64("AIMX_HOPU_W", 80) / 4 * 4);
+  static const int64_t w_max = std::max<int64_t>(4, tune_i64("AIMX_HOPU_W", 80) / 4 * 4);
   static const int64_t pitch_env = [] {  // staged row pitch in units: 0 compact, else a power of two >= 16
-    const int64_t e = opt_i64("AIMX_HOPU_PITCH", 0);
+    const int64_t e = tune_i64("AIMX_HOPU_PITCH", 0);
     if (!e) return (int64_t)0;
     int64_t p = 16;
     while (p < e) p *= 2;
     return p;
   }();
-  static const int64_t tr_env = std::max<int64_t>(1, std::min<int64_t>(kUMaxTile, opt_i64("AIMX_HOPU_TILE", 32)));
-  static const int64_t col_cap_env = (std::max<int64_t>(64, opt_i64("AIMX_HOPU_COL_CAP", 1024)) + 3) / 4 * 4;
-  static const int64_t stage_env = std::max<int64_t>(1024, opt_i64("AIMX_HOPU_STAGE", 20 * 1024));
-  static const int64_t big_env = opt_i64("AIMX_HOPU_BIG", 256);
-  static const int32_t interleave = opt_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
-  static const bool no_seg = opt_i64("AIMX_HOP_NO_SEG", 0) != 0;
+  static const int64_t tr_env = std::max<int64_t>(1, std::min<int64_t>(kUMaxTile, tune_i64("AIMX_HOPU_TILE", 32)));
+  static const int64_t col_cap_env = (std::max<int64_t>(64, tune_i64("AIMX_HOPU_COL_CAP", 1024)) + 3) / 4 * 4;
+  static const int64_t stage_env = std::max<int64_t>(1024, tune_i64("AIMX_HOPU_STAGE", 20 * 1024));
+  static const int64_t big_env = tune_i64("AIMX_HOPU_BIG", 256);
+  static const int32_t interleave = tune_i64("AIMX_HOP_INTERLEAVE", 1) != 0 ? 1 : 0;
+  static const bool no_seg = tune_i64("AIMX_HOP_NO_SEG", 0) != 0;
   const int64_t upr = cdiv(D, 4);
   // slices of cu units; the last slice must hold more than a partial last unit (put_raw writes that
   // unit shifted down over the unit before it, which must be in the same slice)

@@ -998,7 +998,6 @@ __global__ __launch_bounds__(kSMaxThreads) void k_mlps_bwd(const MlpBwd p, const
       int lo = lane;  // opaque copies: see k_mlps_fwd
       asm volatile("" : "+s"(r0), "+v"(lo));
       const int lr = lo & 15, lq = 4 * (lo >> 4);
-      const uint32_t nd = (uint32_t)(N * D);
       // per fragment: the epilogue's operands (dV: v and the dropout mask; dA of block 0: u), every
       // load issued before the first use (one round trip per fragment, see k_mlps_fwd), then its
       // outputs
@@ -1073,7 +1072,7 @@ int mlpw_rt(int64_t N, int64_t D, int64_t nm) {
   const int CF = pad16((int)D) / 16;
   const int64_t tiles = (N + 15) / 16;
   int rt = (int)std::min<int64_t>(4, std::max<int64_t>(1, (tiles + g_num_cus() - 1) / g_num_cus()));
-  if (const int64_t f = opt_i64("AIMX_MLPW_RT", 0)) rt = (int)std::max<int64_t>(1, std::min<int64_t>(4, f));  // tuning build only
+  if (const int64_t f = tune_i64("AIMX_MLPW_RT", 0)) rt = (int)std::max<int64_t>(1, std::min<int64_t>(4, f));  // tuning build only
   while (rt > 1 && (rt * CF > 2 * kWMaxWaves || mlpw_lds_bytes(D, nm, rt) > (size_t)kMlpwDynLds)) --rt;
   return rt;
 }

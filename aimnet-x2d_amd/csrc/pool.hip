@@ -1016,7 +1016,7 @@ extern "C" int aimx_attn_pool_backward(const float* x, int64_t ldx, int64_t N, i
     }
     AIMX_CHECK_LAUNCH();
   }
-  static const bool two_launch = opt_i64("AIMX_ATTN_RED2", 0) != 0;  // tuning build: the two-launch reduction
+  static const bool two_launch = tune_i64("AIMX_ATTN_RED2", 0) != 0;  // tuning build: the two-launch reduction
   if (G > 0 && !two_launch) {
     hipLaunchKernelGGL(k_attn_reduce, dim3((unsigned)n_red_cnt, (unsigned)n_slices), dim3(256), 0, s, G, (int)H, C,
                        dW_part, db_part, dtau_part, slab, red_cnt, dW, db, dtau);

@@ -163,7 +163,7 @@ int gather(const AimxShellStack* st, const float* src, int64_t src_ld, int64_t s
 
 // Empty hop chunks (AimxGemmArgs.zc_*): every GEMM over F's columns trims the all-zero chunks the
 // reference's hop leaves (layers.py:154), detected on the device from the forward CSR row pointers.
-bool zc_on() { return opt_i64("AIMX_NO_ZC", 0) == 0; }  // tuning build: AIMX_NO_ZC=1 disables it
+bool zc_on() { return tune_i64("AIMX_NO_ZC", 0) == 0; }  // tuning build: AIMX_NO_ZC=1 disables it
 
 void set_zc(AimxGemmArgs& a, const AimxShellStack* s, int dim) {
   if (!zc_on() || !s->fwd_rowptr) return;
@@ -402,8 +402,7 @@ int stack_wgrad_problems(const AimxShellStack* s, const AimxShellStackGrad* g, c
 }
 
 BwdLayout bwd_layout(const AimxShellStack* s) {
-  const int64_t N = s->N, D = s->D, h = s->num_hops, L = s->num_layers, nm = s->num_mlp;
-  const int64_t K = D * (h + 1);
+  const int64_t N = s->N, D = s->D, L = s->num_layers, nm = s->num_mlp;
   BwdLayout b;
   b.nA = L * (nm - 1);
   b.nY = L;  // layers 0..L-2: the hop backward's output; L-1: top_dy's aligned copy

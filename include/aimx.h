@@ -43,14 +43,18 @@ const char* aimx_version(void);
 
 /* Path options: test hooks, not a tuning surface. The product library reads no environment
  * variable; every launcher uses its defaults unless an option of the same name was set here (the
- * alternative-path parity tests: "AIMX_MLPW" 0 = per-GEMM node-update MLP, "AIMX_MLPS" 0 / 1 =
- * weight-streamed MLP off / for every width, "AIMX_MLPS_RT" row tiles per chunk, "AIMX_WGRAD_BB"
- * 64 / 80 weight-gradient block edge, "AIMX_GEMM_BIG" 1 / 64 / 128 large-tile GEMM by rule / forced (default off)
- * tile, "AIMX_GEMM_BIG_W" 4 / 8 waves, "AIMX_GEMM_DEEP" 0 = few-row deep-K products on the
- * LDS-staged tiles, "AIMX_HEAD8" 0 = 16-molecule head kernels, "AIMX_HOP_MAX_ROWS"
- * n = the hop's row-range splitting at n rows per launch instead of its 2^31 limit). The tuning build
- * (make tune -> lib/libaimx_tune.so) also reads these names, and its A/B knobs, from the
- * environment. aimx_set_option returns AIMX_EARG for a name longer than 47 bytes or past 16 names. */
+ * alternative-path parity tests):
+ *   "AIMX_MLPW"         0 = per-GEMM node-update MLP instead of the weight-resident kernels
+ *   "AIMX_MLPS"         0 / 1 = weight-streamed MLP off / for every width
+ *   "AIMX_MLPS_RT"      row tiles per chunk of the weight-streamed MLP
+ *   "AIMX_WGRAD_BB"     64 / 80 = weight-gradient block edge
+ *   "AIMX_GEMM_BIG"     1 / 64 / 128 = large-tile GEMM by its rule / forced tile (default off)
+ *   "AIMX_GEMM_DEEP"    0 = few-row deep-K products on the LDS-staged tiles; 8 = 8 waves
+ *   "AIMX_HOP_MAX_ROWS" n = the hop's row-range splitting at n rows per launch (not 2^31)
+ * The tuning build (make tune -> lib/libaimx_tune.so) also reads these names, and its A/B knobs
+ * (tune_i64 in csrc: variants measured slower, kept for re-measurement), from the environment; the
+ * product library compiles those knobs to their defaults. aimx_set_option returns AIMX_EARG for a
+ * name longer than 47 bytes or past 16 names. */
 int aimx_set_option(const char* name, int64_t value);
 int aimx_clear_options(void);
 

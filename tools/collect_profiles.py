@@ -39,7 +39,7 @@ for name in ("bench_plain.log", "roof.log"):
 print(json.dumps(json.load(open(os.path.join(dst, "hop_traffic.json"))), indent=1))
 
 # extra configs (c3/c4/c5 bench lines), the c4 step breakdown and its MFMA utilisation
-for cfgname in ("c3", "c4", "c5", "c2_amp", "c4_amp", "c5_amp"):
+for cfgname in ("c3", "c4", "c5", "c2_amp", "c4_amp", "c5_amp", "c5_stream"):
     p = os.path.join(src, f"bench_{cfgname}.log")
     if os.path.exists(p):
         lines = [ln for ln in open(p) if ln.startswith("{")]
@@ -76,3 +76,16 @@ if os.path.exists(p):
     tail = [ln for ln in open(p) if "passed" in ln or "failed" in ln or ln.startswith("FAILED")]
     with open(os.path.join(dst, f"{tag}_gpu_tests.txt"), "w") as f:
         f.write("".join(tail[-20:]))
+
+# the hop roofline's forward / backward launches separated (same kernel instance at c2), and the
+# c5 stream feed's own rate
+for name in ("roof_split_c2.json", "roof_split_c5.json"):
+    p = os.path.join(src, name)
+    if os.path.exists(p):
+        shutil.copy(p, os.path.join(dst, f"{tag}_{name}"))
+p = os.path.join(src, "feed_rate_c5.log")
+if os.path.exists(p):
+    lines = [ln for ln in open(p) if ln.startswith("{")]
+    if lines:
+        with open(os.path.join(dst, f"{tag}_feed_rate_c5.json"), "w") as f:
+            f.write(lines[-1])

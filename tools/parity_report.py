@@ -105,11 +105,18 @@ def main():
             "max_vs_fp64": max(r["vs_fp64"] for r in rows.values()),
             "relaxed": sorted(k for k, r in rows.items() if r["relaxed"]),
             "all_pass": all(r["pass"] for r in rows.values()),
+            # the literal contract: the fraction of tensors within 1e-5 of fp64, and how close the
+            # rest come to the bound they are judged by (error / the reference's own fp32 floor)
+            "frac_within_1e-5": sum(r["vs_fp64"] <= 1e-5 for r in rows.values()) / max(len(rows), 1),
+            "max_err_over_floor": max((r["vs_fp64"] / r["ref_floor"] for r in rows.values()
+                                       if r["ref_floor"]), default=None),
+            "max_err_over_tol": max(r["vs_fp64"] / r["tol"] for r in rows.values()),
             "per_tensor": rows,
         }
         c = report["cases"][name]
-        print(f"{name:12s} tensors {c['tensors']:3d}  max vs ref32 {c['max_vs_ref32']:.2e}  max vs fp64 "
-              f"{c['max_vs_fp64']:.2e}  relaxed {c['relaxed']}  pass {c['all_pass']}", flush=True)
+        print(f"{name:12s} tensors {c['tensors']:3d}  max vs fp64 {c['max_vs_fp64']:.2e}  within 1e-5 "
+              f"{c['frac_within_1e-5']:.2f}  max err/tol {c['max_err_over_tol']:.2f}  relaxed {c['relaxed']}  "
+              f"pass {c['all_pass']}", flush=True)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(report, f, indent=1, sort_keys=True)

@@ -4,6 +4,8 @@
 #      PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic, the default bench line;
 #   b: the parity tests again, c3/c4/c5 bench lines, step traces of c4/c5, c4's MFMA-busy PMC pass;
 #   b2: AMP bench lines (c2/c4/c5), MFMA-busy PMC passes on c2 and c5 (whole-step MFMA against peak);
+#   s: the c5 1M-molecule 6-hop HDF5 stream line and the feed's own rate at the per-rank thread
+#      count of an 8-rank node (16: the box's CPU share per GPU);
 #   c: the per-tensor parity report, the DDP lines (world-size-1 RCCL with the DDP-wrapped autograph
 #      leg; two gloo ranks sharing the GPU), the k_mlps phase stamps, smoke and the whole -m gpu suite.
 # Outputs under gpurun_out/round/; tools/collect_profiles.py copies the summaries into profiles/.
@@ -15,13 +17,16 @@ A=(
   "300 round/parity.log python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hop_rows.py -q -x --timeout 200 --timeout-method thread"
   "900 round/bench.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/bench -- python3 bench.py --no-cpu-baseline"
   "600 round/roof.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/roof -- python3 bench.py --roofline-only"
+  "60 round/roof_split.log python3 tools/roof_split.py $R/roof $R/roof.log $R/roof_split_c2.json"
+  "600 round/roof_c5.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/roof_c5 -- python3 bench.py --config c5 --roofline-only"
+  "60 round/roof_split_c5.log python3 tools/roof_split.py $R/roof_c5 $R/roof_c5.log $R/roof_split_c5.json"
   "600 round/pmc_fetch.log rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/pmc_fetch -- python3 bench.py --roofline-only"
   "600 round/pmc_write.log rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/pmc_write -- python3 bench.py --roofline-only"
   "900 round/bench_plain.log python3 bench.py"
 )
 B=(
   "400 round/parity_b.log python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hop_rows.py -q -x --timeout 200 --timeout-method thread"
-  "300 round/bench_c3.log python3 bench.py --config c3 --no-cpu-baseline --no-roofline --no-eager"
+  "300 round/bench_c3.log python3 bench.py --config c3 --no-eager"
   "300 round/bench_c4.log python3 bench.py --config c4 --no-cpu-baseline"
   "300 round/bench_c5.log python3 bench.py --config c5 --no-cpu-baseline"
   "600 round/c4_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/c4_trace -- python3 bench.py --config c4 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
@@ -35,6 +40,10 @@ B2=(
   "300 round/bench_c5_amp.log python3 bench.py --config c5 --amp --no-cpu-baseline --no-roofline"
   "600 round/c2_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c2_mfma -- python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
   "600 round/c5_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/c5_mfma -- python3 bench.py --config c5 --no-cpu-baseline --no-roofline --no-eager --steps 10 --warmup 3"
+)
+S=(
+  "900 round/bench_c5_stream.log python3 bench.py --config c5 --feed stream --stream-mols 1000000 --steps 400 --warmup 20 --no-cpu-baseline --no-roofline --no-eager"
+  "600 round/feed_rate_c5.log python3 tools/feed_rate.py --config c5 --feed stream --stream-mols 1000000 --batches 400 --threads 16"
 )
 C=(
   "600 round/c2_trace.log rocprofv3 --kernel-trace --stats --output-format csv -d $R/c2_trace -- python3 bench.py --no-cpu-baseline --no-roofline --no-eager --steps 20 --warmup 5"
@@ -52,5 +61,6 @@ case "$1" in
   b) tools/gpu_steps.sh "${B[@]}" ;;
   b2) tools/gpu_steps.sh "${B2[@]}" ;;
   c) tools/gpu_steps.sh "${C[@]}" ;;
+  s) tools/gpu_steps.sh "${S[@]}" ;;
   *) echo "usage: $0 a|b|c" >&2; exit 2 ;;
 esac
