@@ -300,14 +300,14 @@ def test_gemm_short_k_weight_gradient(M, N, K, ones):
 
 
 @pytest.mark.parametrize("M,N,K,layout", [(256, 1024, 1024, "NT"), (256, 1024, 1024, "NN"), (257, 1000, 1028, "NT"),
-                                          (256, 12, 2048, "NT"), (1, 33, 512, "NN"), (1024, 64, 516, "NN"),
+                                          (256, 12, 2048, "NT"), (1, 4100, 512, "NN"), (1024, 64, 516, "NN"),
                                           (96, 1024, 4100, "NT")])
 @pytest.mark.parametrize("deep", [16, 8, 0])
 def test_gemm_deep_kernel(M, N, K, layout, deep):
     """k_gemm_deep (8 waves per 32 x 32 tile, each 1/8 of K from a register ring, summed in wave
     order) against fp64 and against the LDS-staged tiles (AIMX_GEMM_DEEP option 0): the c5 head's
     forward ([n][k] weights) and input gradient ([k][n]), row / column / K % 8 == 4 tails, the
-    output layer (N = T), one row; the epilogues (bias + residual, SiLU with the pre-activation
+    output layer (N = T: the tiles' rule, too few tiles for the deep kernel), one row; the epilogues (bias + residual, SiLU with the pre-activation
     store, the input gradient's act'(pre) x dropout mask); bitwise deterministic."""
     from aimx import _lib
     with _lib.options(AIMX_GEMM_DEEP=deep):
