@@ -130,6 +130,17 @@ if len(sys.argv) > 1 and sys.argv[1] == "deep":
     run(512, 512, 512, "NN", "c4 head dX")
     sys.exit(0)
 
+if len(sys.argv) > 1 and sys.argv[1] == "ugpad":
+    # c4 / c5 [Wi; Wg] products with the weight rows at their reference stride D(h+1) (odd: dword
+    # staging) against a stride rounded to 4 floats (16-byte staging)
+    for M, D, h in ((20480, 153, 3), (10240, 307, 6)):
+        K_ig = D * (h + 1)
+        ldf = (K_ig + 3) // 4 * 4
+        for ldb in (K_ig, ldf):
+            run(M, 2 * D, 2 * D, "NT", f"D{D} [u|g] fwd ldb={ldb}", lda=ldf, ldb=ldb, torch_ref=False)
+            run(M, 2 * D, 2 * D, "NN", f"D{D} [u|g] dF ldb={ldb}", lda=(2 * D + 3) // 4 * 4, ldb=ldb, torch_ref=False)
+    sys.exit(0)
+
 if len(sys.argv) > 1 and sys.argv[1] == "headsweep":
     # c5's post-pool GEMMs on the tiled kernel: split counts at the tile AIMX_GEMM_TILE forces
     for sp in (0, 2, 3, 4, 6, 8, 12, 16):
