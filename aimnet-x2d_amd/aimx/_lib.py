@@ -359,7 +359,7 @@ def head_cluster(F=256):
     The clustered head (2 workgroups per tile, about 5 % of the c2 step) relies on both workgroups
     of a cluster running at once, which holds while no other process's kernels share the GPU and
     no kernel of this process runs beside the head (see head_cluster_allowed). Otherwise the default
-    is 1, which has no inter-workgroup wait at all. AIMX_HEAD_CLUSTER overrides both. A wait that
+    is 1, which has no inter-workgroup wait at all. A wait that
     still gives up poisons that launch's outputs with NaN (head.hip cluster_poisoned), so the
     per-step NaN count of the train loop sees it on the step it happens. At F = 512 (c4) the
     chain is 4x the work per tile and 4 workgroups per tile measured best (c4 step 3.278 ms vs

@@ -1200,6 +1200,46 @@ def test_fused_head_matches_module_path(name, monkeypatch):
         assert norm_rel(g1[k].cpu().numpy(), g2[k].cpu().numpy()) < 2e-5, k
 
 
+@pytest.mark.parametrize("rows", [None, 200])
+def test_c5_head_path_matches_tiles(rows):
+    """c5 at its configured batch (256 molecules, F = 1024: outside the fused head kernels; its
+    G x F x F chain on k_gemm_deep, 256 tiles) against the same model on the LDS-staged tiles
+    (AIMX_GEMM_DEEP option 0): outputs and every gradient. With the chain restricted to the first
+    `rows` molecules (_aimx_head_rows, what graph capture sets: padding molecules never reach the
+    head) the outputs equal the unrestricted run's first rows, and both paths agree on the
+    gradients of the loss over them."""
+    from aimx import _lib
+    z, cfg, (af, edges, batch, tc), loss_w = full_size_case("c5")
+    e0 = torch.empty(0, 2, dtype=torch.long, device=DEV)
+    d = lambda t: t.to(DEV)  # noqa: E731
+    args = ({k: d(v) for k, v in af.items()}, d(edges), d(batch), d(tc), torch.empty(0, 4, dtype=torch.long, device=DEV),
+            e0, e0)
+    w = torch.from_numpy(loss_w).to(DEV)
+    res = []
+    for deep in (16, 0):
+        with _lib.options(AIMX_GEMM_DEEP=deep):
+            model = _build_model(cfg, int(z["seed"]))
+            assert not model._aimx_head_ok()
+            if rows is not None:
+                model.__dict__["_aimx_head_rows"] = rows
+            out, _, _ = model(*args)
+            (out * w[:out.shape[0]]).sum().backward()
+            g = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+            res.append((out.detach().clone(), g))
+    (o1, g1), (o2, g2) = res
+    if rows is not None:
+        assert o1.shape[0] == rows
+        with torch.no_grad():
+            of, _, _ = _build_model(cfg, int(z["seed"]))(*args)
+        assert norm_rel(o1.cpu().numpy(), of[:rows].cpu().numpy()) < 1e-5
+    assert norm_rel(o1.cpu().numpy(), o2.cpu().numpy()) < 1e-5
+    assert g1.keys() == g2.keys()
+    for k in g1:
+        if "attention_weights" in k and k.endswith("bias"):
+            continue  # exactly 0 in exact arithmetic (softmax shift invariance)
+        assert norm_rel(g1[k].cpu().numpy(), g2[k].cpu().numpy()) < 2e-5, k
+
+
 def test_fused_head_dropout():
     """Train mode: ~p of the head's hidden units dropped, a fixed seed is deterministic, another
     seed differs, and the backward runs (finite gradients)."""

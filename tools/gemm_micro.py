@@ -141,13 +141,6 @@ if len(sys.argv) > 1 and sys.argv[1] == "ugpad":
             run(M, 2 * D, 2 * D, "NN", f"D{D} [u|g] dF ldb={ldb}", lda=(2 * D + 3) // 4 * 4, ldb=ldb, torch_ref=False)
     sys.exit(0)
 
-if len(sys.argv) > 1 and sys.argv[1] == "headsweep":
-    # c5's post-pool GEMMs on the tiled kernel: split counts at the tile AIMX_GEMM_TILE forces
-    for sp in (0, 2, 3, 4, 6, 8, 12, 16):
-        run(258, 1024, 1024, "NT", f"fwd {os.environ.get('AIMX_GEMM_TILE', 'auto')} S={sp}", splits=sp, torch_ref=False)
-        run(258, 1024, 1024, "NN", f"dX  {os.environ.get('AIMX_GEMM_TILE', 'auto')} S={sp}", splits=sp, torch_ref=False)
-    sys.exit(0)
-
 if len(sys.argv) > 1 and sys.argv[1] == "splits":
     for M, N, K, lab in [(76, 77, 9170, "c2 dW mlp"), (152, 305, 9170, "c2 dW_ig"), (256, 257, 9170, "c2 concat dW")]:
         for sp in (0, 4, 8, 12, 16, 24, 32, 48, 64):

@@ -52,7 +52,7 @@ def main():
     def fwdbwd():
         head().backward()
 
-    from aimx import ops
+    from aimx import _lib, ops
     blocks = list(m.ffn.layers)
 
     def fused():
@@ -72,8 +72,8 @@ def main():
     res = {"head_fwd_us": timed(fwd), "head_fwd_bwd_us": timed(fwdbwd)}
     for cfg in os.environ.get("HEAD_CLUSTERS", "1,2,4").split(","):
         S, _, W = cfg.partition("w")  # "4" or "4w8": cluster 4, 8 waves
-        os.environ["AIMX_HEAD_CLUSTER"] = S
-        if W:
+        _lib.HEAD_CLUSTER_FORCE = int(S)
+        if W:  # (tuning build only: AIMX_LIB_PATH=lib/libaimx_tune.so)
             os.environ["AIMX_HEAD_WAVES"] = W
         else:
             os.environ.pop("AIMX_HEAD_WAVES", None)

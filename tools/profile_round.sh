@@ -25,7 +25,6 @@ A=(
   "900 round/bench_plain.log python3 bench.py"
 )
 B=(
-  "400 round/parity_b.log python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hop_rows.py -q -x --timeout 200 --timeout-method thread"
   "300 round/bench_c3.log python3 bench.py --config c3 --no-eager"
   "300 round/bench_c4.log python3 bench.py --config c4 --no-cpu-baseline"
   "300 round/bench_c5.log python3 bench.py --config c5 --no-cpu-baseline"
