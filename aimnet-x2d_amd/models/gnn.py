@@ -210,8 +210,10 @@ class GNN(nn.Module):
         # a caller that reads only the first rows of the output (GraphedTrainStep, the autograph: the
         # rows after them are padding molecules) sets _aimx_head_rows, and the post-pool chain
         # (gnn.py:252-258: a per-molecule function) runs on those rows alone
+        # (only for the module path: the fused head's tiles of 4-8 molecules gain nothing from a
+        # padding molecule less, while the slice's backward costs a zero fill and a copy)
         rows = self.__dict__.get("_aimx_head_rows")
-        if rows is not None and 0 < rows < x_pooled.shape[0]:
+        if rows is not None and 0 < rows < x_pooled.shape[0] and not self._aimx_head_ok():
             x_pooled = x_pooled[:rows]
         try:
             if self._aimx_head_ok():
