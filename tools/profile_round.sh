@@ -4,11 +4,11 @@
 #      PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic, the default bench line;
 #   b: the parity tests again, c3/c4/c5 bench lines, step traces of c4/c5, c4's MFMA-busy PMC pass;
 #   b2: AMP bench lines (c2/c4/c5), MFMA-busy PMC passes on c2 and c5 (whole-step MFMA against peak);
-#   t: the whole -m gpu suite;
+#   t: smoke and the whole -m gpu suite;
 #   s: the c5 1M-molecule 6-hop HDF5 stream line and the feed's own rate at the per-rank thread
 #      count of an 8-rank node (16: the box's CPU share per GPU);
 #   c: the per-tensor parity report, the DDP lines (world-size-1 RCCL with the DDP-wrapped autograph
-#      leg; two gloo ranks sharing the GPU), the k_mlps phase stamps and smoke;
+#      leg; two gloo ranks sharing the GPU) and smoke;
 # Outputs under gpurun_out/round/; tools/collect_profiles.py copies the summaries into profiles/.
 # usage: tools/profile_round.sh a|b|b2|c
 set -o pipefail
@@ -51,11 +51,10 @@ C=(
   "600 round/parity_report.log python3 -u tools/parity_report.py --out $R/parity.json"
   "300 round/bench_ddp_world1.log python3 bench.py --ddp-world1 --no-cpu-baseline --no-roofline"
   "300 round/bench_dp2_gloo.log python3 bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-eager"
-  "120 round/mlps_trace_c4.log python3 -u tools/mlps_trace.py c4"
-  "120 round/mlps_trace_c5.log python3 -u tools/mlps_trace.py c5"
   "300 round/smoke.log python3 -c 'import __graft_entry__ as g; g.smoke()'"
 )
 T=(
+  "300 round/smoke.log python3 -c 'import __graft_entry__ as g; g.smoke()'"
   "?900 round/tests.log python3 -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread"
 )
 case "$1" in
