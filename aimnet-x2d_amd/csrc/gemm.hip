@@ -1539,9 +1539,7 @@ __global__ void k_splitk_reduce(const AimxGemmArgs a, int splits, int tiles_n) {
 // the epilogue operands are loaded before the k loop.
 constexpr int kDpU = 4;  // 8-k groups per register set (two sets alternate: 8 groups in flight)
 
-// IL (tuning build): 8-k groups dealt to the waves round-robin (group g -> wave g % NW), so the NW
-// waves read the same 128-byte lines together, instead of each wave a contiguous K / NW range.
-template <bool BKC, int NW, bool IL = false>
+template <bool BKC, int NW>
 __global__ __launch_bounds__(64 * NW) void k_gemm_deep(const AimxGemmArgs a, int tiles_m, int ntiles, int kq,
                                                        uint32_t a_bytes, uint32_t b_bytes) {
   constexpr int NO = 1024 / (64 * NW);  // outputs finished per thread
@@ -1602,12 +1600,11 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_deep(const AimxGemmArgs a, int
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 
-  const int kend = IL ? K : ke;
   auto load_set = [&](int sidx, floatx4 (&fa)[kDpU], floatx4 (&fb)[kDpU]) {
 #pragma unroll
     for (int u = 0; u < kDpU; ++u) {
-      const int k0 = IL ? 8 * (w + NW * (sidx * kDpU + u)) : kb + 8 * (sidx * kDpU + u);
-      const bool kok = k0 + 4 * h < kend;
+      const int k0 = kb + 8 * (sidx * kDpU + u);
+      const bool kok = k0 + 4 * h < ke;
       fa[u] = bload4(ra, kok ? va : a_bytes, __builtin_amdgcn_readfirstlane(4u * (uint32_t)k0));
       if (BKC) {
         fb[u] = bload4(rb, kok ? vb : b_bytes, __builtin_amdgcn_readfirstlane(4u * (uint32_t)k0));
@@ -1625,8 +1622,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_deep(const AimxGemmArgs a, int
       for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][j], fb[u][j], acc, 0, 0, 0);
   };
   constexpr int KS = 8 * kDpU;
-  const int ngw = IL ? max(0, ((K + 7) / 8 - w + NW - 1) / NW) : 0;  // IL: this wave's groups
-  const int ns = IL ? (ngw + kDpU - 1) / kDpU : (ke > kb ? (ke - kb + KS - 1) / KS : 0);
+  const int ns = ke > kb ? (ke - kb + KS - 1) / KS : 0;
   floatx4 fa0[kDpU], fb0[kDpU], fa1[kDpU], fb1[kDpU];
   if (ns > 0) load_set(0, fa0, fb0);
   // loads unconditional (a set past the range reads 0): conditional ones leave hipcc waiting for
@@ -2057,11 +2053,8 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
     const uint32_t a_bytes = (uint32_t)(4 * ((a.M - 1) * a.sam + a.K));
     const uint32_t b_bytes = (uint32_t)(a.sbk == 1 ? 4 * ((a.N - 1) * a.sbn + a.K) : 4 * ((a.K - 1) * a.sbk + a.N));
     using Fn = void (*)(const AimxGemmArgs, int, int, int, uint32_t, uint32_t);
-    Fn fn = a.sbk == 1 ? (nw == 16 ? k_gemm_deep<true, 16> : k_gemm_deep<true, 8>)
-                       : (nw == 16 ? k_gemm_deep<false, 16> : k_gemm_deep<false, 8>);
-    if (tune_i64("AIMX_GEMM_DEEP_IL", 0) != 0)  // tuning build A/B: round-robin k groups
-      fn = a.sbk == 1 ? (nw == 16 ? k_gemm_deep<true, 16, true> : k_gemm_deep<true, 8, true>)
-                      : (nw == 16 ? k_gemm_deep<false, 16, true> : k_gemm_deep<false, 8, true>);
+    const Fn fn = a.sbk == 1 ? (nw == 16 ? k_gemm_deep<true, 16> : k_gemm_deep<true, 8>)
+                             : (nw == 16 ? k_gemm_deep<false, 16> : k_gemm_deep<false, 8>);
     hipLaunchKernelGGL(fn, dim3((unsigned)nt), dim3(64 * nw), 0, s, a, tm, nt, kq, a_bytes, b_bytes);
     AIMX_CHECK_LAUNCH();
     return AIMX_OK;
