@@ -1826,7 +1826,10 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs, int bb) {
   WgPlan w;
   const int64_t N = p.col_out ? p.N + 1 : p.N;
   if (p.K >= 2048) {
-    // ~512 atoms of K per workgroup: 16 LDS fills, and ~2 workgroups per CU at c2's 36 blocks.
+    // ~512 atoms of K per workgroup (16 LDS fills; ~2 workgroups per CU at c2's 36 blocks), 1024 for
+    // problems of >= 9 blocks (c4 / c5: half the split-K slabs, longer fill pipelines — steps c4
+    // 2.390 -> 2.376, c5 3.524 -> 3.502 ms; c2 keeps 512: 256 measured 0.717 vs 0.702;
+    // profiles/r06_wgrad_kper_ab.txt)
     // (160-wide blocks measured slower: wgrad launch c4 472 -> 490 us, c5 853 -> 880 us, a quarter
     // of the workgroups at 109 VGPRs; profiles/r03_gemm_ab.txt — removed in round 6)
     w.lds = true;
@@ -1834,7 +1837,8 @@ WgPlan wg_plan(const AimxWgradProblem& p, int64_t min_wgs, int bb) {
     w.slab = (int64_t)w.bb * w.bb;
     w.tiles_x = (int)cdiv(p.M, w.bb);
     w.tiles_y = (int)cdiv(N, w.bb);
-    const int64_t kper = 512;  // atoms per workgroup
+    const int64_t kper =
+        std::max<int64_t>(64, tune_i64("AIMX_WGRAD_KPER", (int64_t)w.tiles_x * w.tiles_y >= 9 ? 1024 : 512));
     int64_t sp = std::max<int64_t>(1, std::min<int64_t>(64, p.K / kper));
     if (min_wgs > 0)
       sp = std::max(sp, std::min<int64_t>({64, p.K / 128, cdiv(min_wgs, (int64_t)w.tiles_x * w.tiles_y)}));

@@ -25,10 +25,12 @@ def main():
     bufs = []
     arr = (_lib.WgradProblem * len(shapes))()
     for i, (M, N) in enumerate(shapes):
-        dy, x = torch.randn(K, M, device=dev), torch.randn(K, N, device=dev)
+        # rows rounded to 4 floats, as the stack lays them out (16-byte staging)
+        lm, ln = (M + 3) // 4 * 4, (N + 3) // 4 * 4
+        dy, x = torch.randn(K, lm, device=dev), torch.randn(K, ln, device=dev)
         dw, db = torch.empty(M, N, device=dev), torch.empty(M, device=dev)
         bufs += [dy, x, dw, db]
-        arr[i].dY, arr[i].ld_dy, arr[i].X, arr[i].ld_x = dy.data_ptr(), M, x.data_ptr(), N
+        arr[i].dY, arr[i].ld_dy, arr[i].X, arr[i].ld_x = dy.data_ptr(), lm, x.data_ptr(), ln
         arr[i].dW, arr[i].ld_dw, arr[i].col_out = dw.data_ptr(), N, db.data_ptr()
         arr[i].M, arr[i].N, arr[i].K = M, N, K
     n = len(shapes)
