@@ -1984,7 +1984,7 @@ int launch_big(const AimxGemmArgs& a, const BigPlan& p, hipStream_t s) {
 bool deep_ok(const AimxGemmArgs& a) {
   if (opt_i64("AIMX_GEMM_DEEP", 1) == 0 || a.precision != AIMX_PREC_FP32 || a.splits > 0) return false;
   if (a.ones_col || a.zc_rowptr || a.sak != 1 || (a.sbk != 1 && a.sbn != 1)) return false;
-  if (a.M < 1 || a.M > 1024 || a.N < 1 || a.K < 512 || a.K % 4 != 0) return false;
+  if (a.M < 1 || a.M > 1024 || a.N < 1 || a.K < tune_i64("AIMX_GEMM_DEEP_KMIN", 512) || a.K % 4 != 0) return false;
   // enough tiles to spread over the CUs: the output layer (N = tasks: 8 tiles) is faster on the
   // split-K tiles (7.3 vs 13.4 us, profiles/r06_deep_gemm_micro.txt)
   const int64_t tiles = cdiv(a.M, 32) * cdiv(a.N, 32);

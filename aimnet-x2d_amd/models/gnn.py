@@ -237,19 +237,17 @@ class GNN(nn.Module):
 
     def _aimx_head_ok(self) -> bool:
         """The fused head covers the reference's post-pool chain when every LinearBlock is F -> F
-        with one activation and one dropout setting, F <= 512 (above 256 only where clustered
-        launches are allowed), F and the input width multiples of 32 (FUSED_HEAD = False, a module
-        attribute for tests and A/Bs, disables it)."""
+        with one activation and one dropout setting, F <= 256, F and the input width multiples of 32
+        (FUSED_HEAD = False, a module attribute for tests and A/Bs, disables it). Wider chains run
+        the module path, whose G x F x F products take k_gemm_deep: at c4 (F = 512) it measured
+        2.370 vs 2.388 ms per step on the fused 8-molecule kernels; at c2 (F = 256) the fused
+        kernels keep 0.707 vs 0.815 ms (profiles/r06_head_path_ab.txt). (ops.head itself still
+        takes F up to HEAD_MAX_F = 512.)"""
         if not FUSED_HEAD:
             return False
         pp, blocks = self.post_pooling_projection, list(self.ffn.layers)
         F = pp.out_features
-        if not (32 <= F <= ops.HEAD_MAX_F and F % 32 == 0 and pp.in_features % 32 == 0 and 1 <= len(blocks) <= 8):
-            return False
-        # above F = 256 the fused chain pays off only clustered (c4: 3.28 ms with 4 workgroups per
-        # tile, 3.56 with 1 vs 3.32 on the module path): where clusters are not allowed (ranks sharing
-        # a GPU, auxiliary stream) the module path runs instead
-        if F > 256 and _lib.head_cluster(F) == 1:
+        if not (32 <= F <= 256 and F % 32 == 0 and pp.in_features % 32 == 0 and 1 <= len(blocks) <= 8):
             return False
         if self.skip_transform.in_features != F or self.skip_transform.out_features != F or \
                 self.output_layer.in_features != 2 * F:
