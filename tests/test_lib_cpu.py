@@ -142,3 +142,31 @@ def test_head_cluster_rule(monkeypatch):
     assert _lib.head_cluster(256) == 1  # 8 ranks share one GPU (rehearsal)
     monkeypatch.setattr(_lib, "HEAD_CLUSTER_FORCE", 4)
     assert _lib.head_cluster(256) == 4  # explicit override
+
+
+def test_product_library_switches_are_the_documented_options():
+    """The product library reads no environment variable (getenv only in the tuning build's branch
+    of version.hip), and the only AIMX_* names compiled into it are the path options include/aimx.h
+    documents (tune_i64 knobs compile to their defaults: their names must not be in libaimx.so)."""
+    csrc = os.path.join(ROOT, "aimnet-x2d_amd", "csrc")
+    header = open(os.path.join(ROOT, "include", "aimx.h")).read()
+    block = header[header.index("/* Path options"):header.index("int aimx_set_option")]
+    documented = set(re.findall(r'"(AIMX_[A-Z0-9_]+)"', block))
+    used = set()
+    for dirpath, _, files in os.walk(csrc):
+        for f in files:
+            if not f.endswith((".hip", ".h", ".cpp")):
+                continue
+            src = open(os.path.join(dirpath, f)).read()
+            used |= set(re.findall(r'opt_i64\("(AIMX_[A-Z0-9_]+)"', src))
+            if "getenv" in src:
+                assert f == "version.hip", f
+                i = src.index("getenv")
+                assert src.rfind("#ifdef AIMX_TUNING", 0, i) > src.rfind("#endif", 0, i), "getenv outside the tuning branch"
+    assert used == documented, (sorted(used - documented), sorted(documented - used))
+    assert len(documented) < 10
+    lib = os.path.join(ROOT, "aimnet-x2d_amd", "lib", "libaimx.so")
+    if os.path.exists(lib):
+        names = set(re.findall(rb"AIMX_[A-Z0-9_]{2,}", open(lib, "rb").read()))
+        names = {n.decode() for n in names if not n.decode().startswith(("AIMX_PREC", "AIMX_ACT", "AIMX_OK", "AIMX_EARG"))}
+        assert names <= documented, sorted(names - documented)
