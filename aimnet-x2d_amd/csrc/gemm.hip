@@ -655,338 +655,8 @@ __global__ __launch_bounds__(256) void k_gemm(const AimxGemmArgs a, int kchunk, 
   }
 }
 
-// ---- Large-tile GEMM (round 6): the MFMA-bound products of c4 / c5 --------------------------------
-// Y[M, N] = epi(A[M, K] B) with M = atoms (1e4-2e4) and N, K = 256-1024: the embedding projection,
-// the stack's [Wi; Wg] input projections and their input gradients, the concat and its input
-// gradient (gnn.py:224-246, layers.py:82-87). k_gemm's 64 x 64 blocks give each wave a 32 x 32 tile
-// of 16 x 16 x 4 products: two operand reads per MFMA pair and every operand re-read by twice as
-// many blocks — 47-60 % of the fp32 matrix rate at c5. Here:
-//  * a 128 x BN block (BN = 128 or 64), 4 waves in 2 x 2, each wave 64 x BN/2 as 32 x 32 tiles of
-//    v_mfma_f32_32x32x2_f32 (exact fp32, 64 cycles, 16 accumulators per tile);
-//  * operands staged through LDS as k-contiguous rows of 36 floats ([m][k] and [n][k]; an
-//    n-contiguous B is transposed by the staging writes), 32 k per slice, two LDS stages and one
-//    barrier per slice, the next slice's global loads in flight through the current slice's MFMAs;
-//  * fragments by ds_read_b128 in a k-permuted order: lane (r, h) of k-group g reads k = 8g + 4h
-//    .. 8g + 4h + 3 of its row and MFMA j takes component j (A and B agree on the permutation, so
-//    every product pairs the same k; the stride of 36 floats puts a 16-lane group on 16 distinct
-//    4-bank groups);
-//  * 16-byte global loads at any 4-byte alignment (gfx950 executes dwordx4 at 4-byte-aligned
-//    addresses: odd widths such as the D = 307 weight rows need no dword path), 64-bit addressing
-//    (no 2 GiB operand limit); rows / columns past M / N read a clamped valid row (their outputs
-//    are never stored), k past the end of the slice (K, or the non-empty hop chunks) is zeroed;
-//  * blocks walk the N tiles of one row block on one XCD (shared A rows in that XCD's L2);
-//  * k_gemm's epilogue (bias, residuals, activation, pre-activation, dropout, act', masks) through
-//    an LDS transpose of the tile.
-// No split K (M alone fills the chip), no ones column, fp32 only (the AMP path stays on k_gemm).
-struct __attribute__((packed, aligned(4))) GbF4 {
-  float x, y, z, w;
-};
+// 32 x 32 x 2 fp32 MFMA accumulator (k_gemm_deep)
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-constexpr int kGbBM = 128, kGbBK = 32, kGbS = kGbBK + 4;
-
-__device__ __forceinline__ floatx4 gb_load(const float* p) {
-  const GbF4 v = *reinterpret_cast<const GbF4*>(p);
-  return floatx4{v.x, v.y, v.z, v.w};
-}
-
-// component e of v, 0 for e outside 0..3 (selects only: a branch here would make hipcc wait for the
-// loads one by one)
-__device__ __forceinline__ float gb_pick(const floatx4& v, int e) {
-  const float lo = (e & 1) ? v[1] : v[0], hi = (e & 1) ? v[3] : v[2];
-  const float x = (e & 2) ? hi : lo;
-  return (unsigned)e < 4u ? x : 0.f;
-}
-
-// AK: A k-contiguous ([m][k], the projections) or m-contiguous ([k][m]: a weight gradient's dY^T);
-// BKC: B k-contiguous ([n][k]) or n-contiguous ([k][n]). An m- / n-contiguous operand is staged by
-// 16-byte runs along m / n of 8 k rows per wave (128 bytes per k row) and transposed by the LDS
-// writes. A weight gradient (a.ones_col: column N - 1 of B is the implicit ones column, the bias
-// gradient; zc_dim 1: B's columns past the non-empty hop chunks read as 0) splits K over `splits`
-// blocks per tile: partial tiles go to sc1 slabs in accumulator order, and the last block of a tile
-// to arrive (agent-scope counter, self-resetting) sums them in split order (deterministic) and runs
-// the epilogue, as k_gemm's split-K path.
-template <int BN, int NW, bool AK, bool BKC>
-__global__ __launch_bounds__(64 * NW) void k_gemm_big(const AimxGemmArgs a, int tiles_n, int ntiles, int kchunk,
-                                                     int splits) {
-  constexpr int BM = kGbBM, BK = kGbBK, S = kGbS, NT = 64 * NW;
-  constexpr int WR = NW / 2;                      // wave rows (2 or 4); two wave columns
-  constexpr int FM = BM / (32 * WR), FN = BN / 64;  // 32 x 32 tiles per wave along m / n
-  constexpr int LA = BM * S, LB = BN * S;         // floats per stage and operand
-  constexpr int NA = BM * BK / 4 / NT;            // A float4s per thread per slice
-  constexpr int NB = BN * BK / 4 / NT;            // B float4s per thread per slice
-  constexpr int RS = NT / 8;                      // k-contiguous rows staged per pass
-  __shared__ __attribute__((aligned(16))) float smem[2 * (LA + LB)];
-  static_assert(BM * (BN + 1) <= 2 * (LA + LB), "C tile must fit the staging LDS");
-  static_assert(NA >= 1 && NB >= 1 && FM >= 1 && FN >= 1, "tile geometry");
-
-  // XCD-aware order: the blocks one XCD runs (b % 8 equal under round-robin dispatch) take a
-  // contiguous range of (tile, split) items, row block major, a tile's splits adjacent (bijective
-  // for any grid size)
-  const int bid = blockIdx.x, nb = (int)gridDim.x;
-  const int q = nb / 8, rr = nb % 8, xcd = bid % 8, loc = bid / 8;
-  const int item = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
-  if (item >= ntiles * splits) return;
-  const int tile = item / splits, z = item - tile * splits;
-  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int M = (int)a.M, N = (int)a.N;
-  const int Nreal = a.ones_col ? N - 1 : N;
-  int kend = (int)a.K, nlim = Nreal;  // nlim: B columns past it read as 0 (the ones column aside)
-  if (a.zc_rowptr) {
-    const int zE = zc_extent(a.zc_rowptr, a.zc_rows, a.zc_chunks, a.zc_width);
-    if (a.zc_dim == 0) {
-      kend = min(kend, zE);
-    } else if (n0 >= zE && !(a.ones_col && n0 + BN > Nreal)) {  // never the tile of the ones column
-      if (a.zc_dim == 1 && z == 0)
-        for (int e = tid; e < BM * BN; e += NT) {
-          const int m = m0 + e / BN, n = n0 + e % BN;
-          if (m < M && n < Nreal) a.C[(int64_t)m * a.ldc + n] = 0.f;
-        }
-      return;
-    } else {
-      nlim = min(nlim, zE);
-    }
-  }
-  const int kbeg = z * kchunk;
-  const int kfin = min(kend, kbeg + kchunk);
-
-  // staging coordinates. k-contiguous operands: thread t loads float4 (t & 7) of rows t / 8 + RS i
-  // (8 lanes cover one row's 128 bytes of the slice). m- / n-contiguous operands: float4 q = tid +
-  // NT i is k row (q & 7) + 8 ((q >> 3) / NC), columns 4 ((q >> 3) % NC): a wave covers 8 k rows x 8
-  // float4 columns, 128 contiguous bytes per k row.
-  const int a_c = tid & 7, a_r = tid >> 3;
-  const float* __restrict__ Ap = a.A;
-  const float* __restrict__ Bp = a.B;
-  const int64_t sam = a.sam, sak = a.sak, sbn = a.sbn, sbk = a.sbk;
-  constexpr int NCA = BM / 4, NC = BN / 4;
-  int64_t a_row[NA];
-  int a_kr[NA], a_mc[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    if constexpr (AK) {
-      a_row[i] = (int64_t)min(m0 + a_r + RS * i, M - 1) * sam;
-      a_kr[i] = a_mc[i] = 0;
-    } else {
-      const int qq = tid + NT * i;
-      a_kr[i] = (qq & 7) + 8 * (qq / (8 * NCA));
-      a_mc[i] = 4 * ((qq >> 3) % NCA);
-      a_row[i] = 0;
-    }
-  }
-  int64_t b_row[NB];
-  int b_kr[NB], b_nc[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    if constexpr (BKC) {
-      b_row[i] = (int64_t)min(n0 + a_r + RS * i, N - 1) * sbn;
-      b_kr[i] = b_nc[i] = 0;
-    } else {
-      const int qq = tid + NT * i;
-      b_kr[i] = (qq & 7) + 8 * (qq / (8 * NC));
-      b_nc[i] = 4 * ((qq >> 3) % NC);
-      b_row[i] = 0;
-    }
-  }
-
-  floatx4 ra[NA], rb[NB];
-  auto load_slice = [&](int k0) {
-    const int kk = min(k0 + 4 * a_c, kfin - 4);  // a run that would cross kfin starts 4 before it
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if constexpr (AK) {
-        ra[i] = gb_load(Ap + a_row[i] + kk);
-      } else {
-        const int k = min(k0 + a_kr[i], kfin - 1);
-        const int m = min(m0 + a_mc[i], M - 4);     // a run past M starts 4 before it (M >= 4)
-        ra[i] = gb_load(Ap + (int64_t)k * sak + m);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      if constexpr (BKC) {
-        rb[i] = gb_load(Bp + b_row[i] + kk);
-      } else {
-        const int k = min(k0 + b_kr[i], kfin - 1);
-        const int n = min(n0 + b_nc[i], Nreal - 4);  // a run past B's columns starts 4 before their end
-        rb[i] = gb_load(Bp + (int64_t)k * sbk + n);
-      }
-    }
-  };
-  auto store_slice = [&](int k0, int stage) {
-    float* As = smem + stage * (LA + LB);
-    float* Bs = As + LA;
-    const bool ktail = k0 + BK > kfin;  // block-uniform
-    const int kk = k0 + 4 * a_c;
-    const int sh = kk - min(kk, kfin - 4);  // 0, or how far the run was moved back (4+: all past kfin)
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if constexpr (AK) {
-        floatx4 v = ra[i];
-        if (ktail) v = floatx4{gb_pick(ra[i], sh), gb_pick(ra[i], sh + 1), gb_pick(ra[i], sh + 2), gb_pick(ra[i], sh + 3)};
-        *reinterpret_cast<floatx4*>(&As[(a_r + RS * i) * S + 4 * a_c]) = v;
-      } else {
-        const int mm = m0 + a_mc[i];
-        const int shm = mm - min(mm, M - 4);
-        const bool kin = k0 + a_kr[i] < kfin;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = shm ? gb_pick(ra[i], shm + e) : ra[i][e];
-          As[(a_mc[i] + e) * S + a_kr[i]] = kin ? x : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      if constexpr (BKC) {
-        floatx4 v = rb[i];
-        if (ktail) v = floatx4{gb_pick(rb[i], sh), gb_pick(rb[i], sh + 1), gb_pick(rb[i], sh + 2), gb_pick(rb[i], sh + 3)};
-        *reinterpret_cast<floatx4*>(&Bs[(a_r + RS * i) * S + 4 * a_c]) = v;
-      } else {
-        const int nn = n0 + b_nc[i];
-        const int shn = nn - min(nn, Nreal - 4);
-        const bool kin = k0 + b_kr[i] < kfin;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = shn ? gb_pick(rb[i], shn + e) : rb[i][e];
-          x = nn + e < nlim ? x : 0.f;
-          if (a.ones_col) x = nn + e == Nreal ? 1.f : x;
-          Bs[(b_nc[i] + e) * S + b_kr[i]] = kin ? x : 0.f;
-        }
-      }
-    }
-  };
-
-  floatx16 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int l32 = lane & 31, h = lane >> 5;
-  auto compute_slice = [&](int stage) {
-    const float* As = smem + stage * (LA + LB);
-    const float* Bs = As + LA;
-#pragma unroll
-    for (int g = 0; g < BK / 8; ++g) {
-      floatx4 af[FM], bf[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const floatx4*>(&As[(wr * (BM / WR) + i * 32 + l32) * S + 8 * g + 4 * h]);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bf[j] = *reinterpret_cast<const floatx4*>(&Bs[(wc * (BN / 2) + j * 32 + l32) * S + 8 * g + 4 * h]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // one register stage, two LDS stages, one barrier per slice. The loads run unconditionally (a
-  // slice past the end reloads valid addresses and is never stored) so the wait before each store
-  // sees one pending set (see k_gemm).
-  const int nsl = kfin > kbeg ? (kfin - kbeg + BK - 1) / BK : 0;
-  if (nsl > 0) {
-    load_slice(kbeg);
-    store_slice(kbeg, 0);
-  }
-  __syncthreads();
-  for (int sl = 0; sl < nsl; ++sl) {
-    const int kn = kbeg + min(sl + 1, nsl - 1) * BK;
-    load_slice(kn);
-    // the loads stay ahead of the MFMAs (hipcc would otherwise sink them to their use, after the
-    // compute, and every slice would wait one full memory round trip)
-    __builtin_amdgcn_sched_barrier(0);
-    compute_slice(sl & 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (sl + 1 < nsl) store_slice(kn, (sl + 1) & 1);
-    __syncthreads();
-  }
-
-  if (splits > 1) {
-    // partial tile -> slab in accumulator order (thread tid's 16-float run r of tile (i, j) at
-    // (((i * FN + j) * 4 + r4) * NT + tid) * 4 floats); the last block of the tile to arrive sums
-    // the slabs in split order (sc1 hand-off, MI355X_MICROARCH.md "Valid forms" row 1)
-    constexpr int TILE = BM * BN;
-    const __amdgpu_buffer_rsrc_t rws = make_rsrc(a.workspace, (uint32_t)(4 * (int64_t)splits * ntiles * TILE));
-    const uint32_t slab0 = (uint32_t)(4 * ((int64_t)z * ntiles + tile) * TILE);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-          store_sc1(rws, slab0 + 16u * (uint32_t)(((i * FN + j) * 4 + r4) * NT + tid),
-                    floatx4{acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]});
-    int* flag = reinterpret_cast<int*>(smem);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == splits - 1);
-      if (last) __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // self-reset
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    const uint32_t zstride = (uint32_t)(4 * (int64_t)ntiles * TILE);
-    const uint32_t tile0 = (uint32_t)(4 * (int64_t)tile * TILE);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          const uint32_t off = tile0 + 16u * (uint32_t)(((i * FN + j) * 4 + r4) * NT + tid);
-          floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
-          for (int z0 = 0; z0 < splits; z0 += 8) {
-            floatx4 t[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) t[w] = load_sc1(rws, (uint32_t)min(z0 + w, splits - 1) * zstride + off);
-#pragma unroll
-            for (int w = 0; w < 8; ++w)
-              if (z0 + w < splits) sum += t[w];
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][4 * r4 + e] = sum[e];
-        }
-    __syncthreads();  // the flag word's readers are done before the C tile overwrites it
-  }
-
-  // C/D of 32x32: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5); transposed through
-  // LDS so the epilogue walks rows with consecutive lanes on consecutive columns
-  constexpr int CS = BN + 1;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        smem[(wr * (BM / WR) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CS + wc * (BN / 2) + j * 32 + l32] =
-            acc[i][j][r];
-  __syncthreads();
-  constexpr int NE = BM * BN / NT;
-#pragma unroll
-  for (int q0 = 0; q0 < NE; q0 += 8) {
-    int qm[8], qn[8];
-    float ev[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + (q0 + u) * NT;
-      qm[u] = m0 + e / BN;
-      qn[u] = n0 + e % BN;
-      ev[u] = smem[(e / BN) * CS + e % BN];
-    }
-    epilogue_n<8>(a, qm, qn, ev);
-  }
-}
 
 // ---- Weight-gradient GEMM (K = atoms, small M x N): MFMA fragments straight from L2 ----------
 // dW = dY^T X: A = dY^T is m-contiguous (sam == 1), B = X is n-contiguous (sbn == 1), K is the atom
@@ -1905,78 +1575,6 @@ bool gemm_as_wgrad(const AimxGemmArgs& a, AimxWgradProblem& pr) {
 }
 }  // namespace
 
-// k_gemm_big applies to the large fp32 products (see the kernel): the projections and input
-// gradients (A k-contiguous, one block per tile) and the long-K weight gradients (A m-contiguous, B
-// n-contiguous, K = atoms: K split over blocks). The tile edge BN (128 or 64) minimises the busiest
-// CU's work, ceil(items / CUs) x BN, ties to 128 (fewer operand re-reads). bn = 0: the product stays
-// on k_gemm / k_wgrad_lds.
-struct BigPlan {
-  int bn = 0, nw = 8, splits = 1, kchunk = 0, tiles = 0;
-};
-
-BigPlan big_plan(const AimxGemmArgs& a) {
-  BigPlan p;
-  // off by default (measured slower than k_gemm<64,64> / k_wgrad_lds at c4 / c5, profiles/r06_big_gemm_ab.txt);
-  // test hook / tuning build: 1 = by the rule below, 64 / 128 forced tile
-  const int64_t mode = opt_i64("AIMX_GEMM_BIG", 0);
-  if (mode == 0 || a.precision != AIMX_PREC_FP32 || a.splits > 1) return p;
-  const bool ak = a.sak == 1, wgrad = a.sam == 1 && a.sbn == 1 && a.sak != 1;
-  if (!(ak && (a.sbk == 1 || a.sbn == 1)) && !wgrad) return p;
-  if (a.ones_col && !wgrad) return p;
-  if (a.M < 128 || a.N < 64 || a.K < 64 || a.M >= (1ll << 31) || a.N >= (1ll << 31) || a.K >= (1ll << 31)) return p;
-  if (a.zc_rowptr && a.zc_width < kGbBK) return p;
-  const bool forced = mode == 64 || mode == 128;
-  if (!forced) {
-    if (ak && (a.M < 4096 || a.N < 128 || a.K < 128 || (double)a.M * (double)a.N * (double)a.K < 1.5e9)) return p;
-    if (wgrad && (a.M < 256 || a.N < 256 || a.K < 2048 || (double)a.M * (double)a.N * (double)a.K < 2e9)) return p;
-  }
-  const int64_t tm = cdiv(a.M, kGbBM);
-  auto items = [&](int bn, int sp) { return tm * cdiv(a.N, bn) * sp; };
-  auto splits_for = [&](int bn) -> int {
-    if (!wgrad) return 1;  // rows alone fill the chip
-    // ~512 blocks (two per CU), each >= 512 atoms of K
-    return (int)std::max<int64_t>(1, std::min<int64_t>({cdiv(512, tm * cdiv(a.N, bn)), 64, a.K / 512}));
-  };
-  if (forced) {
-    p.bn = (int)mode;
-  } else {
-    const int s128 = splits_for(128), s64 = splits_for(64);
-    const int64_t w128 = cdiv(items(128, s128), 256) * 128 * cdiv(a.K, s128);
-    const int64_t w64 = cdiv(items(64, s64), 256) * 64 * cdiv(a.K, s64);
-    p.bn = w64 < w128 ? 64 : 128;
-  }
-  p.splits = splits_for(p.bn);
-  p.kchunk = (int)(cdiv(cdiv(a.K, p.splits), kGbBK) * kGbBK);
-  p.splits = (int)cdiv(a.K, p.kchunk);
-  p.tiles = (int)(tm * cdiv(a.N, p.bn));
-  p.nw = tune_i64("AIMX_GEMM_BIG_W", 8) == 4 ? 4 : 8;  // waves per workgroup (test hook / tuning build)
-  if (p.splits > 1 && (!a.counters || p.tiles > a.n_counters)) p.bn = 0;  // no counters: k_wgrad_lds
-  return p;
-}
-
-size_t big_workspace_floats(const BigPlan& p) {
-  return p.bn && p.splits > 1 ? (size_t)p.splits * p.tiles * kGbBM * p.bn : 0;
-}
-
-template <int BN, int NW>
-void launch_big_t(const AimxGemmArgs& a, const BigPlan& p, hipStream_t s) {
-  using Fn = void (*)(const AimxGemmArgs, int, int, int, int);
-  const bool ak = a.sak == 1, bkc = a.sbk == 1;
-  const Fn fn = ak ? (bkc ? k_gemm_big<BN, NW, true, true> : k_gemm_big<BN, NW, true, false>)
-                   : k_gemm_big<BN, NW, false, false>;
-  const int tn = (int)cdiv(a.N, BN);
-  hipLaunchKernelGGL(fn, dim3((unsigned)(p.tiles * p.splits)), dim3(64 * NW), 0, s, a, tn, p.tiles, p.kchunk,
-                     p.splits);
-}
-
-int launch_big(const AimxGemmArgs& a, const BigPlan& p, hipStream_t s) {
-  if (p.nw == 8)
-    p.bn == 128 ? launch_big_t<128, 8>(a, p, s) : launch_big_t<64, 8>(a, p, s);
-  else
-    p.bn == 128 ? launch_big_t<128, 4>(a, p, s) : launch_big_t<64, 4>(a, p, s);
-  AIMX_CHECK_LAUNCH();
-  return AIMX_OK;
-}
 
 // workspace of the tiled kernels' split-K plan
 // k_gemm_deep: few rows, deep K (the post-pool chain at F >= 512: G x F x F, G <= 1024), A
@@ -2009,7 +1607,6 @@ size_t tiled_workspace_floats(const AimxGemmArgs& a) {
 // needs counters, so a caller without them falls back to the tiled plan)
 size_t gemm_workspace_floats(const AimxGemmArgs& a) {
   size_t f = tiled_workspace_floats(a);
-  f = std::max(f, big_workspace_floats(big_plan(a)));
   AimxWgradProblem pr;
   if (gemm_as_wgrad(a, pr)) {
     const WgPlan w = wg_plan(pr, kLoneWgs, wg_bb(&pr, 1));
@@ -2032,11 +1629,6 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
     if (a.zc_dim != 0 && (a.beta != 0.f || a.bias || a.res[0] || a.res[1] || a.res[2] || a.act_ncols > 0 ||
                           a.pre || a.dact_pre || a.mask_in || a.mask_out))
       return AIMX_EARG;
-  }
-  {
-    const BigPlan bp = big_plan(a);
-    if (bp.bn && (bp.splits == 1 || (a.workspace && a.workspace_bytes >= sizeof(float) * big_workspace_floats(bp))))
-      return launch_big(a, bp, s);
   }
   {
     AimxWgradProblem pr;
@@ -2135,53 +1727,11 @@ int launch_gemm(const AimxGemmArgs& a_in, hipStream_t s) {
 
 
 namespace aimx {
-// A weight-gradient problem of a grouped call as a k_gemm_big launch of its own (the long-K
-// products big_plan takes: c5's [Wi; Wg] 614 x 615, K = atoms); bp.bn = 0 when it stays grouped.
-AimxGemmArgs wgrad_args(const AimxWgradProblem& pr) {
-  AimxGemmArgs a{};
-  a.M = pr.M;
-  a.N = pr.col_out ? pr.N + 1 : pr.N;
-  a.K = pr.K;
-  a.A = pr.dY;
-  a.sam = 1;
-  a.sak = pr.ld_dy;
-  a.B = pr.X;
-  a.sbk = pr.ld_x;
-  a.sbn = 1;
-  a.C = pr.dW;
-  a.ldc = pr.ld_dw;
-  a.act = -1;
-  a.dact_kind = -1;
-  a.ones_col = pr.col_out ? 1 : 0;
-  a.col_out = pr.col_out;
-  a.precision = AIMX_PREC_FP32;
-  if (pr.zc_rowptr) {
-    a.zc_rowptr = pr.zc_rowptr;
-    a.zc_rows = pr.zc_rows;
-    a.zc_chunks = pr.zc_chunks;
-    a.zc_width = pr.zc_width;
-    a.zc_dim = 1;
-  }
-  a.counters = reinterpret_cast<int32_t*>(1);  // placeholder: big_plan only checks for counters
-  a.n_counters = INT64_MAX;
-  return a;
-}
-
-BigPlan wgrad_big_plan(const AimxWgradProblem& pr) {
-  if (pr.K < 2048) return BigPlan{};
-  return big_plan(wgrad_args(pr));
-}
-
 size_t wgrad_ws_bytes(const AimxWgradProblem* p, int32_t n, int64_t min_wgs) {
   if (!p || n < 0) return 0;
   size_t f = 0;
   const int bb = wg_bb(p, n);
   for (int32_t i = 0; i < n; ++i) {
-    const BigPlan bp = wgrad_big_plan(p[i]);
-    if (bp.bn) {
-      f += big_workspace_floats(bp);
-      continue;
-    }
     const WgPlan w = wg_plan(p[i], min_wgs, bb);
     if (w.splits > 1) f += (size_t)w.splits * w.tiles_x * w.tiles_y * w.slab;
   }
@@ -2197,11 +1747,6 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   int64_t ctiles = 0;
   const int bb = wg_bb(p, n);
   for (int32_t i = 0; i < n; ++i) {
-    const BigPlan bp = wgrad_big_plan(p[i]);
-    if (bp.bn) {
-      ctiles += bp.tiles;
-      continue;
-    }
     const WgPlan w = wg_plan(p[i], min_wgs, bb);
     ctiles += (int64_t)w.tiles_x * w.tiles_y;
   }
@@ -2244,21 +1789,6 @@ int wgrad_grouped_run(const AimxWgradProblem* p, int32_t n, void* workspace, siz
   };
   for (int32_t i = 0; i < n; ++i) {
     const AimxWgradProblem& pr = p[i];
-    {  // the large long-K problems: k_gemm_big launches of their own (slabs / counters in problem order)
-      const BigPlan bp = wgrad_big_plan(pr);
-      if (bp.bn) {
-        AimxGemmArgs ga = wgrad_args(pr);
-        ga.workspace = (float*)workspace + ws_off;
-        ga.workspace_bytes = sizeof(float) * big_workspace_floats(bp);
-        ga.counters = counters + cnt_off;
-        ga.n_counters = bp.tiles;
-        const int rc = launch_big(ga, bp, (hipStream_t)stream);
-        if (rc != AIMX_OK) return rc;
-        ws_off += (int64_t)big_workspace_floats(bp);
-        cnt_off += bp.tiles;
-        continue;
-      }
-    }
     const WgPlan w = wg_plan(pr, min_wgs, bb);
     const int32_t nt = w.tiles_x * w.tiles_y;
     if (w.lds) {

@@ -48,7 +48,6 @@ const char* aimx_version(void);
  *   "AIMX_MLPS"         0 / 1 = weight-streamed MLP off / for every width
  *   "AIMX_MLPS_RT"      row tiles per chunk of the weight-streamed MLP
  *   "AIMX_WGRAD_BB"     64 / 80 = weight-gradient block edge
- *   "AIMX_GEMM_BIG"     1 / 64 / 128 = large-tile GEMM by its rule / forced tile (default off)
  *   "AIMX_GEMM_DEEP"    0 = few-row deep-K products on the LDS-staged tiles; 8 = 8 waves
  *   "AIMX_HOP_MAX_ROWS" n = the hop's row-range splitting at n rows per launch (not 2^31)
  * The tuning build (make tune -> lib/libaimx_tune.so) also reads these names, and its A/B knobs

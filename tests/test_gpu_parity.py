@@ -433,34 +433,28 @@ def test_gemm_unaligned_rows_and_bases(M, N, K, layout, off):
     (20481, 306, 306, "NT", 3, 306, 306),      # c4 [u|g] (K tail inside a float4 and a slice)
     (9999, 512, 257, "NN", 2, 1, 3),           # K % 32 = 1, every base misaligned
     (4096, 130, 3000, "NT", 1, 0, 1)])         # deep K, a 2-column tail tile
-def test_gemm_big_tiles(M, N, K, layout, off, pa, pb):
-    """k_gemm_big (128-row blocks of 32 x 32 x 2 fp32 MFMA: the c4 / c5 projections and input
-    gradients): odd row strides and bases (16-byte loads at 4-byte alignment), M / N / K tails, both B
+def test_gemm_config_shapes_unaligned(M, N, K, layout, off, pa, pb):
+    """The c4 / c5 projections and input gradients at their row strides: odd row strides and bases (16-byte loads at 4-byte alignment), M / N / K tails, both B
     layouts; within 3e-6 of fp64 (the max error relative to the max entry: K = 3000 accumulates
-    2.3e-6) and bitwise deterministic. (The AIMX_GEMM_BIG option: off by default.)"""
-    from aimx import _lib
-    with _lib.options(AIMX_GEMM_BIG=1):
-        C, _, ref, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
-        C2, _, _, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
+    2.3e-6) and bitwise deterministic."""
+    C, _, ref, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
+    C2, _, _, _ = _gemm_raw(M, N, K, layout, off, pa, pb)
     assert torch.isfinite(C).all()
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 3e-6, err
     assert torch.equal(C, C2)
 
 
-@pytest.mark.parametrize("M,N,K,ones,force", [(1024, 1024, 10240, True, 0), (512, 512, 20480, True, 0),
-                                              (307, 307, 4099, True, 64), (307, 307, 4099, True, 128),
-                                              (130, 70, 2049, False, 64), (256, 257, 9170, True, 128)])
-def test_gemm_big_weight_gradient(M, N, K, ones, force):
-    """k_gemm_big's weight-gradient layout (dW = dY^T X: A m-contiguous, B n-contiguous, K = atoms split
-    over blocks with an ordered slab reduction by the last block of each tile) with the implicit ones
-    column (the bias gradient): the c4 / c5 concat and embedding shapes by the rule, c5's 307-wide MLP
-    weights and small odd shapes forced onto 64- or 128-wide tiles (the AIMX_GEMM_BIG option);
-    within 2e-6 of fp64, bitwise deterministic, counters left at zero."""
+@pytest.mark.parametrize("M,N,K,ones", [(1024, 1024, 10240, True), (512, 512, 20480, True), (307, 307, 4099, True),
+                                        (130, 70, 2049, False), (256, 257, 9170, True)])
+def test_gemm_long_k_weight_gradient(M, N, K, ones):
+    """Long-K weight gradients (dW = dY^T X: A m-contiguous, B n-contiguous, K = atoms split over
+    workgroups with an ordered slab reduction by the last arriver) with the implicit ones column
+    (the bias gradient): the c4 / c5 concat and embedding shapes, c5's 307-wide MLP weights, small
+    odd shapes; within 2e-6 of fp64, bitwise deterministic, counters left at zero."""
     from aimx import _lib
-    with _lib.options(AIMX_GEMM_BIG=force or 1):
-        C, col, _, ref, Am = _gemm(M, N, K, "TN", ones=ones)
-        C2, col2, _, _, _ = _gemm(M, N, K, "TN", ones=ones)
+    C, col, _, ref, Am = _gemm(M, N, K, "TN", ones=ones)
+    C2, col2, _, _, _ = _gemm(M, N, K, "TN", ones=ones)
     assert torch.isfinite(C).all()
     assert (C.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
     if ones:
@@ -470,11 +464,10 @@ def test_gemm_big_weight_gradient(M, N, K, ones, force):
     assert int(_lib.counters(DEV).abs().sum().item()) == 0
 
 
-def test_gemm_big_weight_gradient_trimming():
-    """The weight gradient over F with empty hop chunks (zc_dim 1) on k_gemm_big: blocks wholly past
+def test_gemm_weight_gradient_trimming_c5():
+    """The weight gradient over F with empty hop chunks (zc_dim 1) at c5's width: blocks wholly past
     E are written as zeros without loads, the block straddling E reads F's columns past E as 0 (they
     hold NaN here: the stack's hop leaves them unwritten); equal to the untrimmed product bitwise."""
-    from aimx import _lib
     n, d, h = 12000, 307, 6
     K = d * (h + 1)
     counts = torch.zeros(h * n, dtype=torch.int32)
@@ -487,25 +480,18 @@ def test_gemm_big_weight_gradient_trimming():
     Fnan = F.clone()
     Fnan[:, E:] = float("nan")
     dY = torch.randn(n, 2 * d, generator=g)
-    with _lib.options(AIMX_GEMM_BIG=128):
-        full, fcol, _, ref, _ = _gemm(2 * d, K, n, "TN", A=dY, B=F, ones=True)
-        trim, tcol, _, _, _ = _gemm(2 * d, K, n, "TN", A=dY, B=Fnan, ones=True, zc=(rowptr, n, h, d, 1))
+    full, fcol, _, ref, _ = _gemm(2 * d, K, n, "TN", A=dY, B=F, ones=True)
+    trim, tcol, _, _, _ = _gemm(2 * d, K, n, "TN", A=dY, B=Fnan, ones=True, zc=(rowptr, n, h, d, 1))
     assert torch.equal(full, trim) and torch.equal(fcol, tcol)
     assert not trim[:, E:].any()
     assert (full.double() - ref).abs().max().item() / ref.abs().max().item() < 2e-6
 
 
-def test_gemm_big_tiles_epilogue_and_trimming():
-    """k_gemm_big's fused epilogue (bias, residual, SiLU with the pre-activation store) and the
+def test_gemm_epilogue_and_trimming_c5():
+    """The fused epilogue (bias, residual, SiLU with the pre-activation store) and the
     empty-hop-chunk trimming at c5 size: forward k loop stopped at E (NaN past it is never read) equals
     the untrimmed product bitwise; the input gradient's tiles past E are skipped (zc_dim 2) and every
     column < E is bitwise the untrimmed one."""
-    from aimx import _lib
-    with _lib.options(AIMX_GEMM_BIG=1):
-        _big_epilogue_case()
-
-
-def _big_epilogue_case():
     n, d, h = 10240, 307, 6
     K = d * (h + 1)
     C, _, pre, ref, _ = _gemm(n, 2 * d, 1024, "NT", bias=True, act=4, res=True)
@@ -585,17 +571,16 @@ def test_gemm_weight_grad_forced_splits(splits):
     assert (col.double() - rs).abs().max().item() / rs.abs().max().item() < 2e-6
 
 
-@pytest.mark.parametrize("bb", ["auto", "64", "80", "big"])
+@pytest.mark.parametrize("bb", ["auto", "64", "80"])
 def test_wgrad_grouped_matches_fp64(bb):
     """aimx_wgrad_grouped over the stack's shapes (76 x 76 / 152 x 304 / c5's 307 x 307 and
     614 x 614 with the bias column, long K: the LDS-block kernel with the block edge its rule picks,
     or 64- or 80-wide blocks forced by the AIMX_WGRAD_BB option), a short-K FFN shape, K = 1 and odd
-    widths (unaligned rows: the LDS kernel's dword loads); the c5 [Wi; Wg] product (614 x 615, K =
-    10240) and a 512 x 384 one go to k_gemm_big launches of their own inside the grouped call unless
-    the AIMX_GEMM_BIG option selects the large-tile rule ("big"; the default keeps them grouped): dW = dY^T X and db = sum_k dY against fp64,
-    deterministic, counters left at zero."""
-    from aimx import ops, _lib
-    opts = {} if bb == "auto" else ({"AIMX_GEMM_BIG": 1} if bb == "big" else {"AIMX_WGRAD_BB": int(bb)})
+    widths (unaligned rows: the LDS kernel's dword loads), the c5 [Wi; Wg] product (614 x 615, K =
+    10240) and a 512 x 384 one: dW = dY^T X and db = sum_k dY against fp64, deterministic, counters
+    left at zero."""
+    from aimx import _lib
+    opts = {} if bb == "auto" else {"AIMX_WGRAD_BB": int(bb)}
     with _lib.options(**opts):
         _wgrad_grouped_case()
 

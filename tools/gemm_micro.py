@@ -71,7 +71,7 @@ def run(M, N, K, layout, label, splits=0, torch_ref=True, counters=True, lda=Non
 
 
 if len(sys.argv) > 1 and sys.argv[1] == "big":
-    # the c4 / c5 MFMA-bound GEMMs in the step's layouts (hipBLASLt as a yardstick only): embedding
+    # the c2 / c4 / c5 GEMMs in the step's layouts (hipBLASLt as a yardstick only): embedding
     # projection, [Wi; Wg] input projection (K trimmed to the non-empty chunks, weight rows of the
     # full D(h+1)), its input gradient, the node-update D x D, the concat and its input gradient
     for M, D, h, H in ((9170, 76, 3, 256), (20480, 153, 3, 512), (10240, 307, 6, 1024)):
